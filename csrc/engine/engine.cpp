@@ -1,0 +1,927 @@
+// Engine ops over device-resident KV/KMV tensors. Each op has two branches:
+//   cuda (HIP, MI355X): hand-written kernels from csrc/kernels, on the current
+//        torch stream;
+//   cpu: straightforward host loops with identical semantics and identical
+//        output order (they are the oracle the GPU tests compare against).
+#include "kv.h"
+
+#include <ATen/hip/HIPContext.h>
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <stdexcept>
+
+#include "../kernels/hashfn.h"
+#include "../kernels/launch.h"
+#include "../kernels/rmatfn.h"
+
+namespace mrh {
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream(); }
+
+at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
+
+at::Tensor scratch(size_t bytes, at::Device d) {
+  return at::empty({(int64_t)std::max<size_t>(bytes, 1)}, opt(d, at::kByte));
+}
+
+template <typename T>
+T* P(const at::Tensor& t) {
+  return t.defined() && t.numel() ? reinterpret_cast<T*>(t.data_ptr()) : nullptr;
+}
+template <typename T>
+T* P0(const at::Tensor& t) {  // pointer even for empty tensors with storage
+  return t.defined() ? reinterpret_cast<T*>(t.data_ptr()) : nullptr;
+}
+
+[[noreturn]] void fail(const std::string& m) { throw std::runtime_error("mrhip: " + m); }
+
+int64_t scalar_i64(const at::Tensor& t, int64_t i) { return t[i].item<int64_t>(); }
+
+}  // namespace
+
+int64_t KV::nbytes() const {
+  int64_t b = key_bytes() + value_bytes();
+  if (!kfixed()) b += (n + 1) * 8;
+  if (!vfixed()) b += (n + 1) * 8;
+  return b;
+}
+int64_t KMV::nbytes() const {
+  int64_t b = keys.nbytes() + (nkey + 1) * 8;
+  b += vw >= 0 ? nval * vw : (nval ? voff[nval].item<int64_t>() : 0) + (nval + 1) * 8;
+  return b;
+}
+
+// ====================================================================== construction
+
+KV empty_kv(at::Device dev, int kw, int vw) {
+  KV kv;
+  kv.kdata = at::empty({0}, opt(dev, at::kByte));
+  kv.vdata = at::empty({0}, opt(dev, at::kByte));
+  kv.kw = kw;
+  kv.vw = vw;
+  if (kw < 0) kv.koff = at::zeros({1}, opt(dev, at::kLong));
+  if (vw < 0) kv.voff = at::zeros({1}, opt(dev, at::kLong));
+  kv.n = 0;
+  return kv;
+}
+
+at::Tensor fixed_offsets(int64_t n, int w, at::Device dev) {
+  return at::arange(n + 1, opt(dev, at::kLong)) * (int64_t)w;
+}
+
+KV make_kv(at::Tensor kdata, c10::optional<at::Tensor> koff, at::Tensor vdata, c10::optional<at::Tensor> voff,
+           int64_t n, at::Device dev) {
+  KV kv;
+  kv.n = n;
+  kv.kdata = kdata.contiguous().view(at::kByte).reshape({-1}).to(dev);
+  kv.vdata = vdata.defined() ? vdata.contiguous().view(at::kByte).reshape({-1}).to(dev)
+                             : at::empty({0}, opt(dev, at::kByte));
+  if (koff && koff->defined()) {
+    kv.koff = koff->to(dev, at::kLong).contiguous();
+    kv.kw = -1;
+    if (kv.koff.numel() != n + 1) fail("koff must have n+1 entries");
+  } else {
+    if (n > 0 && kv.kdata.numel() % n) fail("fixed key bytes not divisible by n");
+    kv.kw = n > 0 ? (int)(kv.kdata.numel() / n) : 0;
+  }
+  if (voff && voff->defined()) {
+    kv.voff = voff->to(dev, at::kLong).contiguous();
+    kv.vw = -1;
+    if (kv.voff.numel() != n + 1) fail("voff must have n+1 entries");
+  } else {
+    if (n > 0 && kv.vdata.numel() % n) fail("fixed value bytes not divisible by n");
+    kv.vw = n > 0 ? (int)(kv.vdata.numel() / n) : 0;
+  }
+  return kv;
+}
+
+KV kv_to(const KV& kv, at::Device dev) {
+  KV o = kv;
+  o.kdata = kv.kdata.to(dev);
+  o.vdata = kv.vdata.to(dev);
+  if (kv.koff.defined()) o.koff = kv.koff.to(dev);
+  if (kv.voff.defined()) o.voff = kv.voff.to(dev);
+  return o;
+}
+
+KV to_var_keys(const KV& kv) {
+  if (!kv.kfixed()) return kv;
+  KV o = kv;
+  o.koff = fixed_offsets(kv.n, kv.kw, kv.device());
+  o.kw = -1;
+  return o;
+}
+KV to_var_values(const KV& kv) {
+  if (!kv.vfixed()) return kv;
+  KV o = kv;
+  o.voff = fixed_offsets(kv.n, kv.vw, kv.device());
+  o.vw = -1;
+  return o;
+}
+
+namespace {
+// concat of one column (data + optional offsets)
+void concat_col(const std::vector<const at::Tensor*>& datas, const std::vector<const at::Tensor*>& offs,
+                const std::vector<int64_t>& ns, bool fixed, at::Device dev, at::Tensor* data_out,
+                at::Tensor* off_out) {
+  std::vector<at::Tensor> d;
+  for (auto* t : datas) d.push_back(t->to(dev));
+  *data_out = d.empty() ? at::empty({0}, opt(dev, at::kByte)) : at::cat(d, 0);
+  if (fixed) return;
+  std::vector<at::Tensor> o;
+  int64_t base = 0;
+  for (size_t i = 0; i < offs.size(); ++i) {
+    at::Tensor oi = offs[i]->to(dev);
+    o.push_back((i + 1 < offs.size() ? oi.narrow(0, 0, ns[i]) : oi) + base);
+    base += datas[i]->numel();
+  }
+  *off_out = o.empty() ? at::zeros({1}, opt(dev, at::kLong)) : at::cat(o, 0);
+}
+}  // namespace
+
+KV concat(const std::vector<KV>& parts_in, at::Device dev) {
+  std::vector<KV> parts;
+  for (auto& p : parts_in)
+    if (p.n > 0) parts.push_back(p);
+  if (parts.empty()) {
+    int kw = parts_in.empty() ? 0 : parts_in[0].kw, vw = parts_in.empty() ? 0 : parts_in[0].vw;
+    return empty_kv(dev, kw, vw);
+  }
+  if (parts.size() == 1) return kv_to(parts[0], dev);
+  bool kf = true, vf = true;
+  for (auto& p : parts) {
+    kf = kf && p.kfixed() && p.kw == parts[0].kw;
+    vf = vf && p.vfixed() && p.vw == parts[0].vw;
+  }
+  std::vector<KV> ps;
+  for (auto& p : parts) {
+    KV q = p;
+    if (!kf) q = to_var_keys(q);
+    if (!vf) q = to_var_values(q);
+    ps.push_back(q);
+  }
+  KV o;
+  o.kw = kf ? parts[0].kw : -1;
+  o.vw = vf ? parts[0].vw : -1;
+  std::vector<const at::Tensor*> kd, ko, vd, vo;
+  std::vector<int64_t> ns;
+  for (auto& p : ps) {
+    kd.push_back(&p.kdata);
+    ko.push_back(&p.koff);
+    vd.push_back(&p.vdata);
+    vo.push_back(&p.voff);
+    ns.push_back(p.n);
+    o.n += p.n;
+  }
+  concat_col(kd, ko, ns, kf, dev, &o.kdata, &o.koff);
+  concat_col(vd, vo, ns, vf, dev, &o.vdata, &o.voff);
+  return o;
+}
+
+// ====================================================================== primitives
+
+// int32 lengths or int64 values -> int64 exclusive offsets (n+1)
+at::Tensor exclusive_scan(const at::Tensor& x_in) {
+  at::Tensor x = x_in.contiguous();
+  const int64_t n = x.numel();
+  const at::Device dev = x.device();
+  if (x.is_cuda()) {
+    auto s = cur_stream();
+    at::Tensor tmp = scratch(k::scan_temp_bytes(n), dev);
+    if (x.scalar_type() == at::kInt) {
+      at::Tensor out = at::empty({n + 1}, opt(dev, at::kLong));
+      k::lengths_to_offsets(P0<int32_t>(x), P0<int64_t>(out), n, P0<void>(tmp), s);
+      return out;
+    } else if (x.scalar_type() == at::kLong) {
+      at::Tensor out = at::empty({n + 1}, opt(dev, at::kLong));
+      k::exclusive_scan_i64(P0<int64_t>(x), P0<int64_t>(out), n, P0<void>(tmp), s);
+      return out;
+    }
+    fail("exclusive_scan: unsupported dtype");
+  }
+  at::Tensor out = at::empty({n + 1}, opt(dev, at::kLong));
+  int64_t* o = P0<int64_t>(out);
+  int64_t acc = 0;
+  if (x.scalar_type() == at::kInt) {
+    const int32_t* p = P0<int32_t>(x);
+    for (int64_t i = 0; i < n; ++i) { o[i] = acc; acc += p[i]; }
+  } else {
+    const int64_t* p = P0<int64_t>(x);
+    for (int64_t i = 0; i < n; ++i) { o[i] = acc; acc += p[i]; }
+  }
+  o[n] = acc;
+  return out;
+}
+
+// uint32 (stored in kInt) exclusive scan -> n+1 uint32 (kInt)
+static at::Tensor scan_u32(const at::Tensor& x) {
+  const int64_t n = x.numel();
+  const at::Device dev = x.device();
+  at::Tensor out = at::empty({n + 1}, opt(dev, at::kInt));
+  if (x.is_cuda()) {
+    at::Tensor tmp = scratch(k::scan_temp_bytes(n), dev);
+    k::exclusive_scan_u32(P0<uint32_t>(x), P0<uint32_t>(out), n, P0<void>(tmp), cur_stream());
+    return out;
+  }
+  const uint32_t* p = P0<uint32_t>(x);
+  uint32_t* o = P0<uint32_t>(out);
+  uint32_t acc = 0;
+  for (int64_t i = 0; i < n; ++i) { o[i] = acc; acc += p[i]; }
+  o[n] = acc;
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& keys_in, const at::Tensor& vals_in,
+                                                              int begin_bit, int end_bit) {
+  at::Tensor keys = keys_in.contiguous();
+  at::Tensor vals = vals_in.contiguous();
+  const int64_t n = keys.numel();
+  const at::Device dev = keys.device();
+  if (keys.scalar_type() != at::kLong || vals.scalar_type() != at::kInt) fail("radix_sort_pairs: keys int64, vals int32");
+  begin_bit = (begin_bit / 8) * 8;
+  end_bit = std::min(64, ((end_bit + 7) / 8) * 8);
+  at::Tensor ko = at::empty_like(keys), vo = at::empty_like(vals);
+  int passes = 0;
+  if (n == 0) return {ko, vo, 0};
+  if (keys.is_cuda()) {
+    at::Tensor ka = at::empty_like(keys), va = at::empty_like(vals);
+    at::Tensor tmp = scratch(k::radix_temp_bytes(n), dev);
+    k::radix_sort_u64_u32(P0<uint64_t>(keys), P0<uint32_t>(vals), P0<uint64_t>(ko), P0<uint32_t>(vo),
+                          P0<uint64_t>(ka), P0<uint32_t>(va), n, begin_bit, end_bit, P0<void>(tmp), cur_stream(),
+                          &passes);
+    return {ko, vo, passes};
+  }
+  const uint64_t* k = P0<uint64_t>(keys);
+  const uint32_t* v = P0<uint32_t>(vals);
+  uint64_t mask = 0;
+  for (int b = begin_bit; b < end_bit; ++b) mask |= (1ull << b);
+  std::vector<int64_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return (k[a] & mask) < (k[b] & mask); });
+  uint64_t* kop = P0<uint64_t>(ko);
+  uint32_t* vop = P0<uint32_t>(vo);
+  for (int64_t i = 0; i < n; ++i) {
+    kop[i] = k[idx[i]];
+    vop[i] = v[idx[i]];
+  }
+  return {ko, vo, (end_bit - begin_bit) / 8};
+}
+
+at::Tensor hash32_keys(const KV& kv, uint32_t seed) {
+  const at::Device dev = kv.device();
+  at::Tensor out = at::empty({kv.n}, opt(dev, at::kInt));
+  if (kv.n == 0) return out;
+  if (dev.is_cuda()) {
+    if (kv.kfixed())
+      k::hash32_fixed(P0<uint8_t>(kv.kdata), kv.kw, kv.n, seed, P0<uint32_t>(out), cur_stream());
+    else
+      k::hash32_var(P0<uint8_t>(kv.kdata), P0<int64_t>(kv.koff), kv.n, seed, P0<uint32_t>(out), cur_stream());
+    return out;
+  }
+  const uint8_t* d = P0<uint8_t>(kv.kdata);
+  uint32_t* o = P0<uint32_t>(out);
+  if (kv.kfixed()) {
+    for (int64_t i = 0; i < kv.n; ++i) o[i] = dev::hashlittle(d + i * kv.kw, kv.kw, seed);
+  } else {
+    const int64_t* off = P0<int64_t>(kv.koff);
+    for (int64_t i = 0; i < kv.n; ++i) o[i] = dev::hashlittle(d + off[i], off[i + 1] - off[i], seed);
+  }
+  return out;
+}
+
+at::Tensor hash64_keys(const KV& kv) {
+  const at::Device dev = kv.device();
+  at::Tensor out = at::empty({kv.n}, opt(dev, at::kLong));
+  if (kv.n == 0) return out;
+  if (dev.is_cuda()) {
+    if (kv.kfixed())
+      k::hash64_fixed(P0<uint8_t>(kv.kdata), kv.kw, kv.n, P0<uint64_t>(out), cur_stream());
+    else
+      k::hash64_var(P0<uint8_t>(kv.kdata), P0<int64_t>(kv.koff), kv.n, P0<uint64_t>(out), cur_stream());
+    return out;
+  }
+  const uint8_t* d = P0<uint8_t>(kv.kdata);
+  uint64_t* o = P0<uint64_t>(out);
+  if (kv.kfixed()) {
+    for (int64_t i = 0; i < kv.n; ++i) o[i] = dev::hash64(d + i * kv.kw, kv.kw);
+  } else {
+    const int64_t* off = P0<int64_t>(kv.koff);
+    for (int64_t i = 0; i < kv.n; ++i) o[i] = dev::hash64(d + off[i], off[i + 1] - off[i]);
+  }
+  return out;
+}
+
+// gather rows of a column. perm: int32 (u32) or int64 row indices.
+at::Tensor gather_rows(const at::Tensor& data, const at::Tensor& off, int w, const at::Tensor& perm,
+                       at::Tensor* new_off) {
+  const at::Device dev = data.device();
+  const int64_t n = perm.numel();
+  const bool i64 = perm.scalar_type() == at::kLong;
+  if (w >= 0) {
+    at::Tensor out = at::empty({n * w}, opt(dev, at::kByte));
+    if (n == 0 || w == 0) return out;
+    if (dev.is_cuda()) {
+      if (i64)
+        k::gather_fixed_i64idx(P0<uint8_t>(data), w, P0<int64_t>(perm), n, P0<uint8_t>(out), cur_stream());
+      else
+        k::gather_fixed(P0<uint8_t>(data), w, P0<uint32_t>(perm), n, P0<uint8_t>(out), cur_stream());
+      return out;
+    }
+    const uint8_t* s = P0<uint8_t>(data);
+    uint8_t* o = P0<uint8_t>(out);
+    for (int64_t i = 0; i < n; ++i) {
+      int64_t r = i64 ? P0<int64_t>(perm)[i] : (int64_t)P0<uint32_t>(perm)[i];
+      memcpy(o + i * w, s + r * w, w);
+    }
+    return out;
+  }
+  at::Tensor p32 = i64 ? perm.to(at::kInt) : perm;  // row ids < 2^32 by construction
+  if (dev.is_cuda()) {
+    at::Tensor len = at::empty({n}, opt(dev, at::kInt));
+    k::gather_var_lengths(P0<int64_t>(off), P0<uint32_t>(p32), n, P0<int32_t>(len), cur_stream());
+    *new_off = exclusive_scan(len);
+    int64_t tot = n ? scalar_i64(*new_off, n) : 0;
+    at::Tensor out = at::empty({tot}, opt(dev, at::kByte));
+    k::gather_var_copy(P0<uint8_t>(data), P0<int64_t>(off), P0<uint32_t>(p32), n, P0<uint8_t>(out),
+                       P0<int64_t>(*new_off), cur_stream());
+    return out;
+  }
+  const int64_t* so = P0<int64_t>(off);
+  const uint32_t* pp = P0<uint32_t>(p32);
+  *new_off = at::empty({n + 1}, opt(dev, at::kLong));
+  int64_t* no = P0<int64_t>(*new_off);
+  int64_t acc = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    no[i] = acc;
+    acc += so[pp[i] + 1] - so[pp[i]];
+  }
+  no[n] = acc;
+  at::Tensor out = at::empty({acc}, opt(dev, at::kByte));
+  const uint8_t* s = P0<uint8_t>(data);
+  uint8_t* o = P0<uint8_t>(out);
+  for (int64_t i = 0; i < n; ++i) memcpy(o + no[i], s + so[pp[i]], no[i + 1] - no[i]);
+  return out;
+}
+
+KV gather(const KV& kv, const at::Tensor& perm) {
+  KV o;
+  o.n = perm.numel();
+  o.kw = kv.kw;
+  o.vw = kv.vw;
+  o.kdata = gather_rows(kv.kdata, kv.koff, kv.kw, perm, &o.koff);
+  o.vdata = gather_rows(kv.vdata, kv.voff, kv.vw, perm, &o.voff);
+  return o;
+}
+
+// ====================================================================== group-by
+
+namespace {
+
+at::Tensor iota_u32(int64_t n, at::Device dev) {
+  at::Tensor t = at::empty({n}, opt(dev, at::kInt));
+  if (n == 0) return t;
+  if (dev.is_cuda()) {
+    k::iota_u32(P0<uint32_t>(t), n, cur_stream());
+  } else {
+    uint32_t* p = P0<uint32_t>(t);
+    for (int64_t i = 0; i < n; ++i) p[i] = (uint32_t)i;
+  }
+  return t;
+}
+
+// fixed keys <= 8 bytes -> raw little-endian uint64 (exact group key)
+at::Tensor raw_keys_u64(const KV& kv, int mode, bool desc, const at::Tensor& data, int w, at::Tensor* idx) {
+  const at::Device dev = data.device();
+  const int64_t n = kv.n;
+  at::Tensor keys = at::empty({n}, opt(dev, at::kLong));
+  *idx = at::empty({n}, opt(dev, at::kInt));
+  if (n == 0) return keys;
+  if (dev.is_cuda()) {
+    k::make_sortkeys_fixed(P0<uint8_t>(data), w, n, mode, desc, P0<uint64_t>(keys), P0<uint32_t>(*idx), cur_stream());
+    return keys;
+  }
+  const uint8_t* d = P0<uint8_t>(data);
+  uint64_t* kp = P0<uint64_t>(keys);
+  uint32_t* ip = P0<uint32_t>(*idx);
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t raw = 0;
+    for (int b = 0; b < w; ++b) raw |= (uint64_t)d[i * w + b] << (8 * b);
+    uint64_t kk = dev::sortkey_transform(raw, mode);
+    kp[i] = desc ? ~kk : kk;
+    ip[i] = (uint32_t)i;
+  }
+  return keys;
+}
+
+// sorted keys -> (flags, pos, seg, nseg)
+void segments_from_sorted(const at::Tensor& sk, at::Tensor* flags, at::Tensor* pos, at::Tensor* seg, int64_t* nseg) {
+  const int64_t n = sk.numel();
+  const at::Device dev = sk.device();
+  *flags = at::empty({n}, opt(dev, at::kInt));
+  if (dev.is_cuda()) {
+    k::head_flags_u64(P0<uint64_t>(sk), n, P0<uint32_t>(*flags), cur_stream());
+  } else {
+    const uint64_t* k = P0<uint64_t>(sk);
+    uint32_t* f = P0<uint32_t>(*flags);
+    for (int64_t i = 0; i < n; ++i) f[i] = (i == 0 || k[i] != k[i - 1]) ? 1u : 0u;
+  }
+  *pos = scan_u32(*flags);
+  *nseg = (int64_t)(uint32_t)(*pos)[n].item<int32_t>();
+  *seg = at::empty({*nseg + 1}, opt(dev, at::kLong));
+  if (dev.is_cuda()) {
+    k::compact_heads(P0<uint32_t>(*flags), P0<uint32_t>(*pos), n, P0<int64_t>(*seg), cur_stream());
+  } else {
+    const uint32_t* f = P0<uint32_t>(*flags);
+    const uint32_t* p = P0<uint32_t>(*pos);
+    int64_t* s = P0<int64_t>(*seg);
+    for (int64_t i = 0; i < n; ++i)
+      if (f[i]) s[p[i]] = i;
+    s[*nseg] = n;
+  }
+}
+
+// exact host regroup used only when a 64-bit hash collision was detected
+void exact_regroup_host(const KV& kv, const at::Tensor& h64_sorted_dev, at::Tensor* perm_dev, at::Tensor* seg_dev,
+                        int64_t* nseg) {
+  const at::Device dev = kv.device();
+  KV h = kv_to(kv, at::kCPU);
+  at::Tensor perm = perm_dev->to(at::kCPU);
+  at::Tensor hs = h64_sorted_dev.to(at::kCPU);
+  const int64_t n = kv.n;
+  const uint8_t* d = P0<uint8_t>(h.kdata);
+  const int64_t* off = h.kfixed() ? nullptr : P0<int64_t>(h.koff);
+  auto kp = [&](uint32_t r) { return d + (off ? off[r] : (int64_t)r * h.kw); };
+  auto kl = [&](uint32_t r) { return off ? off[r + 1] - off[r] : (int64_t)h.kw; };
+  uint32_t* pp = P0<uint32_t>(perm);
+  const uint64_t* hp = P0<uint64_t>(hs);
+  std::vector<int64_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  auto less = [&](int64_t a, int64_t b) {
+    if (hp[a] != hp[b]) return hp[a] < hp[b];
+    int64_t la = kl(pp[a]), lb = kl(pp[b]);
+    int c = memcmp(kp(pp[a]), kp(pp[b]), (size_t)std::min(la, lb));
+    if (c) return c < 0;
+    return la < lb;
+  };
+  std::stable_sort(idx.begin(), idx.end(), less);
+  at::Tensor np = at::empty({n}, opt(at::kCPU, at::kInt));
+  uint32_t* npp = P0<uint32_t>(np);
+  std::vector<int64_t> segs;
+  for (int64_t i = 0; i < n; ++i) {
+    npp[i] = pp[idx[i]];
+    if (i == 0 || less(idx[i - 1], idx[i])) segs.push_back(i);
+  }
+  segs.push_back(n);
+  *nseg = (int64_t)segs.size() - 1;
+  *perm_dev = np.to(dev);
+  *seg_dev = at::from_blob(segs.data(), {(int64_t)segs.size()}, opt(at::kCPU, at::kLong)).clone().to(dev);
+}
+
+at::Tensor seg_heads(const at::Tensor& seg, int64_t nseg) { return seg.narrow(0, 0, nseg); }
+
+}  // namespace
+
+KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits) {
+  const at::Device dev = kv.device();
+  KMV out;
+  ConvertStats local;
+  if (!st) st = &local;
+  if (kv.n == 0) {
+    out.keys = empty_kv(dev, kv.kw, 0);
+    out.vw = kv.vw;
+    out.vdata = at::empty({0}, opt(dev, at::kByte));
+    if (kv.vw < 0) out.voff = at::zeros({1}, opt(dev, at::kLong));
+    out.seg = at::zeros({1}, opt(dev, at::kLong));
+    return out;
+  }
+  const int64_t n = kv.n;
+  if (n > 0xFFFFFFFFll) fail("convert: more than 2^32 pairs on one rank");
+  at::Tensor sk_in, idx;
+  int end_bit;
+  st->exact = kv.kfixed() && kv.kw <= 8 && force_hash_bits >= 64;
+  if (st->exact) {
+    sk_in = raw_keys_u64(kv, 0, false, kv.kdata, kv.kw, &idx);
+    end_bit = 8 * kv.kw;
+  } else {
+    sk_in = hash64_keys(kv);
+    if (force_hash_bits < 64) sk_in = at::bitwise_and(sk_in, (int64_t)((1ull << force_hash_bits) - 1));
+    idx = iota_u32(n, dev);
+    end_bit = 64;
+  }
+  auto [sk, perm, passes] = radix_sort_pairs(sk_in, idx, 0, end_bit);
+  st->passes = passes;
+  at::Tensor flags, pos, seg;
+  int64_t nseg = 0;
+  segments_from_sorted(sk, &flags, &pos, &seg, &nseg);
+  if (!st->exact) {
+    int64_t mism = 0;
+    if (dev.is_cuda()) {
+      at::Tensor m = at::zeros({1}, opt(dev, at::kLong));
+      if (kv.kfixed())
+        k::verify_groups_fixed(P0<uint8_t>(kv.kdata), kv.kw, P0<uint32_t>(perm), P0<uint32_t>(flags),
+                               P0<uint32_t>(pos), P0<int64_t>(seg), n, P0<unsigned long long>(m), cur_stream());
+      else
+        k::verify_groups_var(P0<uint8_t>(kv.kdata), P0<int64_t>(kv.koff), P0<uint32_t>(perm), P0<uint32_t>(flags),
+                             P0<uint32_t>(pos), P0<int64_t>(seg), n, P0<unsigned long long>(m), cur_stream());
+      mism = m.item<int64_t>();
+    } else {
+      const uint8_t* d = P0<uint8_t>(kv.kdata);
+      const int64_t* off = kv.kfixed() ? nullptr : P0<int64_t>(kv.koff);
+      const uint32_t* pp = P0<uint32_t>(perm);
+      const uint32_t* f = P0<uint32_t>(flags);
+      const uint32_t* ps = P0<uint32_t>(pos);
+      const int64_t* sg = P0<int64_t>(seg);
+      for (int64_t i = 0; i < n; ++i) {
+        if (f[i]) continue;
+        uint32_t a = pp[i], b = pp[sg[ps[i] - 1]];
+        int64_t a0 = off ? off[a] : (int64_t)a * kv.kw, la = off ? off[a + 1] - a0 : kv.kw;
+        int64_t b0 = off ? off[b] : (int64_t)b * kv.kw, lb = off ? off[b + 1] - b0 : kv.kw;
+        if (la != lb || memcmp(d + a0, d + b0, la)) ++mism;
+      }
+    }
+    st->collisions = mism;
+    if (mism) exact_regroup_host(kv, sk, &perm, &seg, &nseg);
+  }
+  // unique keys: rows perm[seg[s]]
+  at::Tensor head_rows = gather_rows(perm, at::Tensor(), 4, seg_heads(seg, nseg), nullptr).view(at::kInt);
+  out.keys.n = nseg;
+  out.keys.kw = kv.kw;
+  out.keys.vw = 0;
+  out.keys.kdata = gather_rows(kv.kdata, kv.koff, kv.kw, head_rows, &out.keys.koff);
+  out.keys.vdata = at::empty({0}, opt(dev, at::kByte));
+  out.vw = kv.vw;
+  out.vdata = gather_rows(kv.vdata, kv.voff, kv.vw, perm, &out.voff);
+  out.seg = seg;
+  out.nkey = nseg;
+  out.nval = n;
+  return out;
+}
+
+KMV clone(const KV& kv) {
+  KMV out;
+  const at::Device dev = kv.device();
+  out.keys = kv;
+  out.keys.vdata = at::empty({0}, opt(dev, at::kByte));
+  out.keys.voff = at::Tensor();
+  out.keys.vw = 0;
+  out.vdata = kv.vdata;
+  out.voff = kv.voff;
+  out.vw = kv.vw;
+  out.seg = at::arange(0, kv.n + 1, opt(dev, at::kLong));
+  out.nkey = kv.n;
+  out.nval = kv.n;
+  return out;
+}
+
+KMV collapse(const KV& kv_in, const std::string& key) {
+  const at::Device dev = kv_in.device();
+  KV kv = to_var_values(to_var_keys(kv_in));
+  const int64_t n = kv.n;
+  // interleave lengths [k0,v0,k1,v1,...] and bytes
+  at::Tensor kl = kv.koff.narrow(0, 1, n) - kv.koff.narrow(0, 0, n);
+  at::Tensor vl = kv.voff.narrow(0, 1, n) - kv.voff.narrow(0, 0, n);
+  at::Tensor lens = at::stack({kl, vl}, 1).reshape({2 * n});
+  at::Tensor off = exclusive_scan(lens);
+  // build permutation into a combined [keys|values] byte array
+  at::Tensor comb = at::cat({kv.kdata, kv.vdata}, 0);
+  at::Tensor src_off_k = kv.koff.narrow(0, 0, n);
+  at::Tensor src_off_v = kv.voff.narrow(0, 0, n) + kv.kdata.numel();
+  at::Tensor starts = at::stack({src_off_k, src_off_v}, 1).reshape({2 * n});
+  // synthetic offsets array for the combined source: row r = [starts[r], starts[r]+lens[r])
+  // gather_rows needs off[r+1]-off[r] == len, so copy via a host-free torch gather
+  at::Tensor vdata;
+  {
+    int64_t tot = n ? scalar_i64(off, 2 * n) : 0;
+    at::Tensor row_of_byte = at::repeat_interleave(at::arange(2 * n, opt(dev, at::kLong)), lens, tot);
+    at::Tensor within = at::arange(tot, opt(dev, at::kLong)) - off.narrow(0, 0, 2 * n).index_select(0, row_of_byte);
+    vdata = comb.index_select(0, starts.index_select(0, row_of_byte) + within);
+  }
+  KMV out;
+  out.keys = empty_kv(dev, -1, 0);
+  std::vector<uint8_t> kb(key.begin(), key.end());
+  out.keys.kdata = at::from_blob(kb.data(), {(int64_t)kb.size()}, opt(at::kCPU, at::kByte)).clone().to(dev);
+  out.keys.koff = at::tensor({(int64_t)0, (int64_t)kb.size()}, opt(at::kCPU, at::kLong)).to(dev);
+  out.keys.n = 1;
+  out.vw = -1;
+  out.vdata = vdata;
+  out.voff = off;
+  out.seg = at::tensor({(int64_t)0, 2 * n}, opt(at::kCPU, at::kLong)).to(dev);
+  out.nkey = 1;
+  out.nval = 2 * n;
+  return out;
+}
+
+// ====================================================================== reduce builtins
+
+static int dtype_code(const std::string& dt, int* width) {
+  if (dt == "int32" || dt == "int") { *width = 4; return 0; }
+  if (dt == "int64" || dt == "uint64") { *width = 8; return 1; }
+  if (dt == "float32" || dt == "float") { *width = 4; return 2; }
+  if (dt == "float64" || dt == "double") { *width = 8; return 3; }
+  fail("unknown dtype " + dt);
+}
+
+KV reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype) {
+  const at::Device dev = kmv.keys.device();
+  KV out = kmv.keys;
+  out.n = kmv.nkey;
+  const int64_t ns = kmv.nkey;
+  at::Tensor seg = kmv.seg;
+  if (op == "count") {
+    at::Tensor c = at::empty({ns}, opt(dev, at::kInt));
+    if (dev.is_cuda()) k::seg_count(P0<int64_t>(seg), ns, P0<int32_t>(c), cur_stream());
+    else if (ns) c.copy_((seg.narrow(0, 1, ns) - seg.narrow(0, 0, ns)).to(at::kInt));
+    out.vdata = c.view(at::kByte);
+    out.vw = 4;
+    out.voff = at::Tensor();
+    return out;
+  }
+  if (op == "first" || op == "last") {
+    at::Tensor rows = op == "first" ? seg.narrow(0, 0, ns) : (seg.narrow(0, 1, ns) - 1);
+    out.vdata = gather_rows(kmv.vdata, kmv.voff, kmv.vw, rows, &out.voff);
+    out.vw = kmv.vw;
+    return out;
+  }
+  int w = 0;
+  int dc = dtype_code(dtype, &w);
+  if (kmv.vw != w) fail("reduce " + op + ": values are not fixed-width " + dtype);
+  int opc = op == "sum" ? 0 : op == "min" ? 1 : op == "max" ? 2 : -1;
+  if (opc < 0) fail("unknown builtin reduce op " + op);
+  at::Tensor res = at::empty({ns * w}, opt(dev, at::kByte));
+  if (dev.is_cuda()) {
+    k::seg_reduce(P0<void>(kmv.vdata), dc, opc, P0<int64_t>(seg), ns, P0<void>(res), cur_stream());
+  } else if (ns) {
+    const int64_t* sg = P0<int64_t>(seg);
+    auto body = [&](auto* v, auto* o) {
+      using T = std::remove_pointer_t<decltype(o)>;
+      for (int64_t s = 0; s < ns; ++s) {
+        T acc = v[sg[s]];
+        for (int64_t i = sg[s] + 1; i < sg[s + 1]; ++i) {
+          T x = v[i];
+          acc = opc == 0 ? T(acc + x) : opc == 1 ? (x < acc ? x : acc) : (x > acc ? x : acc);
+        }
+        o[s] = acc;
+      }
+    };
+    switch (dc) {
+      case 0: body(P0<int32_t>(kmv.vdata), P0<int32_t>(res)); break;
+      case 1: body(P0<int64_t>(kmv.vdata), P0<int64_t>(res)); break;
+      case 2: body(P0<float>(kmv.vdata), P0<float>(res)); break;
+      default: body(P0<double>(kmv.vdata), P0<double>(res)); break;
+    }
+  }
+  out.vdata = res;
+  out.vw = w;
+  out.voff = at::Tensor();
+  return out;
+}
+
+// ====================================================================== sorting
+
+namespace {
+bool flag_mode(int flag, int w, int* mode, int* bits) {
+  switch (std::abs(flag)) {
+    case 1: *mode = 1; *bits = 32; return w >= 4;
+    case 2: *mode = 2; *bits = 64; return w >= 8;
+    case 3: *mode = 3; *bits = 32; return w >= 4;
+    case 4: *mode = 4; *bits = 64; return w >= 8;
+    case 7: *mode = 7; *bits = 64; return w >= 8;
+    case 8: *mode = 8; *bits = 32; return w >= 4;
+    default: return false;
+  }
+}
+
+// string order on host for tie groups (strcmp semantics: stop at NUL)
+int str_cmp(const uint8_t* a, int64_t la, const uint8_t* b, int64_t lb) {
+  int64_t i = 0;
+  for (;; ++i) {
+    int ca = i < la ? a[i] : 0, cb = i < lb ? b[i] : 0;
+    if (ca != cb) return ca < cb ? -1 : 1;
+    if (ca == 0) return 0;
+  }
+}
+
+// permutation sorting a (data, off, w) column by flag
+at::Tensor sort_perm_column(const at::Tensor& data, const at::Tensor& off, int w, int64_t n, int flag) {
+  const at::Device dev = data.device();
+  const bool desc = flag < 0;
+  int mode = 0, bits = 64;
+  if (flag_mode(flag, w, &mode, &bits)) {
+    KV dummy;
+    dummy.n = n;
+    at::Tensor idx;
+    at::Tensor sk = raw_keys_u64(dummy, mode, desc, data, std::min(w, bits / 8), &idx);
+    auto [ks, perm, passes] = radix_sort_pairs(sk, idx, 0, bits);
+    return perm;
+  }
+  if (std::abs(flag) != 5 && std::abs(flag) != 6) fail("sort flag " + std::to_string(flag) + " unsupported");
+  at::Tensor o = w >= 0 ? fixed_offsets(n, w, dev) : off;
+  at::Tensor sk = at::empty({n}, opt(dev, at::kLong));
+  at::Tensor idx = at::empty({n}, opt(dev, at::kInt));
+  if (dev.is_cuda()) {
+    k::make_sortkeys_strprefix(P0<uint8_t>(data), P0<int64_t>(o), n, 0, desc, P0<uint64_t>(sk), P0<uint32_t>(idx),
+                               cur_stream());
+  } else {
+    const uint8_t* d = P0<uint8_t>(data);
+    const int64_t* op = P0<int64_t>(o);
+    uint64_t* kp = P0<uint64_t>(sk);
+    uint32_t* ip = P0<uint32_t>(idx);
+    for (int64_t i = 0; i < n; ++i) {
+      uint64_t kk = 0;
+      for (int j = 0; j < 8; ++j) kk = (kk << 8) | (op[i] + j < op[i + 1] ? d[op[i] + j] : 0);
+      kp[i] = desc ? ~kk : kk;
+      ip[i] = (uint32_t)i;
+    }
+  }
+  auto [ks, perm, passes] = radix_sort_pairs(sk, idx, 0, 64);
+  // ties beyond the 8-byte prefix: only possible where adjacent prefixes are
+  // equal; resolve those groups on the host with full strcmp semantics.
+  if (n < 2 || !at::any(ks.narrow(0, 1, n - 1) == ks.narrow(0, 0, n - 1)).item<bool>()) return perm;
+  at::Tensor ksh = ks.to(at::kCPU), ph = perm.to(at::kCPU);
+  at::Tensor dh = data.to(at::kCPU), oh = o.to(at::kCPU);
+  const uint64_t* kk = P0<uint64_t>(ksh);
+  uint32_t* pp = P0<uint32_t>(ph);
+  const uint8_t* d = P0<uint8_t>(dh);
+  const int64_t* op = P0<int64_t>(oh);
+  bool changed = false;
+  for (int64_t i = 0; i < n;) {
+    int64_t j = i + 1;
+    while (j < n && kk[j] == kk[i]) ++j;
+    uint64_t pre = desc ? ~kk[i] : kk[i];
+    bool has_nul = false;
+    for (int b = 0; b < 8; ++b) has_nul |= ((pre >> (8 * b)) & 0xff) == 0;
+    if (j - i > 1 && !has_nul) {
+      std::stable_sort(pp + i, pp + j, [&](uint32_t a, uint32_t b) {
+        int c = str_cmp(d + op[a], op[a + 1] - op[a], d + op[b], op[b + 1] - op[b]);
+        return desc ? c > 0 : c < 0;
+      });
+      changed = true;
+    }
+    i = j;
+  }
+  return changed ? ph.to(dev) : perm;
+}
+}  // namespace
+
+KV sort_kv(const KV& kv, int flag, bool by_value) {
+  if (kv.n <= 1) return kv;
+  at::Tensor perm = by_value ? sort_perm_column(kv.vdata, kv.voff, kv.vw, kv.n, flag)
+                             : sort_perm_column(kv.kdata, kv.koff, kv.kw, kv.n, flag);
+  return gather(kv, perm);
+}
+
+namespace {
+// segment id of every value (int64), by binary search over seg
+at::Tensor segment_ids(const at::Tensor& seg, int64_t nseg, int64_t nval) {
+  const at::Device dev = seg.device();
+  if (nval == 0) return at::empty({0}, opt(dev, at::kLong));
+  at::Tensor pos = at::arange(nval, opt(dev, at::kLong));
+  return at::searchsorted(seg.narrow(0, 0, nseg + 1), pos, false, /*right=*/true) - 1;
+}
+}  // namespace
+
+KV expand(const KMV& kmv) {
+  at::Tensor sid = segment_ids(kmv.seg, kmv.nkey, kmv.nval);
+  KV out;
+  out.n = kmv.nval;
+  out.kw = kmv.keys.kw;
+  out.kdata = gather_rows(kmv.keys.kdata, kmv.keys.koff, kmv.keys.kw, sid, &out.koff);
+  out.vw = kmv.vw;
+  out.vdata = kmv.vdata;
+  out.voff = kmv.voff;
+  return out;
+}
+
+KMV sort_multivalues(const KMV& kmv, int flag) {
+  if (kmv.nval <= 1) return kmv;
+  const at::Device dev = kmv.seg.device();
+  at::Tensor perm1 = sort_perm_column(kmv.vdata, kmv.voff, kmv.vw, kmv.nval, flag);
+  // stable re-sort of perm1 by segment id (LSD: segment major, value minor)
+  at::Tensor sid = segment_ids(kmv.seg, kmv.nkey, kmv.nval);
+  at::Tensor sid_p = sid.index_select(0, perm1.to(at::kLong));
+  auto [ks, perm2, passes] = radix_sort_pairs(sid_p, iota_u32(kmv.nval, dev), 0, 64);
+  at::Tensor perm = perm1.to(at::kLong).index_select(0, perm2.to(at::kLong));
+  KMV out = kmv;
+  out.vdata = gather_rows(kmv.vdata, kmv.voff, kmv.vw, perm, &out.voff);
+  return out;
+}
+
+// ====================================================================== text & graph maps
+
+KV map_urls(const at::Tensor& text, int64_t n, int32_t doc_id) {
+  const at::Device dev = text.device();
+  if (text.numel() < n + 32) fail("map_urls: text buffer must be padded by >= 32 bytes");
+  KV kv;
+  kv.kw = -1;
+  kv.vw = 4;
+  if (dev.is_cuda()) {
+    auto s = cur_stream();
+    int64_t nt = k::url_num_tiles(n);
+    at::Tensor cnt = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kInt));
+    k::url_count(P0<uint8_t>(text), n, P0<uint32_t>(cnt), s);
+    at::Tensor toff = scan_u32(cnt.narrow(0, 0, nt));
+    int64_t nurl = (int64_t)(uint32_t)toff[nt].item<int32_t>();
+    at::Tensor starts = at::empty({std::max<int64_t>(nurl, 1)}, opt(dev, at::kLong));
+    k::url_emit_starts(P0<uint8_t>(text), n, P0<uint32_t>(toff), P0<int64_t>(starts), s);
+    at::Tensor klen = at::empty({std::max<int64_t>(nurl, 1)}, opt(dev, at::kInt));
+    k::url_lengths(P0<uint8_t>(text), n, P0<int64_t>(starts), nurl, P0<int32_t>(klen), s);
+    kv.koff = exclusive_scan(klen.narrow(0, 0, nurl));
+    int64_t kb = scalar_i64(kv.koff, nurl);
+    kv.kdata = at::empty({kb}, opt(dev, at::kByte));
+    k::url_copy(P0<uint8_t>(text), P0<int64_t>(starts), P0<int64_t>(kv.koff), nurl, P0<uint8_t>(kv.kdata), s);
+    at::Tensor v = at::empty({nurl}, opt(dev, at::kInt));
+    k::fill_i32(P0<int32_t>(v), nurl, doc_id, s);
+    kv.vdata = v.view(at::kByte);
+    kv.n = nurl;
+    return kv;
+  }
+  const uint8_t* t = P0<uint8_t>(text);
+  static const char pat[] = "<a href=\"";
+  std::vector<int64_t> koff{0};
+  std::vector<uint8_t> kd;
+  for (int64_t i = 0; i + 8 < n; ++i) {
+    if (memcmp(t + i, pat, 9) != 0) continue;
+    int64_t a = i + 9, j = a;
+    while (j < n && t[j] != '"') ++j;
+    kd.insert(kd.end(), t + a, t + j);
+    kd.push_back(0);
+    koff.push_back((int64_t)kd.size());
+  }
+  kv.n = (int64_t)koff.size() - 1;
+  kv.koff = at::from_blob(koff.data(), {(int64_t)koff.size()}, opt(at::kCPU, at::kLong)).clone();
+  kv.kdata = at::from_blob(kd.data(), {(int64_t)kd.size()}, opt(at::kCPU, at::kByte)).clone();
+  kv.vdata = at::full({kv.n}, doc_id, opt(at::kCPU, at::kInt)).view(at::kByte);
+  return kv;
+}
+
+static inline bool is_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\f' || c == '\r' || c == 0; }
+
+KV map_words(const at::Tensor& text, int64_t n) {
+  const at::Device dev = text.device();
+  if (text.numel() < n + 32) fail("map_words: text buffer must be padded by >= 32 bytes");
+  KV kv;
+  kv.kw = -1;
+  kv.vw = 0;
+  kv.vdata = at::empty({0}, opt(dev, at::kByte));
+  if (dev.is_cuda()) {
+    auto s = cur_stream();
+    int64_t nt = k::tok_num_tiles(n);
+    at::Tensor cnt = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kInt));
+    k::tok_count(P0<uint8_t>(text), n, P0<uint32_t>(cnt), s);
+    at::Tensor toff = scan_u32(cnt.narrow(0, 0, nt));
+    int64_t nw = (int64_t)(uint32_t)toff[nt].item<int32_t>();
+    at::Tensor starts = at::empty({std::max<int64_t>(nw, 1)}, opt(dev, at::kLong));
+    at::Tensor klen = at::empty({std::max<int64_t>(nw, 1)}, opt(dev, at::kInt));
+    k::tok_emit(P0<uint8_t>(text), n, P0<uint32_t>(toff), P0<int64_t>(starts), P0<int32_t>(klen), s);
+    kv.koff = exclusive_scan(klen.narrow(0, 0, nw));
+    int64_t kb = scalar_i64(kv.koff, nw);
+    kv.kdata = at::empty({kb}, opt(dev, at::kByte));
+    k::copy_strings_nul(P0<uint8_t>(text), P0<int64_t>(starts), P0<int64_t>(kv.koff), nw, P0<uint8_t>(kv.kdata), s);
+    kv.n = nw;
+    return kv;
+  }
+  const uint8_t* t = P0<uint8_t>(text);
+  std::vector<int64_t> koff{0};
+  std::vector<uint8_t> kd;
+  for (int64_t i = 0; i < n;) {
+    while (i < n && is_ws(t[i])) ++i;
+    if (i >= n) break;
+    int64_t j = i;
+    while (j < n && !is_ws(t[j])) ++j;
+    kd.insert(kd.end(), t + i, t + j);
+    kd.push_back(0);
+    koff.push_back((int64_t)kd.size());
+    i = j;
+  }
+  kv.n = (int64_t)koff.size() - 1;
+  kv.koff = at::from_blob(koff.data(), {(int64_t)koff.size()}, opt(at::kCPU, at::kLong)).clone();
+  kv.kdata = at::from_blob(kd.data(), {(int64_t)kd.size()}, opt(at::kCPU, at::kByte)).clone();
+  return kv;
+}
+
+KV map_rmat(int64_t nedges, int nlevels, double a, double b, double c, double d, double fraction, uint64_t seed,
+            uint64_t first_edge, at::Device dev) {
+  KV kv;
+  kv.kw = 16;
+  kv.vw = 0;
+  kv.n = nedges;
+  kv.vdata = at::empty({0}, opt(dev, at::kByte));
+  at::Tensor e = at::empty({2 * nedges}, opt(dev, at::kLong));
+  if (dev.is_cuda()) {
+    k::rmat_edges(P0<uint64_t>(e), nedges, nlevels, (float)a, (float)b, (float)c, (float)d, (float)fraction, seed,
+                  first_edge, cur_stream());
+  } else {
+    uint64_t* ep = P0<uint64_t>(e);
+    for (int64_t i = 0; i < nedges; ++i)
+      dev::rmat_edge(first_edge + (uint64_t)i, nlevels, (float)a, (float)b, (float)c, (float)d, (float)fraction, seed,
+                     &ep[2 * i], &ep[2 * i + 1]);
+  }
+  kv.kdata = e.view(at::kByte);
+  return kv;
+}
+
+}  // namespace mrh

@@ -1,0 +1,130 @@
+// Device-resident KeyValue / KeyMultiValue containers (SoA) and the engine ops
+// that transform them. This is the MI355X-native replacement for MR-MPI's
+// paged byte stores (reference src/keyvalue.h:23-115, src/keymultivalue.h:23-196,
+// src/spool.h:21-76): instead of fixed-size pages of interleaved
+// [kb|vb|key|value] records, a KV is four flat tensors in HBM:
+//
+//   kdata : uint8  key bytes (packed)        koff : int64 [n+1]  (variable keys)
+//   vdata : uint8  value bytes (packed)      voff : int64 [n+1]  (variable values)
+//
+// Fixed-width keys/values (the common graph case: uint64 vertex, EDGE{u64,u64},
+// int count, double weight) carry kw/vw >= 0 and no offset array.
+//
+// A KMV is the same thing grouped: unique keys + values concatenated in group
+// order + a CSR segment array seg[nkey+1]. A key with millions of values is
+// just a long segment (the reference's multi-page "extended" KMV pair).
+//
+// All tensors live on the engine device: "cuda" (HIP on MI355X) for the real
+// engine, "cpu" for the oracle / CPU test path. Every op dispatches on the
+// tensor device; the CUDA branch always runs the hand-written HIP kernels.
+#pragma once
+#include <ATen/ATen.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mrh {
+
+struct KV {
+  at::Tensor kdata, koff, vdata, voff;
+  int64_t n = 0;
+  int kw = 0;  // >= 0 fixed key width in bytes, -1 variable
+  int vw = 0;  // >= 0 fixed value width in bytes, -1 variable
+
+  bool kfixed() const { return kw >= 0; }
+  bool vfixed() const { return vw >= 0; }
+  at::Device device() const { return kdata.defined() ? kdata.device() : at::Device(at::kCPU); }
+  int64_t key_bytes() const { return kfixed() ? n * kw : (n ? koff[n].item<int64_t>() : 0); }
+  int64_t value_bytes() const { return vfixed() ? n * vw : (n ? voff[n].item<int64_t>() : 0); }
+  int64_t nbytes() const;  // total payload bytes incl. offsets
+};
+
+struct KMV {
+  KV keys;                 // unique keys (values unused: vw == 0)
+  at::Tensor vdata, voff;  // values in group order
+  int vw = 0;
+  at::Tensor seg;          // int64 [nkey+1]
+  int64_t nkey = 0, nval = 0;
+  int64_t nbytes() const;
+};
+
+// ------------------------------------------------------------------ construction
+KV empty_kv(at::Device dev, int kw = 0, int vw = 0);
+// from host/device tensors; widths inferred (offsets undefined => fixed width = numel/n)
+KV make_kv(at::Tensor kdata, c10::optional<at::Tensor> koff, at::Tensor vdata,
+           c10::optional<at::Tensor> voff, int64_t n, at::Device dev);
+KV kv_to(const KV& kv, at::Device dev);
+KV concat(const std::vector<KV>& parts, at::Device dev);
+KV to_var_keys(const KV& kv);
+KV to_var_values(const KV& kv);
+// offsets of a fixed-width column: [0, w, 2w, ...]
+at::Tensor fixed_offsets(int64_t n, int w, at::Device dev);
+
+// ------------------------------------------------------------------ primitives
+// exclusive scan returning n+1 entries (int64 result for int32/int64 input, uint32 for uint32)
+at::Tensor exclusive_scan(const at::Tensor& x);
+// stable sort of (u64 key, u32 val); returns (keys_sorted, vals_sorted, passes)
+std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& keys,
+                                                              const at::Tensor& vals, int begin_bit,
+                                                              int end_bit);
+at::Tensor hash32_keys(const KV& kv, uint32_t seed);   // lookup3 hashlittle
+at::Tensor hash64_keys(const KV& kv);                  // lookup3 hashlittle2
+// rows gathered by u32 permutation
+KV gather(const KV& kv, const at::Tensor& perm);
+at::Tensor gather_rows(const at::Tensor& data, const at::Tensor& off, int w, const at::Tensor& perm,
+                       at::Tensor* new_off);
+
+// ------------------------------------------------------------------ engine ops
+struct ConvertStats {
+  int64_t passes = 0;
+  int64_t collisions = 0;
+  bool exact = true;  // grouped on exact key bits (no hashing)
+};
+// group-by (MR-MPI convert): KV -> KMV. Order of unique keys: sorted by key
+// (fixed <= 8B keys) or by 64-bit hash (others).
+KMV convert(const KV& kv, ConvertStats* st = nullptr, int force_hash_bits = 64);
+// one value per key (MR-MPI clone)
+KMV clone(const KV& kv);
+// whole KV -> one KMV pair key -> [k0,v0,k1,v1,...] (MR-MPI collapse)
+KMV collapse(const KV& kv, const std::string& key);
+// KMV -> KV of (key, reduced value); op in {count,sum,min,max,first,last}
+KV reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype);
+// sort KV by key or value; flag as MR-MPI: 1 int,2 uint64,3 float,4 double,5 str,6 strn,
+// negative = descending; extra: 7 int64, 8 uint32
+KV sort_kv(const KV& kv, int flag, bool by_value);
+// sort values inside each KMV segment
+KMV sort_multivalues(const KMV& kmv, int flag);
+// KMV -> KV with one (key, value) per value (inverse of convert)
+KV expand(const KMV& kmv);
+
+// ------------------------------------------------------------------ shuffle
+struct ShuffleStats {
+  int64_t send_bytes = 0, recv_bytes = 0, send_pairs = 0, recv_pairs = 0;
+  double seconds = 0;
+};
+// destination rank per pair: hashlittle(key, kb, P) % P (MR-MPI default) or a
+// user-provided int32 dest tensor
+at::Tensor partition_dest(const KV& kv, int P, at::Tensor* counts);
+// all-to-all exchange of KV pairs to their destination ranks over the process
+// group (RCCL over xGMI for cuda tensors, gloo for cpu). pg may be null (P=1).
+KV exchange(const KV& kv, const at::Tensor& dest, const c10::intrusive_ptr<c10d::ProcessGroup>& pg,
+            ShuffleStats* st = nullptr);
+// MR-MPI aggregate: partition_dest + exchange
+KV aggregate(const KV& kv, const c10::intrusive_ptr<c10d::ProcessGroup>& pg, ShuffleStats* st = nullptr);
+// move everything to ranks 0..nprocs-1 (rank r sends to r % nprocs)
+KV gather_to(const KV& kv, int nprocs, const c10::intrusive_ptr<c10d::ProcessGroup>& pg,
+             ShuffleStats* st = nullptr);
+// root's KV replicated on every rank
+KV broadcast(const KV& kv, int root, const c10::intrusive_ptr<c10d::ProcessGroup>& pg);
+
+// ------------------------------------------------------------------ text / graph maps
+// InvertedIndex map over one text buffer (padded by >= 32 bytes): KV(url+NUL, int32 doc)
+KV map_urls(const at::Tensor& text, int64_t n, int32_t doc_id);
+// wordfreq map: KV(word+NUL, NULL)
+KV map_words(const at::Tensor& text, int64_t n);
+// R-MAT: KV(EDGE{u64,u64}, NULL)
+KV map_rmat(int64_t nedges, int nlevels, double a, double b, double c, double d, double fraction,
+            uint64_t seed, uint64_t first_edge, at::Device dev);
+
+}  // namespace mrh

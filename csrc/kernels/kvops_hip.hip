@@ -1,0 +1,267 @@
+#include "hip/hip_runtime.h"
+// KV/KMV data-movement kernels: sort-key construction, row gathers (fixed and
+// variable width), segment (group) boundary detection and group verification.
+// These replace KeyValue::add / KeyMultiValue::kv2kmv scatter loops of MR-MPI
+// (reference src/keyvalue.cpp:343-392, src/keymultivalue.cpp:1139-1209).
+#include "common.h"
+#include "launch.h"
+#include <cstdio>
+#include <cstdlib>
+
+namespace mrh {
+namespace k {
+namespace {
+
+constexpr int NT = 256;
+inline unsigned nblk(int64_t n, int per = NT) { return (unsigned)((n + per - 1) / per); }
+
+__device__ __forceinline__ uint64_t load_le(const uint8_t* p, int w) {
+  uint64_t v = 0;
+  for (int b = 0; b < w; ++b) v |= (uint64_t)p[b] << (8 * b);
+  return v;
+}
+
+__global__ __launch_bounds__(NT) void k_sortkeys_fixed(const uint8_t* __restrict__ d, int w, int64_t n,
+                                                      int mode, bool desc, uint64_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ idx) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  uint64_t raw;
+  if (w == 8) raw = *reinterpret_cast<const uint64_t*>(d + i * 8);
+  else if (w == 4) raw = *reinterpret_cast<const uint32_t*>(d + i * 4);
+  else raw = load_le(d + i * w, w);
+  uint64_t k = dev::sortkey_transform(raw, mode);
+  if (desc) k = ~k;
+  keys[i] = k;
+  idx[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(NT) void k_sortkeys_str(const uint8_t* __restrict__ d,
+                                                    const int64_t* __restrict__ off, int64_t n,
+                                                    int64_t start, bool desc, uint64_t* __restrict__ keys,
+                                                    uint32_t* __restrict__ idx) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  int64_t a = off[i] + start, b = off[i + 1];
+  uint64_t k = 0;
+  for (int j = 0; j < 8; ++j) {
+    uint64_t c = (a + j < b) ? d[a + j] : 0;
+    k = (k << 8) | c;
+  }
+  keys[i] = desc ? ~k : k;
+  idx[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(NT) void k_iota(uint32_t* __restrict__ idx, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i < n) idx[i] = (uint32_t)i;
+}
+
+template <typename T, typename I>
+__global__ __launch_bounds__(NT) void k_gather_words(const T* __restrict__ src, int words,
+                                                    const I* __restrict__ idx, int64_t n,
+                                                    T* __restrict__ dst) {
+  // one thread per (row, word); consecutive threads -> consecutive words of a row
+  int64_t t = (int64_t)blockIdx.x * NT + threadIdx.x;
+  int64_t total = n * words;
+  if (t >= total) return;
+  int64_t r = t / words;
+  int c = (int)(t - r * words);
+  dst[t] = src[(int64_t)idx[r] * words + c];
+}
+
+__global__ __launch_bounds__(NT) void k_var_lengths(const int64_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ idx, int64_t n,
+                                                   int32_t* __restrict__ len) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  uint32_t r = idx ? idx[i] : (uint32_t)i;
+  len[i] = (int32_t)(off[r + 1] - off[r]);
+}
+
+// 16 lanes per row, 4 rows per wave in flight.
+__global__ __launch_bounds__(NT) void k_var_copy(const uint8_t* __restrict__ src,
+                                                const int64_t* __restrict__ soff,
+                                                const uint32_t* __restrict__ idx, int64_t n,
+                                                uint8_t* __restrict__ dst,
+                                                const int64_t* __restrict__ doff) {
+  const int g = threadIdx.x & 15;
+  int64_t row = ((int64_t)blockIdx.x * NT + threadIdx.x) >> 4;
+  const int64_t stride = ((int64_t)gridDim.x * NT) >> 4;
+  for (; row < n; row += stride) {
+    uint32_t r = idx ? idx[row] : (uint32_t)row;
+    int64_t a = soff[r], len = soff[r + 1] - a;
+    int64_t o = doff[row];
+    for (int64_t j = g; j < len; j += 16) dst[o + j] = src[a + j];
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_head_flags(const uint64_t* __restrict__ keys, int64_t n,
+                                                  uint32_t* __restrict__ flags) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(NT) void k_compact_heads(const uint32_t* __restrict__ flags,
+                                                     const uint32_t* __restrict__ pos, int64_t n,
+                                                     int64_t* __restrict__ seg) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i < n && flags[i]) seg[pos[i]] = i;
+  if (i == 0) seg[pos[n]] = n;
+}
+
+__global__ __launch_bounds__(NT) void k_verify_var(const uint8_t* __restrict__ kd,
+                                                  const int64_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ perm,
+                                                  const uint32_t* __restrict__ flags,
+                                                  const uint32_t* __restrict__ pos,
+                                                  const int64_t* __restrict__ seg, int64_t n,
+                                                  unsigned long long* mism) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n || flags[i]) return;
+  int64_t h = seg[pos[i] - 1];
+  uint32_t a = perm[i], b = perm[h];
+  int64_t a0 = off[a], la = off[a + 1] - a0, b0 = off[b], lb = off[b + 1] - b0;
+  bool diff = la != lb;
+  for (int64_t j = 0; !diff && j < la; ++j) diff = kd[a0 + j] != kd[b0 + j];
+  if (diff) atomicAdd(mism, 1ull);
+}
+
+__global__ __launch_bounds__(NT) void k_verify_fixed(const uint8_t* __restrict__ kd, int kw,
+                                                    const uint32_t* __restrict__ perm,
+                                                    const uint32_t* __restrict__ flags,
+                                                    const uint32_t* __restrict__ pos,
+                                                    const int64_t* __restrict__ seg, int64_t n,
+                                                    unsigned long long* mism) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n || flags[i]) return;
+  int64_t h = seg[pos[i] - 1];
+  const uint8_t* pa = kd + (int64_t)perm[i] * kw;
+  const uint8_t* pb = kd + (int64_t)perm[h] * kw;
+  bool diff = false;
+  for (int j = 0; !diff && j < kw; ++j) diff = pa[j] != pb[j];
+  if (diff) atomicAdd(mism, 1ull);
+}
+
+__global__ __launch_bounds__(NT) void k_dest_bytes(const int32_t* __restrict__ dest,
+                                                  const int64_t* __restrict__ off, int64_t n, int P,
+                                                  int64_t* __restrict__ bytes) {
+  __shared__ unsigned long long hist[1024];
+  for (int i = threadIdx.x; i < P; i += NT) hist[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+    atomicAdd(&hist[dest[i]], (unsigned long long)(off[i + 1] - off[i]));
+  __syncthreads();
+  for (int i = threadIdx.x; i < P; i += NT)
+    if (hist[i]) atomicAdd((unsigned long long*)&bytes[i], hist[i]);
+}
+
+__global__ __launch_bounds__(NT) void k_off_to_len(const int64_t* __restrict__ off, int64_t n,
+                                                  int32_t* __restrict__ len) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i < n) len[i] = (int32_t)(off[i + 1] - off[i]);
+}
+
+template <typename I>
+void gather_fixed_t(const uint8_t* src, int w, const I* idx, int64_t n, uint8_t* dst, hipStream_t s) {
+  if (n <= 0 || w <= 0) return;
+  if (w % 8 == 0 && ((uintptr_t)src % 8 == 0) && ((uintptr_t)dst % 8 == 0)) {
+    int words = w / 8;
+    hipLaunchKernelGGL((k_gather_words<uint64_t, I>), dim3(nblk(n * words)), dim3(NT), 0, s,
+                       (const uint64_t*)src, words, idx, n, (uint64_t*)dst);
+  } else if (w % 4 == 0 && ((uintptr_t)src % 4 == 0) && ((uintptr_t)dst % 4 == 0)) {
+    int words = w / 4;
+    hipLaunchKernelGGL((k_gather_words<uint32_t, I>), dim3(nblk(n * words)), dim3(NT), 0, s,
+                       (const uint32_t*)src, words, idx, n, (uint32_t*)dst);
+  } else {
+    hipLaunchKernelGGL((k_gather_words<uint8_t, I>), dim3(nblk(n * w)), dim3(NT), 0, s, src, w, idx, n,
+                       dst);
+  }
+  MRH_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+void make_sortkeys_fixed(const uint8_t* data, int w, int64_t n, int mode, bool descending, uint64_t* keys,
+                         uint32_t* idx, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_sortkeys_fixed, dim3(nblk(n)), dim3(NT), 0, s, data, w, n, mode, descending, keys,
+                     idx);
+  MRH_CHECK_LAUNCH();
+}
+void make_sortkeys_strprefix(const uint8_t* data, const int64_t* off, int64_t n, int64_t start,
+                             bool descending, uint64_t* keys, uint32_t* idx, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_sortkeys_str, dim3(nblk(n)), dim3(NT), 0, s, data, off, n, start, descending, keys,
+                     idx);
+  MRH_CHECK_LAUNCH();
+}
+void iota_u32(uint32_t* idx, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_iota, dim3(nblk(n)), dim3(NT), 0, s, idx, n);
+  MRH_CHECK_LAUNCH();
+}
+void gather_fixed(const uint8_t* src, int w, const uint32_t* idx, int64_t n, uint8_t* dst, hipStream_t s) {
+  gather_fixed_t<uint32_t>(src, w, idx, n, dst, s);
+}
+void gather_fixed_i64idx(const uint8_t* src, int w, const int64_t* idx, int64_t n, uint8_t* dst,
+                         hipStream_t s) {
+  gather_fixed_t<int64_t>(src, w, idx, n, dst, s);
+}
+void gather_var_lengths(const int64_t* src_off, const uint32_t* idx, int64_t n, int32_t* len,
+                        hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_var_lengths, dim3(nblk(n)), dim3(NT), 0, s, src_off, idx, n, len);
+  MRH_CHECK_LAUNCH();
+}
+void gather_var_copy(const uint8_t* src, const int64_t* src_off, const uint32_t* idx, int64_t n,
+                     uint8_t* dst, const int64_t* dst_off, hipStream_t s) {
+  if (n <= 0) return;
+  unsigned g = nblk(n * 16);
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(k_var_copy, dim3(g), dim3(NT), 0, s, src, src_off, idx, n, dst, dst_off);
+  MRH_CHECK_LAUNCH();
+}
+void head_flags_u64(const uint64_t* keys, int64_t n, uint32_t* flags, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_head_flags, dim3(nblk(n)), dim3(NT), 0, s, keys, n, flags);
+  MRH_CHECK_LAUNCH();
+}
+void compact_heads(const uint32_t* flags, const uint32_t* pos, int64_t n, int64_t* seg, hipStream_t s) {
+  hipLaunchKernelGGL(k_compact_heads, dim3(n > 0 ? nblk(n) : 1), dim3(NT), 0, s, flags, pos, n, seg);
+  MRH_CHECK_LAUNCH();
+}
+void verify_groups_var(const uint8_t* kdata, const int64_t* koff, const uint32_t* perm, const uint32_t* flags,
+                       const uint32_t* pos, const int64_t* seg, int64_t n, unsigned long long* mism,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_verify_var, dim3(nblk(n)), dim3(NT), 0, s, kdata, koff, perm, flags, pos, seg, n,
+                     mism);
+  MRH_CHECK_LAUNCH();
+}
+void verify_groups_fixed(const uint8_t* kdata, int kw, const uint32_t* perm, const uint32_t* flags,
+                         const uint32_t* pos, const int64_t* seg, int64_t n, unsigned long long* mism,
+                         hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_verify_fixed, dim3(nblk(n)), dim3(NT), 0, s, kdata, kw, perm, flags, pos, seg, n,
+                     mism);
+  MRH_CHECK_LAUNCH();
+}
+void dest_byte_counts(const int32_t* dest, const int64_t* off, int64_t n, int P, int64_t* bytes,
+                      hipStream_t s) {
+  hipMemsetAsync(bytes, 0, sizeof(int64_t) * P, s);
+  if (n <= 0) return;
+  unsigned g = nblk(n);
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(k_dest_bytes, dim3(g), dim3(NT), 0, s, dest, off, n, P, bytes);
+  MRH_CHECK_LAUNCH();
+}
+void offsets_to_lengths(const int64_t* off, int64_t n, int32_t* len, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_off_to_len, dim3(nblk(n)), dim3(NT), 0, s, off, n, len);
+  MRH_CHECK_LAUNCH();
+}
+
+}  // namespace k
+}  // namespace mrh

@@ -1,0 +1,126 @@
+// Host-side launcher declarations for the hand-written CDNA4 (gfx950) kernels.
+//
+// Every launcher takes raw device pointers plus the HIP stream to run on; the
+// engine layer (csrc/engine/*.cpp) owns allocation through the ATen caching
+// allocator and always passes the current torch stream, so kernels, RCCL
+// collectives (issued by c10d on its own stream with event fences) and torch
+// ops are correctly ordered.
+//
+// The kernels replace the CPU hot loops of MR-MPI
+// and the CUDA/Thrust InvertedIndex map (K1-K5, /root/reference/cuda/InvertedIndex.cu:79-135,324-370).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace mrh {
+namespace k {
+
+// ---------------------------------------------------------------- scan.hip
+// Exclusive prefix sum. `out` has n+1 entries: out[n] = total. in/out may not alias.
+// temp must hold scan_temp_bytes(n) bytes.
+size_t scan_temp_bytes(int64_t n);
+void exclusive_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, void* temp, hipStream_t s);
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* temp, hipStream_t s);
+// lengths (int32) -> int64 offsets (n+1)
+void lengths_to_offsets(const int32_t* len, int64_t* off, int64_t n, void* temp, hipStream_t s);
+
+// ---------------------------------------------------------------- radix.hip
+// Stable LSD radix sort of (uint64 key, uint32 value) pairs over digits
+// [begin_bit, end_bit). Passes whose digit is constant over all keys are
+// skipped using a single up-front global histogram. Result ends in keys_out/vals_out.
+// temp must hold radix_temp_bytes(n) bytes. All buffers have n entries.
+size_t radix_temp_bytes(int64_t n);
+void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64_t* keys_out,
+                        uint32_t* vals_out, uint64_t* keys_alt, uint32_t* vals_alt, int64_t n,
+                        int begin_bit, int end_bit, void* temp, hipStream_t s,
+                        int* passes_run = nullptr);
+
+// ---------------------------------------------------------------- hash.hip
+// lookup3 hashlittle(key, len, seed) (bit-exact with Bob Jenkins' reference) per key.
+void hash32_fixed(const uint8_t* kdata, int kw, int64_t n, uint32_t seed, uint32_t* out, hipStream_t s);
+void hash32_var(const uint8_t* kdata, const int64_t* koff, int64_t n, uint32_t seed, uint32_t* out,
+                hipStream_t s);
+// 64-bit grouping hash (lookup3 hashlittle2: c<<32|b)
+void hash64_fixed(const uint8_t* kdata, int kw, int64_t n, uint64_t* out, hipStream_t s);
+void hash64_var(const uint8_t* kdata, const int64_t* koff, int64_t n, uint64_t* out, hipStream_t s);
+// destination rank = h % P, plus per-destination pair counts (atomic, LDS-aggregated)
+void partition_dest(const uint32_t* h, int64_t n, int P, int32_t* dest, int64_t* counts, hipStream_t s);
+
+// ---------------------------------------------------------------- kvops.hip
+// Sort-key construction: fixed-width keys (kw<=8) loaded little-endian into a
+// uint64 and transformed so that unsigned order == requested order.
+// mode: 0 raw unsigned LE, 1 int32, 2 uint64, 3 float, 4 double, 7 int64, 8 uint32
+// descending: bitwise NOT after transform. Also writes iota into idx.
+void make_sortkeys_fixed(const uint8_t* data, int w, int64_t n, int mode, bool descending,
+                         uint64_t* keys, uint32_t* idx, hipStream_t s);
+// String keys (flag 5/6): big-endian 8-byte prefix starting at byte `start` of each
+// key (zero padded); descending inverts.
+void make_sortkeys_strprefix(const uint8_t* data, const int64_t* off, int64_t n, int64_t start,
+                             bool descending, uint64_t* keys, uint32_t* idx, hipStream_t s);
+void iota_u32(uint32_t* idx, int64_t n, hipStream_t s);
+// rows of width w gathered by idx
+void gather_fixed(const uint8_t* src, int w, const uint32_t* idx, int64_t n, uint8_t* dst, hipStream_t s);
+void gather_fixed_i64idx(const uint8_t* src, int w, const int64_t* idx, int64_t n, uint8_t* dst,
+                         hipStream_t s);
+// variable rows: step 1 lengths in gathered order; step 2 copy bytes (dst_off already scanned)
+void gather_var_lengths(const int64_t* src_off, const uint32_t* idx, int64_t n, int32_t* len,
+                        hipStream_t s);
+void gather_var_copy(const uint8_t* src, const int64_t* src_off, const uint32_t* idx, int64_t n,
+                     uint8_t* dst, const int64_t* dst_off, hipStream_t s);
+// sorted u64 keys -> head flags (uint32 0/1)
+void head_flags_u64(const uint64_t* keys, int64_t n, uint32_t* flags, hipStream_t s);
+// head positions: seg[pos[i]] = i where flags[i]; seg[nseg] = n  (pos = exclusive scan of flags)
+void compact_heads(const uint32_t* flags, const uint32_t* pos, int64_t n, int64_t* seg, hipStream_t s);
+// after grouping by 64-bit hash: count elements whose key bytes differ from their group head
+void verify_groups_var(const uint8_t* kdata, const int64_t* koff, const uint32_t* perm,
+                       const uint32_t* flags, const uint32_t* pos, const int64_t* seg, int64_t n,
+                       unsigned long long* mismatches, hipStream_t s);
+void verify_groups_fixed(const uint8_t* kdata, int kw, const uint32_t* perm, const uint32_t* flags,
+                         const uint32_t* pos, const int64_t* seg, int64_t n,
+                         unsigned long long* mismatches, hipStream_t s);
+// per-destination byte totals of variable rows (for alltoallv byte splits)
+void dest_byte_counts(const int32_t* dest, const int64_t* off, int64_t n, int P, int64_t* bytes,
+                      hipStream_t s);
+// offsets -> int32 lengths
+void offsets_to_lengths(const int64_t* off, int64_t n, int32_t* len, hipStream_t s);
+
+// ---------------------------------------------------------------- segreduce.hip
+// Segmented reductions over KMV values (seg has nseg+1 entries).
+// op: 0 sum, 1 min, 2 max ; dtype: 0 int32, 1 int64, 2 float32, 3 float64
+void seg_reduce(const void* vals, int dtype, int op, const int64_t* seg, int64_t nseg, void* out,
+                hipStream_t s);
+void seg_count(const int64_t* seg, int64_t nseg, int32_t* out, hipStream_t s);
+
+// ---------------------------------------------------------------- text.hip
+// InvertedIndex map: find every `<a href="` in text[0,n) and emit the URL that
+// follows (up to the next '"' or end of text). Two passes: count, then emit.
+// Block tile = 4 KiB of text.
+int64_t url_num_tiles(int64_t n);
+void url_count(const uint8_t* text, int64_t n, uint32_t* tile_counts, hipStream_t s);
+// tile_off = exclusive scan of tile_counts (n_tiles+1)
+void url_emit_starts(const uint8_t* text, int64_t n, const uint32_t* tile_off, int64_t* starts,
+                     hipStream_t s);
+// per url: length (excl. terminator) -> key length incl. NUL
+void url_lengths(const uint8_t* text, int64_t n, const int64_t* starts, int64_t nurl,
+                 int32_t* keylen, hipStream_t s);
+void url_copy(const uint8_t* text, const int64_t* starts, const int64_t* koff, int64_t nurl,
+              uint8_t* kdata, hipStream_t s);
+// whitespace tokenizer (wordfreq): word starts/lengths; keys are word + NUL
+int64_t tok_num_tiles(int64_t n);
+void tok_count(const uint8_t* text, int64_t n, uint32_t* tile_counts, hipStream_t s);
+void tok_emit(const uint8_t* text, int64_t n, const uint32_t* tile_off, int64_t* starts,
+              int32_t* keylen, hipStream_t s);
+// copy `n` strings text[starts[i] .. +len-1] into kdata at koff[i], then NUL
+void copy_strings_nul(const uint8_t* text, const int64_t* starts, const int64_t* koff, int64_t n,
+                      uint8_t* kdata, hipStream_t s);
+void fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
+
+// ---------------------------------------------------------------- graph.hip
+// R-MAT edges: counter-based Philox RNG; edge e of stream `seed` is a pure
+// function of (seed, e). Writes (vi, vj) uint64 pairs.
+void rmat_edges(uint64_t* edges, int64_t nedges, int nlevels, float a, float b, float c, float d,
+                float fraction, uint64_t seed, uint64_t first_edge, hipStream_t s);
+
+}  // namespace k
+}  // namespace mrh

@@ -1,0 +1,31 @@
+"""Loader for the native engine extension (gpu_mapreduce_amd/_C*.so).
+
+There is deliberately NO pure-Python fallback: every data-plane op runs in
+the native engine (HIP/CDNA4 kernels on MI355X, host loops on CPU). If the
+extension is missing the import fails loudly with the build command.
+"""
+import importlib
+import os
+
+_here = os.path.dirname(os.path.abspath(__file__))
+
+
+def _load():
+    try:
+        import torch  # noqa: F401  (loads libtorch / HIP runtime first)
+        return importlib.import_module("gpu_mapreduce_amd._C")
+    except ImportError as e:  # pragma: no cover - exercised only on broken installs
+        raise ImportError(
+            "gpu_mapreduce_amd native extension not built. Run:\n"
+            "  PYTORCH_ROCM_ARCH=gfx950 python setup.py build_ext --inplace\n"
+            f"(from {os.path.dirname(_here)}); original error: {e}"
+        ) from e
+
+
+C = _load()
+
+
+def so_path():
+    """Path of the loaded native library (used by tests / smoke to prove the
+    HIP path is the one that ran)."""
+    return C.__file__

@@ -1,0 +1,131 @@
+"""Communicator: one process per MI355X, torch.distributed over RCCL/xGMI.
+
+Replaces MR-MPI's MPI_Comm plumbing (reference src/mapreduce.cpp:93-161) and
+the serial `mpistubs/` fake MPI (mpistubs/mpi.cpp:57-67): with no process
+group (world size 1) every collective is the identity.
+
+Backend choice is not a dispatch layer: device tensors go through the "nccl"
+backend (which IS RCCL on ROCm); the CPU engine path (tests, no GPU) uses
+"gloo". The native shuffle calls the c10d ProcessGroup directly from C++.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+_WORLD = None
+
+
+class Comm:
+    """Thin host-side view of a c10d process group plus the engine device."""
+
+    def __init__(self, group=None, device=None):
+        if group is None and dist.is_available() and dist.is_initialized():
+            group = dist.group.WORLD
+        self.group = group
+        if group is not None:
+            self.rank = dist.get_rank(group)
+            self.size = dist.get_world_size(group)
+            backend = dist.get_backend(group)
+        else:
+            self.rank, self.size, backend = 0, 1, None
+        self.backend = backend
+        if device is None:
+            if backend == "gloo" or not torch.cuda.is_available():
+                device = "cpu"
+            else:
+                device = f"cuda:{torch.cuda.current_device()}"
+        self.device = str(device)
+        self.is_cuda = self.device.startswith("cuda")
+        # the c10d ProcessGroup handed to the native shuffle (None when P == 1)
+        self.pg = group if (group is not None and self.size > 1) else None
+
+    # ---- scalar collectives (every MR op returns a global count) ----------
+    def _t(self, vals, dtype):
+        return torch.tensor(vals, dtype=dtype, device=self.device)
+
+    def allreduce(self, vals, op="sum", dtype=torch.int64):
+        scalar = not isinstance(vals, (list, tuple))
+        v = [vals] if scalar else list(vals)
+        if self.size == 1:
+            return v[0] if scalar else v
+        t = self._t(v, dtype)
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        dist.all_reduce(t, op=rop, group=self.group)
+        out = t.cpu().tolist()
+        return out[0] if scalar else out
+
+    def allgather(self, val, dtype=torch.float64):
+        if self.size == 1:
+            return [val]
+        t = self._t([val], dtype)
+        out = [torch.empty_like(t) for _ in range(self.size)]
+        dist.all_gather(out, t, group=self.group)
+        return [x.item() for x in out]
+
+    def barrier(self):
+        if self.size > 1:
+            if self.is_cuda:
+                # a 1-element allreduce on the device is the RCCL barrier
+                self.allreduce(0)
+            else:
+                dist.barrier(group=self.group)
+
+    def bcast_object(self, obj, root=0):
+        if self.size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=root, group=self.group,
+                                   device=torch.device(self.device) if self.is_cuda else None)
+        return lst[0]
+
+    def wtime(self):
+        if self.is_cuda:
+            torch.cuda.synchronize()
+        return time.perf_counter()
+
+    def split(self, color, key=0):
+        """MPI_Comm_split analog (OINK -partition worlds): new group per color."""
+        if self.size == 1:
+            return self
+        colors = self.allgather(float(color))
+        members = sorted(r for r, c in enumerate(colors) if c == float(color))
+        groups = {}
+        for c in sorted(set(colors)):
+            ranks = [r for r, cc in enumerate(colors) if cc == c]
+            groups[c] = dist.new_group(ranks, backend=self.backend)
+        return Comm(groups[float(color)], device=self.device) if members else None
+
+
+def init(backend=None, timeout_s=600):
+    """Initialise the process group from torchrun-style env vars
+    (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT), bind this process to
+    GPU LOCAL_RANK, and return a Comm. World size 1 needs no env at all."""
+    global _WORLD
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device(f"cuda:{torch.cuda.current_device()}")
+        dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    elif torch.cuda.is_available() and ws == 1:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    _WORLD = Comm()
+    return _WORLD
+
+
+def world():
+    global _WORLD
+    if _WORLD is None:
+        _WORLD = Comm()
+    return _WORLD
