@@ -1,0 +1,152 @@
+#!/usr/bin/env python3
+"""Headline benchmark: KV-pairs/sec (whole node) of InvertedIndex on MI355X.
+
+BASELINE.json metric: "KV-pairs/sec (whole node) for InvertedIndex +
+RMAT-2^26 PageRank at 1/2/4/8 MI355X"; config "InvertedIndex on 1 GB
+synthetic docs, 1xMI355X (map + local sort/reduce)" — weak scaling: every
+GPU owns 1 GiB of synthetic Wikipedia-like HTML in eight 128 MiB part files
+(the reference's part-file shape, cuda/InvertedIndex.cu:282).
+
+One step = the whole job, end to end, as the reference times it
+(cuda/InvertedIndex.cu:170-205): stream the part files host(pinned)->HBM,
+map (find `<a href="`, emit URL->file KVs), aggregate (RCCL all-to-all when
+N>1), convert (group by URL), reduce (format "url\\tfile ...\\n" lines on the
+GPU and copy the text back to host memory). Nothing is cached across steps.
+
+value = total URL KV pairs processed by all ranks / seconds per step.
+The reference publishes no KV/s; its end-to-end input throughput is
+0.85 GB/s aggregate on 20 GK104 GPUs (50 GB in 59.0 s), so
+`vs_baseline` compares our aggregate input GB/s with that number.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload invertedindex|pagerank|wordfreq]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+REF_GBPS = 50.0 * 1e9 / 59.0 / 1e9  # reference end-to-end InvertedIndex, 50 GB in 59.0 s (decimal GB)
+
+
+def _sync(comm):
+    if comm.is_cuda:
+        torch.cuda.synchronize()
+    comm.barrier()
+    if comm.is_cuda:
+        torch.cuda.synchronize()
+
+
+def bench_inverted_index(comm, args):
+    from gpu_mapreduce_amd import MapReduce
+    from gpu_mapreduce_amd.models.inverted_index import InvertedIndex
+    from gpu_mapreduce_amd.utils import synth
+
+    per_gpu = int(args.bytes_per_gpu)
+    gen_dev = comm.device
+    files = synth.html_corpus(per_gpu, file_bytes=args.file_bytes, seed=args.seed, rank=comm.rank, device=gen_dev,
+                              link_gap=args.link_gap)
+    if comm.is_cuda:
+        files = [(n, t.cpu().pin_memory()) for n, t in files]
+        torch.cuda.empty_cache()
+    in_bytes = sum(t.numel() for _, t in files)
+
+    def step():
+        mr = MapReduce(comm)
+        app = InvertedIndex(mr, files)
+        n = app.run()
+        return n, app
+
+    for _ in range(args.warmup):
+        step()
+    _sync(comm)
+    t0 = time.perf_counter()
+    nurl = 0
+    step_ms = []
+    app = None
+    for _ in range(args.steps):
+        del app
+        ts = time.perf_counter()
+        nurl, app = step()
+        step_ms.append(round((time.perf_counter() - ts) * 1e3, 3))
+    _sync(comm)
+    dt = (time.perf_counter() - t0) / args.steps
+    dt = comm.allreduce(dt, "max", dtype=torch.float64)
+    total_in = comm.allreduce(in_bytes, "sum")
+    phases = {}
+    if args.phases:  # separate, device-synced run for the stage breakdown (not the timed steps)
+        mr = MapReduce(comm)
+        InvertedIndex(mr, files).run(phases)
+        phases = {k: round(v * 1e3, 3) for k, v in phases.items()}
+    value = nurl / dt
+    gbps = total_in / dt / 1e9
+    return {
+        "metric": "KV-pairs/sec (whole node), InvertedIndex end-to-end",
+        "value": value,
+        "unit": "KV/s",
+        "ms_per_step": dt * 1e3,
+        "vs_baseline": gbps / REF_GBPS,
+        "baseline_note": "reference publishes no KV/s; vs_baseline = aggregate input GB/s "
+                         f"({gbps:.2f}) / reference end-to-end 0.847 GB/s (50 GB in 59 s on 20x GK104)",
+        "input_GBps": gbps,
+        "kv_pairs_per_step": nurl,
+        "unique_urls": app.nunique,
+        "stage_ms": phases,
+        "step_ms_rank0": step_ms,
+        "config": {"model": "InvertedIndex", "global_batch": total_in, "seq_len": args.file_bytes,
+                   "parallelism": f"dp{comm.size}", "bytes_per_gpu": per_gpu,
+                   "file_bytes": args.file_bytes, "link_gap": args.link_gap},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="invertedindex", choices=["invertedindex", "pagerank", "wordfreq"])
+    ap.add_argument("--bytes-per-gpu", type=float, default=float(1 << 30))
+    ap.add_argument("--file-bytes", type=int, default=128 << 20)
+    ap.add_argument("--link-gap", type=int, default=200)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--phases", type=int, default=1, help="also report a per-stage breakdown (extra run)")
+    ap.add_argument("--scale", type=int, default=26, help="pagerank: RMAT scale")
+    ap.add_argument("--iters", type=int, default=20, help="pagerank iterations per step")
+    args = ap.parse_args()
+
+    from gpu_mapreduce_amd.parallel import comm as pcomm
+    comm = pcomm.init()
+    if args.workload == "invertedindex":
+        res = bench_inverted_index(comm, args)
+    elif args.workload == "pagerank":
+        from gpu_mapreduce_amd.models.pagerank import bench_pagerank
+        res = bench_pagerank(comm, args)
+    else:
+        from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
+        res = bench_wordfreq(comm, args)
+    out = {
+        "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": comm.size,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": res.get("vs_baseline"),
+        "dtype": "bytes+int32 (no float compute in MapReduce)", "data": "synthetic", "config": res["config"],
+    }
+    for k, v in res.items():
+        if k not in out:
+            out[k] = v
+    if comm.rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

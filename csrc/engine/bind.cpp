@@ -267,6 +267,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                        uint64_t first, const std::string& dev) {
     return map_rmat(ne, nl, a, b, c, d, f, seed, first, at::Device(dev));
   });
+  m.def("inverted_index_format", &inverted_index_format);
   m.def("kv_iter", &kv_iter);
   m.def("kmv_iter", &kmv_iter);
   m.def("hip_compiled", []() { return true; });

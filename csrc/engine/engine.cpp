@@ -596,7 +596,7 @@ KMV collapse(const KV& kv_in, const std::string& key) {
   at::Tensor vdata;
   {
     int64_t tot = n ? scalar_i64(off, 2 * n) : 0;
-    at::Tensor row_of_byte = at::repeat_interleave(at::arange(2 * n, opt(dev, at::kLong)), lens, tot);
+    at::Tensor row_of_byte = at::repeat_interleave(at::arange(2 * n, opt(dev, at::kLong)), lens, 0, tot);
     at::Tensor within = at::arange(tot, opt(dev, at::kLong)) - off.narrow(0, 0, 2 * n).index_select(0, row_of_byte);
     vdata = comb.index_select(0, starts.index_select(0, row_of_byte) + within);
   }

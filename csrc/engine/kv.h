@@ -127,4 +127,7 @@ KV map_words(const at::Tensor& text, int64_t n);
 KV map_rmat(int64_t nedges, int nlevels, double a, double b, double c, double d, double fraction,
             uint64_t seed, uint64_t first_edge, at::Device dev);
 
+// ------------------------------------------------------------------ app epilogues
+at::Tensor inverted_index_format(const KMV& kmv, const at::Tensor& names, const at::Tensor& name_off);
+
 }  // namespace mrh

@@ -67,5 +67,75 @@ __device__ __forceinline__ T block_excl_scan(T v, T* sh, T* total) {
   return res;
 }
 
+// ---------------------------------------------------------------- unaligned byte-string access
+// 4 bytes starting at any address p (little-endian) from aligned dword loads
+// + v_alignbyte; never touches a dword that does not contain one of p..p+3.
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const uint32_t r = (uint32_t)(a & 3);
+  const uint32_t lo = w[0];
+  if (r == 0) return lo;
+  return __builtin_amdgcn_alignbyte(w[1], lo, r);
+}
+// 8 bytes starting at p
+__device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {
+  return (uint64_t)ld32u(p) | ((uint64_t)ld32u(p + 4) << 32);
+}
+
+// lookup3 over a device byte string with dword-wide loads (same result as
+// the byte-reader lookup3 in hashfn.h)
+__device__ __forceinline__ void lookup3_wide(const uint8_t* k, int64_t length, uint32_t* pc, uint32_t* pb) {
+  uint32_t a, b, c;
+  a = b = c = 0xdeadbeefu + (uint32_t)length + *pc;
+  c += *pb;
+  while (length > 12) {
+    a += ld32u(k);
+    b += ld32u(k + 4);
+    c += ld32u(k + 8);
+    MRH_L3_MIX(a, b, c);
+    length -= 12;
+    k += 12;
+  }
+  if (length == 0) { *pc = c; *pb = b; return; }
+  // tail: 1..12 bytes, read whole dwords that lie inside the string, bytes otherwise
+  uint32_t t[3] = {0, 0, 0};
+  int i = 0;
+  for (; i + 4 <= length; i += 4) t[i >> 2] = ld32u(k + i);
+  for (; i < length; ++i) t[i >> 2] |= (uint32_t)k[i] << (8 * (i & 3));
+  a += t[0]; b += t[1]; c += t[2];
+  MRH_L3_FINAL(a, b, c);
+  *pc = c;
+  *pb = b;
+}
+
+// index of the first byte == ch in [p, p+len), or len
+__device__ __forceinline__ int64_t find_byte(const uint8_t* p, int64_t len, uint8_t ch) {
+  int64_t j = 0;
+  const uint64_t pat = 0x0101010101010101ull * ch;
+  while (j < len && ((reinterpret_cast<uintptr_t>(p + j)) & 7)) {
+    if (p[j] == ch) return j;
+    ++j;
+  }
+  for (; j + 8 <= len; j += 8) {
+    uint64_t x = *reinterpret_cast<const uint64_t*>(p + j) ^ pat;
+    uint64_t t = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+    if (t) return j + (__builtin_ctzll(t) >> 3);
+  }
+  for (; j < len; ++j)
+    if (p[j] == ch) return j;
+  return len;
+}
+
+// byte-string equality with 8-byte loads
+__device__ __forceinline__ bool bytes_equal(const uint8_t* a, const uint8_t* b, int64_t len) {
+  int64_t j = 0;
+  for (; j + 8 <= len; j += 8)
+    if (ld64u(a + j) != ld64u(b + j)) return false;
+  for (; j < len; ++j)
+    if (a[j] != b[j]) return false;
+  return true;
+}
+
 }  // namespace dev
 }  // namespace mrh

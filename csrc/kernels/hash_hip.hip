@@ -29,7 +29,9 @@ __global__ __launch_bounds__(H_NT) void k_hash32_var(const uint8_t* __restrict__
   int64_t i = (int64_t)blockIdx.x * H_NT + threadIdx.x;
   if (i >= n) return;
   int64_t a = off[i], b = off[i + 1];
-  out[i] = dev::hashlittle(kd + a, b - a, seed);
+  uint32_t c = seed, bb = 0;
+  dev::lookup3_wide(kd + a, b - a, &c, &bb);
+  out[i] = c;
 }
 
 __global__ __launch_bounds__(H_NT) void k_hash64_fixed(const uint8_t* __restrict__ kd, int kw, int64_t n,
@@ -45,7 +47,9 @@ __global__ __launch_bounds__(H_NT) void k_hash64_var(const uint8_t* __restrict__
   int64_t i = (int64_t)blockIdx.x * H_NT + threadIdx.x;
   if (i >= n) return;
   int64_t a = off[i], b = off[i + 1];
-  out[i] = dev::hash64(kd + a, b - a);
+  uint32_t c = 0x9e3779b9u, bb = 0x7f4a7c15u;
+  dev::lookup3_wide(kd + a, b - a, &c, &bb);
+  out[i] = ((uint64_t)c << 32) | bb;
 }
 
 // dest = h % P with an LDS histogram per block (P <= 1024), one global atomic per bin per block.

@@ -122,9 +122,7 @@ __global__ __launch_bounds__(NT) void k_verify_var(const uint8_t* __restrict__ k
   int64_t h = seg[pos[i] - 1];
   uint32_t a = perm[i], b = perm[h];
   int64_t a0 = off[a], la = off[a + 1] - a0, b0 = off[b], lb = off[b + 1] - b0;
-  bool diff = la != lb;
-  for (int64_t j = 0; !diff && j < la; ++j) diff = kd[a0 + j] != kd[b0 + j];
-  if (diff) atomicAdd(mism, 1ull);
+  if (la != lb || !dev::bytes_equal(kd + a0, kd + b0, la)) atomicAdd(mism, 1ull);
 }
 
 __global__ __launch_bounds__(NT) void k_verify_fixed(const uint8_t* __restrict__ kd, int kw,

@@ -122,5 +122,13 @@ void fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 void rmat_edges(uint64_t* edges, int64_t nedges, int nlevels, float a, float b, float c, float d,
                 float fraction, uint64_t seed, uint64_t first_edge, hipStream_t s);
 
+// ---------------------------------------------------------------- apps.hip
+// InvertedIndex output formatting: "key\tname name ... \n" per KMV key.
+void ii_value_len(const int32_t* vals, int64_t nval, const int64_t* name_off, int32_t* lenv, hipStream_t s);
+void ii_key_len(const int64_t* koff, int64_t nseg, int32_t* lens, hipStream_t s);
+void ii_write(const uint8_t* kd, const int64_t* koff, const int32_t* vals, int64_t nval, const int64_t* seg,
+              int64_t nseg, const int64_t* cv, const int64_t* cs, const uint8_t* names, const int64_t* name_off,
+              uint8_t* out, hipStream_t s);
+
 }  // namespace k
 }  // namespace mrh

@@ -93,9 +93,9 @@ __global__ __launch_bounds__(NT) void k_url_len(const uint8_t* __restrict__ text
                                                int32_t* __restrict__ keylen) {
   int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
   if (i >= nurl) return;
-  int64_t a = starts[i], j = a;
-  while (j < n && text[j] != '"') ++j;
-  keylen[i] = (int32_t)(j - a + 1);  // + NUL terminator, as the reference's kv->add(url, len+1)
+  int64_t a = starts[i];
+  int64_t len = dev::find_byte(text + a, n - a, (uint8_t)'"');
+  keylen[i] = (int32_t)(len + 1);  // + NUL terminator, as the reference's kv->add(url, len+1)
 }
 
 __device__ __forceinline__ bool is_ws(uint32_t c) {

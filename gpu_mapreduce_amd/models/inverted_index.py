@@ -1,0 +1,162 @@
+"""InvertedIndex: URL -> list of files that link to it.
+
+Reference: cuda/InvertedIndex.cu (GPU map) — per rank, files
+part-%05d in [me*fpp, (me+1)*fpp) are read, every `<a href="URL"` is found on
+the GPU, URLs are copied back and added to the KV one by one on the host
+(:254-410), then aggregate (:182) -> convert (:186) -> reduce writes
+"url\\tfile file ... \\n" lines with one fopen per key (:463-513).
+
+MI355X design:
+  map       files stream host(pinned) -> HBM on a side HIP stream, double
+            buffered; the fused scan/extract kernels (csrc/kernels/text.hip)
+            emit KV(url+NUL, int32 file id) directly into HBM — no D2H, no
+            per-URL host loop;
+  aggregate hashlittle partition + RCCL all-to-all over xGMI (P > 1);
+  convert   64-bit hash radix sort-by-key + segment detection (+ exact check);
+  reduce    the output text is formatted on the GPU (apps.hip) and copied to
+            the host once; optionally written to `out_dir/InvertedIndex-P-me`.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .._ext import C
+from ..runtime import pools
+from ..runtime.mapreduce import MapReduce
+
+PAD = 64
+
+
+class InvertedIndex:
+    def __init__(self, mr: MapReduce, files, out_dir=None):
+        """files: list of (name, uint8 tensor) for THIS rank (host tensors —
+        ideally pinned — or device tensors)."""
+        self.mr = mr
+        self.files = files
+        self.out_dir = out_dir
+        # doc ids are global (rank-major) so a value means the same file name on
+        # every rank after the shuffle; the reference ships the name string itself
+        all_names = mr.comm.allgather_object([n for n, _ in files])
+        self.doc_base = sum(len(x) for x in all_names[: mr.me])
+        names = [n.encode() for lst in all_names for n in lst]
+        self.names = torch.frombuffer(bytearray(b"".join(names) or b"\0"), dtype=torch.uint8).clone()
+        lens = torch.tensor([0] + [len(n) for n in names], dtype=torch.int64)
+        self.name_off = torch.cumsum(lens, 0)
+        dev = mr.device
+        self.is_cuda = dev.startswith("cuda")
+        self.names_dev = self.names.to(dev)
+        self.name_off_dev = self.name_off.to(dev)
+        maxlen = max((t.numel() for _, t in files), default=0)
+        # two persistent staging buffers (double-buffered H2D); the PAD bytes
+        # past each file are read by the 16-byte scan windows but never matched
+        self.bufs = [pools.device_buffer(dev, maxlen + PAD, slot) for slot in range(2 if files else 0)]
+        self.copy_stream = torch.cuda.Stream() if self.is_cuda else None
+        self.output = None
+        self.nurls = 0
+
+    # -------------------------------------------------------------- map
+    def _map(self, itask, kv):
+        files = self.files
+        if not files:
+            return
+        if not self.is_cuda:
+            for fid, (_, t) in enumerate(files):
+                buf = self.bufs[0]
+                buf[: t.numel()].copy_(t)
+                buf[t.numel():t.numel() + PAD].zero_()
+                kv.add_kv(C.map_urls(buf, t.numel(), self.doc_base + fid))
+            return
+        main = torch.cuda.current_stream()
+        cs = self.copy_stream
+        ready = [torch.cuda.Event(), torch.cuda.Event()]
+        free = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def issue(i):
+            b = i & 1
+            t = files[i][1]
+            with torch.cuda.stream(cs):
+                if i >= 2:
+                    cs.wait_event(free[b])
+                self.bufs[b][: t.numel()].copy_(t, non_blocking=True)
+                ready[b].record(cs)
+
+        issue(0)
+        for i in range(len(files)):
+            if i + 1 < len(files):
+                issue(i + 1)
+            b = i & 1
+            main.wait_event(ready[b])
+            n = files[i][1].numel()
+            kv.add_kv(C.map_urls(self.bufs[b], n, self.doc_base + i))
+            free[b].record(main)
+
+    # -------------------------------------------------------------- reduce
+    def _reduce(self, kmv, kv):
+        text = C.inverted_index_format(kmv, self.names_dev, self.name_off_dev)
+        if self.is_cuda:
+            host = pools.pinned_buffer(text.numel())
+            host.copy_(text, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+        else:
+            host = text
+        self.output = host
+        if self.out_dir is not None:
+            os.makedirs(self.out_dir, exist_ok=True)
+            path = os.path.join(self.out_dir, f"InvertedIndex-{self.mr.nprocs}-{self.mr.me}")
+            with open(path, "wb") as f:
+                f.write(host.numpy().tobytes())
+            MapReduce.wsize += host.numel()
+
+    def run(self, phases=None):
+        """phases: optional dict; if given, per-stage seconds (device-synced)
+        are recorded under the reference's stage names (Map, Network I/O,
+        Sort/Hash, Reduce — chapter_final.pdf Fig. 4/5)."""
+        mr = self.mr
+        tick = _Ticker(phases, mr.comm)
+        # one map task per rank, each maps its own files (reference :175, :278-284)
+        self.nurls = mr.map(mr.nprocs, self._map)
+        tick("Map")
+        mr.aggregate()
+        tick("Network I/O")
+        self.nunique = mr.convert()
+        tick("Sort/Hash")
+        mr.reduce_batch(self._reduce)
+        tick("Reduce")
+        return self.nurls
+
+    def output_lines(self):
+        if self.output is None:
+            return []
+        return bytes(self.output.cpu().numpy()).decode("utf-8", "replace").splitlines()
+
+
+class _Ticker:
+    def __init__(self, phases, comm):
+        self.phases = phases
+        self.comm = comm
+        if phases is not None:
+            self.t = comm.wtime()
+
+    def __call__(self, name):
+        if self.phases is None:
+            return
+        t = self.comm.wtime()
+        self.phases[name] = self.phases.get(name, 0.0) + (t - self.t)
+        self.t = t
+
+
+def reference_inverted_index(files):
+    """Pure-Python oracle: {url: sorted list of file names} over all files."""
+    import re
+    idx = {}
+    pat = re.compile(rb'<a href="')
+    for name, t in files:
+        b = bytes(t.cpu().numpy())
+        for m in pat.finditer(b):
+            s = m.end()
+            e = b.find(b'"', s)
+            e = len(b) if e < 0 else e
+            idx.setdefault(b[s:e], []).append(name)
+    return {k: sorted(v) for k, v in idx.items()}

@@ -67,6 +67,13 @@ class Comm:
         dist.all_gather(out, t, group=self.group)
         return [x.item() for x in out]
 
+    def allgather_object(self, obj):
+        if self.size == 1:
+            return [obj]
+        out = [None] * self.size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
     def barrier(self):
         if self.size > 1:
             if self.is_cuda:

@@ -1,0 +1,181 @@
+"""Multi-process correctness of the distributed path (aggregate / collate /
+gather / broadcast / scrunch / mapstyle 2 / InvertedIndex) with world size 2
+and 3 over gloo on the CPU engine. The same C++ shuffle code runs over RCCL
+on MI355X (device tensors); only the c10d backend differs."""
+import collections
+import os
+import socket
+import struct
+import sys
+import traceback
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn_name, q):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import gpu_mapreduce_amd as g
+        comm = g.Comm(device="cpu")
+        res = globals()[fn_name](comm)
+        q.put((rank, "ok", res))
+    except Exception:
+        q.put((rank, "err", traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def run_world(fn_name, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, status, res = q.get(timeout=240)
+        assert status == "ok", res
+        out[r] = res
+    for p in ps:
+        p.join(60)
+    return out
+
+
+WORDS = [b"w%03d\0" % (i % 97) for i in range(5000)]
+
+
+def case_wordcount(comm):
+    import gpu_mapreduce_amd as g
+    mr = g.MapReduce(comm)
+    n = mr.map(7, lambda i, kv: [kv.add(w) for w in WORDS[i::7]])
+    nu = mr.collate()
+    mr.reduce("count")
+    local = {k: struct.unpack("<i", v)[0] for k, v in mr.kv_pairs()}
+    return n, nu, local
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_collate_wordcount(world):
+    out = run_world("case_wordcount", world)
+    total = {}
+    for r, (n, nu, local) in out.items():
+        assert n == len(WORDS)
+        assert nu == len(set(WORDS))
+        assert not (set(total) & set(local)), "key owned by two ranks"
+        total.update(local)
+    assert total == collections.Counter(WORDS)
+
+
+def case_fixed_and_var_mixed(comm):
+    """rank 0 emits fixed-width keys, others variable + one empty rank."""
+    import gpu_mapreduce_amd as g
+    mr = g.MapReduce(comm)
+
+    def m(i, kv):
+        if comm.rank == 0:
+            for j in range(100):
+                kv.add(struct.pack("<q", j % 10), struct.pack("<i", j))
+        elif comm.rank == 1:
+            for j in range(50):
+                kv.add(b"k" * (1 + j % 4), b"v" * (j % 3))
+    mr.map(comm.size, m)
+    mr.aggregate()
+    mr.convert()
+    return {k: len(v) for k, v in mr.kmv_pairs()}
+
+
+def test_mixed_layouts_and_empty_rank():
+    out = run_world("case_fixed_and_var_mixed", 3)
+    merged = collections.Counter()
+    for r, d in out.items():
+        for k, c in d.items():
+            merged[k] += c
+    assert sum(merged.values()) == 150
+    assert merged[struct.pack("<q", 3)] == 10
+    assert merged[b"kk"] == 13
+
+
+def case_gather_bcast(comm):
+    import gpu_mapreduce_amd as g
+    mr = g.MapReduce(comm)
+    mr.map(comm.size, lambda i, kv: [kv.add(struct.pack("<i", i * 100 + j), b"x" * j) for j in range(5)])
+    n1 = mr.gather(1)
+    local_after_gather = mr.kv.n
+    n2 = mr.broadcast(0)
+    local_after_bcast = mr.kv.n
+    keys = sorted(struct.unpack("<i", k)[0] for k, _ in mr.kv_pairs())
+    mr2 = g.MapReduce(comm)
+    mr2.map(comm.size, lambda i, kv: kv.add(struct.pack("<i", i), None))
+    n3 = mr2.scrunch(1, "all")
+    return n1, local_after_gather, n2, local_after_bcast, keys, n3, mr2.kmv.nval
+
+
+def test_gather_broadcast_scrunch():
+    out = run_world("case_gather_bcast", 3)
+    for r, (n1, lg, n2, lb, keys, n3, nv) in out.items():
+        assert n1 == 15
+        assert lg == (15 if r == 0 else 0)
+        assert n2 == 45 and lb == 15
+        assert keys == sorted(i * 100 + j for i in range(3) for j in range(5))
+        assert n3 == 3  # collapse makes one KMV pair per rank, even empty ones (reference semantics)
+        assert nv == (6 if r == 0 else 0)
+
+
+def case_mapstyle2(comm):
+    import gpu_mapreduce_amd as g
+    mr = g.MapReduce(comm)
+    mr.mapstyle = 2
+    mine = []
+    n = mr.map(40, lambda i, kv: (mine.append(i), kv.add(struct.pack("<i", i), None)))
+    return n, mine
+
+
+def test_mapstyle_dynamic_queue():
+    out = run_world("case_mapstyle2", 2)
+    allt = sorted(t for _, (n, mine) in out.items() for t in mine)
+    assert allt == list(range(40))
+    assert all(n == 40 for n, _ in out.values())
+
+
+def case_inverted_index(comm):
+    import gpu_mapreduce_amd as g
+    from gpu_mapreduce_amd.models.inverted_index import InvertedIndex, reference_inverted_index
+    from gpu_mapreduce_amd.utils import synth
+    files = synth.html_corpus(600_000, file_bytes=200_000, seed=11, rank=comm.rank, nurl=3000)
+    app = InvertedIndex(g.MapReduce(comm), files)
+    app.run()
+    got = {}
+    for line in app.output_lines():
+        url, rest = line.split("\t")
+        got[url] = rest.split()
+    ref = reference_inverted_index(files)
+    return got, {k.decode(): v for k, v in ref.items()}
+
+
+def test_inverted_index_distributed():
+    out = run_world("case_inverted_index", 2)
+    got, ref = {}, collections.defaultdict(list)
+    for r, (g_r, ref_r) in out.items():
+        assert not (set(got) & set(g_r))
+        got.update(g_r)
+        for k, v in ref_r.items():
+            ref[k].extend(v)
+    assert {k: sorted(v) for k, v in got.items()} == {k: sorted(v) for k, v in ref.items()}
