@@ -268,6 +268,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return map_rmat(ne, nl, a, b, c, d, f, seed, first, at::Device(dev));
   });
   m.def("inverted_index_format", &inverted_index_format);
+  m.def("segments_sorted", &segments_sorted);
+  m.def("pr_contrib", &mrh::pr_contrib);
+  m.def("pr_combine", &mrh::pr_combine);
+  m.def("scatter_f32", &mrh::scatter_f32);
+  m.def("pr_update", &mrh::pr_update);
   m.def("kv_iter", &kv_iter);
   m.def("kmv_iter", &kmv_iter);
   m.def("hip_compiled", []() { return true; });

@@ -485,6 +485,13 @@ at::Tensor seg_heads(const at::Tensor& seg, int64_t nseg) { return seg.narrow(0,
 
 }  // namespace
 
+at::Tensor segments_sorted(const at::Tensor& sorted_keys) {
+  at::Tensor flags, pos, seg;
+  int64_t nseg = 0;
+  segments_from_sorted(sorted_keys.contiguous(), &flags, &pos, &seg, &nseg);
+  return seg;
+}
+
 KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits) {
   const at::Device dev = kv.device();
   KMV out;
@@ -653,7 +660,7 @@ KV reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtyp
   if (opc < 0) fail("unknown builtin reduce op " + op);
   at::Tensor res = at::empty({ns * w}, opt(dev, at::kByte));
   if (dev.is_cuda()) {
-    k::seg_reduce(P0<void>(kmv.vdata), dc, opc, P0<int64_t>(seg), ns, P0<void>(res), cur_stream());
+    k::seg_reduce(P0<void>(kmv.vdata), dc, opc, P0<int64_t>(seg), ns, kmv.nval, P0<void>(res), cur_stream());
   } else if (ns) {
     const int64_t* sg = P0<int64_t>(seg);
     auto body = [&](auto* v, auto* o) {

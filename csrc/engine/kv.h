@@ -127,6 +127,18 @@ KV map_words(const at::Tensor& text, int64_t n);
 KV map_rmat(int64_t nedges, int nlevels, double a, double b, double c, double d, double fraction,
             uint64_t seed, uint64_t first_edge, at::Device dev);
 
+// ------------------------------------------------------------------ graph iteration (graph.cpp)
+void pr_contrib(const at::Tensor& seg, const at::Tensor& src, const at::Tensor& w, const at::Tensor& r,
+                at::Tensor& out);
+void pr_combine(const at::Tensor& seg, const at::Tensor& perm, const at::Tensor& recv, const at::Tensor& vid,
+                at::Tensor& acc);
+void scatter_f32(const at::Tensor& v, const at::Tensor& idx, at::Tensor& out);
+at::Tensor pr_update(const at::Tensor& acc, const at::Tensor& r, at::Tensor& rn, const at::Tensor& dangling,
+                     double base, double alpha, const at::Tensor& dmass, double invN, const at::Tensor& invdeg,
+                     at::Tensor& cout);
+// segment boundaries of a sorted int64 key column: seg[nseg+1]
+at::Tensor segments_sorted(const at::Tensor& sorted_keys);
+
 // ------------------------------------------------------------------ app epilogues
 at::Tensor inverted_index_format(const KMV& kmv, const at::Tensor& names, const at::Tensor& name_off);
 

@@ -88,7 +88,7 @@ void offsets_to_lengths(const int64_t* off, int64_t n, int32_t* len, hipStream_t
 // ---------------------------------------------------------------- segreduce.hip
 // Segmented reductions over KMV values (seg has nseg+1 entries).
 // op: 0 sum, 1 min, 2 max ; dtype: 0 int32, 1 int64, 2 float32, 3 float64
-void seg_reduce(const void* vals, int dtype, int op, const int64_t* seg, int64_t nseg, void* out,
+void seg_reduce(const void* vals, int dtype, int op, const int64_t* seg, int64_t nseg, int64_t nval, void* out,
                 hipStream_t s);
 void seg_count(const int64_t* seg, int64_t nseg, int32_t* out, hipStream_t s);
 
@@ -121,6 +121,18 @@ void fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
 // function of (seed, e). Writes (vi, vj) uint64 pairs.
 void rmat_edges(uint64_t* edges, int64_t nedges, int nlevels, float a, float b, float c, float d,
                 float fraction, uint64_t seed, uint64_t first_edge, hipStream_t s);
+
+// ---------------------------------------------------------------- graphops.hip
+size_t pr_scratch_bytes(int64_t nval);
+void pr_contrib(const int64_t* seg, int64_t nseg, int64_t nedge, const int32_t* src, const float* w, const float* r,
+                float* out, void* scratch, hipStream_t s);
+void pr_combine(const int64_t* seg, int64_t ngrp, int64_t nrecv, const int32_t* perm, const float* recv,
+                const int32_t* vid, float* grp, float* acc, void* scratch, hipStream_t s);
+void scatter_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s);
+int pr_update_blocks(int64_t n);
+void pr_update(const float* acc, const float* r, float* rn, const uint8_t* dangling, int64_t n, float base,
+               float alpha, const double* dmass, double invN, const float* invdeg, float* cout, double* partial,
+               hipStream_t s);
 
 // ---------------------------------------------------------------- apps.hip
 // InvertedIndex output formatting: "key\tname name ... \n" per KMV key.

@@ -1,0 +1,209 @@
+// Load-balanced, deterministic segmented reduction (device template).
+//
+// out[s] = OP over i in [seg[s], seg[s+1]) of get(i)
+//
+// Work is split by VALUES, not by segments: block b owns values
+// [b*TILE, (b+1)*TILE) whatever the segment lengths, so a 3M-value R-MAT hub
+// and a million 1-value segments cost the same per value (SURVEY §7.5 skew).
+//   pass 1 (k_segred_tiles): each thread reduces IT consecutive values; runs
+//     that are complete inside the thread are written directly; incomplete
+//     head/tail partials go to an LDS list in thread order, which the block
+//     folds per segment; segments complete inside the block are written, the
+//     block's first/last partial go to a carry array (2 per block);
+//   pass 2 (k_segred_carry): per segment crossing block boundaries, carries
+//     are folded in block order.
+// Every fold happens in a fixed order, so results are bitwise reproducible.
+// Segments must be non-empty (true for every KMV and CSR built by the engine).
+#pragma once
+#include "common.h"
+
+namespace mrh {
+namespace dev {
+
+constexpr int SR_NT = 256;
+constexpr int SR_IT = 16;
+constexpr int SR_TILE = SR_NT * SR_IT;
+
+template <typename T, int OP>
+struct RedOp;
+template <typename T>
+struct RedOp<T, 0> {
+  __device__ static T ident() { return T(0); }
+  __device__ static T f(T a, T b) { return a + b; }
+};
+template <typename T>
+struct RedOp<T, 1> {
+  __device__ static T ident();
+  __device__ static T f(T a, T b) { return b < a ? b : a; }
+};
+template <typename T>
+struct RedOp<T, 2> {
+  __device__ static T ident();
+  __device__ static T f(T a, T b) { return b > a ? b : a; }
+};
+template <> __device__ inline int32_t RedOp<int32_t, 1>::ident() { return 0x7fffffff; }
+template <> __device__ inline int32_t RedOp<int32_t, 2>::ident() { return (int32_t)0x80000000; }
+template <> __device__ inline int64_t RedOp<int64_t, 1>::ident() { return 0x7fffffffffffffffll; }
+template <> __device__ inline int64_t RedOp<int64_t, 2>::ident() { return (int64_t)0x8000000000000000ull; }
+template <> __device__ inline float RedOp<float, 1>::ident() { return 3.402823466e38f; }
+template <> __device__ inline float RedOp<float, 2>::ident() { return -3.402823466e38f; }
+template <> __device__ inline double RedOp<double, 1>::ident() { return 1.7976931348623157e308; }
+template <> __device__ inline double RedOp<double, 2>::ident() { return -1.7976931348623157e308; }
+
+// largest s in [0, nseg) with seg[s] <= i
+__device__ __forceinline__ int64_t seg_upper(const int64_t* __restrict__ seg, int64_t nseg, int64_t i) {
+  int64_t lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if (seg[mid] <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Block layout: values are fetched STRIPED (value b0 + j*NT + t by thread t:
+// coalesced index loads, 16 independent gathers in flight per thread) into
+// LDS, then reduced BLOCKED (IT consecutive values per thread). The segment
+// boundaries overlapping the block are staged in LDS once (two global binary
+// searches per block instead of one per thread).
+template <typename T, int OP, typename G>
+__global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __restrict__ seg, int64_t nseg,
+                                                        int64_t nval, T* __restrict__ out,
+                                                        int64_t* __restrict__ carry_seg, T* __restrict__ carry_val) {
+  using R = RedOp<T, OP>;
+  __shared__ int64_t lseg[SR_TILE + 2];
+  __shared__ T lval[SR_TILE];
+  __shared__ int64_t ls[2 * SR_NT];
+  __shared__ T lv[2 * SR_NT];
+  __shared__ int64_t sb_sh, ns_sh;
+  const int t = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * SR_TILE;
+  const int64_t b1 = min(b0 + (int64_t)SR_TILE, nval);
+  if (t == 0) {
+    int64_t sb = seg_upper(seg, nseg, b0);
+    int64_t se = seg_upper(seg, nseg, b1 - 1);
+    sb_sh = sb;
+    ns_sh = se - sb + 1;  // segments overlapping the block
+  }
+  // striped fetch of the block's values
+  T v[SR_IT];
+#pragma unroll
+  for (int j = 0; j < SR_IT; ++j) {
+    int64_t e = b0 + (int64_t)j * SR_NT + t;
+    v[j] = e < b1 ? get(e) : R::ident();
+  }
+#pragma unroll
+  for (int j = 0; j < SR_IT; ++j) lval[j * SR_NT + t] = v[j];
+  __syncthreads();
+  const int64_t sb = sb_sh, ns = ns_sh;
+  for (int64_t j = t; j <= ns; j += SR_NT) lseg[j] = seg[sb + j];
+  ls[2 * t] = -1;
+  ls[2 * t + 1] = -1;
+  __syncthreads();
+
+  const int64_t t0 = b0 + (int64_t)t * SR_IT;
+  const int64_t t1 = min(t0 + (int64_t)SR_IT, b1);
+  if (t0 < t1) {
+    // local segment of t0: largest q in [0, ns) with lseg[q] <= t0
+    int64_t lo = 0, hi = ns - 1;
+    while (lo < hi) {
+      int64_t mid = (lo + hi + 1) >> 1;
+      if (lseg[mid] <= t0) lo = mid;
+      else hi = mid - 1;
+    }
+    int64_t q = lo;
+    int64_t s_end = lseg[q + 1];
+    T acc = R::ident();
+    bool first_run = true;
+    for (int64_t i = t0; i < t1; ++i) {
+      while (i >= s_end) {  // close run of segment sb+q
+        if (lseg[q] >= t0) out[sb + q] = acc;  // started inside the thread: complete
+        else { ls[2 * t] = sb + q; lv[2 * t] = acc; }
+        first_run = false;
+        ++q;
+        s_end = lseg[q + 1];
+        acc = R::ident();
+      }
+      acc = R::f(acc, lval[i - b0]);
+    }
+    // last run of the thread ends at t1
+    const bool starts_inside = lseg[q] >= t0;
+    const bool ends_inside = s_end <= t1;
+    if (starts_inside && ends_inside) {
+      out[sb + q] = acc;
+    } else if (!starts_inside && first_run) {
+      ls[2 * t] = sb + q;  // one run covering the whole thread range
+      lv[2 * t] = acc;
+    } else {
+      ls[2 * t + 1] = sb + q;
+      lv[2 * t + 1] = acc;
+    }
+  }
+  __syncthreads();
+  // fold incomplete partials per segment, in thread order
+  for (int j = t; j < 2 * SR_NT; j += SR_NT) {
+    int64_t s = ls[j];
+    if (s < 0) continue;
+    int jp = j - 1;
+    while (jp >= 0 && ls[jp] < 0) --jp;
+    if (jp >= 0 && ls[jp] == s) continue;  // not the first entry of this segment
+    T acc = lv[j];
+    for (int k = j + 1; k < 2 * SR_NT; ++k) {
+      if (ls[k] < 0) continue;
+      if (ls[k] != s) break;
+      acc = R::f(acc, lv[k]);
+    }
+    bool inside = seg[s] >= b0 && seg[s + 1] <= b1;
+    if (inside) {
+      out[s] = acc;
+    } else {
+      // the block's first partial (segment started before b0) -> slot 0, else slot 1
+      int slot = seg[s] < b0 ? 0 : 1;
+      carry_seg[2 * blockIdx.x + slot] = s;
+      carry_val[2 * blockIdx.x + slot] = acc;
+    }
+  }
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(SR_NT) void k_segred_carry(const int64_t* __restrict__ carry_seg,
+                                                        const T* __restrict__ carry_val, int64_t ncarry,
+                                                        T* __restrict__ out) {
+  using R = RedOp<T, OP>;
+  int64_t j = (int64_t)blockIdx.x * SR_NT + threadIdx.x;
+  if (j >= ncarry) return;
+  int64_t s = carry_seg[j];
+  if (s < 0) return;
+  int64_t jp = j - 1;
+  while (jp >= 0 && carry_seg[jp] < 0) --jp;
+  if (jp >= 0 && carry_seg[jp] == s) return;
+  T acc = carry_val[j];
+  for (int64_t k = j + 1; k < ncarry; ++k) {
+    int64_t sk = carry_seg[k];
+    if (sk < 0) continue;
+    if (sk != s) break;
+    acc = R::f(acc, carry_val[k]);
+  }
+  out[s] = acc;
+}
+
+// host launcher: carry buffers need 2*nblocks entries each
+template <typename T, int OP, typename G>
+inline void segred_launch(G get, const int64_t* seg, int64_t nseg, int64_t nval, T* out, int64_t* carry_seg,
+                          T* carry_val, hipStream_t s) {
+  if (nseg <= 0 || nval <= 0) return;
+  int64_t nb = (nval + SR_TILE - 1) / SR_TILE;
+  hipMemsetAsync(carry_seg, 0xff, sizeof(int64_t) * 2 * nb, s);  // -1
+  hipLaunchKernelGGL((k_segred_tiles<T, OP, G>), dim3((unsigned)nb), dim3(SR_NT), 0, s, get, seg, nseg, nval, out,
+                     carry_seg, carry_val);
+  MRH_CHECK_LAUNCH();
+  int64_t nc = 2 * nb;
+  hipLaunchKernelGGL((k_segred_carry<T, OP>), dim3((unsigned)((nc + SR_NT - 1) / SR_NT)), dim3(SR_NT), 0, s,
+                     carry_seg, carry_val, nc, out);
+  MRH_CHECK_LAUNCH();
+}
+
+inline size_t segred_carry_entries(int64_t nval) { return 2 * (size_t)((nval + SR_TILE - 1) / SR_TILE) + 2; }
+
+}  // namespace dev
+}  // namespace mrh

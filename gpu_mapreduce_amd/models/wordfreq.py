@@ -1,0 +1,149 @@
+"""wordfreq: word counts + global top-N (reference examples/wordfreq.cpp:42-97,
+oink/wordfreq.cpp:40-90).
+
+Reference pipeline: map(files, strtok words) -> collate -> reduce(count) ->
+sort_values(-1) -> local top 10 -> gather(1) -> sort_values(-1) -> print.
+
+MI355X pipeline (same op sequence on device-resident data):
+  map       text chunks stream host->HBM (double buffered), the whitespace
+            tokenizer kernel emits KV(word+NUL, NULL) in HBM;
+  compress  optional local combiner: convert + count (MR-MPI compress), so the
+            shuffle moves (word, count) once per distinct word per rank;
+  collate   hashlittle partition + RCCL all-to-all + group-by;
+  reduce    "sum:int32" (or "count" without the combiner) segmented reduce;
+  top-N     sort_values(-1) (radix on negated counts) -> slice -> gather(1) ->
+            sort_values(-1).
+"""
+from __future__ import annotations
+
+import struct
+import time
+
+import torch
+
+from .._ext import C
+from ..runtime import pools
+from ..runtime.mapreduce import MapReduce
+
+PAD = 64
+
+
+class WordFreq:
+    def __init__(self, mr: MapReduce, chunks, ntop=10, combiner=True):
+        """chunks: list of uint8 text tensors for this rank (host, ideally pinned)."""
+        self.mr = mr
+        self.chunks = chunks
+        self.ntop = ntop
+        self.combiner = combiner
+        self.is_cuda = mr.device.startswith("cuda")
+        maxlen = max((t.numel() for t in chunks), default=0)
+        self.bufs = [pools.device_buffer(mr.device, maxlen + PAD, 8 + s) for s in range(2 if chunks else 0)]
+        self.copy_stream = torch.cuda.Stream() if self.is_cuda else None
+
+    def _map(self, itask, kv):
+        if not self.chunks:
+            return
+        if not self.is_cuda:
+            for t in self.chunks:
+                b = self.bufs[0]
+                b[: t.numel()].copy_(t)
+                b[t.numel():t.numel() + PAD].zero_()
+                kv.add_kv(C.map_words(b, t.numel()))
+            return
+        main = torch.cuda.current_stream()
+        cs = self.copy_stream
+        ready = [torch.cuda.Event(), torch.cuda.Event()]
+        free = [torch.cuda.Event(), torch.cuda.Event()]
+
+        def issue(i):
+            b = i & 1
+            with torch.cuda.stream(cs):
+                if i >= 2:
+                    cs.wait_event(free[b])
+                self.bufs[b][: self.chunks[i].numel()].copy_(self.chunks[i], non_blocking=True)
+                ready[b].record(cs)
+
+        issue(0)
+        for i in range(len(self.chunks)):
+            if i + 1 < len(self.chunks):
+                issue(i + 1)
+            b = i & 1
+            main.wait_event(ready[b])
+            kv.add_kv(C.map_words(self.bufs[b], self.chunks[i].numel()))
+            free[b].record(main)
+
+    def run(self):
+        mr = self.mr
+        self.nwords = mr.map(mr.nprocs, self._map)
+        if self.combiner:
+            mr.compress("count")          # (word, local count)
+            self.nunique = mr.collate()
+            mr.reduce("sum:int32")
+        else:
+            self.nunique = mr.collate()
+            mr.reduce("count")
+        mr.sort_values(-1)
+        ntop = self.ntop
+
+        def keep_top(src, kv):
+            n = min(ntop, src.n)
+            if n == 0:
+                return
+            koff = src.koff[: n + 1]
+            kv.add_tensors(src.kdata[: int(koff[-1].item())], src.vdata[: 4 * n].view(torch.int32), koff=koff)
+        mr.map_mr_batch(mr, keep_top)
+        mr.gather(1)
+        mr.sort_values(-1)
+        self.top = [(k.rstrip(b"\0").decode("utf-8", "replace"), struct.unpack("<i", v)[0])
+                    for k, v in mr.kv_pairs()][:ntop]
+        return self.nwords
+
+
+def bench_wordfreq(comm, args):
+    from ..utils import synth
+    per_gpu = int(args.bytes_per_gpu)
+    chunk = int(args.file_bytes)
+    chunks = []
+    left = per_gpu
+    i = 0
+    while left > 0:
+        n = min(chunk, left)
+        t = synth.zipf_text(n, seed=args.seed * 7919 + comm.rank * 1000 + i, device=comm.device)
+        chunks.append(t.cpu().pin_memory() if comm.is_cuda else t)
+        left -= n
+        i += 1
+    if comm.is_cuda:
+        torch.cuda.empty_cache()
+
+    def step():
+        app = WordFreq(MapReduce(comm), chunks)
+        app.run()
+        return app
+
+    for _ in range(args.warmup):
+        step()
+    if comm.is_cuda:
+        torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        app = step()
+    if comm.is_cuda:
+        torch.cuda.synchronize()
+    comm.barrier()
+    dt = comm.allreduce((time.perf_counter() - t0) / args.steps, "max", dtype=torch.float64)
+    total = comm.allreduce(per_gpu, "sum")
+    return {
+        "metric": "KV-pairs/sec (whole node), wordfreq words counted end-to-end",
+        "value": app.nwords / dt,
+        "unit": "KV/s",
+        "ms_per_step": dt * 1e3,
+        "vs_baseline": None,
+        "baseline_note": "reference publishes no wordfreq number",
+        "input_GBps": total / dt / 1e9,
+        "words": app.nwords,
+        "unique_words": app.nunique,
+        "top3": app.top[:3],
+        "config": {"model": "wordfreq", "global_batch": total, "seq_len": chunk,
+                   "parallelism": f"dp{comm.size}", "bytes_per_gpu": per_gpu},
+    }

@@ -170,6 +170,32 @@ def case_inverted_index(comm):
     return got, {k.decode(): v for k, v in ref.items()}
 
 
+def case_pagerank(comm):
+    import numpy as np
+    import gpu_mapreduce_amd as g
+    from gpu_mapreduce_amd.models.pagerank import PageRank, rmat_map
+    mr = g.MapReduce(comm)
+    rmat_map(mr, 9, 8, seed=5)
+    edges = mr.kv.kdata.view(torch.int64).view(-1, 2).numpy().copy()
+    pr = PageRank(mr, 1 << 9).build()
+    pr.run(12)
+    ids, r = pr.ranks()
+    return edges, ids.numpy(), r.numpy().copy()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pagerank_distributed(world):
+    import numpy as np
+    from gpu_mapreduce_amd.models.pagerank import reference_pagerank
+    out = run_world("case_pagerank", world)
+    edges = np.concatenate([out[r][0] for r in range(world)])
+    ref = reference_pagerank(edges, 1 << 9, iters=12)
+    got = np.zeros(1 << 9)
+    for r in range(world):
+        got[out[r][1]] = out[r][2]
+    np.testing.assert_allclose(got, ref, rtol=2e-4, atol=1e-9)
+
+
 def test_inverted_index_distributed():
     out = run_world("case_inverted_index", 2)
     got, ref = {}, collections.defaultdict(list)
