@@ -273,6 +273,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pr_combine", &mrh::pr_combine);
   m.def("scatter_f32", &mrh::scatter_f32);
   m.def("pr_update", &mrh::pr_update);
+  m.def("plan_gather_reduce", &mrh::plan_gather_reduce);
+  m.def("plan_combine", &mrh::plan_combine);
+  m.def("wedges", &mrh::wedges);
   m.def("kv_iter", &kv_iter);
   m.def("kmv_iter", &kmv_iter);
   m.def("hip_compiled", []() { return true; });

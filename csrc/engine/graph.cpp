@@ -116,4 +116,105 @@ at::Tensor pr_update(const at::Tensor& acc, const at::Tensor& r, at::Tensor& rn,
   return at::tensor({d, dm}, opt(at::kCPU, at::kDouble));
 }
 
+namespace {
+int dcode(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kLong: return 1;
+    case at::kFloat: return 2;
+    case at::kDouble: return 3;
+    default: throw std::runtime_error("mrhip plan: dtype must be int64, float32 or float64");
+  }
+}
+template <typename T>
+T red(int op, T a, T b) {
+  return op == 0 ? a + b : op == 1 ? (b < a ? b : a) : (b > a ? b : a);
+}
+}  // namespace
+
+// out[g] = OP_{e in seg g} (x[src[e]] (+ w[e]))
+void plan_gather_reduce(const at::Tensor& seg, const at::Tensor& src, const at::Tensor& x, const at::Tensor& w,
+                        int64_t op, at::Tensor& out) {
+  const int64_t ng = seg.numel() - 1, ne = src.numel();
+  const bool hw = w.defined() && w.numel() > 0;
+  need(!hw || w.scalar_type() == x.scalar_type(), "plan weights must match value dtype");
+  need(out.scalar_type() == x.scalar_type() && out.numel() >= ng, "plan out");
+  if (ng <= 0) return;
+  if (seg.is_cuda()) {
+    at::Tensor scratch = at::empty({(int64_t)k::plan_scratch_bytes(ne)}, opt(seg.device(), at::kByte));
+    k::plan_gather_reduce(dcode(x), P0<int64_t>(seg), ng, ne, P0<int32_t>(src), x.data_ptr(),
+                          hw ? w.data_ptr() : nullptr, (int)op, out.data_ptr(), P0<void>(scratch), cur());
+    return;
+  }
+  AT_DISPATCH_ALL_TYPES(x.scalar_type(), "plan_gather_reduce", [&] {
+    const int64_t* sg = P0<int64_t>(seg);
+    const int32_t* s = P0<int32_t>(src);
+    const scalar_t* xp = x.data_ptr<scalar_t>();
+    const scalar_t* wp = hw ? w.data_ptr<scalar_t>() : nullptr;
+    scalar_t* o = out.data_ptr<scalar_t>();
+    for (int64_t g = 0; g < ng; ++g) {
+      scalar_t acc = xp[s[sg[g]]] + (wp ? wp[sg[g]] : scalar_t(0));
+      for (int64_t e = sg[g] + 1; e < sg[g + 1]; ++e) acc = red<scalar_t>((int)op, acc, xp[s[e]] + (wp ? wp[e] : scalar_t(0)));
+      o[g] = acc;
+    }
+  });
+}
+
+// acc[vid[g]] = OP_{i in seg g} recv[perm[i]]
+void plan_combine(const at::Tensor& seg, const at::Tensor& perm, const at::Tensor& recv, const at::Tensor& vid,
+                  int64_t op, at::Tensor& acc) {
+  const int64_t ng = seg.numel() - 1, nr = perm.numel();
+  if (ng <= 0) return;
+  if (seg.is_cuda()) {
+    at::Tensor grp = at::empty({ng}, recv.options());
+    at::Tensor scratch = at::empty({(int64_t)k::plan_scratch_bytes(nr)}, opt(seg.device(), at::kByte));
+    k::plan_combine(dcode(recv), P0<int64_t>(seg), ng, nr, P0<int32_t>(perm), recv.data_ptr(), P0<int32_t>(vid),
+                    (int)op, grp.data_ptr(), acc.data_ptr(), P0<void>(scratch), cur());
+    return;
+  }
+  AT_DISPATCH_ALL_TYPES(recv.scalar_type(), "plan_combine", [&] {
+    const int64_t* sg = P0<int64_t>(seg);
+    const int32_t* pp = P0<int32_t>(perm);
+    const scalar_t* rv = recv.data_ptr<scalar_t>();
+    const int32_t* vp = P0<int32_t>(vid);
+    scalar_t* a = acc.data_ptr<scalar_t>();
+    for (int64_t g = 0; g < ng; ++g) {
+      scalar_t x = rv[pp[sg[g]]];
+      for (int64_t i = sg[g] + 1; i < sg[g + 1]; ++i) x = red<scalar_t>((int)op, x, rv[pp[i]]);
+      a[vp[g]] = x;
+    }
+  });
+}
+
+// all neighbour pairs per group: returns (edges [W,2] int64 (min,max), centre [W])
+std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre) {
+  const int64_t ng = seg.numel() - 1;
+  at::Tensor d = seg.narrow(0, 1, ng) - seg.narrow(0, 0, ng);
+  at::Tensor cnt = at::floor_divide(d * (d - 1), 2);
+  at::Tensor wscan = exclusive_scan(cnt.contiguous());
+  const int64_t nw = ng > 0 ? wscan[ng].item<int64_t>() : 0;
+  at::Tensor oe = at::empty({nw, 2}, nb.options());
+  at::Tensor oc = at::empty({nw}, nb.options());
+  if (nw == 0) return {oe, oc};
+  if (seg.is_cuda()) {
+    k::wedges(P0<int64_t>(seg), P0<int64_t>(wscan), ng, P0<int64_t>(nb), P0<int64_t>(centre), nw, P0<int64_t>(oe),
+              P0<int64_t>(oc), cur());
+    return {oe, oc};
+  }
+  const int64_t* sg = P0<int64_t>(seg);
+  const int64_t* n = P0<int64_t>(nb);
+  const int64_t* c = P0<int64_t>(centre);
+  int64_t* e = P0<int64_t>(oe);
+  int64_t* co = P0<int64_t>(oc);
+  int64_t w = 0;
+  for (int64_t g = 0; g < ng; ++g)
+    for (int64_t j = sg[g]; j < sg[g + 1]; ++j)
+      for (int64_t k2 = j + 1; k2 < sg[g + 1]; ++k2) {
+        uint64_t a = (uint64_t)n[j], b = (uint64_t)n[k2];
+        e[2 * w] = (int64_t)(a < b ? a : b);
+        e[2 * w + 1] = (int64_t)(a < b ? b : a);
+        co[w++] = c[g];
+      }
+  return {oe, oc};
+}
+
 }  // namespace mrh

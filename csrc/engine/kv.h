@@ -136,6 +136,11 @@ void scatter_f32(const at::Tensor& v, const at::Tensor& idx, at::Tensor& out);
 at::Tensor pr_update(const at::Tensor& acc, const at::Tensor& r, at::Tensor& rn, const at::Tensor& dangling,
                      double base, double alpha, const at::Tensor& dmass, double invN, const at::Tensor& invdeg,
                      at::Tensor& cout);
+void plan_gather_reduce(const at::Tensor& seg, const at::Tensor& src, const at::Tensor& x, const at::Tensor& w,
+                        int64_t op, at::Tensor& out);
+void plan_combine(const at::Tensor& seg, const at::Tensor& perm, const at::Tensor& recv, const at::Tensor& vid,
+                  int64_t op, at::Tensor& acc);
+std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre);
 // segment boundaries of a sorted int64 key column: seg[nseg+1]
 at::Tensor segments_sorted(const at::Tensor& sorted_keys);
 

@@ -85,7 +85,120 @@ __global__ __launch_bounds__(NT) void k_pr_update(const float* __restrict__ acc,
   }
 }
 
+// generic plan getters: value carried by edge e = x[src[e]] (+ w[e])
+template <typename T>
+struct XWGet {
+  const int32_t* src;
+  const T* x;
+  const T* w;
+  __device__ __forceinline__ T operator()(int64_t i) const {
+    T v = x[__builtin_nontemporal_load(src + i)];
+    return w ? v + w[i] : v;
+  }
+};
+template <typename T>
+struct PermGetT {
+  const int32_t* perm;
+  const T* v;
+  __device__ __forceinline__ T operator()(int64_t i) const { return v[perm[i]]; }
+};
+template <typename T>
+__global__ __launch_bounds__(NT) void k_scatter_t(const T* __restrict__ v, const int32_t* __restrict__ idx, int64_t n,
+                                                 T* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i < n) out[idx[i]] = v[i];
+}
+
+// Wedges of tri_find (reference oink/tri_find.cpp:207-276, O(d^2) per vertex):
+// for group g with neighbour list nb[seg[g]..seg[g+1]) emit every pair
+// (min, max) with value = centre key[g]. One thread per wedge: the wedge's
+// group is found by binary search over the exclusive scan of C(d,2), then the
+// pair (j, k) is decoded from the triangular index — load-balanced whatever
+// the degree skew.
+__global__ __launch_bounds__(NT) void k_wedges(const int64_t* __restrict__ seg, const int64_t* __restrict__ wscan,
+                                              int64_t ngrp, const int64_t* __restrict__ nb,
+                                              const int64_t* __restrict__ centre, int64_t nwedge,
+                                              int64_t* __restrict__ out_edge, int64_t* __restrict__ out_centre) {
+  int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (w >= nwedge) return;
+  int64_t lo = 0, hi = ngrp - 1;
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if (wscan[mid] <= w) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t g = lo;
+  const int64_t t = w - wscan[g];
+  const int64_t d = seg[g + 1] - seg[g];
+  // row j has (d-1-j) pairs; find j with S(j) <= t < S(j+1), S(j) = j*(2d-j-1)/2
+  double dd = (double)(2 * d - 1);
+  int64_t j = (int64_t)floor((dd - sqrt(dd * dd - 8.0 * (double)t)) * 0.5);
+  if (j < 0) j = 0;
+  while (j > 0 && j * (2 * d - j - 1) / 2 > t) --j;
+  while ((j + 1) * (2 * d - j - 2) / 2 <= t) ++j;
+  const int64_t k = j + 1 + (t - j * (2 * d - j - 1) / 2);
+  const int64_t a = nb[seg[g] + j], b = nb[seg[g] + k];
+  const bool lt = (uint64_t)a < (uint64_t)b;
+  out_edge[2 * w] = lt ? a : b;
+  out_edge[2 * w + 1] = lt ? b : a;
+  out_centre[w] = centre[g];
+}
+
 }  // namespace
+
+template <typename T>
+void plan_gather_reduce_t(const int64_t* seg, int64_t nseg, int64_t ne, const int32_t* src, const T* x, const T* w,
+                          int op, T* out, void* scratch, hipStream_t s) {
+  size_t nc = dev::segred_carry_entries(ne);
+  int64_t* cs = reinterpret_cast<int64_t*>(scratch);
+  T* cv = reinterpret_cast<T*>(reinterpret_cast<char*>(scratch) + nc * sizeof(int64_t));
+  XWGet<T> g{src, x, w};
+  if (op == 0) dev::segred_launch<T, 0>(g, seg, nseg, ne, out, cs, cv, s);
+  else if (op == 1) dev::segred_launch<T, 1>(g, seg, nseg, ne, out, cs, cv, s);
+  else dev::segred_launch<T, 2>(g, seg, nseg, ne, out, cs, cv, s);
+}
+template <typename T>
+void plan_combine_t(const int64_t* seg, int64_t ngrp, int64_t nrecv, const int32_t* perm, const T* recv,
+                    const int32_t* vid, int op, T* grp, T* acc, void* scratch, hipStream_t s) {
+  size_t nc = dev::segred_carry_entries(nrecv);
+  int64_t* cs = reinterpret_cast<int64_t*>(scratch);
+  T* cv = reinterpret_cast<T*>(reinterpret_cast<char*>(scratch) + nc * sizeof(int64_t));
+  PermGetT<T> g{perm, recv};
+  if (op == 0) dev::segred_launch<T, 0>(g, seg, ngrp, nrecv, grp, cs, cv, s);
+  else if (op == 1) dev::segred_launch<T, 1>(g, seg, ngrp, nrecv, grp, cs, cv, s);
+  else dev::segred_launch<T, 2>(g, seg, ngrp, nrecv, grp, cs, cv, s);
+  if (ngrp > 0)
+    hipLaunchKernelGGL(k_scatter_t<T>, dim3((unsigned)((ngrp + NT - 1) / NT)), dim3(NT), 0, s, grp, vid, ngrp, acc);
+  MRH_CHECK_LAUNCH();
+}
+
+size_t plan_scratch_bytes(int64_t n) { return dev::segred_carry_entries(n) * 16 + 64; }
+
+void plan_gather_reduce(int dtype, const int64_t* seg, int64_t nseg, int64_t ne, const int32_t* src, const void* x,
+                        const void* w, int op, void* out, void* scratch, hipStream_t s) {
+  if (nseg <= 0) return;
+  switch (dtype) {
+    case 1: plan_gather_reduce_t<int64_t>(seg, nseg, ne, src, (const int64_t*)x, (const int64_t*)w, op, (int64_t*)out, scratch, s); break;
+    case 2: plan_gather_reduce_t<float>(seg, nseg, ne, src, (const float*)x, (const float*)w, op, (float*)out, scratch, s); break;
+    default: plan_gather_reduce_t<double>(seg, nseg, ne, src, (const double*)x, (const double*)w, op, (double*)out, scratch, s); break;
+  }
+}
+void plan_combine(int dtype, const int64_t* seg, int64_t ngrp, int64_t nrecv, const int32_t* perm, const void* recv,
+                  const int32_t* vid, int op, void* grp, void* acc, void* scratch, hipStream_t s) {
+  if (ngrp <= 0) return;
+  switch (dtype) {
+    case 1: plan_combine_t<int64_t>(seg, ngrp, nrecv, perm, (const int64_t*)recv, vid, op, (int64_t*)grp, (int64_t*)acc, scratch, s); break;
+    case 2: plan_combine_t<float>(seg, ngrp, nrecv, perm, (const float*)recv, vid, op, (float*)grp, (float*)acc, scratch, s); break;
+    default: plan_combine_t<double>(seg, ngrp, nrecv, perm, (const double*)recv, vid, op, (double*)grp, (double*)acc, scratch, s); break;
+  }
+}
+void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
+            int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s) {
+  if (nwedge <= 0 || ngrp <= 0) return;
+  hipLaunchKernelGGL(k_wedges, dim3((unsigned)((nwedge + NT - 1) / NT)), dim3(NT), 0, s, seg, wscan, ngrp, nb, centre,
+                     nwedge, out_edge, out_centre);
+  MRH_CHECK_LAUNCH();
+}
 
 size_t pr_scratch_bytes(int64_t nval) { return dev::segred_carry_entries(nval) * (sizeof(int64_t) + sizeof(float)) + 64; }
 

@@ -134,6 +134,17 @@ void pr_update(const float* acc, const float* r, float* rn, const uint8_t* dangl
                float alpha, const double* dmass, double invN, const float* invdeg, float* cout, double* partial,
                hipStream_t s);
 
+// generic edge-plan propagation (cc_find / sssp / luby_find); dtype 1 int64, 2 float, 3 double;
+// op 0 sum, 1 min, 2 max; w may be null (else value = x[src] + w)
+size_t plan_scratch_bytes(int64_t n);
+void plan_gather_reduce(int dtype, const int64_t* seg, int64_t nseg, int64_t ne, const int32_t* src, const void* x,
+                        const void* w, int op, void* out, void* scratch, hipStream_t s);
+void plan_combine(int dtype, const int64_t* seg, int64_t ngrp, int64_t nrecv, const int32_t* perm, const void* recv,
+                  const int32_t* vid, int op, void* grp, void* acc, void* scratch, hipStream_t s);
+// tri_find wedges: all pairs of each neighbour group
+void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
+            int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);
+
 // ---------------------------------------------------------------- apps.hip
 // InvertedIndex output formatting: "key\tname name ... \n" per KMV key.
 void ii_value_len(const int32_t* vals, int64_t nval, const int64_t* name_off, int32_t* lenv, hipStream_t s);
