@@ -45,10 +45,10 @@ template <> __device__ inline int32_t RedOp<int32_t, 1>::ident() { return 0x7fff
 template <> __device__ inline int32_t RedOp<int32_t, 2>::ident() { return (int32_t)0x80000000; }
 template <> __device__ inline int64_t RedOp<int64_t, 1>::ident() { return 0x7fffffffffffffffll; }
 template <> __device__ inline int64_t RedOp<int64_t, 2>::ident() { return (int64_t)0x8000000000000000ull; }
-template <> __device__ inline float RedOp<float, 1>::ident() { return 3.402823466e38f; }
-template <> __device__ inline float RedOp<float, 2>::ident() { return -3.402823466e38f; }
-template <> __device__ inline double RedOp<double, 1>::ident() { return 1.7976931348623157e308; }
-template <> __device__ inline double RedOp<double, 2>::ident() { return -1.7976931348623157e308; }
+template <> __device__ inline float RedOp<float, 1>::ident() { return __builtin_huge_valf(); }
+template <> __device__ inline float RedOp<float, 2>::ident() { return -__builtin_huge_valf(); }
+template <> __device__ inline double RedOp<double, 1>::ident() { return __builtin_huge_val(); }
+template <> __device__ inline double RedOp<double, 2>::ident() { return -__builtin_huge_val(); }
 
 // largest s in [0, nseg) with seg[s] <= i
 __device__ __forceinline__ int64_t seg_upper(const int64_t* __restrict__ seg, int64_t nseg, int64_t i) {

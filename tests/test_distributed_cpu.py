@@ -205,3 +205,58 @@ def test_inverted_index_distributed():
         for k, v in ref_r.items():
             ref[k].extend(v)
     assert {k: sorted(v) for k, v in got.items()} == {k: sorted(v) for k, v in ref.items()}
+
+
+OINK_SCRIPT = """rmat 8 4 0.25 0.25 0.25 0.25 0.0 12345 -o tmp.rmat mre
+edge_upper -i mre -o NULL mre
+tri_find -i mre -o tmp.tri NULL
+cc_find 0 -i mre -o tmp.cc mrc
+cc_stats -i mrc
+luby_find 7 -i mre -o tmp.mis NULL
+degree_stats 0 -i mre
+pagerank 0.0 8 0.85 -i mre -o tmp.pr NULL
+"""
+
+
+def oink_graph(comm):
+    import io
+    from gpu_mapreduce_amd.oink.interp import OINK
+    os.chdir(os.environ["OINK_TEST_DIR"])
+    out = io.StringIO()
+    o = OINK(comm, screen=out, logfile="none")
+    o.file(text=OINK_SCRIPT)
+    return out.getvalue()
+
+
+def _oink_files(d, stem):
+    lines = []
+    for f in sorted(os.listdir(d)):
+        if f.startswith(stem + "."):
+            lines += open(os.path.join(d, f)).read().split("\n")
+    return sorted(ln for ln in lines if ln)
+
+
+def test_oink_graph_commands_distributed(tmp_path, monkeypatch):
+    import io
+    from gpu_mapreduce_amd.oink.interp import OINK
+    d1, d2 = tmp_path / "p1", tmp_path / "p2"
+    d1.mkdir()
+    d2.mkdir()
+    monkeypatch.chdir(d1)
+    out1 = io.StringIO()
+    OINK(screen=out1, logfile="none").file(text=OINK_SCRIPT)
+    monkeypatch.setenv("OINK_TEST_DIR", str(d2))
+    res = run_world("oink_graph", 2)
+    text1, text2 = out1.getvalue(), res[0]
+
+    def counts(t):
+        keep = ("Tri_find", "CC_find", "CCStats", "Luby_find", "  ", "EdgeUpper", "RMAT:")
+        return [ln.split(" in ")[0] for ln in t.splitlines() if ln.startswith(keep)]
+    assert counts(text1) == counts(text2)
+    for stem in ("tmp.rmat", "tmp.tri", "tmp.cc", "tmp.mis"):
+        assert _oink_files(d1, stem) == _oink_files(d2, stem), stem
+    p1 = dict(ln.split() for ln in _oink_files(d1, "tmp.pr"))
+    p2 = dict(ln.split() for ln in _oink_files(d2, "tmp.pr"))
+    assert p1.keys() == p2.keys()
+    for k in p1:
+        assert abs(float(p1[k]) - float(p2[k])) <= 1e-5 * abs(float(p1[k])) + 1e-9
