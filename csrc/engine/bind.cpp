@@ -1,10 +1,11 @@
 // Python bindings of the native engine (module gpu_mapreduce_amd._C).
 //
 // Exposes the device KV/KMV containers, the engine ops, the process-group
-// shuffle, the native host-side KeyValue builder used by user callbacks
-// (MR-MPI's KeyValue::add, reference src/keyvalue.cpp:343-643) and the
-// host iteration loops that drive Python reduce/scan/map-over-MR callbacks
-// (reference src/mapreduce.cpp:1769-1867,1933-2065,1560-1642).
+// shuffle, the native KeyValue builder, and the native MapReduce object
+// (mapreduce.h) with Python callables adapted to its callback tiers: host
+// callbacks receive bytes (and the reference's per-key value lists), batch
+// callbacks receive the device KV/KMV. The engine itself lives in
+// libmrhip.so, shared with the C API (csrc/capi).
 #include <torch/extension.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 
@@ -12,10 +13,14 @@
 #include <string>
 
 #include "kv.h"
+#include "mapreduce.h"
 
 namespace py = pybind11;
 using namespace mrh;
-using PG = c10::intrusive_ptr<c10d::ProcessGroup>;
+
+namespace mrh {
+std::function<void(const std::string&)>& screen_sink();
+}
 
 namespace {
 
@@ -23,108 +28,6 @@ PG as_pg(py::object o) {
   if (o.is_none()) return PG();
   return o.cast<PG>();
 }
-
-// Native append-only builder behind the callback-facing KeyValue object.
-// Host-emitted pairs accumulate in contiguous byte arrays; device batches
-// (KV objects produced by kernels or torch ops) are kept as chunks, in order,
-// so a map callback can mix both without a host round trip for device data.
-class HostKV {
- public:
-  explicit HostKV(std::string device) : dev_(device) { reset_host(); }
-
-  void add(const std::string& k, const std::string& v) {
-    kd_.append(k);
-    vd_.append(v);
-    note(k.size(), v.size());
-    koff_.push_back((int64_t)kd_.size());
-    voff_.push_back((int64_t)vd_.size());
-    ++nh_;
-  }
-  // n fixed-size keys / values packed in two byte strings (MR-MPI add(n,k,kb,v,vb))
-  void add_fixed(int64_t n, const std::string& ks, int64_t kb, const std::string& vs, int64_t vb) {
-    if ((int64_t)ks.size() != n * kb || (int64_t)vs.size() != n * vb) throw std::runtime_error("add_multi: size mismatch");
-    for (int64_t i = 0; i < n; ++i) {
-      kd_.append(ks, i * kb, kb);
-      vd_.append(vs, i * vb, vb);
-      note(kb, vb);
-      koff_.push_back((int64_t)kd_.size());
-      voff_.push_back((int64_t)vd_.size());
-    }
-    nh_ += n;
-  }
-  // n variable-size keys/values with per-pair byte counts (MR-MPI add(n,k,kb[],v,vb[]))
-  void add_var(const std::string& ks, const std::vector<int64_t>& kb, const std::string& vs,
-               const std::vector<int64_t>& vb) {
-    if (kb.size() != vb.size()) throw std::runtime_error("add_multi: length lists differ");
-    int64_t ka = 0, va = 0;
-    for (size_t i = 0; i < kb.size(); ++i) {
-      kd_.append(ks, ka, kb[i]);
-      vd_.append(vs, va, vb[i]);
-      ka += kb[i];
-      va += vb[i];
-      note(kb[i], vb[i]);
-      koff_.push_back((int64_t)kd_.size());
-      voff_.push_back((int64_t)vd_.size());
-    }
-    nh_ += (int64_t)kb.size();
-  }
-  void add_kv(const KV& kv) {
-    flush();
-    chunks_.push_back(kv);
-  }
-  int64_t size() const {
-    int64_t n = nh_;
-    for (auto& c : chunks_) n += c.n;
-    return n;
-  }
-  KV finish() {
-    flush();
-    at::Device d(dev_);
-    KV out = concat(chunks_, d);
-    chunks_.clear();
-    return out;
-  }
-
- private:
-  void note(int64_t kb, int64_t vb) {
-    if (kw_ == -2) kw_ = (int)kb;
-    else if (kw_ != kb) kw_ = -1;
-    if (vw_ == -2) vw_ = (int)vb;
-    else if (vw_ != vb) vw_ = -1;
-  }
-  void reset_host() {
-    kd_.clear();
-    vd_.clear();
-    koff_.assign(1, 0);
-    voff_.assign(1, 0);
-    nh_ = 0;
-    kw_ = vw_ = -2;
-  }
-  void flush() {
-    if (nh_ == 0) return;
-    KV kv;
-    kv.n = nh_;
-    auto bytes = [](const std::string& s) {
-      return at::from_blob((void*)s.data(), {(int64_t)s.size()}, at::TensorOptions().dtype(at::kByte)).clone();
-    };
-    kv.kdata = bytes(kd_);
-    kv.vdata = bytes(vd_);
-    kv.kw = kw_ >= 0 ? kw_ : -1;
-    kv.vw = vw_ >= 0 ? vw_ : -1;
-    if (kv.kw < 0)
-      kv.koff = at::from_blob(koff_.data(), {(int64_t)koff_.size()}, at::TensorOptions().dtype(at::kLong)).clone();
-    if (kv.vw < 0)
-      kv.voff = at::from_blob(voff_.data(), {(int64_t)voff_.size()}, at::TensorOptions().dtype(at::kLong)).clone();
-    chunks_.push_back(kv_to(kv, at::Device(dev_)));
-    reset_host();
-  }
-  std::string dev_;
-  std::string kd_, vd_;
-  std::vector<int64_t> koff_, voff_;
-  int64_t nh_ = 0;
-  int kw_ = -2, vw_ = -2;
-  std::vector<KV> chunks_;
-};
 
 // ---------------------------------------------------------------- host iteration helpers
 struct HostCol {
@@ -158,6 +61,41 @@ void kmv_iter(const KMV& kmv, py::function fn) {
     for (int64_t j = s[i]; j < s[i + 1]; ++j) vals[j - s[i]] = v.get(j);
     fn(k.get(i), vals);
   }
+}
+
+py::object kvref(KeyValue& kv) { return py::cast(&kv, py::return_value_policy::reference); }
+
+// the values of one key as a list of bytes; in multi-block mode (mv == nullptr)
+// walk the blocks through the MR
+py::list value_list(MapReduce& mr, char* mv, int nv, int* vb) {
+  py::list out;
+  auto one_block = [&](char* p, int n, int* sz) {
+    for (int j = 0; j < n; ++j) {
+      out.append(py::bytes(p, (size_t)sz[j]));
+      p += sz[j];
+    }
+  };
+  if (mv) {
+    one_block(mv, nv, vb);
+  } else {
+    int nb = 0;
+    mr.multivalue_blocks(nb);
+    for (int b = 0; b < nb; ++b) {
+      char* p;
+      int* sz;
+      int n = mr.multivalue_block(b, &p, &sz);
+      one_block(p, n, sz);
+    }
+  }
+  return out;
+}
+
+HashFn py_hash(py::object h) {
+  if (h.is_none()) return nullptr;
+  return [h](char* k, int kb) { return h(py::bytes(k, (size_t)kb)).cast<int>(); };
+}
+CompareFn py_cmp(py::object c) {
+  return [c](char* a, int al, char* b, int bl) { return c(py::bytes(a, (size_t)al), py::bytes(b, (size_t)bl)).cast<int>(); };
 }
 
 }  // namespace
@@ -203,14 +141,195 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("recv_pairs", &ShuffleStats::recv_pairs)
       .def_readwrite("seconds", &ShuffleStats::seconds);
 
-  py::class_<HostKV>(m, "HostKV")
-      .def(py::init<std::string>())
-      .def("add", &HostKV::add)
-      .def("add_fixed", &HostKV::add_fixed)
-      .def("add_var", &HostKV::add_var)
-      .def("add_kv", &HostKV::add_kv)
-      .def("size", &HostKV::size)
-      .def("finish", &HostKV::finish);
+  // native KeyValue builder (MR-MPI KeyValue::add and its multi variants)
+  py::class_<KeyValue>(m, "HostKV")
+      .def(py::init([](const std::string& d) { return new KeyValue(at::Device(d)); }))
+      .def("add", [](KeyValue& kv, const std::string& k,
+                     const std::string& v) { kv.add(k.data(), (int64_t)k.size(), v.data(), (int64_t)v.size()); })
+      .def("add_fixed",
+           [](KeyValue& kv, int64_t n, const std::string& ks, int64_t kb, const std::string& vs, int64_t vb) {
+             if ((int64_t)ks.size() != n * kb || (int64_t)vs.size() != n * vb)
+               throw std::runtime_error("add_multi: size mismatch");
+             kv.add(n, ks.data(), kb, vs.data(), vb);
+           })
+      .def("add_var",
+           [](KeyValue& kv, const std::string& ks, const std::vector<int>& kb, const std::string& vs,
+              const std::vector<int>& vb) {
+             if (kb.size() != vb.size()) throw std::runtime_error("add_multi: length lists differ");
+             kv.add((int64_t)kb.size(), ks.data(), kb.data(), vs.data(), vb.data());
+           })
+      .def("add_kv", &KeyValue::add_kv)
+      .def("size", &KeyValue::size)
+      .def("finish", &KeyValue::finish)
+      .def_property_readonly("device", [](const KeyValue& kv) { return kv.device().str(); });
+
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "NativeComm")
+      .def(py::init([](py::object pg, const std::string& dev, py::object store) {
+             c10::intrusive_ptr<c10d::Store> st;
+             if (!store.is_none()) st = store.cast<c10::intrusive_ptr<c10d::Store>>();
+             PG p = as_pg(pg);
+             if (!p) return std::make_shared<Comm>(at::Device(dev));
+             return std::make_shared<Comm>(p, at::Device(dev), st);
+           }),
+           py::arg("pg"), py::arg("device"), py::arg("store") = py::none())
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("size", &Comm::size)
+      .def("barrier", &Comm::barrier);
+
+  using MR = MapReduce;
+  py::class_<MR>(m, "NativeMapReduce")
+      .def(py::init([](std::shared_ptr<Comm> c) { return new MR(c); }))
+      .def_property("mapstyle", [](MR& r) { return r.set.mapstyle; }, [](MR& r, int v) { r.set.mapstyle = v; })
+      .def_property("all2all", [](MR& r) { return r.set.all2all; }, [](MR& r, int v) { r.set.all2all = v; })
+      .def_property("verbosity", [](MR& r) { return r.set.verbosity; }, [](MR& r, int v) { r.set.verbosity = v; })
+      .def_property("timer", [](MR& r) { return r.set.timer; }, [](MR& r, int v) { r.set.timer = v; })
+      .def_property("memsize", [](MR& r) { return r.set.memsize; }, [](MR& r, int v) { r.set.memsize = v; })
+      .def_property("minpage", [](MR& r) { return r.set.minpage; }, [](MR& r, int v) { r.set.minpage = v; })
+      .def_property("maxpage", [](MR& r) { return r.set.maxpage; }, [](MR& r, int v) { r.set.maxpage = v; })
+      .def_property("freepage", [](MR& r) { return r.set.freepage; }, [](MR& r, int v) { r.set.freepage = v; })
+      .def_property("outofcore", [](MR& r) { return r.set.outofcore; }, [](MR& r, int v) { r.set.outofcore = v; })
+      .def_property("zeropage", [](MR& r) { return r.set.zeropage; }, [](MR& r, int v) { r.set.zeropage = v; })
+      .def_property("keyalign", [](MR& r) { return r.set.keyalign; }, [](MR& r, int v) { r.set.keyalign = v; })
+      .def_property("valuealign", [](MR& r) { return r.set.valuealign; },
+                    [](MR& r, int v) { r.set.valuealign = v; })
+      .def_property("fpath", [](MR& r) { return r.set.fpath; }, [](MR& r, const std::string& v) { r.set.fpath = v; })
+      .def_readwrite("mapfilecount", &MR::mapfilecount)
+      .def_property(
+          "kv", [](MR& r) -> py::object { return r.kv ? py::cast(*r.kv) : py::none(); },
+          [](MR& r, py::object o) {
+            if (o.is_none()) r.kv.reset();
+            else r.kv = o.cast<KV>();
+          })
+      .def_property(
+          "kmv", [](MR& r) -> py::object { return r.kmv ? py::cast(*r.kmv) : py::none(); },
+          [](MR& r, py::object o) {
+            if (o.is_none()) r.kmv.reset();
+            else r.kmv = o.cast<KMV>();
+          })
+      .def_property_readonly("last_convert", [](MR& r) { return r.last_convert; })
+      .def("copy", [](MR& r) { return r.copy().release(); }, py::return_value_policy::take_ownership)
+      .def("add", &MR::add)
+      .def("aggregate", [](MR& r, py::object h) { return r.aggregate(py_hash(h)); })
+      .def("aggregate_dest", &MR::aggregate_dest)
+      .def("broadcast", &MR::broadcast)
+      .def("clone", &MR::clone)
+      .def("close", &MR::close)
+      .def("collapse", [](MR& r, const std::string& k) { return r.collapse(k.data(), (int)k.size()); })
+      .def("collate", [](MR& r, py::object h) { return r.collate(py_hash(h)); })
+      .def("convert", &MR::convert)
+      .def("gather", &MR::gather)
+      .def("open", &MR::open)
+      .def("kv_open", [](MR& r) { return kvref(r.kv_open()); })
+      .def("map", [](MR& r, int nmap, py::function fn,
+                     int add) { return r.map(nmap, [&](int t, KeyValue& kv) { fn(t, kvref(kv)); }, add); })
+      .def("map_file",
+           [](MR& r, std::vector<std::string> files, int self, int rec, int rd, py::function fn, int add) {
+             return r.map_file(files, self, rec, rd, [&](int t, const char* f, KeyValue& kv) { fn(t, f, kvref(kv)); },
+                               add);
+           })
+      .def("map_file_chunks",
+           [](MR& r, int nmap, std::vector<std::string> files, int self, int rec, int rd, const std::string& sep,
+              bool is_char, int delta, py::function fn, int add) {
+             MapChunkFn f = [&](int t, char* s, int n, KeyValue& kv) { fn(t, py::bytes(s, (size_t)n), kvref(kv)); };
+             if (is_char) return r.map_file_char(nmap, files, self, rec, rd, sep.empty() ? '\n' : sep[0], delta, f, add);
+             return r.map_file_str(nmap, files, self, rec, rd, sep, delta, f, add);
+           })
+      .def("map_mr",
+           [](MR& r, MR& src, py::function fn, int add) {
+             return r.map_mr(
+                 src,
+                 [&](uint64_t i, char* k, int kb, char* v, int vb, KeyValue& kv) {
+                   fn(i, py::bytes(k, (size_t)kb), py::bytes(v, (size_t)vb), kvref(kv));
+                 },
+                 add);
+           })
+      .def("map_mr_batch",
+           [](MR& r, MR& src, py::function fn, int add) {
+             return r.map_mr_batch(src, [&](const KV& s, KeyValue& kv) { fn(s, kvref(kv)); }, add);
+           })
+      .def("reduce",
+           [](MR& r, py::function fn) {
+             return r.reduce([&](char* k, int kb, char* mv, int nv, int* vb, KeyValue& kv) {
+               fn(py::bytes(k, (size_t)kb), value_list(r, mv, nv, vb), kvref(kv));
+             });
+           })
+      .def("compress",
+           [](MR& r, py::function fn) {
+             return r.compress([&](char* k, int kb, char* mv, int nv, int* vb, KeyValue& kv) {
+               fn(py::bytes(k, (size_t)kb), value_list(r, mv, nv, vb), kvref(kv));
+             });
+           })
+      .def("reduce_builtin", &MR::reduce_builtin)
+      .def("compress_builtin", &MR::compress_builtin)
+      .def("reduce_batch",
+           [](MR& r, py::function fn) { return r.reduce_batch([&](const KMV& s, KeyValue& kv) { fn(s, kvref(kv)); }); })
+      .def("scan_kv",
+           [](MR& r, py::function fn) {
+             return r.scan_kv(
+                 [&](char* k, int kb, char* v, int vb) { fn(py::bytes(k, (size_t)kb), py::bytes(v, (size_t)vb)); });
+           })
+      .def("scan_kmv",
+           [](MR& r, py::function fn) {
+             return r.scan_kmv([&](char* k, int kb, char* mv, int nv, int* vb) {
+               fn(py::bytes(k, (size_t)kb), value_list(r, mv, nv, vb));
+             });
+           })
+      .def("scrunch", [](MR& r, int n, const std::string& k) { return r.scrunch(n, k.data(), (int)k.size()); })
+      .def("sort_keys", [](MR& r, int f) { return r.sort_keys(f); })
+      .def("sort_keys_fn", [](MR& r, py::function c) { return r.sort_keys(py_cmp(c)); })
+      .def("sort_values", [](MR& r, int f) { return r.sort_values(f); })
+      .def("sort_values_fn", [](MR& r, py::function c) { return r.sort_values(py_cmp(c)); })
+      .def("sort_multivalues", [](MR& r, int f) { return r.sort_multivalues(f); })
+      .def("sort_multivalues_fn", [](MR& r, py::function c) { return r.sort_multivalues(py_cmp(c)); })
+      .def("print",
+           [](MR& r, int proc, int nstride, int kflag, int vflag, py::object file, int fflag) {
+             if (file.is_none()) r.print(proc, nstride, kflag, vflag);
+             else r.print(file.cast<std::string>().c_str(), fflag, proc, nstride, kflag, vflag);
+           })
+      .def("kv_stats", &MR::kv_stats)
+      .def("kmv_stats", &MR::kmv_stats)
+      .def("cummulative_stats", &MR::cummulative_stats)
+      .def("spill", &MR::spill)
+      .def("unspill", &MR::unspill)
+      .def("my_proc", &MR::my_proc)
+      .def("num_procs", &MR::num_procs)
+      .def_property_readonly("device", [](MR& r) { return r.device().str(); });
+
+  m.def("mr_counters", []() {
+    py::dict d;
+    d["instances_now"] = MapReduce::instances_now.load();
+    d["instances_ever"] = MapReduce::instances_ever.load();
+    d["msize"] = MapReduce::msize.load();
+    d["msizemax"] = MapReduce::msizemax.load();
+    d["rsize"] = MapReduce::rsize.load();
+    d["wsize"] = MapReduce::wsize.load();
+    d["cssize"] = MapReduce::cssize.load();
+    d["crsize"] = MapReduce::crsize.load();
+    d["commtime"] = MapReduce::commtime;
+    return d;
+  });
+  m.def("mr_count_io", [](int64_t r, int64_t w) {
+    MapReduce::rsize += r;
+    MapReduce::wsize += w;
+  });
+  m.def("set_screen", [](py::object f) {
+    if (f.is_none()) {
+      screen_sink() = [](const std::string& s) {
+        std::fwrite(s.data(), 1, s.size(), stdout);
+        std::fflush(stdout);
+      };
+    } else {
+      // deliberately leaked: the sink may outlive module teardown
+      auto* h = new py::object(f);
+      screen_sink() = [h](const std::string& s) {
+        py::gil_scoped_acquire g;
+        (*h)(s);
+      };
+    }
+  });
+  m.def("find_files", [](std::shared_ptr<Comm> c, std::vector<std::string> files, int self, int rec, int rd) {
+    return MapReduce::find_files(*c, files, self, rec, rd);
+  });
 
   m.def("empty_kv", [](const std::string& d, int kw, int vw) { return empty_kv(at::Device(d), kw, vw); });
   m.def(
@@ -236,9 +355,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       py::arg("kv"), py::arg("force_hash_bits") = 64);
   m.def("clone", &mrh::clone);
   m.def("collapse", &mrh::collapse);
-  m.def("reduce_builtin", &reduce_builtin);
+  m.def("reduce_builtin", &mrh::reduce_builtin);
   m.def("sort_kv", &sort_kv);
-  m.def("sort_multivalues", &sort_multivalues);
+  m.def("sort_multivalues", &mrh::sort_multivalues);
   m.def("expand", &mrh::expand);
   m.def("partition_dest", [](const KV& kv, int P) {
     at::Tensor c;
@@ -252,7 +371,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("aggregate", [](const KV& kv, py::object pg) {
     ShuffleStats st;
-    KV r = aggregate(kv, as_pg(pg), &st);
+    KV r = mrh::aggregate(kv, as_pg(pg), &st);
     return std::make_pair(r, st);
   });
   m.def("gather_to", [](const KV& kv, int nprocs, py::object pg) {
@@ -260,7 +379,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     KV r = gather_to(kv, nprocs, as_pg(pg), &st);
     return std::make_pair(r, st);
   });
-  m.def("broadcast", [](const KV& kv, int root, py::object pg) { return broadcast(kv, root, as_pg(pg)); });
+  m.def("broadcast", [](const KV& kv, int root, py::object pg) { return mrh::broadcast(kv, root, as_pg(pg)); });
   m.def("map_urls", &map_urls);
   m.def("map_words", &map_words);
   m.def("map_rmat", [](int64_t ne, int nl, double a, double b, double c, double d, double f, uint64_t seed,

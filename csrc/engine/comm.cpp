@@ -1,0 +1,130 @@
+// Native communicator (see comm.h). Scalar collectives run on the engine
+// device: tiny RCCL all-reduces for the GPU engine (the same stream-ordered
+// path as the shuffle), gloo for the CPU engine.
+#define USE_C10D_NCCL 1
+#include "comm.h"
+
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+#include <torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp>
+#include <torch/csrc/distributed/c10d/TCPStore.hpp>
+#include <torch/csrc/distributed/c10d/Types.hpp>
+
+#include <chrono>
+#include <cstdlib>
+#include <stdexcept>
+
+namespace mrh {
+
+namespace {
+int env_int(const char* k, int d) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atoi(v) : d;
+}
+c10d::ReduceOp::RedOpType red(Comm::Op op) {
+  return op == Comm::SUM ? c10d::ReduceOp::SUM : op == Comm::MAX ? c10d::ReduceOp::MAX : c10d::ReduceOp::MIN;
+}
+void allreduce_t(const PG& pg, at::Tensor& t, Comm::Op op) {
+  std::vector<at::Tensor> v{t};
+  c10d::AllreduceOptions o;
+  o.reduceOp = c10d::ReduceOp(red(op));
+  pg->allreduce(v, o)->wait();
+  t = v[0];
+}
+}  // namespace
+
+Comm::Comm(at::Device dev) : dev_(dev) {}
+
+Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store)
+    : dev_(dev), pg_(std::move(pg)), store_(std::move(store)) {
+  if (pg_) {
+    rank_ = pg_->getRank();
+    size_ = pg_->getSize();
+    if (size_ == 1) pg_.reset();
+  }
+}
+
+std::shared_ptr<Comm> Comm::from_env() {
+  const int ws = env_int("WORLD_SIZE", 1), rank = env_int("RANK", 0), local = env_int("LOCAL_RANK", 0);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  at::Device dev(at::kCPU);
+  if (ndev > 0) {
+    const int d = local % ndev;
+    c10::hip::set_device(d);
+    dev = at::Device(at::kCUDA, d);
+  }
+  if (ws <= 1) return std::make_shared<Comm>(dev);
+  if (!dev.is_cuda())
+    throw std::runtime_error("mrhip: WORLD_SIZE > 1 from the native API needs GPUs (RCCL); use the Python API "
+                             "with the gloo backend for multi-process CPU runs");
+  const char* addr = std::getenv("MASTER_ADDR");
+  c10d::TCPStoreOptions so;
+  so.port = (uint16_t)env_int("MASTER_PORT", 29500);
+  so.isServer = rank == 0;
+  so.numWorkers = ws;
+  so.timeout = std::chrono::milliseconds(600000);
+  auto store = c10::make_intrusive<c10d::TCPStore>(addr ? addr : "127.0.0.1", so);
+  auto opts = c10d::ProcessGroupNCCL::Options::create();
+  auto be = c10::make_intrusive<c10d::ProcessGroupNCCL>(store, rank, ws, opts);
+  auto pg = c10::make_intrusive<c10d::ProcessGroup>(store, rank, ws);
+  pg->setBackend(c10::DeviceType::CUDA, c10d::ProcessGroup::BackendType::NCCL, be);
+  pg->setDefaultBackend(c10d::ProcessGroup::BackendType::NCCL);
+  return std::make_shared<Comm>(pg, dev, store);
+}
+
+std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
+  if (!pg_ || v.empty()) return v;
+  at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kLong)).to(dev_);
+  allreduce_t(pg_, t, op);
+  t = t.to(at::kCPU);
+  std::memcpy(v.data(), t.data_ptr<int64_t>(), v.size() * sizeof(int64_t));
+  return v;
+}
+
+std::vector<double> Comm::allreduce_f64(std::vector<double> v, Op op) const {
+  if (!pg_ || v.empty()) return v;
+  at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kDouble)).to(dev_);
+  allreduce_t(pg_, t, op);
+  t = t.to(at::kCPU);
+  std::memcpy(v.data(), t.data_ptr<double>(), v.size() * sizeof(double));
+  return v;
+}
+
+std::vector<double> Comm::allgather_f64(double x) const {
+  std::vector<double> v(size_, 0.0);
+  v[rank_] = x;
+  return allreduce_f64(v, SUM);
+}
+
+std::string Comm::bcast(const std::string& s, int root) const {
+  if (!pg_) return s;
+  int64_t n = rank_ == root ? (int64_t)s.size() : 0;
+  n = allreduce(n, SUM);
+  at::Tensor t = at::zeros({std::max<int64_t>(n, 1)}, at::TensorOptions().dtype(at::kByte));
+  if (rank_ == root && n) std::memcpy(t.data_ptr(), s.data(), n);
+  t = t.to(dev_);
+  std::vector<at::Tensor> v{t};
+  c10d::BroadcastOptions bo;
+  bo.rootRank = root;
+  pg_->broadcast(v, bo)->wait();
+  t = v[0].to(at::kCPU);
+  return std::string((const char*)t.data_ptr(), (size_t)n);
+}
+
+void Comm::barrier() const {
+  if (!pg_) return;
+  allreduce((int64_t)0, SUM);
+}
+
+double Comm::wtime() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+int64_t Comm::next_task(const std::string& key) const {
+  if (!store_) throw std::runtime_error("mrhip: mapstyle 2 needs a c10d store");
+  return store_->add(key, 1) - 1;
+}
+
+}  // namespace mrh

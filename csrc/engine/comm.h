@@ -1,0 +1,64 @@
+// Host-side view of the job's communicator for the native MapReduce object:
+// rank/size, the engine device, the c10d ProcessGroup used by the shuffle
+// (backend "nccl" = RCCL over xGMI for device tensors, "gloo" for host
+// tensors), and the scalar collectives every MR op needs (the Allreduce SUM of
+// pair counts that is each op's return value, stats MAX/MIN, barriers, file
+// list broadcast). Replaces MR-MPI's direct MPI_Comm use and mpistubs/
+// (world size 1 = no process group, identity collectives).
+#pragma once
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/distributed/c10d/Store.hpp>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace mrh {
+
+using PG = c10::intrusive_ptr<c10d::ProcessGroup>;
+
+class Comm {
+ public:
+  enum Op { SUM = 0, MAX = 1, MIN = 2 };
+
+  // world size 1 on `dev`
+  explicit Comm(at::Device dev = at::Device(at::kCPU));
+  // an existing process group (e.g. created by torch.distributed)
+  Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store = {});
+
+  // Bootstrap from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK,
+  // MASTER_ADDR, MASTER_PORT) without Python: binds the process to GPU
+  // LOCAL_RANK when GPUs are visible, and for WORLD_SIZE > 1 creates a
+  // TCPStore rendezvous and an RCCL process group (device engine only).
+  static std::shared_ptr<Comm> from_env();
+
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  at::Device device() const { return dev_; }
+  const PG& pg() const { return pg_; }  // null when size == 1
+  const c10::intrusive_ptr<c10d::Store>& store() const { return store_; }
+  void set_store(c10::intrusive_ptr<c10d::Store> s) { store_ = std::move(s); }
+
+  std::vector<int64_t> allreduce(std::vector<int64_t> v, Op op) const;
+  int64_t allreduce(int64_t v, Op op) const { return allreduce(std::vector<int64_t>{v}, op)[0]; }
+  std::vector<double> allreduce_f64(std::vector<double> v, Op op) const;
+  double allreduce_f64(double v, Op op) const { return allreduce_f64(std::vector<double>{v}, op)[0]; }
+  // every rank's value, in rank order
+  std::vector<double> allgather_f64(double v) const;
+  std::string bcast(const std::string& s, int root) const;
+  void barrier() const;
+  static double wtime();
+
+  // mapstyle 2 work queue: next global task index from a store counter
+  int64_t next_task(const std::string& key) const;
+
+ private:
+  int rank_ = 0, size_ = 1;
+  at::Device dev_;
+  PG pg_;
+  c10::intrusive_ptr<c10d::Store> store_;
+};
+
+using CommPtr = std::shared_ptr<Comm>;
+
+}  // namespace mrh

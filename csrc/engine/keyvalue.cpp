@@ -1,0 +1,32 @@
+// KeyValue builder (see keyvalue.h).
+#include "keyvalue.h"
+
+namespace mrh {
+
+void KeyValue::flush() {
+  if (nh_ == 0) return;
+  KV kv;
+  kv.n = nh_;
+  auto bytes = [](const std::string& s) {
+    return at::from_blob((void*)s.data(), {(int64_t)s.size()}, at::TensorOptions().dtype(at::kByte)).clone();
+  };
+  kv.kdata = bytes(kd_);
+  kv.vdata = bytes(vd_);
+  kv.kw = kw_ >= 0 ? kw_ : -1;
+  kv.vw = vw_ >= 0 ? vw_ : -1;
+  if (kv.kw < 0)
+    kv.koff = at::from_blob(koff_.data(), {(int64_t)koff_.size()}, at::TensorOptions().dtype(at::kLong)).clone();
+  if (kv.vw < 0)
+    kv.voff = at::from_blob(voff_.data(), {(int64_t)voff_.size()}, at::TensorOptions().dtype(at::kLong)).clone();
+  chunks_.push_back(kv_to(kv, dev_));
+  reset_host();
+}
+
+KV KeyValue::finish() {
+  flush();
+  KV out = concat(chunks_, dev_);
+  chunks_.clear();
+  return out;
+}
+
+}  // namespace mrh

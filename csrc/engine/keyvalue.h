@@ -1,0 +1,81 @@
+// Append-only KeyValue builder handed to map/reduce callbacks: the MR-MPI
+// KeyValue::add API (reference src/keyvalue.h:55-57, src/keyvalue.cpp:343-643)
+// over the device-resident SoA KV of kv.h.
+//
+// Host-emitted pairs accumulate in contiguous byte arrays (one memcpy per
+// pair, no per-pair page/alignment bookkeeping); device batches (KV objects
+// produced by kernels or ATen ops inside batch callbacks) are kept as chunks in
+// emission order, so a callback can mix both without a host round trip for
+// device data. finish() uploads the host part once and concatenates.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "kv.h"
+
+namespace mrh {
+
+class KeyValue {
+ public:
+  explicit KeyValue(at::Device dev) : dev_(dev) { reset_host(); }
+
+  // add(key, keybytes, value, valuebytes)
+  void add(const char* k, int64_t kb, const char* v, int64_t vb) {
+    if (kb) kd_.append(k, (size_t)kb);
+    if (vb) vd_.append(v, (size_t)vb);
+    note(kb, vb);
+    koff_.push_back((int64_t)kd_.size());
+    voff_.push_back((int64_t)vd_.size());
+    ++nh_;
+  }
+  // add(n, keys, keybytes, values, valuebytes): n fixed-size pairs, packed
+  void add(int64_t n, const char* ks, int64_t kb, const char* vs, int64_t vb) {
+    for (int64_t i = 0; i < n; ++i) add(ks + i * kb, kb, vs + i * vb, vb);
+  }
+  // add(n, keys, keybytes[], values, valuebytes[]): n variable-size pairs, packed
+  void add(int64_t n, const char* ks, const int* kb, const char* vs, const int* vb) {
+    int64_t ka = 0, va = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      add(ks + ka, kb[i], vs + va, vb[i]);
+      ka += kb[i];
+      va += vb[i];
+    }
+  }
+  void add_kv(const KV& kv) {
+    flush();
+    if (kv.n) chunks_.push_back(kv);
+  }
+  int64_t size() const {
+    int64_t n = nh_;
+    for (auto& c : chunks_) n += c.n;
+    return n;
+  }
+  KV finish();
+  at::Device device() const { return dev_; }
+
+ private:
+  void note(int64_t kb, int64_t vb) {
+    if (kw_ == -2) kw_ = (int)kb;
+    else if (kw_ != kb) kw_ = -1;
+    if (vw_ == -2) vw_ = (int)vb;
+    else if (vw_ != vb) vw_ = -1;
+  }
+  void reset_host() {
+    kd_.clear();
+    vd_.clear();
+    koff_.assign(1, 0);
+    voff_.assign(1, 0);
+    nh_ = 0;
+    kw_ = vw_ = -2;
+  }
+  void flush();
+
+  at::Device dev_;
+  std::string kd_, vd_;
+  std::vector<int64_t> koff_, voff_;
+  int64_t nh_ = 0;
+  int kw_ = -2, vw_ = -2;
+  std::vector<KV> chunks_;
+};
+
+}  // namespace mrh

@@ -1,0 +1,949 @@
+// Native MapReduce object (see mapreduce.h). Reference behaviour cited per
+// method as src/mapreduce.cpp:<lines>.
+#include "mapreduce.h"
+
+#include <algorithm>
+#include <cinttypes>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <numeric>
+#include <sstream>
+#include <stdexcept>
+
+namespace mrh {
+
+std::atomic<int> MapReduce::instances_now{0}, MapReduce::instances_ever{0};
+std::atomic<int64_t> MapReduce::msize{0}, MapReduce::msizemax{0}, MapReduce::rsize{0}, MapReduce::wsize{0},
+    MapReduce::cssize{0}, MapReduce::crsize{0};
+double MapReduce::commtime = 0.0;
+
+std::function<void(const std::string&)>& screen_sink() {
+  static std::function<void(const std::string&)> f = [](const std::string& s) {
+    std::fwrite(s.data(), 1, s.size(), stdout);
+    std::fflush(stdout);
+  };
+  return f;
+}
+
+namespace {
+
+[[noreturn]] void fail(const std::string& m) { throw std::runtime_error(m); }
+
+void out(const std::string& s) { screen_sink()(s); }
+
+std::string fmt(const char* f, ...) __attribute__((format(printf, 1, 2)));
+std::string fmt(const char* f, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return buf;
+}
+
+// one column (keys or values) staged to host memory
+struct HostCol {
+  at::Tensor data, off;
+  int w = 0;
+  char* d() const { return data.numel() ? (char*)data.data_ptr<uint8_t>() : nullptr; }
+  int64_t a(int64_t i) const { return w >= 0 ? i * w : off.data_ptr<int64_t>()[i]; }
+  int64_t len(int64_t i) const { return w >= 0 ? w : off.data_ptr<int64_t>()[i + 1] - off.data_ptr<int64_t>()[i]; }
+  char* at(int64_t i) const { return d() ? d() + a(i) : nullptr; }
+};
+HostCol host_col(const at::Tensor& data, const at::Tensor& off, int w) {
+  HostCol c;
+  c.data = data.defined() ? data.to(at::kCPU).contiguous() : at::empty({0}, at::TensorOptions().dtype(at::kByte));
+  c.off = (w < 0) ? off.to(at::kCPU).contiguous() : at::Tensor();
+  c.w = w;
+  return c;
+}
+
+KV clone_kv(const KV& kv) {
+  KV o = kv;
+  o.kdata = kv.kdata.clone();
+  o.vdata = kv.vdata.clone();
+  if (kv.koff.defined()) o.koff = kv.koff.clone();
+  if (kv.voff.defined()) o.voff = kv.voff.clone();
+  return o;
+}
+KMV clone_kmv(const KMV& m) {
+  KMV o = m;
+  o.keys = clone_kv(m.keys);
+  o.vdata = m.vdata.clone();
+  if (m.voff.defined()) o.voff = m.voff.clone();
+  o.seg = m.seg.clone();
+  return o;
+}
+at::Tensor to_host(const at::Tensor& t, bool pin) {
+  if (!t.defined()) return t;
+  at::Tensor h = t.to(at::kCPU);
+  if (pin && t.is_cuda()) h = h.pin_memory();
+  return h;
+}
+KV kv_host(const KV& kv, bool pin) {
+  KV o = kv;
+  o.kdata = to_host(kv.kdata, pin);
+  o.vdata = to_host(kv.vdata, pin);
+  o.koff = to_host(kv.koff, pin);
+  o.voff = to_host(kv.voff, pin);
+  return o;
+}
+KMV kmv_to(const KMV& m, at::Device d, bool pin) {
+  KMV o = m;
+  if (d.is_cpu()) {
+    o.keys = kv_host(m.keys, pin);
+    o.vdata = to_host(m.vdata, pin);
+    o.voff = to_host(m.voff, pin);
+    o.seg = to_host(m.seg, pin);
+  } else {
+    o.keys = kv_to(m.keys, d);
+    o.vdata = m.vdata.to(d);
+    if (m.voff.defined()) o.voff = m.voff.to(d);
+    o.seg = m.seg.to(d);
+  }
+  return o;
+}
+
+std::string fmt_item(const char* p, int64_t n, int flag) {
+  switch (flag) {
+    case 0: return "NULL";
+    case 1: { int32_t x = 0; std::memcpy(&x, p, std::min<int64_t>(n, 4)); return std::to_string(x); }
+    case 2: { uint64_t x = 0; std::memcpy(&x, p, std::min<int64_t>(n, 8)); return std::to_string(x); }
+    case 3: { float x = 0; std::memcpy(&x, p, std::min<int64_t>(n, 4)); return fmt("%g", x); }
+    case 4: { double x = 0; std::memcpy(&x, p, std::min<int64_t>(n, 8)); return fmt("%g", x); }
+    case 5: return std::string(p, strnlen(p, (size_t)n));
+    case 6: { int32_t x[2] = {0, 0}; std::memcpy(x, p, std::min<int64_t>(n, 8)); return fmt("%d %d", x[0], x[1]); }
+    case 7: { uint64_t x[2] = {0, 0}; std::memcpy(x, p, std::min<int64_t>(n, 16));
+              return fmt("%" PRIu64 " %" PRIu64, x[0], x[1]); }
+  }
+  fail("Invalid print args");
+}
+
+void expand_path(const std::string& path, int recurse, std::vector<std::string>& outv) {
+  namespace fs = std::filesystem;
+  std::error_code ec;
+  if (fs::is_regular_file(path, ec)) {
+    outv.push_back(path);
+  } else if (fs::is_directory(path, ec)) {
+    std::vector<std::string> names;
+    for (auto& e : fs::directory_iterator(path)) names.push_back(e.path().filename().string());
+    std::sort(names.begin(), names.end());
+    for (auto& n : names) {
+      std::string full = (fs::path(path) / n).string();
+      if (fs::is_regular_file(full, ec)) outv.push_back(full);
+      else if (recurse && fs::is_directory(full, ec)) expand_path(full, recurse, outv);
+    }
+  } else {
+    fail("Invalid filename " + path);
+  }
+}
+
+std::string join(const std::vector<std::string>& v) {
+  std::string s;
+  for (auto& x : v) {
+    s += x;
+    s.push_back('\n');
+  }
+  return s;
+}
+std::vector<std::string> split_lines(const std::string& s) {
+  std::vector<std::string> v;
+  size_t a = 0;
+  while (a < s.size()) {
+    size_t b = s.find('\n', a);
+    if (b == std::string::npos) b = s.size();
+    v.push_back(s.substr(a, b - a));
+    a = b + 1;
+  }
+  return v;
+}
+
+struct ChunkTask {
+  int ifile, itask, ntask;
+  int64_t fsize;
+};
+
+}  // namespace
+
+// ====================================================================== lifecycle
+
+MapReduce::MapReduce(CommPtr comm) : comm_(std::move(comm)) {
+  if (!comm_) comm_ = std::make_shared<Comm>();
+  if (const char* p = std::getenv("MRMPI_FPATH")) set.fpath = p;
+  instances_now++;
+  instance_me_ = ++instances_ever;
+}
+
+MapReduce::~MapReduce() { instances_now--; }
+
+std::unique_ptr<MapReduce> MapReduce::copy() const {
+  auto mr = std::make_unique<MapReduce>(comm_);
+  mr->set = set;
+  if (kv) mr->kv = clone_kv(*kv);
+  if (kmv) mr->kmv = clone_kmv(*kmv);
+  return mr;
+}
+
+void MapReduce::need_kv(const char* what) const {
+  if (!kv) fail(std::string("Cannot ") + what + " without KeyValue");
+}
+void MapReduce::need_kmv(const char* what) const {
+  if (!kmv) fail(std::string("Cannot ") + what + " without KeyMultiValue");
+}
+
+void MapReduce::start() {
+  if (set.timer) {
+    if (set.timer == 1) comm_->barrier();
+    t0_ = Comm::wtime();
+  }
+  cs0_ = cssize.load();
+  cr0_ = crsize.load();
+}
+
+void MapReduce::histo(double v, const char* heading) const {
+  std::vector<double> vals = comm_->allgather_f64(v);
+  double ave = 0, mx = vals[0], mn = vals[0];
+  for (double x : vals) {
+    ave += x;
+    mx = std::max(mx, x);
+    mn = std::min(mn, x);
+  }
+  ave /= vals.size();
+  int h[10] = {0};
+  const double d = mx - mn;
+  for (double x : vals) {
+    int m = d == 0.0 ? 0 : (int)((x - mn) / d * 10.0);
+    h[std::min(m, 9)]++;
+  }
+  if (comm_->rank() == 0) {
+    std::string s = fmt("%-13s %g ave %g max %g min\n", heading, ave, mx, mn);
+    s += fmt("%-13s", "  Histogram:");
+    for (int i = 0; i < 10; ++i) s += fmt(" %d", h[i]);
+    out(s + "\n");
+  }
+}
+
+// per-op stats (reference :3112-3179)
+void MapReduce::stats(const char* heading, int which) {
+  int64_t b = 0;
+  if (kv) b += kv->nbytes();
+  if (kmv) b += kmv->nbytes();
+  msize = b;
+  if (b > msizemax) msizemax = b;
+  if (set.timer) {
+    if (set.timer == 1) {
+      comm_->barrier();
+      if (comm_->rank() == 0) out(fmt("%s time (secs) = %g\n", heading, Comm::wtime() - t0_));
+    } else if (set.timer == 2) {
+      histo(Comm::wtime() - t0_, (std::string(heading) + " time (secs) =").c_str());
+    }
+  }
+  if (set.verbosity == 0) return;
+  if (which == 0) {
+    if (comm_->rank() == 0) out(std::string(heading) + " KV = ");
+    kv_stats(set.verbosity);
+  } else {
+    if (comm_->rank() == 0) out(std::string(heading) + " KMV = ");
+    kmv_stats(set.verbosity);
+  }
+  std::vector<int64_t> sr = comm_->allreduce({cssize - cs0_, crsize - cr0_}, Comm::SUM);
+  if (sr[0] || sr[1]) {
+    const double mb = 1024.0 * 1024.0;
+    if (comm_->rank() == 0) out(fmt("%s Comm = %.3g Mb send, %.3g Mb recv\n", heading, sr[0] / mb, sr[1] / mb));
+    if (set.verbosity == 2) {
+      histo((cssize - cs0_) / mb, "  Send (Mb):");
+      histo((crsize - cr0_) / mb, "  Recv (Mb):");
+    }
+  }
+}
+
+void MapReduce::note_shuffle(const ShuffleStats& st) {
+  cssize += st.send_bytes;
+  crsize += st.recv_bytes;
+  commtime += st.seconds;
+}
+
+// ====================================================================== add / open / close
+
+uint64_t MapReduce::add(MapReduce& other) {  // :348-374
+  start();
+  need_kv("add");
+  if (!other.kv) fail("MapReduce passed to add() does not have KeyValue pairs");
+  kv = concat({*kv, *other.kv}, device());
+  stats("Add", 0);
+  return count(kv->n);
+}
+
+void MapReduce::open(int addflag) {  // :1648-1664
+  open_ = std::make_unique<KeyValue>(device());
+  open_add_ = addflag;
+  kmv.reset();
+}
+
+KeyValue& MapReduce::kv_open() {
+  if (!open_) fail("MapReduce is not open");
+  return *open_;
+}
+
+uint64_t MapReduce::close() {  // :658-672
+  if (!open_) fail("Cannot close MapReduce that is not open");
+  KV n = open_->finish();
+  open_.reset();
+  if (open_add_ && kv) kv = concat({*kv, n}, device());
+  else kv = n;
+  stats("Close", 0);
+  return count(kv->n);
+}
+
+// ====================================================================== map
+
+std::vector<int> MapReduce::my_tasks(int nmap) {  // :1102-1225
+  const int P = comm_->size(), me = comm_->rank();
+  std::vector<int> t;
+  if (set.mapstyle == 0 || P == 1) {
+    for (int i = (int)((int64_t)me * nmap / P); i < (int)((int64_t)(me + 1) * nmap / P); ++i) t.push_back(i);
+  } else if (set.mapstyle == 1) {
+    for (int i = me; i < nmap; i += P) t.push_back(i);
+  } else {
+    // mapstyle 2: the reference dedicates rank 0 as a master handing out task
+    // ids over MPI (:1164-1211); here every rank, rank 0 included, pulls the
+    // next id from an atomic counter in the rendezvous store.
+    static std::atomic<int64_t> ncall{0};
+    comm_->barrier();
+    const std::string key = "mrh_mapstyle2_" + std::to_string(instance_me_) + "_" + std::to_string(ncall++);
+    for (int64_t i = comm_->next_task(key); i < nmap; i = comm_->next_task(key)) t.push_back((int)i);
+    comm_->barrier();
+  }
+  return t;
+}
+
+uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) {
+  KV n = kvb.finish();
+  if (addflag && kv) kv = concat({*kv, n}, device());
+  else kv = n;
+  kmv.reset();
+  stats(heading, 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::map(int nmap, const MapTaskFn& fn, int addflag) {  // :1044-1051
+  start();
+  KeyValue kvb(device());
+  for (int t : my_tasks(nmap)) fn(t, kvb);
+  return finish_map(kvb, addflag);
+}
+
+std::vector<std::string> MapReduce::find_files(const Comm& comm, const std::vector<std::string>& files,
+                                               int selfflag, int recurse, int readflag) {  // :2812-2931
+  auto local = [&]() {
+    std::vector<std::string> v;
+    for (auto& f : files) {
+      if (readflag) {
+        std::ifstream in(f);
+        if (!in) fail("Could not open file " + f);
+        std::string line;
+        while (std::getline(in, line)) {
+          std::istringstream ss(line);
+          std::string w;
+          if (ss >> w) expand_path(w, recurse, v);
+        }
+      } else {
+        expand_path(f, recurse, v);
+      }
+    }
+    return v;
+  };
+  if (selfflag) return local();
+  std::string s = comm.rank() == 0 ? join(local()) : std::string();
+  return split_lines(comm.bcast(s, 0));
+}
+
+uint64_t MapReduce::map_file(const std::vector<std::string>& files, int selfflag, int recurse, int readflag,
+                             const MapFileFn& fn, int addflag) {  // :1060-1092
+  start();
+  auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
+  mapfilecount = (int)fl.size();
+  KeyValue kvb(device());
+  if (selfflag) {
+    for (int i = 0; i < (int)fl.size(); ++i) fn(i, fl[i].c_str(), kvb);
+  } else {
+    for (int t : my_tasks((int)fl.size())) fn(t, fl[t].c_str(), kvb);
+  }
+  return finish_map(kvb, addflag);
+}
+
+uint64_t MapReduce::map_file_char(int nmap, const std::vector<std::string>& files, int selfflag, int recurse,
+                                  int readflag, char sepchar, int delta, const MapChunkFn& fn, int addflag) {
+  return map_chunks(nmap, files, selfflag, recurse, readflag, std::string(1, sepchar), true, delta, fn, addflag);
+}
+
+uint64_t MapReduce::map_file_str(int nmap, const std::vector<std::string>& files, int selfflag, int recurse,
+                                 int readflag, const std::string& sepstr, int delta, const MapChunkFn& fn,
+                                 int addflag) {
+  return map_chunks(nmap, files, selfflag, recurse, readflag, sepstr, false, delta, fn, addflag);
+}
+
+// split files into ~nmap byte ranges, fix record boundaries with the
+// separator and a `delta` look-ahead (reference map_chunks/map_file_wrapper
+// :1312-1552)
+uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, int selfflag, int recurse,
+                               int readflag, const std::string& sep, bool is_char, int delta, const MapChunkFn& fn,
+                               int addflag) {
+  start();
+  auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
+  mapfilecount = (int)fl.size();
+  const int nfile = (int)fl.size();
+  std::vector<int64_t> sizes(nfile, 0);
+  if (comm_->rank() == 0 || selfflag)
+    for (int i = 0; i < nfile; ++i) sizes[i] = (int64_t)std::filesystem::file_size(fl[i]);
+  if (!selfflag) sizes = comm_->allreduce(sizes, Comm::SUM);
+  std::vector<ChunkTask> plan;
+  if (nfile) {
+    nmap = std::max(nmap, nfile);
+    int64_t total = std::accumulate(sizes.begin(), sizes.end(), (int64_t)0);
+    int64_t ideal = std::max<int64_t>(1, total / nmap);
+    std::vector<int> tpf(nfile);
+    int ntasks = 0;
+    for (int i = 0; i < nfile; ++i) ntasks += (tpf[i] = (int)std::max<int64_t>(1, sizes[i] / ideal));
+    while (ntasks < nmap) {
+      bool prog = false;
+      for (int i = 0; i < nfile && ntasks < nmap; ++i)
+        if (sizes[i] > ideal) {
+          tpf[i]++;
+          ntasks++;
+          prog = true;
+        }
+      if (!prog) break;
+    }
+    while (ntasks > nmap)
+      for (int i = 0; i < nfile && ntasks > nmap; ++i)
+        if (tpf[i] > 1) {
+          tpf[i]--;
+          ntasks--;
+        }
+    for (int i = 0; i < nfile; ++i)
+      while (tpf[i] > 1 && sizes[i] / tpf[i] <= delta) tpf[i]--;
+    for (int i = 0; i < nfile; ++i)
+      for (int j = 0; j < tpf[i]; ++j) plan.push_back({i, j, tpf[i], sizes[i]});
+  }
+  KeyValue kvb(device());
+  std::vector<int> tasks;
+  if (selfflag) {
+    tasks.resize(plan.size());
+    std::iota(tasks.begin(), tasks.end(), 0);
+  } else {
+    tasks = my_tasks((int)plan.size());
+  }
+  std::string buf;
+  for (int t : tasks) {
+    const ChunkTask& c = plan[t];
+    const int64_t st = (int64_t)c.itask * c.fsize / c.ntask, nx = (int64_t)(c.itask + 1) * c.fsize / c.ntask;
+    const int64_t rs = std::min<int64_t>(nx - st + delta, c.fsize - st);
+    buf.assign((size_t)rs + 1, '\0');
+    std::FILE* f = std::fopen(fl[c.ifile].c_str(), "rb");
+    if (!f) fail("Could not open file " + fl[c.ifile]);
+    std::fseek(f, (long)st, SEEK_SET);
+    size_t got = std::fread(&buf[0], 1, (size_t)rs, f);
+    std::fclose(f);
+    rsize += (int64_t)got;
+    int64_t s0 = 0, s1 = (int64_t)got;
+    if (c.itask > 0) {
+      size_t p = buf.find(sep, 0);
+      if (p == std::string::npos || (int64_t)p > delta) fail("Could not find file separator within delta");
+      s0 = (int64_t)p + (is_char ? (int64_t)sep.size() : 0);
+    }
+    if (c.itask < c.ntask - 1) {
+      size_t p = buf.find(sep, (size_t)(nx - st));
+      if (p == std::string::npos || (int64_t)p >= (int64_t)got) fail("Could not find file separator within delta");
+      s1 = (int64_t)p + (is_char ? 1 : 0);
+    }
+    buf[s1] = '\0';  // the reference NUL-terminates the chunk for strtok-style callbacks
+    fn(t, &buf[s0], (int)(s1 - s0), kvb);
+  }
+  return finish_map(kvb, addflag);
+}
+
+uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  // :1560-1642
+  start();
+  if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
+  KV s = *src.kv;
+  HostCol k = host_col(s.kdata, s.koff, s.kw), v = host_col(s.vdata, s.voff, s.vw);
+  KeyValue kvb(device());
+  for (int64_t i = 0; i < s.n; ++i) fn((uint64_t)i, k.at(i), (int)k.len(i), v.at(i), (int)v.len(i), kvb);
+  if (&src == this && addflag) {
+    KV n = kvb.finish();
+    kv = concat({s, n}, device());
+    kmv.reset();
+    stats("Map", 0);
+    return count(kv->n);
+  }
+  return finish_map(kvb, addflag);
+}
+
+uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addflag) {
+  start();
+  if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
+  KV s = *src.kv;
+  KeyValue kvb(device());
+  fn(s, kvb);
+  if (&src == this && addflag) {
+    KV n = kvb.finish();
+    kv = concat({s, n}, device());
+    kmv.reset();
+    stats("Map", 0);
+    return count(kv->n);
+  }
+  return finish_map(kvb, addflag);
+}
+
+// ====================================================================== shuffle
+
+uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
+  start();
+  need_kv("aggregate");
+  if (comm_->size() > 1) {
+    ShuffleStats st;
+    if (!hash) {
+      kv = mrh::aggregate(*kv, comm_->pg(), &st);
+    } else {
+      HostCol k = host_col(kv->kdata, kv->koff, kv->kw);
+      at::Tensor d = at::empty({kv->n}, at::TensorOptions().dtype(at::kInt));
+      int32_t* dp = d.data_ptr<int32_t>();
+      const int P = comm_->size();
+      for (int64_t i = 0; i < kv->n; ++i) {
+        int h = hash(k.at(i), (int)k.len(i));
+        dp[i] = (int32_t)(((int64_t)h % P + P) % P);
+      }
+      kv = exchange(*kv, d.to(device()), comm_->pg(), &st);
+    }
+    note_shuffle(st);
+  }
+  stats("Aggregate", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
+  start();
+  need_kv("aggregate");
+  if (comm_->size() > 1) {
+    ShuffleStats st;
+    kv = exchange(*kv, dest.to(device()).to(at::kInt), comm_->pg(), &st);
+    note_shuffle(st);
+  }
+  stats("Aggregate", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::broadcast(int root) {  // :569-623
+  start();
+  need_kv("broadcast");
+  if (comm_->size() > 1) kv = mrh::broadcast(*kv, root, comm_->pg());
+  stats("Broadcast", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::gather(int nprocs) {  // :893-1036
+  start();
+  need_kv("gather");
+  if (nprocs < 1 || nprocs > comm_->size()) fail("Invalid proc count for gather");
+  if (comm_->size() > 1 && nprocs < comm_->size()) {
+    ShuffleStats st;
+    kv = gather_to(*kv, nprocs, comm_->pg(), &st);
+    note_shuffle(st);
+  }
+  stats("Gather", 0);
+  return count(kv->n);
+}
+
+// ====================================================================== group-by
+
+uint64_t MapReduce::convert() {  // :861-886
+  start();
+  need_kv("convert");
+  kmv = mrh::convert(*kv, &last_convert);
+  kv.reset();
+  stats("Convert", 1);
+  return count(kmv->nkey);
+}
+
+uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
+  start();
+  need_kv("collate");
+  const int v = set.verbosity, t = set.timer;
+  set.verbosity = set.timer = 0;
+  aggregate(hash);
+  convert();
+  set.verbosity = v;
+  set.timer = t;
+  stats("Collate", 1);
+  return count(kmv->nkey);
+}
+
+uint64_t MapReduce::clone() {  // :631-652
+  start();
+  need_kv("clone");
+  kmv = mrh::clone(*kv);
+  kv.reset();
+  stats("Clone", 1);
+  return count(kmv->nkey);
+}
+
+uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
+  start();
+  need_kv("collapse");
+  kmv = mrh::collapse(*kv, std::string(key, (size_t)kb));
+  kv.reset();
+  stats("Collapse", 1);
+  return count(kmv->nkey);
+}
+
+uint64_t MapReduce::scrunch(int nprocs, const char* key, int kb) {  // :2075-2095
+  start();
+  const int v = set.verbosity, t = set.timer;
+  set.verbosity = set.timer = 0;
+  gather(nprocs);
+  collapse(key, kb);
+  set.verbosity = v;
+  set.timer = t;
+  stats("Scrunch", 1);
+  return count(kmv->nkey);
+}
+
+// ====================================================================== reduce family
+
+int64_t MapReduce::block_bytes() const {
+  // one "page" of values per host block: memsize MB (negative = bytes)
+  return set.memsize > 0 ? (int64_t)set.memsize << 20 : std::max<int64_t>(512, -(int64_t)set.memsize);
+}
+
+// Drive a host callback over every KMV pair. Keys whose values exceed one page
+// use the reference's multi-block protocol (:1828-1848): mv == nullptr,
+// nvalues == 0, valuebytes == (int*)this, then multivalue_blocks/_block.
+void MapReduce::run_host_kmv(const KMV& m, const std::function<void(char*, int, char*, int, int*)>& fn) {
+  HostCol k = host_col(m.keys.kdata, m.keys.koff, m.keys.kw), v = host_col(m.vdata, m.voff, m.vw);
+  at::Tensor seg = m.seg.to(at::kCPU).contiguous();
+  const int64_t* s = seg.data_ptr<int64_t>();
+  std::vector<int> vsz((size_t)m.nval);
+  for (int64_t j = 0; j < m.nval; ++j) vsz[j] = (int)v.len(j);
+  const int64_t page = block_bytes();
+  for (int64_t i = 0; i < m.nkey; ++i) {
+    const int64_t a = s[i], b = s[i + 1];
+    char* mv = v.at(a);
+    const int64_t mvbytes = b > a ? v.a(b - 1) + v.len(b - 1) - v.a(a) : 0;
+    if (mvbytes <= page || b - a <= 1) {
+      fn(k.at(i), (int)k.len(i), mv ? mv : k.at(i), (int)(b - a), vsz.data() + a);
+      continue;
+    }
+    blk_.mv = mv;
+    blk_.sizes = vsz.data() + a;
+    blk_.nval = b - a;
+    blk_.start.clear();
+    blk_.boff.clear();
+    int64_t acc = 0, off = 0;
+    for (int64_t j = 0; j < b - a; ++j) {
+      if (j == 0 || acc + vsz[a + j] > page) {
+        blk_.start.push_back(j);
+        blk_.boff.push_back(off);
+        acc = 0;
+      }
+      acc += vsz[a + j];
+      off += vsz[a + j];
+    }
+    blk_.start.push_back(b - a);
+    fn(k.at(i), (int)k.len(i), nullptr, 0, reinterpret_cast<int*>(this));
+    blk_ = Blocks();
+  }
+}
+
+uint64_t MapReduce::multivalue_blocks(int& nblock) const {
+  nblock = blk_.start.empty() ? 0 : (int)blk_.start.size() - 1;
+  return (uint64_t)blk_.nval;
+}
+
+int MapReduce::multivalue_block(int iblock, char** mv, int** valuebytes) {
+  if (iblock < 0 || iblock + 1 >= (int)blk_.start.size()) fail("Invalid page request for multivalue_block");
+  const int64_t j0 = blk_.start[iblock], j1 = blk_.start[iblock + 1];
+  *mv = blk_.mv + blk_.boff[iblock];
+  *valuebytes = const_cast<int*>(blk_.sizes + j0);
+  return (int)(j1 - j0);
+}
+
+uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
+  start();
+  need_kmv("reduce");
+  KeyValue kvb(device());
+  run_host_kmv(*kmv, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
+  kv = kvb.finish();
+  kmv.reset();
+  stats("Reduce", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dtype) {
+  start();
+  need_kmv("reduce");
+  kv = mrh::reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype);
+  kmv.reset();
+  stats("Reduce", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
+  start();
+  need_kmv("reduce");
+  KeyValue kvb(device());
+  fn(*kmv, kvb);
+  kv = kvb.finish();
+  kmv.reset();
+  stats("Reduce", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
+  start();
+  need_kv("compress");
+  KMV m = mrh::convert(*kv, &last_convert);
+  KeyValue kvb(device());
+  run_host_kmv(m, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
+  kv = kvb.finish();
+  stats("Compress", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& dtype) {
+  start();
+  need_kv("compress");
+  KMV m = mrh::convert(*kv, &last_convert);
+  kv = mrh::reduce_builtin(m, op, dtype.empty() ? "int32" : dtype);
+  stats("Compress", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
+  start();
+  need_kv("scan");
+  HostCol k = host_col(kv->kdata, kv->koff, kv->kw), v = host_col(kv->vdata, kv->voff, kv->vw);
+  for (int64_t i = 0; i < kv->n; ++i) fn(k.at(i), (int)k.len(i), v.at(i), (int)v.len(i));
+  stats("Scan", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::scan_kmv(const ScanKMVFn& fn) {  // :1984-2065
+  start();
+  need_kmv("scan");
+  run_host_kmv(*kmv, fn);
+  stats("Scan", 1);
+  return count(kmv->nkey);
+}
+
+// ====================================================================== sorting
+
+namespace {
+// host stable sort of one column with a user comparator -> device int32 perm
+at::Tensor host_perm(const at::Tensor& data, const at::Tensor& off, int w, int64_t n, const CompareFn& fn,
+                     at::Device dev) {
+  HostCol c = host_col(data, off, w);
+  std::vector<int32_t> p((size_t)n);
+  std::iota(p.begin(), p.end(), 0);
+  std::stable_sort(p.begin(), p.end(),
+                   [&](int32_t a, int32_t b) { return fn(c.at(a), (int)c.len(a), c.at(b), (int)c.len(b)) < 0; });
+  return at::from_blob(p.data(), {n}, at::TensorOptions().dtype(at::kInt)).clone().to(dev);
+}
+}  // namespace
+
+uint64_t MapReduce::sort_keys(int flag) {  // :2102-2126
+  start();
+  need_kv("sort_keys");
+  kv = sort_kv(*kv, flag, false);
+  stats("Sort_keys", 0);
+  return count(kv->n);
+}
+uint64_t MapReduce::sort_keys(const CompareFn& fn) {  // :2134-2149
+  start();
+  need_kv("sort_keys");
+  if (kv->n > 1) kv = mrh::gather(*kv, host_perm(kv->kdata, kv->koff, kv->kw, kv->n, fn, device()));
+  stats("Sort_keys", 0);
+  return count(kv->n);
+}
+uint64_t MapReduce::sort_values(int flag) {  // :2156-2180
+  start();
+  need_kv("sort_values");
+  kv = sort_kv(*kv, flag, true);
+  stats("Sort_values", 0);
+  return count(kv->n);
+}
+uint64_t MapReduce::sort_values(const CompareFn& fn) {  // :2188-2203
+  start();
+  need_kv("sort_values");
+  if (kv->n > 1) kv = mrh::gather(*kv, host_perm(kv->vdata, kv->voff, kv->vw, kv->n, fn, device()));
+  stats("Sort_values", 0);
+  return count(kv->n);
+}
+uint64_t MapReduce::sort_multivalues(int flag) {  // :2210-2352
+  start();
+  need_kmv("sort_multivalues");
+  kmv = mrh::sort_multivalues(*kmv, flag);
+  stats("Sort_multivalues", 1);
+  return count(kmv->nkey);
+}
+uint64_t MapReduce::sort_multivalues(const CompareFn& fn) {
+  start();
+  need_kmv("sort_multivalues");
+  KMV& m = *kmv;
+  HostCol v = host_col(m.vdata, m.voff, m.vw);
+  at::Tensor seg = m.seg.to(at::kCPU).contiguous();
+  const int64_t* s = seg.data_ptr<int64_t>();
+  std::vector<int32_t> p((size_t)m.nval);
+  std::iota(p.begin(), p.end(), 0);
+  for (int64_t i = 0; i < m.nkey; ++i)
+    std::stable_sort(p.begin() + s[i], p.begin() + s[i + 1], [&](int32_t a, int32_t b) {
+      return fn(v.at(a), (int)v.len(a), v.at(b), (int)v.len(b)) < 0;
+    });
+  at::Tensor perm = at::from_blob(p.data(), {m.nval}, at::TensorOptions().dtype(at::kInt)).clone().to(device());
+  at::Tensor noff;
+  m.vdata = gather_rows(m.vdata, m.voff, m.vw, perm, m.vw < 0 ? &noff : nullptr);
+  if (m.vw < 0) m.voff = noff;
+  stats("Sort_multivalues", 1);
+  return count(m.nkey);
+}
+
+// ====================================================================== print
+
+void MapReduce::print(int proc, int nstride, int kflag, int vflag) { print(nullptr, 0, proc, nstride, kflag, vflag); }
+
+void MapReduce::print(const char* file, int fflag, int proc, int nstride, int kflag, int vflag) {
+  if (!kv && !kmv) fail("Cannot print without KeyValue or KeyMultiValue");
+  if (kflag < 0 || kflag > 7 || vflag < 0 || vflag > 7 || nstride < 1) fail("Invalid print args");
+  const int me = comm_->rank();
+  std::string text;
+  int cnt = 0;
+  if (kv) {
+    HostCol k = host_col(kv->kdata, kv->koff, kv->kw), v = host_col(kv->vdata, kv->voff, kv->vw);
+    for (int64_t i = 0; i < kv->n; ++i) {
+      if (++cnt != nstride) continue;
+      cnt = 0;
+      text += fmt("KV pair: proc %d, sizes %d %d, key ", me, (int)k.len(i), (int)v.len(i)) +
+              fmt_item(k.at(i), k.len(i), kflag) + ", value " + fmt_item(v.at(i), v.len(i), vflag) + "\n";
+    }
+  } else {
+    HostCol k = host_col(kmv->keys.kdata, kmv->keys.koff, kmv->keys.kw), v = host_col(kmv->vdata, kmv->voff, kmv->vw);
+    at::Tensor seg = kmv->seg.to(at::kCPU).contiguous();
+    const int64_t* s = seg.data_ptr<int64_t>();
+    for (int64_t i = 0; i < kmv->nkey; ++i) {
+      if (++cnt != nstride) continue;
+      cnt = 0;
+      int64_t mvb = 0;
+      std::string vs;
+      for (int64_t j = s[i]; j < s[i + 1]; ++j) {
+        mvb += v.len(j);
+        if (vflag) vs += fmt_item(v.at(j), v.len(j), vflag) + " ";
+      }
+      if (!vflag) vs = "NULL";
+      text += fmt("KMV pair: proc %d, nvalues %d, sizes %d %d, key ", me, (int)(s[i + 1] - s[i]), (int)k.len(i),
+                  (int)mvb) +
+              fmt_item(k.at(i), k.len(i), kflag) + ", values " + vs + "\n";
+    }
+  }
+  auto emit = [&](const char* path, const char* mode) {
+    if (!path) {
+      out(text);
+      return;
+    }
+    std::FILE* f = std::fopen(path, mode);
+    if (!f) fail(std::string("Could not open print file ") + path);
+    std::fwrite(text.data(), 1, text.size(), f);
+    std::fclose(f);
+    wsize += (int64_t)text.size();
+  };
+  if (proc >= 0) {
+    if (proc == me) emit(file, "w");
+    return;
+  }
+  if (file && fflag == 1) {
+    std::string p = std::string(file) + "." + std::to_string(me);
+    emit(p.c_str(), "w");
+    return;
+  }
+  // token ring: ranks print in order (reference :1696-1709)
+  if (file && me == 0) emit(file, "w");
+  for (int r = 0; r < comm_->size(); ++r) {
+    comm_->barrier();
+    if (r == me && !(file && me == 0)) emit(file, "a");
+  }
+  comm_->barrier();
+}
+
+// ====================================================================== stats
+
+uint64_t MapReduce::kv_stats(int level) {  // :2937-2966
+  need_kv("print stats");
+  std::vector<int64_t> t = comm_->allreduce({kv->n, kv->key_bytes(), kv->value_bytes(), kv->nbytes()}, Comm::SUM);
+  const double mb = 1024.0 * 1024.0;
+  if (level == 1 && comm_->rank() == 0)
+    out(fmt("%" PRId64 " pairs, %.3g Mb keys, %.3g Mb values, %.3g Mb, 1 pages\n", t[0], t[1] / mb, t[2] / mb,
+            t[3] / mb));
+  if (level == 2) {
+    histo((double)kv->n, "  KV pairs:");
+    histo(kv->key_bytes() / mb, "  Kdata (Mb):");
+    histo(kv->value_bytes() / mb, "  Vdata (Mb):");
+  }
+  return (uint64_t)t[0];
+}
+
+uint64_t MapReduce::kmv_stats(int level) {  // :2972-3001
+  need_kmv("print stats");
+  const KMV& m = *kmv;
+  const int64_t vb = m.vw >= 0 ? m.nval * m.vw : (m.nval ? m.voff[m.nval].item<int64_t>() : 0);
+  std::vector<int64_t> t = comm_->allreduce({m.nkey, m.keys.key_bytes(), vb, m.nbytes()}, Comm::SUM);
+  const double mb = 1024.0 * 1024.0;
+  if (level == 1 && comm_->rank() == 0)
+    out(fmt("%" PRId64 " pairs, %.3g Mb keys, %.3g Mb values, %.3g Mb, 1 pages\n", t[0], t[1] / mb, t[2] / mb,
+            t[3] / mb));
+  if (level == 2) {
+    histo((double)m.nkey, "  KMV pairs:");
+    histo(m.keys.key_bytes() / mb, "  Kdata (Mb):");
+    histo(vb / mb, "  Vdata (Mb):");
+  }
+  return (uint64_t)t[0];
+}
+
+void MapReduce::cummulative_stats(int level, int reset) {  // :3007-3066
+  const double mb = 1024.0 * 1024.0, gb = mb * 1024.0;
+  const int me = comm_->rank();
+  if (me == 0) out("MapReduce-MPI (gpu_mapreduce_amd native engine)\n");
+  int64_t mx = comm_->allreduce(msizemax.load(), Comm::MAX), sm = comm_->allreduce(msizemax.load(), Comm::SUM);
+  if (me == 0) out(fmt("Cummulative hi-water mem = %.3g Mb any proc, %.3g Gb all procs\n", mx / mb, sm / gb));
+  std::vector<int64_t> c = comm_->allreduce({cssize.load(), crsize.load()}, Comm::SUM);
+  double ct = comm_->allreduce_f64(commtime, Comm::SUM);
+  if (c[0] || c[1]) {
+    if (me == 0)
+      out(fmt("Cummulative comm = %.3g Mb send, %.3g Mb recv, %.3g secs\n", c[0] / mb, c[1] / mb,
+              ct / comm_->size()));
+    if (level == 2) {
+      histo(cssize / mb, "  Send (Mb):");
+      histo(crsize / mb, "  Recv (Mb):");
+    }
+  }
+  std::vector<int64_t> io = comm_->allreduce({rsize.load(), wsize.load()}, Comm::SUM);
+  if ((io[0] || io[1]) && me == 0) out(fmt("Cummulative I/O = %.3g Mb read, %.3g Mb write\n", io[0] / mb, io[1] / mb));
+  if (reset) rsize = wsize = cssize = crsize = 0;
+}
+
+// ====================================================================== spill tier
+
+void MapReduce::spill() {
+  const bool pin = device().is_cuda();
+  if (kv) kv = kv_host(*kv, pin);
+  if (kmv) kmv = kmv_to(*kmv, at::Device(at::kCPU), pin);
+}
+
+void MapReduce::unspill() {
+  if (kv) kv = kv_to(*kv, device());
+  if (kmv) kmv = kmv_to(*kmv, device(), false);
+}
+
+}  // namespace mrh

@@ -1,0 +1,182 @@
+// The native MapReduce object: MR-MPI's user API (reference src/mapreduce.h:28-126,
+// src/mapreduce.cpp:93-3574) on the device-resident engine of kv.h.
+//
+// Same method names, settings (names, defaults, meaning), and return values
+// (every data op returns the GLOBAL pair count, an Allreduce SUM). The MR owns
+// one KV or one KMV (never both), as SoA tensors in HBM; all data-plane work
+// (hash/partition, RCCL shuffle, group-by, sorts, segmented reduces, gathers)
+// runs in the engine ops.
+//
+// Callbacks come in two tiers:
+//  * host callbacks with the exact MR-MPI shapes (map task / file / chunk / mr,
+//    reduce/compress, scan kv/kmv, hash, compare): the engine stages the data
+//    to host once per op and the callback sees the reference's (key, kb, mv,
+//    nvalues, valuebytes) views, including the multi-block protocol for keys
+//    whose values exceed one page (nvalues == 0 + multivalue_block*());
+//  * batch callbacks that receive the whole device KV/KMV and append device
+//    KVs (kernels / ATen ops), which keep the data in HBM end to end.
+#pragma once
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "comm.h"
+#include "keyvalue.h"
+#include "kv.h"
+
+namespace mrh {
+
+class MapReduce;
+
+using MapTaskFn = std::function<void(int itask, KeyValue& kv)>;
+using MapFileFn = std::function<void(int itask, const char* fname, KeyValue& kv)>;
+using MapChunkFn = std::function<void(int itask, char* str, int size, KeyValue& kv)>;
+using MapKVFn = std::function<void(uint64_t itask, char* key, int kb, char* value, int vb, KeyValue& kv)>;
+using ReduceFn = std::function<void(char* key, int kb, char* mv, int nvalues, int* valuebytes, KeyValue& kv)>;
+using ScanKVFn = std::function<void(char* key, int kb, char* value, int vb)>;
+using ScanKMVFn = std::function<void(char* key, int kb, char* mv, int nvalues, int* valuebytes)>;
+using HashFn = std::function<int(char* key, int kb)>;
+using CompareFn = std::function<int(char* a, int alen, char* b, int blen)>;
+using MapBatchFn = std::function<void(const KV& src, KeyValue& kv)>;
+using ReduceBatchFn = std::function<void(const KMV& src, KeyValue& kv)>;
+
+struct Settings {
+  int mapstyle = 0;    // 0 chunk, 1 stride, 2 dynamic work queue
+  int all2all = 1;     // accepted; the shuffle is always one RCCL all-to-all per column
+  int verbosity = 0;   // 0 none, 1 totals, 2 per-proc histograms
+  int timer = 0;       // 0 none, 1 barrier + rank-0 time, 2 per-proc histogram
+  int memsize = 64;    // MB per page (negative: bytes); sets the host block size of long KMV values
+  int minpage = 0, maxpage = 0, freepage = 1, outofcore = 0, zeropage = 0;
+  int keyalign = 4, valuealign = 4;
+  std::string fpath = ".";
+};
+
+class MapReduce {
+ public:
+  explicit MapReduce(CommPtr comm);
+  ~MapReduce();
+  MapReduce(const MapReduce&) = delete;
+  MapReduce& operator=(const MapReduce&) = delete;
+
+  Settings set;
+  int mapfilecount = 0;
+
+  // ---------------------------------------------------------------- data
+  std::optional<KV> kv;
+  std::optional<KMV> kmv;
+  ConvertStats last_convert;
+
+  // ---------------------------------------------------------------- object ops
+  std::unique_ptr<MapReduce> copy() const;
+  uint64_t add(MapReduce& other);
+  uint64_t aggregate(const HashFn& hash = nullptr);
+  uint64_t aggregate_dest(const at::Tensor& dest);  // explicit int32 destination per pair
+  uint64_t broadcast(int root);
+  uint64_t clone();
+  uint64_t close();
+  uint64_t collapse(const char* key, int kb);
+  uint64_t collate(const HashFn& hash = nullptr);
+  uint64_t compress(const ReduceFn& fn);
+  uint64_t compress_builtin(const std::string& op, const std::string& dtype);
+  uint64_t convert();
+  uint64_t gather(int nprocs);
+  void open(int addflag = 0);
+  KeyValue& kv_open();  // the builder other MRs' callbacks add into while open
+
+  // map variants (reference :1044-1642); addflag 1 appends to the existing KV
+  uint64_t map(int nmap, const MapTaskFn& fn, int addflag = 0);
+  uint64_t map_file(const std::vector<std::string>& files, int selfflag, int recurse, int readflag,
+                    const MapFileFn& fn, int addflag = 0);
+  uint64_t map_file_char(int nmap, const std::vector<std::string>& files, int selfflag, int recurse, int readflag,
+                         char sepchar, int delta, const MapChunkFn& fn, int addflag = 0);
+  uint64_t map_file_str(int nmap, const std::vector<std::string>& files, int selfflag, int recurse, int readflag,
+                        const std::string& sepstr, int delta, const MapChunkFn& fn, int addflag = 0);
+  uint64_t map_mr(MapReduce& src, const MapKVFn& fn, int addflag = 0);
+  uint64_t map_batch(int nmap, const MapTaskFn& fn, int addflag = 0) { return map(nmap, fn, addflag); }
+  uint64_t map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addflag = 0);
+
+  uint64_t reduce(const ReduceFn& fn);
+  uint64_t reduce_builtin(const std::string& op, const std::string& dtype);
+  uint64_t reduce_batch(const ReduceBatchFn& fn);
+  uint64_t scan_kv(const ScanKVFn& fn);
+  uint64_t scan_kmv(const ScanKMVFn& fn);
+  uint64_t scrunch(int nprocs, const char* key, int kb);
+
+  // multi-block access to one long KMV value list from inside reduce/scan
+  // callbacks (reference :1874-1925); `token` is the valuebytes pointer the
+  // callback received with nvalues == 0
+  uint64_t multivalue_blocks(int& nblock) const;
+  void multivalue_block_select(int which) { block_select_ = which; }
+  int multivalue_block(int iblock, char** mv, int** valuebytes);
+
+  uint64_t sort_keys(int flag);
+  uint64_t sort_keys(const CompareFn& fn);
+  uint64_t sort_values(int flag);
+  uint64_t sort_values(const CompareFn& fn);
+  uint64_t sort_multivalues(int flag);
+  uint64_t sort_multivalues(const CompareFn& fn);
+
+  // print (reference :1671-1761): kflag/vflag 0 none,1 int,2 uint64,3 float,4 double,5 str,6 strn,7 raw bytes
+  void print(int proc, int nstride, int kflag, int vflag);
+  void print(const char* file, int fflag, int proc, int nstride, int kflag, int vflag);
+
+  uint64_t kv_stats(int level);
+  uint64_t kmv_stats(int level);
+  void cummulative_stats(int level, int reset);
+  void set_fpath(const std::string& p) { set.fpath = p; }
+
+  // host spill tier: move the data to pinned host DRAM and back
+  void spill();
+  void unspill();
+
+  const CommPtr& comm() const { return comm_; }
+  int my_proc() const { return comm_->rank(); }
+  int num_procs() const { return comm_->size(); }
+  at::Device device() const { return comm_->device(); }
+
+  // ---------------------------------------------------------------- static counters
+  // (reference src/mapreduce.h:46-57)
+  static std::atomic<int> instances_now, instances_ever;
+  static std::atomic<int64_t> msize, msizemax, rsize, wsize, cssize, crsize;
+  static double commtime;
+
+  // file list expansion shared with the Python layer (reference :2812-2931)
+  static std::vector<std::string> find_files(const Comm& comm, const std::vector<std::string>& files, int selfflag,
+                                             int recurse, int readflag);
+
+ private:
+  void start();
+  void stats(const char* heading, int which);
+  void need_kv(const char* what) const;
+  void need_kmv(const char* what) const;
+  void note_shuffle(const ShuffleStats& st);
+  uint64_t count(int64_t n) const { return (uint64_t)comm_->allreduce(n, Comm::SUM); }
+  std::vector<int> my_tasks(int nmap);
+  uint64_t finish_map(KeyValue& kvb, int addflag, const char* heading = "Map");
+  uint64_t map_chunks(int nmap, const std::vector<std::string>& files, int selfflag, int recurse, int readflag,
+                      const std::string& sep, bool is_char, int delta, const MapChunkFn& fn, int addflag);
+  void run_host_kmv(const KMV& kmv, const std::function<void(char*, int, char*, int, int*)>& fn);
+  void histo(double v, const char* heading) const;
+  int64_t block_bytes() const;
+
+  CommPtr comm_;
+  std::unique_ptr<KeyValue> open_;
+  int open_add_ = 0;
+  double t0_ = 0;
+  int64_t cs0_ = 0, cr0_ = 0;
+  int instance_me_ = 0;
+  // multi-block state of the key currently handed to a host callback
+  struct Blocks {
+    char* mv = nullptr;
+    const int* sizes = nullptr;
+    int64_t nval = 0;
+    std::vector<int64_t> start;  // value index at the start of each block
+    std::vector<int64_t> boff;   // byte offset of each block start relative to mv
+  } blk_;
+  int block_select_ = 0;
+};
+
+}  // namespace mrh

@@ -107,7 +107,7 @@ class InvertedIndex:
             path = os.path.join(self.out_dir, f"InvertedIndex-{self.mr.nprocs}-{self.mr.me}")
             with open(path, "wb") as f:
                 f.write(host.numpy().tobytes())
-            MapReduce.wsize += host.numel()
+            MapReduce.count_io(write=host.numel())
 
     def run(self, phases=None):
         """phases: optional dict; if given, per-stage seconds (device-synced)

@@ -43,6 +43,22 @@ class Comm:
         self.is_cuda = self.device.startswith("cuda")
         # the c10d ProcessGroup handed to the native shuffle (None when P == 1)
         self.pg = group if (group is not None and self.size > 1) else None
+        self._native = None
+
+    @property
+    def native(self):
+        """The C++ communicator (csrc/engine/comm.h) the native MapReduce uses:
+        same process group, plus the rendezvous store for mapstyle 2."""
+        if self._native is None:
+            from .._ext import C
+            store = None
+            if self.size > 1:
+                try:
+                    store = dist.distributed_c10d._get_default_store()
+                except Exception:
+                    store = None
+            self._native = C.NativeComm(self.pg, self.device, store)
+        return self._native
 
     # ---- scalar collectives (every MR op returns a global count) ----------
     def _t(self, vals, dtype):

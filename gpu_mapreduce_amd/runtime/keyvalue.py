@@ -56,9 +56,14 @@ def _byte_view(t: torch.Tensor) -> torch.Tensor:
 class KeyValue:
     """Append-only KV builder handed to map/reduce callbacks."""
 
-    def __init__(self, device: str):
-        self._h = C.HostKV(device)
-        self.device = device
+    def __init__(self, device: str | None = None, native=None):
+        self._h = native if native is not None else C.HostKV(device)
+        self.device = self._h.device
+
+    @classmethod
+    def wrap(cls, native):
+        """Python view of a native KeyValue handed to a callback by the engine."""
+        return cls(native=native)
 
     # --- MR-MPI KeyValue::add(key, keybytes, value, valuebytes) ----------------
     def add(self, key, value=None):

@@ -1,65 +1,103 @@
-"""Build the native engine in-tree: gpu_mapreduce_amd/_C*.so
+"""Build the native engine in-tree.
 
-Two explicit stages, no source translation step:
+Three explicit stages, no source translation step:
   1. csrc/kernels/*.hip -> build/kernels/*.o with hipcc, device code for gfx950
-     only (parallel, incremental on source/header mtimes);
-  2. csrc/engine/*.cpp (ATen / c10d / pybind11 host code) with the host C++
-     compiler, linked with the kernel objects, libamdhip64 and torch's HIP libs.
-Usage: python setup.py build_ext --inplace   (MAX_JOBS bounds hipcc parallelism)
+     only;
+  2. csrc/engine/*.cpp (except bind.cpp) + csrc/capi/*.cpp -> build/host/*.o with
+     the host C++ compiler against ATen/c10d, linked with the kernel objects into
+     gpu_mapreduce_amd/libmrhip.so — the engine + native MapReduce + MR_* C API
+     (what C/C++ programs link against);
+  3. the Python module gpu_mapreduce_amd/_C (csrc/engine/bind.cpp), linked to
+     libmrhip.so.
+Steps 1-2 are parallel (MAX_JOBS) and incremental on source/header mtimes.
+Usage: python setup.py build_ext --inplace
 """
 import glob
 import os
 import subprocess
+import sys
 from concurrent.futures import ThreadPoolExecutor
 
 from setuptools import setup
-from torch.utils.cpp_extension import BuildExtension, CppExtension
+from torch.utils.cpp_extension import BuildExtension, CppExtension, include_paths
 
 here = os.path.dirname(os.path.abspath(__file__))
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("MRH_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
-KDIR = os.path.join("csrc", "kernels")
-OBJDIR = os.path.join(here, "build", "kernels")
-hip_sources = sorted(glob.glob(os.path.join(KDIR, "*.hip")))
-kernel_headers = sorted(glob.glob(os.path.join(KDIR, "*.h")))
-cpp_sources = sorted(glob.glob(os.path.join("csrc", "engine", "*.cpp")))
+CXX = os.environ.get("CXX", "g++")
+PKG = os.path.join(here, "gpu_mapreduce_amd")
+BUILD = os.path.join(here, "build")
+LIB = os.path.join(PKG, "libmrhip.so")
+
+hip_sources = sorted(glob.glob(os.path.join(here, "csrc", "kernels", "*.hip")))
+kernel_headers = sorted(glob.glob(os.path.join(here, "csrc", "kernels", "*.h")))
+host_sources = sorted(s for s in glob.glob(os.path.join(here, "csrc", "engine", "*.cpp"))
+                      if not s.endswith("bind.cpp")) + sorted(glob.glob(os.path.join(here, "csrc", "capi", "*.cpp")))
+host_headers = sorted(glob.glob(os.path.join(here, "csrc", "engine", "*.h")) +
+                      glob.glob(os.path.join(here, "csrc", "capi", "*.h"))) + kernel_headers
+
 HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
             "-Wno-unused-result", "-Wno-unused-value", "-I", os.path.join(here, "csrc")]
-
-
-def _obj(src):
-    return os.path.join(OBJDIR, os.path.splitext(os.path.basename(src))[0] + ".o")
-
-
-def compile_kernels():
-    os.makedirs(OBJDIR, exist_ok=True)
-    hdr_t = max([os.path.getmtime(h) for h in kernel_headers] + [0])
-
-    def one(src):
-        o = _obj(src)
-        if os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(src), hdr_t):
-            return o
-        cmd = [HIPCC, *HIPFLAGS, "-c", src, "-o", o]
-        print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-        return o
-    jobs = int(os.environ.get("MAX_JOBS", "8"))
-    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        return list(ex.map(one, hip_sources))
-
-
-class Build(BuildExtension):
-    def build_extensions(self):
-        objs = compile_kernels()
-        for ext in self.extensions:
-            ext.extra_objects = list(objs)
-        super().build_extensions()
 
 
 def _torch_lib():
     import torch
     return os.path.join(os.path.dirname(torch.__file__), "lib")
+
+
+def _abi():
+    import torch
+    return int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+HOSTDEFS = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={_abi()}"]
+HOSTFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-sign-compare", *HOSTDEFS,
+             "-I", os.path.join(here, "csrc"), "-I", os.path.join(ROCM, "include")] + \
+            [f"-I{p}" for p in include_paths()]
+LINKLIBS = [f"-L{os.path.join(ROCM, 'lib')}", f"-L{_torch_lib()}", "-lamdhip64", "-lc10_hip", "-ltorch_hip",
+            "-lc10", "-ltorch", "-ltorch_cpu", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}",
+            f"-Wl,-rpath,{_torch_lib()}"]
+
+
+def _stale(obj, deps):
+    return not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(d) for d in deps)
+
+
+def _compile_all(jobs):
+    os.makedirs(os.path.join(BUILD, "kernels"), exist_ok=True)
+    os.makedirs(os.path.join(BUILD, "host"), exist_ok=True)
+    tasks = []
+    for s in hip_sources:
+        o = os.path.join(BUILD, "kernels", os.path.splitext(os.path.basename(s))[0] + ".o")
+        tasks.append((o, [HIPCC, *HIPFLAGS, "-c", s, "-o", o], [s] + kernel_headers))
+    for s in host_sources:
+        o = os.path.join(BUILD, "host", os.path.splitext(os.path.basename(s))[0] + ".o")
+        tasks.append((o, [CXX, *HOSTFLAGS, "-c", s, "-o", o], [s] + host_headers))
+
+    def one(t):
+        o, cmd, deps = t
+        if _stale(o, deps):
+            print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+        return o
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        return list(ex.map(one, tasks))
+
+
+def build_native():
+    objs = _compile_all(int(os.environ.get("MAX_JOBS", "8")))
+    if _stale(LIB, objs):
+        cmd = [CXX, "-shared", "-o", LIB, *objs, *LINKLIBS]
+        print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+class Build(BuildExtension):
+    def build_extensions(self):
+        build_native()
+        super().build_extensions()
 
 
 setup(
@@ -69,13 +107,13 @@ setup(
     ext_modules=[
         CppExtension(
             "gpu_mapreduce_amd._C",
-            cpp_sources,
+            [os.path.join("csrc", "engine", "bind.cpp")],
             include_dirs=[os.path.join(here, "csrc"), os.path.join(ROCM, "include")],
             define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
-            library_dirs=[os.path.join(ROCM, "lib"), _torch_lib()],
-            libraries=["amdhip64", "c10_hip", "torch_hip"],
+            library_dirs=[PKG, os.path.join(ROCM, "lib"), _torch_lib()],
+            libraries=["mrhip", "amdhip64", "c10_hip", "torch_hip"],
             extra_compile_args=["-O3", "-std=c++17", "-Wno-unused-result", "-Wno-sign-compare"],
-            extra_link_args=[f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"],
+            extra_link_args=["-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"],
         )
     ],
     cmdclass={"build_ext": Build.with_options(use_ninja=True)},
