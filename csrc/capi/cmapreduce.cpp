@@ -226,6 +226,9 @@ uint64_t MR_sort_multivalues_flag(void* p, int flag) {
   return guard([&] { return M(p)->sort_multivalues(flag); }, (uint64_t)0);
 }
 
+void MR_save(void* p, const char* path) { guardv([&] { M(p)->save(path); }); }
+uint64_t MR_load(void* p, const char* path) { return guard([&] { return M(p)->load(path); }, (uint64_t)0); }
+
 uint64_t MR_kv_stats(void* p, int level) { return guard([&] { return M(p)->kv_stats(level); }, (uint64_t)0); }
 uint64_t MR_kmv_stats(void* p, int level) { return guard([&] { return M(p)->kmv_stats(level); }, (uint64_t)0); }
 void MR_cummulative_stats(void* p, int level, int reset) { guardv([&] { M(p)->cummulative_stats(level, reset); }); }

@@ -93,6 +93,10 @@ uint64_t MR_sort_values_flag(void *MRptr, int flag);
 uint64_t MR_sort_multivalues(void *MRptr, int (*mycompare)(char *, int, char *, int));
 uint64_t MR_sort_multivalues_flag(void *MRptr, int flag);
 
+/* checkpoint / restart of this rank's KV or KMV (binary SoA file per rank) */
+void MR_save(void *MRptr, const char *path);
+uint64_t MR_load(void *MRptr, const char *path);
+
 uint64_t MR_kv_stats(void *MRptr, int level);
 uint64_t MR_kmv_stats(void *MRptr, int level);
 void MR_cummulative_stats(void *MRptr, int level, int reset);

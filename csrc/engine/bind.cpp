@@ -289,6 +289,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("kv_stats", &MR::kv_stats)
       .def("kmv_stats", &MR::kmv_stats)
       .def("cummulative_stats", &MR::cummulative_stats)
+      .def("save", &MR::save)
+      .def("load", &MR::load)
       .def("spill", &MR::spill)
       .def("unspill", &MR::unspill)
       .def("my_proc", &MR::my_proc)

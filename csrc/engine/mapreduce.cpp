@@ -2,6 +2,8 @@
 // method as src/mapreduce.cpp:<lines>.
 #include "mapreduce.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <algorithm>
 #include <cinttypes>
 #include <cstdarg>
@@ -30,6 +32,13 @@ std::function<void(const std::string&)>& screen_sink() {
 }
 
 namespace {
+
+// roctx range per MapReduce op: `rocprofv3 --marker-trace` shows every op
+// (map, aggregate, convert, reduce, ...) around its kernels and RCCL calls
+struct OpTrace {
+  explicit OpTrace(const char* name) { roctxRangePushA(name); }
+  ~OpTrace() { roctxRangePop(); }
+};
 
 [[noreturn]] void fail(const std::string& m) { throw std::runtime_error(m); }
 
@@ -271,6 +280,7 @@ void MapReduce::note_shuffle(const ShuffleStats& st) {
 
 uint64_t MapReduce::add(MapReduce& other) {  // :348-374
   start();
+  OpTrace tr_(__func__);
   need_kv("add");
   if (!other.kv) fail("MapReduce passed to add() does not have KeyValue pairs");
   kv = concat({*kv, *other.kv}, device());
@@ -332,6 +342,7 @@ uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) 
 
 uint64_t MapReduce::map(int nmap, const MapTaskFn& fn, int addflag) {  // :1044-1051
   start();
+  OpTrace tr_(__func__);
   KeyValue kvb(device());
   for (int t : my_tasks(nmap)) fn(t, kvb);
   return finish_map(kvb, addflag);
@@ -365,6 +376,7 @@ std::vector<std::string> MapReduce::find_files(const Comm& comm, const std::vect
 uint64_t MapReduce::map_file(const std::vector<std::string>& files, int selfflag, int recurse, int readflag,
                              const MapFileFn& fn, int addflag) {  // :1060-1092
   start();
+  OpTrace tr_(__func__);
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
   KeyValue kvb(device());
@@ -394,6 +406,7 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
                                int readflag, const std::string& sep, bool is_char, int delta, const MapChunkFn& fn,
                                int addflag) {
   start();
+  OpTrace tr_(__func__);
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
   const int nfile = (int)fl.size();
@@ -469,6 +482,7 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
 
 uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  // :1560-1642
   start();
+  OpTrace tr_(__func__);
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   HostCol k = host_col(s.kdata, s.koff, s.kw), v = host_col(s.vdata, s.voff, s.vw);
@@ -486,6 +500,7 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
 
 uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addflag) {
   start();
+  OpTrace tr_(__func__);
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   KeyValue kvb(device());
@@ -504,6 +519,7 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
 
 uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
   start();
+  OpTrace tr_(__func__);
   need_kv("aggregate");
   if (comm_->size() > 1) {
     ShuffleStats st;
@@ -528,6 +544,7 @@ uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
 
 uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
   start();
+  OpTrace tr_(__func__);
   need_kv("aggregate");
   if (comm_->size() > 1) {
     ShuffleStats st;
@@ -540,6 +557,7 @@ uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
 
 uint64_t MapReduce::broadcast(int root) {  // :569-623
   start();
+  OpTrace tr_(__func__);
   need_kv("broadcast");
   if (comm_->size() > 1) kv = mrh::broadcast(*kv, root, comm_->pg());
   stats("Broadcast", 0);
@@ -548,6 +566,7 @@ uint64_t MapReduce::broadcast(int root) {  // :569-623
 
 uint64_t MapReduce::gather(int nprocs) {  // :893-1036
   start();
+  OpTrace tr_(__func__);
   need_kv("gather");
   if (nprocs < 1 || nprocs > comm_->size()) fail("Invalid proc count for gather");
   if (comm_->size() > 1 && nprocs < comm_->size()) {
@@ -563,6 +582,7 @@ uint64_t MapReduce::gather(int nprocs) {  // :893-1036
 
 uint64_t MapReduce::convert() {  // :861-886
   start();
+  OpTrace tr_(__func__);
   need_kv("convert");
   kmv = mrh::convert(*kv, &last_convert);
   kv.reset();
@@ -572,6 +592,7 @@ uint64_t MapReduce::convert() {  // :861-886
 
 uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
   start();
+  OpTrace tr_(__func__);
   need_kv("collate");
   const int v = set.verbosity, t = set.timer;
   set.verbosity = set.timer = 0;
@@ -585,6 +606,7 @@ uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
 
 uint64_t MapReduce::clone() {  // :631-652
   start();
+  OpTrace tr_(__func__);
   need_kv("clone");
   kmv = mrh::clone(*kv);
   kv.reset();
@@ -594,6 +616,7 @@ uint64_t MapReduce::clone() {  // :631-652
 
 uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
   start();
+  OpTrace tr_(__func__);
   need_kv("collapse");
   kmv = mrh::collapse(*kv, std::string(key, (size_t)kb));
   kv.reset();
@@ -603,6 +626,7 @@ uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
 
 uint64_t MapReduce::scrunch(int nprocs, const char* key, int kb) {  // :2075-2095
   start();
+  OpTrace tr_(__func__);
   const int v = set.verbosity, t = set.timer;
   set.verbosity = set.timer = 0;
   gather(nprocs);
@@ -674,6 +698,7 @@ int MapReduce::multivalue_block(int iblock, char** mv, int** valuebytes) {
 
 uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
   start();
+  OpTrace tr_(__func__);
   need_kmv("reduce");
   KeyValue kvb(device());
   run_host_kmv(*kmv, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
@@ -685,6 +710,7 @@ uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
 
 uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dtype) {
   start();
+  OpTrace tr_(__func__);
   need_kmv("reduce");
   kv = mrh::reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype);
   kmv.reset();
@@ -694,6 +720,7 @@ uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dty
 
 uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
   start();
+  OpTrace tr_(__func__);
   need_kmv("reduce");
   KeyValue kvb(device());
   fn(*kmv, kvb);
@@ -705,6 +732,7 @@ uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
 
 uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
   start();
+  OpTrace tr_(__func__);
   need_kv("compress");
   KMV m = mrh::convert(*kv, &last_convert);
   KeyValue kvb(device());
@@ -716,6 +744,7 @@ uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
 
 uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& dtype) {
   start();
+  OpTrace tr_(__func__);
   need_kv("compress");
   KMV m = mrh::convert(*kv, &last_convert);
   kv = mrh::reduce_builtin(m, op, dtype.empty() ? "int32" : dtype);
@@ -725,6 +754,7 @@ uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& d
 
 uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
   start();
+  OpTrace tr_(__func__);
   need_kv("scan");
   HostCol k = host_col(kv->kdata, kv->koff, kv->kw), v = host_col(kv->vdata, kv->voff, kv->vw);
   for (int64_t i = 0; i < kv->n; ++i) fn(k.at(i), (int)k.len(i), v.at(i), (int)v.len(i));
@@ -734,6 +764,7 @@ uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
 
 uint64_t MapReduce::scan_kmv(const ScanKMVFn& fn) {  // :1984-2065
   start();
+  OpTrace tr_(__func__);
   need_kmv("scan");
   run_host_kmv(*kmv, fn);
   stats("Scan", 1);
@@ -757,6 +788,7 @@ at::Tensor host_perm(const at::Tensor& data, const at::Tensor& off, int w, int64
 
 uint64_t MapReduce::sort_keys(int flag) {  // :2102-2126
   start();
+  OpTrace tr_(__func__);
   need_kv("sort_keys");
   kv = sort_kv(*kv, flag, false);
   stats("Sort_keys", 0);
@@ -764,6 +796,7 @@ uint64_t MapReduce::sort_keys(int flag) {  // :2102-2126
 }
 uint64_t MapReduce::sort_keys(const CompareFn& fn) {  // :2134-2149
   start();
+  OpTrace tr_(__func__);
   need_kv("sort_keys");
   if (kv->n > 1) kv = mrh::gather(*kv, host_perm(kv->kdata, kv->koff, kv->kw, kv->n, fn, device()));
   stats("Sort_keys", 0);
@@ -771,6 +804,7 @@ uint64_t MapReduce::sort_keys(const CompareFn& fn) {  // :2134-2149
 }
 uint64_t MapReduce::sort_values(int flag) {  // :2156-2180
   start();
+  OpTrace tr_(__func__);
   need_kv("sort_values");
   kv = sort_kv(*kv, flag, true);
   stats("Sort_values", 0);
@@ -778,6 +812,7 @@ uint64_t MapReduce::sort_values(int flag) {  // :2156-2180
 }
 uint64_t MapReduce::sort_values(const CompareFn& fn) {  // :2188-2203
   start();
+  OpTrace tr_(__func__);
   need_kv("sort_values");
   if (kv->n > 1) kv = mrh::gather(*kv, host_perm(kv->vdata, kv->voff, kv->vw, kv->n, fn, device()));
   stats("Sort_values", 0);
@@ -785,6 +820,7 @@ uint64_t MapReduce::sort_values(const CompareFn& fn) {  // :2188-2203
 }
 uint64_t MapReduce::sort_multivalues(int flag) {  // :2210-2352
   start();
+  OpTrace tr_(__func__);
   need_kmv("sort_multivalues");
   kmv = mrh::sort_multivalues(*kmv, flag);
   stats("Sort_multivalues", 1);
@@ -792,6 +828,7 @@ uint64_t MapReduce::sort_multivalues(int flag) {  // :2210-2352
 }
 uint64_t MapReduce::sort_multivalues(const CompareFn& fn) {
   start();
+  OpTrace tr_(__func__);
   need_kmv("sort_multivalues");
   KMV& m = *kmv;
   HostCol v = host_col(m.vdata, m.voff, m.vw);
@@ -944,6 +981,127 @@ void MapReduce::spill() {
 void MapReduce::unspill() {
   if (kv) kv = kv_to(*kv, device());
   if (kmv) kmv = kmv_to(*kmv, device(), false);
+}
+
+}  // namespace mrh
+
+// ====================================================================== checkpoint
+
+namespace mrh {
+
+namespace {
+constexpr char kMagic[8] = {'M', 'R', 'H', 'K', 'V', '0', '0', '1'};
+
+std::string rank_path(const std::string& p, const Comm& c) {
+  return c.size() > 1 ? p + "." + std::to_string(c.rank()) : p;
+}
+void put_i64(std::FILE* f, int64_t v) {
+  if (std::fwrite(&v, 8, 1, f) != 1) throw std::runtime_error("save: write failed");
+}
+int64_t get_i64(std::FILE* f) {
+  int64_t v = 0;
+  if (std::fread(&v, 8, 1, f) != 1) throw std::runtime_error("load: truncated file");
+  return v;
+}
+// tensor as (present, dtype, numel, bytes)
+void put_t(std::FILE* f, const at::Tensor& t) {
+  put_i64(f, t.defined() ? 1 : 0);
+  if (!t.defined()) return;
+  at::Tensor h = t.to(at::kCPU).contiguous();
+  put_i64(f, (int64_t)h.scalar_type());
+  put_i64(f, h.numel());
+  const size_t nb = (size_t)h.numel() * h.element_size();
+  if (nb && std::fwrite(h.data_ptr(), 1, nb, f) != nb) throw std::runtime_error("save: write failed");
+}
+at::Tensor get_t(std::FILE* f, at::Device dev) {
+  if (!get_i64(f)) return at::Tensor();
+  auto st = (at::ScalarType)get_i64(f);
+  const int64_t n = get_i64(f);
+  at::Tensor h = at::empty({n}, at::TensorOptions().dtype(st));
+  const size_t nb = (size_t)n * h.element_size();
+  if (nb && std::fread(h.data_ptr(), 1, nb, f) != nb) throw std::runtime_error("load: truncated file");
+  return h.to(dev);
+}
+void put_kv(std::FILE* f, const KV& kv) {
+  put_i64(f, kv.n);
+  put_i64(f, kv.kw);
+  put_i64(f, kv.vw);
+  put_t(f, kv.kdata);
+  put_t(f, kv.koff);
+  put_t(f, kv.vdata);
+  put_t(f, kv.voff);
+}
+KV get_kv(std::FILE* f, at::Device dev) {
+  KV kv;
+  kv.n = get_i64(f);
+  kv.kw = (int)get_i64(f);
+  kv.vw = (int)get_i64(f);
+  kv.kdata = get_t(f, dev);
+  kv.koff = get_t(f, dev);
+  kv.vdata = get_t(f, dev);
+  kv.voff = get_t(f, dev);
+  return kv;
+}
+}  // namespace
+
+void MapReduce::save(const std::string& path) const {
+  if (!kv && !kmv) fail("Cannot save without KeyValue or KeyMultiValue");
+  const std::string p = rank_path(path, *comm_);
+  std::FILE* f = std::fopen(p.c_str(), "wb");
+  if (!f) fail("Could not open checkpoint file " + p);
+  std::fwrite(kMagic, 1, 8, f);
+  if (kv) {
+    put_i64(f, 0);
+    put_kv(f, *kv);
+  } else {
+    put_i64(f, 1);
+    put_kv(f, kmv->keys);
+    put_i64(f, kmv->nkey);
+    put_i64(f, kmv->nval);
+    put_i64(f, kmv->vw);
+    put_t(f, kmv->vdata);
+    put_t(f, kmv->voff);
+    put_t(f, kmv->seg);
+  }
+  wsize += std::ftell(f);
+  std::fclose(f);
+}
+
+uint64_t MapReduce::load(const std::string& path) {
+  const std::string p = rank_path(path, *comm_);
+  std::FILE* f = std::fopen(p.c_str(), "rb");
+  if (!f) fail("Could not open checkpoint file " + p);
+  char magic[8];
+  if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, kMagic, 8) != 0) {
+    std::fclose(f);
+    fail("Not a gpu_mapreduce_amd checkpoint: " + p);
+  }
+  int64_t n = 0;
+  try {
+    if (get_i64(f) == 0) {
+      kv = get_kv(f, device());
+      kmv.reset();
+      n = kv->n;
+    } else {
+      KMV m;
+      m.keys = get_kv(f, device());
+      m.nkey = get_i64(f);
+      m.nval = get_i64(f);
+      m.vw = (int)get_i64(f);
+      m.vdata = get_t(f, device());
+      m.voff = get_t(f, device());
+      m.seg = get_t(f, device());
+      kmv = m;
+      kv.reset();
+      n = m.nkey;
+    }
+  } catch (...) {
+    std::fclose(f);
+    throw;
+  }
+  rsize += std::ftell(f);
+  std::fclose(f);
+  return count(n);
 }
 
 }  // namespace mrh

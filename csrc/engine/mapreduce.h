@@ -132,6 +132,12 @@ class MapReduce {
   void spill();
   void unspill();
 
+  // checkpoint / restart of this rank's KV or KMV (binary SoA file, one per
+  // rank: `path` gets ".<rank>" appended when nprocs > 1); load returns the
+  // global pair count like every op
+  void save(const std::string& path) const;
+  uint64_t load(const std::string& path);
+
   const CommPtr& comm() const { return comm_; }
   int my_proc() const { return comm_->rank(); }
   int num_procs() const { return comm_->size(); }

@@ -319,6 +319,15 @@ class MapReduce(metaclass=_Counters):
     def unspill(self):
         self._m.unspill()
 
+    # ------------------------------------------------------------------ checkpoint / restart
+    def save(self, path):
+        """Write this rank's KV/KMV to `path` (".<rank>" appended when nprocs > 1)."""
+        self._m.save(os.fspath(path))
+
+    def load(self, path):
+        """Replace this MR's data with a checkpoint written by save(); returns the global count."""
+        return self._m.load(os.fspath(path))
+
     # ------------------------------------------------------------------ python convenience
     def kv_pairs(self):
         """Local KV pairs as a list of (key_bytes, value_bytes) (host)."""

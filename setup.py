@@ -56,7 +56,7 @@ HOSTFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-sign-comp
              "-I", os.path.join(here, "csrc"), "-I", os.path.join(ROCM, "include")] + \
             [f"-I{p}" for p in include_paths()]
 LINKLIBS = [f"-L{os.path.join(ROCM, 'lib')}", f"-L{_torch_lib()}", "-lamdhip64", "-lc10_hip", "-ltorch_hip",
-            "-lc10", "-ltorch", "-ltorch_cpu", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}",
+            "-lc10", "-ltorch", "-ltorch_cpu", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}",
             f"-Wl,-rpath,{_torch_lib()}"]
 
 

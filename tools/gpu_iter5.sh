@@ -10,6 +10,6 @@ timeout -k 10 300 python bench.py --steps 5 --warmup 2 > gpurun_out/bench_ii.log
 rc=$?; echo "bench ii rc=$rc $(date)" >> $P; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --workload pagerank --steps 3 --warmup 1 > gpurun_out/bench_pr.log 2>&1
 rc=$?; echo "bench pr rc=$rc $(date)" >> $P; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --workload wordfreq --steps 5 --warmup 2 --phases > gpurun_out/bench_wf.log 2>&1
+timeout -k 10 300 python bench.py --workload wordfreq --steps 5 --warmup 2 > gpurun_out/bench_wf.log 2>&1
 rc=$?; echo "bench wf rc=$rc $(date)" >> $P
 exit $rc
