@@ -23,9 +23,24 @@ int g_mode = 0;
 std::mutex g_world_mu;
 std::shared_ptr<mrh::Comm> g_world;
 
+// A C program exits through exit() -> atexit handlers -> DSO destructors. On
+// ROCm 7 the HIP fat-binary unregistration of libtorch_hip can then crash
+// inside the HIP runtime (hipUnregisterFatBinary after the runtime's own
+// teardown). Once the engine runs on a GPU, the C API therefore finishes the
+// process itself: flush stdio and _exit with the program's status, from an
+// on_exit handler that runs before the library destructors. Handlers the
+// program registers after its first MR_* call still run first.
+void finish_process(int status, void*) {
+  std::fflush(nullptr);
+  std::_Exit(status);
+}
+
 std::shared_ptr<mrh::Comm> world() {
   std::lock_guard<std::mutex> l(g_world_mu);
-  if (!g_world) g_world = mrh::Comm::from_env();
+  if (!g_world) {
+    g_world = mrh::Comm::from_env();
+    if (g_world->device().is_cuda()) on_exit(finish_process, nullptr);
+  }
   return g_world;
 }
 
