@@ -18,7 +18,7 @@ The reference publishes no KV/s; its end-to-end input throughput is
 0.85 GB/s aggregate on 20 GK104 GPUs (50 GB in 59.0 s), so
 `vs_baseline` compares our aggregate input GB/s with that number.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload invertedindex|pagerank|wordfreq]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload invertedindex|pagerank|wordfreq|trifind]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -112,15 +112,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="invertedindex", choices=["invertedindex", "pagerank", "wordfreq"])
+    ap.add_argument("--workload", default="invertedindex", choices=["invertedindex", "pagerank", "wordfreq", "trifind"])
     ap.add_argument("--bytes-per-gpu", type=float, default=float(1 << 30))
     ap.add_argument("--file-bytes", type=int, default=128 << 20)
     ap.add_argument("--link-gap", type=int, default=200)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--phases", type=int, default=1, help="also report a per-stage breakdown (extra run)")
-    ap.add_argument("--scale", type=int, default=26, help="pagerank: RMAT scale")
+    ap.add_argument("--scale", type=int, default=None, help="RMAT scale (pagerank 26, trifind 24)")
+    ap.add_argument("--edgefactor", type=int, default=16, help="RMAT edges per vertex")
     ap.add_argument("--iters", type=int, default=20, help="pagerank iterations per step")
     args = ap.parse_args()
+    if args.scale is None:
+        args.scale = 24 if args.workload == "trifind" else 26
 
     from gpu_mapreduce_amd.parallel import comm as pcomm
     comm = pcomm.init()
@@ -129,13 +132,16 @@ def main():
     elif args.workload == "pagerank":
         from gpu_mapreduce_amd.models.pagerank import bench_pagerank
         res = bench_pagerank(comm, args)
+    elif args.workload == "trifind":
+        from gpu_mapreduce_amd.models.triangles import bench_trifind
+        res = bench_trifind(comm, args)
     else:
         from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
         res = bench_wordfreq(comm, args)
     out = {
         "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": comm.size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": res.get("vs_baseline"),
+        "higher_is_better": True, "scaling": res.get("scaling", "weak"), "vs_baseline": res.get("vs_baseline"),
         "dtype": "bytes+int32 (no float compute in MapReduce)", "data": "synthetic", "config": res["config"],
     }
     for k, v in res.items():

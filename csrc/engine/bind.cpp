@@ -14,6 +14,7 @@
 
 #include "kv.h"
 #include "mapreduce.h"
+#include "tri.h"
 
 namespace py = pybind11;
 using namespace mrh;
@@ -397,6 +398,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_gather_reduce", &mrh::plan_gather_reduce);
   m.def("plan_combine", &mrh::plan_combine);
   m.def("wedges", &mrh::wedges);
+  m.def("tri_prepare", &mrh::tri_prepare);
+  m.def("tri_count", &mrh::tri_count);
+  m.def("tri_list", &mrh::tri_list);
   m.def("kv_iter", &kv_iter);
   m.def("kmv_iter", &kmv_iter);
   m.def("hip_compiled", []() { return true; });

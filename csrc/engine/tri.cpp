@@ -1,0 +1,124 @@
+// Triangle enumeration engine ops (kernels: csrc/kernels/tri.hip) with CPU
+// twins of identical semantics.
+#include <ATen/hip/HIPContext.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "../kernels/launch.h"
+#include "kv.h"
+#include "tri.h"
+
+namespace mrh {
+
+namespace {
+at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
+template <typename T>
+T* P0(const at::Tensor& t) {
+  return t.defined() ? reinterpret_cast<T*>(t.data_ptr()) : nullptr;
+}
+hipStream_t cur() { return at::hip::getCurrentHIPStream(); }
+
+template <bool EMIT>
+int64_t intersect_host(const int64_t* rp, const int32_t* col, uint32_t u, uint32_t v, std::vector<int64_t>* out) {
+  int64_t i = rp[u], i1 = rp[u + 1], j = rp[v], j1 = rp[v + 1], n = 0;
+  while (i < i1 && j < j1) {
+    const uint32_t x = (uint32_t)col[i], y = (uint32_t)col[j];
+    if (x < y) ++i;
+    else if (y < x) ++j;
+    else {
+      if (EMIT) {
+        out->push_back(u);
+        out->push_back(v);
+        out->push_back(x);
+      }
+      ++n;
+      ++i;
+      ++j;
+    }
+  }
+  return n;
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq_in, int64_t nvert) {
+  at::Tensor uniq = uniq_in.contiguous();
+  if (uniq.scalar_type() != at::kLong) throw std::runtime_error("tri_prepare: packed int64 edges expected");
+  if (nvert > (int64_t(1) << 32)) throw std::runtime_error("tri_prepare: vertex ids must fit in 32 bits");
+  const at::Device dev = uniq.device();
+  const int64_t m = uniq.numel();
+  at::Tensor deg = at::zeros({std::max<int64_t>(nvert, 1)}, opt(dev, at::kInt));
+  at::Tensor oriented = at::empty({m}, opt(dev, at::kLong));
+  if (uniq.is_cuda()) {
+    k::tri_degree(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), cur());
+    k::tri_orient(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), P0<uint64_t>(oriented), cur());
+  } else {
+    const uint64_t* e = P0<uint64_t>(uniq);
+    int32_t* d = P0<int32_t>(deg);
+    for (int64_t i = 0; i < m; ++i) {
+      d[e[i] >> 32]++;
+      d[(uint32_t)e[i]]++;
+    }
+    uint64_t* o = P0<uint64_t>(oriented);
+    for (int64_t i = 0; i < m; ++i) {
+      const uint32_t a = (uint32_t)(e[i] >> 32), b = (uint32_t)e[i];
+      const bool af = d[a] < d[b] || (d[a] == d[b] && a < b);
+      o[i] = af ? e[i] : ((uint64_t)b << 32 | a);
+    }
+  }
+  at::Tensor okeys;
+  if (m) {
+    auto r = radix_sort_pairs(oriented, at::arange(m, opt(dev, at::kInt)), 0, 64);
+    okeys = std::get<0>(r);
+  } else {
+    okeys = oriented;
+  }
+  at::Tensor col = at::bitwise_and(okeys, (int64_t)0xffffffff).to(at::kInt);
+  at::Tensor src = at::bitwise_right_shift(okeys, 32);
+  at::Tensor cnt = m ? at::bincount(src, {}, nvert) : at::zeros({nvert}, opt(dev, at::kLong));
+  at::Tensor rowptr = exclusive_scan(cnt.to(at::kLong).contiguous());
+  return {rowptr, col, okeys};
+}
+
+int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1) {
+  e1 = std::min<int64_t>(e1, okeys.numel());
+  if (e1 <= e0) return 0;
+  if (okeys.is_cuda()) {
+    at::Tensor tot = at::zeros({1}, opt(okeys.device(), at::kLong));
+    k::tri_count(P0<int64_t>(rowptr), P0<uint32_t>(col), P0<uint64_t>(okeys), e0, e1, nullptr,
+                 P0<unsigned long long>(tot), cur());
+    return tot.item<int64_t>();
+  }
+  const int64_t* rp = P0<int64_t>(rowptr);
+  const int32_t* c = P0<int32_t>(col);
+  const uint64_t* k = P0<uint64_t>(okeys);
+  int64_t n = 0;
+  for (int64_t e = e0; e < e1; ++e) n += intersect_host<false>(rp, c, (uint32_t)(k[e] >> 32), (uint32_t)k[e], nullptr);
+  return n;
+}
+
+at::Tensor tri_list(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1) {
+  e1 = std::min<int64_t>(e1, okeys.numel());
+  const at::Device dev = okeys.device();
+  if (e1 <= e0) return at::empty({0, 3}, opt(dev, at::kLong));
+  if (okeys.is_cuda()) {
+    at::Tensor cnt = at::empty({e1 - e0}, opt(dev, at::kInt));
+    at::Tensor tot = at::zeros({1}, opt(dev, at::kLong));
+    k::tri_count(P0<int64_t>(rowptr), P0<uint32_t>(col), P0<uint64_t>(okeys), e0, e1, P0<uint32_t>(cnt),
+                 P0<unsigned long long>(tot), cur());
+    at::Tensor off = exclusive_scan(cnt);
+    const int64_t T = off[e1 - e0].item<int64_t>();
+    at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
+    if (T) k::tri_emit(P0<int64_t>(rowptr), P0<uint32_t>(col), P0<uint64_t>(okeys), e0, e1, P0<int64_t>(off),
+                       P0<uint64_t>(out), cur());
+    return out;
+  }
+  const int64_t* rp = P0<int64_t>(rowptr);
+  const int32_t* c = P0<int32_t>(col);
+  const uint64_t* k = P0<uint64_t>(okeys);
+  std::vector<int64_t> v;
+  for (int64_t e = e0; e < e1; ++e) intersect_host<true>(rp, c, (uint32_t)(k[e] >> 32), (uint32_t)k[e], &v);
+  return at::from_blob(v.data(), {(int64_t)v.size() / 3, 3}, opt(at::kCPU, at::kLong)).clone();
+}
+
+}  // namespace mrh

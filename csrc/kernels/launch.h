@@ -145,6 +145,17 @@ void plan_combine(int dtype, const int64_t* seg, int64_t ngrp, int64_t nrecv, co
 void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
             int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);
 
+// ---------------------------------------------------------------- tri.hip
+// triangle enumeration on a degree-oriented CSR (packed u64 edges lo<<32|hi)
+void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);
+void tri_orient(const uint64_t* e, int64_t m, const uint32_t* deg, uint64_t* out, hipStream_t s);
+// per oriented edge in [e0,e1): cnt (nullable) and atomic total
+void tri_count(const int64_t* rowptr, const uint32_t* col, const uint64_t* okeys, int64_t e0, int64_t e1,
+               uint32_t* cnt, unsigned long long* total, hipStream_t s);
+// triangles (u,v,w) as 3 u64 at off[e-e0] (off: exclusive scan of cnt, n+1 entries)
+void tri_emit(const int64_t* rowptr, const uint32_t* col, const uint64_t* okeys, int64_t e0, int64_t e1,
+              const int64_t* off, uint64_t* out, hipStream_t s);
+
 // ---------------------------------------------------------------- apps.hip
 // InvertedIndex output formatting: "key\tname name ... \n" per KMV key.
 void ii_value_len(const int32_t* vals, int64_t nval, const int64_t* name_off, int32_t* lenv, hipStream_t s);

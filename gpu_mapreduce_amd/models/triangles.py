@@ -1,0 +1,139 @@
+"""Triangle finding/counting (the tri_find workload).
+
+Reference: oink/tri_find.cpp:43-82 — 4 MapReduce shuffles, O(sum d^2) wedge
+KVs. The MI355X design (csrc/kernels/tri.hip) instead:
+
+  1. packs every local edge as lo<<32|hi (self loops dropped) and, for P > 1,
+     all-gathers the packed list over RCCL (the whole deduplicated RMAT-24 x16
+     graph is ~2 GB; every GPU has 288 GB of HBM, so replication is the
+     cheap option and removes all later communication);
+  2. radix-sorts and deduplicates (the edge_upper step), computes degrees,
+     orients each edge from the lower to the higher (degree, id) endpoint and
+     builds a CSR with sorted rows;
+  3. every rank intersects N+(u) ∩ N+(v) for its slice of the oriented edges
+     (one thread per edge, merge or galloping intersection) and the counts
+     are all-reduced. Each triangle is found exactly once.
+
+The OINK command keeps the reference's MapReduce formulation available as
+`tri_find_mr`; `tri_find` uses this path.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+import torch.distributed as dist
+
+from .._ext import C
+
+SENTINEL = -1
+
+
+def pack_edges(e: torch.Tensor) -> torch.Tensor:
+    """[n,2] int64 (any orientation, duplicates ok) -> packed lo<<32|hi, self loops dropped."""
+    lo = torch.minimum(e[:, 0], e[:, 1])
+    hi = torch.maximum(e[:, 0], e[:, 1])
+    keep = lo != hi
+    return (lo[keep] << 32) | hi[keep]
+
+
+class TriangleGraph:
+    def __init__(self, comm, edges: torch.Tensor, nvert: int | None = None):
+        """edges: this rank's [n,2] int64 edges (any distribution)."""
+        self.comm = comm
+        dev = comm.device
+        p = pack_edges(edges.to(dev))
+        if comm.size > 1:
+            p = _allgather_var(comm, p)
+        n = p.numel()
+        if n:
+            s, _, _ = C.radix_sort_pairs(p, torch.arange(n, dtype=torch.int32, device=dev), 0, 64)
+            seg = C.segments_sorted(s)
+            uniq = s[seg[:-1]]
+            uniq = uniq[uniq != SENTINEL]
+        else:
+            uniq = p
+        self.nedge = uniq.numel()
+        if nvert is None:
+            mx = int(torch.maximum(uniq >> 32, uniq & 0xFFFFFFFF).max().item()) if self.nedge else -1
+            nvert = int(comm.allreduce(mx, "max")) + 1
+        self.nvert = nvert
+        if nvert >= (1 << 32):
+            raise ValueError("triangle path needs vertex ids < 2^32")
+        self.rowptr, self.col, self.okeys = C.tri_prepare(uniq.contiguous(), max(nvert, 1))
+        m = self.okeys.numel()
+        P, me = comm.size, comm.rank
+        self.e0, self.e1 = me * m // P, (me + 1) * m // P
+
+    def count(self) -> int:
+        local = C.tri_count(self.rowptr, self.col, self.okeys, self.e0, self.e1)
+        return int(self.comm.allreduce(local, "sum"))
+
+    def triangles(self) -> torch.Tensor:
+        """This rank's share of the triangles, [T,3] int64, each row sorted (a<b<c)."""
+        t = C.tri_list(self.rowptr, self.col, self.okeys, self.e0, self.e1)
+        return torch.sort(t, dim=1).values if t.numel() else t
+
+
+def _allgather_var(comm, p: torch.Tensor) -> torch.Tensor:
+    sizes = comm.allgather(float(p.numel()))
+    mx = int(max(sizes))
+    buf = torch.full((mx,), SENTINEL, dtype=torch.int64, device=p.device)
+    buf[: p.numel()] = p
+    out = torch.empty(mx * comm.size, dtype=torch.int64, device=p.device)
+    dist.all_gather_into_tensor(out, buf, group=comm.group)
+    return out
+
+
+def brute_force_count(edges) -> int:
+    """numpy oracle for small graphs: trace(A^3)/6 of the simple undirected graph."""
+    import numpy as np
+    e = np.asarray(edges)
+    lo, hi = np.minimum(e[:, 0], e[:, 1]), np.maximum(e[:, 0], e[:, 1])
+    k = lo != hi
+    u = np.unique(np.stack([lo[k], hi[k]], 1), axis=0)
+    n = int(u.max()) + 1 if len(u) else 0
+    A = np.zeros((n, n), dtype=np.int64)
+    A[u[:, 0], u[:, 1]] = 1
+    A = A + A.T
+    return int(np.trace(A @ A @ A) // 6)
+
+
+def bench_trifind(comm, args):
+    """tri_find on an R-MAT graph (BASELINE config: scale 24). One step =
+    dedup + orientation + CSR + count from the raw generated edge list (the
+    generation itself is the separate `rmat` command and is not timed)."""
+    from .pagerank import GRAPH500
+    scale, ef = args.scale, args.edgefactor
+    ntotal = (1 << scale) * ef
+    P, me = comm.size, comm.rank
+    lo, hi = me * ntotal // P, (me + 1) * ntotal // P
+    kv = C.map_rmat(hi - lo, scale, *GRAPH500, 0.0, args.seed, lo, comm.device)
+    edges = kv.kdata.view(torch.int64).view(-1, 2)
+    del kv
+
+    def sync():
+        if comm.is_cuda:
+            torch.cuda.synchronize()
+        comm.barrier()
+
+    def step():
+        g = TriangleGraph(comm, edges, 1 << scale)
+        return g, g.count()
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g, ntri = step()
+    sync()
+    dt = comm.allreduce((time.perf_counter() - t0) / args.steps, "max", dtype=torch.float64)
+    return {
+        "metric": f"KV-pairs/sec (whole node), tri_find edges processed (RMAT-2^{scale}, ef{ef})",
+        "value": ntotal / dt, "unit": "KV/s", "ms_per_step": dt * 1e3, "vs_baseline": None,
+        "baseline_note": "reference publishes no tri_find number",
+        "config": {"model": "tri_find", "global_batch": ntotal, "seq_len": 1, "parallelism": f"dp{P}",
+                   "scale": scale, "edgefactor": ef, "rmat": "graph500 a=.57 b=c=.19"},
+        "triangles": ntri, "unique_edges": g.nedge, "scaling": "strong",
+    }

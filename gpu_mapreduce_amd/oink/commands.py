@@ -491,6 +491,28 @@ def _expand_lists(src, kv):
 
 @command("tri_find")
 class TriFind(Command):
+    """tri_find -i edges -o file mr: every triangle once, as (vi, vj, vk) with
+    vi < vj < vk. Degree-oriented CSR + per-edge sorted-list intersection on
+    the GPU (models/triangles.py); same result as the reference's 4-shuffle
+    pipeline (oink/tri_find.cpp:43-82), which remains available as tri_find_mr."""
+    ninputs = noutputs = 1
+
+    def run(self):
+        from ..models.triangles import TriangleGraph
+        mre = self.obj.input(1, cb.read_edge)
+        g = TriangleGraph(self.comm, _edges_from(mre))
+        tri = g.triangles()
+        ntri = self.comm.allreduce(int(tri.shape[0]), "sum")
+        mrt = self.obj.create_mr()
+        mrt.map(self.nprocs, lambda i, kv: kv.add_tensors(tri) if tri.shape[0] else None)
+        self.obj.output(1, mrt, _print_tri)
+        self.message(f"Tri_find: {ntri} triangles")
+        self.ntri = ntri
+        self.obj.cleanup()
+
+
+@command("tri_find_mr")
+class TriFindMR(Command):
     """triangle enumeration, 4 shuffles (oink/tri_find.cpp:43-82); the O(d^2)
     wedge generation is the load-balanced k_wedges kernel"""
     ninputs = noutputs = 1
