@@ -57,6 +57,7 @@ def test_oink_tri_find_matches_mapreduce_pipeline(tmp_path, monkeypatch):
     out = io.StringIO()
     OINK(screen=out, logfile="none").file(text=(
         "rmat 9 8 0.57 0.19 0.19 0.05 0.0 11 -o NULL mre\n"
+        "edge_upper -i mre -o NULL mre\n"     # the MR pipeline needs upper-triangular input (examples/in.tri)
         "tri_find -i mre -o tmp.fast NULL\n"
         "tri_find_mr -i mre -o tmp.mr NULL\n"))
     msgs = [ln for ln in out.getvalue().splitlines() if ln.startswith("Tri_find")]
