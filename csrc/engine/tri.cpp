@@ -41,17 +41,16 @@ int64_t intersect_host(const int64_t* rp, const int32_t* col, uint32_t u, uint32
 }
 }  // namespace
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq_in, int64_t nvert) {
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq_in, int64_t nvert) {
   at::Tensor uniq = uniq_in.contiguous();
   if (uniq.scalar_type() != at::kLong) throw std::runtime_error("tri_prepare: packed int64 edges expected");
   if (nvert > (int64_t(1) << 32)) throw std::runtime_error("tri_prepare: vertex ids must fit in 32 bits");
   const at::Device dev = uniq.device();
   const int64_t m = uniq.numel();
-  at::Tensor deg = at::zeros({std::max<int64_t>(nvert, 1)}, opt(dev, at::kInt));
-  at::Tensor oriented = at::empty({m}, opt(dev, at::kLong));
+  nvert = std::max<int64_t>(nvert, 1);
+  at::Tensor deg = at::zeros({nvert}, opt(dev, at::kInt));
   if (uniq.is_cuda()) {
     k::tri_degree(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), cur());
-    k::tri_orient(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), P0<uint64_t>(oriented), cur());
   } else {
     const uint64_t* e = P0<uint64_t>(uniq);
     int32_t* d = P0<int32_t>(deg);
@@ -59,11 +58,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uni
       d[e[i] >> 32]++;
       d[(uint32_t)e[i]]++;
     }
+  }
+  // rank = position in (degree, id) order; perm[rank] = original id
+  at::Tensor ids = at::arange(nvert, opt(dev, at::kLong));
+  at::Tensor dkey = at::bitwise_or(at::bitwise_left_shift(deg.to(at::kLong), 32), ids);
+  at::Tensor perm = std::get<1>(radix_sort_pairs(dkey, ids.to(at::kInt), 0, 64)).to(at::kLong);
+  at::Tensor rank = at::empty({nvert}, opt(dev, at::kInt));
+  rank.index_put_({perm}, ids.to(at::kInt));
+  at::Tensor oriented = at::empty({m}, opt(dev, at::kLong));
+  if (uniq.is_cuda()) {
+    k::tri_orient(P0<uint64_t>(uniq), m, P0<uint32_t>(rank), P0<uint64_t>(oriented), cur());
+  } else {
+    const uint64_t* e = P0<uint64_t>(uniq);
+    const int32_t* r = P0<int32_t>(rank);
     uint64_t* o = P0<uint64_t>(oriented);
     for (int64_t i = 0; i < m; ++i) {
-      const uint32_t a = (uint32_t)(e[i] >> 32), b = (uint32_t)e[i];
-      const bool af = d[a] < d[b] || (d[a] == d[b] && a < b);
-      o[i] = af ? e[i] : ((uint64_t)b << 32 | a);
+      const uint64_t ra = (uint32_t)r[e[i] >> 32], rb = (uint32_t)r[(uint32_t)e[i]];
+      o[i] = ra < rb ? (ra << 32 | rb) : (rb << 32 | ra);
     }
   }
   at::Tensor okeys;
@@ -74,19 +85,32 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uni
     okeys = oriented;
   }
   at::Tensor col = at::bitwise_and(okeys, (int64_t)0xffffffff).to(at::kInt);
-  at::Tensor src = at::bitwise_right_shift(okeys, 32);
-  at::Tensor cnt = m ? at::bincount(src, {}, nvert) : at::zeros({nvert}, opt(dev, at::kLong));
-  at::Tensor rowptr = exclusive_scan(cnt.to(at::kLong).contiguous());
-  return {rowptr, col, okeys};
+  at::Tensor rowptr;
+  if (okeys.is_cuda()) {
+    rowptr = at::empty({nvert + 1}, opt(dev, at::kLong));
+    k::tri_rowptr(P0<uint64_t>(okeys), m, nvert, P0<int64_t>(rowptr), cur());
+  } else {
+    at::Tensor src = at::bitwise_right_shift(okeys, 32);
+    at::Tensor cnt = m ? at::bincount(src, {}, nvert) : at::zeros({nvert}, opt(dev, at::kLong));
+    rowptr = exclusive_scan(cnt.to(at::kLong).contiguous());
+  }
+  return {rowptr, col, okeys, perm};
 }
 
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1) {
   e1 = std::min<int64_t>(e1, okeys.numel());
   if (e1 <= e0) return 0;
   if (okeys.is_cuda()) {
+    // vertex-centric: this call owns the vertices whose first out-edge lies in [e0, e1)
+    const int64_t m = okeys.numel(), nvert = rowptr.numel() - 1;
+    auto src = [&](int64_t e) { return (int64_t)((uint64_t)okeys[e].item<int64_t>() >> 32); };
+    const int64_t u0 = e0 == 0 ? 0 : src(e0 - 1) + 1;
+    const int64_t u1 = e1 == m ? nvert : src(e1 - 1) + 1;
     at::Tensor tot = at::zeros({1}, opt(okeys.device(), at::kLong));
-    k::tri_count(P0<int64_t>(rowptr), P0<uint32_t>(col), P0<uint64_t>(okeys), e0, e1, nullptr,
-                 P0<unsigned long long>(tot), cur());
+    at::Tensor big = at::empty({2 * std::max<int64_t>(u1 - u0, 1)}, opt(okeys.device(), at::kInt));
+    at::Tensor nbig = at::zeros({2}, opt(okeys.device(), at::kInt));
+    k::tri_count_hash(P0<int64_t>(rowptr), P0<uint32_t>(col), u0, u1, P0<uint32_t>(big), P0<uint32_t>(nbig),
+                      P0<unsigned long long>(tot), cur());
     return tot.item<int64_t>();
   }
   const int64_t* rp = P0<int64_t>(rowptr);

@@ -148,10 +148,16 @@ void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_
 // ---------------------------------------------------------------- tri.hip
 // triangle enumeration on a degree-oriented CSR (packed u64 edges lo<<32|hi)
 void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);
-void tri_orient(const uint64_t* e, int64_t m, const uint32_t* deg, uint64_t* out, hipStream_t s);
+// packed (a,b) -> rank ids (min<<32|max) with rank = (degree, id) order
+void tri_orient(const uint64_t* e, int64_t m, const uint32_t* rank, uint64_t* out, hipStream_t s);
 // per oriented edge in [e0,e1): cnt (nullable) and atomic total
 void tri_count(const int64_t* rowptr, const uint32_t* col, const uint64_t* okeys, int64_t e0, int64_t e1,
                uint32_t* cnt, unsigned long long* total, hipStream_t s);
+// vertex-centric LDS-hash count over vertices [u0,u1); big: scratch u32[2*(u1-u0)], nbig: zeroed u32[2]
+void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int64_t u1, uint32_t* big,
+                    uint32_t* nbig, unsigned long long* total, hipStream_t s);
+// CSR row pointers of sorted oriented keys
+void tri_rowptr(const uint64_t* okeys, int64_t m, int64_t nvert, int64_t* rowptr, hipStream_t s);
 // triangles (u,v,w) as 3 u64 at off[e-e0] (off: exclusive scan of cnt, n+1 entries)
 void tri_emit(const int64_t* rowptr, const uint32_t* col, const uint64_t* okeys, int64_t e0, int64_t e1,
               const int64_t* off, uint64_t* out, hipStream_t s);

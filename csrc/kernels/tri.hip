@@ -34,14 +34,15 @@ __global__ __launch_bounds__(NT) void k_tri_degree(const uint64_t* __restrict__ 
   }
 }
 
+// rank[v] = position of v in (degree, id) order; the edge points from the
+// lower to the higher rank and is stored in rank ids, so every row holds only
+// higher ids and sorted rows can be cut at any id bound
 __global__ __launch_bounds__(NT) void k_tri_orient(const uint64_t* __restrict__ e, int64_t m,
-                                                  const uint32_t* __restrict__ deg, uint64_t* __restrict__ out) {
+                                                  const uint32_t* __restrict__ rank, uint64_t* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (int64_t)gridDim.x * NT) {
     const uint64_t x = e[i];
-    const uint32_t a = (uint32_t)(x >> 32), b = (uint32_t)x;
-    const uint32_t da = deg[a], db = deg[b];
-    const bool a_first = da < db || (da == db && a < b);
-    out[i] = a_first ? x : ((uint64_t)b << 32 | a);
+    const uint32_t ra = rank[(uint32_t)(x >> 32)], rb = rank[(uint32_t)x];
+    out[i] = ra < rb ? ((uint64_t)ra << 32 | rb) : ((uint64_t)rb << 32 | ra);
   }
 }
 
@@ -140,6 +141,191 @@ __global__ __launch_bounds__(NT) void k_tri_emit(const int64_t* __restrict__ row
   }
 }
 
+// ---------------------------------------------------------------- hash-based vertex-centric count
+// For every vertex u, the triangles found on its out-edges (u,v) are
+// |N+(u) ∩ N+(v)| summed over v ∈ N+(u). N+(u) goes into an LDS hash table
+// once; then the flattened (v, w ∈ N+(v)) pairs of all v are spread evenly
+// over the 64 lanes of the wave (a prefix sum of the out-degrees of 64 v's at
+// a time), so the work is Σ_e d+(v) coalesced reads + LDS probes instead of a
+// divergent per-edge merge of d+(u) + d+(v).
+constexpr uint32_t EMPTY = 0xffffffffu;
+constexpr int TW = 2048;          // per-wave table slots in the small kernel: d+(u) <= 1024
+constexpr int BIG_NT = 1024;      // one block per big vertex
+constexpr int BIG_TAB = 32768;    // 128 KB table: d+(u) <= 16384
+constexpr int HASH_NW = NT / MRH_WAVE;
+
+// murmur3 finaliser: R-MAT vertex ids share low-bit patterns, so the low
+// bits of a plain multiplicative hash would chain badly
+__device__ __forceinline__ uint32_t hslot(uint32_t x, uint32_t mask) {
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x & mask;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void tab_insert(uint32_t* tab, uint32_t mask, uint32_t x) {
+  uint32_t s = hslot(x, mask);
+  while (true) {
+    const uint32_t old = atomicCAS(tab + s, EMPTY, x);
+    if (old == EMPTY || old == x) return;
+    s = (s + 1) & mask;
+  }
+}
+
+__device__ __forceinline__ bool tab_has(const uint32_t* tab, uint32_t mask, uint32_t x) {
+  uint32_t s = hslot(x, mask);
+  while (true) {
+    const uint32_t y = tab[s];
+    if (y == x) return true;
+    if (y == EMPTY) return false;
+    s = (s + 1) & mask;
+  }
+}
+
+// one wave walks the v's of N+(u) in chunks of 64: returns the number of w ∈ N+(v) found in tab
+// rows hold rank ids in increasing order, so only the prefix of N+(v) up to
+// max N+(u) can match: cut each row there (binary search) before probing
+__device__ __forceinline__ uint64_t probe_chunks(const int64_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
+                                                 int64_t c0, int64_t b, int64_t cstep, const uint32_t* tab,
+                                                 uint32_t mask, uint32_t maxu, int64_t* pre, int64_t* st) {
+  const int l = dev::lane_id();
+  uint64_t cnt = 0;
+  for (int64_t c = c0; c < b; c += cstep) {
+    int64_t len = 0, vs = 0;
+    if (c + l < b) {
+      const uint32_t v = col[c + l];
+      vs = rowptr[v];
+      len = lower_bound(col, vs, rowptr[v + 1], maxu + 1u) - vs;
+    }
+    const int64_t inc = dev::wave_incl_scan(len);
+    const int64_t tot = __shfl(inc, MRH_WAVE - 1, MRH_WAVE);
+    pre[l + 1] = inc;
+    if (l == 0) pre[0] = 0;
+    st[l] = vs;
+    wave_sync();
+    // lane l takes flat items l, l+64, ...: its owning v only moves forward, so
+    // a short monotone walk replaces a binary search; two items per trip keep
+    // two independent global loads in flight
+    int j = 0;
+    for (int64_t t = l; t < tot; t += 2 * MRH_WAVE) {
+      while (pre[j + 1] <= t) ++j;
+      const uint32_t x0 = col[st[j] + (t - pre[j])];
+      const int64_t t1 = t + MRH_WAVE;
+      uint32_t x1 = EMPTY;
+      if (t1 < tot) {
+        while (pre[j + 1] <= t1) ++j;
+        x1 = col[st[j] + (t1 - pre[j])];
+      }
+      cnt += tab_has(tab, mask, x0) ? 1u : 0u;
+      if (x1 != EMPTY) cnt += tab_has(tab, mask, x1) ? 1u : 0u;
+    }
+    wave_sync();
+  }
+  return cnt;
+}
+
+// wave per vertex with a per-wave LDS table of TWN slots (d+(u) <= TWN/2);
+// larger vertices go to the next tier's list. Tier 1 walks the vertex range
+// [u0,u1) (list == null), later tiers the list filled by the previous one.
+// Small tables keep LDS per block low, so tier 1 (nearly every vertex) runs
+// at high occupancy to hide the dependent global loads.
+template <int TWN>
+__global__ __launch_bounds__(NT) void k_tri_hash_wave(const int64_t* __restrict__ rowptr,
+                                                     const uint32_t* __restrict__ col, int64_t u0, int64_t u1,
+                                                     const uint32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ nlist,
+                                                     uint32_t* __restrict__ next, uint32_t* __restrict__ nnext,
+                                                     unsigned long long* __restrict__ total) {
+  __shared__ uint32_t tab[HASH_NW][TWN];
+  __shared__ int64_t pre[HASH_NW][MRH_WAVE + 1];
+  __shared__ int64_t st[HASH_NW][MRH_WAVE];
+  const int w = dev::wave_id(), l = dev::lane_id();
+  uint64_t cnt = 0;
+  const int64_t nw = (int64_t)gridDim.x * HASH_NW;
+  const int64_t nitems = list ? (int64_t)*nlist : u1 - u0;
+  for (int64_t it = (int64_t)blockIdx.x * HASH_NW + w; it < nitems; it += nw) {
+    const int64_t u = list ? (int64_t)list[it] : u0 + it;
+    const int64_t a = rowptr[u], b = rowptr[u + 1], d = b - a;
+    if (d < 2) continue;
+    if (d > TWN / 2) {
+      if (l == 0) next[atomicAdd(nnext, 1u)] = (uint32_t)u;
+      continue;
+    }
+    uint32_t size = 64;
+    while (size < 2 * d) size <<= 1;
+    const uint32_t mask = size - 1;
+    for (uint32_t i = l; i < size; i += MRH_WAVE) tab[w][i] = EMPTY;
+    wave_sync();
+    for (int64_t i = a + l; i < b; i += MRH_WAVE) tab_insert(tab[w], mask, col[i]);
+    wave_sync();
+    cnt += probe_chunks(rowptr, col, a, b, MRH_WAVE, tab[w], mask, col[b - 1], pre[w], st[w]);
+  }
+  cnt = dev::wave_sum(cnt);
+  if (l == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
+}
+
+// one block per big vertex (d+(u) > 1024); beyond the LDS table a per-edge merge
+__global__ __launch_bounds__(BIG_NT) void k_tri_hash_big(const int64_t* __restrict__ rowptr,
+                                                        const uint32_t* __restrict__ col,
+                                                        const uint32_t* __restrict__ big,
+                                                        const uint32_t* __restrict__ nbig,
+                                                        unsigned long long* __restrict__ total) {
+  __shared__ uint32_t tab[BIG_TAB];
+  __shared__ int64_t pre[BIG_NT / MRH_WAVE][MRH_WAVE + 1];
+  __shared__ int64_t st[BIG_NT / MRH_WAVE][MRH_WAVE];
+  const int w = dev::wave_id(), l = dev::lane_id();
+  const uint32_t n = *nbig;
+  uint64_t cnt = 0;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t u = big[i];
+    const int64_t a = rowptr[u], b = rowptr[u + 1], d = b - a;
+    if (2 * d > BIG_TAB) {
+      for (int64_t e = a + threadIdx.x; e < b; e += BIG_NT) {
+        const uint32_t v = col[e];
+        cnt += intersect<false>(col, a, b, rowptr[v], rowptr[v + 1], nullptr, u, v);
+      }
+      continue;
+    }
+    uint32_t size = 64;
+    while (size < 2 * d) size <<= 1;
+    const uint32_t mask = size - 1;
+    for (uint32_t j = threadIdx.x; j < size; j += BIG_NT) tab[j] = EMPTY;
+    __syncthreads();
+    for (int64_t j = a + threadIdx.x; j < b; j += BIG_NT) tab_insert(tab, mask, col[j]);
+    __syncthreads();
+    cnt += probe_chunks(rowptr, col, a + (int64_t)w * MRH_WAVE, b, (int64_t)BIG_NT, tab, mask, col[b - 1], pre[w],
+                        st[w]);
+    __syncthreads();
+  }
+  cnt = dev::wave_sum(cnt);
+  if (l == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
+}
+
+// rowptr[v] = first index of src v in the sorted oriented keys (rowptr[nvert] = m)
+// one thread per vertex: binary search (the top ranks have no out-edges, so a
+// per-edge gap fill would leave one thread walking millions of vertices)
+__global__ __launch_bounds__(NT) void k_rowptr(const uint64_t* __restrict__ okeys, int64_t m, int64_t nvert,
+                                              int64_t* __restrict__ rowptr) {
+  for (int64_t v = (int64_t)blockIdx.x * NT + threadIdx.x; v <= nvert; v += (int64_t)gridDim.x * NT) {
+    const uint64_t key = (uint64_t)v << 32;
+    int64_t lo = 0, hi = m;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (okeys[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    rowptr[v] = lo;
+  }
+}
+
 unsigned grid_for(int64_t n) {
   int64_t b = (n + NT - 1) / NT;
   return (unsigned)(b < 1 ? 1 : (b > 65536 ? 65536 : b));
@@ -153,9 +339,9 @@ void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s) {
   MRH_CHECK_LAUNCH();
 }
 
-void tri_orient(const uint64_t* e, int64_t m, const uint32_t* deg, uint64_t* out, hipStream_t s) {
+void tri_orient(const uint64_t* e, int64_t m, const uint32_t* rank, uint64_t* out, hipStream_t s) {
   if (m <= 0) return;
-  hipLaunchKernelGGL(k_tri_orient, dim3(grid_for(m)), dim3(NT), 0, s, e, m, deg, out);
+  hipLaunchKernelGGL(k_tri_orient, dim3(grid_for(m)), dim3(NT), 0, s, e, m, rank, out);
   MRH_CHECK_LAUNCH();
 }
 
@@ -163,6 +349,30 @@ void tri_count(const int64_t* rowptr, const uint32_t* col, const uint64_t* okeys
                uint32_t* cnt, unsigned long long* total, hipStream_t s) {
   if (e1 <= e0) return;
   hipLaunchKernelGGL(k_tri_count, dim3(grid_for(e1 - e0)), dim3(NT), 0, s, rowptr, col, okeys, e0, e1, cnt, total);
+  MRH_CHECK_LAUNCH();
+}
+
+void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int64_t u1, uint32_t* big,
+                    uint32_t* nbig, unsigned long long* total, hipStream_t s) {
+  if (u1 <= u0) return;
+  // scratch: big = [mid list | big list] each u1-u0 entries; nbig = [nmid, nbig]
+  const int64_t nv = u1 - u0;
+  uint32_t* mid = big;
+  uint32_t* bigl = big + nv;
+  int64_t blocks = (nv + HASH_NW - 1) / HASH_NW;
+  if (blocks > 16384) blocks = 16384;  // waves grid-stride over the vertices
+  hipLaunchKernelGGL(k_tri_hash_wave<256>, dim3((unsigned)blocks), dim3(NT), 0, s, rowptr, col, u0, u1,
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, mid, nbig, total);
+  MRH_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_tri_hash_wave<TW>, dim3(2048), dim3(NT), 0, s, rowptr, col, u0, u1, (const uint32_t*)mid,
+                     (const uint32_t*)nbig, bigl, nbig + 1, total);
+  MRH_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_tri_hash_big, dim3(512), dim3(BIG_NT), 0, s, rowptr, col, bigl, nbig + 1, total);
+  MRH_CHECK_LAUNCH();
+}
+
+void tri_rowptr(const uint64_t* okeys, int64_t m, int64_t nvert, int64_t* rowptr, hipStream_t s) {
+  hipLaunchKernelGGL(k_rowptr, dim3(grid_for(nvert + 1)), dim3(NT), 0, s, okeys, m, nvert, rowptr);
   MRH_CHECK_LAUNCH();
 }
 

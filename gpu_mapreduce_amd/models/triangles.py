@@ -60,7 +60,7 @@ class TriangleGraph:
         self.nvert = nvert
         if nvert >= (1 << 32):
             raise ValueError("triangle path needs vertex ids < 2^32")
-        self.rowptr, self.col, self.okeys = C.tri_prepare(uniq.contiguous(), max(nvert, 1))
+        self.rowptr, self.col, self.okeys, self.perm = C.tri_prepare(uniq.contiguous(), max(nvert, 1))
         m = self.okeys.numel()
         P, me = comm.size, comm.rank
         self.e0, self.e1 = me * m // P, (me + 1) * m // P
@@ -72,7 +72,9 @@ class TriangleGraph:
     def triangles(self) -> torch.Tensor:
         """This rank's share of the triangles, [T,3] int64, each row sorted (a<b<c)."""
         t = C.tri_list(self.rowptr, self.col, self.okeys, self.e0, self.e1)
-        return torch.sort(t, dim=1).values if t.numel() else t
+        if not t.numel():
+            return t
+        return torch.sort(self.perm[t], dim=1).values
 
 
 def _allgather_var(comm, p: torch.Tensor) -> torch.Tensor:
