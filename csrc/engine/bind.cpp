@@ -13,6 +13,7 @@
 #include <string>
 
 #include "kv.h"
+#include "graphplan.h"
 #include "mapreduce.h"
 #include "tri.h"
 
@@ -398,10 +399,66 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_gather_reduce", &mrh::plan_gather_reduce);
   m.def("plan_combine", &mrh::plan_combine);
   m.def("wedges", &mrh::wedges);
+  py::class_<EdgePlan>(m, "EdgePlan")
+      .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t nvert, c10::optional<at::Tensor> w,
+                       bool symmetric) {
+             return new EdgePlan(c, e, nvert, w ? std::optional<at::Tensor>(*w) : std::nullopt, symmetric);
+           }),
+           py::arg("comm"), py::arg("edges"), py::arg("nvert"), py::arg("weights") = py::none(),
+           py::arg("symmetric") = false)
+      .def("propagate", &EdgePlan::propagate)
+      .def("count_global", &EdgePlan::count_global)
+      .def_readonly("N", &EdgePlan::N)
+      .def_readonly("nlocal", &EdgePlan::nlocal)
+      .def_readonly("nedge", &EdgePlan::nedge)
+      .def_readonly("ngrp", &EdgePlan::ngrp)
+      .def_readonly("src", &EdgePlan::src)
+      .def_readonly("w", &EdgePlan::w)
+      .def_readonly("seg", &EdgePlan::seg)
+      .def_readonly("local_ids", &EdgePlan::local_ids)
+      .def_readonly("P", &EdgePlan::P)
+      .def_readonly("me", &EdgePlan::me);
+  m.def("connected_components", [](const EdgePlan& p, int mx) { return connected_components(p, mx); },
+        py::arg("plan"), py::arg("max_iter") = 100000);
+  m.def(
+      "luby_mis",
+      [](const EdgePlan& p, int64_t seed, c10::optional<at::Tensor> act, int mx) {
+        return luby_mis(p, seed, act ? std::optional<at::Tensor>(*act) : std::nullopt, mx);
+      },
+      py::arg("plan"), py::arg("seed"), py::arg("active") = py::none(), py::arg("max_iter") = 100000);
+  m.def("sssp", [](const EdgePlan& p, int64_t s, int mx) { return sssp(p, s, mx); }, py::arg("plan"),
+        py::arg("source"), py::arg("max_iter") = 1000000);
+  py::class_<PageRankPlan>(m, "PageRankPlan")
+      .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t n, double a) {
+        return new PageRankPlan(c, e, n, a);
+      }))
+      .def("reset", &PageRankPlan::reset)
+      .def("step", &PageRankPlan::step)
+      .def("run", &PageRankPlan::run)
+      .def("delta", &PageRankPlan::delta)
+      .def("ids", &PageRankPlan::ids)
+      .def("ranks", &PageRankPlan::ranks)
+      .def_readonly("N", &PageRankPlan::N)
+      .def_readonly("nlocal", &PageRankPlan::nlocal)
+      .def_readonly("nedge", &PageRankPlan::nedge)
+      .def_readonly("ndangling", &PageRankPlan::ndangling);
+  py::class_<TriangleGraph>(m, "TriangleGraph")
+      .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t n) { return new TriangleGraph(c, e, n); }),
+           py::arg("comm"), py::arg("edges"), py::arg("nvert") = -1)
+      .def("count", &TriangleGraph::count)
+      .def("triangles", &TriangleGraph::triangles)
+      .def_readonly("nvert", &TriangleGraph::nvert)
+      .def_readonly("nedge", &TriangleGraph::nedge)
+      .def_readonly("rowptr", &TriangleGraph::rowptr)
+      .def_readonly("col", &TriangleGraph::col)
+      .def_readonly("okeys", &TriangleGraph::okeys)
+      .def_readonly("perm", &TriangleGraph::perm);
   m.def("tri_prepare", &mrh::tri_prepare);
   m.def("tri_count", &mrh::tri_count);
   m.def("tri_list", &mrh::tri_list);
   m.def("kv_iter", &kv_iter);
   m.def("kmv_iter", &kmv_iter);
   m.def("hip_compiled", []() { return true; });
+  // PCI bus id of a visible GPU ("" if none), for NUMA-local CPU/memory binding
+  m.def("gpu_pci_bus_id", &mrh::gpu_pci_bus_id);
 }

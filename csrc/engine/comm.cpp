@@ -122,6 +122,58 @@ double Comm::wtime() {
   return duration<double>(steady_clock::now().time_since_epoch()).count();
 }
 
+std::vector<int64_t> Comm::alltoall_counts(const std::vector<int64_t>& send) const {
+  if (!pg_) return send;
+  at::Tensor s = at::tensor(send, at::TensorOptions().dtype(at::kLong)).to(dev_);
+  at::Tensor r = at::empty_like(s);
+  std::vector<int64_t> eq(size_, 1);
+  pg_->alltoall_base(r, s, eq, eq)->wait();
+  r = r.to(at::kCPU);
+  return std::vector<int64_t>(r.data_ptr<int64_t>(), r.data_ptr<int64_t>() + size_);
+}
+
+at::Tensor Comm::alltoallv(const at::Tensor& in, const std::vector<int64_t>& send,
+                           const std::vector<int64_t>& recv) const {
+  if (!pg_) return in;
+  int64_t tot = 0;
+  for (auto x : recv) tot += x;
+  std::vector<int64_t> shape = in.sizes().vec();
+  shape[0] = tot;
+  at::Tensor out = at::empty(shape, in.options());
+  at::Tensor src = in.contiguous();
+  std::vector<int64_t> s = send, r = recv;
+  pg_->alltoall_base(out, src, r, s)->wait();
+  return out;
+}
+
+at::Tensor Comm::allgather_var(const at::Tensor& in) const {
+  if (!pg_) return in;
+  std::vector<double> sizes = allgather_f64((double)in.numel());
+  int64_t mx = 0, tot = 0;
+  for (double s : sizes) {
+    mx = std::max<int64_t>(mx, (int64_t)s);
+    tot += (int64_t)s;
+  }
+  at::Tensor buf = at::zeros({std::max<int64_t>(mx, 1)}, in.options());
+  if (in.numel()) buf.narrow(0, 0, in.numel()).copy_(in.reshape({-1}));
+  at::Tensor all = at::empty({buf.numel() * size_}, in.options());
+  pg_->_allgather_base(all, buf)->wait();
+  std::vector<at::Tensor> parts;
+  for (int r = 0; r < size_; ++r) parts.push_back(all.narrow(0, r * buf.numel(), (int64_t)sizes[r]));
+  return at::cat(parts);
+}
+
+void Comm::allreduce_tensor(at::Tensor& t, Op op) const {
+  if (!pg_) return;
+  allreduce_t(pg_, t, op);
+}
+
+std::string gpu_pci_bus_id(int dev) {
+  char buf[64] = {0};
+  if (hipDeviceGetPCIBusId(buf, sizeof(buf), dev) != hipSuccess) return std::string();
+  return std::string(buf);
+}
+
 int64_t Comm::next_task(const std::string& key) const {
   if (!store_) throw std::runtime_error("mrhip: mapstyle 2 needs a c10d store");
   return store_->add(key, 1) - 1;

@@ -52,6 +52,16 @@ class Comm {
   // mapstyle 2 work queue: next global task index from a store counter
   int64_t next_task(const std::string& key) const;
 
+  // device-data collectives on the engine device (RCCL over xGMI for cuda)
+  // per-peer element counts -> counts received from every peer
+  std::vector<int64_t> alltoall_counts(const std::vector<int64_t>& send) const;
+  // variable all-to-all along dim 0 (splits in rows); identity when size == 1
+  at::Tensor alltoallv(const at::Tensor& in, const std::vector<int64_t>& send, const std::vector<int64_t>& recv) const;
+  // every rank's 1-D tensor concatenated in rank order
+  at::Tensor allgather_var(const at::Tensor& in) const;
+  // in-place sum/max/min allreduce of a device tensor
+  void allreduce_tensor(at::Tensor& t, Op op) const;
+
  private:
   int rank_ = 0, size_ = 1;
   at::Device dev_;
@@ -60,5 +70,8 @@ class Comm {
 };
 
 using CommPtr = std::shared_ptr<Comm>;
+
+// PCI bus id ("0000:05:00.0") of visible GPU `dev`, "" if unavailable
+std::string gpu_pci_bus_id(int dev);
 
 }  // namespace mrh

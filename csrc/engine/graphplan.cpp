@@ -1,0 +1,305 @@
+// Native graph engines (see graphplan.h).
+#include "graphplan.h"
+
+#include <cmath>
+#include <limits>
+#include <stdexcept>
+
+#include "tri.h"
+
+namespace mrh {
+
+namespace {
+constexpr int64_t VMASK = (int64_t(1) << 40) - 1;
+at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
+
+at::Tensor iota32(int64_t n, at::Device d) { return at::arange(n, opt(d, at::kInt)); }
+
+// stable (keys, perm) sort; tolerates n == 0
+std::pair<at::Tensor, at::Tensor> sort_with_perm(const at::Tensor& key, int end_bit = 64) {
+  const int64_t n = key.numel();
+  if (n == 0) return {key, at::empty({0}, key.options().dtype(at::kInt))};
+  auto r = radix_sort_pairs(key.contiguous(), iota32(n, key.device()), 0, end_bit);
+  return {std::get<0>(r), std::get<1>(r)};
+}
+
+at::Tensor segments(const at::Tensor& sorted) {
+  if (sorted.numel() == 0) return at::zeros({1}, sorted.options().dtype(at::kLong));
+  return segments_sorted(sorted);
+}
+
+std::vector<int64_t> to_vec(const at::Tensor& t) {
+  at::Tensor c = t.to(at::kCPU).to(at::kLong).contiguous();
+  return std::vector<int64_t>(c.data_ptr<int64_t>(), c.data_ptr<int64_t>() + c.numel());
+}
+
+// route edges to the owner of their source (engine shuffle), keeping weights
+void to_source_owner(const Comm& comm, at::Tensor& e, at::Tensor& w) {
+  const int P = comm.size();
+  if (P <= 1) return;
+  const at::Device dev = e.device();
+  const int64_t n = e.size(0);
+  at::Tensor vb = w.defined() ? w.contiguous().view(at::kByte) : at::empty({0}, opt(dev, at::kByte));
+  KV kv = make_kv(e.contiguous().view(at::kByte), std::nullopt, vb, std::nullopt, n, dev);
+  at::Tensor dest = at::remainder(e.select(1, 0), P).to(at::kInt);
+  KV out = exchange(kv, dest, comm.pg());
+  e = out.kdata.view(at::kLong).view({-1, 2});
+  if (w.defined()) w = out.vdata.view(w.scalar_type());
+}
+}  // namespace
+
+// ====================================================================== EdgePlan
+
+EdgePlan::EdgePlan(CommPtr c, const at::Tensor& edges, int64_t nvert, const std::optional<at::Tensor>& weights,
+                   bool symmetric)
+    : comm(std::move(c)), P(comm->size()), me(comm->rank()), dev(comm->device()), N(nvert) {
+  nlocal = std::max<int64_t>(0, (N - me + P - 1) / P);
+  at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2});
+  at::Tensor wt = weights ? weights->to(dev) : at::Tensor();
+  if (symmetric) {
+    e = at::cat({e, e.flip(1)});
+    if (wt.defined()) wt = at::cat({wt, wt});
+  }
+  to_source_owner(*comm, e, wt);
+  nedge = e.size(0);
+  at::Tensor src_local = at::floor_divide(e.select(1, 0), P).to(at::kInt);
+  at::Tensor vj = e.select(1, 1).contiguous();
+  at::Tensor key = P > 1 ? at::bitwise_or(at::bitwise_left_shift(at::remainder(vj, P), 40), vj) : vj;
+  auto [ks, perm] = sort_with_perm(key);
+  at::Tensor pl = perm.to(at::kLong);
+  src = src_local.index_select(0, pl).contiguous();
+  if (wt.defined()) w = wt.index_select(0, pl).contiguous();
+  seg = segments(ks);
+  ngrp = seg.numel() - 1;
+  at::Tensor ujv = at::bitwise_and(ks.index_select(0, seg.narrow(0, 0, ngrp)), VMASK);
+  if (P > 1) {
+    at::Tensor scount = at::bincount(at::remainder(ujv, P), {}, P);
+    send_splits_ = to_vec(scount);
+    recv_splits_ = comm->alltoall_counts(send_splits_);
+    at::Tensor rids = comm->alltoallv(ujv.contiguous(), send_splits_, recv_splits_);
+    auto [rs, rperm] = sort_with_perm(at::floor_divide(rids, P));
+    rseg_ = segments(rs);
+    rperm_ = rperm;
+    rvid_ = rs.index_select(0, rseg_.narrow(0, 0, rseg_.numel() - 1)).to(at::kInt);
+  } else {
+    vid_ = at::floor_divide(ujv, P).to(at::kLong);
+  }
+  local_ids = at::arange(nlocal, opt(dev, at::kLong)) * P + me;
+}
+
+at::Tensor EdgePlan::propagate(const at::Tensor& x, int op, double identity, bool use_weights) const {
+  at::Tensor send = at::empty({ngrp}, x.options());
+  at::Tensor wv = (use_weights && w.defined()) ? w : at::empty({0}, x.options());
+  if (ngrp > 0) plan_gather_reduce(seg, src, x.contiguous(), wv, op, send);
+  at::Tensor acc = at::full({nlocal}, identity, x.options());
+  if (P > 1) {
+    at::Tensor recv = comm->alltoallv(send, send_splits_, recv_splits_);
+    if (recv.numel()) plan_combine(rseg_, rperm_, recv, rvid_, op, acc);
+  } else if (ngrp > 0) {
+    acc.index_put_({vid_}, send);
+  }
+  return acc;
+}
+
+int64_t EdgePlan::count_global(const at::Tensor& mask) const {
+  return comm->allreduce(mask.numel() ? mask.sum().item<int64_t>() : 0, Comm::SUM);
+}
+
+std::pair<at::Tensor, int> connected_components(const EdgePlan& plan, int max_iter) {
+  at::Tensor lab = plan.local_ids.clone();
+  const double big = (double)(int64_t(1) << 62);
+  int it = 0;
+  while (it < max_iter) {
+    ++it;
+    at::Tensor m = plan.propagate(lab, PLAN_MIN, big, false);
+    at::Tensor nw = at::minimum(lab, m);
+    const int64_t changed = plan.count_global(nw != lab);
+    lab = nw;
+    if (!changed) break;
+  }
+  return {lab, it};
+}
+
+std::pair<at::Tensor, int> luby_mis(const EdgePlan& plan, int64_t seed, const std::optional<at::Tensor>& active,
+                                    int max_iter) {
+  const at::Tensor& ids = plan.local_ids;
+  at::Tensor act = active ? active->to(plan.dev).to(at::kBool).clone() : at::ones({plan.nlocal}, opt(plan.dev, at::kBool));
+  at::Tensor mis = at::zeros({plan.nlocal}, opt(plan.dev, at::kBool));
+  int it = 0;
+  while (it < max_iter && plan.count_global(act) > 0) {
+    ++it;
+    // priority = (23 hashed bits of (vertex, seed, round), vertex id): unique per round
+    const uint64_t salt = (uint64_t)(seed + 1) * 0x632BE59BD9B4E019ull + (uint64_t)it * 0x8CB92BA72F3D8DD7ull;
+    at::Tensor h = ids * (int64_t)0x9E3779B97F4A7C15ull + (int64_t)salt;
+    h = at::bitwise_xor(h, at::bitwise_right_shift(h, 31)) * (int64_t)0x94D049BB133111EBull;
+    h = at::bitwise_xor(h, at::bitwise_right_shift(h, 29));
+    at::Tensor r = at::bitwise_or(at::bitwise_left_shift(at::bitwise_and(at::bitwise_right_shift(h, 40),
+                                                                          (int64_t)((1 << 23) - 1)),
+                                                         40),
+                                  at::bitwise_and(ids, VMASK));
+    at::Tensor pri = at::where(act, r, at::full_like(r, -1));
+    at::Tensor m = plan.propagate(pri, PLAN_MAX, -1.0, false);
+    at::Tensor join = at::logical_and(act, pri > m);
+    mis = at::logical_or(mis, join);
+    at::Tensor nb = plan.propagate(join.to(at::kLong), PLAN_MAX, 0.0, false);
+    act = at::logical_and(act, at::logical_not(at::logical_or(join, nb > 0)));
+  }
+  return {mis, it};
+}
+
+std::pair<at::Tensor, int> sssp(const EdgePlan& plan, int64_t source, int max_iter) {
+  const double inf = std::numeric_limits<double>::infinity();
+  at::Tensor d = at::full({plan.nlocal}, inf, opt(plan.dev, at::kDouble));
+  if (source % plan.P == plan.me) d.index_put_({source / plan.P}, 0.0);
+  int it = 0;
+  while (it < max_iter) {
+    ++it;
+    at::Tensor m = plan.propagate(d, PLAN_MIN, inf, true);
+    at::Tensor nw = at::minimum(d, m);
+    const int64_t changed = plan.count_global(nw != d);
+    d = nw;
+    if (!changed) break;
+  }
+  return {d, it};
+}
+
+// ====================================================================== PageRank
+
+PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, double a)
+    : comm(std::move(c)), P(comm->size()), me(comm->rank()), dev(comm->device()), N(nvert), alpha(a) {
+  nlocal = std::max<int64_t>(0, (N - me + P - 1) / P);
+  at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2});
+  at::Tensor none;
+  to_source_owner(*comm, e, none);
+  nedge = e.size(0);
+  // out-degree = group-by source (convert on u64 keys)
+  KV kv = make_kv(e.select(1, 0).contiguous().view(at::kByte), std::nullopt, e.select(1, 1).contiguous().view(at::kByte),
+                  std::nullopt, nedge, dev);
+  at::Tensor vi, deg, vj;
+  if (nedge) {
+    KMV kmv = convert(kv);
+    vi = kmv.keys.kdata.view(at::kLong);
+    deg = kmv.seg.narrow(0, 1, kmv.nkey) - kmv.seg.narrow(0, 0, kmv.nkey);
+    vj = kmv.vdata.view(at::kLong);
+  } else {
+    vi = deg = vj = at::empty({0}, opt(dev, at::kLong));
+  }
+  at::Tensor outdeg = at::zeros({nlocal}, opt(dev, at::kLong));
+  if (vi.numel()) outdeg.index_put_({at::floor_divide(vi, P)}, deg);
+  // relabel local vertices by out-degree (descending, stable): R-MAT hubs are
+  // spread over ids with few 1-bits; clustering them keeps the hot part of the
+  // gathered rank array cache-resident
+  at::Tensor dkey = (int64_t(1) << 40) - outdeg;
+  order_ = sort_with_perm(dkey, 48).second.to(at::kLong);
+  at::Tensor new_of_old = at::empty({nlocal}, opt(dev, at::kInt));
+  new_of_old.index_put_({order_}, iota32(nlocal, dev));
+  at::Tensor src_local = nedge ? at::repeat_interleave(new_of_old.index_select(0, at::floor_divide(vi, P)), deg, 0, nedge)
+                               : at::empty({0}, opt(dev, at::kInt));
+  at::Tensor key = P > 1 ? at::bitwise_or(at::bitwise_left_shift(at::remainder(vj, P), 40), vj) : vj.clone();
+  auto [ks, perm] = sort_with_perm(key);
+  src_ = src_local.index_select(0, perm.to(at::kLong)).contiguous();
+  w_ = at::empty({0}, opt(dev, at::kFloat));  // weights folded into c = r / outdeg
+  seg_ = segments(ks);
+  const int64_t ngrp = seg_.numel() - 1;
+  at::Tensor ujv = at::bitwise_and(ks.index_select(0, seg_.narrow(0, 0, ngrp)), VMASK);
+  send_ = at::empty({ngrp}, opt(dev, at::kFloat));
+  if (P > 1) {
+    send_splits_ = to_vec(at::bincount(at::remainder(ujv, P), {}, P));
+    recv_splits_ = comm->alltoall_counts(send_splits_);
+    at::Tensor rids = comm->alltoallv(ujv.contiguous(), send_splits_, recv_splits_);
+    auto [rs, rperm] = sort_with_perm(at::floor_divide(rids, P));
+    rseg_ = segments(rs);
+    rperm_ = rperm;
+    rvid_ = new_of_old.index_select(0, rs.index_select(0, rseg_.narrow(0, 0, rseg_.numel() - 1))).contiguous();
+    recv_ = at::empty({rids.numel()}, opt(dev, at::kFloat));
+  } else {
+    vid_ = new_of_old.index_select(0, at::floor_divide(ujv, P)).contiguous();
+  }
+  at::Tensor deg_new = outdeg.index_select(0, order_);
+  dangling_ = (deg_new == 0).to(at::kByte);
+  invdeg_ = at::where(deg_new > 0, 1.0 / deg_new.clamp_min(1).to(at::kDouble), at::zeros_like(deg_new, at::kDouble))
+                .to(at::kFloat);
+  ndangling = comm->allreduce(dangling_.sum().item<int64_t>(), Comm::SUM);
+  acc_ = at::empty({nlocal}, opt(dev, at::kFloat));
+  reset();
+}
+
+void PageRankPlan::reset() {
+  r_ = at::full({nlocal}, 1.0 / (double)N, opt(dev, at::kFloat));
+  rn_ = at::empty_like(r_);
+  c_ = r_ * invdeg_;
+  dmass_ = at::full({1}, (double)ndangling / (double)N, opt(dev, at::kDouble));
+  stats_ = at::zeros({2}, opt(dev, at::kDouble));
+}
+
+void PageRankPlan::step() {
+  if (send_.numel()) pr_contrib(seg_, src_, w_, c_, send_);
+  acc_.zero_();
+  if (P > 1) {
+    at::Tensor recv = comm->alltoallv(send_, send_splits_, recv_splits_);
+    if (recv.numel()) pr_combine(rseg_, rperm_, recv, rvid_, acc_);
+  } else if (send_.numel()) {
+    scatter_f32(send_, vid_, acc_);
+  }
+  const double base = (1.0 - alpha) / (double)N;
+  at::Tensor st = pr_update(acc_, r_, rn_, dangling_, base, alpha, dmass_, 1.0 / (double)N, invdeg_, c_);
+  st = st.to(dev);
+  comm->allreduce_tensor(st, Comm::SUM);
+  dmass_ = st.narrow(0, 1, 1);
+  stats_ = st;
+  std::swap(r_, rn_);
+}
+
+int PageRankPlan::run(int maxiter, double tol) {
+  int it = 0;
+  for (it = 1; it <= maxiter; ++it) {
+    step();
+    if (tol > 0 && delta() < tol) break;
+  }
+  return std::min(it, maxiter);
+}
+
+double PageRankPlan::delta() const { return stats_[0].item<double>(); }
+
+at::Tensor PageRankPlan::ids() const { return order_ * P + me; }
+
+// ====================================================================== triangles
+
+TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : comm(std::move(c)) {
+  const at::Device dev = comm->device();
+  at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2});
+  at::Tensor lo = at::minimum(e.select(1, 0), e.select(1, 1)), hi = at::maximum(e.select(1, 0), e.select(1, 1));
+  at::Tensor keep = lo != hi;
+  at::Tensor p = at::bitwise_or(at::bitwise_left_shift(lo.index({keep}), 32), hi.index({keep})).contiguous();
+  if (comm->size() > 1) p = comm->allgather_var(p);
+  at::Tensor uniq = p;
+  if (p.numel()) {
+    at::Tensor s = sort_with_perm(p).first;
+    at::Tensor sg = segments(s);
+    uniq = s.index_select(0, sg.narrow(0, 0, sg.numel() - 1)).contiguous();
+  }
+  nedge = uniq.numel();
+  if (nv < 0) {
+    const int64_t mx = nedge ? at::maximum(at::bitwise_right_shift(uniq, 32), at::bitwise_and(uniq, (int64_t)0xffffffff))
+                                   .max()
+                                   .item<int64_t>()
+                             : -1;
+    nv = comm->allreduce(mx, Comm::MAX) + 1;
+  }
+  nvert = nv;
+  if (nvert >= (int64_t(1) << 32) - 1) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^32-1");
+  std::tie(rowptr, col, okeys, perm) = tri_prepare(uniq, std::max<int64_t>(nvert, 1));
+  const int64_t m = okeys.numel(), P = comm->size(), me = comm->rank();
+  e0 = me * m / P;
+  e1 = (me + 1) * m / P;
+}
+
+int64_t TriangleGraph::count() const { return comm->allreduce(tri_count(rowptr, col, okeys, e0, e1), Comm::SUM); }
+
+at::Tensor TriangleGraph::triangles() const {
+  at::Tensor t = tri_list(rowptr, col, okeys, e0, e1);
+  if (!t.numel()) return t;
+  return std::get<0>(at::sort(perm.index_select(0, t.reshape({-1})).view({-1, 3}), 1));
+}
+
+}  // namespace mrh

@@ -1,0 +1,98 @@
+// Native graph engines on top of the MapReduce primitives: the reusable
+// "edge plan" for iterative propagation (CC, Luby MIS, SSSP), PageRank, and
+// the replicated-CSR triangle finder. Used by the OINK commands (csrc/oink)
+// and, through the bindings, by the Python models.
+//
+// Edge plan = the MapReduce dataflow of one propagation step
+//     map      edge (i -> j)  ->  (j, f(x_i, w_ij))
+//     combine  OP per j on the sender           (MR-MPI compress)
+//     shuffle  to owner(j) = j % P               (RCCL all-to-all over xGMI)
+//     reduce   OP per j on the owner
+// whose keys never change between iterations: the sort / group / routing is
+// built once, and each iteration moves only values (one fused gather +
+// segmented-reduce kernel, one all-to-all, one combine kernel). The
+// reference re-shuffles every edge 2-4 times per iteration
+// (oink/cc_find.cpp:73-92, oink/sssp.cpp:49-184, oink/luby_find.cpp:53-97).
+#pragma once
+#include <ATen/ATen.h>
+
+#include <optional>
+#include <utility>
+#include <vector>
+
+#include "comm.h"
+#include "kv.h"
+
+namespace mrh {
+
+enum PlanOp { PLAN_SUM = 0, PLAN_MIN = 1, PLAN_MAX = 2 };
+
+class EdgePlan {
+ public:
+  // edges: this rank's [n,2] int64 (vi, vj), any distribution; weights: optional
+  // per-edge values in the dtype of the propagated vectors
+  EdgePlan(CommPtr comm, const at::Tensor& edges, int64_t nvert, const std::optional<at::Tensor>& weights,
+           bool symmetric);
+  // acc[v] = OP over in-edges (i -> v) of x[i] (+ w); vertices without in-edges get `identity`
+  at::Tensor propagate(const at::Tensor& x, int op, double identity, bool use_weights) const;
+  int64_t count_global(const at::Tensor& mask) const;
+
+  CommPtr comm;
+  int P, me;
+  at::Device dev;
+  int64_t N, nlocal, nedge = 0, ngrp = 0;
+  at::Tensor src;        // int32 local source id per planned edge
+  at::Tensor w;          // planned per-edge weights (undefined if none)
+  at::Tensor seg;        // int64 [ngrp+1] groups of edges with the same destination
+  at::Tensor local_ids;  // int64 global ids of this rank's vertices (v = i*P + me)
+
+ private:
+  at::Tensor vid_, rseg_, rperm_, rvid_;
+  std::vector<int64_t> send_splits_, recv_splits_;
+};
+
+// label(v) = min vertex id of v's component; returns (labels, iterations)
+std::pair<at::Tensor, int> connected_components(const EdgePlan& plan, int max_iter = 100000);
+// Luby's maximal independent set; returns (in_set bool, rounds)
+std::pair<at::Tensor, int> luby_mis(const EdgePlan& plan, int64_t seed, const std::optional<at::Tensor>& active,
+                                    int max_iter = 100000);
+// Bellman-Ford from `source` over float64 weights; returns (dist with +inf, iterations)
+std::pair<at::Tensor, int> sssp(const EdgePlan& plan, int64_t source, int max_iter = 1000000);
+
+// PageRank on edges partitioned by source (oinkdoc/pagerank.txt; the
+// reference command is a stub, oink/pagerank.cpp:54-56)
+class PageRankPlan {
+ public:
+  PageRankPlan(CommPtr comm, const at::Tensor& edges, int64_t nvert, double alpha);
+  void reset();
+  void step();
+  int run(int maxiter, double tol);
+  double delta() const;
+  at::Tensor ids() const;  // global ids of this rank's vertices, same order as ranks()
+  at::Tensor ranks() const { return r_; }
+
+  CommPtr comm;
+  int P, me;
+  at::Device dev;
+  int64_t N, nlocal, nedge = 0, ndangling = 0;
+  double alpha;
+
+ private:
+  at::Tensor order_, src_, w_, seg_, send_, recv_, rseg_, rperm_, rvid_, vid_, dangling_, invdeg_, acc_;
+  at::Tensor r_, rn_, c_, dmass_, stats_;
+  std::vector<int64_t> send_splits_, recv_splits_;
+};
+
+// Triangle finder on the replicated degree-oriented CSR (tri.cpp kernels)
+class TriangleGraph {
+ public:
+  TriangleGraph(CommPtr comm, const at::Tensor& edges, int64_t nvert = -1);
+  int64_t count() const;          // global triangle count
+  at::Tensor triangles() const;   // this rank's triangles [T,3] int64 original ids, rows ascending
+
+  CommPtr comm;
+  int64_t nvert = 0, nedge = 0, e0 = 0, e1 = 0;
+  at::Tensor rowptr, col, okeys, perm;
+};
+
+}  // namespace mrh

@@ -22,11 +22,8 @@ from __future__ import annotations
 import time
 
 import torch
-import torch.distributed as dist
 
 from .._ext import C
-
-SENTINEL = -1
 
 
 def pack_edges(e: torch.Tensor) -> torch.Tensor:
@@ -38,53 +35,21 @@ def pack_edges(e: torch.Tensor) -> torch.Tensor:
 
 
 class TriangleGraph:
+    """Python face of the native TriangleGraph (csrc/engine/graphplan.cpp)."""
+
     def __init__(self, comm, edges: torch.Tensor, nvert: int | None = None):
         """edges: this rank's [n,2] int64 edges (any distribution)."""
         self.comm = comm
-        dev = comm.device
-        p = pack_edges(edges.to(dev))
-        if comm.size > 1:
-            p = _allgather_var(comm, p)
-        n = p.numel()
-        if n:
-            s, _, _ = C.radix_sort_pairs(p, torch.arange(n, dtype=torch.int32, device=dev), 0, 64)
-            seg = C.segments_sorted(s)
-            uniq = s[seg[:-1]]
-            uniq = uniq[uniq != SENTINEL]
-        else:
-            uniq = p
-        self.nedge = uniq.numel()
-        if nvert is None:
-            mx = int(torch.maximum(uniq >> 32, uniq & 0xFFFFFFFF).max().item()) if self.nedge else -1
-            nvert = int(comm.allreduce(mx, "max")) + 1
-        self.nvert = nvert
-        if nvert >= (1 << 32):
-            raise ValueError("triangle path needs vertex ids < 2^32")
-        self.rowptr, self.col, self.okeys, self.perm = C.tri_prepare(uniq.contiguous(), max(nvert, 1))
-        m = self.okeys.numel()
-        P, me = comm.size, comm.rank
-        self.e0, self.e1 = me * m // P, (me + 1) * m // P
+        self._g = C.TriangleGraph(comm.native, edges, -1 if nvert is None else int(nvert))
+        self.nedge, self.nvert = self._g.nedge, self._g.nvert
+        self.rowptr, self.col, self.okeys, self.perm = self._g.rowptr, self._g.col, self._g.okeys, self._g.perm
 
     def count(self) -> int:
-        local = C.tri_count(self.rowptr, self.col, self.okeys, self.e0, self.e1)
-        return int(self.comm.allreduce(local, "sum"))
+        return int(self._g.count())
 
     def triangles(self) -> torch.Tensor:
         """This rank's share of the triangles, [T,3] int64, each row sorted (a<b<c)."""
-        t = C.tri_list(self.rowptr, self.col, self.okeys, self.e0, self.e1)
-        if not t.numel():
-            return t
-        return torch.sort(self.perm[t], dim=1).values
-
-
-def _allgather_var(comm, p: torch.Tensor) -> torch.Tensor:
-    sizes = comm.allgather(float(p.numel()))
-    mx = int(max(sizes))
-    buf = torch.full((mx,), SENTINEL, dtype=torch.int64, device=p.device)
-    buf[: p.numel()] = p
-    out = torch.empty(mx * comm.size, dtype=torch.int64, device=p.device)
-    dist.all_gather_into_tensor(out, buf, group=comm.group)
-    return out
+        return self._g.triangles()
 
 
 def brute_force_count(edges) -> int:
