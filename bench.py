@@ -18,7 +18,7 @@ The reference publishes no KV/s; its end-to-end input throughput is
 0.85 GB/s aggregate on 20 GK104 GPUs (50 GB in 59.0 s), so
 `vs_baseline` compares our aggregate input GB/s with that number.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload invertedindex|pagerank|wordfreq|trifind]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload invertedindex|pagerank|wordfreq|trifind|intcount]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="invertedindex", choices=["invertedindex", "pagerank", "wordfreq", "trifind"])
+    ap.add_argument("--workload", default="invertedindex", choices=["invertedindex", "pagerank", "wordfreq", "trifind", "intcount"])
     ap.add_argument("--bytes-per-gpu", type=float, default=float(1 << 30))
     ap.add_argument("--file-bytes", type=int, default=128 << 20)
     ap.add_argument("--link-gap", type=int, default=200)
@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--phases", type=int, default=1, help="also report a per-stage breakdown (extra run)")
     ap.add_argument("--scale", type=int, default=None, help="RMAT scale (pagerank 26, trifind 24)")
     ap.add_argument("--edgefactor", type=int, default=16, help="RMAT edges per vertex")
+    ap.add_argument("--intcount-bytes", type=int, default=128 << 20, help="intcount: raw int32 bytes per GPU")
+    ap.add_argument("--key-range", type=int, default=1 << 24, help="intcount: keys uniform in [0, key_range)")
     ap.add_argument("--iters", type=int, default=20, help="pagerank iterations per step")
     args = ap.parse_args()
     if args.scale is None:
@@ -132,6 +134,9 @@ def main():
     elif args.workload == "pagerank":
         from gpu_mapreduce_amd.models.pagerank import bench_pagerank
         res = bench_pagerank(comm, args)
+    elif args.workload == "intcount":
+        from gpu_mapreduce_amd.models.intcount import bench_intcount
+        res = bench_intcount(comm, args)
     elif args.workload == "trifind":
         from gpu_mapreduce_amd.models.triangles import bench_trifind
         res = bench_trifind(comm, args)

@@ -399,6 +399,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_gather_reduce", &mrh::plan_gather_reduce);
   m.def("plan_combine", &mrh::plan_combine);
   m.def("wedges", &mrh::wedges);
+  // one-shot static-segment gather-reduce (builds the index each call; tests)
+  m.def("seg_gather_reduce", [](const at::Tensor& seg, const at::Tensor& src, const at::Tensor& x,
+                                c10::optional<at::Tensor> w, int64_t op) {
+    const int64_t ng = seg.numel() - 1;
+    at::Tensor out = at::empty({std::max<int64_t>(ng, 0)}, x.options());
+    if (ng <= 0) return out;
+    SegIndex ix = seg_index(seg, src.numel());
+    seg_gather_reduce(ix, src.contiguous(), x.contiguous(), w ? *w : at::Tensor(), op, out);
+    return out;
+  });
   py::class_<EdgePlan>(m, "EdgePlan")
       .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t nvert, c10::optional<at::Tensor> w,
                        bool symmetric) {

@@ -185,6 +185,30 @@ void plan_combine(const at::Tensor& seg, const at::Tensor& perm, const at::Tenso
   });
 }
 
+SegIndex seg_index(const at::Tensor& seg, int64_t nval) {
+  SegIndex ix;
+  need(seg.is_cuda(), "seg_index: device plans only");
+  const at::Device d = seg.device();
+  ix.nval = nval;
+  ix.H = at::empty({k::ws_words(nval)}, opt(d, at::kInt));
+  ix.wbase = at::empty({std::max<int64_t>(k::ws_waves(nval), 1)}, opt(d, at::kLong));
+  ix.scratch = at::empty({(int64_t)k::ws_scratch_bytes(nval)}, opt(d, at::kByte));
+  k::ws_index(P0<int64_t>(seg), seg.numel() - 1, nval, P0<uint32_t>(ix.H), P0<int64_t>(ix.wbase), cur());
+  return ix;
+}
+
+void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tensor& x, const at::Tensor& w, int64_t op,
+                       at::Tensor& out) {
+  const bool hw = w.defined() && w.numel() > 0;
+  need(ix.defined() && src.numel() == ix.nval && src.scalar_type() == at::kInt && src.is_contiguous(),
+       "seg_gather_reduce: src must be the plan's contiguous int32 source ids");
+  need(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0, "seg_gather_reduce: src must be 16-byte aligned");
+  need(!hw || (w.scalar_type() == x.scalar_type() && w.numel() == ix.nval), "seg_gather_reduce: weights");
+  need(out.scalar_type() == x.scalar_type() && x.is_contiguous() && out.is_contiguous(), "seg_gather_reduce: out");
+  k::ws_gather_reduce(dcode(x), P0<uint32_t>(ix.H), P0<int64_t>(ix.wbase), ix.nval, P0<int32_t>(src), x.data_ptr(),
+                      hw ? w.data_ptr() : nullptr, (int)op, out.data_ptr(), P0<void>(ix.scratch), cur());
+}
+
 // all neighbour pairs per group: returns (edges [W,2] int64 (min,max), centre [W])
 std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre) {
   const int64_t ng = seg.numel() - 1;

@@ -2,6 +2,8 @@
 #include "graphplan.h"
 
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <limits>
 #include <stdexcept>
 
@@ -48,6 +50,11 @@ void to_source_owner(const Comm& comm, at::Tensor& e, at::Tensor& w) {
 }
 }  // namespace
 
+bool use_seg_index(const at::Device& d) {
+  const char* e = std::getenv("MRH_PLAN_KERNEL");
+  return d.is_cuda() && !(e && std::strcmp(e, "tiles") == 0);
+}
+
 // ====================================================================== EdgePlan
 
 EdgePlan::EdgePlan(CommPtr c, const at::Tensor& edges, int64_t nvert, const std::optional<at::Tensor>& weights,
@@ -85,12 +92,16 @@ EdgePlan::EdgePlan(CommPtr c, const at::Tensor& edges, int64_t nvert, const std:
     vid_ = at::floor_divide(ujv, P).to(at::kLong);
   }
   local_ids = at::arange(nlocal, opt(dev, at::kLong)) * P + me;
+  if (ngrp > 0 && use_seg_index(dev)) six_ = seg_index(seg, nedge);
 }
 
 at::Tensor EdgePlan::propagate(const at::Tensor& x, int op, double identity, bool use_weights) const {
   at::Tensor send = at::empty({ngrp}, x.options());
   at::Tensor wv = (use_weights && w.defined()) ? w : at::empty({0}, x.options());
-  if (ngrp > 0) plan_gather_reduce(seg, src, x.contiguous(), wv, op, send);
+  if (ngrp > 0) {
+    if (six_.defined()) seg_gather_reduce(six_, src, x.contiguous(), wv, op, send);
+    else plan_gather_reduce(seg, src, x.contiguous(), wv, op, send);
+  }
   at::Tensor acc = at::full({nlocal}, identity, x.options());
   if (P > 1) {
     at::Tensor recv = comm->alltoallv(send, send_splits_, recv_splits_);
@@ -221,6 +232,7 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
                 .to(at::kFloat);
   ndangling = comm->allreduce(dangling_.sum().item<int64_t>(), Comm::SUM);
   acc_ = at::empty({nlocal}, opt(dev, at::kFloat));
+  if (ngrp > 0 && use_seg_index(dev)) six_ = seg_index(seg_, nedge);
   reset();
 }
 
@@ -233,7 +245,8 @@ void PageRankPlan::reset() {
 }
 
 void PageRankPlan::step() {
-  if (send_.numel()) pr_contrib(seg_, src_, w_, c_, send_);
+  if (six_.defined()) seg_gather_reduce(six_, src_, c_, at::Tensor(), 0, send_);
+  else if (send_.numel()) pr_contrib(seg_, src_, w_, c_, send_);
   acc_.zero_();
   if (P > 1) {
     at::Tensor recv = comm->alltoallv(send_, send_splits_, recv_splits_);

@@ -48,8 +48,13 @@ class EdgePlan {
 
  private:
   at::Tensor vid_, rseg_, rperm_, rvid_;
+  SegIndex six_;  // static-segment index of `seg` (device plans)
   std::vector<int64_t> send_splits_, recv_splits_;
 };
+
+// true when device plans should use the static-segment wave kernel
+// (wavesegred.h); MRH_PLAN_KERNEL=tiles selects the generic segred kernel
+bool use_seg_index(const at::Device& d);
 
 // label(v) = min vertex id of v's component; returns (labels, iterations)
 std::pair<at::Tensor, int> connected_components(const EdgePlan& plan, int max_iter = 100000);
@@ -80,6 +85,7 @@ class PageRankPlan {
  private:
   at::Tensor order_, src_, w_, seg_, send_, recv_, rseg_, rperm_, rvid_, vid_, dangling_, invdeg_, acc_;
   at::Tensor r_, rn_, c_, dmass_, stats_;
+  SegIndex six_;
   std::vector<int64_t> send_splits_, recv_splits_;
 };
 

@@ -140,6 +140,17 @@ void plan_gather_reduce(const at::Tensor& seg, const at::Tensor& src, const at::
                         int64_t op, at::Tensor& out);
 void plan_combine(const at::Tensor& seg, const at::Tensor& perm, const at::Tensor& recv, const at::Tensor& vid,
                   int64_t op, at::Tensor& acc);
+// static-segment index for plans whose segments never change (CUDA only;
+// csrc/kernels/wavesegred.h): per-iteration gather-reduce with no segment search
+struct SegIndex {
+  at::Tensor H, wbase, scratch;
+  int64_t nval = 0;
+  bool defined() const { return H.defined(); }
+};
+SegIndex seg_index(const at::Tensor& seg, int64_t nval);
+// out[s] = OP_{e in seg s} (x[src[e]] (+ w[e])), op 0 sum / 1 min / 2 max
+void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tensor& x, const at::Tensor& w, int64_t op,
+                       at::Tensor& out);
 std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre);
 // segment boundaries of a sorted int64 key column: seg[nseg+1]
 at::Tensor segments_sorted(const at::Tensor& sorted_keys);

@@ -13,6 +13,7 @@
 #include "common.h"
 #include "launch.h"
 #include "segred.h"
+#include "wavesegred.h"
 
 namespace mrh {
 namespace k {
@@ -192,6 +193,40 @@ void plan_combine(int dtype, const int64_t* seg, int64_t ngrp, int64_t nrecv, co
     default: plan_combine_t<double>(seg, ngrp, nrecv, perm, (const double*)recv, vid, op, (double*)grp, (double*)acc, scratch, s); break;
   }
 }
+int64_t ws_words(int64_t nval) { return dev::ws_head_words(nval); }
+int64_t ws_waves(int64_t nval) { return dev::ws_nwave(nval); }
+size_t ws_scratch_bytes(int64_t nval) { return (size_t)dev::ws_nwave(nval) * 2 * 16 + 64; }
+
+void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64_t* wbase, hipStream_t s) {
+  const int64_t nw = dev::ws_nwave(nval);
+  hipMemsetAsync(H, 0, sizeof(uint32_t) * dev::ws_head_words(nval), s);
+  if (nseg > 0)
+    hipLaunchKernelGGL(dev::k_ws_heads, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, seg, nseg, H);
+  if (nw > 0)
+    hipLaunchKernelGGL(dev::k_ws_base, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, seg, nseg, nw, wbase);
+  MRH_CHECK_LAUNCH();
+}
+
+template <typename T>
+static void ws_gr_t(const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src, const T* x, const T* w,
+                    int op, T* out, void* scratch, hipStream_t s) {
+  int64_t* cs = reinterpret_cast<int64_t*>(scratch);
+  T* cv = reinterpret_cast<T*>(reinterpret_cast<char*>(scratch) + (size_t)dev::ws_nwave(nval) * 2 * sizeof(int64_t));
+  if (op == 0) dev::ws_gather_reduce<T, 0>(H, wbase, nval, src, x, w, out, cs, cv, s);
+  else if (op == 1) dev::ws_gather_reduce<T, 1>(H, wbase, nval, src, x, w, out, cs, cv, s);
+  else dev::ws_gather_reduce<T, 2>(H, wbase, nval, src, x, w, out, cs, cv, s);
+}
+
+void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src,
+                      const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s) {
+  if (nval <= 0) return;
+  switch (dtype) {
+    case 1: ws_gr_t<int64_t>(H, wbase, nval, src, (const int64_t*)x, (const int64_t*)w, op, (int64_t*)out, scratch, s); break;
+    case 2: ws_gr_t<float>(H, wbase, nval, src, (const float*)x, (const float*)w, op, (float*)out, scratch, s); break;
+    default: ws_gr_t<double>(H, wbase, nval, src, (const double*)x, (const double*)w, op, (double*)out, scratch, s); break;
+  }
+}
+
 void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
             int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s) {
   if (nwedge <= 0 || ngrp <= 0) return;

@@ -141,6 +141,16 @@ void plan_gather_reduce(int dtype, const int64_t* seg, int64_t nseg, int64_t ne,
                         const void* w, int op, void* out, void* scratch, hipStream_t s);
 void plan_combine(int dtype, const int64_t* seg, int64_t ngrp, int64_t nrecv, const int32_t* perm, const void* recv,
                   const int32_t* vid, int op, void* grp, void* acc, void* scratch, hipStream_t s);
+// static-segment index (wavesegred.h) for plans whose segments never change:
+// head bitmap H (ws_words(nval) u32) + per-wave segment base (ws_waves(nval) i64)
+int64_t ws_words(int64_t nval);
+int64_t ws_waves(int64_t nval);
+void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64_t* wbase, hipStream_t s);
+// out[s] = OP_{e in seg s} x[src[e]] (+ w[e]); dtype/op as plan_gather_reduce;
+// scratch: ws_scratch_bytes(nval)
+size_t ws_scratch_bytes(int64_t nval);
+void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src,
+                      const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s);
 // tri_find wedges: all pairs of each neighbour group
 void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
             int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);

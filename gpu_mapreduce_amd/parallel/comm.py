@@ -130,12 +130,15 @@ def init(backend=None, timeout_s=600):
     GPU LOCAL_RANK, and return a Comm. World size 1 needs no env at all."""
     global _WORLD
     ws = int(os.environ.get("WORLD_SIZE", "1"))
+    # MRH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a
+    # device, LOCAL_RANK modulo the device count); production is "nccl" = RCCL
+    backend = backend or os.environ.get("MRH_DIST_BACKEND") or None
     if ws > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        if torch.cuda.is_available():
             local = int(os.environ.get("LOCAL_RANK", "0"))
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {}
         if backend == "nccl":
@@ -145,7 +148,8 @@ def init(backend=None, timeout_s=600):
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     if torch.cuda.is_available():
         bind_numa_local(torch.cuda.current_device())
-    _WORLD = Comm()
+    dev = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
+    _WORLD = Comm(device=dev)
     return _WORLD
 
 

@@ -32,8 +32,13 @@ def _worker(rank, world, port, fn_name, q):
                           WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import gpu_mapreduce_amd as g
-        comm = g.Comm(device="cpu")
-        res = globals()[fn_name](comm)
+        dev = os.environ.get("MRH_DIST_DEVICE", "cpu")
+        if dev.startswith("cuda"):
+            torch.cuda.set_device(0)  # every rank shares the box's one GPU
+        comm = g.Comm(device=dev)
+        mod, _, name = fn_name.rpartition(":")
+        fn = getattr(__import__(mod), name) if mod else globals()[name]
+        res = fn(comm)
         q.put((rank, "ok", res))
     except Exception:
         q.put((rank, "err", traceback.format_exc()))
@@ -42,7 +47,8 @@ def _worker(rank, world, port, fn_name, q):
             dist.destroy_process_group()
 
 
-def run_world(fn_name, world):
+def run_world(fn_name, world, device="cpu"):
+    os.environ["MRH_DIST_DEVICE"] = device
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -176,11 +182,11 @@ def case_pagerank(comm):
     from gpu_mapreduce_amd.models.pagerank import PageRank, rmat_map
     mr = g.MapReduce(comm)
     rmat_map(mr, 9, 8, seed=5)
-    edges = mr.kv.kdata.view(torch.int64).view(-1, 2).numpy().copy()
+    edges = mr.kv.kdata.view(torch.int64).view(-1, 2).cpu().numpy().copy()
     pr = PageRank(mr, 1 << 9).build()
     pr.run(12)
     ids, r = pr.ranks()
-    return edges, ids.numpy(), r.numpy().copy()
+    return edges, ids.cpu().numpy(), r.cpu().numpy().copy()
 
 
 @pytest.mark.parametrize("world", [2, 3])
