@@ -134,4 +134,5 @@ def bench_pagerank(comm, args):
         "l1_delta_last": pr.delta(),
         "config": {"model": "PageRank", "global_batch": nedge, "seq_len": iters,
                    "parallelism": f"dp{comm.size}", "scale": scale, "edgefactor": ef, "alpha": 0.85},
+        "scaling": "strong",
     }
