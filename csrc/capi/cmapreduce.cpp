@@ -66,6 +66,11 @@ std::vector<std::string> strs(int n, char** s) { return std::vector<std::string>
 
 }  // namespace
 
+namespace mrh {
+// the job communicator shared by the C APIs (MR_*, oink_*) and the oink executable
+std::shared_ptr<Comm> capi_world() { return world(); }
+}  // namespace mrh
+
 extern "C" {
 
 void* MR_comm_world(void) {

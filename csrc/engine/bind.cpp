@@ -16,6 +16,7 @@
 #include "graphplan.h"
 #include "mapreduce.h"
 #include "tri.h"
+#include "oink/oink.h"
 
 namespace py = pybind11;
 using namespace mrh;
@@ -468,6 +469,52 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tri_list", &mrh::tri_list);
   m.def("kv_iter", &kv_iter);
   m.def("kmv_iter", &kmv_iter);
+  // native OINK interpreter (csrc/oink)
+  py::register_exception<mrh::oink::Error>(m, "OinkError", PyExc_RuntimeError);
+  py::class_<mrh::oink::Oink>(m, "Oink")
+      .def(py::init([](std::shared_ptr<Comm> u, std::vector<std::string> parts, py::object screen,
+                       const std::string& logfile, std::vector<std::pair<std::string, std::vector<std::string>>> vars,
+                       const std::string& echo, std::shared_ptr<Comm> world) {
+             mrh::oink::Oink::Sink sink;
+             if (!screen.is_none()) {
+               std::shared_ptr<py::object> h(new py::object(screen), [](py::object* p) {
+                 py::gil_scoped_acquire g;
+                 delete p;
+               });
+               sink = [h](const std::string& s) {
+                 py::gil_scoped_acquire g;
+                 (*h)(s);
+               };
+             }
+             return new mrh::oink::Oink(u, parts, sink, logfile, vars, echo, world);
+           }),
+           py::arg("comm"), py::arg("partitions"), py::arg("screen"), py::arg("logfile"), py::arg("variables"),
+           py::arg("echo"), py::arg("world") = nullptr)
+      .def("file", &mrh::oink::Oink::file)
+      .def("text", &mrh::oink::Oink::text)
+      .def("one", &mrh::oink::Oink::one)
+      .def("close", &mrh::oink::Oink::close)
+      .def_readonly("deltatime", &mrh::oink::Oink::deltatime)
+      .def_property_readonly("nworlds", [](mrh::oink::Oink& o) { return o.universe->nworlds; })
+      .def_property_readonly("iworld", [](mrh::oink::Oink& o) { return o.universe->iworld; })
+      .def("mr_names",
+           [](mrh::oink::Oink& o) {
+             std::vector<std::string> v;
+             for (auto& e : o.obj->mrs)
+               if (e.permanent) v.push_back(e.name);
+             return v;
+           })
+      .def(
+          "mr",
+          [](mrh::oink::Oink& o, const std::string& name) -> MapReduce* {
+            int i = o.obj->find_mr(name);
+            if (i < 0) throw mrh::oink::Error("no MR object named " + name);
+            return o.obj->mrs[i].mr.get();
+          },
+          py::return_value_policy::reference_internal);
+  m.def("oink_main", [](std::shared_ptr<Comm> u, std::vector<std::string> argv) {
+    return mrh::oink::main_args(u, argv);
+  });
   m.def("hip_compiled", []() { return true; });
   // PCI bus id of a visible GPU ("" if none), for NUMA-local CPU/memory binding
   m.def("gpu_pci_bus_id", &mrh::gpu_pci_bus_id);

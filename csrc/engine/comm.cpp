@@ -6,10 +6,12 @@
 
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
+#include <torch/csrc/distributed/c10d/PrefixStore.hpp>
 #include <torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp>
 #include <torch/csrc/distributed/c10d/TCPStore.hpp>
 #include <torch/csrc/distributed/c10d/Types.hpp>
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <stdexcept>
@@ -172,6 +174,35 @@ std::string gpu_pci_bus_id(int dev) {
   char buf[64] = {0};
   if (hipDeviceGetPCIBusId(buf, sizeof(buf), dev) != hipSuccess) return std::string();
   return std::string(buf);
+}
+
+std::shared_ptr<Comm> Comm::split(int color) const {
+  if (size_ == 1) return std::make_shared<Comm>(*this);
+  static std::atomic<int> nsplit{0};
+  const int id = nsplit++;  // every rank splits in the same sequence
+  std::vector<double> colors = allgather_f64((double)color);
+  int newrank = 0, newsize = 0;
+  for (int r = 0; r < size_; ++r)
+    if (colors[r] == (double)color) {
+      if (r == rank_) newrank = newsize;
+      ++newsize;
+    }
+  if (newsize == 1) return std::make_shared<Comm>(dev_);
+  if (!store_) throw std::runtime_error("mrhip: Comm::split needs the rendezvous store");
+  auto pst = c10::make_intrusive<c10d::PrefixStore>("mrh_split_" + std::to_string(id) + "_" + std::to_string(color),
+                                                    store_);
+  auto pg = c10::make_intrusive<c10d::ProcessGroup>(pst, newrank, newsize);
+  if (dev_.is_cuda()) {
+    auto be = c10::make_intrusive<c10d::ProcessGroupNCCL>(pst, newrank, newsize,
+                                                          c10d::ProcessGroupNCCL::Options::create());
+    pg->setBackend(c10::DeviceType::CUDA, c10d::ProcessGroup::BackendType::NCCL, be);
+    pg->setDefaultBackend(c10d::ProcessGroup::BackendType::NCCL);
+  } else {
+    // host engines split through torch.distributed (the Python layer passes
+    // the sub-communicator in); gloo is not reachable from C++ here
+    throw std::runtime_error("mrhip: Comm::split of a host-engine communicator must be done by the caller");
+  }
+  return std::make_shared<Comm>(pg, dev_, pst);
 }
 
 int64_t Comm::next_task(const std::string& key) const {

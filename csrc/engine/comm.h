@@ -49,6 +49,11 @@ class Comm {
   void barrier() const;
   static double wtime();
 
+  // MPI_Comm_split analog: a new communicator over the ranks with the same
+  // color, ordered by rank (RCCL, device engines; host engines split in Python);
+  // every rank of this communicator must call it
+  std::shared_ptr<Comm> split(int color) const;
+
   // mapstyle 2 work queue: next global task index from a store counter
   int64_t next_task(const std::string& key) const;
 

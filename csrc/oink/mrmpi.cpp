@@ -1,0 +1,230 @@
+// Script-level access to every MapReduce method on a named MR object:
+// `<mrname> <method> args` (reference oink/mrmpi.cpp:36-348, callback lookups
+// :354-460). Named callbacks come from callbacks.cpp; map/mr callbacks run on
+// the whole device KV. Reference defect not reproduced: its `set` method
+// checks narg != 2 but reads arg[1], arg[2] (mrmpi.cpp:330-344); here it is
+// `<mr> set <key> <value>`.
+#include <cstdlib>
+#include <cstring>
+
+#include "callbacks.h"
+#include "oink.h"
+
+namespace mrh {
+namespace oink {
+
+namespace {
+std::string key_bytes(const std::string& type, const std::string& val) {
+  std::string k;
+  if (type == "int") {
+    int32_t x = (int32_t)std::strtol(val.c_str(), nullptr, 10);
+    k.assign((const char*)&x, 4);
+  } else if (type == "uint64") {
+    uint64_t x = std::strtoull(val.c_str(), nullptr, 10);
+    k.assign((const char*)&x, 8);
+  } else if (type == "double") {
+    double x = std::strtod(val.c_str(), nullptr);
+    k.assign((const char*)&x, 8);
+  } else if (type == "str") {
+    k = val;
+    k.push_back('\0');
+  } else {
+    throw Error("Illegal MR object collapse command");
+  }
+  return k;
+}
+int ival(const std::string& s) {
+  char* e = nullptr;
+  long v = std::strtol(s.c_str(), &e, 10);
+  if (!e || *e || s.empty()) throw Error("Illegal MR object command argument " + s);
+  return (int)v;
+}
+}  // namespace
+
+void run_mr_method(Oink& o, int index, const Args& args) {
+  Object& obj = *o.obj;
+  if (args.empty()) throw Error("Illegal MapReduce object command");
+  std::shared_ptr<MapReduce> keep = obj.mrs[index].mr;
+  MapReduce& mr = *keep;
+  const std::string& cmd = args[0];
+  const Args a(args.begin() + 1, args.end());
+  const size_t n = a.size();
+  auto need = [&](size_t lo, size_t hi) {
+    if (n < lo || n > hi) throw Error("Illegal MR object " + cmd + " command");
+  };
+  auto strings = [&](const std::string& s) -> std::vector<std::string> {
+    if (s.rfind("v_", 0) == 0) {
+      if (!o.variable->find(s.substr(2))) throw Error("MR object map command variable is unknown");
+      return o.variable->retrieve_all(s.substr(2));
+    }
+    return {s};
+  };
+  auto hash = [&](const std::string& name) -> HashFn {
+    if (name == "NULL") return nullptr;
+    auto it = hashes().find(name);
+    if (it == hashes().end()) throw Error("Unknown hash function " + name);
+    return it->second;
+  };
+
+  if (cmd == "delete") {
+    need(0, 0);
+    obj.delete_mr(index);
+  } else if (cmd == "copy") {
+    need(1, 1);
+    if (obj.find_mr(a[0]) >= 0) throw Error("MR object copy ID already in use");
+    obj.mrs.push_back({std::shared_ptr<MapReduce>(mr.copy().release()), a[0], true});
+  } else if (cmd == "add") {
+    need(1, 1);
+    const int j = obj.find_mr(a[0]);
+    if (j < 0) throw Error("MR object add ID does not exist");
+    mr.add(*obj.mrs[j].mr);
+  } else if (cmd == "aggregate") {
+    need(1, 1);
+    mr.aggregate(hash(a[0]));
+  } else if (cmd == "collate") {
+    need(1, 1);
+    mr.collate(hash(a[0]));
+  } else if (cmd == "broadcast") {
+    need(1, 1);
+    mr.broadcast(ival(a[0]));
+  } else if (cmd == "clone") {
+    need(0, 0);
+    mr.clone();
+  } else if (cmd == "close") {
+    need(0, 0);
+    mr.close();
+  } else if (cmd == "convert") {
+    need(0, 0);
+    mr.convert();
+  } else if (cmd == "open") {
+    need(0, 1);
+    mr.open(n ? ival(a[0]) : 0);
+  } else if (cmd == "collapse") {
+    need(2, 2);
+    std::string k = key_bytes(a[0], a[1]);
+    mr.collapse(&k[0], (int)k.size());
+  } else if (cmd == "compress" || cmd == "reduce") {
+    need(1, 1);
+    auto it = reduces().find(a[0]);
+    if (it == reduces().end()) throw Error("Unknown reduce function " + a[0]);
+    if (cmd == "compress") mr.compress_builtin(it->second, "");
+    else mr.reduce_builtin(it->second, "");
+  } else if (cmd == "gather") {
+    need(1, 1);
+    mr.gather(ival(a[0]));
+  } else if (cmd == "map/task") {
+    need(2, 3);
+    throw Error("Unknown map/task function " + a[1]);
+  } else if (cmd == "map/file") {
+    // map/file files self recurse readfile func [addflag]
+    need(5, 6);
+    auto it = file_parsers().find(a[4]);
+    if (it == file_parsers().end()) throw Error("Unknown map/file function " + a[4]);
+    mr.map_file(strings(a[0]), ival(a[1]), ival(a[2]), ival(a[3]), file_reader(it->second), n == 6 ? ival(a[5]) : 0);
+  } else if (cmd == "map/char" || cmd == "map/string") {
+    // map/char nmap files recurse readfile sep delta func [addflag]
+    need(7, 8);
+    auto it = file_parsers().find(a[6]);
+    if (it == file_parsers().end()) throw Error("Unknown map/string function " + a[6]);
+    const int add = n == 8 ? ival(a[7]) : 0;
+    if (cmd == "map/char")
+      mr.map_file_char(ival(a[0]), strings(a[1]), 0, ival(a[2]), ival(a[3]), a[4].empty() ? '\n' : a[4][0], ival(a[5]),
+                       chunk_reader(it->second), add);
+    else
+      mr.map_file_str(ival(a[0]), strings(a[1]), 0, ival(a[2]), ival(a[3]), a[4], ival(a[5]), chunk_reader(it->second),
+                      add);
+  } else if (cmd == "map/mr") {
+    need(2, 3);
+    const int j = obj.find_mr(a[0]);
+    if (j < 0) throw Error("MR object map/mr ID does not exist");
+    auto it = mr_maps().find(a[1]);
+    if (it == mr_maps().end()) throw Error("Unknown map/mr function " + a[1]);
+    std::shared_ptr<MapReduce> src = obj.mrs[j].mr;
+    mr.map_mr_batch(*src, it->second, n == 3 ? ival(a[2]) : 0);
+  } else if (cmd == "print") {
+    if (n == 4) mr.print(ival(a[0]), ival(a[1]), ival(a[2]), ival(a[3]));
+    else if (n == 6) mr.print(a[0].c_str(), ival(a[1]), ival(a[2]), ival(a[3]), ival(a[4]), ival(a[5]));
+    else throw Error("Illegal MR object print command");
+  } else if (cmd == "scan/kv" || cmd == "scan/kmv") {
+    need(1, 1);
+    auto it = scans().find(a[0]);
+    if (it == scans().end()) throw Error("Unknown scan function " + a[0]);
+    ScanKVFn fn = it->second;
+    if (cmd == "scan/kv") {
+      mr.scan_kv(fn);
+    } else {
+      mr.scan_kmv([fn, &mr](char* k, int kb, char* mv, int nv, int* vb) {
+        auto walk = [&](char* p, int cnt, int* sz) {
+          for (int i = 0; i < cnt; ++i) {
+            fn(k, kb, p, sz[i]);
+            p += sz[i];
+          }
+        };
+        if (mv) {
+          walk(mv, nv, vb);
+        } else {
+          int nb = 0;
+          mr.multivalue_blocks(nb);
+          for (int b = 0; b < nb; ++b) {
+            char* p;
+            int* sz;
+            int cnt = mr.multivalue_block(b, &p, &sz);
+            walk(p, cnt, sz);
+          }
+        }
+      });
+    }
+    std::fflush(stdout);
+  } else if (cmd == "scrunch") {
+    need(3, 3);
+    std::string k = key_bytes(a[1], a[2]);
+    mr.scrunch(ival(a[0]), &k[0], (int)k.size());
+  } else if (cmd == "sort_keys" || cmd == "sort_values" || cmd == "sort_multivalues") {
+    need(1, 1);
+    char* e = nullptr;
+    long flag = std::strtol(a[0].c_str(), &e, 10);
+    if (e && !*e && !a[0].empty()) {
+      if (cmd == "sort_keys") mr.sort_keys((int)flag);
+      else if (cmd == "sort_values") mr.sort_values((int)flag);
+      else mr.sort_multivalues((int)flag);
+    } else {
+      auto it = compares().find(a[0]);
+      if (it == compares().end()) throw Error("Unknown compare function " + a[0]);
+      if (cmd == "sort_keys") mr.sort_keys(it->second);
+      else if (cmd == "sort_values") mr.sort_values(it->second);
+      else mr.sort_multivalues(it->second);
+    }
+  } else if (cmd == "kv_stats") {
+    need(1, 1);
+    mr.kv_stats(ival(a[0]));
+  } else if (cmd == "kmv_stats") {
+    need(1, 1);
+    mr.kmv_stats(ival(a[0]));
+  } else if (cmd == "cummulative_stats") {
+    need(2, 2);
+    mr.cummulative_stats(ival(a[0]), ival(a[1]));
+  } else if (cmd == "set") {
+    need(2, 2);
+    const std::string &k = a[0], &v = a[1];
+    Settings& s = mr.set;
+    if (k == "fpath") s.fpath = v;
+    else if (k == "mapstyle") s.mapstyle = ival(v);
+    else if (k == "all2all") s.all2all = ival(v);
+    else if (k == "verbosity") s.verbosity = ival(v);
+    else if (k == "timer") s.timer = ival(v);
+    else if (k == "memsize") s.memsize = ival(v);
+    else if (k == "minpage") s.minpage = ival(v);
+    else if (k == "maxpage") s.maxpage = ival(v);
+    else if (k == "freepage") s.freepage = ival(v);
+    else if (k == "outofcore") s.outofcore = ival(v);
+    else if (k == "zeropage") s.zeropage = ival(v);
+    else if (k == "keyalign") s.keyalign = ival(v);
+    else if (k == "valuealign") s.valuealign = ival(v);
+    else throw Error("Illegal MR object set command");
+  } else {
+    throw Error("Illegal MR object command");
+  }
+}
+
+}  // namespace oink
+}  // namespace mrh

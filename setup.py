@@ -33,9 +33,13 @@ LIB = os.path.join(PKG, "libmrhip.so")
 hip_sources = sorted(glob.glob(os.path.join(here, "csrc", "kernels", "*.hip")))
 kernel_headers = sorted(glob.glob(os.path.join(here, "csrc", "kernels", "*.h")))
 host_sources = sorted(s for s in glob.glob(os.path.join(here, "csrc", "engine", "*.cpp"))
-                      if not s.endswith("bind.cpp")) + sorted(glob.glob(os.path.join(here, "csrc", "capi", "*.cpp")))
+                      if not s.endswith("bind.cpp")) + sorted(glob.glob(os.path.join(here, "csrc", "capi", "*.cpp"))) + \
+    sorted(s for s in glob.glob(os.path.join(here, "csrc", "oink", "*.cpp")) if not s.endswith("main.cpp"))
 host_headers = sorted(glob.glob(os.path.join(here, "csrc", "engine", "*.h")) +
-                      glob.glob(os.path.join(here, "csrc", "capi", "*.h"))) + kernel_headers
+                      glob.glob(os.path.join(here, "csrc", "capi", "*.h")) +
+                      glob.glob(os.path.join(here, "csrc", "oink", "*.h"))) + kernel_headers
+OINK_MAIN = os.path.join(here, "csrc", "oink", "main.cpp")
+OINK_BIN = os.path.join(PKG, "bin", "oink")
 
 HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
             "-Wno-unused-result", "-Wno-unused-value", "-I", os.path.join(here, "csrc")]
@@ -72,7 +76,8 @@ def _compile_all(jobs):
         o = os.path.join(BUILD, "kernels", os.path.splitext(os.path.basename(s))[0] + ".o")
         tasks.append((o, [HIPCC, *HIPFLAGS, "-c", s, "-o", o], [s] + kernel_headers))
     for s in host_sources:
-        o = os.path.join(BUILD, "host", os.path.splitext(os.path.basename(s))[0] + ".o")
+        sub = os.path.basename(os.path.dirname(s))
+        o = os.path.join(BUILD, "host", sub + "_" + os.path.splitext(os.path.basename(s))[0] + ".o")
         tasks.append((o, [CXX, *HOSTFLAGS, "-c", s, "-o", o], [s] + host_headers))
 
     def one(t):
@@ -89,6 +94,12 @@ def build_native():
     objs = _compile_all(int(os.environ.get("MAX_JOBS", "8")))
     if _stale(LIB, objs):
         cmd = [CXX, "-shared", "-o", LIB, *objs, *LINKLIBS]
+        print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    # the oink executable (reference oink/main.cpp), linked to libmrhip.so
+    if _stale(OINK_BIN, [OINK_MAIN, LIB] + host_headers):
+        os.makedirs(os.path.dirname(OINK_BIN), exist_ok=True)
+        cmd = [CXX, *HOSTFLAGS, OINK_MAIN, "-o", OINK_BIN, f"-L{PKG}", "-lmrhip", "-Wl,-rpath,$ORIGIN/..", *LINKLIBS]
         print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
     return LIB
