@@ -40,6 +40,9 @@ std::shared_ptr<mrh::Comm> world() {
   if (!g_world) {
     g_world = mrh::Comm::from_env();
     if (g_world->device().is_cuda()) on_exit(finish_process, nullptr);
+    // registered last so it runs first: rank 0 (the rendezvous server) waits
+    // for every rank to be done with the store before the process ends
+    if (g_world->size() > 1) on_exit([](int, void*) { g_world->shutdown(); }, nullptr);
   }
   return g_world;
 }

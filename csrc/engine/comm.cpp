@@ -3,6 +3,7 @@
 // path as the shuffle), gloo for the CPU engine.
 #define USE_C10D_NCCL 1
 #include "comm.h"
+#include "storepg.h"
 
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -15,6 +16,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <stdexcept>
+#include <thread>
 
 namespace mrh {
 
@@ -57,22 +59,29 @@ std::shared_ptr<Comm> Comm::from_env() {
     dev = at::Device(at::kCUDA, d);
   }
   if (ws <= 1) return std::make_shared<Comm>(dev);
-  if (!dev.is_cuda())
-    throw std::runtime_error("mrhip: WORLD_SIZE > 1 from the native API needs GPUs (RCCL); use the Python API "
-                             "with the gloo backend for multi-process CPU runs");
   const char* addr = std::getenv("MASTER_ADDR");
   c10d::TCPStoreOptions so;
   so.port = (uint16_t)env_int("MASTER_PORT", 29500);
   so.isServer = rank == 0;
   so.numWorkers = ws;
   so.timeout = std::chrono::milliseconds(600000);
-  auto store = c10::make_intrusive<c10d::TCPStore>(addr ? addr : "127.0.0.1", so);
-  auto opts = c10d::ProcessGroupNCCL::Options::create();
-  auto be = c10::make_intrusive<c10d::ProcessGroupNCCL>(store, rank, ws, opts);
-  auto pg = c10::make_intrusive<c10d::ProcessGroup>(store, rank, ws);
-  pg->setBackend(c10::DeviceType::CUDA, c10d::ProcessGroup::BackendType::NCCL, be);
-  pg->setDefaultBackend(c10d::ProcessGroup::BackendType::NCCL);
-  return std::make_shared<Comm>(pg, dev, store);
+  c10::intrusive_ptr<c10d::Store> store = c10::make_intrusive<c10d::TCPStore>(addr ? addr : "127.0.0.1", so);
+  return std::make_shared<Comm>(make_pg(store, rank, ws, dev), dev, store);
+}
+
+// RCCL for the device engine; the store transport (storepg.h) for host engines
+PG Comm::make_pg(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size, at::Device dev) {
+  auto pg = c10::make_intrusive<c10d::ProcessGroup>(store, rank, size);
+  if (dev.is_cuda()) {
+    auto be = c10::make_intrusive<c10d::ProcessGroupNCCL>(store, rank, size, c10d::ProcessGroupNCCL::Options::create());
+    pg->setBackend(c10::DeviceType::CUDA, c10d::ProcessGroup::BackendType::NCCL, be);
+    pg->setDefaultBackend(c10d::ProcessGroup::BackendType::NCCL);
+  } else {
+    auto be = c10::make_intrusive<StoreBackend>(store, rank, size);
+    pg->setBackend(c10::DeviceType::CPU, c10d::ProcessGroup::BackendType::CUSTOM, be);
+    pg->setDefaultBackend(c10d::ProcessGroup::BackendType::CUSTOM);
+  }
+  return pg;
 }
 
 std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
@@ -191,18 +200,20 @@ std::shared_ptr<Comm> Comm::split(int color) const {
   if (!store_) throw std::runtime_error("mrhip: Comm::split needs the rendezvous store");
   auto pst = c10::make_intrusive<c10d::PrefixStore>("mrh_split_" + std::to_string(id) + "_" + std::to_string(color),
                                                     store_);
-  auto pg = c10::make_intrusive<c10d::ProcessGroup>(pst, newrank, newsize);
-  if (dev_.is_cuda()) {
-    auto be = c10::make_intrusive<c10d::ProcessGroupNCCL>(pst, newrank, newsize,
-                                                          c10d::ProcessGroupNCCL::Options::create());
-    pg->setBackend(c10::DeviceType::CUDA, c10d::ProcessGroup::BackendType::NCCL, be);
-    pg->setDefaultBackend(c10d::ProcessGroup::BackendType::NCCL);
-  } else {
-    // host engines split through torch.distributed (the Python layer passes
-    // the sub-communicator in); gloo is not reachable from C++ here
-    throw std::runtime_error("mrhip: Comm::split of a host-engine communicator must be done by the caller");
+  return std::make_shared<Comm>(make_pg(pst, newrank, newsize, dev_), dev_, pst);
+}
+
+void Comm::shutdown() const {
+  if (!store_ || size_ == 1) return;
+  try {
+    store_->add("mrh_shutdown", 1);
+    if (rank_ != 0) return;
+    const double t0 = wtime();
+    while (store_->add("mrh_shutdown", 0) < size_ && wtime() - t0 < 60.0)
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  } catch (const std::exception&) {
+    // a peer already tore the store down: nothing left to wait for
   }
-  return std::make_shared<Comm>(pg, dev_, pst);
 }
 
 int64_t Comm::next_task(const std::string& key) const {

@@ -29,8 +29,11 @@ class Comm {
   // Bootstrap from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK,
   // MASTER_ADDR, MASTER_PORT) without Python: binds the process to GPU
   // LOCAL_RANK when GPUs are visible, and for WORLD_SIZE > 1 creates a
-  // TCPStore rendezvous and an RCCL process group (device engine only).
+  // TCPStore rendezvous and an RCCL process group (device engine) or the
+  // store transport of storepg.h (host engine, e.g. CPU-only CI).
   static std::shared_ptr<Comm> from_env();
+  // process group over `store`: RCCL for a cuda device, StoreBackend for cpu
+  static PG make_pg(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size, at::Device dev);
 
   int rank() const { return rank_; }
   int size() const { return size_; }
@@ -50,9 +53,14 @@ class Comm {
   static double wtime();
 
   // MPI_Comm_split analog: a new communicator over the ranks with the same
-  // color, ordered by rank (RCCL, device engines; host engines split in Python);
+  // color, ordered by rank (RCCL for device engines, the store transport for host ones);
   // every rank of this communicator must call it
   std::shared_ptr<Comm> split(int color) const;
+
+  // end-of-job handshake: every rank checks in; rank 0, which serves the
+  // rendezvous store, returns only when all ranks have (or after 60 s), so no
+  // rank's last store operation races the server's exit
+  void shutdown() const;
 
   // mapstyle 2 work queue: next global task index from a store counter
   int64_t next_task(const std::string& key) const;

@@ -125,7 +125,7 @@ int main(int argc, char **argv) {
   MR_gather(rows, 1);
   MR_sort_keys_flag(rows, 1);
   MR_convert(rows); /* groups equal counts; fixed-width keys come out in key order */
-  if (me == 0) MR_scan_kmv(rows, print_histo, NULL);
+  MR_scan_kmv(rows, print_histo, NULL); /* collective; only rank 0 has pairs */
   MR_destroy(rows);
   MR_destroy(mr);
   return 0;

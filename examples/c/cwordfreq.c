@@ -91,7 +91,9 @@ int main(int argc, char **argv) {
   MR_gather(top, 1);
   MR_sort_values_flag(top, -1);
   int left = ntop;
-  if (me == 0) MR_scan_kv(top, print_top, &left);
+  /* scan returns the global pair count (a collective): every rank calls it;
+     after gather(1) only rank 0 holds pairs */
+  MR_scan_kv(top, print_top, &left);
   if (me == 0) printf("%llu total words, %llu unique words\n", (unsigned long long)nwords, (unsigned long long)nunique);
   MR_destroy(top);
   MR_destroy(mr);
