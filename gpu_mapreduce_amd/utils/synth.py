@@ -140,3 +140,45 @@ def pad_text(t: torch.Tensor, pad=64) -> torch.Tensor:
     out = torch.zeros(t.numel() + pad, dtype=torch.uint8, device=t.device)
     out[: t.numel()] = t
     return out
+
+
+def _main(argv=None):
+    """Write synthetic input files for the native apps (csrc/apps):
+        python -m gpu_mapreduce_amd.utils.synth html  DIR NFILES FILE_BYTES   # part-%05d HTML files
+        python -m gpu_mapreduce_amd.utils.synth text  DIR NFILES FILE_BYTES   # Zipf word text files
+        python -m gpu_mapreduce_amd.utils.synth ints  FILE NBYTES KEY_RANGE   # raw int32 file (IntCount)
+    """
+    import argparse
+    import os
+
+    ap = argparse.ArgumentParser(prog="python -m gpu_mapreduce_amd.utils.synth")
+    ap.add_argument("kind", choices=["html", "text", "ints"])
+    ap.add_argument("path")
+    ap.add_argument("a", type=int)
+    ap.add_argument("b", type=int)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--nurl", type=int, default=1 << 16)
+    ap.add_argument("--device", default="cpu", help="generate on this torch device (e.g. cuda) and write from host")
+    args = ap.parse_args(argv)
+    dev = args.device
+    if args.kind == "ints":
+        g = _gen(args.seed, "cpu")
+        v = torch.randint(0, args.b, (args.a // 4,), generator=g, dtype=torch.int32)
+        with open(args.path, "wb") as f:
+            f.write(v.numpy().tobytes())
+        return
+    os.makedirs(args.path, exist_ok=True)
+    vocab = url_vocab(args.nurl, device=dev) if args.kind == "html" else None
+    for i in range(args.a):
+        if args.kind == "html":
+            t = html_file(args.b, args.seed * 1000003 + i, device=dev, vocab=vocab)
+            name = f"part-{i:05d}"
+        else:
+            t = zipf_text(args.b, seed=args.seed * 1000003 + i, device=dev)
+            name = f"text-{i:05d}.txt"
+        with open(os.path.join(args.path, name), "wb") as f:
+            f.write(t.cpu().numpy().tobytes())
+
+
+if __name__ == "__main__":
+    _main()

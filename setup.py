@@ -40,6 +40,9 @@ host_headers = sorted(glob.glob(os.path.join(here, "csrc", "engine", "*.h")) +
                       glob.glob(os.path.join(here, "csrc", "oink", "*.h"))) + kernel_headers
 OINK_MAIN = os.path.join(here, "csrc", "oink", "main.cpp")
 OINK_BIN = os.path.join(PKG, "bin", "oink")
+# native app programs (csrc/apps/*.cpp -> gpu_mapreduce_amd/bin/<name>)
+APP_SOURCES = sorted(glob.glob(os.path.join(here, "csrc", "apps", "*.cpp")))
+APP_HEADERS = sorted(glob.glob(os.path.join(here, "csrc", "apps", "*.h")))
 
 HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
             "-Wno-unused-result", "-Wno-unused-value", "-I", os.path.join(here, "csrc")]
@@ -102,6 +105,15 @@ def build_native():
         cmd = [CXX, *HOSTFLAGS, OINK_MAIN, "-o", OINK_BIN, f"-L{PKG}", "-lmrhip", "-Wl,-rpath,$ORIGIN/..", *LINKLIBS]
         print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+    def app(src):
+        exe = os.path.join(PKG, "bin", os.path.splitext(os.path.basename(src))[0])
+        if _stale(exe, [src, LIB] + host_headers + APP_HEADERS):
+            cmd = [CXX, *HOSTFLAGS, src, "-o", exe, f"-L{PKG}", "-lmrhip", "-Wl,-rpath,$ORIGIN/..", *LINKLIBS]
+            print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+    os.makedirs(os.path.join(PKG, "bin"), exist_ok=True)
+    with ThreadPoolExecutor(max_workers=max(1, int(os.environ.get("MAX_JOBS", "8")))) as ex:
+        list(ex.map(app, APP_SOURCES))
     return LIB
 
 

@@ -157,3 +157,102 @@ def test_oink_scripts_native_gpu(tmp_path, script):
     if script == "in.pagerank":
         keys = ("RMAT",)
     assert _lines(cpu, *keys) == _lines(gpu, *keys) != []
+
+
+# ---------------------------------------------------------------- native apps (csrc/apps)
+BIN = os.path.join(PKG, "bin")
+
+
+def _synth(*args):
+    env = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES="")
+    subprocess.run(["python", "-m", "gpu_mapreduce_amd.utils.synth", *map(str, args)], check=True, env=env,
+                   timeout=240)
+
+
+def _ii_oracle(d, nfile):
+    import re
+    idx = {}
+    for i in range(nfile):
+        name = f"part-{i:05d}"
+        b = (d / name).read_bytes()
+        for m in re.finditer(rb'<a href="', b):
+            e = b.find(b'"', m.end())
+            idx.setdefault(b[m.end():e if e >= 0 else len(b)], []).append(name)
+    return {k: sorted(v) for k, v in idx.items()}
+
+
+def _ii_output(outdir):
+    got = {}
+    for f in sorted(os.listdir(outdir)):
+        for ln in (outdir / f).read_bytes().splitlines():
+            url, rest = ln.split(b"\t")
+            assert url not in got, "a URL must be reduced on exactly one rank"
+            got[url] = sorted(x.decode() for x in rest.split())
+    return got
+
+
+def _run_invertedindex(tmp_path, n, gpu):
+    d = tmp_path / "html"
+    _synth("html", d, 5, 60000, "--nurl", 500)
+    out = tmp_path / f"out{n}"
+    out.mkdir()
+    log = launch([os.path.join(BIN, "invertedindex"), str(d), "5", str(out)], n, tmp_path, gpu=gpu)
+    ref = _ii_oracle(d, 5)
+    assert _ii_output(out) == ref
+    assert f"{sum(len(v) for v in ref.values())} URL KVs, {len(ref)} unique URLs" in log
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_invertedindex_app(tmp_path, n):
+    _run_invertedindex(tmp_path, n, gpu=False)
+
+
+def test_intcount_app(tmp_path):
+    import numpy as np
+    _synth("ints", tmp_path / "ints.bin", 80000, 3000)
+    v = np.fromfile(tmp_path / "ints.bin", dtype=np.int32)
+    one = launch([os.path.join(BIN, "intcount"), "ints.bin"], 1, tmp_path)
+    two = launch([os.path.join(BIN, "intcount"), "ints.bin"], 2, tmp_path)
+    assert f"IntCount: {v.size} ints, {np.unique(v).size} unique" in one
+    assert f"IntCount: {2 * v.size} ints, {np.unique(v).size} unique" in two   # every rank maps the file
+    assert f"Counts sum: {2 * v.size}" in two
+
+
+def test_wordfreq_app(tmp_path):
+    cnt = _docs(tmp_path / "docs")
+    one = launch([os.path.join(BIN, "wordfreq"), "-n", "3", "docs"], 1, tmp_path)
+    two = launch([os.path.join(BIN, "wordfreq"), "-n", "3", "docs"], 2, tmp_path)
+    top = [ln for ln in one.splitlines()[:3]]
+    assert [int(x.split()[0]) for x in top] == sorted(cnt.values(), reverse=True)[:3]
+    assert two.splitlines()[:4] == one.splitlines()[:4]
+    assert f"{sum(cnt.values())} total words, {len(cnt)} unique words" in two
+    assert "Time to process 5 files on 2 procs" in two
+
+
+def test_rmat_app(tmp_path):
+    args = [os.path.join(BIN, "rmat"), "10", "4", "0.57", "0.19", "0.19", "0.05", "0.1", "3", "m.mtx"]
+    one = launch(args, 1, tmp_path)
+    two = launch(args, 2, tmp_path)
+    assert one.splitlines()[:2] == ["1024 rows in matrix", "4096 nonzeroes in matrix"]
+    histo = lambda o: [ln for ln in o.splitlines() if "rows with" in ln]
+    assert sum(int(h.split()[0]) * int(h.split()[3]) for h in histo(one)) == 4096
+    # the generator is counter-based: the matrix does not depend on the rank count
+    assert histo(one) == histo(two)
+    lines = (tmp_path / "m.mtx").read_text().splitlines()
+    assert lines[1] == "1024 1024 4096" and len(lines) == 2 + 4096
+
+
+@pytest.mark.gpu
+def test_native_apps_gpu(tmp_path):
+    _run_invertedindex(tmp_path, 1, gpu=True)
+    _synth("ints", tmp_path / "ints.bin", 80000, 3000)
+    out = launch([os.path.join(BIN, "intcount"), "ints.bin"], 1, tmp_path, gpu=True)
+    assert "Counts sum: 20000" in out and "(gpu)" in out
+    cnt = _docs(tmp_path / "docs")
+    out = launch([os.path.join(BIN, "wordfreq"), "-n", "3", "docs"], 1, tmp_path, gpu=True)
+    assert f"{sum(cnt.values())} total words, {len(cnt)} unique words" in out
+    cpu = launch([os.path.join(BIN, "rmat"), "10", "4", "0.57", "0.19", "0.19", "0.05", "0.1", "3"], 1, tmp_path)
+    gpu = launch([os.path.join(BIN, "rmat"), "10", "4", "0.57", "0.19", "0.19", "0.05", "0.1", "3"], 1, tmp_path,
+                 gpu=True)
+    histo = lambda o: [ln for ln in o.splitlines() if "rows with" in ln]
+    assert histo(cpu) == histo(gpu) != []
