@@ -3,6 +3,7 @@
 // path as the shuffle), gloo for the CPU engine.
 #define USE_C10D_NCCL 1
 #include "comm.h"
+#include "guard.h"
 #include "storepg.h"
 
 #include <ATen/hip/HIPContext.h>
@@ -64,7 +65,7 @@ std::shared_ptr<Comm> Comm::from_env() {
   so.port = (uint16_t)env_int("MASTER_PORT", 29500);
   so.isServer = rank == 0;
   so.numWorkers = ws;
-  so.timeout = std::chrono::milliseconds(600000);
+  so.timeout = std::chrono::milliseconds(1000LL * guard::comm_timeout_seconds());
   c10::intrusive_ptr<c10d::Store> store = c10::make_intrusive<c10d::TCPStore>(addr ? addr : "127.0.0.1", so);
   return std::make_shared<Comm>(make_pg(store, rank, ws, dev), dev, store);
 }
@@ -73,7 +74,9 @@ std::shared_ptr<Comm> Comm::from_env() {
 PG Comm::make_pg(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size, at::Device dev) {
   auto pg = c10::make_intrusive<c10d::ProcessGroup>(store, rank, size);
   if (dev.is_cuda()) {
-    auto be = c10::make_intrusive<c10d::ProcessGroupNCCL>(store, rank, size, c10d::ProcessGroupNCCL::Options::create());
+    auto opts = c10d::ProcessGroupNCCL::Options::create();
+    opts->timeout = std::chrono::milliseconds(1000LL * guard::comm_timeout_seconds());  // watchdog bound
+    auto be = c10::make_intrusive<c10d::ProcessGroupNCCL>(store, rank, size, opts);
     pg->setBackend(c10::DeviceType::CUDA, c10d::ProcessGroup::BackendType::NCCL, be);
     pg->setDefaultBackend(c10d::ProcessGroup::BackendType::NCCL);
   } else {

@@ -1,6 +1,7 @@
 // Native MapReduce object (see mapreduce.h). Reference behaviour cited per
 // method as src/mapreduce.cpp:<lines>.
 #include "mapreduce.h"
+#include "guard.h"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
@@ -185,9 +186,20 @@ MapReduce::MapReduce(CommPtr comm) : comm_(std::move(comm)) {
   if (const char* p = std::getenv("MRMPI_FPATH")) set.fpath = p;
   instances_now++;
   instance_me_ = ++instances_ever;
+  guard::register_mr(this);
 }
 
-MapReduce::~MapReduce() { instances_now--; }
+MapReduce::~MapReduce() {
+  guard::unregister_mr(this);
+  instances_now--;
+}
+
+// every op's entry: fault injection point, and data spilled to host (spill()
+// or spill-on-OOM) comes back to HBM before the op touches it
+void MapReduce::enter(const char* op) {
+  guard::fault_point(op, comm_->rank());
+  if (device().is_cuda() && ((kv && !kv->device().is_cuda()) || (kmv && !kmv->keys.device().is_cuda()))) unspill();
+}
 
 std::unique_ptr<MapReduce> MapReduce::copy() const {
   auto mr = std::make_unique<MapReduce>(comm_);
@@ -238,6 +250,10 @@ void MapReduce::histo(double v, const char* heading) const {
 
 // per-op stats (reference :3112-3179)
 void MapReduce::stats(const char* heading, int which) {
+  if (guard::check_enabled()) {
+    if (kv) guard::check_kv(*kv, heading);
+    if (kmv) guard::check_kmv(*kmv, heading);
+  }
   int64_t b = 0;
   if (kv) b += kv->nbytes();
   if (kmv) b += kmv->nbytes();
@@ -281,6 +297,7 @@ void MapReduce::note_shuffle(const ShuffleStats& st) {
 uint64_t MapReduce::add(MapReduce& other) {  // :348-374
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("add");
   if (!other.kv) fail("MapReduce passed to add() does not have KeyValue pairs");
   kv = concat({*kv, *other.kv}, device());
@@ -343,6 +360,7 @@ uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) 
 uint64_t MapReduce::map(int nmap, const MapTaskFn& fn, int addflag) {  // :1044-1051
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   KeyValue kvb(device());
   for (int t : my_tasks(nmap)) fn(t, kvb);
   return finish_map(kvb, addflag);
@@ -377,6 +395,7 @@ uint64_t MapReduce::map_file(const std::vector<std::string>& files, int selfflag
                              const MapFileFn& fn, int addflag) {  // :1060-1092
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
   KeyValue kvb(device());
@@ -407,6 +426,7 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
                                int addflag) {
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
   const int nfile = (int)fl.size();
@@ -483,6 +503,7 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
 uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  // :1560-1642
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   HostCol k = host_col(s.kdata, s.koff, s.kw), v = host_col(s.vdata, s.voff, s.vw);
@@ -501,6 +522,7 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
 uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addflag) {
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   KeyValue kvb(device());
@@ -520,11 +542,12 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
 uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("aggregate");
   if (comm_->size() > 1) {
     ShuffleStats st;
     if (!hash) {
-      kv = mrh::aggregate(*kv, comm_->pg(), &st);
+      kv = oom_retry(this, device(), my_proc(), "aggregate", [&] { return mrh::aggregate(*kv, comm_->pg(), &st); });
     } else {
       HostCol k = host_col(kv->kdata, kv->koff, kv->kw);
       at::Tensor d = at::empty({kv->n}, at::TensorOptions().dtype(at::kInt));
@@ -545,6 +568,7 @@ uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
 uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("aggregate");
   if (comm_->size() > 1) {
     ShuffleStats st;
@@ -558,6 +582,7 @@ uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
 uint64_t MapReduce::broadcast(int root) {  // :569-623
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("broadcast");
   if (comm_->size() > 1) kv = mrh::broadcast(*kv, root, comm_->pg());
   stats("Broadcast", 0);
@@ -567,6 +592,7 @@ uint64_t MapReduce::broadcast(int root) {  // :569-623
 uint64_t MapReduce::gather(int nprocs) {  // :893-1036
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("gather");
   if (nprocs < 1 || nprocs > comm_->size()) fail("Invalid proc count for gather");
   if (comm_->size() > 1 && nprocs < comm_->size()) {
@@ -583,8 +609,9 @@ uint64_t MapReduce::gather(int nprocs) {  // :893-1036
 uint64_t MapReduce::convert() {  // :861-886
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("convert");
-  kmv = mrh::convert(*kv, &last_convert);
+  kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert); });
   kv.reset();
   stats("Convert", 1);
   return count(kmv->nkey);
@@ -593,6 +620,7 @@ uint64_t MapReduce::convert() {  // :861-886
 uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("collate");
   const int v = set.verbosity, t = set.timer;
   set.verbosity = set.timer = 0;
@@ -607,8 +635,9 @@ uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
 uint64_t MapReduce::clone() {  // :631-652
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("clone");
-  kmv = mrh::clone(*kv);
+  kmv = oom_retry(this, device(), my_proc(), "clone", [&] { return mrh::clone(*kv); });
   kv.reset();
   stats("Clone", 1);
   return count(kmv->nkey);
@@ -617,6 +646,7 @@ uint64_t MapReduce::clone() {  // :631-652
 uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("collapse");
   kmv = mrh::collapse(*kv, std::string(key, (size_t)kb));
   kv.reset();
@@ -627,6 +657,7 @@ uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
 uint64_t MapReduce::scrunch(int nprocs, const char* key, int kb) {  // :2075-2095
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   const int v = set.verbosity, t = set.timer;
   set.verbosity = set.timer = 0;
   gather(nprocs);
@@ -699,6 +730,7 @@ int MapReduce::multivalue_block(int iblock, char** mv, int** valuebytes) {
 uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kmv("reduce");
   KeyValue kvb(device());
   run_host_kmv(*kmv, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
@@ -711,8 +743,10 @@ uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
 uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dtype) {
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kmv("reduce");
-  kv = mrh::reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype);
+  kv = oom_retry(this, device(), my_proc(), "reduce_builtin",
+                 [&] { return mrh::reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype); });
   kmv.reset();
   stats("Reduce", 0);
   return count(kv->n);
@@ -721,6 +755,7 @@ uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dty
 uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kmv("reduce");
   KeyValue kvb(device());
   fn(*kmv, kvb);
@@ -733,6 +768,7 @@ uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
 uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("compress");
   KMV m = mrh::convert(*kv, &last_convert);
   KeyValue kvb(device());
@@ -745,6 +781,7 @@ uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
 uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& dtype) {
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("compress");
   KMV m = mrh::convert(*kv, &last_convert);
   kv = mrh::reduce_builtin(m, op, dtype.empty() ? "int32" : dtype);
@@ -755,6 +792,7 @@ uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& d
 uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("scan");
   HostCol k = host_col(kv->kdata, kv->koff, kv->kw), v = host_col(kv->vdata, kv->voff, kv->vw);
   for (int64_t i = 0; i < kv->n; ++i) fn(k.at(i), (int)k.len(i), v.at(i), (int)v.len(i));
@@ -765,6 +803,7 @@ uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
 uint64_t MapReduce::scan_kmv(const ScanKMVFn& fn) {  // :1984-2065
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kmv("scan");
   run_host_kmv(*kmv, fn);
   stats("Scan", 1);
@@ -789,14 +828,16 @@ at::Tensor host_perm(const at::Tensor& data, const at::Tensor& off, int w, int64
 uint64_t MapReduce::sort_keys(int flag) {  // :2102-2126
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("sort_keys");
-  kv = sort_kv(*kv, flag, false);
+  kv = oom_retry(this, device(), my_proc(), "sort_keys", [&] { return sort_kv(*kv, flag, false); });
   stats("Sort_keys", 0);
   return count(kv->n);
 }
 uint64_t MapReduce::sort_keys(const CompareFn& fn) {  // :2134-2149
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("sort_keys");
   if (kv->n > 1) kv = mrh::gather(*kv, host_perm(kv->kdata, kv->koff, kv->kw, kv->n, fn, device()));
   stats("Sort_keys", 0);
@@ -805,14 +846,16 @@ uint64_t MapReduce::sort_keys(const CompareFn& fn) {  // :2134-2149
 uint64_t MapReduce::sort_values(int flag) {  // :2156-2180
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("sort_values");
-  kv = sort_kv(*kv, flag, true);
+  kv = oom_retry(this, device(), my_proc(), "sort_values", [&] { return sort_kv(*kv, flag, true); });
   stats("Sort_values", 0);
   return count(kv->n);
 }
 uint64_t MapReduce::sort_values(const CompareFn& fn) {  // :2188-2203
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kv("sort_values");
   if (kv->n > 1) kv = mrh::gather(*kv, host_perm(kv->vdata, kv->voff, kv->vw, kv->n, fn, device()));
   stats("Sort_values", 0);
@@ -821,6 +864,7 @@ uint64_t MapReduce::sort_values(const CompareFn& fn) {  // :2188-2203
 uint64_t MapReduce::sort_multivalues(int flag) {  // :2210-2352
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kmv("sort_multivalues");
   kmv = mrh::sort_multivalues(*kmv, flag);
   stats("Sort_multivalues", 1);
@@ -829,6 +873,7 @@ uint64_t MapReduce::sort_multivalues(int flag) {  // :2210-2352
 uint64_t MapReduce::sort_multivalues(const CompareFn& fn) {
   start();
   OpTrace tr_(__func__);
+  enter(__func__);
   need_kmv("sort_multivalues");
   KMV& m = *kmv;
   HostCol v = host_col(m.vdata, m.voff, m.vw);

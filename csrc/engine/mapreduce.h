@@ -155,6 +155,7 @@ class MapReduce {
 
  private:
   void start();
+  void enter(const char* op);
   void stats(const char* heading, int which);
   void need_kv(const char* what) const;
   void need_kmv(const char* what) const;

@@ -124,11 +124,15 @@ class Comm:
         return Comm(groups[float(color)], device=self.device) if members else None
 
 
-def init(backend=None, timeout_s=600):
+def init(backend=None, timeout_s=None):
     """Initialise the process group from torchrun-style env vars
     (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT), bind this process to
-    GPU LOCAL_RANK, and return a Comm. World size 1 needs no env at all."""
+    GPU LOCAL_RANK, and return a Comm. World size 1 needs no env at all.
+    Collectives are bounded by timeout_s (default MRH_COMM_TIMEOUT or 600 s):
+    a dead peer becomes an error on the other ranks, not a hang."""
     global _WORLD
+    if timeout_s is None:
+        timeout_s = int(os.environ.get("MRH_COMM_TIMEOUT", "600"))
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     # MRH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a
     # device, LOCAL_RANK modulo the device count); production is "nccl" = RCCL
