@@ -5,10 +5,12 @@
 //   wordfreq [-n NTOP] [-v verbosity] [-t timer] FILE_OR_DIR ...
 //
 // map_file hands each rank its files; each file goes to HBM once and the
-// whitespace tokenizer kernel emits KV(word+NUL, NULL) on the device (the
-// reference strtok()s on the host and adds words one by one, :122-127).
-// collate (hash partition + RCCL all-to-all + group-by) -> reduce(count) ->
-// sort_values(-1) -> per-rank top N -> gather(1) -> sort_values(-1) -> print.
+// in-mapper combining kernels (WordCounter, csrc/kernels/wordcount.hip)
+// tokenize and count it on the device, emitting KV(word+NUL, count) once per
+// distinct word of the file (the reference strtok()s on the host and adds
+// every word, :122-127). collate (hash partition + RCCL all-to-all +
+// group-by) -> reduce(sum) -> sort_values(-1) -> per-rank top N ->
+// gather(1) -> sort_values(-1) -> print.
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -16,6 +18,7 @@
 
 #include "apps/app_util.h"
 #include "engine/mapreduce.h"
+#include "engine/wordcount.h"
 
 using namespace mrh;
 
@@ -41,7 +44,8 @@ int main(int argc, char** argv) {
     mr.set.timer = timer;
     comm->barrier();
     const double t0 = Comm::wtime();
-    const uint64_t nwords = mr.map_file(files, 0, 1, 0, [&](int, const char* fname, KeyValue& kv) {
+    int64_t local_words = 0;
+    mr.map_file(files, 0, 1, 0, [&](int, const char* fname, KeyValue& kv) {
       const int64_t n = apps::file_size(fname);
       if (n < 0) {
         std::fprintf(stderr, "ERROR: cannot open %s\n", fname);
@@ -52,10 +56,14 @@ int main(int argc, char** argv) {
       const size_t got = std::fread(host.data_ptr(), 1, (size_t)n, f);
       std::fclose(f);
       MapReduce::rsize += (int64_t)got;
-      kv.add_kv(map_words(host.to(dev, /*non_blocking=*/true), (int64_t)got));
+      WordCounter wc(dev);
+      wc.add(host.to(dev, /*non_blocking=*/true), (int64_t)got);
+      local_words += wc.words();
+      kv.add_kv(wc.finish());
     });
+    const uint64_t nwords = (uint64_t)comm->allreduce(local_words, Comm::SUM);
     mr.collate();
-    const uint64_t nunique = mr.reduce_builtin("count", "int32");
+    const uint64_t nunique = mr.reduce_builtin("sum", "int32");
     comm->barrier();
     const double t1 = Comm::wtime();
 

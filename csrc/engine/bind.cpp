@@ -16,6 +16,7 @@
 #include "graphplan.h"
 #include "mapreduce.h"
 #include "tri.h"
+#include "wordcount.h"
 #include "oink/oink.h"
 
 namespace py = pybind11;
@@ -145,6 +146,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("seconds", &ShuffleStats::seconds);
 
   // native KeyValue builder (MR-MPI KeyValue::add and its multi variants)
+  py::class_<WordCounter>(m, "WordCounter")
+      .def(py::init([](const std::string& d, int64_t init) { return new WordCounter(at::Device(d), init); }),
+           py::arg("device"), py::arg("init_slots") = 1 << 20)
+      .def("add", &WordCounter::add)
+      .def("finish", &WordCounter::finish)
+      .def_property_readonly("words", &WordCounter::words)
+      .def_property_readonly("capacity", &WordCounter::capacity);
   py::class_<KeyValue>(m, "HostKV")
       .def(py::init([](const std::string& d) { return new KeyValue(at::Device(d)); }))
       .def("add", [](KeyValue& kv, const std::string& k,

@@ -182,3 +182,20 @@ void ii_write(const uint8_t* kd, const int64_t* koff, const int32_t* vals, int64
 
 }  // namespace k
 }  // namespace mrh
+
+// ---------------------------------------------------------------- wordcount.hip
+// In-mapper combining word count (see wordcount.hip). slots/counts: table of
+// `cap` (power of two) entries; ctr[0] used slots, ctr[1] arena bytes;
+// newlist receives the slots claimed by this chunk (>= words-in-chunk entries).
+namespace mrh {
+namespace k {
+void wc_count(const uint8_t* text, int64_t n, uint64_t* slots, uint32_t* counts, int64_t cap, int32_t* newlist,
+              uint64_t* ctr, uint64_t used0, const uint8_t* arena, hipStream_t s);
+void wc_migrate(const uint8_t* text, int64_t n, uint64_t* slots, int64_t cap, int32_t* newlist, uint64_t* ctr,
+                uint64_t used0, uint8_t* arena, int64_t max_new, hipStream_t s);
+void wc_rehash(const uint64_t* old_slots, const uint32_t* old_counts, int64_t old_cap, const uint8_t* arena,
+               uint64_t* new_slots, uint32_t* new_counts, int64_t new_cap, hipStream_t s);
+void wc_keys(const uint64_t* slots, const int64_t* idx, int64_t nk, const uint8_t* arena, int64_t* starts,
+             int32_t* lens, hipStream_t s);
+}  // namespace k
+}  // namespace mrh

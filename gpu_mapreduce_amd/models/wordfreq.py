@@ -5,10 +5,14 @@ Reference pipeline: map(files, strtok words) -> collate -> reduce(count) ->
 sort_values(-1) -> local top 10 -> gather(1) -> sort_values(-1) -> print.
 
 MI355X pipeline (same op sequence on device-resident data):
-  map       text chunks stream host->HBM (double buffered), the whitespace
-            tokenizer kernel emits KV(word+NUL, NULL) in HBM;
-  compress  optional local combiner: convert + count (MR-MPI compress), so the
-            shuffle moves (word, count) once per distinct word per rank;
+  map       text chunks stream host->HBM (double buffered); with the combiner
+            (default) the in-mapper combining kernels (csrc/kernels/
+            wordcount.hip) tokenize and count every chunk into a device hash
+            table (LDS pre-aggregation, exact byte-compare matching) and the
+            map emits KV(word+NUL, int32 count) once per distinct word — the
+            pairs map + compress(count) would leave, without materialising a
+            KV per occurrence; without it the tokenizer kernel emits
+            KV(word+NUL, NULL) per occurrence;
   collate   hashlittle partition + RCCL all-to-all + group-by;
   reduce    "sum:int32" (or "count" without the combiner) segmented reduce;
   top-N     sort_values(-1) (radix on negated counts) -> slice -> gather(1) ->
@@ -41,15 +45,29 @@ class WordFreq:
         self.copy_stream = torch.cuda.Stream() if self.is_cuda else None
 
     def _map(self, itask, kv):
+        self.local_words = 0
         if not self.chunks:
             return
+        wc = C.WordCounter(self.mr.device) if self.combiner else None
+
+        def consume(buf, n):
+            if wc is not None:
+                wc.add(buf, n)
+            else:
+                kv.add_kv(C.map_words(buf, n))
         if not self.is_cuda:
             for t in self.chunks:
                 b = self.bufs[0]
                 b[: t.numel()].copy_(t)
                 b[t.numel():t.numel() + PAD].zero_()
-                kv.add_kv(C.map_words(b, t.numel()))
-            return
+                consume(b, t.numel())
+        else:
+            self._stream_chunks(consume)
+        if wc is not None:
+            self.local_words = wc.words
+            kv.add_kv(wc.finish())
+
+    def _stream_chunks(self, consume):
         main = torch.cuda.current_stream()
         cs = self.copy_stream
         ready = [torch.cuda.Event(), torch.cuda.Event()]
@@ -69,17 +87,19 @@ class WordFreq:
                 issue(i + 1)
             b = i & 1
             main.wait_event(ready[b])
-            kv.add_kv(C.map_words(self.bufs[b], self.chunks[i].numel()))
+            consume(self.bufs[b], self.chunks[i].numel())
             free[b].record(main)
 
     def run(self):
         mr = self.mr
-        self.nwords = mr.map(mr.nprocs, self._map)
+        nkv = mr.map(mr.nprocs, self._map)
         if self.combiner:
-            mr.compress("count")          # (word, local count)
+            # pairs are (word, local count): total words = sum of the counts
+            self.nwords = int(mr.comm.allreduce(self.local_words, "sum"))
             self.nunique = mr.collate()
             mr.reduce("sum:int32")
         else:
+            self.nwords = nkv
             self.nunique = mr.collate()
             mr.reduce("count")
         mr.sort_values(-1)
