@@ -44,3 +44,17 @@ def test_mrmpi_ops():
     got = []
     mr.scan_kv(lambda k, v: got.append(v))
     assert sorted(got) == [4, 4, 6, 6, 10, 10]
+
+
+def test_rmat_python_example():
+    """examples/python/rmat.py (reference examples/rmat.py) on the CPU engine"""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "rmat_example", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples",
+                                     "python", "rmat.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    order, ntotal, histo = mod.main(["8", "4", "0.57", "0.19", "0.19", "0.05", "0.1", "3"])
+    assert (order, ntotal) == (256, 1024)
+    assert sum(k * v for k, v in histo) == ntotal
