@@ -206,13 +206,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property("fpath", [](MR& r) { return r.set.fpath; }, [](MR& r, const std::string& v) { r.set.fpath = v; })
       .def_readwrite("mapfilecount", &MR::mapfilecount)
       .def_property(
-          "kv", [](MR& r) -> py::object { return r.kv ? py::cast(*r.kv) : py::none(); },
+          "kv", [](MR& r) -> py::object {
+            r.ensure_resident();
+            return r.kv ? py::cast(*r.kv) : py::none();
+          },
           [](MR& r, py::object o) {
             if (o.is_none()) r.kv.reset();
             else r.kv = o.cast<KV>();
           })
       .def_property(
-          "kmv", [](MR& r) -> py::object { return r.kmv ? py::cast(*r.kmv) : py::none(); },
+          "kmv", [](MR& r) -> py::object {
+            r.ensure_resident();
+            return r.kmv ? py::cast(*r.kmv) : py::none();
+          },
           [](MR& r, py::object o) {
             if (o.is_none()) r.kmv.reset();
             else r.kmv = o.cast<KMV>();
@@ -304,6 +310,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("load", &MR::load)
       .def("spill", &MR::spill)
       .def("unspill", &MR::unspill)
+      .def("spill_disk", &MR::spill_disk)
+      .def("ensure_resident", &MR::ensure_resident)
+      .def_property_readonly("on_disk", &MR::on_disk)
       .def("my_proc", &MR::my_proc)
       .def("num_procs", &MR::num_procs)
       .def_property_readonly("device", [](MR& r) { return r.device().str(); });

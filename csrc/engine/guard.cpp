@@ -148,10 +148,17 @@ int spill_others(const MapReduce* keep, at::Device dev) {
   {
     std::lock_guard<std::mutex> l(g_mu);
     for (MapReduce* m : live())
-      if (m != keep && m->device() == dev && ((m->kv && m->kv->device() == dev) || (m->kmv && m->kmv->keys.device() == dev)))
+      if (m != keep && m->set.outofcore != -1 && m->device() == dev &&
+          ((m->kv && m->kv->device() == dev) || (m->kmv && m->kmv->keys.device() == dev)))
         victims.push_back(m);
   }
-  for (MapReduce* m : victims) m->spill();
+  for (MapReduce* m : victims) {
+    try {
+      m->spill();  // pinned host DRAM
+    } catch (const std::exception&) {
+      m->spill_disk();  // host memory exhausted too: last tier
+    }
+  }
   if (dev.is_cuda()) c10::hip::HIPCachingAllocator::emptyCache();
   if (!victims.empty())
     std::fprintf(stderr, "mrhip: out of device memory; spilled %zu MapReduce object(s) to host and retrying\n",

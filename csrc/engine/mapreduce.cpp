@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <filesystem>
 #include <fstream>
 #include <numeric>
@@ -36,9 +37,22 @@ namespace {
 
 // roctx range per MapReduce op: `rocprofv3 --marker-trace` shows every op
 // (map, aggregate, convert, reduce, ...) around its kernels and RCCL calls
+// On scope exit (after the op's return value is computed) an MR with
+// outofcore == 1 writes its data to disk — the reference's forced
+// out-of-core mode (src/keyvalue.cpp:122,223); the next op reads it back.
 struct OpTrace {
-  explicit OpTrace(const char* name) { roctxRangePushA(name); }
-  ~OpTrace() { roctxRangePop(); }
+  OpTrace(const char* name, MapReduce* mr) : mr_(mr) { roctxRangePushA(name); }
+  ~OpTrace() {
+    if (mr_->set.outofcore == 1 && std::uncaught_exceptions() == 0) {
+      try {
+        mr_->spill_disk();
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "mrhip: out-of-core write failed: %s\n", e.what());
+      }
+    }
+    roctxRangePop();
+  }
+  MapReduce* mr_;
 };
 
 [[noreturn]] void fail(const std::string& m) { throw std::runtime_error(m); }
@@ -190,6 +204,7 @@ MapReduce::MapReduce(CommPtr comm) : comm_(std::move(comm)) {
 }
 
 MapReduce::~MapReduce() {
+  drop_disk();
   guard::unregister_mr(this);
   instances_now--;
 }
@@ -198,6 +213,7 @@ MapReduce::~MapReduce() {
 // or spill-on-OOM) comes back to HBM before the op touches it
 void MapReduce::enter(const char* op) {
   guard::fault_point(op, comm_->rank());
+  ensure_resident();
   if (device().is_cuda() && ((kv && !kv->device().is_cuda()) || (kmv && !kmv->keys.device().is_cuda()))) unspill();
 }
 
@@ -296,9 +312,10 @@ void MapReduce::note_shuffle(const ShuffleStats& st) {
 
 uint64_t MapReduce::add(MapReduce& other) {  // :348-374
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("add");
+  other.ensure_resident();
   if (!other.kv) fail("MapReduce passed to add() does not have KeyValue pairs");
   kv = concat({*kv, *other.kv}, device());
   stats("Add", 0);
@@ -359,7 +376,7 @@ uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) 
 
 uint64_t MapReduce::map(int nmap, const MapTaskFn& fn, int addflag) {  // :1044-1051
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   KeyValue kvb(device());
   for (int t : my_tasks(nmap)) fn(t, kvb);
@@ -394,7 +411,7 @@ std::vector<std::string> MapReduce::find_files(const Comm& comm, const std::vect
 uint64_t MapReduce::map_file(const std::vector<std::string>& files, int selfflag, int recurse, int readflag,
                              const MapFileFn& fn, int addflag) {  // :1060-1092
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
@@ -425,7 +442,7 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
                                int readflag, const std::string& sep, bool is_char, int delta, const MapChunkFn& fn,
                                int addflag) {
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
@@ -502,8 +519,9 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
 
 uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  // :1560-1642
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
+  src.ensure_resident();
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   HostCol k = host_col(s.kdata, s.koff, s.kw), v = host_col(s.vdata, s.voff, s.vw);
@@ -521,8 +539,9 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
 
 uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addflag) {
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
+  src.ensure_resident();
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   KeyValue kvb(device());
@@ -541,7 +560,7 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
 
 uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("aggregate");
   if (comm_->size() > 1) {
@@ -567,7 +586,7 @@ uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
 
 uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("aggregate");
   if (comm_->size() > 1) {
@@ -581,7 +600,7 @@ uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
 
 uint64_t MapReduce::broadcast(int root) {  // :569-623
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("broadcast");
   if (comm_->size() > 1) kv = mrh::broadcast(*kv, root, comm_->pg());
@@ -591,7 +610,7 @@ uint64_t MapReduce::broadcast(int root) {  // :569-623
 
 uint64_t MapReduce::gather(int nprocs) {  // :893-1036
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("gather");
   if (nprocs < 1 || nprocs > comm_->size()) fail("Invalid proc count for gather");
@@ -608,7 +627,7 @@ uint64_t MapReduce::gather(int nprocs) {  // :893-1036
 
 uint64_t MapReduce::convert() {  // :861-886
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("convert");
   kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert); });
@@ -619,7 +638,7 @@ uint64_t MapReduce::convert() {  // :861-886
 
 uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("collate");
   const int v = set.verbosity, t = set.timer;
@@ -634,7 +653,7 @@ uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
 
 uint64_t MapReduce::clone() {  // :631-652
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("clone");
   kmv = oom_retry(this, device(), my_proc(), "clone", [&] { return mrh::clone(*kv); });
@@ -645,7 +664,7 @@ uint64_t MapReduce::clone() {  // :631-652
 
 uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("collapse");
   kmv = mrh::collapse(*kv, std::string(key, (size_t)kb));
@@ -656,7 +675,7 @@ uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
 
 uint64_t MapReduce::scrunch(int nprocs, const char* key, int kb) {  // :2075-2095
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   const int v = set.verbosity, t = set.timer;
   set.verbosity = set.timer = 0;
@@ -729,7 +748,7 @@ int MapReduce::multivalue_block(int iblock, char** mv, int** valuebytes) {
 
 uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kmv("reduce");
   KeyValue kvb(device());
@@ -742,7 +761,7 @@ uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
 
 uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dtype) {
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kmv("reduce");
   kv = oom_retry(this, device(), my_proc(), "reduce_builtin",
@@ -754,7 +773,7 @@ uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dty
 
 uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kmv("reduce");
   KeyValue kvb(device());
@@ -767,7 +786,7 @@ uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
 
 uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("compress");
   KMV m = mrh::convert(*kv, &last_convert);
@@ -780,7 +799,7 @@ uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
 
 uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& dtype) {
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("compress");
   KMV m = mrh::convert(*kv, &last_convert);
@@ -791,7 +810,7 @@ uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& d
 
 uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("scan");
   HostCol k = host_col(kv->kdata, kv->koff, kv->kw), v = host_col(kv->vdata, kv->voff, kv->vw);
@@ -802,7 +821,7 @@ uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
 
 uint64_t MapReduce::scan_kmv(const ScanKMVFn& fn) {  // :1984-2065
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kmv("scan");
   run_host_kmv(*kmv, fn);
@@ -827,7 +846,7 @@ at::Tensor host_perm(const at::Tensor& data, const at::Tensor& off, int w, int64
 
 uint64_t MapReduce::sort_keys(int flag) {  // :2102-2126
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("sort_keys");
   kv = oom_retry(this, device(), my_proc(), "sort_keys", [&] { return sort_kv(*kv, flag, false); });
@@ -836,7 +855,7 @@ uint64_t MapReduce::sort_keys(int flag) {  // :2102-2126
 }
 uint64_t MapReduce::sort_keys(const CompareFn& fn) {  // :2134-2149
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("sort_keys");
   if (kv->n > 1) kv = mrh::gather(*kv, host_perm(kv->kdata, kv->koff, kv->kw, kv->n, fn, device()));
@@ -845,7 +864,7 @@ uint64_t MapReduce::sort_keys(const CompareFn& fn) {  // :2134-2149
 }
 uint64_t MapReduce::sort_values(int flag) {  // :2156-2180
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("sort_values");
   kv = oom_retry(this, device(), my_proc(), "sort_values", [&] { return sort_kv(*kv, flag, true); });
@@ -854,7 +873,7 @@ uint64_t MapReduce::sort_values(int flag) {  // :2156-2180
 }
 uint64_t MapReduce::sort_values(const CompareFn& fn) {  // :2188-2203
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("sort_values");
   if (kv->n > 1) kv = mrh::gather(*kv, host_perm(kv->vdata, kv->voff, kv->vw, kv->n, fn, device()));
@@ -863,7 +882,7 @@ uint64_t MapReduce::sort_values(const CompareFn& fn) {  // :2188-2203
 }
 uint64_t MapReduce::sort_multivalues(int flag) {  // :2210-2352
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kmv("sort_multivalues");
   kmv = mrh::sort_multivalues(*kmv, flag);
@@ -872,7 +891,7 @@ uint64_t MapReduce::sort_multivalues(int flag) {  // :2210-2352
 }
 uint64_t MapReduce::sort_multivalues(const CompareFn& fn) {
   start();
-  OpTrace tr_(__func__);
+  OpTrace tr_(__func__, this);
   enter(__func__);
   need_kmv("sort_multivalues");
   KMV& m = *kmv;
@@ -1090,8 +1109,12 @@ KV get_kv(std::FILE* f, at::Device dev) {
 }  // namespace
 
 void MapReduce::save(const std::string& path) const {
-  if (!kv && !kmv) fail("Cannot save without KeyValue or KeyMultiValue");
-  const std::string p = rank_path(path, *comm_);
+  if (disk_path_.empty() && !kv && !kmv) fail("Cannot save without KeyValue or KeyMultiValue");
+  const_cast<MapReduce*>(this)->ensure_resident();
+  write_file(rank_path(path, *comm_));
+}
+
+void MapReduce::write_file(const std::string& p) const {
   std::FILE* f = std::fopen(p.c_str(), "wb");
   if (!f) fail("Could not open checkpoint file " + p);
   std::fwrite(kMagic, 1, 8, f);
@@ -1113,7 +1136,11 @@ void MapReduce::save(const std::string& path) const {
 }
 
 uint64_t MapReduce::load(const std::string& path) {
-  const std::string p = rank_path(path, *comm_);
+  drop_disk();
+  return count(read_file(rank_path(path, *comm_)));
+}
+
+int64_t MapReduce::read_file(const std::string& p) {
   std::FILE* f = std::fopen(p.c_str(), "rb");
   if (!f) fail("Could not open checkpoint file " + p);
   char magic[8];
@@ -1146,7 +1173,38 @@ uint64_t MapReduce::load(const std::string& path) {
   }
   rsize += std::ftell(f);
   std::fclose(f);
-  return count(n);
+  return n;
+}
+
+// ---------------------------------------------------------------- disk tier
+// The third memory tier (HBM -> pinned host -> disk): the data goes to a
+// per-rank file named like the reference's out-of-core files
+// (fpath/mrmpi.<kv|kmv>.<instance>.<counter>.<rank>, src/mapreduce.cpp:3187-3205)
+// and comes back on the MR's next op (ensure_resident, called from enter()).
+void MapReduce::spill_disk() {
+  if (!kv && !kmv) return;
+  char name[96];
+  std::snprintf(name, sizeof(name), "mrmpi.%s.%d.%d.%d", kv ? "kv" : "kmv", instance_me_, ++disk_counter_,
+                comm_->rank());
+  const std::string p = (std::filesystem::path(set.fpath) / name).string();
+  write_file(p);
+  kv.reset();
+  kmv.reset();
+  disk_path_ = p;
+}
+
+void MapReduce::ensure_resident() {
+  if (disk_path_.empty()) return;
+  const std::string p = disk_path_;
+  disk_path_.clear();
+  read_file(p);
+  std::remove(p.c_str());
+}
+
+void MapReduce::drop_disk() {
+  if (disk_path_.empty()) return;
+  std::remove(disk_path_.c_str());
+  disk_path_.clear();
 }
 
 }  // namespace mrh

@@ -131,6 +131,11 @@ class MapReduce {
   // host spill tier: move the data to pinned host DRAM and back
   void spill();
   void unspill();
+  // disk tier: write the data to fpath/mrmpi.<kv|kmv>.<instance>.<n>.<rank>
+  // and free it; it is read back (and the file removed) on the next op
+  void spill_disk();
+  void ensure_resident();
+  bool on_disk() const { return !disk_path_.empty(); }
 
   // checkpoint / restart of this rank's KV or KMV (binary SoA file, one per
   // rank: `path` gets ".<rank>" appended when nprocs > 1); load returns the
@@ -169,7 +174,13 @@ class MapReduce {
   void histo(double v, const char* heading) const;
   int64_t block_bytes() const;
 
+  void write_file(const std::string& p) const;
+  int64_t read_file(const std::string& p);
+  void drop_disk();
+
   CommPtr comm_;
+  std::string disk_path_;
+  int disk_counter_ = 0;
   std::unique_ptr<KeyValue> open_;
   int open_add_ = 0;
   double t0_ = 0;

@@ -319,6 +319,15 @@ class MapReduce(metaclass=_Counters):
     def unspill(self):
         self._m.unspill()
 
+    def spill_disk(self):
+        """Write the data to fpath/mrmpi.<kv|kmv>.<instance>.<n>.<rank> and free
+        it (disk tier); the next op reads it back."""
+        self._m.spill_disk()
+
+    @property
+    def on_disk(self):
+        return self._m.on_disk
+
     # ------------------------------------------------------------------ checkpoint / restart
     def save(self, path):
         """Write this rank's KV/KMV to `path` (".<rank>" appended when nprocs > 1)."""

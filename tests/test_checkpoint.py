@@ -64,3 +64,49 @@ def test_verbosity_and_timer_output(capsys):
     assert "Map KV = 800 pairs" in out
     assert "Collate KMV = 17 pairs" in out
     assert "Cummulative hi-water mem" in out
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_outofcore_disk_tier(tmp_path, dev):
+    """outofcore=1 (the reference's forced out-of-core mode): every op's result
+    goes to fpath/mrmpi.<kv|kmv>.* and is read back by the next op; results
+    equal the in-memory run and the files are gone afterwards"""
+    import os
+
+    def pipeline(mr, other):
+        _fill(mr)
+        mr.collate()
+        mr.reduce("count")
+        mr.sort_values(-1)
+        other.map_mr(mr, lambda i, k, v, kv: kv.add(k, v))   # reads an MR that sits on disk
+        return other.kv_pairs()
+
+    ref = pipeline(g.MapReduce(device=dev), g.MapReduce(device=dev))
+    mr, other = g.MapReduce(device=dev), g.MapReduce(device=dev)
+    for m in (mr, other):
+        m.outofcore = 1
+        m.fpath = str(tmp_path)
+    _fill(mr)
+    assert mr.on_disk and any(f.startswith("mrmpi.kv.") for f in os.listdir(tmp_path))
+    mr.collate()
+    assert mr.on_disk and any(f.startswith("mrmpi.kmv.") for f in os.listdir(tmp_path))
+    mr.reduce("count")
+    mr.sort_values(-1)
+    other.map_mr(mr, lambda i, k, v, kv: kv.add(k, v))
+    assert other.kv_pairs() == ref
+    del mr, other
+    import gc
+    gc.collect()
+    assert [f for f in os.listdir(tmp_path) if f.startswith("mrmpi.")] == []
+
+
+def test_spill_disk_manual(tmp_path):
+    mr = g.MapReduce(device="cpu")
+    mr.fpath = str(tmp_path)
+    _fill(mr)
+    before = mr.kv_pairs()
+    mr.spill_disk()
+    assert mr.on_disk
+    assert mr.kv_pairs() == before and not mr.on_disk     # reading brings it back
+    mr.spill_disk()
+    assert mr.collate() == 17 and not mr.on_disk
