@@ -117,3 +117,12 @@ def test_oom_spill_retry_gpu():
     assert r.returncode == 0, r.stderr
     # the victim was moved to host memory: its next op brought it back to HBM
     assert "OOM-RETRY-OK" in r.stdout and "spilled 1 MapReduce object(s)" in r.stderr
+
+
+@pytest.mark.skipif(os.environ.get("MRH_ASAN") != "1", reason="slow (rebuilds the host code with ASan); MRH_ASAN=1")
+def test_host_asan_clean():
+    """host AddressSanitizer build of the engine + C API + OINK runs the C API
+    test, a 2-rank C job and two OINK scripts cleanly (tools/asan_check.sh)"""
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "asan_check.sh")], capture_output=True, text=True,
+                       timeout=1800)
+    assert r.returncode == 0 and "ASAN CLEAN" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
