@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="invertedindex", choices=["invertedindex", "pagerank", "wordfreq", "trifind", "intcount"])
+    ap.add_argument("--workload", default="invertedindex", choices=["invertedindex", "pagerank", "wordfreq", "trifind", "intcount", "kmeans"])
     ap.add_argument("--bytes-per-gpu", type=float, default=float(1 << 30))
     ap.add_argument("--file-bytes", type=int, default=128 << 20)
     ap.add_argument("--link-gap", type=int, default=200)
@@ -122,7 +122,10 @@ def main():
     ap.add_argument("--edgefactor", type=int, default=16, help="RMAT edges per vertex")
     ap.add_argument("--intcount-bytes", type=int, default=128 << 20, help="intcount: raw int32 bytes per GPU")
     ap.add_argument("--key-range", type=int, default=1 << 24, help="intcount: keys uniform in [0, key_range)")
-    ap.add_argument("--iters", type=int, default=20, help="pagerank iterations per step")
+    ap.add_argument("--iters", type=int, default=20, help="pagerank / kmeans iterations per step")
+    ap.add_argument("--kmeans-points", type=int, default=32 << 20, help="kmeans: points per GPU")
+    ap.add_argument("--kmeans-dim", type=int, default=2)
+    ap.add_argument("--kmeans-k", type=int, default=32)
     args = ap.parse_args()
     if args.scale is None:
         args.scale = 24 if args.workload == "trifind" else 26
@@ -140,6 +143,9 @@ def main():
     elif args.workload == "trifind":
         from gpu_mapreduce_amd.models.triangles import bench_trifind
         res = bench_trifind(comm, args)
+    elif args.workload == "kmeans":
+        from gpu_mapreduce_amd.models.kmeans import bench_kmeans
+        res = bench_kmeans(comm, args)
     else:
         from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
         res = bench_wordfreq(comm, args)
@@ -147,7 +153,8 @@ def main():
         "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": comm.size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
         "higher_is_better": True, "scaling": res.get("scaling", "weak"), "vs_baseline": res.get("vs_baseline"),
-        "dtype": "bytes+int32 (no float compute in MapReduce)", "data": "synthetic", "config": res["config"],
+        "dtype": res.get("dtype", "bytes+int32 (no float compute in MapReduce)"), "data": "synthetic",
+        "config": res["config"],
     }
     for k, v in res.items():
         if k not in out:

@@ -403,6 +403,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("broadcast", [](const KV& kv, int root, py::object pg) { return mrh::broadcast(kv, root, as_pg(pg)); });
   m.def("map_urls", &map_urls);
+  m.def("kmeans_map", &kmeans_map);
   m.def("map_words", &map_words);
   m.def("map_rmat", [](int64_t ne, int nl, double a, double b, double c, double d, double f, uint64_t seed,
                        uint64_t first, const std::string& dev) {

@@ -155,6 +155,9 @@ std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor
 // segment boundaries of a sorted int64 key column: seg[nseg+1]
 at::Tensor segments_sorted(const at::Tensor& sorted_keys);
 
+// K-means map with in-mapper combining (kmeans.cpp): KV(int32 cluster*(D+1)+j, double)
+KV kmeans_map(const at::Tensor& points, const at::Tensor& centroids);
+
 // ------------------------------------------------------------------ app epilogues
 at::Tensor inverted_index_format(const KMV& kmv, const at::Tensor& names, const at::Tensor& name_off);
 

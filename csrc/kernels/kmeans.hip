@@ -1,0 +1,237 @@
+// K-means map with in-mapper combining (the GPMR K-means workload of
+// chapter_final.pdf Fig. 6a: 32 M 2-D points per GPU; not in the reference
+// code, which only runs IntCount-style jobs on MR-MPI).
+//
+// One pass over the points: each lane assigns its points to the nearest
+// centroid (centroids staged in LDS, D <= 8 dims in registers) and adds the
+// point to its workgroup's per-cluster LDS accumulators (fp32 sums + count);
+// the workgroup then flushes its K x (D+1) partials into a global fp64 array
+// with device atomics (global_atomic_add_f64). The map emits (cluster, sums,
+// count) KVs from that array — GPMR's "emit (cluster, point) then combine"
+// without materialising one KV per point.
+#include "common.h"
+#include "launch.h"
+#include <cstdio>
+#include <cstdlib>
+#include <cfloat>
+
+namespace mrh {
+namespace k {
+namespace {
+
+constexpr int NT = 256;
+constexpr int PTS_PER_THREAD = 8;
+
+template <int D>
+__global__ __launch_bounds__(NT) void k_kmeans(const float* __restrict__ pts, int64_t n,
+                                              const float* __restrict__ cen, int K, double* __restrict__ acc) {
+  extern __shared__ float sh[];
+  float* c = sh;                 // K*D centroids
+  float* part = sh + K * D;      // K*(D+1) partial sums (+count)
+  for (int i = threadIdx.x; i < K * D; i += NT) c[i] = cen[i];
+  for (int i = threadIdx.x; i < K * (D + 1); i += NT) part[i] = 0.f;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * NT * PTS_PER_THREAD;
+#pragma unroll 1
+  for (int r = 0; r < PTS_PER_THREAD; ++r) {
+    const int64_t i = base + (int64_t)r * NT + threadIdx.x;  // coalesced across the block
+    if (i >= n) break;
+    float x[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) x[d] = pts[i * D + d];
+    float best = FLT_MAX;
+    int bk = 0;
+    for (int kk = 0; kk < K; ++kk) {
+      float dist = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const float t = x[d] - c[kk * D + d];
+        dist = fmaf(t, t, dist);
+      }
+      if (dist < best) {
+        best = dist;
+        bk = kk;
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) atomicAdd(&part[bk * (D + 1) + d], x[d]);
+    atomicAdd(&part[bk * (D + 1) + D], 1.f);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < K * (D + 1); i += NT)
+    if (part[i] != 0.f) atomicAdd(&acc[i], (double)part[i]);
+}
+
+// Private-accumulator variant (K*(D+1) <= 120): every lane owns a column of
+// LDS accumulators laid out [value][lane], so the per-point update is a plain
+// conflict-free LDS read-modify-write (no atomics, no contention on popular
+// clusters); the workgroup then reduces each accumulator row with one wave
+// (64-lane shuffles) and issues one fp64 global atomic per row. Grid-stride
+// over the points with a capped grid (~8 workgroups per CU), so each lane
+// sees hundreds of points.
+constexpr int PNT = 128;
+template <int D>
+__global__ __launch_bounds__(PNT) void k_kmeans_priv(const float* __restrict__ pts, int64_t n,
+                                                    const float* __restrict__ cen, int K, double* __restrict__ acc) {
+  extern __shared__ float sh[];
+  const int R = K * (D + 1);
+  float* c = sh;                    // K*D centroids
+  float* priv = sh + ((K * D + 3) & ~3);  // R rows x PNT lanes
+  for (int i = threadIdx.x; i < K * D; i += PNT) c[i] = cen[i];
+  for (int i = threadIdx.x; i < R * PNT; i += PNT) priv[i] = 0.f;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * PNT;
+  for (int64_t i = (int64_t)blockIdx.x * PNT + threadIdx.x; i < n; i += stride) {
+    float x[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) x[d] = pts[i * D + d];
+    float best = FLT_MAX;
+    int bk = 0;
+    for (int kk = 0; kk < K; ++kk) {
+      float dist = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const float t = x[d] - c[kk * D + d];
+        dist = fmaf(t, t, dist);
+      }
+      if (dist < best) {
+        best = dist;
+        bk = kk;
+      }
+    }
+    float* row = priv + (bk * (D + 1)) * PNT + threadIdx.x;
+#pragma unroll
+    for (int d = 0; d < D; ++d) row[d * PNT] += x[d];
+    row[D * PNT] += 1.f;
+  }
+  __syncthreads();
+  const int w = threadIdx.x / MRH_WAVE, l = dev::lane_id();
+  for (int r = w; r < R; r += PNT / MRH_WAVE) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < PNT / MRH_WAVE; ++j) v += priv[r * PNT + j * MRH_WAVE + l];
+    v = dev::wave_sum(v);
+    if (l == 0 && v != 0.f) atomicAdd(&acc[r], (double)v);
+  }
+}
+
+// Batched variant: every lane loads its PB points up front (independent
+// loads in flight instead of one dependent load per loop trip), scores
+// centroids as ||c||^2 - 2 x.c from one 16-byte LDS broadcast read per
+// centroid ({-2c, ||c||^2}, D <= 3), and adds into per-workgroup LDS
+// partials with LDS float atomics.
+constexpr int BNT = 256, PB = 8;
+template <int D>
+__global__ __launch_bounds__(BNT) void k_kmeans_batch(const float* __restrict__ pts, int64_t n,
+                                                     const float* __restrict__ cen, int K, double* __restrict__ acc) {
+  static_assert(D <= 3, "one float4 per centroid");
+  extern __shared__ float sh[];
+  float4* c4 = reinterpret_cast<float4*>(sh);      // K x {-2c0, -2c1, -2c2, |c|^2}
+  float* part = sh + 4 * K;                          // K*(D+1)
+  for (int kk = threadIdx.x; kk < K; kk += BNT) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    float cc = 0.f;
+    for (int d = 0; d < D; ++d) {
+      const float cd = cen[kk * D + d];
+      v[d] = -2.f * cd;
+      cc = fmaf(cd, cd, cc);
+    }
+    v[3] = cc;
+    c4[kk] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  for (int i = threadIdx.x; i < K * (D + 1); i += BNT) part[i] = 0.f;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * BNT * PB + threadIdx.x;
+  float x[PB][D];
+#pragma unroll
+  for (int r = 0; r < PB; ++r) {
+    const int64_t i = base + (int64_t)r * BNT;
+#pragma unroll
+    for (int d = 0; d < D; ++d) x[r][d] = (i < n) ? pts[i * D + d] : 0.f;
+  }
+  float best[PB];
+  int bk[PB];
+#pragma unroll
+  for (int r = 0; r < PB; ++r) {
+    best[r] = FLT_MAX;
+    bk[r] = 0;
+  }
+  for (int kk = 0; kk < K; ++kk) {
+    const float4 c = c4[kk];
+#pragma unroll
+    for (int r = 0; r < PB; ++r) {
+      float sc = c.w;
+      sc = fmaf(x[r][0], c.x, sc);
+      if (D > 1) sc = fmaf(x[r][1], c.y, sc);
+      if (D > 2) sc = fmaf(x[r][2], c.z, sc);
+      const bool lt = sc < best[r];
+      best[r] = lt ? sc : best[r];
+      bk[r] = lt ? kk : bk[r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < PB; ++r) {
+    if (base + (int64_t)r * BNT >= n) break;
+#pragma unroll
+    for (int d = 0; d < D; ++d) atomicAdd(&part[bk[r] * (D + 1) + d], x[r][d]);
+    atomicAdd(&part[bk[r] * (D + 1) + D], 1.f);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < K * (D + 1); i += BNT)
+    if (part[i] != 0.f) atomicAdd(&acc[i], (double)part[i]);
+}
+
+template <int D>
+void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, hipStream_t s) {
+  static const int variant = [] {
+    const char* e = std::getenv("MRH_KMEANS_KERNEL");
+    return e ? std::atoi(e) : 0;
+  }();
+  if constexpr (D <= 3) {
+    if (variant == 0 && (size_t)K * (4 + D + 1) * 4 <= 64 * 1024) {
+      const int64_t nb = (n + (int64_t)BNT * PB - 1) / ((int64_t)BNT * PB);
+      const size_t lds = sizeof(float) * (size_t)K * (4 + D + 1);
+      hipLaunchKernelGGL((k_kmeans_batch<D>), dim3((unsigned)nb), dim3(BNT), lds, s, pts, n, cen, K, acc);
+      MRH_CHECK_LAUNCH();
+      return;
+    }
+  }
+  if (variant == 1 && K * (D + 1) <= 120) {  // <= 61.5 KB of private accumulators
+    int64_t nb = (n + PNT - 1) / PNT;
+    if (nb > 2048) nb = 2048;
+    const size_t lds = sizeof(float) * (size_t)(((K * D + 3) & ~3) + K * (D + 1) * PNT);
+    hipLaunchKernelGGL((k_kmeans_priv<D>), dim3((unsigned)nb), dim3(PNT), lds, s, pts, n, cen, K, acc);
+    MRH_CHECK_LAUNCH();
+    return;
+  }
+  const int64_t nb = (n + (int64_t)NT * PTS_PER_THREAD - 1) / ((int64_t)NT * PTS_PER_THREAD);
+  const size_t lds = sizeof(float) * (size_t)K * (2 * D + 1);
+  hipLaunchKernelGGL((k_kmeans<D>), dim3((unsigned)nb), dim3(NT), lds, s, pts, n, cen, K, acc);
+  MRH_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+// fp32 LDS partials hold at most NT*PTS_PER_THREAD = 2048 points per workgroup,
+// so per-cluster counts are exact and sums lose no more than fp32 rounding of
+// 2048 terms before the fp64 global accumulation.
+bool kmeans_supported(int D, int K) {
+  return (D == 1 || D == 2 || D == 3 || D == 4 || D == 8) && K >= 1 && (size_t)K * (2 * D + 1) * 4 <= 64 * 1024;
+}
+// (the private-accumulator kernel uses < 62 KB of LDS: K*(D+1) <= 120 rows x 128 lanes + centroids)
+
+void kmeans_assign_accumulate(const float* pts, int64_t n, int D, const float* cen, int K, double* acc,
+                              hipStream_t s) {
+  if (n <= 0) return;
+  switch (D) {
+    case 1: launch<1>(pts, n, cen, K, acc, s); break;
+    case 2: launch<2>(pts, n, cen, K, acc, s); break;
+    case 3: launch<3>(pts, n, cen, K, acc, s); break;
+    case 4: launch<4>(pts, n, cen, K, acc, s); break;
+    case 8: launch<8>(pts, n, cen, K, acc, s); break;
+    default: fprintf(stderr, "kmeans: unsupported D=%d\n", D); abort();
+  }
+}
+
+}  // namespace k
+}  // namespace mrh

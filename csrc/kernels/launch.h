@@ -199,3 +199,13 @@ void wc_keys(const uint64_t* slots, const int64_t* idx, int64_t nk, const uint8_
              int32_t* lens, hipStream_t s);
 }  // namespace k
 }  // namespace mrh
+
+// ---------------------------------------------------------------- kmeans.hip
+namespace mrh {
+namespace k {
+bool kmeans_supported(int D, int K);
+// acc[K*(D+1)] (fp64, zeroed by the caller) += per-cluster coordinate sums and counts
+void kmeans_assign_accumulate(const float* pts, int64_t n, int D, const float* cen, int K, double* acc,
+                              hipStream_t s);
+}  // namespace k
+}  // namespace mrh
