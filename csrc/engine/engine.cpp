@@ -655,6 +655,12 @@ KV reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtyp
   }
   int w = 0;
   int dc = dtype_code(dtype, &w);
+  if (ns == 0) {  // nothing on this rank (e.g. after a shuffle): an empty result of the requested width
+    out.vdata = at::empty({0}, opt(dev, at::kByte));
+    out.voff = at::Tensor();
+    out.vw = w;
+    return out;
+  }
   if (kmv.vw != w) fail("reduce " + op + ": values are not fixed-width " + dtype);
   int opc = op == "sum" ? 0 : op == "min" ? 1 : op == "max" ? 2 : -1;
   if (opc < 0) fail("unknown builtin reduce op " + op);

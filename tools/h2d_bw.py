@@ -23,3 +23,16 @@ for r in range(3):
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t) / 3
 print(f"D2H: {n / dt / 1e9:.1f} GB/s")
+# the same GiB split over several copy streams (several SDMA engines in flight)
+for ns in (2, 4):
+    streams = [torch.cuda.Stream() for _ in range(ns)]
+    part = n // ns
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for r in range(3):
+        for i, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                d[i * part:(i + 1) * part].copy_(h[i * part:(i + 1) * part], non_blocking=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / 3
+    print(f"H2D {ns} streams: {n / dt / 1e9:.1f} GB/s ({dt * 1e3:.2f} ms per GiB)")
