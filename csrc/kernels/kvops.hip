@@ -110,6 +110,9 @@ __global__ __launch_bounds__(NT) void k_compact_heads(const uint32_t* __restrict
   if (i == 0) seg[pos[n]] = n;
 }
 
+// 16 lanes per pair: each group compares one non-head key with its segment
+// head, 4 bytes per lane per step, so a ~64-byte URL is two coalesced 64-byte
+// reads instead of one lane walking both keys with unaligned 8-byte loads
 __global__ __launch_bounds__(NT) void k_verify_var(const uint8_t* __restrict__ kd,
                                                   const int64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ perm,
@@ -117,12 +120,27 @@ __global__ __launch_bounds__(NT) void k_verify_var(const uint8_t* __restrict__ k
                                                   const uint32_t* __restrict__ pos,
                                                   const int64_t* __restrict__ seg, int64_t n,
                                                   unsigned long long* mism) {
-  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (i >= n || flags[i]) return;
-  int64_t h = seg[pos[i] - 1];
-  uint32_t a = perm[i], b = perm[h];
-  int64_t a0 = off[a], la = off[a + 1] - a0, b0 = off[b], lb = off[b + 1] - b0;
-  if (la != lb || !dev::bytes_equal(kd + a0, kd + b0, la)) atomicAdd(mism, 1ull);
+  const int g = threadIdx.x & 15;
+  const int gbase = (threadIdx.x & 63) & ~15;
+  int64_t row = ((int64_t)blockIdx.x * NT + threadIdx.x) >> 4;
+  const int64_t stride = ((int64_t)gridDim.x * NT) >> 4;
+  int64_t bad = 0;
+  for (; row < n; row += stride) {  // row is uniform within a 16-lane group
+    if (flags[row]) continue;
+    const int64_t h = seg[pos[row] - 1];
+    const uint32_t a = perm[row], b = perm[h];
+    const int64_t a0 = off[a], la = off[a + 1] - a0, b0 = off[b], lb = off[b + 1] - b0;
+    bool diff = la != lb;
+    if (!diff) {
+      for (int64_t j = 4 * g; j < la; j += 64) {
+        const int64_t e = la - j < 4 ? la - j : 4;
+        for (int64_t t = 0; t < e; ++t) diff |= kd[a0 + j + t] != kd[b0 + j + t];
+      }
+    }
+    const unsigned long long m = __ballot(diff);
+    if (g == 0 && ((m >> gbase) & 0xffffull)) ++bad;
+  }
+  if (bad) atomicAdd(mism, (unsigned long long)bad);
 }
 
 __global__ __launch_bounds__(NT) void k_verify_fixed(const uint8_t* __restrict__ kd, int kw,
@@ -233,7 +251,9 @@ void verify_groups_var(const uint8_t* kdata, const int64_t* koff, const uint32_t
                        const uint32_t* pos, const int64_t* seg, int64_t n, unsigned long long* mism,
                        hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_verify_var, dim3(nblk(n)), dim3(NT), 0, s, kdata, koff, perm, flags, pos, seg, n,
+  int64_t g = (n * 16 + NT - 1) / NT;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(k_verify_var, dim3((unsigned)g), dim3(NT), 0, s, kdata, koff, perm, flags, pos, seg, n,
                      mism);
   MRH_CHECK_LAUNCH();
 }
