@@ -133,6 +133,31 @@ void check_kmv(const KMV& kmv, const char* op) {
   check_col(kmv.vdata, kmv.voff, kmv.vw, kmv.nval, op, "multivalue");
 }
 
+bool trace_enabled() {
+  static const bool on = std::getenv("MRH_TRACE") && *std::getenv("MRH_TRACE");
+  return on;
+}
+
+void trace_op(int rank, const char* op, int instance, int depth, double t0, double ms, int64_t nkv, int64_t nkmv,
+              int64_t bytes, int64_t sent, int64_t recv) {
+  static std::FILE* f = nullptr;
+  static int frank = -1;
+  std::lock_guard<std::mutex> l(g_mu);
+  if (!f || frank != rank) {
+    if (f) std::fclose(f);
+    const std::string p = std::string(std::getenv("MRH_TRACE")) + "." + std::to_string(rank);
+    f = std::fopen(p.c_str(), "a");
+    frank = rank;
+    if (!f) return;
+  }
+  std::fprintf(f,
+               "{\"op\": \"%s\", \"instance\": %d, \"depth\": %d, \"t0\": %.6f, \"ms\": %.4f, \"kv\": %lld, "
+               "\"kmv\": %lld, \"bytes\": %lld, \"sent\": %lld, \"recv\": %lld}\n",
+               op, instance, depth, t0, ms, (long long)nkv, (long long)nkmv, (long long)bytes, (long long)sent,
+               (long long)recv);
+  std::fflush(f);
+}
+
 void register_mr(MapReduce* mr) {
   std::lock_guard<std::mutex> l(g_mu);
   live().insert(mr);

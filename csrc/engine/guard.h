@@ -50,6 +50,13 @@ bool check_enabled();
 void check_kv(const KV& kv, const char* op);
 void check_kmv(const KMV& kmv, const char* op);
 
+// op trace (MRH_TRACE=path): one JSON line per MapReduce op to path.<rank>
+// {"op","instance","depth","t0","ms","kv","kmv","bytes","sent","recv"}; device
+// work is synchronised at op boundaries while tracing (diagnostic mode)
+bool trace_enabled();
+void trace_op(int rank, const char* op, int instance, int depth, double t0, double ms, int64_t nkv, int64_t nkmv,
+              int64_t bytes, int64_t sent, int64_t recv);
+
 // live MapReduce objects (for spill-on-OOM)
 void register_mr(MapReduce* mr);
 void unregister_mr(MapReduce* mr);

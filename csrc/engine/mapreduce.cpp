@@ -3,6 +3,7 @@
 #include "mapreduce.h"
 #include "guard.h"
 
+#include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
@@ -40,9 +41,37 @@ namespace {
 // On scope exit (after the op's return value is computed) an MR with
 // outofcore == 1 writes its data to disk — the reference's forced
 // out-of-core mode (src/keyvalue.cpp:122,223); the next op reads it back.
+//
+// With MRH_TRACE set, every op also appends a JSON line (guard.h trace_op):
+// wall time with the device synchronised at both ends, local pair counts and
+// bytes, and the bytes this rank sent/received in shuffles during the op.
+thread_local int g_op_depth = 0;
+void device_sync(const MapReduce* mr) {
+  if (mr->device().is_cuda()) (void)hipDeviceSynchronize();
+}
 struct OpTrace {
-  OpTrace(const char* name, MapReduce* mr) : mr_(mr) { roctxRangePushA(name); }
+  OpTrace(const char* name, MapReduce* mr) : mr_(mr), name_(name) {
+    roctxRangePushA(name);
+    if (guard::trace_enabled()) {
+      device_sync(mr);
+      t0_ = Comm::wtime();
+      s0_ = MapReduce::cssize.load();
+      r0_ = MapReduce::crsize.load();
+    }
+    ++g_op_depth;
+  }
   ~OpTrace() {
+    --g_op_depth;
+    if (guard::trace_enabled() && std::uncaught_exceptions() == 0) {
+      device_sync(mr_);
+      const double t1 = Comm::wtime();
+      int64_t b = 0;
+      if (mr_->kv) b += mr_->kv->nbytes();
+      if (mr_->kmv) b += mr_->kmv->nbytes();
+      guard::trace_op(mr_->my_proc(), name_, mr_->instance(), g_op_depth, t0_, (t1 - t0_) * 1e3,
+                      mr_->kv ? mr_->kv->n : 0, mr_->kmv ? mr_->kmv->nkey : 0, b, MapReduce::cssize.load() - s0_,
+                      MapReduce::crsize.load() - r0_);
+    }
     if (mr_->set.outofcore == 1 && std::uncaught_exceptions() == 0) {
       try {
         mr_->spill_disk();
@@ -53,6 +82,9 @@ struct OpTrace {
     roctxRangePop();
   }
   MapReduce* mr_;
+  const char* name_;
+  double t0_ = 0;
+  int64_t s0_ = 0, r0_ = 0;
 };
 
 [[noreturn]] void fail(const std::string& m) { throw std::runtime_error(m); }

@@ -146,6 +146,7 @@ class MapReduce {
   const CommPtr& comm() const { return comm_; }
   int my_proc() const { return comm_->rank(); }
   int num_procs() const { return comm_->size(); }
+  int instance() const { return instance_me_; }
   at::Device device() const { return comm_->device(); }
 
   // ---------------------------------------------------------------- static counters

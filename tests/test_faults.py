@@ -126,3 +126,34 @@ def test_host_asan_clean():
     r = subprocess.run(["bash", os.path.join(ROOT, "tools", "asan_check.sh")], capture_output=True, text=True,
                        timeout=1800)
     assert r.returncode == 0 and "ASAN CLEAN" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_op_trace_two_ranks(tmp_path):
+    """MRH_TRACE: every MapReduce op of every rank is one JSON line; the
+    summary tool groups them into the reference's stages"""
+    import importlib.util
+    exe = _cc(os.path.join(ROOT, "examples", "c", "cwordfreq.c"), tmp_path / "cwordfreq")
+    _docs(tmp_path / "docs")
+    port = _port()
+    procs = []
+    for r in range(2):
+        env = dict(ENV0, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HIP_VISIBLE_DEVICES="", MRH_TRACE=str(tmp_path / "trace"))
+        procs.append(subprocess.Popen([exe, "docs"], cwd=tmp_path, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    for p in procs:
+        p.communicate(timeout=120)
+        assert p.returncode == 0
+    spec = importlib.util.spec_from_file_location("trace_summary", os.path.join(ROOT, "tools", "trace_summary.py"))
+    ts = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ts)
+    recs = ts.load(str(tmp_path / "trace"))
+    assert {r["rank"] for r in recs} == {0, 1}
+    ops = {r["op"] for r in recs}
+    assert {"map_file", "collate", "aggregate", "convert", "reduce", "gather", "sort_values"} <= ops
+    # collate is traced with its nested aggregate + convert one level deeper
+    col = [r for r in recs if r["op"] == "collate" and r["rank"] == 0][0]
+    assert any(r["op"] == "aggregate" and r["depth"] == col["depth"] + 1 for r in recs)
+    assert sum(r["sent"] for r in recs if r["op"] == "aggregate") > 0
+    s = ts.summarise(recs)
+    assert {"Map", "Network I/O", "Sort/Hash", "Reduce"} <= set(s["stages_ms"])
