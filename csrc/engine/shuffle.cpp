@@ -167,6 +167,71 @@ at::Tensor partition_dest(const KV& kv, int P, at::Tensor* counts) {
   return dest;
 }
 
+// Exchange protocol (2 host round trips, then the payload streams):
+//  1. local stable radix pass on the destination rank -> P contiguous buckets;
+//  2. ONE int64 all-to-all of a [P x 5] header {pairs, key bytes, value bytes,
+//     key width code, value width code}: every rank learns what it will
+//     receive AND every rank's layout, so all ranks derive the same global
+//     layout locally (no separate layout allreduce, no per-column count
+//     exchanges);
+//  3. the 2-4 column all-to-alls (key lengths, key bytes, value lengths, value
+//     bytes) are issued back to back as async works and waited once: on RCCL
+//     they queue on the communicator's stream while this rank's stream goes on
+//     (offset scans of the received lengths wait only on their own column).
+namespace {
+constexpr int64_t kEmpty = -2;  // width code of a rank with no pairs
+
+int global_width(const std::vector<int64_t>& codes) {
+  int64_t w = kEmpty;
+  for (int64_t c : codes) {
+    if (c == kEmpty) continue;
+    if (w == kEmpty) w = c;
+    else if (w != c) return -1;
+  }
+  return (int)w;  // kEmpty if every rank is empty
+}
+
+struct Pending {
+  at::Tensor out;
+  c10::intrusive_ptr<c10d::Work> work;
+};
+
+Pending alltoallv_async(const at::Tensor& in, std::vector<int64_t> send, std::vector<int64_t> recv, const PG& pg) {
+  int64_t tot = 0;
+  for (auto r : recv) tot += r;
+  Pending p;
+  p.out = at::empty({tot}, in.options());
+  at::Tensor inc = in.contiguous();
+  p.work = pg->alltoall_base(p.out, inc, recv, send);
+  return p;
+}
+
+at::Tensor lengths_of(const at::Tensor& off, int64_t n, at::Device dev) {
+  at::Tensor len = at::empty({n}, opt(dev, at::kInt));
+  if (dev.is_cuda()) {
+    if (n) k::offsets_to_lengths(P0<int64_t>(off), n, P0<int32_t>(len), cur_stream());
+  } else if (n) {
+    len.copy_((off.narrow(0, 1, n) - off.narrow(0, 0, n)).to(at::kInt));
+  }
+  return len;
+}
+
+// per-destination byte totals of one column of a bucket-sorted KV
+std::vector<int64_t> bucket_bytes(const at::Tensor& off, int w, const std::vector<int64_t>& counts, at::Device dev) {
+  const int P = (int)counts.size();
+  std::vector<int64_t> out(P, 0);
+  if (w >= 0) {
+    for (int i = 0; i < P; ++i) out[i] = counts[i] * w;
+    return out;
+  }
+  std::vector<int64_t> cum(P + 1, 0);
+  for (int i = 0; i < P; ++i) cum[i + 1] = cum[i] + counts[i];
+  std::vector<int64_t> b = to_vec(off.index_select(0, at::tensor(cum, opt(at::kCPU, at::kLong)).to(dev)));
+  for (int i = 0; i < P; ++i) out[i] = b[i + 1] - b[i];
+  return out;
+}
+}  // namespace
+
 KV exchange(const KV& kv_in, const at::Tensor& dest, const PG& pg, ShuffleStats* st) {
   auto t0 = std::chrono::steady_clock::now();
   const at::Device dev = kv_in.device();
@@ -175,39 +240,83 @@ KV exchange(const KV& kv_in, const at::Tensor& dest, const PG& pg, ShuffleStats*
     return kv_in;
   }
   const int P = pg->getSize();
-  auto [kw, vw] = agree_layout(kv_in, pg);
-  KV kv = with_layout(kv_in, kw, vw);
-  // stable bucket sort by destination (one radix pass for P <= 256)
-  at::Tensor counts;
-  KV sorted = kv;
-  if (kv.n) {
-    at::Tensor dk = dest.to(at::kLong);
-    at::Tensor iota = at::arange(kv.n, opt(dev, at::kInt));
+  // 1. bucket by destination (stable: one radix pass for P <= 256)
+  KV sorted = kv_in;
+  at::Tensor counts_t;
+  if (kv_in.n) {
+    at::Tensor iota = at::arange(kv_in.n, opt(dev, at::kInt));
     int bits = 8;
     while ((1 << bits) < P) bits += 8;
-    auto [ks, perm, passes] = radix_sort_pairs(dk, iota, 0, bits);
-    sorted = gather(kv, perm);
-    counts = at::bincount(dest.to(at::kLong), {}, P);
+    auto [ks, perm, passes] = radix_sort_pairs(dest.to(at::kLong), iota, 0, bits);
+    sorted = gather(kv_in, perm);
+    counts_t = at::bincount(dest.to(at::kLong), {}, P).to(at::kLong);
   } else {
-    counts = at::zeros({P}, opt(dev, at::kLong));
+    counts_t = at::zeros({P}, opt(dev, at::kLong));
   }
-  counts = counts.to(at::kLong);
-  std::vector<int64_t> ones(P, 1);
-  at::Tensor rcounts_t = alltoallv(counts.to(dev), ones, ones, pg);
-  std::vector<int64_t> scount = to_vec(counts), rcount = to_vec(rcounts_t);
-  int64_t n_recv = 0;
-  for (auto c : rcount) n_recv += c;
+  std::vector<int64_t> scount = to_vec(counts_t);
+  const int64_t kcode = kv_in.n ? kv_in.kw : kEmpty, vcode = kv_in.n ? kv_in.vw : kEmpty;
+  std::vector<int64_t> skb = bucket_bytes(sorted.koff, sorted.kw, scount, dev);
+  std::vector<int64_t> svb = bucket_bytes(sorted.voff, sorted.vw, scount, dev);
+  // 2. one header all-to-all
+  std::vector<int64_t> hdr(5 * P);
+  for (int i = 0; i < P; ++i) {
+    hdr[5 * i + 0] = scount[i];
+    hdr[5 * i + 1] = skb[i];
+    hdr[5 * i + 2] = svb[i];
+    hdr[5 * i + 3] = kcode;
+    hdr[5 * i + 4] = vcode;
+  }
+  std::vector<int64_t> fives(P, 5);
+  std::vector<int64_t> rh = to_vec(alltoallv(at::tensor(hdr, opt(at::kCPU, at::kLong)).to(dev), fives, fives, pg));
+  std::vector<int64_t> rcount(P), rkb(P), rvb(P), kcodes(P), vcodes(P);
+  int64_t n_recv = 0, sb = 0, rb = 0;
+  for (int i = 0; i < P; ++i) {
+    rcount[i] = rh[5 * i];
+    rkb[i] = rh[5 * i + 1];
+    rvb[i] = rh[5 * i + 2];
+    kcodes[i] = rh[5 * i + 3];
+    vcodes[i] = rh[5 * i + 4];
+    n_recv += rcount[i];
+    sb += skb[i] + svb[i];
+    rb += rkb[i] + rvb[i];
+  }
+  int kw = global_width(kcodes), vw = global_width(vcodes);
+  if (kw == kEmpty) kw = kv_in.kw;  // nobody has pairs: keep the local layout
+  if (vw == kEmpty) vw = kv_in.vw;
+  if (kw < 0 && sorted.kfixed()) sorted = to_var_keys(sorted);  // same bytes, now with offsets
+  if (vw < 0 && sorted.vfixed()) sorted = to_var_values(sorted);
+  // 3. payload: every column all-to-all in flight before the first wait
+  const int64_t n = kv_in.n;
+  std::vector<Pending> q;
+  int klen_i = -1, vlen_i = -1;
+  if (kw < 0) {
+    klen_i = (int)q.size();
+    q.push_back(alltoallv_async(lengths_of(sorted.koff, n, dev), scount, rcount, pg));
+  }
+  // a column that is fixed-width 0 on every rank (e.g. MR-MPI NULL values) moves nothing
+  const int kd_i = kw == 0 ? -1 : (int)q.size();
+  if (kw != 0)
+    q.push_back(alltoallv_async(sorted.kdata.defined() ? sorted.kdata : at::empty({0}, opt(dev, at::kByte)), skb,
+                                rkb, pg));
+  if (vw < 0) {
+    vlen_i = (int)q.size();
+    q.push_back(alltoallv_async(lengths_of(sorted.voff, n, dev), scount, rcount, pg));
+  }
+  const int vd_i = vw == 0 ? -1 : (int)q.size();
+  if (vw != 0)
+    q.push_back(alltoallv_async(sorted.vdata.defined() ? sorted.vdata : at::empty({0}, opt(dev, at::kByte)), svb,
+                                rvb, pg));
+  for (auto& p : q) p.work->wait();
   KV out;
   out.n = n_recv;
   out.kw = kw;
   out.vw = vw;
-  int64_t sb = 0, rb = 0;
-  exchange_col(sorted.kdata, sorted.koff, kw, scount, rcount, n_recv, pg, &out.kdata, &out.koff, &sb, &rb);
-  exchange_col(sorted.vdata, sorted.voff, vw, scount, rcount, n_recv, pg, &out.vdata, &out.voff, &sb, &rb);
-  if (kw < 0 && !out.koff.defined()) out.koff = at::zeros({1}, opt(dev, at::kLong));
-  if (vw < 0 && !out.voff.defined()) out.voff = at::zeros({1}, opt(dev, at::kLong));
+  out.kdata = kd_i >= 0 ? q[kd_i].out : at::empty({0}, opt(dev, at::kByte));
+  out.vdata = vd_i >= 0 ? q[vd_i].out : at::empty({0}, opt(dev, at::kByte));
+  if (kw < 0) out.koff = exclusive_scan(q[klen_i].out);
+  if (vw < 0) out.voff = exclusive_scan(q[vlen_i].out);
   if (st) {
-    st->send_pairs += kv.n;
+    st->send_pairs += n;
     st->recv_pairs += n_recv;
     st->send_bytes += sb;
     st->recv_bytes += rb;
