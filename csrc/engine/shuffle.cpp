@@ -8,13 +8,12 @@
 //  * one stable device-side partition (radix pass on the destination rank)
 //    turns the KV into P contiguous buckets, so the send buffers ARE the
 //    sorted columns: no pack loop, no per-KV memcpy;
-//  * counts are exchanged once as an int64 [P] all-to-all (replaces the
-//    Alltoall + Reduce_scatter + 3 Allreduce of Irregular::setup);
+//  * pair counts, byte totals and layouts travel in ONE int64 [P x 5] header
+//    all-to-all (replaces the Alltoall + Reduce_scatter + 3 Allreduce of
+//    Irregular::setup); a rank with an empty KV never forces a conversion;
 //  * the payload moves as at most 4 column all-to-alls (key lengths, key
-//    bytes, value lengths, value bytes) with 64-bit byte counts, so there is
-//    no INTMAX limit and no 0.9x scale-back retry loop;
-//  * layouts (fixed vs variable width) are agreed with one tiny allreduce so a
-//    rank with an empty KV never forces a conversion.
+//    bytes, value lengths, value bytes), all in flight before one wait, with
+//    64-bit byte counts: no INTMAX limit and no 0.9x scale-back retry loop.
 #include <torch/csrc/distributed/c10d/Types.hpp>
 
 #include <chrono>
