@@ -181,6 +181,80 @@ __global__ __launch_bounds__(BNT) void k_kmeans_batch(const float* __restrict__ 
     if (part[i] != 0.f) atomicAdd(&acc[i], (double)part[i]);
 }
 
+// Register-accumulator variant (opt-in, MRH_KMEANS_KERNEL=4; K <= KM = 32,
+// D <= 3) — an experiment kept for reference: PMC counters showed the
+// batched kernel's waves spending ~60 % of their cycles waiting on LDS
+// (SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES) — the per-point LDS float atomics on a
+// few hot cluster addresses. Here each lane keeps K x (D+1) running sums in
+// VGPRs (a predicated FMA per cluster per point, no memory traffic), walks
+// ~128 points grid-stride, and only at the end folds its registers with one
+// fp64 wave reduction per accumulator + one global atomic per wave: 8192
+// points per wave share each atomic instead of one LDS atomic per point.
+constexpr int RNT = 256;
+template <int D, int KM>
+__global__ __launch_bounds__(RNT) void k_kmeans_reg(const float* __restrict__ pts, int64_t n,
+                                                   const float* __restrict__ cen, int K, double* __restrict__ acc) {
+  static_assert(D <= 3, "one float4 per centroid");
+  __shared__ float4 c4[KM];
+  for (int kk = threadIdx.x; kk < KM; kk += RNT) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    float cc = 0.f;
+    if (kk < K) {
+      for (int d = 0; d < D; ++d) {
+        const float cd = cen[kk * D + d];
+        v[d] = -2.f * cd;
+        cc = fmaf(cd, cd, cc);
+      }
+      v[3] = cc;
+    } else {
+      v[3] = FLT_MAX;  // padding centroids never win
+    }
+    c4[kk] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  __syncthreads();
+  float a[KM][D + 1];
+#pragma unroll
+  for (int kk = 0; kk < KM; ++kk)
+#pragma unroll
+    for (int d = 0; d <= D; ++d) a[kk][d] = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * RNT;
+  for (int64_t i = (int64_t)blockIdx.x * RNT + threadIdx.x; i < n; i += stride) {
+    float x[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) x[d] = pts[i * D + d];
+    float best = FLT_MAX;
+    int bk = 0;
+#pragma unroll
+    for (int kk = 0; kk < KM; ++kk) {
+      const float4 c = c4[kk];
+      float sc = c.w;
+      sc = fmaf(x[0], c.x, sc);
+      if (D > 1) sc = fmaf(x[1], c.y, sc);
+      if (D > 2) sc = fmaf(x[2], c.z, sc);
+      const bool lt = sc < best;
+      best = lt ? sc : best;
+      bk = lt ? kk : bk;
+    }
+#pragma unroll
+    for (int kk = 0; kk < KM; ++kk) {
+      const float m = kk == bk ? 1.f : 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) a[kk][d] = fmaf(m, x[d], a[kk][d]);
+      a[kk][D] += m;
+    }
+  }
+  // fold in fp64 (per-lane fp32 sums cover only ~128 points): one wave
+  // reduction per accumulator, one fp64 global atomic per wave
+  const int lane = dev::lane_id();
+#pragma unroll
+  for (int kk = 0; kk < KM; ++kk)
+#pragma unroll
+    for (int d = 0; d <= D; ++d) {
+      const double v = dev::wave_sum((double)a[kk][d]);
+      if (lane == 0 && kk < K && v != 0.0) atomicAdd(&acc[kk * (D + 1) + d], v);
+    }
+}
+
 template <int D>
 void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, hipStream_t s) {
   static const int variant = [] {
@@ -188,7 +262,18 @@ void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, h
     return e ? std::atoi(e) : 0;
   }();
   if constexpr (D <= 3) {
-    if (variant == 0 && (size_t)K * (4 + D + 1) * 4 <= 64 * 1024) {
+    // MRH_KMEANS_KERNEL=4: the register-accumulator kernel. Measured slower
+    // (26.0 vs 15.8 ms per 20 iterations, profiles/r1_kmeans_variants.txt):
+    // its 128 predicated FMAs per point cost more than the LDS-atomic waits
+    // they remove, so the batched kernel stays the default.
+    if (variant == 4 && K <= 32) {
+      int64_t nb = (n + RNT - 1) / RNT;
+      if (nb > 1024) nb = 1024;  // ~128 points per lane at 32 M points
+      hipLaunchKernelGGL((k_kmeans_reg<D, 32>), dim3((unsigned)nb), dim3(RNT), 0, s, pts, n, cen, K, acc);
+      MRH_CHECK_LAUNCH();
+      return;
+    }
+    if (variant != 1 && (size_t)K * (4 + D + 1) * 4 <= 64 * 1024) {
       const int64_t nb = (n + (int64_t)BNT * PB - 1) / ((int64_t)BNT * PB);
       const size_t lds = sizeof(float) * (size_t)K * (4 + D + 1);
       hipLaunchKernelGGL((k_kmeans_batch<D>), dim3((unsigned)nb), dim3(BNT), lds, s, pts, n, cen, K, acc);

@@ -72,4 +72,7 @@ def test_kmeans_job_gpu_matches_cpu():
     for _ in range(5):
         cpu.iterate()
         gpu.iterate()
-    np.testing.assert_allclose(gpu.centroids.cpu().double().numpy(), cpu.centroids.double().numpy(), atol=1e-4)
+    # the engines score ||c||^2 - 2 x.c in different fp32 orders, so a point
+    # within rounding of two centroids may go either way (each such point
+    # moves a centroid by ~1e-5 here)
+    np.testing.assert_allclose(gpu.centroids.cpu().double().numpy(), cpu.centroids.double().numpy(), atol=5e-4)
