@@ -369,6 +369,7 @@ uint64_t MapReduce::close() {  // :658-672
   if (!open_) fail("Cannot close MapReduce that is not open");
   KV n = open_->finish();
   open_.reset();
+  if (open_add_) ensure_resident();  // appending to data that was spilled to disk
   if (open_add_ && kv) kv = concat({*kv, n}, device());
   else kv = n;
   stats("Close", 0);
