@@ -540,11 +540,9 @@ KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits) {
       const int64_t* off = kv.kfixed() ? nullptr : P0<int64_t>(kv.koff);
       const uint32_t* pp = P0<uint32_t>(perm);
       const uint32_t* f = P0<uint32_t>(flags);
-      const uint32_t* ps = P0<uint32_t>(pos);
-      const int64_t* sg = P0<int64_t>(seg);
       for (int64_t i = 0; i < n; ++i) {
         if (f[i]) continue;
-        uint32_t a = pp[i], b = pp[sg[ps[i] - 1]];
+        uint32_t a = pp[i], b = pp[i - 1];  // sorted predecessor, same segment (as the device kernel)
         int64_t a0 = off ? off[a] : (int64_t)a * kv.kw, la = off ? off[a + 1] - a0 : kv.kw;
         int64_t b0 = off ? off[b] : (int64_t)b * kv.kw, lb = off ? off[b + 1] - b0 : kv.kw;
         if (la != lb || memcmp(d + a0, d + b0, la)) ++mism;

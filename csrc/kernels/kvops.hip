@@ -110,15 +110,17 @@ __global__ __launch_bounds__(NT) void k_compact_heads(const uint32_t* __restrict
   if (i == 0) seg[pos[n]] = n;
 }
 
-// 16 lanes per pair: each group compares one non-head key with its segment
-// head, 4 bytes per lane per step, so a ~64-byte URL is two coalesced 64-byte
-// reads instead of one lane walking both keys with unaligned 8-byte loads
+// 16 lanes per pair: each group compares one non-head key with its sorted
+// predecessor (same segment, so equality along the chain = equality with the
+// head; the count is > 0 iff some segment mixes keys). The predecessor's perm
+// entry sits next to the row's own, so the dependent-load chain is
+// perm -> off -> bytes (3 levels, not pos -> seg -> perm -> off -> bytes).
+// Bytes: 4 per lane per step via aligned dword loads + v_alignbyte (ld32u), so
+// a ~64-byte URL is one 64-byte sweep per key; the < 4-byte tail uses bytes.
 __global__ __launch_bounds__(NT) void k_verify_var(const uint8_t* __restrict__ kd,
                                                   const int64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ perm,
-                                                  const uint32_t* __restrict__ flags,
-                                                  const uint32_t* __restrict__ pos,
-                                                  const int64_t* __restrict__ seg, int64_t n,
+                                                  const uint32_t* __restrict__ flags, int64_t n,
                                                   unsigned long long* mism) {
   const int g = threadIdx.x & 15;
   const int gbase = (threadIdx.x & 63) & ~15;
@@ -126,15 +128,17 @@ __global__ __launch_bounds__(NT) void k_verify_var(const uint8_t* __restrict__ k
   const int64_t stride = ((int64_t)gridDim.x * NT) >> 4;
   int64_t bad = 0;
   for (; row < n; row += stride) {  // row is uniform within a 16-lane group
-    if (flags[row]) continue;
-    const int64_t h = seg[pos[row] - 1];
-    const uint32_t a = perm[row], b = perm[h];
+    if (flags[row]) continue;       // row 0 is always a head, so row - 1 >= 0
+    const uint32_t a = perm[row], b = perm[row - 1];
     const int64_t a0 = off[a], la = off[a + 1] - a0, b0 = off[b], lb = off[b + 1] - b0;
     bool diff = la != lb;
     if (!diff) {
       for (int64_t j = 4 * g; j < la; j += 64) {
-        const int64_t e = la - j < 4 ? la - j : 4;
-        for (int64_t t = 0; t < e; ++t) diff |= kd[a0 + j + t] != kd[b0 + j + t];
+        if (la - j >= 4) {
+          diff |= dev::ld32u(kd + a0 + j) != dev::ld32u(kd + b0 + j);
+        } else {
+          for (int64_t t = j; t < la; ++t) diff |= kd[a0 + t] != kd[b0 + t];
+        }
       }
     }
     const unsigned long long m = __ballot(diff);
@@ -151,9 +155,8 @@ __global__ __launch_bounds__(NT) void k_verify_fixed(const uint8_t* __restrict__
                                                     unsigned long long* mism) {
   int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n || flags[i]) return;
-  int64_t h = seg[pos[i] - 1];
   const uint8_t* pa = kd + (int64_t)perm[i] * kw;
-  const uint8_t* pb = kd + (int64_t)perm[h] * kw;
+  const uint8_t* pb = kd + (int64_t)perm[i - 1] * kw;  // sorted predecessor, as k_verify_var
   bool diff = false;
   for (int j = 0; !diff && j < kw; ++j) diff = pa[j] != pb[j];
   if (diff) atomicAdd(mism, 1ull);
@@ -253,8 +256,7 @@ void verify_groups_var(const uint8_t* kdata, const int64_t* koff, const uint32_t
   if (n <= 0) return;
   int64_t g = (n * 16 + NT - 1) / NT;
   if (g > 65536) g = 65536;
-  hipLaunchKernelGGL(k_verify_var, dim3((unsigned)g), dim3(NT), 0, s, kdata, koff, perm, flags, pos, seg, n,
-                     mism);
+  hipLaunchKernelGGL(k_verify_var, dim3((unsigned)g), dim3(NT), 0, s, kdata, koff, perm, flags, n, mism);
   MRH_CHECK_LAUNCH();
 }
 void verify_groups_fixed(const uint8_t* kdata, int kw, const uint32_t* perm, const uint32_t* flags,
