@@ -3,19 +3,39 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include "hashfn.h"
 
 #define MRH_WAVE 64
 
-#define MRH_CHECK_LAUNCH()                                                       \
-  do {                                                                           \
-    hipError_t e__ = hipGetLastError();                                          \
-    if (e__ != hipSuccess) {                                                     \
-      fprintf(stderr, "mrhip kernel launch failed: %s at %s:%d\n",               \
-              hipGetErrorString(e__), __FILE__, __LINE__);                       \
-      abort();                                                                   \
-    }                                                                            \
-  } while (0)
+namespace mrh {
+namespace k {
+// Serialize mode (SURVEY.md §5 "race detection"): MRH_SYNC=1 synchronises the
+// device after every launch, so an asynchronous fault, or a kernel racing a
+// later one on another stream, is reported at the launch site (file:line)
+// instead of at some later sync. Diagnostic only: it removes all overlap.
+inline bool sync_mode() {
+  static const bool on = [] {
+    const char* v = std::getenv("MRH_SYNC");
+    return v && *v && *v != '0';
+  }();
+  return on;
+}
+inline void check_launch(const char* file, int line) {
+  hipError_t e = hipGetLastError();
+  const bool launched = e == hipSuccess;
+  if (launched && sync_mode()) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "mrhip kernel %s: %s at %s:%d\n", launched ? "execution failed" : "launch failed",
+                 hipGetErrorString(e), file, line);
+    std::abort();
+  }
+}
+}  // namespace k
+}  // namespace mrh
+
+#define MRH_CHECK_LAUNCH() ::mrh::k::check_launch(__FILE__, __LINE__)
 
 namespace mrh {
 namespace dev {

@@ -90,6 +90,33 @@ def test_collate_wordcount(world):
     assert total == collections.Counter(WORDS)
 
 
+def case_shuffle_determinism(comm):
+    """SURVEY.md §5 "deterministic-order checks for the shuffle": the same job
+    run twice must give byte-identical KV and KMV sequences, in order, on every
+    rank (stable partition, rank-ordered receive, stable sort)."""
+    import gpu_mapreduce_amd as g
+    rng = [(comm.rank * 7919 + j * 104729) % 613 for j in range(3000)]
+
+    def job():
+        mr = g.MapReduce(comm)
+        mr.map(comm.size, lambda i, kv: [kv.add(b"key%d" % (x % 211), struct.pack("<ii", i, x)) for x in rng])
+        mr.aggregate()
+        kv = list(mr.kv_pairs())
+        mr.convert()
+        kmv = [(k, list(v)) for k, v in mr.kmv_pairs()]
+        return kv, kmv
+
+    a, b = job(), job()
+    return a == b, len(a[0]), len(a[1])
+
+
+def test_shuffle_is_deterministic():
+    out = run_world("case_shuffle_determinism", 3)
+    assert all(same for same, _, _ in out.values()), out
+    assert sum(n for _, n, _ in out.values()) == 3 * 3000
+    assert sum(u for _, _, u in out.values()) == 211
+
+
 def case_fixed_and_var_mixed(comm):
     """rank 0 emits fixed-width keys, others variable + one empty rank."""
     import gpu_mapreduce_amd as g

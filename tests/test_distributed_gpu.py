@@ -60,3 +60,10 @@ def test_pagerank_gpu_two_ranks():
     for r in range(2):
         got[out[r][1]] = out[r][2]
     np.testing.assert_allclose(got, ref, rtol=2e-4, atol=1e-9)
+
+
+def test_shuffle_is_deterministic_gpu():
+    out = run_world("case_shuffle_determinism", 2, DEV)
+    assert all(same for same, _, _ in out.values()), out
+    assert sum(n for _, n, _ in out.values()) == 2 * 3000
+    assert sum(u for _, _, u in out.values()) == 211

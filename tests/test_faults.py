@@ -119,6 +119,28 @@ def test_oom_spill_retry_gpu():
     assert "OOM-RETRY-OK" in r.stdout and "spilled 1 MapReduce object(s)" in r.stderr
 
 
+@pytest.mark.gpu
+def test_serialize_mode_gpu():
+    """MRH_SYNC=1: every kernel launch is followed by a device sync (faults are
+    reported at their launch site); the job's results must not change."""
+    code = """
+    import collections, struct
+    import gpu_mapreduce_amd as g
+    words = ("a bb ccc a dddd bb a eeeee https://x.org/y " * 300).split()
+    mr = g.MapReduce(g.Comm(device="cuda:0"))
+    mr.map(3, lambda i, kv: [kv.add(w.encode() + b"\\0") for w in words[i::3]])
+    mr.collate()
+    mr.reduce("count")
+    mr.sort_values(-1)
+    got = {k[:-1].decode(): struct.unpack("<i", v)[0] for k, v in mr.kv_pairs()}
+    assert got == dict(collections.Counter(words)), got
+    print("SYNC-OK")
+    """
+    r = _py(code, {"MRH_SYNC": "1", "MRH_CHECK": "1"}, gpu=True)
+    assert r.returncode == 0, r.stderr
+    assert "SYNC-OK" in r.stdout
+
+
 @pytest.mark.skipif(os.environ.get("MRH_ASAN") != "1", reason="slow (rebuilds the host code with ASan); MRH_ASAN=1")
 def test_host_asan_clean():
     """host AddressSanitizer build of the engine + C API + OINK runs the C API
