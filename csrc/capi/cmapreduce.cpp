@@ -54,9 +54,12 @@ R guard(F&& f, R bad) {
   } catch (const std::exception& e) {
     g_err = e.what();
     if (g_mode) return bad;
+    // reference Error::one -> MPI_Abort (src/error.cpp:47-57): the whole job
+    // ends; peers are told through the communicator and fail within seconds
     std::fprintf(stderr, "ERROR: %s\n", e.what());
-    std::fflush(stderr);
-    std::abort();
+    std::fflush(nullptr);
+    if (g_world) g_world->poison(e.what());
+    std::_Exit(1);
   }
 }
 template <typename F>

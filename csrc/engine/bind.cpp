@@ -143,7 +143,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("recv_bytes", &ShuffleStats::recv_bytes)
       .def_readwrite("send_pairs", &ShuffleStats::send_pairs)
       .def_readwrite("recv_pairs", &ShuffleStats::recv_pairs)
-      .def_readwrite("seconds", &ShuffleStats::seconds);
+      .def_readwrite("seconds", &ShuffleStats::seconds)
+      .def_readwrite("rounds", &ShuffleStats::rounds);
 
   // native KeyValue builder (MR-MPI KeyValue::add and its multi variants)
   py::class_<WordCounter>(m, "WordCounter")
@@ -175,17 +176,29 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("device", [](const KeyValue& kv) { return kv.device().str(); });
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "NativeComm")
-      .def(py::init([](py::object pg, const std::string& dev, py::object store) {
+      .def(py::init([](py::object pg, const std::string& dev, py::object store, const std::string& transport) {
              c10::intrusive_ptr<c10d::Store> st;
              if (!store.is_none()) st = store.cast<c10::intrusive_ptr<c10d::Store>>();
              PG p = as_pg(pg);
+             py::gil_scoped_release nogil;  // RCCL bootstrap blocks until every rank arrives
              if (!p) return std::make_shared<Comm>(at::Device(dev));
-             return std::make_shared<Comm>(p, at::Device(dev), st);
+             return std::make_shared<Comm>(p, at::Device(dev), st, transport);
            }),
-           py::arg("pg"), py::arg("device"), py::arg("store") = py::none())
+           py::arg("pg"), py::arg("device"), py::arg("store") = py::none(), py::arg("transport") = "")
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("size", &Comm::size)
-      .def("barrier", &Comm::barrier);
+      .def_property_readonly("transport", &Comm::transport)
+      .def_property_readonly("distributed", &Comm::distributed)
+      .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce", [](const Comm& c, std::vector<int64_t> v, int op) { return c.allreduce(v, (Comm::Op)op); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("alltoall_counts", &Comm::alltoall_counts, py::call_guard<py::gil_scoped_release>())
+      .def("alltoallv", &Comm::alltoallv, py::call_guard<py::gil_scoped_release>())
+      .def("allgather_var", &Comm::allgather_var, py::call_guard<py::gil_scoped_release>())
+      .def("host_wait", &Comm::host_wait, py::call_guard<py::gil_scoped_release>())
+      .def("check_peers", &Comm::check_peers)
+      .def("poison", &Comm::poison)
+      .def("shutdown", &Comm::shutdown, py::call_guard<py::gil_scoped_release>());
 
   using MR = MapReduce;
   py::class_<MR>(m, "NativeMapReduce")
@@ -204,6 +217,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property("valuealign", [](MR& r) { return r.set.valuealign; },
                     [](MR& r, int v) { r.set.valuealign = v; })
       .def_property("fpath", [](MR& r) { return r.set.fpath; }, [](MR& r, const std::string& v) { r.set.fpath = v; })
+      .def_property("chunk_bytes", [](MR& r) { return r.set.chunk_bytes; },
+                    [](MR& r, int64_t v) { r.set.chunk_bytes = v; })
+      .def_property("hbm_budget", [](MR& r) { return r.set.hbm_budget; },
+                    [](MR& r, int64_t v) { r.set.hbm_budget = v; })
+      .def_property("host_budget", [](MR& r) { return r.set.host_budget; },
+                    [](MR& r, int64_t v) { r.set.host_budget = v; })
+      .def_property("streams", [](MR& r) { return r.set.streams; }, [](MR& r, int v) { r.set.streams = v; })
       .def_readwrite("mapfilecount", &MR::mapfilecount)
       .def_property(
           "kv", [](MR& r) -> py::object {
@@ -386,22 +406,43 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     at::Tensor d = partition_dest(kv, P, &c);
     return std::make_pair(d, c);
   });
-  m.def("exchange", [](const KV& kv, const at::Tensor& dest, py::object pg) {
-    ShuffleStats st;
-    KV r = exchange(kv, dest, as_pg(pg), &st);
-    return std::make_pair(r, st);
-  });
-  m.def("aggregate", [](const KV& kv, py::object pg) {
-    ShuffleStats st;
-    KV r = mrh::aggregate(kv, as_pg(pg), &st);
-    return std::make_pair(r, st);
-  });
-  m.def("gather_to", [](const KV& kv, int nprocs, py::object pg) {
-    ShuffleStats st;
-    KV r = gather_to(kv, nprocs, as_pg(pg), &st);
-    return std::make_pair(r, st);
-  });
-  m.def("broadcast", [](const KV& kv, int root, py::object pg) { return mrh::broadcast(kv, root, as_pg(pg)); });
+  auto xo = [](int64_t chunk, bool host_sink, int all2all) {
+    ExchangeOpts o;
+    o.chunk_bytes = chunk;
+    o.host_sink = host_sink;
+    o.all2all = all2all;
+    return o;
+  };
+  m.def(
+      "exchange",
+      [xo](const KV& kv, c10::optional<at::Tensor> dest, std::shared_ptr<Comm> c, int64_t chunk, bool host_sink,
+           int all2all) {
+        ShuffleStats st;
+        KV r = exchange(kv, dest ? *dest : at::Tensor(), *c, xo(chunk, host_sink, all2all), &st);
+        return std::make_pair(r, st);
+      },
+      py::arg("kv"), py::arg("dest"), py::arg("comm"), py::arg("chunk_bytes") = 0, py::arg("host_sink") = false,
+      py::arg("all2all") = 1, py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "aggregate",
+      [xo](const KV& kv, std::shared_ptr<Comm> c, int64_t chunk, bool host_sink, int all2all) {
+        ShuffleStats st;
+        KV r = mrh::aggregate(kv, *c, xo(chunk, host_sink, all2all), &st);
+        return std::make_pair(r, st);
+      },
+      py::arg("kv"), py::arg("comm"), py::arg("chunk_bytes") = 0, py::arg("host_sink") = false,
+      py::arg("all2all") = 1, py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "gather_to",
+      [](const KV& kv, int nprocs, std::shared_ptr<Comm> c) {
+        ShuffleStats st;
+        KV r = gather_to(kv, nprocs, *c, ExchangeOpts(), &st);
+        return std::make_pair(r, st);
+      },
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "broadcast", [](const KV& kv, int root, std::shared_ptr<Comm> c) { return mrh::broadcast(kv, root, *c); },
+      py::call_guard<py::gil_scoped_release>());
   m.def("map_urls", &map_urls);
   m.def("kmeans_map", &kmeans_map);
   m.def("map_words", &map_words);

@@ -1,23 +1,23 @@
-// Native communicator (see comm.h). Scalar collectives run on the engine
-// device: tiny RCCL all-reduces for the GPU engine (the same stream-ordered
-// path as the shuffle), gloo for the CPU engine.
-#define USE_C10D_NCCL 1
+// Native communicator (see comm.h).
 #include "comm.h"
-#include "guard.h"
-#include "storepg.h"
 
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 #include <torch/csrc/distributed/c10d/PrefixStore.hpp>
-#include <torch/csrc/distributed/c10d/ProcessGroupNCCL.hpp>
 #include <torch/csrc/distributed/c10d/TCPStore.hpp>
 #include <torch/csrc/distributed/c10d/Types.hpp>
 
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <thread>
+
+#include "guard.h"
+#include "storepg.h"
 
 namespace mrh {
 
@@ -26,27 +26,86 @@ int env_int(const char* k, int d) {
   const char* v = std::getenv(k);
   return v && *v ? std::atoi(v) : d;
 }
+bool force_rccl() { return env_int("MRH_FORCE_RCCL", 0) != 0; }
+
 c10d::ReduceOp::RedOpType red(Comm::Op op) {
   return op == Comm::SUM ? c10d::ReduceOp::SUM : op == Comm::MAX ? c10d::ReduceOp::MAX : c10d::ReduceOp::MIN;
 }
-void allreduce_t(const PG& pg, at::Tensor& t, Comm::Op op) {
+ncclRedOp_t nred(Comm::Op op) { return op == Comm::SUM ? ncclSum : op == Comm::MAX ? ncclMax : ncclMin; }
+ncclDataType_t ndt(at::ScalarType t) {
+  switch (t) {
+    case at::kLong: return ncclInt64;
+    case at::kInt: return ncclInt32;
+    case at::kDouble: return ncclFloat64;
+    case at::kFloat: return ncclFloat32;
+    case at::kByte: return ncclUint8;
+    default: throw std::runtime_error("mrhip: unsupported allreduce dtype");
+  }
+}
+void pg_allreduce(const PG& pg, at::Tensor& t, Comm::Op op) {
   std::vector<at::Tensor> v{t};
   c10d::AllreduceOptions o;
   o.reduceOp = c10d::ReduceOp(red(op));
   pg->allreduce(v, o)->wait();
   t = v[0];
 }
+hipStream_t cur(at::Device d) { return at::hip::getCurrentHIPStream(d.index()).stream(); }
+
+// one heartbeat monitor per (process, root store)
+std::shared_ptr<Monitor> shared_monitor(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size) {
+  static std::mutex mu;
+  static std::map<c10d::Store*, std::weak_ptr<Monitor>> reg;
+  std::lock_guard<std::mutex> l(mu);
+  auto& w = reg[store.get()];
+  if (auto m = w.lock()) return m;
+  auto m = std::make_shared<Monitor>(store, rank, size);
+  w = m;
+  return m;
+}
+
+// bytes of a per-peer list of transfers, peer order, as one contiguous tensor
+void copy_bytes(void* dst, const void* src, int64_t n, at::Device dev) {
+  if (n <= 0) return;
+  if (dev.is_cuda()) {
+    if (hipMemcpyAsync(dst, src, (size_t)n, hipMemcpyDeviceToDevice, cur(dev)) != hipSuccess)
+      throw std::runtime_error("mrhip: device copy failed");
+  } else {
+    std::memcpy(dst, src, (size_t)n);
+  }
+}
 }  // namespace
 
-Comm::Comm(at::Device dev) : dev_(dev) {}
+Comm::Comm(at::Device dev) : dev_(dev) {
+  if (dev_.is_cuda() && force_rccl()) init_transport("", "self");
+}
 
-Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store)
+Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const std::string& transport)
     : dev_(dev), pg_(std::move(pg)), store_(std::move(store)) {
   if (pg_) {
     rank_ = pg_->getRank();
     size_ = pg_->getSize();
-    if (size_ == 1) pg_.reset();
   }
+  if (size_ > 1 && store_) mon_ = shared_monitor(store_, rank_, size_);
+  if (size_ == 1) pg_.reset();
+  init_transport(transport, "world");
+}
+
+void Comm::init_transport(const std::string& transport, const std::string& tag) {
+  if (!dev_.is_cuda() || transport == "pg") return;
+  if (size_ == 1 && !force_rccl()) return;
+  if (size_ > 1 && !store_) {
+    if (pg_) return;  // no store to bootstrap from: keep the process group
+    throw std::runtime_error("mrhip: multi-rank RCCL communicator needs a rendezvous store");
+  }
+  rccl_ = std::make_shared<Rccl>(rank_, size_, dev_.index(), store_, tag);
+}
+
+Comm::~Comm() = default;
+
+std::string Comm::transport() const {
+  if (rccl_) return "rccl";
+  if (pg_) return "pg:" + pg_->getBackendName();
+  return "local";
 }
 
 std::shared_ptr<Comm> Comm::from_env() {
@@ -67,40 +126,100 @@ std::shared_ptr<Comm> Comm::from_env() {
   so.numWorkers = ws;
   so.timeout = std::chrono::milliseconds(1000LL * guard::comm_timeout_seconds());
   c10::intrusive_ptr<c10d::Store> store = c10::make_intrusive<c10d::TCPStore>(addr ? addr : "127.0.0.1", so);
-  return std::make_shared<Comm>(make_pg(store, rank, ws, dev), dev, store);
+  auto mon = shared_monitor(store, rank, ws);
+  const bool pg_only = dev.is_cpu() || (std::getenv("MRH_TRANSPORT") && std::string(std::getenv("MRH_TRANSPORT")) == "pg");
+  PG pg = make_host_pg(store, rank, ws, mon);
+  return std::make_shared<Comm>(pg, dev, store, pg_only ? "pg" : "");
 }
 
-// RCCL for the device engine; the store transport (storepg.h) for host engines
-PG Comm::make_pg(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size, at::Device dev) {
+// the store transport (storepg.h): host tensors only
+PG Comm::make_host_pg(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size, std::shared_ptr<Monitor> mon) {
   auto pg = c10::make_intrusive<c10d::ProcessGroup>(store, rank, size);
-  if (dev.is_cuda()) {
-    auto opts = c10d::ProcessGroupNCCL::Options::create();
-    opts->timeout = std::chrono::milliseconds(1000LL * guard::comm_timeout_seconds());  // watchdog bound
-    auto be = c10::make_intrusive<c10d::ProcessGroupNCCL>(store, rank, size, opts);
-    pg->setBackend(c10::DeviceType::CUDA, c10d::ProcessGroup::BackendType::NCCL, be);
-    pg->setDefaultBackend(c10d::ProcessGroup::BackendType::NCCL);
-  } else {
-    auto be = c10::make_intrusive<StoreBackend>(store, rank, size);
-    pg->setBackend(c10::DeviceType::CPU, c10d::ProcessGroup::BackendType::CUSTOM, be);
-    pg->setDefaultBackend(c10d::ProcessGroup::BackendType::CUSTOM);
-  }
+  auto be = c10::make_intrusive<StoreBackend>(store, rank, size, std::move(mon));
+  pg->setBackend(c10::DeviceType::CPU, c10d::ProcessGroup::BackendType::CUSTOM, be);
+  pg->setDefaultBackend(c10d::ProcessGroup::BackendType::CUSTOM);
   return pg;
 }
 
+// ---------------------------------------------------------------- failure handling
+
+void Comm::check_peers() const {
+  if (mon_) mon_->check();
+}
+
+void Comm::fail_now(const std::string& why) const {
+  if (mon_) mon_->poison(why);
+  if (rccl_) rccl_->abort();
+  throw PeerFailure(why);
+}
+
+void Comm::poison(const std::string& why) const {
+  if (mon_) mon_->poison(why);
+  if (rccl_) rccl_->abort();
+}
+
+void Comm::host_wait() const {
+  if (!dev_.is_cuda()) return;
+  hipEvent_t ev;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+    throw std::runtime_error("mrhip: hipEventCreate failed");
+  struct Drop {
+    hipEvent_t e;
+    ~Drop() { (void)hipEventDestroy(e); }
+  } drop{ev};
+  if (hipEventRecord(ev, cur(dev_)) != hipSuccess) throw std::runtime_error("mrhip: hipEventRecord failed");
+  for (int spin = 0;; ++spin) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) throw std::runtime_error(std::string("mrhip: device error: ") + hipGetErrorString(q));
+    if (rccl_) {
+      const ncclResult_t r = rccl_->async_error();
+      if (r != ncclSuccess && r != ncclInProgress)
+        fail_now(std::string("mrhip: RCCL async error: ") + ncclGetErrorString(r));
+    }
+    if (mon_) {
+      try {
+        mon_->check();
+      } catch (const PeerFailure& e) {
+        fail_now(e.what());
+      }
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 200 : 20));
+  }
+}
+
+// ---------------------------------------------------------------- scalars
+
 std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
-  if (!pg_ || v.empty()) return v;
-  at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kLong)).to(dev_);
-  allreduce_t(pg_, t, op);
-  t = t.to(at::kCPU);
+  if (v.empty() || !distributed()) return v;
+  at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kLong));
+  if (rccl_) {
+    t = t.to(dev_);
+    rccl_->allreduce(t.data_ptr(), v.size(), ncclInt64, nred(op), cur(dev_));
+    host_wait();
+    t = t.to(at::kCPU);
+  } else {
+    t = t.to(dev_);
+    pg_allreduce(pg_, t, op);
+    t = t.to(at::kCPU);
+  }
   std::memcpy(v.data(), t.data_ptr<int64_t>(), v.size() * sizeof(int64_t));
   return v;
 }
 
 std::vector<double> Comm::allreduce_f64(std::vector<double> v, Op op) const {
-  if (!pg_ || v.empty()) return v;
-  at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kDouble)).to(dev_);
-  allreduce_t(pg_, t, op);
-  t = t.to(at::kCPU);
+  if (v.empty() || !distributed()) return v;
+  at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kDouble));
+  if (rccl_) {
+    t = t.to(dev_);
+    rccl_->allreduce(t.data_ptr(), v.size(), ncclFloat64, nred(op), cur(dev_));
+    host_wait();
+    t = t.to(at::kCPU);
+  } else {
+    t = t.to(dev_);
+    pg_allreduce(pg_, t, op);
+    t = t.to(at::kCPU);
+  }
   std::memcpy(v.data(), t.data_ptr<double>(), v.size() * sizeof(double));
   return v;
 }
@@ -112,22 +231,20 @@ std::vector<double> Comm::allgather_f64(double x) const {
 }
 
 std::string Comm::bcast(const std::string& s, int root) const {
-  if (!pg_) return s;
+  if (!distributed()) return s;
   int64_t n = rank_ == root ? (int64_t)s.size() : 0;
   n = allreduce(n, SUM);
   at::Tensor t = at::zeros({std::max<int64_t>(n, 1)}, at::TensorOptions().dtype(at::kByte));
   if (rank_ == root && n) std::memcpy(t.data_ptr(), s.data(), n);
   t = t.to(dev_);
-  std::vector<at::Tensor> v{t};
-  c10d::BroadcastOptions bo;
-  bo.rootRank = root;
-  pg_->broadcast(v, bo)->wait();
-  t = v[0].to(at::kCPU);
+  broadcast_tensor(t, root);
+  if (rccl_) host_wait();
+  t = t.to(at::kCPU);
   return std::string((const char*)t.data_ptr(), (size_t)n);
 }
 
 void Comm::barrier() const {
-  if (!pg_) return;
+  if (!distributed()) return;
   allreduce((int64_t)0, SUM);
 }
 
@@ -136,50 +253,149 @@ double Comm::wtime() {
   return duration<double>(steady_clock::now().time_since_epoch()).count();
 }
 
+// ---------------------------------------------------------------- data plane
+
+void Comm::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) const {
+  if (rccl_) {
+    rccl_->sendrecv(sends, recvs, cur(dev_));
+    return;
+  }
+  if (!pg_) {  // world size 1: self copies, in order
+    size_t j = 0;
+    for (const Xfer& s : sends) {
+      while (j < recvs.size() && recvs[j].bytes == 0) ++j;
+      if (s.bytes == 0) continue;
+      if (j >= recvs.size() || recvs[j].bytes != s.bytes) throw std::runtime_error("mrhip sendrecv: unmatched self transfer");
+      copy_bytes(recvs[j].ptr, s.ptr, s.bytes, dev_);
+      ++j;
+    }
+    return;
+  }
+  // process group: pack per peer in order, one byte all-to-all, unpack
+  const int P = size_;
+  std::vector<int64_t> sb(P, 0), rb(P, 0);
+  for (const Xfer& x : sends) sb[x.peer] += x.bytes;
+  for (const Xfer& x : recvs) rb[x.peer] += x.bytes;
+  int64_t st = 0, rt = 0;
+  std::vector<int64_t> soff(P + 1, 0), roff(P + 1, 0);
+  for (int p = 0; p < P; ++p) {
+    soff[p + 1] = soff[p] + sb[p];
+    roff[p + 1] = roff[p] + rb[p];
+  }
+  st = soff[P];
+  rt = roff[P];
+  auto bo = at::TensorOptions().device(dev_).dtype(at::kByte);
+  at::Tensor sbuf = at::empty({st}, bo), rbuf = at::empty({rt}, bo);
+  std::vector<int64_t> fill = soff;
+  for (const Xfer& x : sends) {
+    copy_bytes((uint8_t*)sbuf.data_ptr() + fill[x.peer], x.ptr, x.bytes, dev_);
+    fill[x.peer] += x.bytes;
+  }
+  pg_->alltoall_base(rbuf, sbuf, rb, sb)->wait();
+  fill = roff;
+  for (const Xfer& x : recvs) {
+    copy_bytes(x.ptr, (uint8_t*)rbuf.data_ptr() + fill[x.peer], x.bytes, dev_);
+    fill[x.peer] += x.bytes;
+  }
+  if (dev_.is_cuda()) host_wait();  // staging buffers die here
+}
+
+void Comm::allgather_bytes(const void* send, void* recv, int64_t bytes) const {
+  if (rccl_) {
+    rccl_->allgather(send, recv, (size_t)bytes, cur(dev_));
+    return;
+  }
+  if (!pg_) {
+    copy_bytes(recv, send, bytes, dev_);
+    return;
+  }
+  auto bo = at::TensorOptions().device(dev_).dtype(at::kByte);
+  at::Tensor in = at::empty({bytes}, bo), out = at::empty({bytes * size_}, bo);
+  copy_bytes(in.data_ptr(), send, bytes, dev_);
+  pg_->_allgather_base(out, in)->wait();
+  copy_bytes(recv, out.data_ptr(), bytes * size_, dev_);
+  if (dev_.is_cuda()) host_wait();
+}
+
 std::vector<int64_t> Comm::alltoall_counts(const std::vector<int64_t>& send) const {
-  if (!pg_) return send;
-  at::Tensor s = at::tensor(send, at::TensorOptions().dtype(at::kLong)).to(dev_);
-  at::Tensor r = at::empty_like(s);
-  std::vector<int64_t> eq(size_, 1);
-  pg_->alltoall_base(r, s, eq, eq)->wait();
+  if (!distributed()) return send;
+  auto lo = at::TensorOptions().dtype(at::kLong);
+  at::Tensor s = at::tensor(send, lo).to(dev_);
+  at::Tensor r = at::empty({size_}, lo.device(dev_));
+  std::vector<Xfer> xs, xr;
+  for (int p = 0; p < size_; ++p) {
+    xs.push_back({p, s.data_ptr<int64_t>() + p, 8});
+    xr.push_back({p, r.data_ptr<int64_t>() + p, 8});
+  }
+  sendrecv(xs, xr);
+  host_wait();
   r = r.to(at::kCPU);
   return std::vector<int64_t>(r.data_ptr<int64_t>(), r.data_ptr<int64_t>() + size_);
 }
 
 at::Tensor Comm::alltoallv(const at::Tensor& in, const std::vector<int64_t>& send,
                            const std::vector<int64_t>& recv) const {
-  if (!pg_) return in;
+  if (!distributed()) return in;
   int64_t tot = 0;
   for (auto x : recv) tot += x;
   std::vector<int64_t> shape = in.sizes().vec();
   shape[0] = tot;
   at::Tensor out = at::empty(shape, in.options());
   at::Tensor src = in.contiguous();
-  std::vector<int64_t> s = send, r = recv;
-  pg_->alltoall_base(out, src, r, s)->wait();
+  const int64_t row = (in.dim() > 1 ? src.numel() / std::max<int64_t>(1, in.size(0)) : 1) * in.element_size();
+  std::vector<Xfer> xs, xr;
+  int64_t so = 0, ro = 0;
+  for (int p = 0; p < size_; ++p) {
+    xs.push_back({p, (uint8_t*)src.data_ptr() + so * row, send[p] * row});
+    xr.push_back({p, (uint8_t*)out.data_ptr() + ro * row, recv[p] * row});
+    so += send[p];
+    ro += recv[p];
+  }
+  sendrecv(xs, xr);
   return out;
 }
 
 at::Tensor Comm::allgather_var(const at::Tensor& in) const {
-  if (!pg_) return in;
+  if (!distributed()) return in;
   std::vector<double> sizes = allgather_f64((double)in.numel());
-  int64_t mx = 0, tot = 0;
-  for (double s : sizes) {
-    mx = std::max<int64_t>(mx, (int64_t)s);
-    tot += (int64_t)s;
+  int64_t tot = 0;
+  for (double s : sizes) tot += (int64_t)s;
+  at::Tensor src = in.contiguous().reshape({-1});
+  at::Tensor out = at::empty({tot}, in.options());
+  const int64_t es = in.element_size();
+  std::vector<Xfer> xs, xr;
+  int64_t o = 0;
+  for (int p = 0; p < size_; ++p) {
+    xs.push_back({p, src.data_ptr(), src.numel() * es});
+    xr.push_back({p, (uint8_t*)out.data_ptr() + o * es, (int64_t)sizes[p] * es});
+    o += (int64_t)sizes[p];
   }
-  at::Tensor buf = at::zeros({std::max<int64_t>(mx, 1)}, in.options());
-  if (in.numel()) buf.narrow(0, 0, in.numel()).copy_(in.reshape({-1}));
-  at::Tensor all = at::empty({buf.numel() * size_}, in.options());
-  pg_->_allgather_base(all, buf)->wait();
-  std::vector<at::Tensor> parts;
-  for (int r = 0; r < size_; ++r) parts.push_back(all.narrow(0, r * buf.numel(), (int64_t)sizes[r]));
-  return at::cat(parts);
+  sendrecv(xs, xr);
+  return out;
 }
 
 void Comm::allreduce_tensor(at::Tensor& t, Op op) const {
-  if (!pg_) return;
-  allreduce_t(pg_, t, op);
+  if (!distributed()) return;
+  if (rccl_) {
+    if (!t.is_contiguous()) t = t.contiguous();
+    rccl_->allreduce(t.data_ptr(), (size_t)t.numel(), ndt(t.scalar_type()), nred(op), cur(dev_));
+    return;
+  }
+  pg_allreduce(pg_, t, op);
+}
+
+void Comm::broadcast_tensor(at::Tensor& t, int root) const {
+  if (!distributed()) return;
+  if (rccl_) {
+    if (!t.is_contiguous()) t = t.contiguous();
+    rccl_->broadcast(t.data_ptr(), (size_t)(t.numel() * t.element_size()), root, cur(dev_));
+    return;
+  }
+  std::vector<at::Tensor> v{t};
+  c10d::BroadcastOptions bo;
+  bo.rootRank = root;
+  pg_->broadcast(v, bo)->wait();
+  t = v[0];
 }
 
 std::string gpu_pci_bus_id(int dev) {
@@ -189,7 +405,7 @@ std::string gpu_pci_bus_id(int dev) {
 }
 
 std::shared_ptr<Comm> Comm::split(int color) const {
-  if (size_ == 1) return std::make_shared<Comm>(*this);
+  if (size_ == 1) return std::make_shared<Comm>(dev_);
   static std::atomic<int> nsplit{0};
   const int id = nsplit++;  // every rank splits in the same sequence
   std::vector<double> colors = allgather_f64((double)color);
@@ -203,11 +419,23 @@ std::shared_ptr<Comm> Comm::split(int color) const {
   if (!store_) throw std::runtime_error("mrhip: Comm::split needs the rendezvous store");
   auto pst = c10::make_intrusive<c10d::PrefixStore>("mrh_split_" + std::to_string(id) + "_" + std::to_string(color),
                                                     store_);
-  return std::make_shared<Comm>(make_pg(pst, newrank, newsize, dev_), dev_, pst);
+  auto c = std::make_shared<Comm>(dev_);
+  c->rank_ = newrank;
+  c->size_ = newsize;
+  c->store_ = pst;
+  c->mon_ = mon_;  // failure detection stays job-wide
+  c->rccl_.reset();
+  if (rccl_) {
+    c->rccl_ = std::make_shared<Rccl>(newrank, newsize, dev_.index(), pst, "split");
+  } else {
+    c->pg_ = make_host_pg(pst, newrank, newsize, mon_);
+  }
+  return c;
 }
 
 void Comm::shutdown() const {
   if (!store_ || size_ == 1) return;
+  if (mon_) mon_->retire();
   try {
     store_->add("mrh_shutdown", 1);
     if (rank_ != 0) return;
@@ -221,6 +449,7 @@ void Comm::shutdown() const {
 
 int64_t Comm::next_task(const std::string& key) const {
   if (!store_) throw std::runtime_error("mrhip: mapstyle 2 needs a c10d store");
+  check_peers();
   return store_->add(key, 1) - 1;
 }
 

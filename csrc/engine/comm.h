@@ -1,17 +1,36 @@
 // Host-side view of the job's communicator for the native MapReduce object:
-// rank/size, the engine device, the c10d ProcessGroup used by the shuffle
-// (backend "nccl" = RCCL over xGMI for device tensors, "gloo" for host
-// tensors), and the scalar collectives every MR op needs (the Allreduce SUM of
-// pair counts that is each op's return value, stats MAX/MIN, barriers, file
-// list broadcast). Replaces MR-MPI's direct MPI_Comm use and mpistubs/
-// (world size 1 = no process group, identity collectives).
+// rank/size, the engine device, the data-plane transport, and the scalar
+// collectives every MR op needs (the Allreduce SUM of pair counts that is each
+// op's return value, stats MAX/MIN, barriers, file list broadcast). Replaces
+// MR-MPI's direct MPI_Comm use and mpistubs/ (world size 1 = identity
+// collectives).
+//
+// Transports (one per communicator, chosen at construction, no per-call
+// dispatch):
+//  * RCCL (device engine): the native RCCL communicator of rccl.h over xGMI,
+//    bootstrapped through the job's rendezvous store. Used whenever the
+//    engine device is a GPU and the job has more than one rank — and at world
+//    size 1 too when MRH_FORCE_RCCL=1, so the complete RCCL data path (header
+//    allgather, grouped send/recv rounds, allreduce, broadcast) runs and is
+//    tested on a single GPU;
+//  * PG (host engine / rehearsal): a c10d ProcessGroup — gloo from
+//    torch.distributed, or the store transport of storepg.h for the native
+//    programs on CPU — moving packed host (or staged device) buffers.
+//
+// Every host wait on communication is polled against the peer monitor
+// (rccl.h): a failed or vanished peer turns into a PeerFailure on every rank
+// within seconds (SURVEY.md §5 "failure detection"; reference Error::one ->
+// MPI_Abort, src/error.cpp:47-57).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/distributed/c10d/Store.hpp>
 
 #include <memory>
 #include <string>
 #include <vector>
+
+#include "rccl.h"
 
 namespace mrh {
 
@@ -21,26 +40,35 @@ class Comm {
  public:
   enum Op { SUM = 0, MAX = 1, MIN = 2 };
 
-  // world size 1 on `dev`
+  // world size 1 on `dev` (an RCCL loopback communicator if MRH_FORCE_RCCL=1)
   explicit Comm(at::Device dev = at::Device(at::kCPU));
-  // an existing process group (e.g. created by torch.distributed)
-  Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store = {});
+  // an existing process group (e.g. created by torch.distributed) + its store;
+  // transport "" = automatic (RCCL for a GPU device), "pg" = stay on the group
+  Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store = {}, const std::string& transport = "");
+  ~Comm();
 
   // Bootstrap from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK,
   // MASTER_ADDR, MASTER_PORT) without Python: binds the process to GPU
   // LOCAL_RANK when GPUs are visible, and for WORLD_SIZE > 1 creates a
-  // TCPStore rendezvous and an RCCL process group (device engine) or the
-  // store transport of storepg.h (host engine, e.g. CPU-only CI).
+  // TCPStore rendezvous plus the RCCL communicator (device engine) or the store
+  // transport of storepg.h (host engine, e.g. CPU-only CI).
   static std::shared_ptr<Comm> from_env();
-  // process group over `store`: RCCL for a cuda device, StoreBackend for cpu
-  static PG make_pg(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size, at::Device dev);
+  // host process group over `store` (storepg.h)
+  static PG make_host_pg(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size,
+                         std::shared_ptr<Monitor> mon);
 
   int rank() const { return rank_; }
   int size() const { return size_; }
   at::Device device() const { return dev_; }
-  const PG& pg() const { return pg_; }  // null when size == 1
+  // true when ops must run the distributed code path (size > 1, or the forced
+  // single-rank RCCL mode)
+  bool distributed() const { return size_ > 1 || rccl_ != nullptr; }
+  bool uses_rccl() const { return rccl_ != nullptr; }
+  std::string transport() const;
+  const PG& pg() const { return pg_; }
+  const std::shared_ptr<Rccl>& rccl() const { return rccl_; }
+  const std::shared_ptr<Monitor>& monitor() const { return mon_; }
   const c10::intrusive_ptr<c10d::Store>& store() const { return store_; }
-  void set_store(c10::intrusive_ptr<c10d::Store> s) { store_ = std::move(s); }
 
   std::vector<int64_t> allreduce(std::vector<int64_t> v, Op op) const;
   int64_t allreduce(int64_t v, Op op) const { return allreduce(std::vector<int64_t>{v}, op)[0]; }
@@ -53,8 +81,7 @@ class Comm {
   static double wtime();
 
   // MPI_Comm_split analog: a new communicator over the ranks with the same
-  // color, ordered by rank (RCCL for device engines, the store transport for host ones);
-  // every rank of this communicator must call it
+  // color, ordered by rank; every rank of this communicator must call it
   std::shared_ptr<Comm> split(int color) const;
 
   // end-of-job handshake: every rank checks in; rank 0, which serves the
@@ -65,21 +92,45 @@ class Comm {
   // mapstyle 2 work queue: next global task index from a store counter
   int64_t next_task(const std::string& key) const;
 
-  // device-data collectives on the engine device (RCCL over xGMI for cuda)
+  // ---------------------------------------------------------------- data plane
+  // One grouped round of point-to-point byte transfers between this rank and
+  // any peers (self included): RCCL send/recv on the comm stream fenced
+  // against the current stream, or packed through the process group. Buffers
+  // live on the engine device. Synchronous with respect to the current stream.
+  void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) const;
+  // all ranks' `bytes`-byte blocks concatenated in rank order into recv
+  // (device buffers of the engine device)
+  void allgather_bytes(const void* send, void* recv, int64_t bytes) const;
   // per-peer element counts -> counts received from every peer
   std::vector<int64_t> alltoall_counts(const std::vector<int64_t>& send) const;
-  // variable all-to-all along dim 0 (splits in rows); identity when size == 1
+  // variable all-to-all along dim 0 (splits in rows); identity when not distributed
   at::Tensor alltoallv(const at::Tensor& in, const std::vector<int64_t>& send, const std::vector<int64_t>& recv) const;
   // every rank's 1-D tensor concatenated in rank order
   at::Tensor allgather_var(const at::Tensor& in) const;
   // in-place sum/max/min allreduce of a device tensor
   void allreduce_tensor(at::Tensor& t, Op op) const;
+  void broadcast_tensor(at::Tensor& t, int root) const;
+
+  // Block the host until the work queued so far on the current stream is
+  // done, polling for peer failure and RCCL async errors (throws PeerFailure
+  // after aborting the communicator). Every host read of data that depends on
+  // communication goes through here first.
+  void host_wait() const;
+  // fatal error on this rank: tell every peer and abort the communicator
+  void poison(const std::string& why) const;
+  // throws if a peer failed (cheap, rate limited)
+  void check_peers() const;
 
  private:
+  void init_transport(const std::string& transport, const std::string& tag);
+  void fail_now(const std::string& why) const;
+
   int rank_ = 0, size_ = 1;
   at::Device dev_;
   PG pg_;
   c10::intrusive_ptr<c10d::Store> store_;
+  std::shared_ptr<Rccl> rccl_;
+  std::shared_ptr<Monitor> mon_;
 };
 
 using CommPtr = std::shared_ptr<Comm>;

@@ -7,6 +7,9 @@
 #include <limits>
 #include <stdexcept>
 
+#include <ATen/hip/HIPContext.h>
+
+#include "../kernels/launch.h"
 #include "tri.h"
 
 namespace mrh {
@@ -25,6 +28,22 @@ std::pair<at::Tensor, at::Tensor> sort_with_perm(const at::Tensor& key, int end_
   return {std::get<0>(r), std::get<1>(r)};
 }
 
+// pairs per owner rank (v % P) of an int64 id column, on the engine device
+at::Tensor owner_counts(const at::Tensor& ids, int P) {
+  at::Tensor c = at::zeros({P}, ids.options().dtype(at::kLong));
+  if (ids.numel() == 0) return c;
+  if (ids.is_cuda()) {
+    k::count_mod(reinterpret_cast<const int64_t*>(ids.data_ptr()), ids.numel(), P,
+                 reinterpret_cast<int64_t*>(c.data_ptr()), at::hip::getCurrentHIPStream());
+  } else {
+    at::Tensor h = ids.contiguous();
+    const int64_t* p = h.data_ptr<int64_t>();
+    int64_t* o = c.data_ptr<int64_t>();
+    for (int64_t i = 0; i < h.numel(); ++i) o[p[i] % P]++;
+  }
+  return c;
+}
+
 at::Tensor segments(const at::Tensor& sorted) {
   if (sorted.numel() == 0) return at::zeros({1}, sorted.options().dtype(at::kLong));
   return segments_sorted(sorted);
@@ -38,13 +57,13 @@ std::vector<int64_t> to_vec(const at::Tensor& t) {
 // route edges to the owner of their source (engine shuffle), keeping weights
 void to_source_owner(const Comm& comm, at::Tensor& e, at::Tensor& w) {
   const int P = comm.size();
-  if (P <= 1) return;
+  if (!comm.distributed()) return;
   const at::Device dev = e.device();
   const int64_t n = e.size(0);
   at::Tensor vb = w.defined() ? w.contiguous().view(at::kByte) : at::empty({0}, opt(dev, at::kByte));
   KV kv = make_kv(e.contiguous().view(at::kByte), std::nullopt, vb, std::nullopt, n, dev);
   at::Tensor dest = at::remainder(e.select(1, 0), P).to(at::kInt);
-  KV out = exchange(kv, dest, comm.pg());
+  KV out = exchange(std::move(kv), dest, comm);
   e = out.kdata.view(at::kLong).view({-1, 2});
   if (w.defined()) w = out.vdata.view(w.scalar_type());
 }
@@ -71,7 +90,8 @@ EdgePlan::EdgePlan(CommPtr c, const at::Tensor& edges, int64_t nvert, const std:
   nedge = e.size(0);
   at::Tensor src_local = at::floor_divide(e.select(1, 0), P).to(at::kInt);
   at::Tensor vj = e.select(1, 1).contiguous();
-  at::Tensor key = P > 1 ? at::bitwise_or(at::bitwise_left_shift(at::remainder(vj, P), 40), vj) : vj;
+  const bool dist = comm->distributed();
+  at::Tensor key = dist ? at::bitwise_or(at::bitwise_left_shift(at::remainder(vj, P), 40), vj) : vj;
   auto [ks, perm] = sort_with_perm(key);
   at::Tensor pl = perm.to(at::kLong);
   src = src_local.index_select(0, pl).contiguous();
@@ -79,9 +99,8 @@ EdgePlan::EdgePlan(CommPtr c, const at::Tensor& edges, int64_t nvert, const std:
   seg = segments(ks);
   ngrp = seg.numel() - 1;
   at::Tensor ujv = at::bitwise_and(ks.index_select(0, seg.narrow(0, 0, ngrp)), VMASK);
-  if (P > 1) {
-    at::Tensor scount = at::bincount(at::remainder(ujv, P), {}, P);
-    send_splits_ = to_vec(scount);
+  if (dist) {
+    send_splits_ = to_vec(owner_counts(ujv, P));
     recv_splits_ = comm->alltoall_counts(send_splits_);
     at::Tensor rids = comm->alltoallv(ujv.contiguous(), send_splits_, recv_splits_);
     auto [rs, rperm] = sort_with_perm(at::floor_divide(rids, P));
@@ -103,7 +122,7 @@ at::Tensor EdgePlan::propagate(const at::Tensor& x, int op, double identity, boo
     else plan_gather_reduce(seg, src, x.contiguous(), wv, op, send);
   }
   at::Tensor acc = at::full({nlocal}, identity, x.options());
-  if (P > 1) {
+  if (comm->distributed()) {
     at::Tensor recv = comm->alltoallv(send, send_splits_, recv_splits_);
     if (recv.numel()) plan_combine(rseg_, rperm_, recv, rvid_, op, acc);
   } else if (ngrp > 0) {
@@ -206,7 +225,8 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
   new_of_old.index_put_({order_}, iota32(nlocal, dev));
   at::Tensor src_local = nedge ? at::repeat_interleave(new_of_old.index_select(0, at::floor_divide(vi, P)), deg, 0, nedge)
                                : at::empty({0}, opt(dev, at::kInt));
-  at::Tensor key = P > 1 ? at::bitwise_or(at::bitwise_left_shift(at::remainder(vj, P), 40), vj) : vj.clone();
+  const bool dist = comm->distributed();
+  at::Tensor key = dist ? at::bitwise_or(at::bitwise_left_shift(at::remainder(vj, P), 40), vj) : vj.clone();
   auto [ks, perm] = sort_with_perm(key);
   src_ = src_local.index_select(0, perm.to(at::kLong)).contiguous();
   w_ = at::empty({0}, opt(dev, at::kFloat));  // weights folded into c = r / outdeg
@@ -214,8 +234,8 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
   const int64_t ngrp = seg_.numel() - 1;
   at::Tensor ujv = at::bitwise_and(ks.index_select(0, seg_.narrow(0, 0, ngrp)), VMASK);
   send_ = at::empty({ngrp}, opt(dev, at::kFloat));
-  if (P > 1) {
-    send_splits_ = to_vec(at::bincount(at::remainder(ujv, P), {}, P));
+  if (dist) {
+    send_splits_ = to_vec(owner_counts(ujv, P));
     recv_splits_ = comm->alltoall_counts(send_splits_);
     at::Tensor rids = comm->alltoallv(ujv.contiguous(), send_splits_, recv_splits_);
     auto [rs, rperm] = sort_with_perm(at::floor_divide(rids, P));
@@ -248,7 +268,7 @@ void PageRankPlan::step() {
   if (six_.defined()) seg_gather_reduce(six_, src_, c_, at::Tensor(), 0, send_);
   else if (send_.numel()) pr_contrib(seg_, src_, w_, c_, send_);
   acc_.zero_();
-  if (P > 1) {
+  if (comm->distributed()) {
     at::Tensor recv = comm->alltoallv(send_, send_splits_, recv_splits_);
     if (recv.numel()) pr_combine(rseg_, rperm_, recv, rvid_, acc_);
   } else if (send_.numel()) {
@@ -284,7 +304,7 @@ TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : c
   at::Tensor lo = at::minimum(e.select(1, 0), e.select(1, 1)), hi = at::maximum(e.select(1, 0), e.select(1, 1));
   at::Tensor keep = lo != hi;
   at::Tensor p = at::bitwise_or(at::bitwise_left_shift(lo.index({keep}), 32), hi.index({keep})).contiguous();
-  if (comm->size() > 1) p = comm->allgather_var(p);
+  if (comm->distributed()) p = comm->allgather_var(p);
   at::Tensor uniq = p;
   if (p.numel()) {
     at::Tensor s = sort_with_perm(p).first;

@@ -81,6 +81,7 @@ void check_col(const at::Tensor& data, const at::Tensor& off, int w, int64_t n, 
     if (bytes < n * w) bad(op, std::string(col) + " arena smaller than n * width");
     return;
   }
+  if (n == 0 && !off.defined()) return;  // empty variable column: offsets optional
   if (!off.defined() || off.numel() != n + 1) bad(op, std::string(col) + " offsets must have n+1 entries");
   at::Tensor o = off.to(at::kCPU);
   if (o.scalar_type() != at::kLong) bad(op, std::string(col) + " offsets must be int64");

@@ -19,12 +19,13 @@
 // tensor device; the CUDA branch always runs the hand-written HIP kernels.
 #pragma once
 #include <ATen/ATen.h>
-#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <cstdint>
 #include <string>
 #include <vector>
 
 namespace mrh {
+
+class Comm;
 
 struct KV {
   at::Tensor kdata, koff, vdata, voff;
@@ -98,25 +99,40 @@ KMV sort_multivalues(const KMV& kmv, int flag);
 // KMV -> KV with one (key, value) per value (inverse of convert)
 KV expand(const KMV& kmv);
 
-// ------------------------------------------------------------------ shuffle
+// ------------------------------------------------------------------ shuffle (shuffle.cpp)
 struct ShuffleStats {
-  int64_t send_bytes = 0, recv_bytes = 0, send_pairs = 0, recv_pairs = 0;
+  int64_t send_bytes = 0, recv_bytes = 0, send_pairs = 0, recv_pairs = 0, rounds = 0;
   double seconds = 0;
 };
-// destination rank per pair: hashlittle(key, kb, P) % P (MR-MPI default) or a
-// user-provided int32 dest tensor
+struct ExchangeOpts {
+  // receive cap per round in bytes (0 = one round): the exchange runs in
+  // R = max_r ceil(recv_bytes_r / chunk_bytes) lock-step rounds
+  int64_t chunk_bytes = 0;
+  // received pairs land in pinned host memory through two HBM staging
+  // buffers (out-of-core aggregate: HBM never holds the output)
+  bool host_sink = false;
+  // or choose the host sink by itself when this rank's received bytes exceed
+  // this HBM budget (0 = unlimited)
+  int64_t hbm_budget = 0;
+  // 1: each round is one grouped all-to-all over every peer (RCCL group);
+  // 0: the reference's custom exchange order (src/irregular.cpp:200-215,
+  // 311-363): P pairwise steps per round, step j sends to me+j and receives
+  // from me-j, one peer link busy at a time
+  int all2all = 1;
+};
+// destination rank per pair: hashlittle(key, kb, P) % P (MR-MPI default)
 at::Tensor partition_dest(const KV& kv, int P, at::Tensor* counts);
-// all-to-all exchange of KV pairs to their destination ranks over the process
-// group (RCCL over xGMI for cuda tensors, gloo for cpu). pg may be null (P=1).
-KV exchange(const KV& kv, const at::Tensor& dest, const c10::intrusive_ptr<c10d::ProcessGroup>& pg,
+// all-to-all exchange of KV pairs to their destination ranks (dest: int32 per
+// pair; undefined = hash partitioning fused into the partition kernel). The
+// KV is consumed (its memory is released once packed).
+KV exchange(KV kv, const at::Tensor& dest, const Comm& comm, const ExchangeOpts& o = {},
             ShuffleStats* st = nullptr);
-// MR-MPI aggregate: partition_dest + exchange
-KV aggregate(const KV& kv, const c10::intrusive_ptr<c10d::ProcessGroup>& pg, ShuffleStats* st = nullptr);
+// MR-MPI aggregate: hash partition + exchange
+KV aggregate(KV kv, const Comm& comm, const ExchangeOpts& o = {}, ShuffleStats* st = nullptr);
 // move everything to ranks 0..nprocs-1 (rank r sends to r % nprocs)
-KV gather_to(const KV& kv, int nprocs, const c10::intrusive_ptr<c10d::ProcessGroup>& pg,
-             ShuffleStats* st = nullptr);
+KV gather_to(KV kv, int nprocs, const Comm& comm, const ExchangeOpts& o = {}, ShuffleStats* st = nullptr);
 // root's KV replicated on every rank
-KV broadcast(const KV& kv, int root, const c10::intrusive_ptr<c10d::ProcessGroup>& pg);
+KV broadcast(const KV& kv, int root, const Comm& comm);
 
 // ------------------------------------------------------------------ text / graph maps
 // InvertedIndex map over one text buffer (padded by >= 32 bytes): KV(url+NUL, int32 doc)

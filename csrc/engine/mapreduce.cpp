@@ -250,6 +250,7 @@ void MapReduce::enter(const char* op) {
 }
 
 std::unique_ptr<MapReduce> MapReduce::copy() const {
+  const_cast<MapReduce*>(this)->ensure_resident();  // a disk-resident MR copies its data, not nothing
   auto mr = std::make_unique<MapReduce>(comm_);
   mr->set = set;
   if (kv) mr->kv = clone_kv(*kv);
@@ -370,6 +371,7 @@ uint64_t MapReduce::close() {  // :658-672
   KV n = open_->finish();
   open_.reset();
   if (open_add_) ensure_resident();  // appending to data that was spilled to disk
+  else drop_disk();                  // replacing it: the spilled copy must never be read back over n
   if (open_add_ && kv) kv = concat({*kv, n}, device());
   else kv = n;
   stats("Close", 0);
@@ -596,10 +598,10 @@ uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
   OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("aggregate");
-  if (comm_->size() > 1) {
+  if (comm_->distributed()) {
     ShuffleStats st;
     if (!hash) {
-      kv = oom_retry(this, device(), my_proc(), "aggregate", [&] { return mrh::aggregate(*kv, comm_->pg(), &st); });
+      kv = oom_retry(this, device(), my_proc(), "aggregate", [&] { return mrh::aggregate(*kv, *comm_, xopts(), &st); });
     } else {
       HostCol k = host_col(kv->kdata, kv->koff, kv->kw);
       at::Tensor d = at::empty({kv->n}, at::TensorOptions().dtype(at::kInt));
@@ -609,7 +611,7 @@ uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
         int h = hash(k.at(i), (int)k.len(i));
         dp[i] = (int32_t)(((int64_t)h % P + P) % P);
       }
-      kv = exchange(*kv, d.to(device()), comm_->pg(), &st);
+      kv = exchange(std::move(*kv), d.to(device()), *comm_, xopts(), &st);
     }
     note_shuffle(st);
   }
@@ -622,9 +624,16 @@ uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
   OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("aggregate");
-  if (comm_->size() > 1) {
+  if (comm_->distributed()) {
     ShuffleStats st;
-    kv = exchange(*kv, dest.to(device()).to(at::kInt), comm_->pg(), &st);
+    at::Tensor d = dest.to(device()).to(at::kInt).contiguous();
+    if (d.numel() != kv->n) fail("aggregate: one destination per pair");
+    if (d.numel()) {
+      auto mm = at::aminmax(d);
+      if (std::get<0>(mm).item<int>() < 0 || std::get<1>(mm).item<int>() >= comm_->size())
+        fail("aggregate: destination rank out of range");
+    }
+    kv = exchange(std::move(*kv), d, *comm_, xopts(), &st);
     note_shuffle(st);
   }
   stats("Aggregate", 0);
@@ -636,7 +645,7 @@ uint64_t MapReduce::broadcast(int root) {  // :569-623
   OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("broadcast");
-  if (comm_->size() > 1) kv = mrh::broadcast(*kv, root, comm_->pg());
+  if (comm_->distributed()) kv = mrh::broadcast(*kv, root, *comm_);
   stats("Broadcast", 0);
   return count(kv->n);
 }
@@ -647,9 +656,9 @@ uint64_t MapReduce::gather(int nprocs) {  // :893-1036
   enter(__func__);
   need_kv("gather");
   if (nprocs < 1 || nprocs > comm_->size()) fail("Invalid proc count for gather");
-  if (comm_->size() > 1 && nprocs < comm_->size()) {
+  if (comm_->distributed() && (nprocs < comm_->size() || comm_->uses_rccl())) {
     ShuffleStats st;
-    kv = gather_to(*kv, nprocs, comm_->pg(), &st);
+    kv = gather_to(std::move(*kv), nprocs, *comm_, xopts(), &st);
     note_shuffle(st);
   }
   stats("Gather", 0);
@@ -721,6 +730,20 @@ uint64_t MapReduce::scrunch(int nprocs, const char* key, int kb) {  // :2075-209
 }
 
 // ====================================================================== reduce family
+
+ExchangeOpts MapReduce::xopts() const {
+  ExchangeOpts o;
+  o.chunk_bytes = set.chunk_bytes > 0 ? set.chunk_bytes : 2 * block_bytes();
+  o.hbm_budget = budget();
+  o.all2all = set.all2all;
+  return o;
+}
+
+int64_t MapReduce::budget() const {
+  if (set.hbm_budget > 0) return set.hbm_budget;
+  if (set.maxpage > 0) return (int64_t)set.maxpage * block_bytes();
+  return 0;
+}
 
 int64_t MapReduce::block_bytes() const {
   // one "page" of values per host block: memsize MB (negative = bytes)
@@ -950,6 +973,7 @@ uint64_t MapReduce::sort_multivalues(const CompareFn& fn) {
 void MapReduce::print(int proc, int nstride, int kflag, int vflag) { print(nullptr, 0, proc, nstride, kflag, vflag); }
 
 void MapReduce::print(const char* file, int fflag, int proc, int nstride, int kflag, int vflag) {
+  ensure_resident();
   if (!kv && !kmv) fail("Cannot print without KeyValue or KeyMultiValue");
   if (kflag < 0 || kflag > 7 || vflag < 0 || vflag > 7 || nstride < 1) fail("Invalid print args");
   const int me = comm_->rank();
@@ -1014,6 +1038,7 @@ void MapReduce::print(const char* file, int fflag, int proc, int nstride, int kf
 // ====================================================================== stats
 
 uint64_t MapReduce::kv_stats(int level) {  // :2937-2966
+  ensure_resident();
   need_kv("print stats");
   std::vector<int64_t> t = comm_->allreduce({kv->n, kv->key_bytes(), kv->value_bytes(), kv->nbytes()}, Comm::SUM);
   const double mb = 1024.0 * 1024.0;
@@ -1029,6 +1054,7 @@ uint64_t MapReduce::kv_stats(int level) {  // :2937-2966
 }
 
 uint64_t MapReduce::kmv_stats(int level) {  // :2972-3001
+  ensure_resident();
   need_kmv("print stats");
   const KMV& m = *kmv;
   const int64_t vb = m.vw >= 0 ? m.nval * m.vw : (m.nval ? m.voff[m.nval].item<int64_t>() : 0);
@@ -1111,10 +1137,16 @@ void put_t(std::FILE* f, const at::Tensor& t) {
   if (nb && std::fwrite(h.data_ptr(), 1, nb, f) != nb) throw std::runtime_error("save: write failed");
 }
 at::Tensor get_t(std::FILE* f, at::Device dev) {
-  if (!get_i64(f)) return at::Tensor();
-  auto st = (at::ScalarType)get_i64(f);
+  const int64_t present = get_i64(f);
+  if (present == 0) return at::Tensor();
+  if (present != 1) throw std::runtime_error("load: corrupt tensor header");
+  const int64_t code = get_i64(f);
+  // only the dtypes a KV/KMV column can have (byte arenas, int32/int64 offsets)
+  if (code != (int64_t)at::kByte && code != (int64_t)at::kInt && code != (int64_t)at::kLong)
+    throw std::runtime_error("load: unexpected tensor dtype code " + std::to_string(code));
   const int64_t n = get_i64(f);
-  at::Tensor h = at::empty({n}, at::TensorOptions().dtype(st));
+  if (n < 0 || n > (int64_t(1) << 46)) throw std::runtime_error("load: corrupt tensor length");
+  at::Tensor h = at::empty({n}, at::TensorOptions().dtype((at::ScalarType)code));
   const size_t nb = (size_t)n * h.element_size();
   if (nb && std::fread(h.data_ptr(), 1, nb, f) != nb) throw std::runtime_error("load: truncated file");
   return h.to(dev);
@@ -1131,8 +1163,11 @@ void put_kv(std::FILE* f, const KV& kv) {
 KV get_kv(std::FILE* f, at::Device dev) {
   KV kv;
   kv.n = get_i64(f);
-  kv.kw = (int)get_i64(f);
-  kv.vw = (int)get_i64(f);
+  const int64_t kw = get_i64(f), vw = get_i64(f);
+  if (kv.n < 0 || kw < -1 || vw < -1 || kw > (1 << 30) || vw > (1 << 30))
+    throw std::runtime_error("load: corrupt KV header");
+  kv.kw = (int)kw;
+  kv.vw = (int)vw;
   kv.kdata = get_t(f, dev);
   kv.koff = get_t(f, dev);
   kv.vdata = get_t(f, dev);
@@ -1147,25 +1182,42 @@ void MapReduce::save(const std::string& path) const {
   write_file(rank_path(path, *comm_));
 }
 
-void MapReduce::write_file(const std::string& p) const {
-  std::FILE* f = std::fopen(p.c_str(), "wb");
-  if (!f) fail("Could not open checkpoint file " + p);
-  std::fwrite(kMagic, 1, 8, f);
-  if (kv) {
-    put_i64(f, 0);
-    put_kv(f, *kv);
-  } else {
-    put_i64(f, 1);
-    put_kv(f, kmv->keys);
-    put_i64(f, kmv->nkey);
-    put_i64(f, kmv->nval);
-    put_i64(f, kmv->vw);
-    put_t(f, kmv->vdata);
-    put_t(f, kmv->voff);
-    put_t(f, kmv->seg);
+namespace {
+struct FileCloser {
+  void operator()(std::FILE* f) const {
+    if (f) std::fclose(f);
   }
-  wsize += std::ftell(f);
-  std::fclose(f);
+};
+using FilePtr = std::unique_ptr<std::FILE, FileCloser>;
+}  // namespace
+
+void MapReduce::write_file(const std::string& p) const {
+  FilePtr f(std::fopen(p.c_str(), "wb"));
+  if (!f) fail("Could not open checkpoint file " + p);
+  try {
+    if (std::fwrite(kMagic, 1, 8, f.get()) != 8) throw std::runtime_error("save: write failed");
+    if (kv) {
+      put_i64(f.get(), 0);
+      put_kv(f.get(), *kv);
+    } else {
+      put_i64(f.get(), 1);
+      put_kv(f.get(), kmv->keys);
+      put_i64(f.get(), kmv->nkey);
+      put_i64(f.get(), kmv->nval);
+      put_i64(f.get(), kmv->vw);
+      put_t(f.get(), kmv->vdata);
+      put_t(f.get(), kmv->voff);
+      put_t(f.get(), kmv->seg);
+    }
+    const long bytes = std::ftell(f.get());
+    // a full disk shows up at the final flush: never leave a truncated file that looks valid
+    if (std::fclose(f.release()) != 0) throw std::runtime_error("save: close failed (disk full?)");
+    wsize += bytes;
+  } catch (...) {
+    f.reset();
+    std::remove(p.c_str());
+    throw;
+  }
 }
 
 uint64_t MapReduce::load(const std::string& path) {
@@ -1174,38 +1226,38 @@ uint64_t MapReduce::load(const std::string& path) {
 }
 
 int64_t MapReduce::read_file(const std::string& p) {
-  std::FILE* f = std::fopen(p.c_str(), "rb");
+  FilePtr f(std::fopen(p.c_str(), "rb"));
   if (!f) fail("Could not open checkpoint file " + p);
   char magic[8];
-  if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, kMagic, 8) != 0) {
-    std::fclose(f);
+  if (std::fread(magic, 1, 8, f.get()) != 8 || std::memcmp(magic, kMagic, 8) != 0)
     fail("Not a gpu_mapreduce_amd checkpoint: " + p);
-  }
   int64_t n = 0;
-  try {
-    if (get_i64(f) == 0) {
-      kv = get_kv(f, device());
-      kmv.reset();
-      n = kv->n;
-    } else {
-      KMV m;
-      m.keys = get_kv(f, device());
-      m.nkey = get_i64(f);
-      m.nval = get_i64(f);
-      m.vw = (int)get_i64(f);
-      m.vdata = get_t(f, device());
-      m.voff = get_t(f, device());
-      m.seg = get_t(f, device());
-      kmv = m;
-      kv.reset();
-      n = m.nkey;
-    }
-  } catch (...) {
-    std::fclose(f);
-    throw;
+  const int64_t kind = get_i64(f.get());
+  if (kind == 0) {
+    KV k = get_kv(f.get(), device());
+    guard::check_kv(k, "load");  // offsets/arena sizes consistent before any kernel reads them
+    kv = k;
+    kmv.reset();
+    n = kv->n;
+  } else if (kind == 1) {
+    KMV m;
+    m.keys = get_kv(f.get(), device());
+    m.nkey = get_i64(f.get());
+    m.nval = get_i64(f.get());
+    const int64_t vw = get_i64(f.get());
+    if (m.nkey < 0 || m.nval < 0 || vw < -1 || vw > (1 << 30)) throw std::runtime_error("load: corrupt KMV header");
+    m.vw = (int)vw;
+    m.vdata = get_t(f.get(), device());
+    m.voff = get_t(f.get(), device());
+    m.seg = get_t(f.get(), device());
+    guard::check_kmv(m, "load");
+    kmv = m;
+    kv.reset();
+    n = m.nkey;
+  } else {
+    fail("load: corrupt checkpoint kind in " + p);
   }
-  rsize += std::ftell(f);
-  std::fclose(f);
+  rsize += std::ftell(f.get());
   return n;
 }
 

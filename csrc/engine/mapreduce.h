@@ -45,13 +45,26 @@ using ReduceBatchFn = std::function<void(const KMV& src, KeyValue& kv)>;
 
 struct Settings {
   int mapstyle = 0;    // 0 chunk, 1 stride, 2 dynamic work queue
-  int all2all = 1;     // accepted; the shuffle is always one RCCL all-to-all per column
+  int all2all = 1;     // 1 grouped all-to-all rounds, 0 ring-ordered pairwise steps (shuffle.cpp)
   int verbosity = 0;   // 0 none, 1 totals, 2 per-proc histograms
   int timer = 0;       // 0 none, 1 barrier + rank-0 time, 2 per-proc histogram
   int memsize = 64;    // MB per page (negative: bytes); sets the host block size of long KMV values
   int minpage = 0, maxpage = 0, freepage = 1, outofcore = 0, zeropage = 0;
   int keyalign = 4, valuealign = 4;
   std::string fpath = ".";
+  // ---- MI355X-native settings
+  // receive cap per shuffle round in bytes; 0 = the reference's 2 pages
+  // (2 x memsize, src/mapreduce.cpp:418)
+  int64_t chunk_bytes = 0;
+  // HBM budget of this MR's data in bytes (0 = maxpage x memsize if maxpage
+  // > 0, else unlimited): an aggregate whose received data would exceed it
+  // lands in pinned host memory, and convert / sort_keys / sort_values run
+  // out of core in budget-sized runs + a device merge
+  int64_t hbm_budget = 0;
+  // pinned host bytes the spill tier may hold before it writes to disk (0 = unlimited)
+  int64_t host_budget = 0;
+  // HIP streams the pipelined apps overlap (H2D copy / compute / shuffle)
+  int streams = 2;
 };
 
 class MapReduce {
@@ -174,6 +187,9 @@ class MapReduce {
   void run_host_kmv(const KMV& kmv, const std::function<void(char*, int, char*, int, int*)>& fn);
   void histo(double v, const char* heading) const;
   int64_t block_bytes() const;
+  // shuffle options from the settings
+  ExchangeOpts xopts() const;
+  int64_t budget() const;
 
   void write_file(const std::string& p) const;
   int64_t read_file(const std::string& p);

@@ -1,0 +1,244 @@
+// Native RCCL transport + peer monitor (see rccl.h).
+#include "rccl.h"
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "guard.h"
+
+namespace mrh {
+
+namespace {
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+int env_int(const char* k, int d) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atoi(v) : d;
+}
+double env_f(const char* k, double d) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atof(v) : d;
+}
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("mrhip rccl: ") + what + ": " + hipGetErrorString(e));
+}
+constexpr int64_t kPoison = -(int64_t(1) << 40);
+}  // namespace
+
+// ====================================================================== Monitor
+
+Monitor::Monitor(c10::intrusive_ptr<c10d::Store> root, int rank, int size)
+    : store_(std::move(root)), rank_(rank), size_(size), last_val_(size, -1), last_change_(size, now_s()) {
+  peer_timeout_ = env_f("MRH_PEER_TIMEOUT", 5.0);
+  store_->add(hb_key(rank_), 1);  // exists before any peer checks it
+  thread_ = std::thread([this] { beat_loop(); });
+}
+
+Monitor::~Monitor() {
+  if (!failed_) retire();  // orderly teardown is not a crash
+  stop_ = true;
+  if (thread_.joinable()) thread_.join();
+}
+
+void Monitor::beat_loop() {
+  const int ms = std::max(10, env_int("MRH_HEARTBEAT_MS", 250));
+  while (!stop_) {
+    for (int t = 0; t < ms && !stop_; t += 10) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    if (stop_ || poisoned_) break;
+    try {
+      store_->add(hb_key(rank_), 1);
+    } catch (const std::exception&) {
+      break;  // store server gone: the job is ending one way or another
+    }
+  }
+}
+
+void Monitor::retire() {
+  if (retired_.exchange(true)) return;
+  try {
+    store_->set("mrh/bye/" + std::to_string(rank_), std::vector<uint8_t>{1});
+  } catch (const std::exception&) {
+  }
+}
+
+void Monitor::poison(const std::string& why) {
+  if (poisoned_.exchange(true)) return;
+  failed_ = true;
+  try {
+    store_->set("mrh/why/" + std::to_string(rank_), std::vector<uint8_t>(why.begin(), why.end()));
+    store_->add(hb_key(rank_), kPoison);
+  } catch (const std::exception&) {
+    // store unreachable: peers detect the silent counter instead
+  }
+}
+
+void Monitor::check() {
+  std::lock_guard<std::mutex> l(mu_);
+  if (failed_ && !why_.empty()) throw PeerFailure(why_);
+  const double t = now_s();
+  static const double gap = env_int("MRH_MONITOR_MS", 50) * 1e-3;
+  if (t - last_check_ < gap) return;
+  last_check_ = t;
+  std::vector<std::string> keys;
+  for (int r = 0; r < size_; ++r) keys.push_back(hb_key(r));
+  std::vector<std::vector<uint8_t>> vals;
+  try {
+    vals = store_->multiGet(keys);
+  } catch (const std::exception& e) {
+    failed_ = true;
+    why_ = std::string("mrhip: rendezvous store unreachable (rank 0 gone?): ") + e.what();
+    throw PeerFailure(why_);
+  }
+  for (int r = 0; r < size_; ++r) {
+    if (r == rank_) continue;
+    const int64_t v = std::atoll(std::string(vals[r].begin(), vals[r].end()).c_str());
+    if (v < 0) {
+      std::string why;
+      try {
+        auto w = store_->get("mrh/why/" + std::to_string(r));
+        why.assign(w.begin(), w.end());
+      } catch (const std::exception&) {
+      }
+      failed_ = true;
+      why_ = "mrhip: rank " + std::to_string(r) + " failed: " + why;
+      throw PeerFailure(why_);
+    }
+    if (v != last_val_[r]) {
+      last_val_[r] = v;
+      last_change_[r] = t;
+    } else if (t - last_change_[r] > peer_timeout_) {
+      bool bye = false;
+      try {
+        bye = store_->check({"mrh/bye/" + std::to_string(r)});
+      } catch (const std::exception&) {
+      }
+      if (bye) continue;
+      failed_ = true;
+      why_ = "mrhip: rank " + std::to_string(r) + " stopped responding (no heartbeat for " +
+             std::to_string((int)(t - last_change_[r])) + " s): process crashed or was killed";
+      throw PeerFailure(why_);
+    }
+  }
+}
+
+// ====================================================================== Rccl
+
+void Rccl::check(ncclResult_t r, const char* what) {
+  if (r == ncclSuccess || r == ncclInProgress) return;
+  std::string msg = std::string("mrhip rccl: ") + what + " failed: " + ncclGetErrorString(r);
+  if (comm_) {
+    const char* last = ncclGetLastError(comm_);
+    if (last && *last) msg += std::string(" (") + last + ")";
+  }
+  throw std::runtime_error(msg);
+}
+
+Rccl::Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>& store, const std::string& tag)
+    : rank_(rank), size_(size) {
+  hip_ok(hipSetDevice(device), "hipSetDevice");
+  ncclUniqueId id;
+  if (size == 1) {
+    check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  } else {
+    if (!store) throw std::runtime_error("mrhip rccl: multi-rank communicator needs the rendezvous store");
+    const std::string key = "mrh/rccl_id/" + tag;
+    if (rank == 0) {
+      check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+      store->set(key, std::vector<uint8_t>((uint8_t*)&id, (uint8_t*)&id + sizeof(id)));
+    } else {
+      auto b = store->get(key);  // bounded by the store timeout (MRH_COMM_TIMEOUT)
+      if (b.size() != sizeof(id)) throw std::runtime_error("mrhip rccl: bad unique id in store");
+      std::memcpy(&id, b.data(), sizeof(id));
+    }
+  }
+  check(ncclCommInitRank(&comm_, size, id, rank), "ncclCommInitRank");
+  int lo = 0, hi = 0;
+  hip_ok(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+  hip_ok(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
+  ev_.resize(64);
+  for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+}
+
+Rccl::~Rccl() {
+  if (stream_) {
+    if (!aborted_) (void)hipStreamSynchronize(stream_);
+  }
+  if (comm_) {
+    if (aborted_) {
+      // already aborted: nothing left to release
+    } else {
+      (void)ncclCommDestroy(comm_);
+    }
+  }
+  for (auto& e : ev_) (void)hipEventDestroy(e);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Rccl::fence_in(hipStream_t s) {
+  hipEvent_t e = ev_[ev_next_++ % ev_.size()];
+  hip_ok(hipEventRecord(e, s), "hipEventRecord");
+  hip_ok(hipStreamWaitEvent(stream_, e, 0), "hipStreamWaitEvent");
+}
+
+hipEvent_t Rccl::fence_out() {
+  hipEvent_t e = ev_[ev_next_++ % ev_.size()];
+  hip_ok(hipEventRecord(e, stream_), "hipEventRecord");
+  return e;
+}
+
+hipEvent_t Rccl::sendrecv_async(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
+  if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
+  fence_in(s);
+  check(ncclGroupStart(), "ncclGroupStart");
+  for (const Xfer& x : recvs)
+    if (x.bytes > 0) check(ncclRecv(x.ptr, (size_t)x.bytes, ncclUint8, x.peer, comm_, stream_), "ncclRecv");
+  for (const Xfer& x : sends)
+    if (x.bytes > 0) check(ncclSend(x.ptr, (size_t)x.bytes, ncclUint8, x.peer, comm_, stream_), "ncclSend");
+  check(ncclGroupEnd(), "ncclGroupEnd");
+  return fence_out();
+}
+
+void Rccl::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
+  hipEvent_t e = sendrecv_async(sends, recvs, s);
+  hip_ok(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
+}
+
+void Rccl::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s) {
+  if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
+  fence_in(s);
+  check(ncclAllReduce(buf, buf, count, dt, op, comm_, stream_), "ncclAllReduce");
+  hip_ok(hipStreamWaitEvent(s, fence_out(), 0), "hipStreamWaitEvent");
+}
+
+void Rccl::allgather(const void* send, void* recv, size_t bytes, hipStream_t s) {
+  if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
+  fence_in(s);
+  check(ncclAllGather(send, recv, bytes, ncclUint8, comm_, stream_), "ncclAllGather");
+  hip_ok(hipStreamWaitEvent(s, fence_out(), 0), "hipStreamWaitEvent");
+}
+
+void Rccl::broadcast(void* buf, size_t bytes, int root, hipStream_t s) {
+  if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
+  fence_in(s);
+  check(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
+  hip_ok(hipStreamWaitEvent(s, fence_out(), 0), "hipStreamWaitEvent");
+}
+
+ncclResult_t Rccl::async_error() {
+  if (!comm_ || aborted_) return ncclSuccess;
+  ncclResult_t r = ncclSuccess;
+  if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return ncclSystemError;
+  return r;
+}
+
+void Rccl::abort() {
+  if (aborted_ || !comm_) return;
+  aborted_ = true;
+  (void)ncclCommAbort(comm_);
+}
+
+}  // namespace mrh

@@ -1,0 +1,139 @@
+// Native RCCL transport and peer-failure monitor for the device engine.
+//
+// The reference moves every byte through MPI (src/irregular.cpp:269-363,
+// src/mapreduce.cpp:569-623, 893-1036) and handles failure by MPI_Abort from
+// the failing rank (src/error.cpp:47-57). On MI355X the data plane is RCCL
+// over xGMI, driven directly (not through c10d), because the shuffle needs
+// what c10d's all-to-all cannot give:
+//
+//  * grouped point-to-point rounds (ncclGroupStart / ncclSend / ncclRecv /
+//    ncclGroupEnd) whose per-peer send and receive buffers are arbitrary device
+//    pointers: a chunk of a bucket is sent from where it lies and received
+//    straight into its final place in the output KV, so a chunked exchange
+//    needs no per-round pack or unpack copies;
+//  * a dedicated communication stream with event fences, so a round can be in
+//    flight on the xGMI links while the compute stream works on the previous
+//    one;
+//  * fail-fast: every host wait on RCCL work is a polled wait that also checks
+//    the communicator's async error and the peer monitor below, and calls
+//    ncclCommAbort (which releases RCCL kernels spinning on a dead peer), so a
+//    rank failure ends the job on every rank in seconds instead of at a
+//    600 s watchdog.
+//
+// Bootstrap without MPI: rank 0 creates the ncclUniqueId and publishes it in
+// the job's rendezvous store (the c10d TCPStore that torchrun / the native
+// launcher already run); the other ranks read it and ncclCommInitRank.
+//
+// Monitor: each rank of a multi-rank job runs a heartbeat thread that adds 1
+// to its store counter every MRH_HEARTBEAT_MS (default 250 ms). Any wait that
+// polls checks all peers' counters in one multiGet: a counter that stops
+// moving for MRH_PEER_TIMEOUT seconds (default 5) means that process is gone
+// (crashed, killed, aborted); a counter driven negative means the peer hit a
+// fatal error and poisoned the job (poison(), called when a MapReduce op
+// throws on a multi-rank communicator), with the reason in a side key.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <torch/csrc/distributed/c10d/Store.hpp>
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace mrh {
+
+// a peer failed (or poisoned the job): the op that observed it cannot complete
+struct PeerFailure : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+class Monitor {
+ public:
+  // root: the job's root store (never a per-split prefix store); rank/size in
+  // the WORLD (every process of the job heartbeats exactly once)
+  Monitor(c10::intrusive_ptr<c10d::Store> root, int rank, int size);
+  ~Monitor();
+  Monitor(const Monitor&) = delete;
+  Monitor& operator=(const Monitor&) = delete;
+
+  // throws PeerFailure if a peer poisoned the job or stopped heartbeating;
+  // rate limited (at most one store round trip per MRH_MONITOR_MS, default 50 ms)
+  void check();
+  // tell every peer this rank hit a fatal error (idempotent)
+  void poison(const std::string& why);
+  bool failed() const { return failed_.load(); }
+  // clean exit: peers stop treating this rank's silent counter as a crash
+  void retire();
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+
+ private:
+  void beat_loop();
+  std::string hb_key(int r) const { return "mrh/hb/" + std::to_string(r); }
+
+  c10::intrusive_ptr<c10d::Store> store_;
+  int rank_, size_;
+  std::thread thread_;
+  std::atomic<bool> stop_{false}, failed_{false}, poisoned_{false}, retired_{false};
+  std::mutex mu_;
+  std::vector<int64_t> last_val_;
+  std::vector<double> last_change_;
+  double last_check_ = 0;
+  double peer_timeout_ = 5.0;
+  std::string why_;
+};
+
+struct Xfer {
+  int peer;
+  void* ptr;
+  int64_t bytes;
+};
+
+class Rccl {
+ public:
+  // store may be null when size == 1 (the id is created locally)
+  Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>& store, const std::string& tag);
+  ~Rccl();
+  Rccl(const Rccl&) = delete;
+  Rccl& operator=(const Rccl&) = delete;
+
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  hipStream_t stream() const { return stream_; }
+
+  // ---- collectives enqueued on the communication stream, fenced against `s`:
+  // they start after the work already queued on `s`, and work queued on `s`
+  // afterwards sees their results (no host synchronisation)
+  // one grouped round of point-to-point transfers (any peer, self included)
+  void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s);
+  // same, but the compute stream is NOT made to wait: returns an event that
+  // completes with the round (the caller fences when it needs the data)
+  hipEvent_t sendrecv_async(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s);
+  void allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s);
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s);
+  void broadcast(void* buf, size_t bytes, int root, hipStream_t s);
+
+  // nccl async error (ncclSuccess / ncclInProgress when healthy)
+  ncclResult_t async_error();
+  // tear the communicator down (unblocks kernels waiting on a dead peer)
+  void abort();
+  bool aborted() const { return aborted_; }
+
+ private:
+  void fence_in(hipStream_t s);
+  hipEvent_t fence_out();
+  void check(ncclResult_t r, const char* what);
+
+  int rank_, size_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  std::vector<hipEvent_t> ev_;  // ring of fence events
+  size_t ev_next_ = 0;
+  bool aborted_ = false;
+};
+
+}  // namespace mrh

@@ -1,27 +1,47 @@
-// Distributed KV movement over a c10d ProcessGroup: backend "nccl" (= RCCL on
-// ROCm, all-to-all over xGMI between the GPUs of a node) for device tensors,
-// "gloo" for the CPU path. Replaces MR-MPI's Irregular class and the
-// collectives embedded in MapReduce::aggregate/gather/broadcast
-// (reference src/irregular.cpp:95-363, src/mapreduce.cpp:385-623,893-1036).
+// Distributed KV movement: MapReduce::aggregate / gather / broadcast on the
+// communicator's data plane (comm.h: native RCCL over xGMI for the device
+// engine, a c10d process group for the host engine). Replaces MR-MPI's
+// Irregular class and the collectives embedded in aggregate/gather/broadcast
+// (reference src/irregular.cpp:95-363, src/mapreduce.cpp:385-623, 893-1036).
 //
-// Design differences from the reference:
-//  * one stable device-side partition (radix pass on the destination rank)
-//    turns the KV into P contiguous buckets, so the send buffers ARE the
-//    sorted columns: no pack loop, no per-KV memcpy;
-//  * pair counts, byte totals and layouts travel in ONE int64 [P x 5] header
-//    all-to-all (replaces the Alltoall + Reduce_scatter + 3 Allreduce of
-//    Irregular::setup); a rank with an empty KV never forces a conversion;
-//  * the payload moves as at most 4 column all-to-alls (key lengths, key
-//    bytes, value lengths, value bytes), all in flight before one wait, with
-//    64-bit byte counts: no INTMAX limit and no 0.9x scale-back retry loop.
-#include <torch/csrc/distributed/c10d/Types.hpp>
+// Exchange protocol — at most two host synchronisations per exchange:
+//  1. partition (device, shuffle.hip): owner per pair + per-(owner, block)
+//     pair/byte tables, scanned, reduced to this rank's header row
+//     {pairs, key bytes, value bytes} x P + {key width code, value width code};
+//  2. ONE allgather of the header rows (sync #1): every rank now knows the
+//     whole P x P traffic matrix, so every rank derives locally, identically:
+//     the global column layout, what it receives from whom, and the number of
+//     rounds R = max over receivers of ceil(received bytes / chunk_bytes) —
+//     the receive cap of the reference (2 pages, src/mapreduce.cpp:418;
+//     src/irregular.cpp:113-164), made deterministic: no 0.9x scale-back
+//     retry loop (src/mapreduce.cpp:498-513), no INTMAX limits;
+//  3. pack (device): one stable scatter into owner buckets; fixed-width
+//     columns move straight into the send buffer, variable ones through a
+//     lengths scan + one byte copy. The input KV is released here;
+//  4. piece table (variable columns and R > 1 only, sync #2): bucket d is cut
+//     into R pieces of equal pair count; their byte sizes go to the receivers
+//     in one small exchange;
+//  5. R lock-step rounds (reference :426-432) of ONE grouped send/recv each
+//     (every column of every peer in one RCCL group): piece k of every bucket
+//     is sent from where it lies and received straight into its final place in
+//     the output (sender-major, then piece order — the same order as a single
+//     round, so the result does not depend on the cap). With a host sink
+//     (out-of-core aggregate) a round lands in one of two HBM staging buffers
+//     and drains to pinned host memory on a copy stream while the next round
+//     is on the wire: HBM holds the send buffer + 2 rounds, never the output.
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPStream.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <stdexcept>
 
+#include "../kernels/hashfn.h"
 #include "../kernels/launch.h"
+#include "comm.h"
+#include "guard.h"
 #include "kv.h"
-#include <ATen/hip/HIPContext.h>
 
 namespace mrh {
 
@@ -35,117 +55,488 @@ T* P0(const at::Tensor& t) {
 }
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream(); }
 
-using PG = c10::intrusive_ptr<c10d::ProcessGroup>;
+constexpr int64_t kEmpty = -2;  // width code of a rank with no pairs
 
-void wait(c10::intrusive_ptr<c10d::Work> w) { w->wait(); }
-
-at::Tensor allreduce(at::Tensor t, c10d::ReduceOp::RedOpType op, const PG& pg) {
-  std::vector<at::Tensor> v{t};
-  c10d::AllreduceOptions o;
-  o.reduceOp = c10d::ReduceOp(op);
-  wait(pg->allreduce(v, o));
-  return v[0];
+int global_width(const std::vector<int64_t>& codes) {
+  int64_t w = kEmpty;
+  for (int64_t c : codes) {
+    if (c == kEmpty) continue;
+    if (w == kEmpty) w = c;
+    else if (w != c) return -1;
+  }
+  return (int)w;
 }
 
-// out sized by recv_splits; splits in elements of dim 0
-at::Tensor alltoallv(const at::Tensor& in, const std::vector<int64_t>& send, const std::vector<int64_t>& recv,
-                     const PG& pg) {
-  int64_t tot = 0;
-  for (auto r : recv) tot += r;
-  at::Tensor out = at::empty({tot}, in.options());
-  std::vector<int64_t> s = send, r = recv;
-  at::Tensor inc = in.contiguous();
-  wait(pg->alltoall_base(out, inc, r, s));
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------- host (CPU engine) twins of shuffle.hip
+void cpu_part_count(const int32_t* dest_in, const uint8_t* kd, int kw, const int64_t* koff, const int64_t* voff,
+                    int64_t n, int P, int nb, int tile, int32_t* dest_out, int64_t* cnt, int64_t* kb, int64_t* vb) {
+  std::fill(cnt, cnt + (int64_t)P * nb, 0);
+  if (kb) std::fill(kb, kb + (int64_t)P * nb, 0);
+  if (vb) std::fill(vb, vb + (int64_t)P * nb, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    int d;
+    if (dest_in) {
+      d = dest_in[i];
+    } else {
+      const uint32_t h = koff ? dev::hashlittle(kd + koff[i], koff[i + 1] - koff[i], (uint32_t)P)
+                              : dev::hashlittle(kd + i * kw, kw, (uint32_t)P);
+      d = (int)(h % (uint32_t)P);
+      dest_out[i] = d;
+    }
+    if (d < 0 || d >= P) fail("exchange: destination rank out of range");
+    const int64_t o = (int64_t)d * nb + i / tile;
+    cnt[o]++;
+    if (kb) kb[o] += koff[i + 1] - koff[i];
+    if (vb) vb[o] += voff[i + 1] - voff[i];
+  }
+}
+
+void cpu_part_scatter(const int32_t* dest, int64_t n, int P, int nb, int tile, const int64_t* cbase,
+                      const uint8_t* kd, int kw, const uint8_t* vd, int vw, const int64_t* koff, const int64_t* voff,
+                      uint8_t* ksend, uint8_t* vsend, int64_t* perm, int32_t* klen, int32_t* vlen) {
+  std::vector<int64_t> run((size_t)P);
+  for (int b = 0; b < nb; ++b) {
+    for (int d = 0; d < P; ++d) run[d] = cbase[(int64_t)d * nb + b];
+    for (int64_t i = (int64_t)b * tile; i < std::min<int64_t>(n, (int64_t)(b + 1) * tile); ++i) {
+      const int64_t pos = run[dest[i]]++;
+      if (kw > 0) std::memcpy(ksend + pos * kw, kd + i * kw, kw);
+      if (vw > 0) std::memcpy(vsend + pos * vw, vd + i * vw, vw);
+      if (perm) perm[pos] = i;
+      if (klen) klen[pos] = (int32_t)(koff[i + 1] - koff[i]);
+      if (vlen) vlen[pos] = (int32_t)(voff[i + 1] - voff[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- one variable column of the send side
+struct VarCol {
+  at::Tensor len;   // int32 [n] in send order
+  at::Tensor soff;  // int64 [n+1] send byte offsets
+  at::Tensor data;  // send bytes
+};
+
+VarCol pack_var(const at::Tensor& data, const at::Tensor& off, const at::Tensor& perm, const at::Tensor& len,
+                int64_t n, int64_t total_bytes, at::Device dev) {
+  VarCol c;
+  c.len = len;
+  c.soff = exclusive_scan(len);
+  c.data = at::empty({total_bytes}, opt(dev, at::kByte));
+  if (dev.is_cuda()) {
+    k::copy_var_i64(P0<uint8_t>(data), P0<int64_t>(off), P0<int64_t>(perm), n, P0<uint8_t>(c.data),
+                    P0<int64_t>(c.soff), cur_stream());
+  } else {
+    const uint8_t* s = P0<uint8_t>(data);
+    const int64_t* so = P0<int64_t>(off);
+    const int64_t* pm = P0<int64_t>(perm);
+    const int64_t* doff = P0<int64_t>(c.soff);
+    uint8_t* d = P0<uint8_t>(c.data);
+    for (int64_t j = 0; j < n; ++j) std::memcpy(d + doff[j], s + so[pm[j]], (size_t)(so[pm[j] + 1] - so[pm[j]]));
+  }
+  return c;
+}
+
+// piece k of a bucket of c pairs covers [c*k/R, c*(k+1)/R)
+int64_t piece_lo(int64_t c, int k, int R) { return c * k / R; }
+
+}  // namespace
+
+// =========================================================================== exchange
+
+KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const ExchangeOpts& o, ShuffleStats* st) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const at::Device dev = comm.device();
+  if (!comm.distributed()) {
+    if (st) st->send_pairs = st->recv_pairs = kv.n;
+    return kv;
+  }
+  const int P = comm.size(), me = comm.rank();
+  const int64_t n = kv.n;
+  if (kv.n && kv.device() != dev) kv = kv_to(kv, dev);
+  const bool cuda = dev.is_cuda();
+  const hipStream_t s = cuda ? cur_stream() : nullptr;
+  const int tile = cuda ? k::part_tile() : 4096;
+  const int nb = (int)cdiv(n, tile);
+
+  // ---- 1. partition tables
+  const bool kvar0 = !kv.kfixed(), vvar0 = !kv.vfixed();
+  at::Tensor dest;
+  at::Tensor cnt = at::empty({(int64_t)P * nb}, opt(dev, at::kLong));
+  at::Tensor kbt = kvar0 ? at::empty({(int64_t)P * nb}, opt(dev, at::kLong)) : at::Tensor();
+  at::Tensor vbt = vvar0 ? at::empty({(int64_t)P * nb}, opt(dev, at::kLong)) : at::Tensor();
+  const bool hashing = !dest_given.defined();
+  if (!hashing) {
+    dest = dest_given.to(dev).to(at::kInt).contiguous();
+    if (dest.numel() != n) fail("exchange: dest must have one entry per pair");
+  } else {
+    dest = at::empty({n}, opt(dev, at::kInt));
+  }
+  if (cuda) {
+    k::part_count(hashing ? nullptr : P0<int32_t>(dest), P0<uint8_t>(kv.kdata), kv.kw,
+                  kvar0 ? P0<int64_t>(kv.koff) : nullptr, vvar0 ? P0<int64_t>(kv.voff) : nullptr, n, P, nb,
+                  hashing ? P0<int32_t>(dest) : nullptr, P0<int64_t>(cnt), P0<int64_t>(kbt), P0<int64_t>(vbt), s);
+  } else {
+    cpu_part_count(hashing ? nullptr : P0<int32_t>(dest), P0<uint8_t>(kv.kdata), kv.kw,
+                   kvar0 ? P0<int64_t>(kv.koff) : nullptr, vvar0 ? P0<int64_t>(kv.voff) : nullptr, n, P, nb, tile,
+                   hashing ? P0<int32_t>(dest) : nullptr, P0<int64_t>(cnt), P0<int64_t>(kbt), P0<int64_t>(vbt));
+  }
+  at::Tensor cs = exclusive_scan(cnt);
+  at::Tensor ks = kvar0 ? exclusive_scan(kbt) : at::Tensor();
+  at::Tensor vs = vvar0 ? exclusive_scan(vbt) : at::Tensor();
+  const int64_t kcode = n ? kv.kw : kEmpty, vcode = n ? kv.vw : kEmpty;
+  const int64_t H = 3 * (int64_t)P + 2;
+  at::Tensor hdr = at::empty({H}, opt(dev, at::kLong));
+  if (cuda) {
+    k::part_header(P0<int64_t>(cs), P0<int64_t>(ks), P0<int64_t>(vs), P, nb, kv.kfixed() ? kv.kw : -1,
+                   kv.vfixed() ? kv.vw : -1, kcode, vcode, P0<int64_t>(hdr), s);
+  } else {
+    int64_t* h = P0<int64_t>(hdr);
+    const int64_t *c = P0<int64_t>(cs), *kk = P0<int64_t>(ks), *vv = P0<int64_t>(vs);
+    for (int d = 0; d < P; ++d) {
+      const int64_t a = (int64_t)d * nb, b = a + nb, cc = c[b] - c[a];
+      h[3 * d] = cc;
+      h[3 * d + 1] = kvar0 ? kk[b] - kk[a] : cc * kv.kw;
+      h[3 * d + 2] = vvar0 ? vv[b] - vv[a] : cc * kv.vw;
+    }
+    h[3 * P] = kcode;
+    h[3 * P + 1] = vcode;
+  }
+
+  // ---- 2. one allgather of the header rows (host sync #1)
+  at::Tensor all = at::empty({P * H}, opt(dev, at::kLong));
+  comm.allgather_bytes(hdr.data_ptr(), all.data_ptr(), H * 8);
+  comm.host_wait();
+  at::Tensor allh = all.to(at::kCPU);
+  const int64_t* A = allh.data_ptr<int64_t>();
+  auto C = [&](int src, int d) { return A[src * H + 3 * d]; };
+  auto KB = [&](int src, int d) { return A[src * H + 3 * d + 1]; };
+  auto VB = [&](int src, int d) { return A[src * H + 3 * d + 2]; };
+  std::vector<int64_t> kcodes(P), vcodes(P);
+  for (int r = 0; r < P; ++r) {
+    kcodes[r] = A[r * H + 3 * P];
+    vcodes[r] = A[r * H + 3 * P + 1];
+  }
+  int kw = global_width(kcodes), vw = global_width(vcodes);
+  if (kw == kEmpty && vw == kEmpty) {
+    // nobody has pairs: no column traffic at all (every rank takes this branch)
+    if (st) st->seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return empty_kv(dev, kv.kw, kv.vw);
+  }
+  if (kw < 0 && kv.kfixed()) kv = to_var_keys(kv);  // same bytes, now with offsets
+  if (vw < 0 && kv.vfixed()) kv = to_var_values(kv);
+  const bool kvar = kw < 0, vvar = vw < 0;
+  std::vector<int64_t> rcount(P), rkb(P), rvb(P);
+  int64_t nrecv = 0, rkb_tot = 0, rvb_tot = 0, sent_pairs = 0, sent_bytes = 0;
+  for (int r = 0; r < P; ++r) {
+    rcount[r] = C(r, me);
+    rkb[r] = KB(r, me);
+    rvb[r] = VB(r, me);
+    nrecv += rcount[r];
+    rkb_tot += rkb[r];
+    rvb_tot += rvb[r];
+    sent_pairs += C(me, r);
+    sent_bytes += KB(me, r) + VB(me, r);
+  }
+  const int64_t lenb = (kvar ? 4 : 0) + (vvar ? 4 : 0);
+  int R = 1;
+  if (o.chunk_bytes > 0) {
+    int64_t worst = 1;
+    for (int r = 0; r < P; ++r) {
+      int64_t b = 0, c = 0;
+      for (int src = 0; src < P; ++src) {
+        b += KB(src, r) + VB(src, r);
+        c += C(src, r);
+      }
+      worst = std::max<int64_t>(worst, cdiv(b + c * lenb, o.chunk_bytes));
+    }
+    R = (int)std::min<int64_t>(worst, 1 << 16);
+  }
+
+  // ---- 3. pack: stable scatter into owner buckets
+  int64_t my_kb = 0, my_vb = 0;
+  for (int d = 0; d < P; ++d) {
+    my_kb += KB(me, d);
+    my_vb += VB(me, d);
+  }
+  at::Tensor ksend, vsend, perm, klen, vlen;
+  if (!kvar) ksend = at::empty({n * kw}, opt(dev, at::kByte));
+  if (!vvar) vsend = at::empty({n * vw}, opt(dev, at::kByte));
+  if (kvar || vvar) perm = at::empty({n}, opt(dev, at::kLong));
+  if (kvar) klen = at::empty({n}, opt(dev, at::kInt));
+  if (vvar) vlen = at::empty({n}, opt(dev, at::kInt));
+  if (n) {
+    if (cuda) {
+      k::part_scatter(P0<int32_t>(dest), n, P, nb, P0<int64_t>(cs), P0<uint8_t>(kv.kdata), kvar ? -1 : kw,
+                      P0<uint8_t>(kv.vdata), vvar ? -1 : vw, kvar ? P0<int64_t>(kv.koff) : nullptr,
+                      vvar ? P0<int64_t>(kv.voff) : nullptr, P0<uint8_t>(ksend), P0<uint8_t>(vsend),
+                      P0<int64_t>(perm), P0<int32_t>(klen), P0<int32_t>(vlen), s);
+    } else {
+      cpu_part_scatter(P0<int32_t>(dest), n, P, nb, tile, P0<int64_t>(cs), P0<uint8_t>(kv.kdata), kvar ? -1 : kw,
+                       P0<uint8_t>(kv.vdata), vvar ? -1 : vw, kvar ? P0<int64_t>(kv.koff) : nullptr,
+                       vvar ? P0<int64_t>(kv.voff) : nullptr, P0<uint8_t>(ksend), P0<uint8_t>(vsend),
+                       P0<int64_t>(perm), P0<int32_t>(klen), P0<int32_t>(vlen));
+    }
+  }
+  VarCol kc, vc;
+  if (kvar) kc = pack_var(kv.kdata, kv.koff, perm, klen, n, my_kb, dev);
+  if (vvar) vc = pack_var(kv.vdata, kv.voff, perm, vlen, n, my_vb, dev);
+  if (kvar) ksend = kc.data;
+  if (vvar) vsend = vc.data;
+  kv = KV();  // the input is no longer needed: HBM now holds the send buffer, not both
+  dest = perm = cnt = kbt = vbt = cs = ks = vs = at::Tensor();
+
+  // ---- 4. piece byte tables (variable columns, R > 1; host sync #2)
+  // mine[d][c][k] (bytes of my piece k to d, column c in {K, V}), theirs[s][c][k]
+  std::vector<int64_t> mine, theirs;
+  const bool need_tab = (kvar || vvar) && R > 1;
+  if (need_tab) {
+    std::vector<int64_t> start(P + 1, 0);
+    for (int d = 0; d < P; ++d) start[d + 1] = start[d] + C(me, d);
+    at::Tensor tab = at::zeros({(int64_t)P * 2 * R}, opt(dev, at::kLong));
+    at::Tensor rtab = at::empty({(int64_t)P * 2 * R}, opt(dev, at::kLong));
+    at::Tensor kt = at::zeros({(int64_t)P * R}, opt(dev, at::kLong)), vt = at::zeros({(int64_t)P * R}, opt(dev, at::kLong));
+    at::Tensor sdev = at::tensor(start, opt(at::kCPU, at::kLong)).to(dev);
+    for (int c = 0; c < 2; ++c) {
+      const VarCol& col = c == 0 ? kc : vc;
+      if (!(c == 0 ? kvar : vvar)) continue;
+      at::Tensor& t = c == 0 ? kt : vt;
+      if (cuda) {
+        k::piece_bytes(P0<int64_t>(col.soff), P0<int64_t>(sdev), P, R, P0<int64_t>(t), s);
+      } else {
+        const int64_t* so = P0<int64_t>(col.soff);
+        int64_t* tp = P0<int64_t>(t);
+        for (int d = 0; d < P; ++d)
+          for (int k = 0; k < R; ++k) {
+            const int64_t cc = start[d + 1] - start[d];
+            tp[(int64_t)d * R + k] = so[start[d] + piece_lo(cc, k + 1, R)] - so[start[d] + piece_lo(cc, k, R)];
+          }
+      }
+    }
+    tab.view({P, 2, R}).select(1, 0).copy_(kt.view({P, R}));
+    tab.view({P, 2, R}).select(1, 1).copy_(vt.view({P, R}));
+    std::vector<Xfer> xs, xr;
+    for (int p = 0; p < P; ++p) {
+      xs.push_back({p, P0<int64_t>(tab) + (int64_t)p * 2 * R, 16 * (int64_t)R});
+      xr.push_back({p, P0<int64_t>(rtab) + (int64_t)p * 2 * R, 16 * (int64_t)R});
+    }
+    comm.sendrecv(xs, xr);
+    comm.host_wait();
+    at::Tensor both = at::cat({tab, rtab}).to(at::kCPU);
+    const int64_t* bp = both.data_ptr<int64_t>();
+    mine.assign(bp, bp + (int64_t)P * 2 * R);
+    theirs.assign(bp + (int64_t)P * 2 * R, bp + (int64_t)P * 4 * R);
+  }
+  auto pairs_of = [&](int src, int d, int k) { return piece_lo(C(src, d), k + 1, R) - piece_lo(C(src, d), k, R); };
+  // bytes of piece k from src to d in column c (fixed: pairs x width)
+  auto bytes_of = [&](int src, int d, int c, int k) -> int64_t {
+    const int w = c == 0 ? kw : vw;
+    if (w >= 0) return pairs_of(src, d, k) * w;
+    if (R == 1) return c == 0 ? KB(src, d) : VB(src, d);
+    if (src == me) return mine[((int64_t)d * 2 + c) * R + k];
+    if (d == me) return theirs[((int64_t)src * 2 + c) * R + k];
+    fail("exchange: piece table lookup");
+  };
+
+  // ---- 5. output
+  const bool host_sink =
+      cuda && (o.host_sink || (o.hbm_budget > 0 && rkb_tot + rvb_tot + nrecv * (lenb + 8) > o.hbm_budget));
+  const at::Device odev = host_sink ? at::Device(at::kCPU) : dev;
+  auto oopt = [&](at::ScalarType t) {
+    auto x = opt(odev, t);
+    return host_sink ? x.pinned_memory(true) : x;
+  };
+  KV out;
+  out.n = nrecv;
+  out.kw = kw;
+  out.vw = vw;
+  out.kdata = at::empty({kvar ? rkb_tot : nrecv * std::max(kw, 0)}, oopt(at::kByte));
+  out.vdata = at::empty({vvar ? rvb_tot : nrecv * std::max(vw, 0)}, oopt(at::kByte));
+  at::Tensor rklen = kvar ? at::empty({nrecv}, oopt(at::kInt)) : at::Tensor();
+  at::Tensor rvlen = vvar ? at::empty({nrecv}, oopt(at::kInt)) : at::Tensor();
+
+  // per-column send bases (bytes) of bucket d, piece k; receive bases of (src, k)
+  // columns: 0 key bytes, 1 value bytes, 2 key lengths, 3 value lengths
+  struct Col {
+    uint8_t* send;  // this rank's bucketed send buffer
+    uint8_t* recv;  // final output (device sink) or host output (host sink)
+    bool on;
+    int c;          // 0 key, 1 value
+    bool lens;      // int32 lengths column
+  };
+  std::vector<Col> cols = {
+      {P0<uint8_t>(ksend), P0<uint8_t>(out.kdata), kw != 0, 0, false},
+      {P0<uint8_t>(vsend), P0<uint8_t>(out.vdata), vw != 0, 1, false},
+      {kvar ? P0<uint8_t>(kc.len) : nullptr, P0<uint8_t>(rklen), kvar, 0, true},
+      {vvar ? P0<uint8_t>(vc.len) : nullptr, P0<uint8_t>(rvlen), vvar, 1, true},
+  };
+  // running offsets: send side per (col, d), receive side per (col, src)
+  std::vector<std::vector<int64_t>> soff(4, std::vector<int64_t>(P, 0)), roff(4, std::vector<int64_t>(P, 0));
+  for (int ci = 0; ci < 4; ++ci) {
+    if (!cols[ci].on) continue;
+    int64_t a = 0, b = 0;
+    for (int p = 0; p < P; ++p) {
+      soff[ci][p] = a;
+      roff[ci][p] = b;
+      const int c = cols[ci].c;
+      if (cols[ci].lens) {
+        a += C(me, p) * 4;
+        b += C(p, me) * 4;
+      } else {
+        a += c == 0 ? KB(me, p) : VB(me, p);
+        b += c == 0 ? KB(p, me) : VB(p, me);
+      }
+    }
+  }
+  auto piece_col_bytes = [&](int ci, int src, int d, int k) -> int64_t {
+    return cols[ci].lens ? pairs_of(src, d, k) * 4 : bytes_of(src, d, cols[ci].c, k);
+  };
+
+  // ---- 6. rounds
+  const hipStream_t cs_ = s;
+  at::Tensor stage[2];
+  hipEvent_t drained[2] = {nullptr, nullptr};
+  c10::optional<c10::hip::HIPStream> copy_stream;
+  int64_t stage_bytes = 0;
+  if (host_sink) {
+    for (int k = 0; k < R; ++k) {
+      int64_t b = 0;
+      for (int ci = 0; ci < 4; ++ci)
+        if (cols[ci].on)
+          for (int src = 0; src < P; ++src) b += piece_col_bytes(ci, src, me, k);
+      stage_bytes = std::max(stage_bytes, b);
+    }
+    for (auto& t : stage) t = at::empty({std::max<int64_t>(stage_bytes, 1)}, opt(dev, at::kByte));
+    copy_stream = c10::hip::getStreamFromPool(false, dev.index());
+    for (auto& e : drained) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  }
+  for (int k = 0; k < R; ++k) {
+    guard::fault_point("exchange_round", me);
+    std::vector<Xfer> xs, xr;
+    struct Drain {
+      uint8_t* dst;
+      int64_t stage_off, bytes;
+    };
+    std::vector<Drain> drains;
+    int64_t sbuf = 0;
+    for (int ci = 0; ci < 4; ++ci) {
+      if (!cols[ci].on) continue;
+      for (int p = 0; p < P; ++p) {
+        const int64_t sb = piece_col_bytes(ci, me, p, k);
+        xs.push_back({p, cols[ci].send + soff[ci][p], sb});
+        soff[ci][p] += sb;
+        const int64_t rb = piece_col_bytes(ci, p, me, k);
+        if (host_sink) {
+          xr.push_back({p, P0<uint8_t>(stage[k % 2]) + sbuf, rb});
+          drains.push_back({cols[ci].recv + roff[ci][p], sbuf, rb});
+          sbuf += rb;
+        } else {
+          xr.push_back({p, cols[ci].recv + roff[ci][p], rb});
+        }
+        roff[ci][p] += rb;
+      }
+    }
+    if (!host_sink) {
+      if (o.all2all) {
+        comm.sendrecv(xs, xr);
+      } else {
+        for (int j = 0; j < P; ++j) {  // ring order: step j pairs me -> me+j with me-j -> me
+          const int to = (me + j) % P, from = (me - j + P) % P;
+          std::vector<Xfer> s1, r1;
+          for (const Xfer& x : xs)
+            if (x.peer == to) s1.push_back(x);
+          for (const Xfer& x : xr)
+            if (x.peer == from) r1.push_back(x);
+          comm.sendrecv(s1, r1);
+        }
+      }
+      continue;
+    }
+    // staging buffer k%2 is free once the drain of round k-2 finished
+    if (k >= 2) (void)hipStreamWaitEvent(cs_, drained[k % 2], 0);
+    hipEvent_t landed = nullptr;
+    if (comm.uses_rccl()) {
+      landed = comm.rccl()->sendrecv_async(xs, xr, cs_);
+    } else {
+      comm.sendrecv(xs, xr);
+      (void)hipEventCreateWithFlags(&landed, hipEventDisableTiming);
+      (void)hipEventRecord(landed, cs_);
+    }
+    const hipStream_t cp = copy_stream->stream();
+    (void)hipStreamWaitEvent(cp, landed, 0);
+    for (const Drain& d : drains)
+      if (d.bytes)
+        (void)hipMemcpyAsync(d.dst, P0<uint8_t>(stage[k % 2]) + d.stage_off, (size_t)d.bytes, hipMemcpyDeviceToHost,
+                             cp);
+    (void)hipEventRecord(drained[k % 2], cp);
+    if (!comm.uses_rccl()) (void)hipEventDestroy(landed);
+  }
+  if (host_sink) {
+    for (int k = std::max(0, R - 2); k < R; ++k) (void)hipStreamWaitEvent(cs_, drained[k % 2], 0);
+    comm.host_wait();  // pinned host output complete before the host reads it
+    for (auto& e : drained) (void)hipEventDestroy(e);
+  }
+
+  // ---- 7. offsets of variable columns
+  if (kvar) out.koff = exclusive_scan(rklen);
+  if (vvar) out.voff = exclusive_scan(rvlen);
+  if (st) {
+    st->send_pairs += sent_pairs;
+    st->recv_pairs += nrecv;
+    st->send_bytes += sent_bytes;
+    st->recv_bytes += rkb_tot + rvb_tot;
+    st->rounds += R;
+    st->seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
   return out;
 }
 
-std::vector<int64_t> to_vec(const at::Tensor& t) {
-  at::Tensor c = t.to(at::kCPU).to(at::kLong).contiguous();
-  return std::vector<int64_t>(c.data_ptr<int64_t>(), c.data_ptr<int64_t>() + c.numel());
+KV aggregate(KV kv, const Comm& comm, const ExchangeOpts& o, ShuffleStats* st) {
+  if (!comm.distributed()) return kv;
+  return exchange(std::move(kv), at::Tensor(), comm, o, st);
 }
 
-// agree on fixed/variable widths across ranks. Returns (kw, vw) with -1 = variable.
-std::pair<int, int> agree_layout(const KV& kv, const PG& pg) {
-  const at::Device dev = kv.device();
-  // encode: [max kw, max -kw, max vw, max -vw] over non-empty ranks; empty ranks contribute -inf
-  const int64_t NEG = -(1ll << 40);
-  int64_t kw = kv.n ? kv.kw : NEG, vw = kv.n ? kv.vw : NEG;
-  at::Tensor t = at::tensor({kw, kv.n ? -kv.kw : NEG, vw, kv.n ? -kv.vw : NEG}, opt(at::kCPU, at::kLong)).to(dev);
-  t = allreduce(t, c10d::ReduceOp::MAX, pg).to(at::kCPU);
-  int64_t kmax = t[0].item<int64_t>(), kmin = -t[1].item<int64_t>();
-  int64_t vmax = t[2].item<int64_t>(), vmin = -t[3].item<int64_t>();
-  int okw, ovw;
-  if (kmax == NEG) okw = kv.kw;  // everyone empty
-  else okw = (kmax == kmin && kmax >= 0) ? (int)kmax : -1;
-  if (vmax == NEG) ovw = kv.vw;
-  else ovw = (vmax == vmin && vmax >= 0) ? (int)vmax : -1;
-  return {okw, ovw};
+KV gather_to(KV kv, int nprocs, const Comm& comm, const ExchangeOpts& o, ShuffleStats* st) {
+  if (!comm.distributed()) return kv;
+  const int target = comm.rank() % nprocs;
+  at::Tensor dest = at::full({kv.n}, target, opt(comm.device(), at::kInt));
+  return exchange(std::move(kv), dest, comm, o, st);
 }
 
-KV with_layout(const KV& kv, int kw, int vw) {
-  KV o = kv;
-  if (kw < 0 && o.kfixed()) o = to_var_keys(o);
-  if (vw < 0 && o.vfixed()) o = to_var_values(o);
-  if (o.n == 0) {
-    o.kw = kw;
-    o.vw = vw;
-    if (kw < 0 && !o.koff.defined()) o.koff = at::zeros({1}, opt(kv.device(), at::kLong));
-    if (vw < 0 && !o.voff.defined()) o.voff = at::zeros({1}, opt(kv.device(), at::kLong));
+KV broadcast(const KV& kv_in, int root, const Comm& comm) {
+  if (!comm.distributed()) return kv_in;
+  const at::Device dev = comm.device();
+  const bool me_root = comm.rank() == root;
+  KV kv = kv_in.n && kv_in.device() != dev ? kv_to(kv_in, dev) : kv_in;
+  at::Tensor hdr = at::zeros({5}, opt(at::kCPU, at::kLong));
+  if (me_root) {
+    int64_t* h = hdr.data_ptr<int64_t>();
+    h[0] = kv.n;
+    h[1] = kv.kw;
+    h[2] = kv.vw;
+    h[3] = kv.kdata.defined() ? kv.kdata.numel() : 0;
+    h[4] = kv.vdata.defined() ? kv.vdata.numel() : 0;
   }
+  hdr = hdr.to(dev);
+  comm.broadcast_tensor(hdr, root);
+  comm.host_wait();
+  at::Tensor h = hdr.to(at::kCPU);
+  KV o;
+  o.n = h[0].item<int64_t>();
+  o.kw = (int)h[1].item<int64_t>();
+  o.vw = (int)h[2].item<int64_t>();
+  const int64_t kb = h[3].item<int64_t>(), vb = h[4].item<int64_t>();
+  auto bc = [&](const at::Tensor& t, int64_t numel, at::ScalarType ty) {
+    at::Tensor x = me_root ? t.contiguous() : at::empty({numel}, opt(dev, ty));
+    if (numel) comm.broadcast_tensor(x, root);
+    return x;
+  };
+  o.kdata = bc(kv.kdata, kb, at::kByte);
+  o.vdata = bc(kv.vdata, vb, at::kByte);
+  if (o.kw < 0) o.koff = bc(kv.koff, o.n + 1, at::kLong);
+  if (o.vw < 0) o.voff = bc(kv.voff, o.n + 1, at::kLong);
   return o;
 }
-
-// move one column of a bucket-sorted KV
-void exchange_col(const at::Tensor& data, const at::Tensor& off, int w, const std::vector<int64_t>& scount,
-                  const std::vector<int64_t>& rcount, int64_t n_recv, const PG& pg, at::Tensor* rdata,
-                  at::Tensor* roff, int64_t* sbytes, int64_t* rbytes) {
-  const int P = (int)scount.size();
-  const at::Device dev = data.device();
-  if (w >= 0) {
-    std::vector<int64_t> sb(P), rb(P);
-    for (int i = 0; i < P; ++i) {
-      sb[i] = scount[i] * w;
-      rb[i] = rcount[i] * w;
-      *sbytes += sb[i];
-      *rbytes += rb[i];
-    }
-    *rdata = w ? alltoallv(data, sb, rb, pg) : at::empty({0}, opt(dev, at::kByte));
-    return;
-  }
-  // variable: lengths first, then bytes split at bucket boundaries of the offsets
-  int64_t n = 0;
-  for (auto c : scount) n += c;
-  at::Tensor len = at::empty({n}, opt(dev, at::kInt));
-  if (dev.is_cuda()) {
-    k::offsets_to_lengths(P0<int64_t>(off), n, P0<int32_t>(len), cur_stream());
-  } else if (n) {
-    len.copy_((off.narrow(0, 1, n) - off.narrow(0, 0, n)).to(at::kInt));
-  }
-  at::Tensor rlen = alltoallv(len, scount, rcount, pg);
-  // byte split points: off at cumulative counts
-  std::vector<int64_t> cum(P + 1, 0);
-  for (int i = 0; i < P; ++i) cum[i + 1] = cum[i] + scount[i];
-  at::Tensor idx = at::tensor(cum, opt(at::kCPU, at::kLong)).to(dev);
-  std::vector<int64_t> b = to_vec(off.index_select(0, idx));
-  std::vector<int64_t> sb(P);
-  for (int i = 0; i < P; ++i) {
-    sb[i] = b[i + 1] - b[i];
-    *sbytes += sb[i];
-  }
-  // receivers need byte counts: all-to-all of the per-dest byte totals
-  at::Tensor sbt = at::tensor(sb, opt(at::kCPU, at::kLong)).to(dev);
-  at::Tensor rbt = at::empty_like(sbt);
-  {
-    std::vector<int64_t> ones(P, 1);
-    rbt = alltoallv(sbt, ones, ones, pg);
-  }
-  std::vector<int64_t> rb = to_vec(rbt);
-  for (auto x : rb) *rbytes += x;
-  *rdata = alltoallv(data, sb, rb, pg);
-  *roff = exclusive_scan(rlen.narrow(0, 0, n_recv));
-}
-
-}  // namespace
 
 at::Tensor partition_dest(const KV& kv, int P, at::Tensor* counts) {
   const at::Device dev = kv.device();
@@ -164,216 +555,6 @@ at::Tensor partition_dest(const KV& kv, int P, at::Tensor* counts) {
     }
   }
   return dest;
-}
-
-// Exchange protocol (2 host round trips, then the payload streams):
-//  1. local stable radix pass on the destination rank -> P contiguous buckets;
-//  2. ONE int64 all-to-all of a [P x 5] header {pairs, key bytes, value bytes,
-//     key width code, value width code}: every rank learns what it will
-//     receive AND every rank's layout, so all ranks derive the same global
-//     layout locally (no separate layout allreduce, no per-column count
-//     exchanges);
-//  3. the 2-4 column all-to-alls (key lengths, key bytes, value lengths, value
-//     bytes) are issued back to back as async works and waited once: on RCCL
-//     they queue on the communicator's stream while this rank's stream goes on
-//     (offset scans of the received lengths wait only on their own column).
-namespace {
-constexpr int64_t kEmpty = -2;  // width code of a rank with no pairs
-
-int global_width(const std::vector<int64_t>& codes) {
-  int64_t w = kEmpty;
-  for (int64_t c : codes) {
-    if (c == kEmpty) continue;
-    if (w == kEmpty) w = c;
-    else if (w != c) return -1;
-  }
-  return (int)w;  // kEmpty if every rank is empty
-}
-
-struct Pending {
-  at::Tensor out;
-  c10::intrusive_ptr<c10d::Work> work;
-};
-
-Pending alltoallv_async(const at::Tensor& in, std::vector<int64_t> send, std::vector<int64_t> recv, const PG& pg) {
-  int64_t tot = 0;
-  for (auto r : recv) tot += r;
-  Pending p;
-  p.out = at::empty({tot}, in.options());
-  at::Tensor inc = in.contiguous();
-  p.work = pg->alltoall_base(p.out, inc, recv, send);
-  return p;
-}
-
-at::Tensor lengths_of(const at::Tensor& off, int64_t n, at::Device dev) {
-  at::Tensor len = at::empty({n}, opt(dev, at::kInt));
-  if (dev.is_cuda()) {
-    if (n) k::offsets_to_lengths(P0<int64_t>(off), n, P0<int32_t>(len), cur_stream());
-  } else if (n) {
-    len.copy_((off.narrow(0, 1, n) - off.narrow(0, 0, n)).to(at::kInt));
-  }
-  return len;
-}
-
-// per-destination byte totals of one column of a bucket-sorted KV
-std::vector<int64_t> bucket_bytes(const at::Tensor& off, int w, const std::vector<int64_t>& counts, at::Device dev) {
-  const int P = (int)counts.size();
-  std::vector<int64_t> out(P, 0);
-  if (w >= 0) {
-    for (int i = 0; i < P; ++i) out[i] = counts[i] * w;
-    return out;
-  }
-  std::vector<int64_t> cum(P + 1, 0);
-  for (int i = 0; i < P; ++i) cum[i + 1] = cum[i] + counts[i];
-  std::vector<int64_t> b = to_vec(off.index_select(0, at::tensor(cum, opt(at::kCPU, at::kLong)).to(dev)));
-  for (int i = 0; i < P; ++i) out[i] = b[i + 1] - b[i];
-  return out;
-}
-}  // namespace
-
-KV exchange(const KV& kv_in, const at::Tensor& dest, const PG& pg, ShuffleStats* st) {
-  auto t0 = std::chrono::steady_clock::now();
-  const at::Device dev = kv_in.device();
-  if (!pg || pg->getSize() == 1) {
-    if (st) st->send_pairs = st->recv_pairs = kv_in.n;
-    return kv_in;
-  }
-  const int P = pg->getSize();
-  // 1. bucket by destination (stable: one radix pass for P <= 256)
-  KV sorted = kv_in;
-  at::Tensor counts_t;
-  if (kv_in.n) {
-    at::Tensor iota = at::arange(kv_in.n, opt(dev, at::kInt));
-    int bits = 8;
-    while ((1 << bits) < P) bits += 8;
-    auto [ks, perm, passes] = radix_sort_pairs(dest.to(at::kLong), iota, 0, bits);
-    sorted = gather(kv_in, perm);
-    counts_t = at::bincount(dest.to(at::kLong), {}, P).to(at::kLong);
-  } else {
-    counts_t = at::zeros({P}, opt(dev, at::kLong));
-  }
-  std::vector<int64_t> scount = to_vec(counts_t);
-  const int64_t kcode = kv_in.n ? kv_in.kw : kEmpty, vcode = kv_in.n ? kv_in.vw : kEmpty;
-  std::vector<int64_t> skb = bucket_bytes(sorted.koff, sorted.kw, scount, dev);
-  std::vector<int64_t> svb = bucket_bytes(sorted.voff, sorted.vw, scount, dev);
-  // 2. one header all-to-all
-  std::vector<int64_t> hdr(5 * P);
-  for (int i = 0; i < P; ++i) {
-    hdr[5 * i + 0] = scount[i];
-    hdr[5 * i + 1] = skb[i];
-    hdr[5 * i + 2] = svb[i];
-    hdr[5 * i + 3] = kcode;
-    hdr[5 * i + 4] = vcode;
-  }
-  std::vector<int64_t> fives(P, 5);
-  std::vector<int64_t> rh = to_vec(alltoallv(at::tensor(hdr, opt(at::kCPU, at::kLong)).to(dev), fives, fives, pg));
-  std::vector<int64_t> rcount(P), rkb(P), rvb(P), kcodes(P), vcodes(P);
-  int64_t n_recv = 0, sb = 0, rb = 0;
-  for (int i = 0; i < P; ++i) {
-    rcount[i] = rh[5 * i];
-    rkb[i] = rh[5 * i + 1];
-    rvb[i] = rh[5 * i + 2];
-    kcodes[i] = rh[5 * i + 3];
-    vcodes[i] = rh[5 * i + 4];
-    n_recv += rcount[i];
-    sb += skb[i] + svb[i];
-    rb += rkb[i] + rvb[i];
-  }
-  int kw = global_width(kcodes), vw = global_width(vcodes);
-  if (kw == kEmpty) kw = kv_in.kw;  // nobody has pairs: keep the local layout
-  if (vw == kEmpty) vw = kv_in.vw;
-  if (kw < 0 && sorted.kfixed()) sorted = to_var_keys(sorted);  // same bytes, now with offsets
-  if (vw < 0 && sorted.vfixed()) sorted = to_var_values(sorted);
-  // 3. payload: every column all-to-all in flight before the first wait
-  const int64_t n = kv_in.n;
-  std::vector<Pending> q;
-  int klen_i = -1, vlen_i = -1;
-  if (kw < 0) {
-    klen_i = (int)q.size();
-    q.push_back(alltoallv_async(lengths_of(sorted.koff, n, dev), scount, rcount, pg));
-  }
-  // a column that is fixed-width 0 on every rank (e.g. MR-MPI NULL values) moves nothing
-  const int kd_i = kw == 0 ? -1 : (int)q.size();
-  if (kw != 0)
-    q.push_back(alltoallv_async(sorted.kdata.defined() ? sorted.kdata : at::empty({0}, opt(dev, at::kByte)), skb,
-                                rkb, pg));
-  if (vw < 0) {
-    vlen_i = (int)q.size();
-    q.push_back(alltoallv_async(lengths_of(sorted.voff, n, dev), scount, rcount, pg));
-  }
-  const int vd_i = vw == 0 ? -1 : (int)q.size();
-  if (vw != 0)
-    q.push_back(alltoallv_async(sorted.vdata.defined() ? sorted.vdata : at::empty({0}, opt(dev, at::kByte)), svb,
-                                rvb, pg));
-  for (auto& p : q) p.work->wait();
-  KV out;
-  out.n = n_recv;
-  out.kw = kw;
-  out.vw = vw;
-  out.kdata = kd_i >= 0 ? q[kd_i].out : at::empty({0}, opt(dev, at::kByte));
-  out.vdata = vd_i >= 0 ? q[vd_i].out : at::empty({0}, opt(dev, at::kByte));
-  if (kw < 0) out.koff = exclusive_scan(q[klen_i].out);
-  if (vw < 0) out.voff = exclusive_scan(q[vlen_i].out);
-  if (st) {
-    st->send_pairs += n;
-    st->recv_pairs += n_recv;
-    st->send_bytes += sb;
-    st->recv_bytes += rb;
-    st->seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  }
-  return out;
-}
-
-KV aggregate(const KV& kv, const PG& pg, ShuffleStats* st) {
-  if (!pg || pg->getSize() == 1) return kv;
-  at::Tensor counts;
-  at::Tensor dest = partition_dest(kv, pg->getSize(), &counts);
-  return exchange(kv, dest, pg, st);
-}
-
-KV gather_to(const KV& kv, int nprocs, const PG& pg, ShuffleStats* st) {
-  if (!pg || pg->getSize() == 1) return kv;
-  const int me = pg->getRank();
-  int target = me % nprocs;
-  at::Tensor dest = at::full({kv.n}, target, opt(kv.device(), at::kInt));
-  return exchange(kv, dest, pg, st);
-}
-
-KV broadcast(const KV& kv_in, int root, const PG& pg) {
-  if (!pg || pg->getSize() == 1) return kv_in;
-  const at::Device dev = kv_in.device();
-  const bool me_root = pg->getRank() == root;
-  KV kv = kv_in;
-  at::Tensor hdr = at::zeros({5}, opt(at::kCPU, at::kLong));
-  if (me_root) {
-    hdr[0] = kv.n;
-    hdr[1] = kv.kw;
-    hdr[2] = kv.vw;
-    hdr[3] = kv.kdata.numel();
-    hdr[4] = kv.vdata.numel();
-  }
-  std::vector<at::Tensor> v{hdr.to(dev)};
-  c10d::BroadcastOptions bo;
-  bo.rootRank = root;
-  wait(pg->broadcast(v, bo));
-  at::Tensor h = v[0].to(at::kCPU);
-  KV o;
-  o.n = h[0].item<int64_t>();
-  o.kw = (int)h[1].item<int64_t>();
-  o.vw = (int)h[2].item<int64_t>();
-  int64_t kb = h[3].item<int64_t>(), vb = h[4].item<int64_t>();
-  auto bcast = [&](at::Tensor t, int64_t numel, at::ScalarType ty) {
-    at::Tensor x = me_root ? t.contiguous() : at::empty({numel}, opt(dev, ty));
-    if (numel == 0) return x;
-    std::vector<at::Tensor> vv{x};
-    wait(pg->broadcast(vv, bo));
-    return vv[0];
-  };
-  o.kdata = bcast(kv.kdata, kb, at::kByte);
-  o.vdata = bcast(kv.vdata, vb, at::kByte);
-  if (o.kw < 0) o.koff = bcast(kv.koff, o.n + 1, at::kLong);
-  if (o.vw < 0) o.voff = bcast(kv.voff, o.n + 1, at::kLong);
-  return o;
 }
 
 }  // namespace mrh

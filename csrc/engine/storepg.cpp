@@ -3,6 +3,11 @@
 
 #include <ATen/ATen.h>
 
+#include <chrono>
+#include <thread>
+
+#include "rccl.h"
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,8 +45,21 @@ void copy_into(at::Tensor& dst, const uint8_t* src, size_t nbytes) {
 
 }  // namespace
 
-StoreBackend::StoreBackend(c10::intrusive_ptr<c10d::Store> store, int rank, int size)
-    : c10d::Backend(rank, size), store_(std::move(store)) {}
+StoreBackend::StoreBackend(c10::intrusive_ptr<c10d::Store> store, int rank, int size, std::shared_ptr<Monitor> mon)
+    : c10d::Backend(rank, size), store_(std::move(store)), mon_(std::move(mon)) {}
+
+// blocking read of a peer's blob; with a monitor it polls (check + backoff up
+// to 5 ms) so a peer that died before publishing fails the read in seconds
+std::vector<uint8_t> StoreBackend::get(const std::string& k) {
+  if (!mon_) return store_->get(k);
+  int sleep_us = 50;
+  while (!store_->check({k})) {
+    mon_->check();
+    std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
+    sleep_us = std::min(sleep_us * 2, 5000);
+  }
+  return store_->get(k);
+}
 
 std::string StoreBackend::key(const char* op, int64_t seq, int a, int b) const {
   static const bool dbg = std::getenv("MRH_STORE_DEBUG") != nullptr;
@@ -66,7 +84,7 @@ std::vector<std::vector<uint8_t>> StoreBackend::exchange_all(const char* op, con
   std::vector<std::string> keys;
   for (int r = 0; r < size_; ++r) {
     keys.push_back(key(op, s, r));
-    all[r] = store_->get(keys.back());
+    all[r] = get(keys.back());
   }
   release(key(op, s, -1) + "done", keys);
   return all;
@@ -103,7 +121,7 @@ c10::intrusive_ptr<c10d::Work> StoreBackend::broadcast(std::vector<at::Tensor>& 
   const int64_t s = seq_++;
   const std::string k = key("bc", s, (int)opts.rootRank);
   if (rank_ == opts.rootRank) store_->set(k, bytes_of(tensors[0]));
-  auto b = store_->get(k);
+  auto b = get(k);
   if ((int64_t)b.size() != tensors[0].numel() * tensors[0].element_size())
     throw std::runtime_error("mrh_store broadcast: size mismatch between ranks");
   if (rank_ != opts.rootRank) copy_into(tensors[0], b.data(), b.size());
@@ -151,7 +169,7 @@ c10::intrusive_ptr<c10d::Work> StoreBackend::alltoall_base(at::Tensor& out, at::
   std::vector<uint8_t> recv;
   for (int p = 0; p < size_; ++p) {
     const std::string k = key("a2a", s, p, rank_);
-    auto b = store_->get(k);
+    auto b = get(k);
     if ((int64_t)b.size() != out_splits[p] * orow)
       throw std::runtime_error("mrh_store alltoall: received size does not match the output split");
     recv.insert(recv.end(), b.begin(), b.end());

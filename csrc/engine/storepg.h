@@ -15,13 +15,18 @@
 #include <torch/csrc/distributed/c10d/Backend.hpp>
 #include <torch/csrc/distributed/c10d/Store.hpp>
 
+#include <memory>
 #include <string>
 
 namespace mrh {
 
+class Monitor;
+
 class StoreBackend : public c10d::Backend {
  public:
-  StoreBackend(c10::intrusive_ptr<c10d::Store> store, int rank, int size);
+  // mon (may be null): every blocking read polls it, so a dead or failed peer
+  // ends the collective with PeerFailure instead of a store timeout
+  StoreBackend(c10::intrusive_ptr<c10d::Store> store, int rank, int size, std::shared_ptr<Monitor> mon = {});
 
   const std::string getBackendName() const override { return "mrh_store"; }
 
@@ -41,8 +46,10 @@ class StoreBackend : public c10d::Backend {
   // publish this rank's blob, read every rank's, delete after the last reader
   std::vector<std::vector<uint8_t>> exchange_all(const char* op, const at::Tensor& mine);
   void release(const std::string& done_key, const std::vector<std::string>& keys);
+  std::vector<uint8_t> get(const std::string& key);
 
   c10::intrusive_ptr<c10d::Store> store_;
+  std::shared_ptr<Monitor> mon_;
   int64_t seq_ = 0;
 };
 

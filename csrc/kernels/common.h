@@ -5,6 +5,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <stdexcept>
+#include <string>
 #include "hashfn.h"
 
 #define MRH_WAVE 64
@@ -22,15 +24,26 @@ inline bool sync_mode() {
   }();
   return on;
 }
+// A failed launch or (in serialize mode) a failed kernel is a typed error,
+// never a local abort(): the exception unwinds through the op, which poisons
+// the job's communicator on the way out (comm.h), so peers fail fast too.
+struct KernelError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 inline void check_launch(const char* file, int line) {
   hipError_t e = hipGetLastError();
   const bool launched = e == hipSuccess;
   if (launched && sync_mode()) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
-    std::fprintf(stderr, "mrhip kernel %s: %s at %s:%d\n", launched ? "execution failed" : "launch failed",
-                 hipGetErrorString(e), file, line);
-    std::abort();
+    char buf[512];
+    std::snprintf(buf, sizeof(buf), "mrhip kernel %s: %s at %s:%d", launched ? "execution failed" : "launch failed",
+                  hipGetErrorString(e), file, line);
+    throw KernelError(buf);
   }
+}
+// host-side precondition of a launcher (shapes, limits): std::invalid_argument
+inline void check_arg(bool ok, const char* what) {
+  if (!ok) throw std::invalid_argument(std::string("mrhip: ") + what);
 }
 }  // namespace k
 }  // namespace mrh

@@ -96,10 +96,7 @@ void hash64_var(const uint8_t* kdata, const int64_t* koff, int64_t n, uint64_t* 
 void partition_dest(const uint32_t* h, int64_t n, int P, int32_t* dest, int64_t* counts, hipStream_t s) {
   hipMemsetAsync(counts, 0, sizeof(int64_t) * P, s);
   if (n <= 0) return;
-  if (P > 1024) {
-    fprintf(stderr, "mrhip partition: P=%d > 1024 unsupported\n", P);
-    abort();
-  }
+  check_arg(P <= 1024, "partition: more than 1024 ranks unsupported");
   unsigned g = nblk(n);
   if (g > 2048) g = 2048;
   hipLaunchKernelGGL(k_partition, dim3(g), dim3(H_NT), 0, s, h, n, P, dest, counts);

@@ -314,7 +314,7 @@ void kmeans_assign_accumulate(const float* pts, int64_t n, int D, const float* c
     case 3: launch<3>(pts, n, cen, K, acc, s); break;
     case 4: launch<4>(pts, n, cen, K, acc, s); break;
     case 8: launch<8>(pts, n, cen, K, acc, s); break;
-    default: fprintf(stderr, "kmeans: unsupported D=%d\n", D); abort();
+    default: check_arg(false, "kmeans: unsupported dimension D");
   }
 }
 

@@ -47,6 +47,33 @@ void hash64_var(const uint8_t* kdata, const int64_t* koff, int64_t n, uint64_t* 
 // destination rank = h % P, plus per-destination pair counts (atomic, LDS-aggregated)
 void partition_dest(const uint32_t* h, int64_t n, int P, int32_t* dest, int64_t* counts, hipStream_t s);
 
+// ---------------------------------------------------------------- shuffle.hip
+// Pairs per partition tile (block): nb = ceil(n / part_tile()) blocks.
+int part_tile();
+// owner per pair (dest_in given, or hashlittle(key, kb, P) % P written to
+// dest_out) and per-(owner d, block b) tables at [d*nb + b]: pair counts, and
+// key / value byte sums for variable columns (koff / voff non-null; kbytes /
+// vbytes null otherwise)
+void part_count(const int32_t* dest_in, const uint8_t* kd, int kw, const int64_t* koff, const int64_t* voff,
+                int64_t n, int P, int nb, int32_t* dest_out, int64_t* cnt, int64_t* kbytes, int64_t* vbytes,
+                hipStream_t s);
+// stable scatter into owner buckets: cbase = exclusive scan of cnt. Fixed
+// columns (kw / vw >= 0) are copied into ksend / vsend; for variable columns
+// perm (send position -> input pair) and klen / vlen are written instead
+void part_scatter(const int32_t* dest, int64_t n, int P, int nb, const int64_t* cbase, const uint8_t* kd, int kw,
+                  const uint8_t* vd, int vw, const int64_t* koff, const int64_t* voff, uint8_t* ksend,
+                  uint8_t* vsend, int64_t* perm, int32_t* klen, int32_t* vlen, hipStream_t s);
+// variable rows gathered by an int64 permutation into dst at doff
+void copy_var_i64(const uint8_t* src, const int64_t* soff, const int64_t* perm, int64_t n, uint8_t* dst,
+                  const int64_t* doff, hipStream_t s);
+// this rank's exchange header row (3P + 2 int64) from the scanned tables
+void part_header(const int64_t* cs, const int64_t* ks, const int64_t* vs, int P, int nb, int kw, int vw,
+                 int64_t kcode, int64_t vcode, int64_t* hdr, hipStream_t s);
+// counts[v % P] (counts zeroed by the caller) of non-negative int64 ids
+void count_mod(const int64_t* v, int64_t n, int P, int64_t* counts, hipStream_t s);
+// byte sizes [P][R] of the R pieces of each bucket of a variable column
+void piece_bytes(const int64_t* soff, const int64_t* start, int P, int R, int64_t* out, hipStream_t s);
+
 // ---------------------------------------------------------------- kvops.hip
 // Sort-key construction: fixed-width keys (kw<=8) loaded little-endian into a
 // uint64 and transformed so that unsigned order == requested order.

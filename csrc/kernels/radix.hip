@@ -164,10 +164,7 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
                         int begin_bit, int end_bit, void* temp, hipStream_t s, int* passes_run) {
   if (passes_run) *passes_run = 0;
   if (n <= 0) return;
-  if (n > 0xFFFFFFFFll) {
-    fprintf(stderr, "mrhip radix sort: n=%lld exceeds 2^32-1 pairs per call\n", (long long)n);
-    abort();
-  }
+  check_arg(n <= 0xFFFFFFFFll, "radix sort: more than 2^32-1 pairs per call (the out-of-core sort splits larger inputs)");
   const int64_t nb = (n + RX_TILE - 1) / RX_TILE;
   char* t = reinterpret_cast<char*>(temp);
   size_t hist_bytes = ((((size_t)RX_BINS * nb + 1) * sizeof(uint32_t)) + 255) & ~size_t(255);

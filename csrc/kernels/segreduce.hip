@@ -42,7 +42,7 @@ void run_op(int op, const void* vals, const int64_t* seg, int64_t nseg, int64_t 
     case 0: run<T, 0>(vals, seg, nseg, nval, out, s); break;
     case 1: run<T, 1>(vals, seg, nseg, nval, out, s); break;
     case 2: run<T, 2>(vals, seg, nseg, nval, out, s); break;
-    default: fprintf(stderr, "mrhip seg_reduce: bad op %d\n", op); abort();
+    default: check_arg(false, "seg_reduce: bad op");
   }
 }
 
@@ -56,7 +56,7 @@ void seg_reduce(const void* vals, int dtype, int op, const int64_t* seg, int64_t
     case 1: run_op<int64_t>(op, vals, seg, nseg, nval, out, s); break;
     case 2: run_op<float>(op, vals, seg, nseg, nval, out, s); break;
     case 3: run_op<double>(op, vals, seg, nseg, nval, out, s); break;
-    default: fprintf(stderr, "mrhip seg_reduce: bad dtype %d\n", dtype); abort();
+    default: check_arg(false, "seg_reduce: bad dtype");
   }
 }
 

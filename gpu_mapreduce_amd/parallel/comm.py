@@ -57,7 +57,12 @@ class Comm:
                     store = dist.distributed_c10d._get_default_store()
                 except Exception:
                     store = None
-            self._native = C.NativeComm(self.pg, self.device, store)
+            # RCCL (native communicator over xGMI) for device engines whose
+            # group is the nccl backend or that run alone; a gloo group (CPU
+            # engine, or the MRH_DIST_BACKEND=gloo rehearsal of several ranks
+            # on one GPU) keeps its process group as the transport
+            transport = "pg" if self.backend == "gloo" else ""
+            self._native = C.NativeComm(self.pg, self.device, store, transport)
         return self._native
 
     # ---- scalar collectives (every MR op returns a global count) ----------

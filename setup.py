@@ -63,8 +63,12 @@ HOSTFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-sign-comp
              "-I", os.path.join(here, "csrc"), "-I", os.path.join(ROCM, "include")] + \
             [f"-I{p}" for p in include_paths()]
 LINKLIBS = [f"-L{os.path.join(ROCM, 'lib')}", f"-L{_torch_lib()}", "-lamdhip64", "-lc10_hip", "-ltorch_hip",
-            "-lc10", "-ltorch", "-ltorch_cpu", "-lrocprofiler-sdk-roctx", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}",
-            f"-Wl,-rpath,{_torch_lib()}"]
+            "-lc10", "-ltorch", "-ltorch_cpu", "-lrocprofiler-sdk-roctx",
+            # RCCL: no -lrccl on purpose. The nccl* symbols resolve at load
+            # time from the librccl that libtorch_hip already depends on, so a
+            # process never maps two RCCL copies (torch ships its own; a
+            # NEEDED librccl.so.1 would pull /opt/rocm's in beside it)
+            f"-Wl,-rpath,{_torch_lib()}", f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}"]
 
 
 def _stale(obj, deps):
