@@ -18,14 +18,28 @@ The reference publishes no KV/s; its end-to-end input throughput is
 0.85 GB/s aggregate on 20 GK104 GPUs (50 GB in 59.0 s), so
 `vs_baseline` compares our aggregate input GB/s with that number.
 
+The same invocation also runs the BASELINE headline's second workload,
+PageRank on RMAT-2^26 (edge factor 16, 20 iterations, strong scaling: the
+same graph for every N), and reports it in extra keys: pagerank_kvps (edge
+contributions per second over the timed iterations), pagerank_ms (one
+20-iteration run), pagerank_setup_ms (R-MAT generation + aggregate to the
+source owner + plan build) and pagerank_kvps_incl_setup.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload invertedindex|pagerank|wordfreq|trifind|intcount]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`--gpus N` without torchrun spawns the N ranks itself (one process per GPU,
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set per
+child, before anything touches the GPU), like the reference's one MPI rank
+per GPU (cuda/InvertedIndex.cu:142-145, cuda/nodefile).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -97,6 +111,8 @@ def bench_inverted_index(comm, args):
         "baseline_note": "reference publishes no KV/s; vs_baseline = aggregate input GB/s "
                          f"({gbps:.2f}) / reference end-to-end 0.847 GB/s (50 GB in 59 s on 20x GK104)",
         "input_GBps": gbps,
+        "timed_step": "host(pinned)->HBM part files, map, aggregate (RCCL when N>1), convert, reduce; the reduce "
+                      "formats url\\tfile lines on the GPU into pinned host memory (not written to a file)",
         "kv_pairs_per_step": nurl,
         "unique_urls": app.nunique,
         "stage_ms": phases,
@@ -105,6 +121,82 @@ def bench_inverted_index(comm, args):
                    "parallelism": f"dp{comm.size}", "bytes_per_gpu": per_gpu,
                    "file_bytes": args.file_bytes, "link_gap": args.link_gap},
     }
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n, argv):
+    """One child process per rank (this process never touches the GPU);
+    returns the first non-zero child exit code, or 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in procs:  # a failed rank ends the job (the others fail fast anyway)
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def bench_pagerank_extra(comm, args):
+    """PageRank RMAT-2^scale x iters inside the headline run (extra keys)."""
+    from gpu_mapreduce_amd import MapReduce
+    from gpu_mapreduce_amd.models.pagerank import PageRank, rmat_map
+    scale, ef, iters = args.pagerank_scale, args.edgefactor, args.iters
+    _sync(comm)
+    t0 = time.perf_counter()
+    mr = MapReduce(comm)
+    rmat_map(mr, scale, ef, seed=args.seed)
+    pr = PageRank(mr, 1 << scale).build()
+    del mr
+    _sync(comm)
+    setup = comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
+    nedge = comm.allreduce(pr.nedge, "sum")
+    for _ in range(max(1, args.pagerank_warmup)):
+        pr.reset()
+        pr.run(iters)
+    _sync(comm)
+    t0 = time.perf_counter()
+    for _ in range(args.pagerank_steps):
+        pr.reset()
+        pr.run(iters)
+    _sync(comm)
+    dt = comm.allreduce((time.perf_counter() - t0) / args.pagerank_steps, "max", dtype=torch.float64)
+    out = {
+        "pagerank_kvps": nedge * iters / dt,
+        "pagerank_ms": dt * 1e3,
+        "pagerank_setup_ms": setup * 1e3,
+        "pagerank_kvps_incl_setup": nedge * iters / (dt + setup),
+        "pagerank_config": {"graph": f"RMAT-2^{scale}", "edgefactor": ef, "edges": nedge, "iters": iters,
+                            "runs_timed": args.pagerank_steps, "alpha": 0.85, "scaling": "strong",
+                            "rank_dtype": "fp32 ranks, fp64 L1/dangling reductions"},
+    }
+    del pr
+    if comm.is_cuda:
+        torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -126,12 +218,27 @@ def main():
     ap.add_argument("--kmeans-points", type=int, default=32 << 20, help="kmeans: points per GPU")
     ap.add_argument("--kmeans-dim", type=int, default=2)
     ap.add_argument("--kmeans-k", type=int, default=32)
+    ap.add_argument("--pagerank-scale", type=int, default=None,
+                    help="RMAT scale of the PageRank extra (26 on GPU, 14 on CPU; 0 = skip)")
+    ap.add_argument("--pagerank-steps", type=int, default=3, help="timed 20-iteration PageRank runs")
+    ap.add_argument("--pagerank-warmup", type=int, default=1)
     args = ap.parse_args()
     if args.scale is None:
         args.scale = 24 if args.workload == "trifind" else 26
 
+    ws_env = os.environ.get("WORLD_SIZE")
+    if ws_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if ws_env is not None and int(ws_env) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws_env}", file=sys.stderr)
+        sys.exit(2)
+
     from gpu_mapreduce_amd.parallel import comm as pcomm
     comm = pcomm.init()
+    if comm.size != args.gpus:
+        raise SystemExit(f"bench.py: {comm.size} ranks joined, expected {args.gpus}")
+    if args.pagerank_scale is None:
+        args.pagerank_scale = 26 if comm.is_cuda else 14
     if args.workload == "invertedindex":
         res = bench_inverted_index(comm, args)
     elif args.workload == "pagerank":
@@ -149,6 +256,11 @@ def main():
     else:
         from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
         res = bench_wordfreq(comm, args)
+    if args.workload == "invertedindex" and args.pagerank_scale > 0:
+        res.update(bench_pagerank_extra(comm, args))
+    res["rccl_ranks"] = comm.size
+    res["backend"] = {"torch.distributed": comm.backend or "none (world size 1)",
+                      "engine_transport": comm.native.transport}
     out = {
         "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": comm.size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],

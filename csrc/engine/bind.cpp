@@ -96,10 +96,16 @@ py::list value_list(MapReduce& mr, char* mv, int nv, int* vb) {
 
 HashFn py_hash(py::object h) {
   if (h.is_none()) return nullptr;
-  return [h](char* k, int kb) { return h(py::bytes(k, (size_t)kb)).cast<int>(); };
+  return [h](char* k, int kb) {
+    py::gil_scoped_acquire g;
+    return h(py::bytes(k, (size_t)kb)).cast<int>();
+  };
 }
 CompareFn py_cmp(py::object c) {
-  return [c](char* a, int al, char* b, int bl) { return c(py::bytes(a, (size_t)al), py::bytes(b, (size_t)bl)).cast<int>(); };
+  return [c](char* a, int al, char* b, int bl) {
+    py::gil_scoped_acquire g;
+    return c(py::bytes(a, (size_t)al), py::bytes(b, (size_t)bl)).cast<int>();
+  };
 }
 
 }  // namespace
@@ -245,93 +251,129 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           })
       .def_property_readonly("last_convert", [](MR& r) { return r.last_convert; })
       .def("copy", [](MR& r) { return r.copy().release(); }, py::return_value_policy::take_ownership)
-      .def("add", &MR::add)
-      .def("aggregate", [](MR& r, py::object h) { return r.aggregate(py_hash(h)); })
-      .def("aggregate_dest", &MR::aggregate_dest)
-      .def("broadcast", &MR::broadcast)
-      .def("clone", &MR::clone)
-      .def("close", &MR::close)
-      .def("collapse", [](MR& r, const std::string& k) { return r.collapse(k.data(), (int)k.size()); })
-      .def("collate", [](MR& r, py::object h) { return r.collate(py_hash(h)); })
-      .def("convert", &MR::convert)
-      .def("gather", &MR::gather)
-      .def("open", &MR::open)
+      .def("add", &MR::add, py::call_guard<py::gil_scoped_release>())
+      .def("aggregate", [](MR& r, py::object h) {
+        HashFn f = py_hash(h);
+        py::gil_scoped_release nogil;
+        return r.aggregate(f);
+      })
+      .def("aggregate_dest", &MR::aggregate_dest, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &MR::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("clone", &MR::clone, py::call_guard<py::gil_scoped_release>())
+      .def("close", &MR::close, py::call_guard<py::gil_scoped_release>())
+      .def("collapse", [](MR& r, const std::string& k) { return r.collapse(k.data(), (int)k.size()); }, py::call_guard<py::gil_scoped_release>())
+      .def("collate", [](MR& r, py::object h) {
+        HashFn f = py_hash(h);
+        py::gil_scoped_release nogil;
+        return r.collate(f);
+      })
+      .def("convert", &MR::convert, py::call_guard<py::gil_scoped_release>())
+      .def("gather", &MR::gather, py::call_guard<py::gil_scoped_release>())
+      .def("open", &MR::open, py::call_guard<py::gil_scoped_release>())
       .def("kv_open", [](MR& r) { return kvref(r.kv_open()); })
       .def("map", [](MR& r, int nmap, py::function fn,
-                     int add) { return r.map(nmap, [&](int t, KeyValue& kv) { fn(t, kvref(kv)); }, add); })
+                     int add) {
+        py::gil_scoped_release nogil;
+        return r.map(nmap, [&](int t, KeyValue& kv) { py::gil_scoped_acquire g; fn(t, kvref(kv)); }, add);
+      })
       .def("map_file",
            [](MR& r, std::vector<std::string> files, int self, int rec, int rd, py::function fn, int add) {
-             return r.map_file(files, self, rec, rd, [&](int t, const char* f, KeyValue& kv) { fn(t, f, kvref(kv)); },
-                               add);
+             py::gil_scoped_release nogil;
+             return r.map_file(files, self, rec, rd, [&](int t, const char* f, KeyValue& kv) {
+               py::gil_scoped_acquire g;
+               fn(t, f, kvref(kv));
+             }, add);
            })
       .def("map_file_chunks",
            [](MR& r, int nmap, std::vector<std::string> files, int self, int rec, int rd, const std::string& sep,
               bool is_char, int delta, py::function fn, int add) {
-             MapChunkFn f = [&](int t, char* s, int n, KeyValue& kv) { fn(t, py::bytes(s, (size_t)n), kvref(kv)); };
+             MapChunkFn f = [&](int t, char* s, int n, KeyValue& kv) {
+               py::gil_scoped_acquire g;
+               fn(t, py::bytes(s, (size_t)n), kvref(kv));
+             };
+             py::gil_scoped_release nogil;
              if (is_char) return r.map_file_char(nmap, files, self, rec, rd, sep.empty() ? '\n' : sep[0], delta, f, add);
              return r.map_file_str(nmap, files, self, rec, rd, sep, delta, f, add);
            })
       .def("map_mr",
            [](MR& r, MR& src, py::function fn, int add) {
+             py::gil_scoped_release nogil;
              return r.map_mr(
                  src,
                  [&](uint64_t i, char* k, int kb, char* v, int vb, KeyValue& kv) {
+                   py::gil_scoped_acquire g;
                    fn(i, py::bytes(k, (size_t)kb), py::bytes(v, (size_t)vb), kvref(kv));
                  },
                  add);
            })
       .def("map_mr_batch",
            [](MR& r, MR& src, py::function fn, int add) {
-             return r.map_mr_batch(src, [&](const KV& s, KeyValue& kv) { fn(s, kvref(kv)); }, add);
+             py::gil_scoped_release nogil;
+             return r.map_mr_batch(src, [&](const KV& s, KeyValue& kv) { py::gil_scoped_acquire g; fn(s, kvref(kv)); }, add);
            })
       .def("reduce",
            [](MR& r, py::function fn) {
+             py::gil_scoped_release nogil;
              return r.reduce([&](char* k, int kb, char* mv, int nv, int* vb, KeyValue& kv) {
+               py::gil_scoped_acquire g;
                fn(py::bytes(k, (size_t)kb), value_list(r, mv, nv, vb), kvref(kv));
              });
            })
       .def("compress",
            [](MR& r, py::function fn) {
+             py::gil_scoped_release nogil;
              return r.compress([&](char* k, int kb, char* mv, int nv, int* vb, KeyValue& kv) {
+               py::gil_scoped_acquire g;
                fn(py::bytes(k, (size_t)kb), value_list(r, mv, nv, vb), kvref(kv));
              });
            })
-      .def("reduce_builtin", &MR::reduce_builtin)
-      .def("compress_builtin", &MR::compress_builtin)
+      .def("reduce_builtin", &MR::reduce_builtin, py::call_guard<py::gil_scoped_release>())
+      .def("compress_builtin", &MR::compress_builtin, py::call_guard<py::gil_scoped_release>())
       .def("reduce_batch",
-           [](MR& r, py::function fn) { return r.reduce_batch([&](const KMV& s, KeyValue& kv) { fn(s, kvref(kv)); }); })
+           [](MR& r, py::function fn) {
+             py::gil_scoped_release nogil;
+             return r.reduce_batch([&](const KMV& s, KeyValue& kv) { py::gil_scoped_acquire g; fn(s, kvref(kv)); });
+           })
       .def("scan_kv",
            [](MR& r, py::function fn) {
-             return r.scan_kv(
-                 [&](char* k, int kb, char* v, int vb) { fn(py::bytes(k, (size_t)kb), py::bytes(v, (size_t)vb)); });
+             py::gil_scoped_release nogil;
+             return r.scan_kv([&](char* k, int kb, char* v, int vb) {
+               py::gil_scoped_acquire g;
+               fn(py::bytes(k, (size_t)kb), py::bytes(v, (size_t)vb));
+             });
            })
       .def("scan_kmv",
            [](MR& r, py::function fn) {
+             py::gil_scoped_release nogil;
              return r.scan_kmv([&](char* k, int kb, char* mv, int nv, int* vb) {
+               py::gil_scoped_acquire g;
                fn(py::bytes(k, (size_t)kb), value_list(r, mv, nv, vb));
              });
            })
-      .def("scrunch", [](MR& r, int n, const std::string& k) { return r.scrunch(n, k.data(), (int)k.size()); })
-      .def("sort_keys", [](MR& r, int f) { return r.sort_keys(f); })
-      .def("sort_keys_fn", [](MR& r, py::function c) { return r.sort_keys(py_cmp(c)); })
-      .def("sort_values", [](MR& r, int f) { return r.sort_values(f); })
-      .def("sort_values_fn", [](MR& r, py::function c) { return r.sort_values(py_cmp(c)); })
-      .def("sort_multivalues", [](MR& r, int f) { return r.sort_multivalues(f); })
-      .def("sort_multivalues_fn", [](MR& r, py::function c) { return r.sort_multivalues(py_cmp(c)); })
+      .def("scrunch", [](MR& r, int n, const std::string& k) { return r.scrunch(n, k.data(), (int)k.size()); }, py::call_guard<py::gil_scoped_release>())
+      .def("sort_keys", [](MR& r, int f) { return r.sort_keys(f); }, py::call_guard<py::gil_scoped_release>())
+      .def("sort_keys_fn", [](MR& r, py::function c) { CompareFn f = py_cmp(c); py::gil_scoped_release nogil; return r.sort_keys(f); })
+      .def("sort_values", [](MR& r, int f) { return r.sort_values(f); }, py::call_guard<py::gil_scoped_release>())
+      .def("sort_values_fn", [](MR& r, py::function c) { CompareFn f = py_cmp(c); py::gil_scoped_release nogil; return r.sort_values(f); })
+      .def("sort_multivalues", [](MR& r, int f) { return r.sort_multivalues(f); }, py::call_guard<py::gil_scoped_release>())
+      .def("sort_multivalues_fn", [](MR& r, py::function c) { CompareFn f = py_cmp(c); py::gil_scoped_release nogil; return r.sort_multivalues(f); })
       .def("print",
            [](MR& r, int proc, int nstride, int kflag, int vflag, py::object file, int fflag) {
-             if (file.is_none()) r.print(proc, nstride, kflag, vflag);
-             else r.print(file.cast<std::string>().c_str(), fflag, proc, nstride, kflag, vflag);
+             const bool nofile = file.is_none();
+             const std::string path = nofile ? std::string() : file.cast<std::string>();
+             py::gil_scoped_release nogil;
+             if (nofile) r.print(proc, nstride, kflag, vflag);
+             else r.print(path.c_str(), fflag, proc, nstride, kflag, vflag);
            })
-      .def("kv_stats", &MR::kv_stats)
-      .def("kmv_stats", &MR::kmv_stats)
-      .def("cummulative_stats", &MR::cummulative_stats)
-      .def("save", &MR::save)
-      .def("load", &MR::load)
-      .def("spill", &MR::spill)
-      .def("unspill", &MR::unspill)
-      .def("spill_disk", &MR::spill_disk)
-      .def("ensure_resident", &MR::ensure_resident)
+      .def("kv_stats", &MR::kv_stats, py::call_guard<py::gil_scoped_release>())
+      .def("kmv_stats", &MR::kmv_stats, py::call_guard<py::gil_scoped_release>())
+      .def("cummulative_stats", &MR::cummulative_stats, py::call_guard<py::gil_scoped_release>())
+      .def("save", &MR::save, py::call_guard<py::gil_scoped_release>())
+      .def("load", &MR::load, py::call_guard<py::gil_scoped_release>())
+      .def("spill", &MR::spill, py::call_guard<py::gil_scoped_release>())
+      .def("unspill", &MR::unspill, py::call_guard<py::gil_scoped_release>())
+      .def("spill_disk", &MR::spill_disk, py::call_guard<py::gil_scoped_release>())
+      .def("ensure_resident", &MR::ensure_resident, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("on_disk", &MR::on_disk)
       .def("my_proc", &MR::my_proc)
       .def("num_procs", &MR::num_procs)
@@ -370,6 +412,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
   });
   m.def("find_files", [](std::shared_ptr<Comm> c, std::vector<std::string> files, int self, int rec, int rd) {
+    py::gil_scoped_release nogil;
     return MapReduce::find_files(*c, files, self, rec, rd);
   });
 
@@ -472,12 +515,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<EdgePlan>(m, "EdgePlan")
       .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t nvert, c10::optional<at::Tensor> w,
                        bool symmetric) {
-             return new EdgePlan(c, e, nvert, w ? std::optional<at::Tensor>(*w) : std::nullopt, symmetric);
+             std::optional<at::Tensor> ww = w ? std::optional<at::Tensor>(*w) : std::nullopt;
+             py::gil_scoped_release nogil;
+             return new EdgePlan(c, e, nvert, ww, symmetric);
            }),
            py::arg("comm"), py::arg("edges"), py::arg("nvert"), py::arg("weights") = py::none(),
            py::arg("symmetric") = false)
-      .def("propagate", &EdgePlan::propagate)
-      .def("count_global", &EdgePlan::count_global)
+      .def("propagate", &EdgePlan::propagate, py::call_guard<py::gil_scoped_release>())
+      .def("count_global", &EdgePlan::count_global, py::call_guard<py::gil_scoped_release>())
       .def_readonly("N", &EdgePlan::N)
       .def_readonly("nlocal", &EdgePlan::nlocal)
       .def_readonly("nedge", &EdgePlan::nedge)
@@ -489,23 +534,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("P", &EdgePlan::P)
       .def_readonly("me", &EdgePlan::me);
   m.def("connected_components", [](const EdgePlan& p, int mx) { return connected_components(p, mx); },
-        py::arg("plan"), py::arg("max_iter") = 100000);
+        py::arg("plan"), py::arg("max_iter") = 100000, py::call_guard<py::gil_scoped_release>());
   m.def(
       "luby_mis",
       [](const EdgePlan& p, int64_t seed, c10::optional<at::Tensor> act, int mx) {
-        return luby_mis(p, seed, act ? std::optional<at::Tensor>(*act) : std::nullopt, mx);
+        std::optional<at::Tensor> a = act ? std::optional<at::Tensor>(*act) : std::nullopt;
+        py::gil_scoped_release nogil;
+        return luby_mis(p, seed, a, mx);
       },
       py::arg("plan"), py::arg("seed"), py::arg("active") = py::none(), py::arg("max_iter") = 100000);
   m.def("sssp", [](const EdgePlan& p, int64_t s, int mx) { return sssp(p, s, mx); }, py::arg("plan"),
-        py::arg("source"), py::arg("max_iter") = 1000000);
+        py::arg("source"), py::arg("max_iter") = 1000000, py::call_guard<py::gil_scoped_release>());
   py::class_<PageRankPlan>(m, "PageRankPlan")
       .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t n, double a) {
+        py::gil_scoped_release nogil;
         return new PageRankPlan(c, e, n, a);
       }))
-      .def("reset", &PageRankPlan::reset)
-      .def("step", &PageRankPlan::step)
-      .def("run", &PageRankPlan::run)
-      .def("delta", &PageRankPlan::delta)
+      .def("reset", &PageRankPlan::reset, py::call_guard<py::gil_scoped_release>())
+      .def("step", &PageRankPlan::step, py::call_guard<py::gil_scoped_release>())
+      .def("run", &PageRankPlan::run, py::call_guard<py::gil_scoped_release>())
+      .def("delta", &PageRankPlan::delta, py::call_guard<py::gil_scoped_release>())
       .def("ids", &PageRankPlan::ids)
       .def("ranks", &PageRankPlan::ranks)
       .def_readonly("N", &PageRankPlan::N)
@@ -513,10 +561,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("nedge", &PageRankPlan::nedge)
       .def_readonly("ndangling", &PageRankPlan::ndangling);
   py::class_<TriangleGraph>(m, "TriangleGraph")
-      .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t n) { return new TriangleGraph(c, e, n); }),
+      .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t n) {
+             py::gil_scoped_release nogil;
+             return new TriangleGraph(c, e, n);
+           }),
            py::arg("comm"), py::arg("edges"), py::arg("nvert") = -1)
-      .def("count", &TriangleGraph::count)
-      .def("triangles", &TriangleGraph::triangles)
+      .def("count", &TriangleGraph::count, py::call_guard<py::gil_scoped_release>())
+      .def("triangles", &TriangleGraph::triangles, py::call_guard<py::gil_scoped_release>())
       .def_readonly("nvert", &TriangleGraph::nvert)
       .def_readonly("nedge", &TriangleGraph::nedge)
       .def_readonly("rowptr", &TriangleGraph::rowptr)
@@ -549,9 +600,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            }),
            py::arg("comm"), py::arg("partitions"), py::arg("screen"), py::arg("logfile"), py::arg("variables"),
            py::arg("echo"), py::arg("world") = nullptr)
-      .def("file", &mrh::oink::Oink::file)
-      .def("text", &mrh::oink::Oink::text)
-      .def("one", &mrh::oink::Oink::one)
+      .def("file", &mrh::oink::Oink::file, py::call_guard<py::gil_scoped_release>())
+      .def("text", &mrh::oink::Oink::text, py::call_guard<py::gil_scoped_release>())
+      .def("one", &mrh::oink::Oink::one, py::call_guard<py::gil_scoped_release>())
       .def("close", &mrh::oink::Oink::close)
       .def_readonly("deltatime", &mrh::oink::Oink::deltatime)
       .def_property_readonly("nworlds", [](mrh::oink::Oink& o) { return o.universe->nworlds; })
@@ -572,6 +623,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           },
           py::return_value_policy::reference_internal);
   m.def("oink_main", [](std::shared_ptr<Comm> u, std::vector<std::string> argv) {
+    py::gil_scoped_release nogil;
     return mrh::oink::main_args(u, argv);
   });
   m.def("hip_compiled", []() { return true; });

@@ -51,8 +51,18 @@ void pg_allreduce(const PG& pg, at::Tensor& t, Comm::Op op) {
 }
 hipStream_t cur(at::Device d) { return at::hip::getCurrentHIPStream(d.index()).stream(); }
 
+// MRH_TRACE_COLL=1: one stderr line per collective (sequence, kind, bytes) to
+// diff the collective order of ranks after a hang
+void trace_coll(int rank, const char* kind, int64_t a, int64_t b) {
+  static const bool on = env_int("MRH_TRACE_COLL", 0) != 0;
+  if (!on) return;
+  static std::atomic<int64_t> seq{0};
+  std::fprintf(stderr, "[coll r%d #%lld] %s %lld %lld\n", rank, (long long)seq++, kind, (long long)a, (long long)b);
+}
+
 // one heartbeat monitor per (process, root store)
 std::shared_ptr<Monitor> shared_monitor(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size) {
+  if (env_int("MRH_MONITOR", 1) == 0) return nullptr;  // no heartbeats / peer checks (debugging)
   static std::mutex mu;
   static std::map<c10d::Store*, std::weak_ptr<Monitor>> reg;
   std::lock_guard<std::mutex> l(mu);
@@ -192,6 +202,7 @@ void Comm::host_wait() const {
 
 std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
   if (v.empty() || !distributed()) return v;
+  trace_coll(rank_, "allreduce_i64", (int64_t)v.size(), op);
   at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kLong));
   if (rccl_) {
     t = t.to(dev_);
@@ -209,6 +220,7 @@ std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
 
 std::vector<double> Comm::allreduce_f64(std::vector<double> v, Op op) const {
   if (v.empty() || !distributed()) return v;
+  trace_coll(rank_, "allreduce_f64", (int64_t)v.size(), op);
   at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kDouble));
   if (rccl_) {
     t = t.to(dev_);
@@ -256,6 +268,12 @@ double Comm::wtime() {
 // ---------------------------------------------------------------- data plane
 
 void Comm::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) const {
+  {
+    int64_t a = 0, b = 0;
+    for (auto& x : sends) a += x.bytes;
+    for (auto& x : recvs) b += x.bytes;
+    trace_coll(rank_, "sendrecv", a, b);
+  }
   if (rccl_) {
     rccl_->sendrecv(sends, recvs, cur(dev_));
     return;
@@ -301,6 +319,7 @@ void Comm::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& rec
 }
 
 void Comm::allgather_bytes(const void* send, void* recv, int64_t bytes) const {
+  trace_coll(rank_, "allgather", bytes, 0);
   if (rccl_) {
     rccl_->allgather(send, recv, (size_t)bytes, cur(dev_));
     return;
@@ -376,6 +395,7 @@ at::Tensor Comm::allgather_var(const at::Tensor& in) const {
 
 void Comm::allreduce_tensor(at::Tensor& t, Op op) const {
   if (!distributed()) return;
+  trace_coll(rank_, "allreduce_tensor", t.numel(), op);
   if (rccl_) {
     if (!t.is_contiguous()) t = t.contiguous();
     rccl_->allreduce(t.data_ptr(), (size_t)t.numel(), ndt(t.scalar_type()), nred(op), cur(dev_));
@@ -386,6 +406,7 @@ void Comm::allreduce_tensor(at::Tensor& t, Op op) const {
 
 void Comm::broadcast_tensor(at::Tensor& t, int root) const {
   if (!distributed()) return;
+  trace_coll(rank_, "broadcast", t.numel(), root);
   if (rccl_) {
     if (!t.is_contiguous()) t = t.contiguous();
     rccl_->broadcast(t.data_ptr(), (size_t)(t.numel() * t.element_size()), root, cur(dev_));

@@ -3,6 +3,9 @@
 #include "guard.h"
 
 #include <c10/hip/HIPCachingAllocator.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -91,6 +94,22 @@ void check_col(const at::Tensor& data, const at::Tensor& off, int w, int64_t n, 
     bad(op, std::string(col) + " offsets are not monotone");
   if (p[n] > bytes) bad(op, std::string(col) + " offsets run past the arena");
 }
+
+// MRH_STACK_SIGNAL=1: SIGUSR2 prints the native backtrace of the thread that
+// receives it (hang diagnosis without a debugger: `kill -USR2 <pid>`)
+void on_usr2(int) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char hdr[] = "mrhip: SIGUSR2 native backtrace:\n";
+  (void)!write(2, hdr, sizeof(hdr) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+}
+struct StackSignal {
+  StackSignal() {
+    const char* v = std::getenv("MRH_STACK_SIGNAL");
+    if (v && *v == '1') signal(SIGUSR2, on_usr2);
+  }
+} g_stack_signal;
 
 }  // namespace
 

@@ -62,6 +62,13 @@ struct OpTrace {
   }
   ~OpTrace() {
     --g_op_depth;
+    if (std::uncaught_exceptions() > 0 && g_op_depth == 0 && mr_->comm()->size() > 1) {
+      // an op failing on one rank can never complete its collectives on the
+      // others: fail the whole job now (reference Error::one -> MPI_Abort,
+      // src/error.cpp:47-57) instead of leaving peers blocked in a shuffle
+      mr_->comm()->poison(std::string("MapReduce ") + name_ + " raised an error on rank " +
+                          std::to_string(mr_->my_proc()));
+    }
     if (guard::trace_enabled() && std::uncaught_exceptions() == 0) {
       device_sync(mr_);
       const double t1 = Comm::wtime();

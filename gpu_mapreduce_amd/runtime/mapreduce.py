@@ -31,7 +31,10 @@ from .keyvalue import KeyValue, to_bytes
 MRMPI_VERSION = "gpu_mapreduce_amd 0.1 (MR-MPI 11 Mar 2013 API)"
 
 _SETTINGS = ("mapstyle", "all2all", "verbosity", "timer", "memsize", "minpage", "maxpage", "freepage",
-             "outofcore", "zeropage", "keyalign", "valuealign", "fpath")
+             "outofcore", "zeropage", "keyalign", "valuealign", "fpath",
+             # MI355X-native settings (mapreduce.h): shuffle receive cap, HBM /
+             # pinned-host budgets of the out-of-core tiers, pipelined streams
+             "chunk_bytes", "hbm_budget", "host_budget", "streams")
 
 
 def _arity(fn):

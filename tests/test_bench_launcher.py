@@ -1,0 +1,45 @@
+"""bench.py's own multi-rank launcher (`--gpus N` without torchrun): it must
+spawn N ranks that really join one job (n_gpus / rccl_ranks = N, global
+counts = N x the 1-rank counts for this weak-scaling workload) and keep the
+single-rank path unchanged. CPU engine, gloo; the driver runs the same script
+under torchrun on an 8-GPU node."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--bytes-per-gpu", "4e6", "--file-bytes", "1000000", "--steps", "1", "--warmup", "1", "--phases", "0",
+        "--pagerank-scale", "10", "--pagerank-steps", "1"]
+
+
+def _bench(n):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), *ARGS], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_n_ranks():
+    one, three = _bench(1), _bench(3)
+    assert one["n_gpus"] == 1 and one["rccl_ranks"] == 1
+    assert three["n_gpus"] == 3 and three["rccl_ranks"] == 3
+    assert three["config"]["parallelism"] == "dp3"
+    assert three["kv_pairs_per_step"] == 3 * one["kv_pairs_per_step"]
+    assert three["config"]["global_batch"] == 3 * one["config"]["global_batch"]
+    # the PageRank extra is strong scaling: same graph, same edge count
+    assert three["pagerank_config"]["edges"] == one["pagerank_config"]["edges"] == 16 * 1024
+    for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
+              "data", "pagerank_kvps", "pagerank_ms", "pagerank_setup_ms"):
+        assert k in three
+
+
+def test_bench_rejects_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", *ARGS], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

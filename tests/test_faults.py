@@ -39,8 +39,7 @@ def test_dead_rank_is_detected_not_hung(tmp_path):
     t0 = time.time()
     for r in range(2):
         env = dict(ENV0, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HIP_VISIBLE_DEVICES="", MRH_FAULT="abort:aggregate:1",
-                   MRH_COMM_TIMEOUT="5")
+                   MASTER_PORT=str(port), HIP_VISIBLE_DEVICES="", MRH_FAULT="abort:aggregate:1")
         procs.append(subprocess.Popen([exe, "docs"], cwd=tmp_path, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     try:
@@ -52,7 +51,7 @@ def test_dead_rank_is_detected_not_hung(tmp_path):
     elapsed = time.time() - t0
     assert procs[1].returncode == 3 and "rank 1 aborts at aggregate" in res[1][1]
     assert procs[0].returncode != 0, "the surviving rank must fail, not report success"
-    assert elapsed < 90, f"failure took {elapsed:.0f} s to surface"
+    assert elapsed < 30, f"failure took {elapsed:.0f} s to surface (MRH_COMM_TIMEOUT left at 600 s)"
 
 
 OOM_SCRIPT = """
@@ -179,3 +178,52 @@ def test_op_trace_two_ranks(tmp_path):
     assert sum(r["sent"] for r in recs if r["op"] == "aggregate") > 0
     s = ts.summarise(recs)
     assert {"Map", "Network I/O", "Sort/Hash", "Reduce"} <= set(s["stages_ms"])
+
+
+def _run_ranks(exe, args, n, cwd, extra, timeout=120):
+    """n native ranks; returns [(returncode, stderr, exit_time)] with exit
+    times measured by polling, so the test can bound how long the survivors
+    outlive the failed rank."""
+    port = _port()
+    procs = []
+    for r in range(n):
+        env = dict(ENV0, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HIP_VISIBLE_DEVICES="", **extra)
+        procs.append(subprocess.Popen([exe, *args], cwd=cwd, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    t_exit = [None] * n
+    t0 = time.time()
+    try:
+        while any(t is None for t in t_exit) and time.time() - t0 < timeout:
+            for i, p in enumerate(procs):
+                if t_exit[i] is None and p.poll() is not None:
+                    t_exit[i] = time.time()
+            time.sleep(0.02)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return [(p.returncode, p.communicate()[1], t) for p, t in zip(procs, t_exit)]
+
+
+@pytest.mark.parametrize("kind", ["abort", "throw"])
+def test_rank_failure_inside_shuffle_ends_job_fast(tmp_path, kind):
+    """One rank fails INSIDE the chunked exchange (first round of the first
+    aggregate); MRH_COMM_TIMEOUT stays at its 600 s default. Every rank must
+    exit non-zero within 10 s of the failure: a crash ("abort", no chance to
+    say goodbye) is seen through the stopped heartbeat, an error ("throw") is
+    broadcast by poisoning the job (reference Error::one -> MPI_Abort,
+    src/error.cpp:47-57)."""
+    exe = _cc(os.path.join(ROOT, "examples", "c", "cwordfreq.c"), tmp_path / "cwordfreq")
+    _docs(tmp_path / "docs")
+    res = _run_ranks(exe, ["docs"], 3, tmp_path, {"MRH_FAULT": f"{kind}:exchange_round:1"})
+    codes = [r[0] for r in res]
+    assert all(t is not None for _, _, t in res), f"a rank hung: {codes}"
+    assert all(c != 0 for c in codes), codes
+    t_fail = res[1][2]
+    for r in (0, 2):
+        assert res[r][2] - t_fail < 10.0, f"rank {r} outlived the failure by {res[r][2] - t_fail:.1f} s"
+        msg = res[r][1]
+        assert ("stopped responding" in msg) if kind == "abort" else ("rank 1 failed" in msg), msg[-2000:]
+    if kind == "abort":
+        assert codes[1] == 3 and "rank 1 aborts at exchange_round" in res[1][1]
