@@ -328,12 +328,14 @@ void Comm::allgather_bytes(const void* send, void* recv, int64_t bytes) const {
     copy_bytes(recv, send, bytes, dev_);
     return;
   }
-  auto bo = at::TensorOptions().device(dev_).dtype(at::kByte);
-  at::Tensor in = at::empty({bytes}, bo), out = at::empty({bytes * size_}, bo);
-  copy_bytes(in.data_ptr(), send, bytes, dev_);
-  pg_->_allgather_base(out, in)->wait();
-  copy_bytes(recv, out.data_ptr(), bytes * size_, dev_);
-  if (dev_.is_cuda()) host_wait();
+  // process group: the block to every peer through the all-to-all (every
+  // backend here implements it; gloo's and the store's allgather flavours differ)
+  std::vector<Xfer> xs, xr;
+  for (int p = 0; p < size_; ++p) {
+    xs.push_back({p, const_cast<void*>(send), bytes});
+    xr.push_back({p, (uint8_t*)recv + p * bytes, bytes});
+  }
+  sendrecv(xs, xr);
 }
 
 std::vector<int64_t> Comm::alltoall_counts(const std::vector<int64_t>& send) const {
