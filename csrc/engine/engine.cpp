@@ -778,6 +778,37 @@ at::Tensor sort_perm_column(const at::Tensor& data, const at::Tensor& off, int w
 }
 }  // namespace
 
+at::Tensor column_sort_keys(const at::Tensor& data, const at::Tensor& off, int w, int64_t n, int flag) {
+  const at::Device dev = data.device();
+  const bool desc = flag < 0;
+  int mode = 0, bits = 64;
+  if (flag_mode(flag, w, &mode, &bits)) {
+    KV dummy;
+    dummy.n = n;
+    at::Tensor idx;
+    return raw_keys_u64(dummy, mode, desc, data, std::min(w, bits / 8), &idx);
+  }
+  if (std::abs(flag) != 5 && std::abs(flag) != 6) fail("sort flag " + std::to_string(flag) + " unsupported");
+  at::Tensor o = w >= 0 ? fixed_offsets(n, w, dev) : off;
+  at::Tensor sk = at::empty({n}, opt(dev, at::kLong));
+  if (n == 0) return sk;
+  at::Tensor idx = at::empty({n}, opt(dev, at::kInt));
+  if (dev.is_cuda()) {
+    k::make_sortkeys_strprefix(P0<uint8_t>(data), P0<int64_t>(o), n, 0, desc, P0<uint64_t>(sk), P0<uint32_t>(idx),
+                               cur_stream());
+  } else {
+    const uint8_t* d = P0<uint8_t>(data);
+    const int64_t* op = P0<int64_t>(o);
+    uint64_t* kp = P0<uint64_t>(sk);
+    for (int64_t i = 0; i < n; ++i) {
+      uint64_t kk = 0;
+      for (int j = 0; j < 8; ++j) kk = (kk << 8) | (op[i] + j < op[i + 1] ? d[op[i] + j] : 0);
+      kp[i] = desc ? ~kk : kk;
+    }
+  }
+  return sk;
+}
+
 KV sort_kv(const KV& kv, int flag, bool by_value) {
   if (kv.n <= 1) return kv;
   at::Tensor perm = by_value ? sort_perm_column(kv.vdata, kv.voff, kv.vw, kv.n, flag)

@@ -94,6 +94,10 @@ KV reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtyp
 // sort KV by key or value; flag as MR-MPI: 1 int,2 uint64,3 float,4 double,5 str,6 strn,
 // negative = descending; extra: 7 int64, 8 uint32
 KV sort_kv(const KV& kv, int flag, bool by_value);
+// the unsigned 64-bit radix key sort_kv orders a column by (flag as sort_kv;
+// flags 5/6: the big-endian 8-byte prefix) — the range-partition key of the
+// out-of-core sort
+at::Tensor column_sort_keys(const at::Tensor& data, const at::Tensor& off, int w, int64_t n, int flag);
 // sort values inside each KMV segment
 KMV sort_multivalues(const KMV& kmv, int flag);
 // KMV -> KV with one (key, value) per value (inverse of convert)
@@ -131,6 +135,14 @@ KV exchange(KV kv, const at::Tensor& dest, const Comm& comm, const ExchangeOpts&
 KV aggregate(KV kv, const Comm& comm, const ExchangeOpts& o = {}, ShuffleStats* st = nullptr);
 // move everything to ranks 0..nprocs-1 (rank r sends to r % nprocs)
 KV gather_to(KV kv, int nprocs, const Comm& comm, const ExchangeOpts& o = {}, ShuffleStats* st = nullptr);
+// local stable partition of a KV into P contiguous buckets by dest (int32 in
+// [0, P)): the exchange's partition kernels without the exchange (the
+// out-of-core ops' spool partitioning, ooc.cpp)
+struct Buckets {
+  KV kv;                       // bucket-ordered pairs (bucket d is contiguous)
+  std::vector<int64_t> count;  // pairs per bucket
+};
+Buckets bucket_local(const KV& kv, const at::Tensor& dest, int P);
 // root's KV replicated on every rank
 KV broadcast(const KV& kv, int root, const Comm& comm);
 

@@ -2,6 +2,7 @@
 // method as src/mapreduce.cpp:<lines>.
 #include "mapreduce.h"
 #include "guard.h"
+#include "ooc.h"
 
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -250,10 +251,29 @@ MapReduce::~MapReduce() {
 
 // every op's entry: fault injection point, and data spilled to host (spill()
 // or spill-on-OOM) comes back to HBM before the op touches it
-void MapReduce::enter(const char* op) {
+void MapReduce::enter(const char* op, bool ooc_ok) {
   guard::fault_point(op, comm_->rank());
   ensure_resident();
-  if (device().is_cuda() && ((kv && !kv->device().is_cuda()) || (kmv && !kmv->keys.device().is_cuda()))) unspill();
+  const bool on_host = (kv && !kv->device().is_cuda()) || (kmv && !kmv->keys.device().is_cuda());
+  if (!device().is_cuda() || !on_host) return;
+  // an op with an out-of-core path leaves host-resident data larger than the
+  // HBM budget where it is and streams it; every other op brings it back
+  if (ooc_ok && needs_ooc(data_bytes(), budget(), 2.0)) return;
+  unspill();
+}
+
+int64_t MapReduce::data_bytes() const {
+  int64_t b = 0;
+  if (kv) b += kv->nbytes();
+  if (kmv) b += kmv->nbytes();
+  return b;
+}
+
+void MapReduce::note_ooc(const char* op, const OocStats& st) {
+  pages_ = std::max<int64_t>(pages_, st.parts);
+  if (set.verbosity > 0 && comm_->rank() == 0)
+    out(fmt("%s out of core: %" PRId64 " partitions, %" PRId64 " budget-sized chunks through HBM\n", op, st.parts,
+            st.chunks));
 }
 
 std::unique_ptr<MapReduce> MapReduce::copy() const {
@@ -677,9 +697,15 @@ uint64_t MapReduce::gather(int nprocs) {  // :893-1036
 uint64_t MapReduce::convert() {  // :861-886
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kv("convert");
-  kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert); });
+  if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
+    OocStats os;
+    kmv = ooc_convert(*kv, budget(), device(), &os);  // hash-partitioned spools (src/keymultivalue.cpp:645-789)
+    note_ooc("Convert", os);
+  } else {
+    kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert); });
+  }
   kv.reset();
   stats("Convert", 1);
   return count(kmv->nkey);
@@ -812,7 +838,7 @@ int MapReduce::multivalue_block(int iblock, char** mv, int** valuebytes) {
 uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);  // host callbacks read host-resident data in place
   need_kmv("reduce");
   KeyValue kvb(device());
   run_host_kmv(*kmv, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
@@ -825,10 +851,16 @@ uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
 uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dtype) {
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kmv("reduce");
-  kv = oom_retry(this, device(), my_proc(), "reduce_builtin",
-                 [&] { return mrh::reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype); });
+  if (needs_ooc(kmv->nbytes(), budget(), 2.0)) {  // values stream through HBM in budget-sized key ranges
+    OocStats os;
+    kv = ooc_reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype, budget(), device(), &os);
+    note_ooc("Reduce", os);
+  } else {
+    kv = oom_retry(this, device(), my_proc(), "reduce_builtin",
+                   [&] { return mrh::reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype); });
+  }
   kmv.reset();
   stats("Reduce", 0);
   return count(kv->n);
@@ -874,7 +906,7 @@ uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& d
 uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);  // host callbacks read host-resident data in place
   need_kv("scan");
   HostCol k = host_col(kv->kdata, kv->koff, kv->kw), v = host_col(kv->vdata, kv->voff, kv->vw);
   for (int64_t i = 0; i < kv->n; ++i) fn(k.at(i), (int)k.len(i), v.at(i), (int)v.len(i));
@@ -885,7 +917,7 @@ uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
 uint64_t MapReduce::scan_kmv(const ScanKMVFn& fn) {  // :1984-2065
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);  // host callbacks read host-resident data in place
   need_kmv("scan");
   run_host_kmv(*kmv, fn);
   stats("Scan", 1);
@@ -910,9 +942,15 @@ at::Tensor host_perm(const at::Tensor& data, const at::Tensor& off, int w, int64
 uint64_t MapReduce::sort_keys(int flag) {  // :2102-2126
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kv("sort_keys");
-  kv = oom_retry(this, device(), my_proc(), "sort_keys", [&] { return sort_kv(*kv, flag, false); });
+  if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
+    OocStats os;
+    kv = ooc_sort(*kv, flag, false, budget(), device(), &os);  // sample sort over host spools
+    note_ooc("Sort_keys", os);
+  } else {
+    kv = oom_retry(this, device(), my_proc(), "sort_keys", [&] { return sort_kv(*kv, flag, false); });
+  }
   stats("Sort_keys", 0);
   return count(kv->n);
 }
@@ -928,9 +966,15 @@ uint64_t MapReduce::sort_keys(const CompareFn& fn) {  // :2134-2149
 uint64_t MapReduce::sort_values(int flag) {  // :2156-2180
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kv("sort_values");
-  kv = oom_retry(this, device(), my_proc(), "sort_values", [&] { return sort_kv(*kv, flag, true); });
+  if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
+    OocStats os;
+    kv = ooc_sort(*kv, flag, true, budget(), device(), &os);
+    note_ooc("Sort_values", os);
+  } else {
+    kv = oom_retry(this, device(), my_proc(), "sort_values", [&] { return sort_kv(*kv, flag, true); });
+  }
   stats("Sort_values", 0);
   return count(kv->n);
 }
@@ -1047,11 +1091,12 @@ void MapReduce::print(const char* file, int fflag, int proc, int nstride, int kf
 uint64_t MapReduce::kv_stats(int level) {  // :2937-2966
   ensure_resident();
   need_kv("print stats");
-  std::vector<int64_t> t = comm_->allreduce({kv->n, kv->key_bytes(), kv->value_bytes(), kv->nbytes()}, Comm::SUM);
+  std::vector<int64_t> t =
+      comm_->allreduce({kv->n, kv->key_bytes(), kv->value_bytes(), kv->nbytes(), pages(kv->nbytes())}, Comm::SUM);
   const double mb = 1024.0 * 1024.0;
   if (level == 1 && comm_->rank() == 0)
-    out(fmt("%" PRId64 " pairs, %.3g Mb keys, %.3g Mb values, %.3g Mb, 1 pages\n", t[0], t[1] / mb, t[2] / mb,
-            t[3] / mb));
+    out(fmt("%" PRId64 " pairs, %.3g Mb keys, %.3g Mb values, %.3g Mb, %" PRId64 " pages\n", t[0], t[1] / mb,
+            t[2] / mb, t[3] / mb, t[4]));
   if (level == 2) {
     histo((double)kv->n, "  KV pairs:");
     histo(kv->key_bytes() / mb, "  Kdata (Mb):");
@@ -1065,11 +1110,11 @@ uint64_t MapReduce::kmv_stats(int level) {  // :2972-3001
   need_kmv("print stats");
   const KMV& m = *kmv;
   const int64_t vb = m.vw >= 0 ? m.nval * m.vw : (m.nval ? m.voff[m.nval].item<int64_t>() : 0);
-  std::vector<int64_t> t = comm_->allreduce({m.nkey, m.keys.key_bytes(), vb, m.nbytes()}, Comm::SUM);
+  std::vector<int64_t> t = comm_->allreduce({m.nkey, m.keys.key_bytes(), vb, m.nbytes(), pages(m.nbytes())}, Comm::SUM);
   const double mb = 1024.0 * 1024.0;
   if (level == 1 && comm_->rank() == 0)
-    out(fmt("%" PRId64 " pairs, %.3g Mb keys, %.3g Mb values, %.3g Mb, 1 pages\n", t[0], t[1] / mb, t[2] / mb,
-            t[3] / mb));
+    out(fmt("%" PRId64 " pairs, %.3g Mb keys, %.3g Mb values, %.3g Mb, %" PRId64 " pages\n", t[0], t[1] / mb,
+            t[2] / mb, t[3] / mb, t[4]));
   if (level == 2) {
     histo((double)m.nkey, "  KMV pairs:");
     histo(m.keys.key_bytes() / mb, "  Kdata (Mb):");

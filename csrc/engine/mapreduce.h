@@ -30,6 +30,7 @@
 namespace mrh {
 
 class MapReduce;
+struct OocStats;
 
 using MapTaskFn = std::function<void(int itask, KeyValue& kv)>;
 using MapFileFn = std::function<void(int itask, const char* fname, KeyValue& kv)>;
@@ -58,8 +59,8 @@ struct Settings {
   int64_t chunk_bytes = 0;
   // HBM budget of this MR's data in bytes (0 = maxpage x memsize if maxpage
   // > 0, else unlimited): an aggregate whose received data would exceed it
-  // lands in pinned host memory, and convert / sort_keys / sort_values run
-  // out of core in budget-sized runs + a device merge
+  // lands in pinned host memory, and convert / sort_keys / sort_values /
+  // builtin reduces run out of core over host spools (ooc.cpp)
   int64_t hbm_budget = 0;
   // pinned host bytes the spill tier may hold before it writes to disk (0 = unlimited)
   int64_t host_budget = 0;
@@ -174,7 +175,9 @@ class MapReduce {
 
  private:
   void start();
-  void enter(const char* op);
+  void enter(const char* op, bool ooc_ok = false);
+  int64_t data_bytes() const;
+  void note_ooc(const char* op, const OocStats& st);
   void stats(const char* heading, int which);
   void need_kv(const char* what) const;
   void need_kmv(const char* what) const;
@@ -187,6 +190,11 @@ class MapReduce {
   void run_host_kmv(const KMV& kmv, const std::function<void(char*, int, char*, int, int*)>& fn);
   void histo(double v, const char* heading) const;
   int64_t block_bytes() const;
+ public:
+  // memsize-sized pages a local KV/KMV of `bytes` spans (reference kv_stats
+  // "N pages"; the out-of-core ops record their partition count too)
+  int64_t pages(int64_t bytes) const { return std::max<int64_t>({int64_t(1), (bytes + block_bytes() - 1) / block_bytes(), pages_}); }
+ private:
   // shuffle options from the settings
   ExchangeOpts xopts() const;
   int64_t budget() const;
@@ -212,6 +220,7 @@ class MapReduce {
     std::vector<int64_t> boff;   // byte offset of each block start relative to mv
   } blk_;
   int block_select_ = 0;
+  int64_t pages_ = 0;
 };
 
 }  // namespace mrh

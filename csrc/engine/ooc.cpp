@@ -1,0 +1,313 @@
+// Out-of-core engine ops: convert, sort and builtin reduce over a KV / KMV
+// larger than the MapReduce object's HBM budget (mapreduce.h Settings::
+// hbm_budget, or maxpage x memsize).
+//
+// The reference pages everything through fixed-size pages and disk spools:
+// convert partitions the unique-key table by hash bits into Spools when it
+// overflows (src/keymultivalue.cpp:645-789, partition2sets :1056-1132), sort
+// sorts page-sized runs and 2-way merges them on disk (src/mapreduce.cpp:
+// 2395-2445, 2547-2633). Here the data sits in pinned host memory (the spill
+// tier) and HBM holds one budget-sized piece at a time:
+//
+//  convert  pass 1: each chunk goes to HBM, a 64-bit key hash picks one of M
+//           partitions, the shuffle's partition kernels (bucket_local) cut the
+//           chunk into M contiguous buckets, which drain to M host spools;
+//           pass 2: each partition (all values of a key live in one) is
+//           converted in HBM and its KMV drains to the host. M is chosen so a
+//           partition and its working set fit the budget.
+//  sort     sample sort instead of a run merge: pass 1 samples the radix sort
+//           key (column_sort_keys) of every chunk and picks M-1 splitters;
+//           pass 2 range-partitions every chunk into M host spools (equal keys
+//           always share a bucket; the partition is stable); pass 3 sorts each
+//           bucket in HBM and appends it. Bucket order is key order, so no
+//           merge is needed, and stability holds end to end.
+//  reduce   builtin segmented reduces stream the KMV in key ranges whose values
+//           fit the budget.
+// Every result lives in pinned host memory; the MapReduce object brings it
+// back to HBM on a later op when it fits.
+#include <ATen/ATen.h>
+
+#include <algorithm>
+#include <cstring>
+#include <limits>
+#include <stdexcept>
+
+#include "kv.h"
+#include "ooc.h"
+
+namespace mrh {
+
+namespace {
+
+at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
+
+at::Tensor host(const at::Tensor& t) {
+  if (!t.defined()) return t;
+  if (t.is_cpu()) return t.contiguous();
+  return t.to(at::TensorOptions().device(at::kCPU).pinned_memory(true), /*non_blocking=*/false, /*copy=*/true);
+}
+KV kv_host(const KV& kv) {
+  KV o = kv;
+  o.kdata = host(kv.kdata);
+  o.vdata = host(kv.vdata);
+  o.koff = host(kv.koff);
+  o.voff = host(kv.voff);
+  return o;
+}
+KMV kmv_host(const KMV& m) {
+  KMV o = m;
+  o.keys = kv_host(m.keys);
+  o.vdata = host(m.vdata);
+  o.voff = host(m.voff);
+  o.seg = host(m.seg);
+  return o;
+}
+
+// pairs [a, b) of a KV as a KV of their own (views of fixed columns; offsets rebased)
+KV kv_slice(const KV& kv, int64_t a, int64_t b, const int64_t* hkoff, const int64_t* hvoff) {
+  KV o;
+  o.n = b - a;
+  o.kw = kv.kw;
+  o.vw = kv.vw;
+  const at::Device dev = kv.device();
+  if (kv.kfixed()) {
+    o.kdata = kv.kdata.narrow(0, a * kv.kw, (b - a) * kv.kw);
+  } else {
+    o.kdata = kv.kdata.narrow(0, hkoff[a], hkoff[b] - hkoff[a]);
+    o.koff = kv.koff.narrow(0, a, b - a + 1) - hkoff[a];
+  }
+  if (kv.vfixed()) {
+    o.vdata = kv.vdata.narrow(0, a * kv.vw, (b - a) * kv.vw);
+  } else {
+    o.vdata = kv.vdata.narrow(0, hvoff[a], hvoff[b] - hvoff[a]);
+    o.voff = kv.voff.narrow(0, a, b - a + 1) - hvoff[a];
+  }
+  (void)dev;
+  return o;
+}
+
+// host copies of the offset columns (for byte-sized chunking and slicing)
+struct HostOff {
+  at::Tensor k, v;
+  const int64_t* kp() const { return k.defined() ? k.data_ptr<int64_t>() : nullptr; }
+  const int64_t* vp() const { return v.defined() ? v.data_ptr<int64_t>() : nullptr; }
+};
+HostOff host_off(const KV& kv) {
+  HostOff h;
+  if (!kv.kfixed()) h.k = kv.koff.to(at::kCPU).contiguous();
+  if (!kv.vfixed()) h.v = kv.voff.to(at::kCPU).contiguous();
+  return h;
+}
+
+int64_t row_bytes(const KV& kv, const HostOff& h, int64_t a, int64_t b) {
+  int64_t x = 0;
+  x += kv.kfixed() ? (b - a) * kv.kw : h.kp()[b] - h.kp()[a] + 8 * (b - a);
+  x += kv.vfixed() ? (b - a) * kv.vw : h.vp()[b] - h.vp()[a] + 8 * (b - a);
+  return x;
+}
+
+// largest b in (a, n] with fits(b) (fits is monotone, b = a + 1 always taken)
+template <typename F>
+int64_t grow(int64_t a, int64_t n, F&& fits) {
+  int64_t b = a + 1, step = 1;
+  while (b < n) {
+    const int64_t nb = std::min(n, b + step);
+    if (!fits(nb)) break;
+    b = nb;
+    step *= 2;
+  }
+  int64_t lo = b, hi = std::min(n, b + step);
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) / 2;
+    if (fits(mid)) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// pair ranges whose bytes are <= cap (at least one pair each)
+std::vector<std::pair<int64_t, int64_t>> chunks(const KV& kv, const HostOff& h, int64_t cap) {
+  std::vector<std::pair<int64_t, int64_t>> out;
+  for (int64_t a = 0; a < kv.n;) {
+    const int64_t b = grow(a, kv.n, [&](int64_t e) { return row_bytes(kv, h, a, e) <= cap; });
+    out.push_back({a, b});
+    a = b;
+  }
+  return out;
+}
+
+// spool the chunks of kv into M host buckets by a per-pair bucket id
+// produced on the device by `dest_of(chunk)`
+template <typename F>
+std::vector<std::vector<KV>> spool(const KV& kv, int64_t cap, at::Device dev, int M, F&& dest_of, OocStats* st) {
+  std::vector<std::vector<KV>> parts((size_t)M);
+  const HostOff h = host_off(kv);
+  for (auto [a, b] : chunks(kv, h, cap)) {
+    KV c = kv_to(kv_slice(kv, a, b, h.kp(), h.vp()), dev);
+    at::Tensor dest = dest_of(c);
+    Buckets B = bucket_local(c, dest, M);
+    const HostOff bh = host_off(B.kv);
+    int64_t s = 0;
+    for (int d = 0; d < M; ++d) {
+      const int64_t e = s + B.count[d];
+      if (e > s) parts[d].push_back(kv_host(kv_slice(B.kv, s, e, bh.kp(), bh.vp())));
+      s = e;
+    }
+    if (st) {
+      st->chunks++;
+      st->bytes_staged += row_bytes(kv, h, a, b);
+    }
+  }
+  return parts;
+}
+
+int parts_for(int64_t bytes, int64_t budget, double factor) {
+  const int64_t per = std::max<int64_t>(1, (int64_t)(budget / factor));
+  return (int)std::min<int64_t>(std::max<int64_t>(2, (bytes + per - 1) / per), 4096);
+}
+
+KMV kmv_concat_host(const std::vector<KMV>& parts, const KV& like) {
+  KMV out;
+  std::vector<KV> keys, vals;
+  std::vector<at::Tensor> segs;
+  int64_t base = 0;
+  for (const KMV& m : parts) {
+    keys.push_back(m.keys);
+    KV v;
+    v.n = m.nval;
+    v.kw = 0;
+    v.vw = m.vw;
+    v.kdata = at::empty({0}, opt(at::kCPU, at::kByte));
+    v.vdata = m.vdata;
+    v.voff = m.voff;
+    vals.push_back(v);
+    segs.push_back(m.seg.narrow(0, 0, m.nkey) + base);
+    base += m.nval;
+    out.nkey += m.nkey;
+  }
+  segs.push_back(at::full({1}, base, opt(at::kCPU, at::kLong)));
+  out.keys = parts.empty() ? empty_kv(at::Device(at::kCPU), like.kw, 0) : concat(keys, at::Device(at::kCPU));
+  out.keys.vw = 0;
+  KV vcat = parts.empty() ? empty_kv(at::Device(at::kCPU), 0, like.vw) : concat(vals, at::Device(at::kCPU));
+  out.vdata = vcat.vdata;
+  out.voff = vcat.voff;
+  out.vw = vcat.vw;
+  out.nval = base;
+  out.seg = at::cat(segs);
+  return kmv_host(out);
+}
+
+}  // namespace
+
+bool needs_ooc(int64_t bytes, int64_t budget, double factor) { return budget > 0 && bytes * factor > budget; }
+
+KMV ooc_convert(const KV& kv, int64_t budget, at::Device dev, OocStats* st) {
+  const int M = parts_for(kv.nbytes(), budget, 4.0);
+  if (st) st->parts = M;
+  auto parts = spool(kv, std::max<int64_t>(budget / 4, 1), dev, M, [&](const KV& c) {
+    // a hash independent of the shuffle's owner hash (every key on this rank
+    // has the same owner hash mod P): bits 20.. of the 64-bit grouping hash
+    at::Tensor h = hash64_keys(c);
+    return at::remainder(at::bitwise_right_shift(h, 20).bitwise_and_((int64_t(1) << 40) - 1), M).to(at::kInt);
+  }, st);
+  std::vector<KMV> out;
+  for (int d = 0; d < M; ++d) {
+    if (parts[d].empty()) continue;
+    KV p = kv_to(concat(parts[d], at::Device(at::kCPU)), dev);
+    parts[d].clear();
+    out.push_back(kmv_host(convert(p)));
+  }
+  return kmv_concat_host(out, kv);
+}
+
+KV ooc_sort(const KV& kv, int flag, bool by_value, int64_t budget, at::Device dev, OocStats* st) {
+  const int M = parts_for(kv.nbytes(), budget, 4.0);
+  if (st) st->parts = M;
+  const int64_t cap = std::max<int64_t>(budget / 4, 1);
+  auto skeys = [&](const KV& c) {
+    return by_value ? column_sort_keys(c.vdata, c.voff, c.vw, c.n, flag)
+                    : column_sort_keys(c.kdata, c.koff, c.kw, c.n, flag);
+  };
+  // pass 1: sample the unsigned radix keys of every chunk
+  const HostOff h = host_off(kv);
+  const auto ch = chunks(kv, h, cap);
+  std::vector<uint64_t> sample;
+  const int64_t want = std::max<int64_t>(64, 32 * M);
+  for (auto [a, b] : ch) {
+    KV c = kv_to(kv_slice(kv, a, b, h.kp(), h.vp()), dev);
+    at::Tensor sk = skeys(c);
+    const int64_t stride = std::max<int64_t>(1, (b - a) * (int64_t)ch.size() / want);
+    at::Tensor smp = sk.slice(0, 0, sk.numel(), stride).to(at::kCPU).contiguous();
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(smp.data_ptr<int64_t>());
+    sample.insert(sample.end(), p, p + smp.numel());
+  }
+  std::sort(sample.begin(), sample.end());
+  // M-1 splitters as sign-flipped int64 (signed order == unsigned order)
+  std::vector<int64_t> split;
+  for (int j = 1; j < M && !sample.empty(); ++j) {
+    const uint64_t v = sample[std::min(sample.size() - 1, sample.size() * j / M)];
+    if (split.empty() || (int64_t)(v ^ (1ull << 63)) != split.back()) split.push_back((int64_t)(v ^ (1ull << 63)));
+  }
+  const int MB = (int)split.size() + 1;
+  at::Tensor sp = at::tensor(split, opt(at::kCPU, at::kLong)).to(dev);
+  // pass 2: range partition (bucket = number of splitters below the key)
+  auto parts = spool(kv, cap, dev, MB, [&](const KV& c) {
+    at::Tensor k = at::bitwise_xor(skeys(c), std::numeric_limits<int64_t>::min());
+    if (split.empty()) return at::zeros({c.n}, opt(dev, at::kInt));
+    return (k.unsqueeze(1) > sp.unsqueeze(0)).sum(1).to(at::kInt);
+  }, st);
+  if (st) st->parts = MB;
+  // pass 3: sort each bucket in HBM, append in bucket (= key) order
+  std::vector<KV> out;
+  for (int d = 0; d < MB; ++d) {
+    if (parts[d].empty()) continue;
+    KV p = kv_to(concat(parts[d], at::Device(at::kCPU)), dev);
+    parts[d].clear();
+    out.push_back(kv_host(sort_kv(p, flag, by_value)));
+  }
+  if (out.empty()) return kv_host(kv);
+  return kv_host(concat(out, at::Device(at::kCPU)));
+}
+
+KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, int64_t budget, at::Device dev,
+                      OocStats* st) {
+  at::Tensor seg = kmv.seg.to(at::kCPU).contiguous();
+  const int64_t* s = seg.data_ptr<int64_t>();
+  at::Tensor vo = kmv.vw < 0 ? kmv.voff.to(at::kCPU).contiguous() : at::Tensor();
+  at::Tensor ko = kmv.keys.kw < 0 ? kmv.keys.koff.to(at::kCPU).contiguous() : at::Tensor();
+  const int64_t* vop = vo.defined() ? vo.data_ptr<int64_t>() : nullptr;
+  const int64_t* kop = ko.defined() ? ko.data_ptr<int64_t>() : nullptr;
+  auto vbytes = [&](int64_t a, int64_t b) {  // values of keys [a, b)
+    return kmv.vw >= 0 ? (s[b] - s[a]) * kmv.vw : vop[s[b]] - vop[s[a]] + 8 * (s[b] - s[a]);
+  };
+  const int64_t cap = std::max<int64_t>(budget / 4, 1);
+  std::vector<KV> out;
+  int64_t a = 0;
+  while (a < kmv.nkey) {
+    const int64_t b = grow(a, kmv.nkey, [&](int64_t e) { return vbytes(a, e) <= cap; });
+    KMV m;
+    m.nkey = b - a;
+    m.nval = s[b] - s[a];
+    m.keys = kv_slice(kmv.keys, a, b, kop, nullptr);
+    m.vw = kmv.vw;
+    if (kmv.vw >= 0) {
+      m.vdata = kmv.vdata.narrow(0, s[a] * kmv.vw, m.nval * kmv.vw);
+    } else {
+      m.vdata = kmv.vdata.narrow(0, vop[s[a]], vop[s[b]] - vop[s[a]]);
+      m.voff = kmv.voff.narrow(0, s[a], m.nval + 1) - vop[s[a]];
+    }
+    m.seg = kmv.seg.narrow(0, a, m.nkey + 1) - s[a];
+    KMV md = m;
+    md.keys = kv_to(m.keys, dev);
+    md.vdata = m.vdata.to(dev);
+    if (m.voff.defined()) md.voff = m.voff.to(dev);
+    md.seg = m.seg.to(dev);
+    out.push_back(kv_host(reduce_builtin(md, op, dtype)));
+    if (st) st->chunks++;
+    a = b;
+  }
+  if (out.empty()) return kv_host(reduce_builtin(kmv, op, dtype));
+  return kv_host(concat(out, at::Device(at::kCPU)));
+}
+
+}  // namespace mrh

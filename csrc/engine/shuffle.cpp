@@ -491,6 +491,95 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
   return out;
 }
 
+// ------------------------------------------------------------------ local partition
+Buckets bucket_local(const KV& kv_in, const at::Tensor& dest_in, int P) {
+  const at::Device dev = kv_in.device();
+  const bool cuda = dev.is_cuda();
+  const hipStream_t s = cuda ? cur_stream() : nullptr;
+  const int64_t n = kv_in.n;
+  const int tile = cuda ? k::part_tile() : 4096;
+  const int nb = (int)cdiv(n, tile);
+  const KV& kv = kv_in;
+  const bool kvar = !kv.kfixed(), vvar = !kv.vfixed();
+  at::Tensor dest = dest_in.to(dev).to(at::kInt).contiguous();
+  if (dest.numel() != n) fail("bucket_local: one destination per pair");
+  at::Tensor cnt = at::empty({(int64_t)P * nb}, opt(dev, at::kLong));
+  at::Tensor kbt = kvar ? at::empty({(int64_t)P * nb}, opt(dev, at::kLong)) : at::Tensor();
+  at::Tensor vbt = vvar ? at::empty({(int64_t)P * nb}, opt(dev, at::kLong)) : at::Tensor();
+  if (cuda) {
+    k::part_count(P0<int32_t>(dest), P0<uint8_t>(kv.kdata), kv.kw, kvar ? P0<int64_t>(kv.koff) : nullptr,
+                  vvar ? P0<int64_t>(kv.voff) : nullptr, n, P, nb, nullptr, P0<int64_t>(cnt), P0<int64_t>(kbt),
+                  P0<int64_t>(vbt), s);
+  } else {
+    cpu_part_count(P0<int32_t>(dest), P0<uint8_t>(kv.kdata), kv.kw, kvar ? P0<int64_t>(kv.koff) : nullptr,
+                   vvar ? P0<int64_t>(kv.voff) : nullptr, n, P, nb, tile, nullptr, P0<int64_t>(cnt),
+                   P0<int64_t>(kbt), P0<int64_t>(vbt));
+  }
+  at::Tensor cs = exclusive_scan(cnt);
+  at::Tensor ks = kvar ? exclusive_scan(kbt) : at::Tensor();
+  at::Tensor vs = vvar ? exclusive_scan(vbt) : at::Tensor();
+  // per-bucket totals to the host (one sync)
+  at::Tensor hdr = at::empty({3 * (int64_t)P + 2}, opt(dev, at::kLong));
+  if (cuda) {
+    k::part_header(P0<int64_t>(cs), P0<int64_t>(ks), P0<int64_t>(vs), P, nb, kvar ? -1 : kv.kw, vvar ? -1 : kv.vw, 0,
+                   0, P0<int64_t>(hdr), s);
+  } else {
+    int64_t* h = P0<int64_t>(hdr);
+    const int64_t *c = P0<int64_t>(cs), *kk = P0<int64_t>(ks), *vv = P0<int64_t>(vs);
+    for (int d = 0; d < P; ++d) {
+      const int64_t a = (int64_t)d * nb, b = a + nb, cc = c[b] - c[a];
+      h[3 * d] = cc;
+      h[3 * d + 1] = kvar ? kk[b] - kk[a] : cc * kv.kw;
+      h[3 * d + 2] = vvar ? vv[b] - vv[a] : cc * kv.vw;
+    }
+  }
+  at::Tensor hh = hdr.to(at::kCPU);
+  Buckets out;
+  int64_t kb_tot = 0, vb_tot = 0;
+  for (int d = 0; d < P; ++d) {
+    out.count.push_back(hh[3 * d].item<int64_t>());
+    kb_tot += hh[3 * d + 1].item<int64_t>();
+    vb_tot += hh[3 * d + 2].item<int64_t>();
+  }
+  at::Tensor ksend, vsend, perm, klen, vlen;
+  if (!kvar) ksend = at::empty({n * kv.kw}, opt(dev, at::kByte));
+  if (!vvar) vsend = at::empty({n * kv.vw}, opt(dev, at::kByte));
+  if (kvar || vvar) perm = at::empty({n}, opt(dev, at::kLong));
+  if (kvar) klen = at::empty({n}, opt(dev, at::kInt));
+  if (vvar) vlen = at::empty({n}, opt(dev, at::kInt));
+  if (n) {
+    if (cuda) {
+      k::part_scatter(P0<int32_t>(dest), n, P, nb, P0<int64_t>(cs), P0<uint8_t>(kv.kdata), kvar ? -1 : kv.kw,
+                      P0<uint8_t>(kv.vdata), vvar ? -1 : kv.vw, kvar ? P0<int64_t>(kv.koff) : nullptr,
+                      vvar ? P0<int64_t>(kv.voff) : nullptr, P0<uint8_t>(ksend), P0<uint8_t>(vsend),
+                      P0<int64_t>(perm), P0<int32_t>(klen), P0<int32_t>(vlen), s);
+    } else {
+      cpu_part_scatter(P0<int32_t>(dest), n, P, nb, tile, P0<int64_t>(cs), P0<uint8_t>(kv.kdata), kvar ? -1 : kv.kw,
+                       P0<uint8_t>(kv.vdata), vvar ? -1 : kv.vw, kvar ? P0<int64_t>(kv.koff) : nullptr,
+                       vvar ? P0<int64_t>(kv.voff) : nullptr, P0<uint8_t>(ksend), P0<uint8_t>(vsend),
+                       P0<int64_t>(perm), P0<int32_t>(klen), P0<int32_t>(vlen));
+    }
+  }
+  out.kv.n = n;
+  out.kv.kw = kv.kw;
+  out.kv.vw = kv.vw;
+  if (kvar) {
+    VarCol c = pack_var(kv.kdata, kv.koff, perm, klen, n, kb_tot, dev);
+    out.kv.kdata = c.data;
+    out.kv.koff = c.soff;
+  } else {
+    out.kv.kdata = ksend;
+  }
+  if (vvar) {
+    VarCol c = pack_var(kv.vdata, kv.voff, perm, vlen, n, vb_tot, dev);
+    out.kv.vdata = c.data;
+    out.kv.voff = c.soff;
+  } else {
+    out.kv.vdata = vsend;
+  }
+  return out;
+}
+
 KV aggregate(KV kv, const Comm& comm, const ExchangeOpts& o, ShuffleStats* st) {
   if (!comm.distributed()) return kv;
   return exchange(std::move(kv), at::Tensor(), comm, o, st);

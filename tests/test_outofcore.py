@@ -1,0 +1,80 @@
+"""Out-of-core convert / sort / builtin reduce under an HBM budget ~10x
+smaller than the data (csrc/engine/ooc.cpp).
+
+The reference pages its KV through `memsize` pages and spools partitions and
+sort runs to disk when they overflow (src/keymultivalue.cpp:645-789,
+src/mapreduce.cpp:2395-2445). Here `memsize` (page size) x `maxpage` (or
+`hbm_budget` directly) is the HBM budget: an op over more data than that
+streams budget-sized pieces through the device and keeps the result in pinned
+host memory. Every result must equal the in-memory op (the oracle), and
+kv_stats must report the data spanning more than one page."""
+import collections
+import struct
+
+import pytest
+import torch
+
+import gpu_mapreduce_amd as g
+from gpu_mapreduce_amd import MapReduce
+
+WORDS = [b"w%d-%s\0" % (j % 1711, b"x" * (j % 13)) for j in range(60000)]
+
+
+def _mr(comm, budget):
+    mr = MapReduce(comm)
+    if budget:
+        mr.memsize = -16384           # 16 KB pages (negative = bytes, reference semantics)
+        mr.maxpage = budget // 16384  # budget = maxpage x memsize
+    return mr
+
+
+def _wordcount(comm, budget):
+    mr = _mr(comm, budget)
+    mr.map(3, lambda i, kv: [kv.add(w, struct.pack("<i", j)) for j, w in enumerate(WORDS[i::3])])
+    assert mr.kv.nbytes() > 10 * budget if budget else True
+    nu = mr.convert()
+    mr.reduce("count")
+    return nu, dict((k, struct.unpack("<i", v)[0]) for k, v in mr.kv_pairs())
+
+
+def _sorted(comm, budget, flag, by_value):
+    mr = _mr(comm, budget)
+    vals = [(j * 2654435761) % 100003 - 50000 for j in range(40000)]
+    if by_value:
+        mr.map(1, lambda i, kv: [kv.add(WORDS[j], struct.pack("<i", v)) for j, v in enumerate(vals)])
+        mr.sort_values(flag)
+    else:
+        mr.map(1, lambda i, kv: [kv.add(WORDS[j], struct.pack("<i", v)) for j, v in enumerate(vals)])
+        mr.sort_keys(flag)
+    return list(mr.kv_pairs())
+
+
+def _run(dev):
+    comm = g.Comm(device=dev)
+    budget = 64 * 1024
+    nu0, c0 = _wordcount(comm, 0)
+    nu1, c1 = _wordcount(comm, budget)
+    assert nu0 == nu1 == len(set(WORDS))
+    assert c0 == c1 == dict(collections.Counter(WORDS))
+    for flag, by_value in ((5, False), (-5, False), (1, True), (-1, True)):
+        assert _sorted(comm, budget, flag, by_value) == _sorted(comm, 0, flag, by_value), (flag, by_value)
+    # stats: a KV ~20x the page spans many pages
+    mr = _mr(comm, budget)
+    mr.map(1, lambda i, kv: [kv.add(w) for w in WORDS])
+    lines = []
+    g._ext.C.set_screen(lambda s: lines.append(s))
+    try:
+        mr.kv_stats(1)
+    finally:
+        g._ext.C.set_screen(None)
+    pages = int("".join(lines).split(" Mb, ")[-1].split()[0])
+    assert pages > 10, lines
+
+
+def test_out_of_core_cpu():
+    _run("cpu")
+
+
+@pytest.mark.gpu
+def test_out_of_core_gpu():
+    _run("cuda:0")

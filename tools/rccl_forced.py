@@ -15,7 +15,9 @@ dev = "cuda:0"
 
 def comm(force):
     os.environ["MRH_FORCE_RCCL"] = "1" if force else "0"
-    return g.Comm(device=dev)
+    c = g.Comm(device=dev)
+    c.native  # the native communicator (and its RCCL transport) is created here, under this env
+    return c
 
 rc, lc = comm(True), comm(False)
 assert rc.native.transport == "rccl", rc.native.transport
