@@ -601,7 +601,7 @@ KMV collapse(const KV& kv_in, const std::string& key) {
   at::Tensor vdata;
   {
     int64_t tot = n ? scalar_i64(off, 2 * n) : 0;
-    at::Tensor row_of_byte = at::repeat_interleave(at::arange(2 * n, opt(dev, at::kLong)), lens, 0, tot);
+    at::Tensor row_of_byte = segment_ids(off, 2 * n, tot);
     at::Tensor within = at::arange(tot, opt(dev, at::kLong)) - off.narrow(0, 0, 2 * n).index_select(0, row_of_byte);
     vdata = comb.index_select(0, starts.index_select(0, row_of_byte) + within);
   }
@@ -816,15 +816,49 @@ KV sort_kv(const KV& kv, int flag, bool by_value) {
   return gather(kv, perm);
 }
 
-namespace {
-// segment id of every value (int64), by binary search over seg
-at::Tensor segment_ids(const at::Tensor& seg, int64_t nseg, int64_t nval) {
-  const at::Device dev = seg.device();
-  if (nval == 0) return at::empty({0}, opt(dev, at::kLong));
-  at::Tensor pos = at::arange(nval, opt(dev, at::kLong));
-  return at::searchsorted(seg.narrow(0, 0, nseg + 1), pos, false, /*right=*/true) - 1;
+// segment id of every value (int64): marks at segment starts + inclusive scan
+at::Tensor segment_ids(const at::Tensor& seg_in, int64_t nseg, int64_t nval) {
+  const at::Device dev = seg_in.device();
+  if (nval <= 0) return at::empty({0}, opt(dev, at::kLong));
+  at::Tensor seg = seg_in.contiguous();
+  if (dev.is_cuda()) {
+    at::Tensor marks = at::empty({nval}, opt(dev, at::kLong));
+    k::seg_marks(P0<int64_t>(seg), nseg, nval, P0<int64_t>(marks), cur_stream());
+    return exclusive_scan(marks).narrow(0, 1, nval);
+  }
+  at::Tensor out = at::empty({nval}, opt(dev, at::kLong));
+  const int64_t* sp = P0<int64_t>(seg);
+  int64_t* o = P0<int64_t>(out);
+  int64_t s = 0;
+  for (int64_t i = 0; i < nval; ++i) {
+    while (s + 1 < nseg && sp[s + 1] <= i) ++s;
+    o[i] = s;
+  }
+  return out;
 }
-}  // namespace
+
+at::Tensor bincount_dev(const at::Tensor& idx_in, int64_t K) {
+  const at::Device dev = idx_in.device();
+  at::Tensor idx = idx_in.to(at::kLong).contiguous();
+  at::Tensor c = at::zeros({std::max<int64_t>(K, 0)}, opt(dev, at::kLong));
+  if (idx.numel() == 0 || K <= 0) return c;
+  if (dev.is_cuda()) {
+    k::histogram(P0<int64_t>(idx), idx.numel(), K, P0<int64_t>(c), cur_stream());
+    return c;
+  }
+  const int64_t* p = P0<int64_t>(idx);
+  int64_t* o = P0<int64_t>(c);
+  for (int64_t i = 0; i < idx.numel(); ++i)
+    if (p[i] >= 0 && p[i] < K) o[p[i]]++;
+  return c;
+}
+
+at::Tensor repeat_index(const at::Tensor& counts) {
+  at::Tensor off = exclusive_scan(counts.to(at::kLong));
+  const int64_t n = counts.numel();
+  const int64_t tot = n ? off[n].item<int64_t>() : 0;
+  return segment_ids(off, n, tot);
+}
 
 KV expand(const KMV& kmv) {
   at::Tensor sid = segment_ids(kmv.seg, kmv.nkey, kmv.nval);

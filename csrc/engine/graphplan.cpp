@@ -193,6 +193,37 @@ std::pair<at::Tensor, int> sssp(const EdgePlan& plan, int64_t source, int max_it
   return {d, it};
 }
 
+at::Tensor sssp_predecessors(const EdgePlan& plan, const at::Tensor& edges, const at::Tensor& weights,
+                             const at::Tensor& dist, int64_t source) {
+  const Comm& comm = *plan.comm;
+  const int P = plan.P;
+  const at::Device dev = plan.dev;
+  at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2}).contiguous();
+  at::Tensor w = weights.to(dev).to(at::kDouble).contiguous();
+  // 1. every edge u -> v to the owner of u, where d[u] lives: candidate d[u] + w
+  KV kv = make_kv(e.select(1, 0).contiguous().view(at::kByte), std::nullopt,
+                  at::stack({e.select(1, 1), w.view(at::kLong)}, 1).contiguous().view(at::kByte), std::nullopt,
+                  e.size(0), dev);
+  kv = exchange(std::move(kv), at::remainder(e.select(1, 0), P).to(at::kInt), comm);
+  at::Tensor u = kv.kdata.view(at::kLong), vw = kv.vdata.view(at::kLong).view({-1, 2});
+  at::Tensor cand = dist.index_select(0, at::floor_divide(u, P)) + vw.select(1, 1).contiguous().view(at::kDouble);
+  // 2. (v, candidate, u) to the owner of v: u is a predecessor iff its candidate
+  //    equals d[v] (the same double sum the relaxation computed)
+  KV kv2 = make_kv(vw.select(1, 0).contiguous().view(at::kByte), std::nullopt,
+                   at::stack({cand.view(at::kLong), u}, 1).contiguous().view(at::kByte), std::nullopt, u.numel(), dev);
+  kv2 = exchange(std::move(kv2), at::remainder(vw.select(1, 0), P).to(at::kInt), comm);
+  at::Tensor v = kv2.kdata.view(at::kLong), cu = kv2.vdata.view(at::kLong).view({-1, 2});
+  at::Tensor lv = at::floor_divide(v, P);
+  at::Tensor ok = at::logical_and(cu.select(1, 0).contiguous().view(at::kDouble) == dist.index_select(0, lv),
+                                  at::isfinite(dist.index_select(0, lv)));
+  // deterministic tie-break across equal-length paths: the smallest predecessor id
+  at::Tensor pred = at::full({plan.nlocal}, std::numeric_limits<int64_t>::max(), at::TensorOptions().device(dev).dtype(at::kLong));
+  if (ok.any().item<bool>()) pred.scatter_reduce_(0, lv.index({ok}), cu.select(1, 1).index({ok}), "amin", true);
+  pred.masked_fill_(pred == std::numeric_limits<int64_t>::max(), -1);
+  if (source % P == plan.me) pred.index_put_({source / P}, 0);  // the source: DISTANCE() default, e.v = 0
+  return pred;
+}
+
 // ====================================================================== PageRank
 
 PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, double a)
@@ -223,7 +254,7 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
   order_ = sort_with_perm(dkey, 48).second.to(at::kLong);
   at::Tensor new_of_old = at::empty({nlocal}, opt(dev, at::kInt));
   new_of_old.index_put_({order_}, iota32(nlocal, dev));
-  at::Tensor src_local = nedge ? at::repeat_interleave(new_of_old.index_select(0, at::floor_divide(vi, P)), deg, 0, nedge)
+  at::Tensor src_local = nedge ? new_of_old.index_select(0, at::floor_divide(vi, P)).index_select(0, repeat_index(deg))
                                : at::empty({0}, opt(dev, at::kInt));
   const bool dist = comm->distributed();
   at::Tensor key = dist ? at::bitwise_or(at::bitwise_left_shift(at::remainder(vj, P), 40), vj) : vj.clone();

@@ -64,6 +64,12 @@ std::pair<at::Tensor, int> luby_mis(const EdgePlan& plan, int64_t seed, const st
 // Bellman-Ford from `source` over float64 weights; returns (dist with +inf, iterations)
 std::pair<at::Tensor, int> sssp(const EdgePlan& plan, int64_t source, int max_iter = 1000000);
 
+// predecessor of every local vertex on a shortest path from `source` (the
+// reference's DISTANCE e.v, oink/sssp.cpp:405-411): the smallest u with an
+// edge u -> v and d[u] + w(u,v) == d[v]; 0 for the source, -1 if unreached
+at::Tensor sssp_predecessors(const EdgePlan& plan, const at::Tensor& edges, const at::Tensor& weights,
+                             const at::Tensor& dist, int64_t source);
+
 // PageRank on edges partitioned by source (oinkdoc/pagerank.txt; the
 // reference command is a stub, oink/pagerank.cpp:54-56)
 class PageRankPlan {

@@ -30,7 +30,7 @@ KV kmeans_map(const at::Tensor& points, const at::Tensor& centroids) {
     at::Tensor score = (c * c).sum(1).unsqueeze(0) - 2.0 * at::matmul(p, c.t());  // [N, K]
     at::Tensor idx = score.argmin(1);
     at::Tensor sums = at::zeros({K, D}, acc.options()).index_add_(0, idx, p.to(at::kDouble));
-    at::Tensor cnt = at::bincount(idx, {}, K).to(at::kDouble).unsqueeze(1);
+    at::Tensor cnt = bincount_dev(idx, K).to(at::kDouble).unsqueeze(1);
     acc = at::cat({sums, cnt}, 1).reshape({-1});
   }
   KV kv;

@@ -180,6 +180,12 @@ SegIndex seg_index(const at::Tensor& seg, int64_t nval);
 void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tensor& x, const at::Tensor& w, int64_t op,
                        at::Tensor& out);
 std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre);
+// segment id of every value of a CSR segment array (seg[nseg+1], nval values)
+at::Tensor segment_ids(const at::Tensor& seg, int64_t nseg, int64_t nval);
+// counts of each bin in [0, K) of an integer index column (device histogram)
+at::Tensor bincount_dev(const at::Tensor& idx, int64_t K);
+// i repeated counts[i] times (the row index of every expanded element)
+at::Tensor repeat_index(const at::Tensor& counts);
 // segment boundaries of a sorted int64 key column: seg[nseg+1]
 at::Tensor segments_sorted(const at::Tensor& sorted_keys);
 

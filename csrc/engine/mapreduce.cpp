@@ -4,6 +4,7 @@
 #include "guard.h"
 #include "ooc.h"
 
+#include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
@@ -80,6 +81,12 @@ struct OpTrace {
                       mr_->kv ? mr_->kv->n : 0, mr_->kmv ? mr_->kmv->nkey : 0, b, MapReduce::cssize.load() - s0_,
                       MapReduce::crsize.load() - r0_);
     }
+    // freepage (reference: pages freed after every op, src/mapreduce.cpp:
+    // 3483-3517): with an HBM budget in force, blocks the op freed go back to
+    // the driver too, so the footprint between ops stays within the budget
+    if (mr_->set.freepage && mr_->budget() > 0 && g_op_depth == 0 && mr_->device().is_cuda() &&
+        std::uncaught_exceptions() == 0)
+      c10::hip::HIPCachingAllocator::emptyCache();
     if (mr_->set.outofcore == 1 && std::uncaught_exceptions() == 0) {
       try {
         mr_->spill_disk();
@@ -113,8 +120,13 @@ std::string fmt(const char* f, ...) {
 struct HostCol {
   at::Tensor data, off;
   int w = 0;
-  char* d() const { return data.numel() ? (char*)data.data_ptr<uint8_t>() : nullptr; }
-  int64_t a(int64_t i) const { return w >= 0 ? i * w : off.data_ptr<int64_t>()[i]; }
+  int64_t base = 0;             // byte shift that makes data + base aligned (aligned layouts)
+  std::vector<int64_t> pstart;  // padded row starts (keyalign / valuealign layouts), else empty
+  char* d() const { return data.numel() ? (char*)data.data_ptr<uint8_t>() + base : nullptr; }
+  int64_t a(int64_t i) const {
+    if (!pstart.empty()) return pstart[i];
+    return w >= 0 ? i * w : off.data_ptr<int64_t>()[i];
+  }
   int64_t len(int64_t i) const { return w >= 0 ? w : off.data_ptr<int64_t>()[i + 1] - off.data_ptr<int64_t>()[i]; }
   char* at(int64_t i) const { return d() ? d() + a(i) : nullptr; }
 };
@@ -124,6 +136,44 @@ HostCol host_col(const at::Tensor& data, const at::Tensor& off, int w) {
   c.off = (w < 0) ? off.to(at::kCPU).contiguous() : at::Tensor();
   c.w = w;
   return c;
+}
+
+// keyalign / valuealign (reference src/keyvalue.cpp:345-352, page layout
+// `kb | vb | pad | key | pad | value`): the pointer a host callback receives
+// for each key (or KV value) is a multiple of `align`; for KMV multivalues
+// (seg given) the start of each key's value list is aligned and its values
+// stay packed back to back, as in the reference KMV page (src/keymultivalue.
+// cpp:830-839). Alignments must be powers of two (src/mapreduce.cpp:3327-3332).
+void align_col(HostCol& c, int64_t n, int align, const int64_t* seg = nullptr, int64_t nseg = 0, bool zero = false) {
+  if (align < 1 || (align & (align - 1))) throw std::runtime_error("Invalid alignment (keyalign/valuealign must be a power of 2)");
+  if (align == 1 || n == 0) return;
+  auto up = [&](int64_t x) { return (x + align - 1) & ~(int64_t)(align - 1); };
+  std::vector<int64_t> st((size_t)n);
+  int64_t pos = 0;
+  bool same = ((uintptr_t)c.d() % align) == 0;
+  auto place = [&](int64_t i, bool aligned_start) {
+    if (aligned_start) pos = up(pos);
+    st[i] = pos;
+    same = same && pos == c.a(i);
+    pos += c.len(i);
+  };
+  if (seg) {
+    for (int64_t s = 0; s < nseg; ++s)
+      for (int64_t i = seg[s]; i < seg[s + 1]; ++i) place(i, i == seg[s]);
+  } else {
+    for (int64_t i = 0; i < n; ++i) place(i, true);
+  }
+  if (same) return;  // already aligned in place (e.g. fixed widths that are multiples of align)
+  // zeropage (reference: pages zeroed when allocated): padding bytes are 0
+  at::Tensor buf = zero ? at::zeros({pos + align}, at::TensorOptions().dtype(at::kByte))
+                        : at::empty({pos + align}, at::TensorOptions().dtype(at::kByte));
+  const int64_t shift = (align - (int64_t)((uintptr_t)buf.data_ptr<uint8_t>() % align)) % align;
+  char* dst = (char*)buf.data_ptr<uint8_t>() + shift;
+  for (int64_t i = 0; i < n; ++i)
+    if (c.len(i)) std::memcpy(dst + st[i], c.at(i), (size_t)c.len(i));
+  c.data = buf;
+  c.base = shift;
+  c.pstart = std::move(st);
 }
 
 KV clone_kv(const KV& kv) {
@@ -253,6 +303,15 @@ MapReduce::~MapReduce() {
 // or spill-on-OOM) comes back to HBM before the op touches it
 void MapReduce::enter(const char* op, bool ooc_ok) {
   guard::fault_point(op, comm_->rank());
+  if (!started_) {
+    started_ = true;
+    // minpage (reference allocate(), src/mapreduce.cpp:3318-3357): pages
+    // claimed up front; here the caching allocator's pool is grown by
+    // minpage x memsize once, so the first ops do not pay for hipMalloc
+    if (set.minpage > 0 && device().is_cuda()) {
+      at::Tensor t = at::empty({(int64_t)set.minpage * block_bytes()}, at::TensorOptions().device(device()).dtype(at::kByte));
+    }
+  }
   ensure_resident();
   const bool on_host = (kv && !kv->device().is_cuda()) || (kmv && !kmv->keys.device().is_cuda());
   if (!device().is_cuda() || !on_host) return;
@@ -587,6 +646,8 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   HostCol k = host_col(s.kdata, s.koff, s.kw), v = host_col(s.vdata, s.voff, s.vw);
+  align_col(k, s.n, src.set.keyalign, nullptr, 0, src.set.zeropage);
+  align_col(v, s.n, src.set.valuealign, nullptr, 0, src.set.zeropage);
   KeyValue kvb(device());
   for (int64_t i = 0; i < s.n; ++i) fn((uint64_t)i, k.at(i), (int)k.len(i), v.at(i), (int)v.len(i), kvb);
   if (&src == this && addflag) {
@@ -790,6 +851,8 @@ void MapReduce::run_host_kmv(const KMV& m, const std::function<void(char*, int, 
   HostCol k = host_col(m.keys.kdata, m.keys.koff, m.keys.kw), v = host_col(m.vdata, m.voff, m.vw);
   at::Tensor seg = m.seg.to(at::kCPU).contiguous();
   const int64_t* s = seg.data_ptr<int64_t>();
+  align_col(k, m.nkey, set.keyalign, nullptr, 0, set.zeropage);
+  align_col(v, m.nval, set.valuealign, s, m.nkey, set.zeropage);
   std::vector<int> vsz((size_t)m.nval);
   for (int64_t j = 0; j < m.nval; ++j) vsz[j] = (int)v.len(j);
   const int64_t page = block_bytes();
@@ -909,6 +972,8 @@ uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
   enter(__func__, true);  // host callbacks read host-resident data in place
   need_kv("scan");
   HostCol k = host_col(kv->kdata, kv->koff, kv->kw), v = host_col(kv->vdata, kv->voff, kv->vw);
+  align_col(k, kv->n, set.keyalign, nullptr, 0, set.zeropage);
+  align_col(v, kv->n, set.valuealign, nullptr, 0, set.zeropage);
   for (int64_t i = 0; i < kv->n; ++i) fn(k.at(i), (int)k.len(i), v.at(i), (int)v.len(i));
   stats("Scan", 0);
   return count(kv->n);

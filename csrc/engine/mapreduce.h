@@ -50,6 +50,10 @@ struct Settings {
   int verbosity = 0;   // 0 none, 1 totals, 2 per-proc histograms
   int timer = 0;       // 0 none, 1 barrier + rank-0 time, 2 per-proc histogram
   int memsize = 64;    // MB per page (negative: bytes); sets the host block size of long KMV values
+  // minpage: pool pre-grown by minpage pages at the first op; maxpage: HBM
+  // budget = maxpage pages (out-of-core beyond it); freepage: with a budget,
+  // freed HBM returns to the driver after every op; zeropage: padding bytes of
+  // aligned host-callback layouts are zeroed (reference src/mapreduce.cpp:3318-3547)
   int minpage = 0, maxpage = 0, freepage = 1, outofcore = 0, zeropage = 0;
   int keyalign = 4, valuealign = 4;
   std::string fpath = ".";
@@ -191,13 +195,14 @@ class MapReduce {
   void histo(double v, const char* heading) const;
   int64_t block_bytes() const;
  public:
+  // HBM budget of this object's data in bytes (0 = unlimited)
+  int64_t budget() const;
   // memsize-sized pages a local KV/KMV of `bytes` spans (reference kv_stats
   // "N pages"; the out-of-core ops record their partition count too)
   int64_t pages(int64_t bytes) const { return std::max<int64_t>({int64_t(1), (bytes + block_bytes() - 1) / block_bytes(), pages_}); }
  private:
   // shuffle options from the settings
   ExchangeOpts xopts() const;
-  int64_t budget() const;
 
   void write_file(const std::string& p) const;
   int64_t read_file(const std::string& p);
@@ -221,6 +226,7 @@ class MapReduce {
   } blk_;
   int block_select_ = 0;
   int64_t pages_ = 0;
+  bool started_ = false;
 };
 
 }  // namespace mrh

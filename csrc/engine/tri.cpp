@@ -91,7 +91,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
     k::tri_rowptr(P0<uint64_t>(okeys), m, nvert, P0<int64_t>(rowptr), cur());
   } else {
     at::Tensor src = at::bitwise_right_shift(okeys, 32);
-    at::Tensor cnt = m ? at::bincount(src, {}, nvert) : at::zeros({nvert}, opt(dev, at::kLong));
+    at::Tensor cnt = bincount_dev(src, nvert);
     rowptr = exclusive_scan(cnt.to(at::kLong).contiguous());
   }
   return {rowptr, col, okeys, perm};

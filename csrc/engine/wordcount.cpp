@@ -135,8 +135,14 @@ KV WordCounter::finish() {
     return kv;
   }
   hipStream_t s = cur();
-  at::Tensor idx = at::nonzero(slots_ != 0).view({-1});
-  const int64_t nk = idx.numel();
+  // occupied slots, in slot order: flags + scan + scatter (no rocPRIM compaction)
+  const int64_t cap = slots_.numel();
+  at::Tensor flags = at::empty({cap}, opt(dev_, at::kInt));
+  k::nz_flags(P<uint64_t>(slots_), cap, P<int32_t>(flags), s);
+  at::Tensor pos = exclusive_scan(flags);
+  const int64_t nk = pos[cap].item<int64_t>();
+  at::Tensor idx = at::empty({std::max<int64_t>(nk, 1)}, opt(dev_, at::kLong));
+  k::compact_nz(P<uint64_t>(slots_), P<int64_t>(pos), cap, P<int64_t>(idx), s);
   at::Tensor starts = at::empty({std::max<int64_t>(nk, 1)}, opt(dev_, at::kLong));
   at::Tensor lens = at::empty({std::max<int64_t>(nk, 1)}, opt(dev_, at::kInt));
   k::wc_keys(P<uint64_t>(slots_), P<int64_t>(idx), nk, P<uint8_t>(arena_), P<int64_t>(starts), P<int32_t>(lens), s);

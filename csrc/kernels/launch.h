@@ -74,6 +74,16 @@ void count_mod(const int64_t* v, int64_t n, int P, int64_t* counts, hipStream_t 
 // byte sizes [P][R] of the R pieces of each bucket of a variable column
 void piece_bytes(const int64_t* soff, const int64_t* start, int P, int R, int64_t* out, hipStream_t s);
 
+// ---------------------------------------------------------------- segops.hip
+// marks[seg[s]] += 1 for s in [1, nseg) with seg[s] < nval (marks zeroed
+// here, nval entries): inclusive scan -> segment id per value
+void seg_marks(const int64_t* seg, int64_t nseg, int64_t nval, int64_t* marks, hipStream_t s);
+// counts[idx[i]]++ over K bins (zeroed here), global atomics
+void histogram(const int64_t* idx, int64_t n, int64_t K, int64_t* counts, hipStream_t s);
+// f[i] = v[i] != 0 ; out[pos[i]] = i for non-zero v (pos = exclusive scan of f)
+void nz_flags(const uint64_t* v, int64_t n, int32_t* f, hipStream_t s);
+void compact_nz(const uint64_t* v, const int64_t* pos, int64_t n, int64_t* out, hipStream_t s);
+
 // ---------------------------------------------------------------- kvops.hip
 // Sort-key construction: fixed-width keys (kw<=8) loaded little-endian into a
 // uint64 and transformed so that unsigned order == requested order.

@@ -11,7 +11,10 @@
 #include <cstdarg>
 #include <cstdlib>
 #include <filesystem>
+#include <limits>
 #include <random>
+
+#include <ATen/CPUGeneratorImpl.h>
 
 #include "callbacks.h"
 #include "engine/graphplan.h"
@@ -60,7 +63,7 @@ at::Tensor kmv_vstart(const KMV& m) {
 }
 at::Tensor kmv_lens(const KMV& m) { return m.seg.narrow(0, 1, m.nkey) - m.seg.narrow(0, 0, m.nkey); }
 at::Tensor kmv_sid(const KMV& m) {
-  return at::repeat_interleave(at::arange(m.nkey, opt(m.seg.device(), at::kLong)), kmv_lens(m), 0, m.nval);
+  return segment_ids(m.seg, m.nkey, m.nval);
 }
 // w-byte items at byte offsets pos of vdata, as a [n, w] uint8 tensor
 at::Tensor gather_bytes(const at::Tensor& vdata, const at::Tensor& pos, int w) {
@@ -419,7 +422,7 @@ class NeighTri : public Command {
       if (src.vw >= 0 && src.vw % 8) throw Error("neighbor values must be lists of vertices");
       at::Tensor cnt = src.vw >= 0 ? at::full({src.n}, (int64_t)(src.vw / 8), opt(src.device(), at::kLong))
                                    : at::floor_divide(src.voff.narrow(0, 1, src.n) - src.voff.narrow(0, 0, src.n), 8);
-      add_tensors(kv, at::repeat_interleave(src.kdata.view(at::kLong), cnt), src.vdata.view(at::kLong));
+      add_tensors(kv, src.kdata.view(at::kLong).index_select(0, repeat_index(cnt)), src.vdata.view(at::kLong));
     });
     mrnplus.map_mr_batch(
         mrt,
@@ -563,12 +566,14 @@ class TriFindMR : public Command {
 
 at::Tensor present(const EdgePlan& p) {  // local vertices that appear in any edge
   if (p.nlocal == 0) return at::zeros({0}, opt(p.dev, at::kBool));
-  return at::bincount(p.src.to(at::kLong), {}, p.nlocal).narrow(0, 0, p.nlocal) > 0;
+  return bincount_dev(p.src, p.nlocal) > 0;
 }
 
 // cc_find nthresh: (vertex, component id = min vertex id) (oink/cc_find.cpp:38-109).
-// nthresh (hot-zone splitting) is accepted; the plan's segments are
-// load-balanced by value count, so hot zones need no splitting.
+// nthresh (hot-zone splitting) is accepted and unused here: on the edge plan
+// a vertex is one key and a hub's in-edges are one load-balanced segment, so
+// no zone ever gathers on one rank. cc_find_mr runs the reference's zone
+// pipeline, where nthresh does split hot zones over ranks.
 class CCFind : public Command {
  public:
   CCFind(Oink& o) : Command(o) { ninputs = noutputs = 1; }
@@ -591,6 +596,141 @@ class CCFind : public Command {
     obj.output(1, mrv, print_vertex_u64);
     const int64_t ncc = comm->allreduce(ids.numel() ? (zl == ids).sum().item<int64_t>() : 0, Comm::SUM);
     message(fmt("CC_find: %" PRId64 " components in %d iterations", ncc, niter));
+    obj.cleanup();
+  }
+};
+
+// cc_find_mr nthresh: the reference's MapReduce formulation of connected
+// components (oink/cc_find.cpp:38-109) with its hot-zone splitting: a zone
+// holding more than nthresh vertices is marked with the high bit, and from
+// then on its vertices are scattered over random ranks (a random rank id in
+// the bits under the high bit of the key, :224-234) while zone-change records
+// for it are replicated to every such salted key (:240-265) — so no single
+// rank has to reduce a giant zone. Per iteration: 2 collates to attach the
+// current zone to both ends of every edge, a winner reduce that emits
+// (loser zone -> winner zone) pairs, and a salted collate + reassign reduce.
+// Every callback is a batch callback on device tensors.
+class CCFindMR : public Command {
+ public:
+  CCFindMR(Oink& o) : Command(o) { ninputs = noutputs = 1; }
+  int64_t nthresh = 0;
+  void params(const Args& a) override {
+    if (a.size() != 1) throw Error("Illegal cc_find_mr command");
+    nthresh = lval(a[0], "cc_find_mr");
+  }
+  void run() override {
+    constexpr int64_t HIBIT = std::numeric_limits<int64_t>::min();  // bit 63
+    const int64_t P = nprocs;
+    int pbits = 0;
+    while ((int64_t(1) << pbits) < P) ++pbits;
+    const int pshift = 63 - pbits;                         // rank id sits just under the high bit
+    const int64_t lmask = (int64_t)(~0ull >> (pbits + 1));  // strips the high bit and the rank id
+    at::Generator gen = at::make_generator<at::CPUGeneratorImpl>(123456789 + (uint64_t)me);
+    MapReduce& mre = obj.input(1, rd(parse_edge), rc(parse_edge));
+    MapReduce& mrv = obj.create_mr();
+    MapReduce& mrz = obj.create_mr();
+    const at::Device dev = comm->device();
+    // every vertex starts in its own zone
+    mrv.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {
+      if (!src.n) return;
+      at::Tensor e = edges_of(src);
+      add_tensors(kv, at::cat({e.select(1, 0), e.select(1, 1)}));
+    });
+    mrv.collate();
+    mrv.reduce_batch([](const KMV& m, KeyValue& kv) {
+      if (m.nkey) add_tensors(kv, m.keys.kdata.view(at::kLong), m.keys.kdata.view(at::kLong));
+    });
+    int niter = 0;
+    while (true) {
+      ++niter;
+      // (v, edge) for both ends + (v, zone): the zone rides along to every edge
+      mrz.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {
+        if (!src.n) return;
+        at::Tensor e = edges_of(src);
+        add_tensors(kv, at::cat({e.select(1, 0), e.select(1, 1)}), at::cat({e, e}));
+      });
+      mrz.add(mrv);
+      mrz.collate();
+      mrz.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_edge_zone: (edge, zone of this end)
+        if (!m.nval) return;
+        at::Tensor vl = kmv_vlens(m), vs = kmv_vstart(m), sid = kmv_sid(m);
+        at::Tensor is_zone = vl == 8, is_edge = vl == 16;
+        at::Tensor zone_of = at::zeros({m.nkey}, opt(m.seg.device(), at::kLong));
+        zone_of.index_put_({sid.index({is_zone})}, gather_bytes(m.vdata, vs.index({is_zone}), 8).view(at::kLong).reshape({-1}));
+        at::Tensor ed = gather_bytes(m.vdata, vs.index({is_edge}), 16).view(at::kLong).view({-1, 2});
+        if (ed.numel()) add_tensors(kv, ed, zone_of.index({sid.index({is_edge})}));
+      });
+      mrz.collate();
+      int64_t changed = 0;
+      mrz.reduce_batch([&](const KMV& m, KeyValue& kv) {  // reduce_zone_winner
+        if (!m.nkey) return;
+        at::Tensor z = m.vdata.view(at::kLong), h = m.seg.narrow(0, 0, m.nkey);
+        at::Tensor z0 = z.index({h}), z1 = z.index({at::clamp_max(h + 1, m.nval - 1)});
+        at::Tensor s0 = at::bitwise_and(z0, ~HIBIT), s1 = at::bitwise_and(z1, ~HIBIT);
+        at::Tensor diff = s0 != s1;
+        changed = diff.sum().item<int64_t>();
+        if (!changed) return;
+        at::Tensor big = at::where(s0 > s1, z0, z1).index({diff}), small = at::where(s0 > s1, z1, z0).index({diff});
+        // value = PAD {winner zone, pad}: 16 bytes tell it apart from an 8-byte vertex
+        add_tensors(kv, big, at::stack({small, at::zeros_like(small)}, 1));
+      });
+      if (comm->allreduce(changed, Comm::SUM) == 0) break;
+      // vertices of hot zones go to a random salted copy of their zone key
+      mrv.map_mr_batch(mrv, [&](const KV& src, KeyValue& kv) {  // map_invert_multi
+        if (!src.n) return;
+        at::Tensor v = src.kdata.view(at::kLong), zn = src.vdata.view(at::kLong);
+        at::Tensor hot = zn < 0;
+        at::Tensor rp = at::randint(P, {src.n}, gen, at::TensorOptions().dtype(at::kLong)).to(zn.device());
+        add_tensors(kv, at::where(hot, at::bitwise_or(zn, at::bitwise_left_shift(rp, pshift)), zn), v);
+      });
+      mrv.map_mr_batch(mrz, [&](const KV& src, KeyValue& kv) {  // map_zone_multi: replicate to every salted key
+        if (!src.n) return;
+        at::Tensor zn = src.kdata.view(at::kLong), pad = src.vdata.view(at::kLong).view({-1, 2});
+        at::Tensor hot = zn < 0, strip = at::bitwise_and(zn, ~HIBIT);
+        add_tensors(kv, strip, pad);
+        if (!hot.any().item<bool>()) return;
+        at::Tensor hz = strip.index({hot}), hp = pad.index({hot});
+        for (int64_t r = 0; r < P; ++r)
+          add_tensors(kv, at::bitwise_or(at::bitwise_or(hz, r << pshift), HIBIT), hp);
+      }, 1);
+      mrv.collate();
+      mrv.reduce_batch([&](const KMV& m, KeyValue& kv) {  // reduce_zone_reassign
+        if (!m.nkey) return;
+        at::Tensor key = m.keys.kdata.view(at::kLong);
+        at::Tensor vl = kmv_vlens(m), vs = kmv_vstart(m), sid = kmv_sid(m);
+        at::Tensor isv = vl == 8, isp = vl == 16;
+        at::Tensor zone = at::bitwise_and(key, lmask), hkey = key < 0;
+        at::Tensor hwin = at::zeros({m.nkey}, opt(m.seg.device(), at::kBool));
+        if (isp.any().item<bool>()) {
+          at::Tensor pz = gather_bytes(m.vdata, vs.index({isp}), 8).view(at::kLong).reshape({-1});
+          at::Tensor ps = sid.index({isp}), pzs = at::bitwise_and(pz, ~HIBIT);
+          at::Tensor best = zone.clone().scatter_reduce_(0, ps, pzs, "amin", true);
+          // the winner's high bit comes along when a strictly smaller zone wins
+          at::Tensor won = at::logical_and(pzs == best.index({ps}), pzs < zone.index({ps}));
+          hwin.index_put_({ps.index({at::logical_and(won, pz < 0)})}, true);
+          zone = best;
+        }
+        at::Tensor nvert = bincount_dev(sid.index({isv}), m.nkey);
+        at::Tensor hot = at::logical_or(at::logical_or(hkey, hwin), nvert > nthresh);
+        zone = at::where(hot, at::bitwise_or(zone, HIBIT), zone);
+        at::Tensor v = gather_bytes(m.vdata, vs.index({isv}), 8).view(at::kLong).reshape({-1});
+        if (v.numel()) add_tensors(kv, v, zone.index({sid.index({isv})}));
+      });
+    }
+    mrv.map_mr_batch(mrv, [&](const KV& src, KeyValue& kv) {  // map_strip
+      if (src.n) add_tensors(kv, src.kdata.view(at::kLong), at::bitwise_and(src.vdata.view(at::kLong), ~HIBIT));
+    });
+    obj.output(1, mrv, print_vertex_u64);
+    uint64_t ncc = 0;
+    {
+      MapReduce& mrc = obj.create_mr();
+      mrc.map_mr_batch(mrv, [](const KV& src, KeyValue& kv) {
+        if (src.n) add_tensors(kv, src.vdata.view(at::kLong), src.kdata.view(at::kLong));
+      });
+      ncc = mrc.collate();
+    }
+    (void)dev;
+    message(fmt("CC_find: %" PRIu64 " components in %d iterations", ncc, niter));
     obj.cleanup();
   }
 };
@@ -645,7 +785,8 @@ class LubyFind : public Command {
 
 // sssp ncnt seed -i weighted-edges -o file mr: single-source shortest paths
 // from ncnt random sources with out-edges (oink/sssp.cpp:49-184). Output
-// lines are "v distance source" (the reference's 3rd column is the predecessor).
+// lines are "v distance predecessor" as the reference prints them
+// (oink/sssp.cpp:405-411); the source's predecessor is 0 (DISTANCE()).
 class SSSP : public Command {
  public:
   SSSP(Oink& o) : Command(o) { ninputs = noutputs = 1; }
@@ -663,8 +804,7 @@ class SSSP : public Command {
                                                : at::ones({e.size(0)}, opt(dev, at::kDouble));
     const int64_t N = nvert_global(*comm, e);
     EdgePlan plan(comm, e, N, w, false);
-    at::Tensor outdeg = plan.nlocal ? at::bincount(plan.src.to(at::kLong), {}, plan.nlocal).narrow(0, 0, plan.nlocal)
-                                    : at::zeros({0}, opt(dev, at::kLong));
+    at::Tensor outdeg = bincount_dev(plan.src, plan.nlocal);
     at::Tensor cand = plan.local_ids.index({outdeg > 0}).contiguous();
     at::Tensor all = comm->allgather_var(cand).to(at::kCPU);
     std::vector<int64_t> c(all.data_ptr<int64_t>(), all.data_ptr<int64_t>() + all.numel());
@@ -679,8 +819,9 @@ class SSSP : public Command {
       at::Tensor ok = at::isfinite(d);
       const int64_t nlab = comm->allreduce(ok.sum().item<int64_t>(), Comm::SUM);
       message(fmt("%zu:  Source = %" PRId64 "; Iterations = %d; Num Vtx Labeled = %" PRId64, i, s, niter, nlab));
+      at::Tensor pred = sssp_predecessors(plan, e, w, d, s);
       at::Tensor ids = plan.local_ids.index({ok}), dd = d.index({ok});
-      at::Tensor vals = at::stack({dd.view(at::kLong), at::full_like(ids, s)}, 1);
+      at::Tensor vals = at::stack({dd.view(at::kLong), pred.index({ok})}, 1);
       mr.map(
           nprocs,
           [&](int, KeyValue& kv) {
@@ -745,6 +886,7 @@ struct Registrar {
     r["tri_find"] = factory<TriFind>();
     r["tri_find_mr"] = factory<TriFindMR>();
     r["cc_find"] = factory<CCFind>();
+    r["cc_find_mr"] = factory<CCFindMR>();
     r["cc_stats"] = factory<CCStats>();
     r["luby_find"] = factory<LubyFind>();
     r["sssp"] = factory<SSSP>();

@@ -106,6 +106,31 @@ static void chunk_map(int itask, char *str, int size, void *kv, void *app) {
   (void)app;
 }
 
+/* keyalign / valuealign: every pointer handed to a host callback is aligned
+   (reference src/keyvalue.cpp:345-352); odd-length keys make the packed
+   layout misaligned, so the engine must re-lay them out */
+static int misaligned = 0, aligned_seen = 0;
+static void gen_odd(int itask, void *kv, void *app) {
+  char k[32], v[32];
+  (void)app;
+  for (int i = 0; i < 300; ++i) {
+    int kl = 1 + (i * 7 + itask) % 11, vl = 1 + (i * 5) % 13;
+    for (int j = 0; j < kl; ++j) k[j] = (char)('a' + (i + j) % 5);
+    for (int j = 0; j < vl; ++j) v[j] = (char)('0' + (i + j) % 10);
+    MR_kv_add(kv, k, kl, v, vl);
+  }
+}
+static void scan_aligned(char *k, int kb, char *v, int vb, void *app) {
+  (void)kb; (void)vb; (void)app;
+  aligned_seen++;
+  if (((uintptr_t)k % 8) || ((uintptr_t)v % 16)) misaligned++;
+}
+static void reduce_aligned(char *k, int kb, char *mv, int nv, int *vb, void *kv, void *app) {
+  (void)kb; (void)nv; (void)vb; (void)kv; (void)app;
+  aligned_seen++;
+  if (((uintptr_t)k % 8) || ((uintptr_t)mv % 16)) misaligned++;
+}
+
 int main(int argc, char **argv) {
   const char *tmpdir = argc > 1 ? argv[1] : ".";
   MR_set_error_mode(1);
@@ -203,6 +228,22 @@ int main(int argc, char **argv) {
   while (f && fgets(buf, sizeof buf, f)) lines++;
   if (f) fclose(f);
   CHECK(lines == 7);
+
+  /* alignment of callback pointers */
+  void *al = MR_create(NULL);
+  MR_set_keyalign(al, 8);
+  MR_set_valuealign(al, 16);
+  CHECK(MR_map(al, 2, gen_odd, NULL) == 600);
+  MR_scan_kv(al, scan_aligned, NULL);
+  CHECK(aligned_seen == 600 && misaligned == 0);
+  MR_collate(al, NULL);
+  aligned_seen = 0;
+  MR_reduce(al, reduce_aligned, NULL);
+  CHECK(aligned_seen > 10 && misaligned == 0);
+  MR_set_keyalign(al, 3);
+  MR_map(al, 1, gen_odd, NULL);
+  CHECK(MR_scan_kv(al, scan_aligned, NULL) == 0 && strstr(MR_last_error(), "alignment") != NULL);
+  MR_destroy(al);
 
   /* errors come back as codes in error mode 1 */
   void *e = MR_create(NULL);

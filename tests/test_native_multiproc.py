@@ -96,6 +96,7 @@ def test_crmat_ranks(tmp_path):
 SCRIPTS_CASES = [
     ("in.tri", [], ("EdgeUpper", "Tri_find")),
     ("in.cc", [], ("EdgeUpper", "CC_find", "CCStats", "  ")),
+    ("in.ccmr", [], ("EdgeUpper", "CC_find", "CCStats", "  ")),
     ("in.luby", [], ("EdgeUpper", "Luby_find")),
     ("in.pagerank", [], ("PageRank: 2",)),
     ("in.rmat", [], ("RMAT: 256", "DegreeStats", "  ")),
@@ -123,6 +124,16 @@ def test_oink_scripts_native_ranks(tmp_path, script, extra, keys):
         assert pick(one) and pick(one) == pick(two)
         return
     assert _lines(one, *keys) and _lines(one, *keys) == _lines(two, *keys)
+
+
+def test_cc_find_mr_salted_matches_plan_3_ranks(tmp_path):
+    """hot-zone splitting across 3 ranks (every zone above 2 vertices is
+    salted) gives the same components as the edge-plan cc_find"""
+    plan = _oink("in.cc", 3, tmp_path, [])
+    mr = _oink("in.ccmr", 3, tmp_path, ["-var", "nthresh", "2"])
+    keys = ("CC_find", "CCStats", "  ")
+    pick = lambda o: [ln.split(" in ")[0] for ln in _lines(o, *keys)]
+    assert pick(plan) and pick(plan) == pick(mr)
 
 
 def test_oink_wordfreq_script_ranks(tmp_path):

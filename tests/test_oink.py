@@ -105,6 +105,31 @@ def test_cc_find_stats(tmp_path, monkeypatch):
     assert f"CCStats: {ncc} components, {present.sum()} vertices" in text
 
 
+@pytest.mark.parametrize("nthresh", [1000000, 2])
+def test_cc_find_mr_zone_salting(tmp_path, monkeypatch, nthresh):
+    """cc_find_mr: the reference's zone pipeline (oink/cc_find.cpp:38-109).
+    With nthresh = 2 nearly every zone becomes 'hot' and its vertices are
+    salted over ranks; the components must not change."""
+    from gpu_mapreduce_amd.models.graph import reference_cc
+    s = ("rmat 8 1 0.25 0.25 0.25 0.25 0.0 99 -o tmp.rmat mre\n"
+         "edge_upper -i mre -o NULL mre\n"
+         f"cc_find_mr {nthresh} -i mre -o tmp.ccmr mrc\n"
+         "cc_stats -i mrc\n")
+    o, text = run(s, tmp_path, monkeypatch)
+    e = _upper(load_edges(tmp_path / "tmp.rmat.0"))
+    n = int(e.max()) + 1
+    lab = reference_cc(e, n)
+    got = np.loadtxt(tmp_path / "tmp.ccmr.0", dtype=np.int64, ndmin=2)
+    gd = dict(zip(got[:, 0], got[:, 1]))
+    present = np.zeros(n, bool)
+    present[e.ravel()] = True
+    assert set(gd) == set(np.nonzero(present)[0])
+    for v in gd:
+        assert gd[v] == lab[v]
+    ncc = len(set(lab[present]))
+    assert f"CC_find: {ncc} components" in text
+
+
 def test_luby_find(tmp_path, monkeypatch):
     s = (RMAT.format(out="tmp.rmat") + "edge_upper -i mre -o NULL mre\n"
          "luby_find 12345 -i mre -o tmp.mis NULL\n")
@@ -123,6 +148,11 @@ def test_luby_find(tmp_path, monkeypatch):
 
 
 def test_sssp(tmp_path, monkeypatch):
+    """distances match Dijkstra, and the third column is the predecessor as the
+    reference prints it (oink/sssp.cpp:405-411): 0 for the source, otherwise a
+    u with an edge u -> v and d[u] + w == d[v] (the smallest such u: our
+    deterministic tie-break)."""
+    import re
     from scipy.sparse import csr_matrix
     from scipy.sparse.csgraph import dijkstra
     s = ("rmat 5 3 0.25 0.25 0.25 0.25 0.0 12345 -o tmp.rmat mre\n"
@@ -133,16 +163,27 @@ def test_sssp(tmp_path, monkeypatch):
     n = int(e.max()) + 1
     G = csr_matrix((np.ones(len(e)), (e[:, 0], e[:, 1])), shape=(n, n))
     rows = np.loadtxt(tmp_path / "tmp.sssp.0", ndmin=2)
-    srcs = sorted(set(rows[:, 2].astype(np.int64)))
-    assert len(srcs) == 3
-    for sidx in srcs:
+    blocks = [(int(a), int(b)) for a, b in re.findall(r"Source = (\d+); Iterations = \d+; Num Vtx Labeled = (\d+)", text)]
+    assert len(blocks) == 3 and sum(b for _, b in blocks) == len(rows)
+    inn = {}
+    for a, b in e:
+        inn.setdefault(int(b), set()).add(int(a))
+    start = 0
+    for sidx, cnt in blocks:
+        r = rows[start:start + cnt]
+        start += cnt
         d = dijkstra(G, indices=sidx)
-        r = rows[rows[:, 2] == sidx]
         got = dict(zip(r[:, 0].astype(np.int64), r[:, 1]))
         want = {i: d[i] for i in range(n) if np.isfinite(d[i])}
         assert got.keys() == want.keys()
         for k in got:
             assert got[k] == pytest.approx(want[k])
+        for v, dv, pv in zip(r[:, 0].astype(np.int64), r[:, 1], r[:, 2].astype(np.int64)):
+            if v == sidx:
+                assert pv == 0 and dv == 0
+                continue
+            cands = sorted(u for u in inn.get(int(v), ()) if np.isfinite(d[u]) and d[u] + 1 == d[v])
+            assert cands and pv == cands[0], (v, pv, cands)
 
 
 def test_wordfreq_histo(tmp_path, monkeypatch):
