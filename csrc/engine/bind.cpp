@@ -573,7 +573,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("rowptr", &TriangleGraph::rowptr)
       .def_readonly("col", &TriangleGraph::col)
       .def_readonly("okeys", &TriangleGraph::okeys)
-      .def_readonly("perm", &TriangleGraph::perm);
+      .def_readonly("perm", &TriangleGraph::perm)
+      .def_readonly("distributed", &TriangleGraph::distributed)
+      .def_readonly("nlocal", &TriangleGraph::nlocal)
+      .def_readonly("nrows", &TriangleGraph::nrows)
+      .def_readonly("row_gid", &TriangleGraph::row_gid);
   m.def("tri_prepare", &mrh::tri_prepare);
   m.def("tri_count", &mrh::tri_count);
   m.def("tri_list", &mrh::tri_list);

@@ -1,6 +1,7 @@
 // Native graph engines (see graphplan.h).
 #include "graphplan.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -329,41 +330,187 @@ at::Tensor PageRankPlan::ids() const { return order_ * P + me; }
 
 // ====================================================================== triangles
 
+namespace {
+// route the int64 rows of a [n, k] tensor to ranks `dest` (engine shuffle)
+at::Tensor route_rows(const Comm& comm, const at::Tensor& rows, const at::Tensor& dest, int k) {
+  const at::Device dev = comm.device();
+  const int64_t n = rows.size(0);
+  KV kv;
+  kv.n = n;
+  kv.kw = 8 * k;
+  kv.vw = 0;
+  kv.kdata = rows.contiguous().view(at::kByte).reshape({-1});
+  kv.vdata = at::empty({0}, opt(dev, at::kByte));
+  kv = exchange(std::move(kv), dest.to(at::kInt), comm);
+  return kv.kdata.view(at::kLong).view({-1, k});
+}
+
+// position of every query in sorted unique keys, -1 if absent
+at::Tensor lookup(const at::Tensor& keys, const at::Tensor& q) {
+  at::Tensor out = at::empty({q.numel()}, q.options().dtype(at::kLong));
+  if (!q.numel()) return out;
+  if (q.is_cuda()) {
+    k::lookup_sorted(keys.data_ptr<int64_t>(), keys.numel(), q.data_ptr<int64_t>(), q.numel(), out.data_ptr<int64_t>(),
+                     at::hip::getCurrentHIPStream());
+    return out;
+  }
+  const int64_t* kp = keys.data_ptr<int64_t>();
+  const int64_t* qp = q.data_ptr<int64_t>();
+  int64_t* o = out.data_ptr<int64_t>();
+  for (int64_t j = 0; j < q.numel(); ++j) {
+    const int64_t* it = std::lower_bound(kp, kp + keys.numel(), qp[j]);
+    o[j] = (it != kp + keys.numel() && *it == qp[j]) ? it - kp : -1;
+  }
+  return out;
+}
+
+// sorted unique values of an int64 column
+at::Tensor unique_sorted(const at::Tensor& x) {
+  if (x.numel() == 0) return x.contiguous();
+  at::Tensor s = sort_with_perm(x.contiguous()).first;
+  at::Tensor sg = segments(s);
+  return s.index_select(0, sg.narrow(0, 0, sg.numel() - 1)).contiguous();
+}
+
+// a spread of the packed edge bits (the owner of an undirected edge)
+at::Tensor edge_owner(const at::Tensor& p, int P) {
+  at::Tensor h = at::bitwise_xor(p, at::bitwise_right_shift(p, 29)) * (int64_t)0x9E3779B97F4A7C15ull;
+  return at::remainder(at::bitwise_and(at::bitwise_right_shift(h, 24), (int64_t(1) << 39) - 1), P);
+}
+}  // namespace
+
 TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : comm(std::move(c)) {
   const at::Device dev = comm->device();
   at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2});
   at::Tensor lo = at::minimum(e.select(1, 0), e.select(1, 1)), hi = at::maximum(e.select(1, 0), e.select(1, 1));
   at::Tensor keep = lo != hi;
-  at::Tensor p = at::bitwise_or(at::bitwise_left_shift(lo.index({keep}), 32), hi.index({keep})).contiguous();
-  if (comm->distributed()) p = comm->allgather_var(p);
-  at::Tensor uniq = p;
-  if (p.numel()) {
-    at::Tensor s = sort_with_perm(p).first;
-    at::Tensor sg = segments(s);
-    uniq = s.index_select(0, sg.narrow(0, 0, sg.numel() - 1)).contiguous();
-  }
-  nedge = uniq.numel();
-  if (nv < 0) {
-    const int64_t mx = nedge ? at::maximum(at::bitwise_right_shift(uniq, 32), at::bitwise_and(uniq, (int64_t)0xffffffff))
-                                   .max()
-                                   .item<int64_t>()
-                             : -1;
-    nv = comm->allreduce(mx, Comm::MAX) + 1;
-  }
+  lo = lo.index({keep});
+  hi = hi.index({keep});
+  if (nv < 0) nv = comm->allreduce(hi.numel() ? hi.max().item<int64_t>() : -1, Comm::MAX) + 1;
   nvert = nv;
-  if (nvert >= (int64_t(1) << 32) - 1) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^32-1");
+  if (nvert >= (int64_t(1) << 31)) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^31");
+  const char* rep = std::getenv("MRH_TRI_REPLICATED");
+  if (comm->distributed() && !(rep && *rep == '1')) {
+    build_distributed(lo, hi);
+    return;
+  }
+  // replicated degree-oriented CSR (every rank holds the whole graph and
+  // counts a 1/P slice of its oriented edges)
+  distributed = false;
+  at::Tensor p = at::bitwise_or(at::bitwise_left_shift(lo, 32), hi).contiguous();
+  if (comm->distributed()) p = comm->allgather_var(p);
+  at::Tensor uniq = unique_sorted(p);
+  nedge = uniq.numel();
   std::tie(rowptr, col, okeys, perm) = tri_prepare(uniq, std::max<int64_t>(nvert, 1));
   const int64_t m = okeys.numel(), P = comm->size(), me = comm->rank();
   e0 = me * m / P;
   e1 = (me + 1) * m / P;
 }
 
-int64_t TriangleGraph::count() const { return comm->allreduce(tri_count(rowptr, col, okeys, e0, e1), Comm::SUM); }
+// Distributed build (reference tri_find shuffles every edge 4 times,
+// oink/tri_find.cpp:43-82): memory per rank is O(E/P + halo), never the
+// whole graph.
+//  1. dedup: every undirected edge to a hashed owner, sort + unique;
+//  2. degrees at the vertex owners (v % P);
+//  3. orientation u -> v by (degree, id): the edge visits the owners of both
+//     ends to pick up their degrees, then lands at the owner of u;
+//  4. local CSR of the owned rows N+(u), u % P == me;
+//  5. halo: the owners of the remote targets v return N+(v) (one request /
+//     response all-to-all pair), keeping only entries that are rows here
+//     (any w of a triangle u, v, w lies in N+(u), so nothing else can match);
+//  6. rows relabelled into one local id space (owned u -> u / P, halo -> nlocal
+//     + index) with every row sorted, so the LDS-hash / merge kernels of the
+//     replicated path count the owned rows unchanged.
+void TriangleGraph::build_distributed(const at::Tensor& lo_in, const at::Tensor& hi_in) {
+  distributed = true;
+  const Comm& cm = *comm;
+  const int P = cm.size(), me = cm.rank();
+  const at::Device dev = cm.device();
+  auto L = at::TensorOptions().device(dev).dtype(at::kLong);
+  nlocal = std::max<int64_t>(0, (nvert - me + P - 1) / P);
+  // 1. dedup at hashed owners
+  at::Tensor p = at::bitwise_or(at::bitwise_left_shift(lo_in, 32), hi_in).contiguous();
+  p = route_rows(cm, p.view({-1, 1}), edge_owner(p, P), 1).reshape({-1});
+  p = unique_sorted(p);
+  nedge = cm.allreduce(p.numel(), Comm::SUM);
+  at::Tensor lo = at::bitwise_right_shift(p, 32), hi = at::bitwise_and(p, (int64_t)0xffffffff);
+  // 2. degrees at the owners
+  at::Tensor ends = at::cat({lo, hi}).view({-1, 1});
+  at::Tensor got = route_rows(cm, ends, at::remainder(ends.reshape({-1}), P), 1).reshape({-1});
+  at::Tensor deg = bincount_dev(at::floor_divide(got, P), nlocal);
+  // 3. orientation: pick up deg(lo) at owner(lo), deg(hi) at owner(hi)
+  at::Tensor r = route_rows(cm, at::stack({lo, hi}, 1), at::remainder(lo, P), 2);
+  r = at::stack({r.select(1, 0), r.select(1, 1), deg.index_select(0, at::floor_divide(r.select(1, 0), P))}, 1);
+  r = route_rows(cm, r, at::remainder(r.select(1, 1), P), 3);
+  at::Tensor a = r.select(1, 0), b = r.select(1, 1), da = r.select(1, 2);
+  at::Tensor db = deg.index_select(0, at::floor_divide(b, P));
+  at::Tensor a_first = at::logical_or(da < db, at::logical_and(da == db, a < b));
+  at::Tensor u = at::where(a_first, a, b), v = at::where(a_first, b, a);
+  at::Tensor uv = route_rows(cm, at::stack({u, v}, 1), at::remainder(u, P), 2);
+  u = uv.select(1, 0).contiguous();
+  v = uv.select(1, 1).contiguous();
+  // 4. owned rows, sorted by (local row, target id)
+  at::Tensor lu = at::floor_divide(u, P);
+  {
+    auto sp = sort_with_perm(at::bitwise_or(at::bitwise_left_shift(lu, 32), v));
+    at::Tensor pl = sp.second.to(at::kLong);
+    u = u.index_select(0, pl);
+    v = v.index_select(0, pl);
+    lu = lu.index_select(0, pl);
+  }
+  at::Tensor own_rp = exclusive_scan(bincount_dev(lu, nlocal));
+  // 5. halo rows: request N+(v) for remote targets
+  at::Tensor remote = at::remainder(v, P) != me;
+  at::Tensor hids = unique_sorted(v.index({remote}));
+  at::Tensor req = route_rows(cm, at::stack({hids, at::full_like(hids, me)}, 1), at::remainder(hids, P), 2);
+  at::Tensor rv = req.select(1, 0).contiguous(), rq = req.select(1, 1).contiguous();
+  at::Tensor rrow = at::floor_divide(rv, P);
+  at::Tensor rcnt = own_rp.index_select(0, rrow + 1) - own_rp.index_select(0, rrow);
+  at::Tensor rep = repeat_index(rcnt);                       // request of every response entry
+  at::Tensor pos = own_rp.index_select(0, rrow).index_select(0, rep) +
+                   (at::arange(rep.numel(), L) - exclusive_scan(rcnt).narrow(0, 0, rcnt.numel()).index_select(0, rep));
+  at::Tensor resp = at::stack({rv.index_select(0, rep), v.index_select(0, pos)}, 1);
+  resp = route_rows(cm, resp, rq.index_select(0, rep), 2);
+  at::Tensor hv = resp.select(1, 0).contiguous(), hw = resp.select(1, 1).contiguous();
+  // keep only entries that are rows here (owned, or a requested halo id)
+  at::Tensor hw_halo = lookup(hids, hw);
+  at::Tensor keep = at::logical_or(at::remainder(hw, P) == me, hw_halo >= 0);
+  hv = hv.index({keep});
+  hw = hw.index({keep});
+  hw_halo = hw_halo.index({keep});
+  // 6. one local id space, rows sorted by local id
+  const int64_t nh = hids.numel();
+  nrows = nlocal + nh;
+  auto relabel = [&](const at::Tensor& x, const at::Tensor& halo_idx) {
+    return at::where(at::remainder(x, P) == me, at::floor_divide(x, P), halo_idx + nlocal);
+  };
+  at::Tensor own_col = relabel(v, lookup(hids, v));
+  at::Tensor h_row = lookup(hids, hv) + nlocal;
+  at::Tensor h_col = relabel(hw, hw_halo);
+  at::Tensor rows_all = at::cat({lu, h_row}), cols_all = at::cat({own_col, h_col});
+  auto sp = sort_with_perm(at::bitwise_or(at::bitwise_left_shift(rows_all, 32), cols_all));
+  at::Tensor keys = sp.first;
+  col = at::bitwise_and(keys, (int64_t)0xffffffff).to(at::kInt).contiguous();
+  rowptr = exclusive_scan(bincount_dev(at::bitwise_right_shift(keys, 32), nrows));
+  // owned oriented edges in the local space (row < nlocal), for counting and listing
+  at::Tensor owned = at::bitwise_right_shift(keys, 32) < nlocal;
+  okeys = keys.index({owned}).contiguous();
+  e0 = 0;
+  e1 = okeys.numel();
+  // global id of every local row
+  row_gid = at::cat({at::arange(nlocal, L) * P + me, hids});
+}
+
+int64_t TriangleGraph::count() const {
+  if (!distributed) return comm->allreduce(tri_count(rowptr, col, okeys, e0, e1), Comm::SUM);
+  return comm->allreduce(tri_count_rows(rowptr, col, 0, nlocal), Comm::SUM);
+}
 
 at::Tensor TriangleGraph::triangles() const {
   at::Tensor t = tri_list(rowptr, col, okeys, e0, e1);
   if (!t.numel()) return t;
-  return std::get<0>(at::sort(perm.index_select(0, t.reshape({-1})).view({-1, 3}), 1));
+  const at::Tensor& ids = distributed ? row_gid : perm;
+  return std::get<0>(at::sort(ids.index_select(0, t.reshape({-1})).view({-1, 3}), 1));
 }
 
 }  // namespace mrh

@@ -95,7 +95,9 @@ class PageRankPlan {
   std::vector<int64_t> send_splits_, recv_splits_;
 };
 
-// Triangle finder on the replicated degree-oriented CSR (tri.cpp kernels)
+// Triangle finder on a degree-oriented CSR (tri.cpp kernels). Multi-rank jobs
+// build it distributed (owned rows + fetched halo rows, O(E/P + halo) per
+// rank); MRH_TRI_REPLICATED=1 (or a single rank) replicates the whole graph.
 class TriangleGraph {
  public:
   TriangleGraph(CommPtr comm, const at::Tensor& edges, int64_t nvert = -1);
@@ -104,7 +106,12 @@ class TriangleGraph {
 
   CommPtr comm;
   int64_t nvert = 0, nedge = 0, e0 = 0, e1 = 0;
-  at::Tensor rowptr, col, okeys, perm;
+  bool distributed = false;
+  int64_t nlocal = 0, nrows = 0;  // distributed: owned rows, owned + halo rows
+  at::Tensor rowptr, col, okeys, perm, row_gid;
+
+ private:
+  void build_distributed(const at::Tensor& lo, const at::Tensor& hi);
 };
 
 }  // namespace mrh

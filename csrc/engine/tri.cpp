@@ -121,6 +121,26 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
   return n;
 }
 
+int64_t tri_count_rows(const at::Tensor& rowptr, const at::Tensor& col, int64_t u0, int64_t u1) {
+  if (u1 <= u0) return 0;
+  if (rowptr.is_cuda()) {
+    const at::Device dev = rowptr.device();
+    at::Tensor tot = at::zeros({1}, opt(dev, at::kLong));
+    at::Tensor big = at::empty({2 * std::max<int64_t>(u1 - u0, 1)}, opt(dev, at::kInt));
+    at::Tensor nbig = at::zeros({2}, opt(dev, at::kInt));
+    k::tri_count_hash(P0<int64_t>(rowptr), P0<uint32_t>(col), u0, u1, P0<uint32_t>(big), P0<uint32_t>(nbig),
+                      P0<unsigned long long>(tot), cur());
+    return tot.item<int64_t>();
+  }
+  at::Tensor rp_h = rowptr.to(at::kCPU).contiguous(), col_h = col.to(at::kCPU).contiguous();
+  const int64_t* rp = P0<int64_t>(rp_h);
+  const int32_t* c = P0<int32_t>(col_h);
+  int64_t n = 0;
+  for (int64_t u = u0; u < u1; ++u)
+    for (int64_t e = rp[u]; e < rp[u + 1]; ++e) n += intersect_host<false>(rp, c, (uint32_t)u, (uint32_t)c[e], nullptr);
+  return n;
+}
+
 at::Tensor tri_list(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1) {
   e1 = std::min<int64_t>(e1, okeys.numel());
   const at::Device dev = okeys.device();

@@ -13,6 +13,10 @@ namespace mrh {
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq, int64_t nvert);
 // number of triangles whose first oriented edge lies in [e0, e1)
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1);
+// number of triangles u < v < w (in the CSR's id order) over the rows u in
+// [u0, u1): rows outside the range are only looked up (the distributed
+// graph's halo)
+int64_t tri_count_rows(const at::Tensor& rowptr, const at::Tensor& col, int64_t u0, int64_t u1);
 // the triangles found on oriented edges [e0, e1) as [T,3] int64 rank ids
 at::Tensor tri_list(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1);
 }  // namespace mrh

@@ -48,7 +48,29 @@ __global__ __launch_bounds__(NT) void k_compact_nz(const uint64_t* __restrict__ 
     if (v[i]) out[pos[i]] = i;
 }
 
+// idx[j] = position of q[j] in the sorted unique keys, or -1
+__global__ __launch_bounds__(NT) void k_lookup_sorted(const int64_t* __restrict__ keys, int64_t n,
+                                                     const int64_t* __restrict__ q, int64_t m,
+                                                     int64_t* __restrict__ idx) {
+  for (int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x; j < m; j += (int64_t)gridDim.x * NT) {
+    const int64_t x = q[j];
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (keys[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    idx[j] = (lo < n && keys[lo] == x) ? lo : -1;
+  }
+}
+
 }  // namespace
+
+void lookup_sorted(const int64_t* keys, int64_t n, const int64_t* q, int64_t m, int64_t* idx, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_lookup_sorted, dim3(blocks(m)), dim3(NT), 0, s, keys, n, q, m, idx);
+  MRH_CHECK_LAUNCH();
+}
 
 void seg_marks(const int64_t* seg, int64_t nseg, int64_t nval, int64_t* marks, hipStream_t s) {
   (void)hipMemsetAsync(marks, 0, sizeof(int64_t) * std::max<int64_t>(nval, 1), s);

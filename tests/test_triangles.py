@@ -81,3 +81,33 @@ def test_gpu_matches_cpu(scale, ef):
         a = a[np.lexsort(a.numpy().T[::-1])]
         b = b[np.lexsort(b.numpy().T[::-1])]
         assert torch.equal(a, b)
+
+
+def case_tri_distributed(comm):
+    """each rank holds a slice of the edges; the distributed graph (owned rows
+    + halo) must count and list exactly the replicated graph's triangles"""
+    import os
+    e = _rmat(11, 8, 7)
+    mine = e[comm.rank::comm.size]
+    g = TriangleGraph(comm, mine)
+    os.environ["MRH_TRI_REPLICATED"] = "1"
+    r = TriangleGraph(comm, mine)
+    os.environ.pop("MRH_TRI_REPLICATED")
+    return (g.count(), r.count(), g._g.distributed, g._g.nrows, g.nvert, g._g.okeys.numel(),
+            [tuple(t) for t in g.triangles().tolist()])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_triangles_match_replicated(world):
+    from test_distributed_cpu import run_world
+    out = run_world("test_triangles:case_tri_distributed", world)
+    want = _brute_list(_rmat(11, 8, 7).numpy())
+    tris = set()
+    owned_edges = 0
+    for r, (cnt, rcnt, dist, nrows, nvert, nown, lst) in out.items():
+        assert dist and cnt == rcnt == len(want)
+        assert nrows < nvert, "a rank must not hold every vertex's row"
+        owned_edges += nown
+        assert not (tris & set(lst)), "a triangle listed on two ranks"
+        tris |= set(lst)
+    assert tris == want
