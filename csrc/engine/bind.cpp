@@ -268,6 +268,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         return r.collate(f);
       })
       .def("convert", &MR::convert, py::call_guard<py::gil_scoped_release>())
+      .def("convert_prehashed", &MR::convert_prehashed, py::call_guard<py::gil_scoped_release>())
       .def("gather", &MR::gather, py::call_guard<py::gil_scoped_release>())
       .def("open", &MR::open, py::call_guard<py::gil_scoped_release>())
       .def("kv_open", [](MR& r) { return kvref(r.kv_open()); })

@@ -492,7 +492,7 @@ at::Tensor segments_sorted(const at::Tensor& sorted_keys) {
   return seg;
 }
 
-KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits) {
+KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tensor& prehash) {
   const at::Device dev = kv.device();
   KMV out;
   ConvertStats local;
@@ -514,7 +514,15 @@ KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits) {
     sk_in = raw_keys_u64(kv, 0, false, kv.kdata, kv.kw, &idx);
     end_bit = 8 * kv.kw;
   } else {
-    sk_in = hash64_keys(kv);
+    // the 64-bit grouping hash of every key, unless the producer already
+    // computed it (the pipelined InvertedIndex map hashes each file's URLs
+    // while the next file is still on the PCIe link)
+    if (prehash.defined()) {
+      if (prehash.numel() != n || prehash.scalar_type() != at::kLong) fail("convert: prehash must be int64 [n]");
+      sk_in = prehash.to(dev).contiguous();
+    } else {
+      sk_in = hash64_keys(kv);
+    }
     if (force_hash_bits < 64) sk_in = at::bitwise_and(sk_in, (int64_t)((1ull << force_hash_bits) - 1));
     idx = iota_u32(n, dev);
     end_bit = 64;

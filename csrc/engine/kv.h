@@ -84,7 +84,8 @@ struct ConvertStats {
 };
 // group-by (MR-MPI convert): KV -> KMV. Order of unique keys: sorted by key
 // (fixed <= 8B keys) or by 64-bit hash (others).
-KMV convert(const KV& kv, ConvertStats* st = nullptr, int force_hash_bits = 64);
+// prehash (optional): hash64_keys(kv) already computed by the producer
+KMV convert(const KV& kv, ConvertStats* st = nullptr, int force_hash_bits = 64, const at::Tensor& prehash = {});
 // one value per key (MR-MPI clone)
 KMV clone(const KV& kv);
 // whole KV -> one KMV pair key -> [k0,v0,k1,v1,...] (MR-MPI collapse)

@@ -755,17 +755,20 @@ uint64_t MapReduce::gather(int nprocs) {  // :893-1036
 
 // ====================================================================== group-by
 
-uint64_t MapReduce::convert() {  // :861-886
+uint64_t MapReduce::convert() { return convert_prehashed(at::Tensor()); }
+
+uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
   start();
-  OpTrace tr_(__func__, this);
-  enter(__func__, true);
+  OpTrace tr_("convert", this);
+  enter("convert", true);
   need_kv("convert");
   if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
     OocStats os;
     kmv = ooc_convert(*kv, budget(), device(), &os);  // hash-partitioned spools (src/keymultivalue.cpp:645-789)
     note_ooc("Convert", os);
   } else {
-    kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert); });
+    kmv = oom_retry(this, device(), my_proc(), "convert",
+                    [&] { return mrh::convert(*kv, &last_convert, 64, prehash); });
   }
   kv.reset();
   stats("Convert", 1);

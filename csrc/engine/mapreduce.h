@@ -100,6 +100,8 @@ class MapReduce {
   uint64_t compress(const ReduceFn& fn);
   uint64_t compress_builtin(const std::string& op, const std::string& dtype);
   uint64_t convert();
+  // convert with the keys' hash64_keys() already computed by the producer
+  uint64_t convert_prehashed(const at::Tensor& prehash);
   uint64_t gather(int nprocs);
   void open(int addflag = 0);
   KeyValue& kv_open();  // the builder other MRs' callbacks add into while open

@@ -6,15 +6,25 @@ the GPU, URLs are copied back and added to the KV one by one on the host
 (:254-410), then aggregate (:182) -> convert (:186) -> reduce writes
 "url\\tfile file ... \\n" lines with one fopen per key (:463-513).
 
-MI355X design:
+MI355X design, pipelined per part file:
   map       files stream host(pinned) -> HBM on a side HIP stream, double
             buffered; the fused scan/extract kernels (csrc/kernels/text.hip)
             emit KV(url+NUL, int32 file id) directly into HBM — no D2H, no
             per-URL host loop;
-  aggregate hashlittle partition + RCCL all-to-all over xGMI (P > 1);
-  convert   64-bit hash radix sort-by-key + segment detection (+ exact check);
-  reduce    the output text is formatted on the GPU (apps.hip) and copied to
-            the host once; optionally written to `out_dir/InvertedIndex-P-me`.
+  aggregate (P > 1) each file's URLs go through the chunked RCCL exchange as
+            soon as they are mapped, while the next file is still on the PCIe
+            link — the shuffle hides behind the input stream instead of
+            following it (the map chunk k+1 || shuffle chunk k pipeline of
+            SURVEY.md §2.10);
+  hash      each file's (received) URLs get their 64-bit grouping hash in the
+            same shadow of the H2D, so convert only sorts;
+  convert   radix sort of the precomputed hashes + segment detection (+ exact
+            byte check of every group);
+  reduce    the output text is formatted on the GPU (apps.hip) and drains to
+            pinned host memory on a D2H copy stream (the PCIe link is full
+            duplex: the drain overlaps the next job's input stream); the
+            output is complete once `output_ready()` (or any device sync).
+            Optionally written to `out_dir/InvertedIndex-P-me`.
 """
 from __future__ import annotations
 
@@ -30,21 +40,24 @@ PAD = 64
 
 
 class InvertedIndex:
-    def __init__(self, mr: MapReduce, files, out_dir=None):
+    def __init__(self, mr: MapReduce, files, out_dir=None, pipelined=True):
         """files: list of (name, uint8 tensor) for THIS rank (host tensors —
         ideally pinned — or device tensors)."""
         self.mr = mr
         self.files = files
         self.out_dir = out_dir
+        self.pipelined = pipelined
         # doc ids are global (rank-major) so a value means the same file name on
         # every rank after the shuffle; the reference ships the name string itself
         all_names = mr.comm.allgather_object([n for n, _ in files])
         self.doc_base = sum(len(x) for x in all_names[: mr.me])
+        self.max_files = max(len(x) for x in all_names)
         names = [n.encode() for lst in all_names for n in lst]
         self.names = torch.frombuffer(bytearray(b"".join(names) or b"\0"), dtype=torch.uint8).clone()
         lens = torch.tensor([0] + [len(n) for n in names], dtype=torch.int64)
         self.name_off = torch.cumsum(lens, 0)
         dev = mr.device
+        self.dev = dev
         self.is_cuda = dev.startswith("cuda")
         self.names_dev = self.names.to(dev)
         self.name_off_dev = self.name_off.to(dev)
@@ -52,83 +65,122 @@ class InvertedIndex:
         # two persistent staging buffers (double-buffered H2D); the PAD bytes
         # past each file are read by the 16-byte scan windows but never matched
         self.bufs = [pools.device_buffer(dev, maxlen + PAD, slot) for slot in range(2 if files else 0)]
-        self.copy_stream = torch.cuda.Stream() if self.is_cuda else None
+        self.copy_stream = pools.stream(dev, "h2d") if self.is_cuda else None
         self.output = None
+        self._done = None
+        self._hashes = []
+        self.exchanged = False
         self.nurls = 0
 
     # -------------------------------------------------------------- map
+    def _emit(self, kv, part):
+        """one file's KV: shuffled right away (P > 1) and hashed, in the shadow
+        of the next file's H2D"""
+        mr = self.mr
+        if self.pipelined and mr.nprocs > 1:
+            part, _ = C.aggregate(part, mr.comm.native, chunk_bytes=mr.chunk_bytes)
+        if self.pipelined:
+            self._hashes.append(C.hash64_keys(part))
+        kv.add_kv(part)
+
     def _map(self, itask, kv):
         files = self.files
-        if not files:
-            return
+        empty = lambda: C.map_urls(torch.zeros(PAD, dtype=torch.uint8, device=self.dev), 0, 0)
         if not self.is_cuda:
             for fid, (_, t) in enumerate(files):
                 buf = self.bufs[0]
                 buf[: t.numel()].copy_(t)
                 buf[t.numel():t.numel() + PAD].zero_()
-                kv.add_kv(C.map_urls(buf, t.numel(), self.doc_base + fid))
-            return
-        main = torch.cuda.current_stream()
-        cs = self.copy_stream
-        ready = [torch.cuda.Event(), torch.cuda.Event()]
-        free = [torch.cuda.Event(), torch.cuda.Event()]
+                self._emit(kv, C.map_urls(buf, t.numel(), self.doc_base + fid))
+        else:
+            main = torch.cuda.current_stream()
+            cs = self.copy_stream
+            ready = [torch.cuda.Event(), torch.cuda.Event()]
 
-        def issue(i):
-            b = i & 1
-            t = files[i][1]
-            with torch.cuda.stream(cs):
-                if i >= 2:
-                    cs.wait_event(free[b])
-                self.bufs[b][: t.numel()].copy_(t, non_blocking=True)
-                ready[b].record(cs)
+            def issue(i):
+                b = i & 1
+                t = files[i][1]
+                with torch.cuda.stream(cs):
+                    prev = pools.last_use(self.dev, b)  # the last kernel (any job) that read this buffer
+                    if prev is not None:
+                        cs.wait_event(prev)
+                    self.bufs[b][: t.numel()].copy_(t, non_blocking=True)
+                    ready[b].record(cs)
 
-        issue(0)
-        for i in range(len(files)):
-            if i + 1 < len(files):
-                issue(i + 1)
-            b = i & 1
-            main.wait_event(ready[b])
-            n = files[i][1].numel()
-            kv.add_kv(C.map_urls(self.bufs[b], n, self.doc_base + i))
-            free[b].record(main)
+            if files:
+                issue(0)
+            for i in range(len(files)):
+                if i + 1 < len(files):
+                    issue(i + 1)
+                b = i & 1
+                main.wait_event(ready[b])
+                n = files[i][1].numel()
+                part = C.map_urls(self.bufs[b], n, self.doc_base + i)
+                pools.mark_use(self.dev, b, main)
+                self._emit(kv, part)
+        # lock-step exchanges: ranks with fewer files join with empty parts
+        if self.pipelined and self.mr.nprocs > 1:
+            for _ in range(len(files), self.max_files):
+                self._emit(kv, empty())
+            self.exchanged = True
 
     # -------------------------------------------------------------- reduce
     def _reduce(self, kmv, kv):
         text = C.inverted_index_format(kmv, self.names_dev, self.name_off_dev)
         if self.is_cuda:
-            host = pools.pinned_buffer(text.numel())
-            host.copy_(text, non_blocking=True)
-            torch.cuda.current_stream().synchronize()
+            host = pools.pinned_buffer(text.numel(), slot=100 + pools.next_slot("ii_out"))
+            d2h = pools.stream(self.dev, "d2h")
+            d2h.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(d2h):
+                host.copy_(text, non_blocking=True)
+            text.record_stream(d2h)
+            self._done = torch.cuda.Event()
+            self._done.record(d2h)
         else:
             host = text
         self.output = host
         if self.out_dir is not None:
+            self.output_ready()
             os.makedirs(self.out_dir, exist_ok=True)
             path = os.path.join(self.out_dir, f"InvertedIndex-{self.mr.nprocs}-{self.mr.me}")
             with open(path, "wb") as f:
                 f.write(host.numpy().tobytes())
             MapReduce.count_io(write=host.numel())
 
+    def output_ready(self):
+        """block until the output text has drained to host memory"""
+        if self._done is not None:
+            self._done.synchronize()
+
     def run(self, phases=None):
         """phases: optional dict; if given, per-stage seconds (device-synced)
         are recorded under the reference's stage names (Map, Network I/O,
-        Sort/Hash, Reduce — chapter_final.pdf Fig. 4/5)."""
+        Sort/Hash, Reduce — chapter_final.pdf Fig. 4/5). With the pipelined
+        map the per-file shuffle runs inside Map (Network I/O = 0)."""
         mr = self.mr
         tick = _Ticker(phases, mr.comm)
         # one map task per rank, each maps its own files (reference :175, :278-284)
         self.nurls = mr.map(mr.nprocs, self._map)
         tick("Map")
-        mr.aggregate()
+        if not self.exchanged:
+            mr.aggregate()
         tick("Network I/O")
-        self.nunique = mr.convert()
+        if self.pipelined and self._hashes:
+            self.nunique = mr.convert_prehashed(torch.cat(self._hashes))
+        else:
+            self.nunique = mr.convert()
+        self._hashes = []
         tick("Sort/Hash")
         mr.reduce_batch(self._reduce)
+        if phases is not None:
+            self.output_ready()
         tick("Reduce")
         return self.nurls
 
     def output_lines(self):
         if self.output is None:
             return []
+        self.output_ready()
         return bytes(self.output.cpu().numpy()).decode("utf-8", "replace").splitlines()
 
 

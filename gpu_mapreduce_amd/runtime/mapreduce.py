@@ -214,6 +214,10 @@ class MapReduce(metaclass=_Counters):
     def convert(self):
         return self._m.convert()
 
+    def convert_prehashed(self, hashes):
+        """convert with hash64_keys(kv) already computed by the producer (int64 [n])"""
+        return self._m.convert_prehashed(hashes)
+
     def collate(self, hash=None):
         return self._m.collate(hash)
 

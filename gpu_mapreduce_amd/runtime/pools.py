@@ -10,6 +10,9 @@ import torch
 
 _dev = {}
 _host = {}
+_streams = {}
+_events = {}
+_ring = {}
 
 
 def device_buffer(device: str, nbytes: int, slot: int = 0) -> torch.Tensor:
@@ -29,6 +32,38 @@ def pinned_buffer(nbytes: int, slot: int = 0) -> torch.Tensor:
     return b[:nbytes]
 
 
+def stream(device: str, name: str):
+    """A persistent side stream (H2D staging, D2H output drain) per device."""
+    key = (str(device), name)
+    st = _streams.get(key)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _streams[key] = st
+    return st
+
+
+def last_use(device: str, slot: int):
+    """Event recorded after the last kernel that read staging buffer `slot`
+    (None before first use): a later job's H2D into the slot waits on it."""
+    return _events.get((str(device), slot))
+
+
+def mark_use(device: str, slot: int, stream) -> None:
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    _events[(str(device), slot)] = ev
+
+
+def next_slot(name: str, n: int = 2) -> int:
+    """Round-robin slot index for double-buffered outputs (job k uses slot k % n)."""
+    i = _ring.get(name, 0)
+    _ring[name] = i + 1
+    return i % n
+
+
 def clear():
     _dev.clear()
     _host.clear()
+    _streams.clear()
+    _events.clear()
+    _ring.clear()
