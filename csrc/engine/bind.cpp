@@ -142,6 +142,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<>())
       .def_readonly("passes", &ConvertStats::passes)
       .def_readonly("collisions", &ConvertStats::collisions)
+      .def_readonly("grouped", &ConvertStats::grouped)
       .def_readonly("exact", &ConvertStats::exact);
   py::class_<ShuffleStats>(m, "ShuffleStats")
       .def(py::init<>())
@@ -176,7 +177,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              if (kb.size() != vb.size()) throw std::runtime_error("add_multi: length lists differ");
              kv.add((int64_t)kb.size(), ks.data(), kb.data(), vs.data(), vb.data());
            })
-      .def("add_kv", &KeyValue::add_kv)
+      .def("add_kv", &KeyValue::add_kv, py::call_guard<py::gil_scoped_release>())
+      .def("enable_grouping", &KeyValue::enable_grouping)
+      .def_property_readonly("grouping", &KeyValue::grouping)
       .def("size", &KeyValue::size)
       .def("finish", &KeyValue::finish)
       .def_property_readonly("device", [](const KeyValue& kv) { return kv.device().str(); });

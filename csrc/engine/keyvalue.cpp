@@ -18,12 +18,32 @@ void KeyValue::flush() {
     kv.koff = at::from_blob(koff_.data(), {(int64_t)koff_.size()}, at::TensorOptions().dtype(at::kLong)).clone();
   if (kv.vw < 0)
     kv.voff = at::from_blob(voff_.data(), {(int64_t)voff_.size()}, at::TensorOptions().dtype(at::kLong)).clone();
-  chunks_.push_back(kv_to(kv, dev_));
+  push(kv_to(kv, dev_));
   reset_host();
+}
+
+void KeyValue::push(const KV& c) {
+  if (grp_) {
+    if (grp_->accepts(c)) {
+      grp_->add(c);
+      return;
+    }
+    // a chunk of another layout: grouping stops, what it holds becomes a chunk
+    if (grp_->size()) chunks_.push_back(grp_->kv());
+    grp_.reset();
+  }
+  chunks_.push_back(c);
 }
 
 KV KeyValue::finish() {
   flush();
+  done_.reset();
+  if (grp_) {
+    KV out = grp_->size() ? grp_->kv() : empty_kv(dev_, 0, 0);
+    if (grp_->size()) done_ = std::move(grp_);
+    grp_.reset();
+    return out;
+  }
   KV out = concat(chunks_, dev_);
   chunks_.clear();
   return out;

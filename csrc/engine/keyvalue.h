@@ -7,10 +7,17 @@
 // produced by kernels or ATen ops inside batch callbacks) are kept as chunks in
 // emission order, so a callback can mix both without a host round trip for
 // device data. finish() uploads the host part once and concatenates.
+//
+// enable_grouping() (before the first add): every chunk is instead appended
+// to a GroupIndex (grouper.h), which groups it by key as it arrives, so a
+// convert() right after the map finds the group-by already done; finish()
+// then returns the index's arenas (no concat) and take_group() the index.
 #pragma once
+#include <memory>
 #include <string>
 #include <vector>
 
+#include "grouper.h"
 #include "kv.h"
 
 namespace mrh {
@@ -43,10 +50,16 @@ class KeyValue {
   }
   void add_kv(const KV& kv) {
     flush();
-    if (kv.n) chunks_.push_back(kv);
+    if (kv.n) push(kv);
   }
+  void enable_grouping() {
+    if (!grp_ && chunks_.empty() && nh_ == 0) grp_ = std::make_shared<GroupIndex>(dev_);
+  }
+  bool grouping() const { return grp_ != nullptr; }
+  // the index of the KV the last finish() returned (null if not grouped)
+  std::shared_ptr<GroupIndex> take_group() { return std::move(done_); }
   int64_t size() const {
-    int64_t n = nh_;
+    int64_t n = nh_ + (grp_ ? grp_->size() : 0);
     for (auto& c : chunks_) n += c.n;
     return n;
   }
@@ -69,6 +82,7 @@ class KeyValue {
     kw_ = vw_ = -2;
   }
   void flush();
+  void push(const KV& chunk);
 
   at::Device dev_;
   std::string kd_, vd_;
@@ -76,6 +90,7 @@ class KeyValue {
   int64_t nh_ = 0;
   int kw_ = -2, vw_ = -2;
   std::vector<KV> chunks_;
+  std::shared_ptr<GroupIndex> grp_, done_;
 };
 
 }  // namespace mrh

@@ -81,6 +81,9 @@ struct ConvertStats {
   int64_t passes = 0;
   int64_t collisions = 0;
   bool exact = true;  // grouped on exact key bits (no hashing)
+  // incremental group-by (grouper.h): 0 not used, 1 used, 2 a hash collision
+  // sent it to the ordinary convert
+  int grouped = 0;
 };
 // group-by (MR-MPI convert): KV -> KMV. Order of unique keys: sorted by key
 // (fixed <= 8B keys) or by 64-bit hash (others).

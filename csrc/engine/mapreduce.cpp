@@ -313,6 +313,8 @@ void MapReduce::enter(const char* op, bool ooc_ok) {
     }
   }
   ensure_resident();
+  // a group-by index outlives its KV only until the next op sees the KV changed
+  if (grouped_ && (!kv || !grouped_->describes(*kv))) grouped_.reset();
   const bool on_host = (kv && !kv->device().is_cuda()) || (kmv && !kmv->keys.device().is_cuda());
   if (!device().is_cuda() || !on_host) return;
   // an op with an out-of-core path leaves host-resident data larger than the
@@ -455,11 +457,17 @@ KeyValue& MapReduce::kv_open() {
 uint64_t MapReduce::close() {  // :658-672
   if (!open_) fail("Cannot close MapReduce that is not open");
   KV n = open_->finish();
+  std::shared_ptr<GroupIndex> g = open_->take_group();
   open_.reset();
   if (open_add_) ensure_resident();  // appending to data that was spilled to disk
   else drop_disk();                  // replacing it: the spilled copy must never be read back over n
-  if (open_add_ && kv) kv = concat({*kv, n}, device());
-  else kv = n;
+  if (open_add_ && kv) {
+    kv = concat({*kv, n}, device());
+    grouped_.reset();
+  } else {
+    kv = n;
+    grouped_ = g;
+  }
   stats("Close", 0);
   return count(kv->n);
 }
@@ -488,8 +496,14 @@ std::vector<int> MapReduce::my_tasks(int nmap) {  // :1102-1225
 
 uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) {
   KV n = kvb.finish();
-  if (addflag && kv) kv = concat({*kv, n}, device());
-  else kv = n;
+  std::shared_ptr<GroupIndex> g = kvb.take_group();
+  if (addflag && kv) {
+    kv = concat({*kv, n}, device());
+    grouped_.reset();
+  } else {
+    kv = n;
+    grouped_ = g;
+  }
   kmv.reset();
   stats(heading, 0);
   return count(kv->n);
@@ -762,14 +776,27 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
   OpTrace tr_("convert", this);
   enter("convert", true);
   need_kv("convert");
+  last_convert = ConvertStats();
   if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
     OocStats os;
     kmv = ooc_convert(*kv, budget(), device(), &os);  // hash-partitioned spools (src/keymultivalue.cpp:645-789)
     note_ooc("Convert", os);
+  } else if (grouped_ && grouped_->describes(*kv) && !prehash.defined()) {
+    // grouped while the map produced it: only the two short sorts are left
+    KMV m;
+    if (grouped_->finish(&m, &last_convert)) {
+      kmv = std::move(m);
+      last_convert.grouped = 1;
+    } else {
+      last_convert = ConvertStats();
+      kmv = mrh::convert(*kv, &last_convert, 64);  // a 64-bit hash collision: exact regroup
+      last_convert.grouped = 2;
+    }
   } else {
     kmv = oom_retry(this, device(), my_proc(), "convert",
                     [&] { return mrh::convert(*kv, &last_convert, 64, prehash); });
   }
+  grouped_.reset();
   kv.reset();
   stats("Convert", 1);
   return count(kmv->nkey);

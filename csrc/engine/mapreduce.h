@@ -213,6 +213,9 @@ class MapReduce {
   CommPtr comm_;
   std::string disk_path_;
   int disk_counter_ = 0;
+  // group-by index of the KV built by the last map / close with grouping
+  // enabled (keyvalue.h); convert() uses it while it still describes kv
+  std::shared_ptr<GroupIndex> grouped_;
   std::unique_ptr<KeyValue> open_;
   int open_add_ = 0;
   double t0_ = 0;

@@ -222,6 +222,30 @@ void ii_write(const uint8_t* kd, const int64_t* koff, const int32_t* vals, int64
 }  // namespace k
 }  // namespace mrh
 
+// ---------------------------------------------------------------- group.hip
+// incremental exact group-by (GroupIndex, csrc/engine/grouper.h). Table of
+// `cap` (power of two) u64 hash slots + i32 group ids; ctr = [ngroups, collisions].
+namespace mrh {
+namespace k {
+// code[i] = CLAIM|g (pair i created group g: rep[g] = row0+i, ghash[g] = hash) or its slot
+void grp_insert(const uint64_t* h, int64_t n, int64_t row0, uint64_t* slots, int32_t* sgid, int64_t cap,
+                uint64_t* ctr, int64_t* rep, uint64_t* ghash, uint32_t* code, hipStream_t s);
+// gid[row0+i] from code; key bytes of every non-claiming row checked against rep (ctr[1] += mismatches)
+void grp_resolve(const uint32_t* code, int64_t n, int64_t row0, const int32_t* sgid, const int64_t* rep,
+                 const uint8_t* kd, const int64_t* koff, int kw, int32_t* gid, uint64_t* ctr, hipStream_t s);
+void grp_rehash(const uint64_t* old_slots, const int32_t* old_gid, int64_t old_cap, uint64_t* new_slots,
+                int32_t* new_gid, int64_t new_cap, hipStream_t s);
+// aoff[i] = poff[i] + base for i in [0, n]
+void grp_append_off(const int64_t* poff, int64_t n, int64_t base, int64_t* aoff, hipStream_t s);
+// rank[order[j]] = j, heads[j] = rep[order[j]]
+void grp_rank(const uint32_t* order, int64_t m, const int64_t* rep, uint32_t* rank, uint32_t* heads, hipStream_t s);
+// key[i] = rank[gid[i]]
+void grp_pairkey(const int32_t* gid, int64_t n, const uint32_t* rank, uint64_t* key, hipStream_t s);
+// CSR segments of dense sorted ranks 0..m-1
+void grp_seg(const uint64_t* sorted_rank, int64_t n, int64_t m, int64_t* seg, hipStream_t s);
+}  // namespace k
+}  // namespace mrh
+
 // ---------------------------------------------------------------- wordcount.hip
 // In-mapper combining word count (see wordcount.hip). slots/counts: table of
 // `cap` (power of two) entries; ctr[0] used slots, ctr[1] arena bytes;

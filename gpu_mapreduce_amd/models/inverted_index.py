@@ -16,10 +16,13 @@ MI355X design, pipelined per part file:
             link — the shuffle hides behind the input stream instead of
             following it (the map chunk k+1 || shuffle chunk k pipeline of
             SURVEY.md §2.10);
-  hash      each file's (received) URLs get their 64-bit grouping hash in the
-            same shadow of the H2D, so convert only sorts;
-  convert   radix sort of the precomputed hashes + segment detection (+ exact
-            byte check of every group);
+  group     each file's (received) URLs are grouped by key in the same shadow
+            of the H2D: the map's KeyValue has grouping enabled, so every
+            part is appended to device arenas (no final concat), hashed, and
+            inserted into an exact HBM hash table (byte check per pair)
+            (csrc/engine/grouper.h, csrc/kernels/group.hip);
+  convert   finds the group-by done: it only orders the ~600 K groups by hash
+            and the pairs by group (two short radix sorts);
   reduce    the output text is formatted on the GPU (apps.hip) and drains to
             pinned host memory on a D2H copy stream (the PCIe link is full
             duplex: the drain overlaps the next job's input stream); the
@@ -68,23 +71,22 @@ class InvertedIndex:
         self.copy_stream = pools.stream(dev, "h2d") if self.is_cuda else None
         self.output = None
         self._done = None
-        self._hashes = []
         self.exchanged = False
         self.nurls = 0
 
     # -------------------------------------------------------------- map
     def _emit(self, kv, part):
-        """one file's KV: shuffled right away (P > 1) and hashed, in the shadow
-        of the next file's H2D"""
+        """one file's KV: shuffled right away (P > 1) and grouped (the
+        KeyValue's GroupIndex), in the shadow of the next file's H2D"""
         mr = self.mr
         if self.pipelined and mr.nprocs > 1:
             part, _ = C.aggregate(part, mr.comm.native, chunk_bytes=mr.chunk_bytes)
-        if self.pipelined:
-            self._hashes.append(C.hash64_keys(part))
         kv.add_kv(part)
 
     def _map(self, itask, kv):
         files = self.files
+        if self.pipelined:
+            kv.enable_grouping()
         empty = lambda: C.map_urls(torch.zeros(PAD, dtype=torch.uint8, device=self.dev), 0, 0)
         if not self.is_cuda:
             for fid, (_, t) in enumerate(files):
@@ -165,11 +167,7 @@ class InvertedIndex:
         if not self.exchanged:
             mr.aggregate()
         tick("Network I/O")
-        if self.pipelined and self._hashes:
-            self.nunique = mr.convert_prehashed(torch.cat(self._hashes))
-        else:
-            self.nunique = mr.convert()
-        self._hashes = []
+        self.nunique = mr.convert()
         tick("Sort/Hash")
         mr.reduce_batch(self._reduce)
         if phases is not None:

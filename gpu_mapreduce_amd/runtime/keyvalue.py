@@ -91,6 +91,17 @@ class KeyValue:
         """Append a native KV batch (e.g. from a kernel) without host copies."""
         self._h.add_kv(kv)
 
+    def enable_grouping(self):
+        """Group pairs by key as they are added (call before the first add):
+        a convert() right after this map then finds the group-by done
+        (csrc/engine/grouper.h). Worth it when the map streams its input and
+        the device would otherwise idle between batches."""
+        self._h.enable_grouping()
+
+    @property
+    def grouping(self) -> bool:
+        return self._h.grouping
+
     def add_tensors(self, keys: torch.Tensor, values: torch.Tensor | None = None,
                     koff: torch.Tensor | None = None, voff: torch.Tensor | None = None):
         """Append n pairs from tensors. Fixed width: `keys` is [n, ...] and each
