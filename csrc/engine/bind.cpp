@@ -7,6 +7,7 @@
 // callbacks receive the device KV/KMV. The engine itself lives in
 // libmrhip.so, shared with the C API (csrc/capi).
 #include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 
 #include <cstring>
@@ -14,6 +15,8 @@
 
 #include "kv.h"
 #include "graphplan.h"
+#include "guardalloc.h"
+#include "kernels/launch.h"
 #include "mapreduce.h"
 #include "tri.h"
 #include "wordcount.h"
@@ -430,7 +433,36 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("to_var_keys", &to_var_keys);
   m.def("to_var_values", &to_var_values);
   m.def("exclusive_scan", &exclusive_scan);
-  m.def("radix_sort_pairs", &radix_sort_pairs);
+  // MRH_GUARD device bounds-check mode (guardalloc.h)
+  m.def("install_alloc_guard", &guard::install_alloc_guard);
+  m.def("alloc_guard_active", &guard::alloc_guard_active);
+  m.def("guard_check", [](const std::string& op) { return guard::check_all_blocks(op.c_str()); },
+        py::call_guard<py::gil_scoped_release>());
+  m.def("guard_blocks_live", &guard::guarded_blocks_live);
+  m.def("guard_reports", [] {
+    py::list out;
+    for (const auto& r : guard::guard_reports()) {
+      py::dict d;
+      d["ptr"] = r.ptr;
+      d["size"] = r.size;
+      d["front_bad"] = r.front_bad;
+      d["back_bad"] = r.back_bad;
+      d["alloc_op"] = r.alloc_op;
+      d["found_op"] = r.found_op;
+      out.append(d);
+    }
+    return out;
+  });
+  // test hook: a deliberate overrun of `past` bytes past the end of a guarded
+  // int32 device tensor (lands in its back canary; refused without the guard)
+  m.def("_guard_selftest_overrun", [](at::Tensor t, int64_t past) {
+    if (!guard::alloc_guard_active()) throw std::runtime_error("_guard_selftest_overrun needs MRH_GUARD=1");
+    if (!t.is_cuda() || t.scalar_type() != at::kInt || !t.is_contiguous() || past < 4 || past > 4096 || past % 4)
+      throw std::runtime_error("_guard_selftest_overrun: contiguous int32 HIP tensor, past in [4, 4096], multiple of 4");
+    k::fill_i32(t.data_ptr<int32_t>(), t.numel() + past / 4, 7, at::hip::getCurrentHIPStream());
+  });
+  m.def("radix_sort_pairs", &radix_sort_pairs, py::arg("keys"), py::arg("vals"), py::arg("begin_bit"),
+        py::arg("end_bit"), py::arg("skip_trivial") = true);
   m.def("hash32_keys", &hash32_keys);
   m.def("hash64_keys", &hash64_keys);
   m.def("gather", &mrh::gather);

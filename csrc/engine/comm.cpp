@@ -1,5 +1,6 @@
 // Native communicator (see comm.h).
 #include "comm.h"
+#include "guardalloc.h"
 
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -86,11 +87,13 @@ void copy_bytes(void* dst, const void* src, int64_t n, at::Device dev) {
 }  // namespace
 
 Comm::Comm(at::Device dev) : dev_(dev) {
+  if (dev_.is_cuda()) guard::install_alloc_guard();  // MRH_GUARD: before the job's first HBM allocation
   if (dev_.is_cuda() && force_rccl()) init_transport("", "self");
 }
 
 Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const std::string& transport)
     : dev_(dev), pg_(std::move(pg)), store_(std::move(store)) {
+  if (dev_.is_cuda()) guard::install_alloc_guard();
   if (pg_) {
     rank_ = pg_->getRank();
     size_ = pg_->getSize();

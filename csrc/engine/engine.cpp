@@ -236,7 +236,7 @@ static at::Tensor scan_u32(const at::Tensor& x) {
 }
 
 std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& keys_in, const at::Tensor& vals_in,
-                                                              int begin_bit, int end_bit) {
+                                                              int begin_bit, int end_bit, bool skip_trivial) {
   at::Tensor keys = keys_in.contiguous();
   at::Tensor vals = vals_in.contiguous();
   const int64_t n = keys.numel();
@@ -252,7 +252,7 @@ std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& k
     at::Tensor tmp = scratch(k::radix_temp_bytes(n), dev);
     k::radix_sort_u64_u32(P0<uint64_t>(keys), P0<uint32_t>(vals), P0<uint64_t>(ko), P0<uint32_t>(vo),
                           P0<uint64_t>(ka), P0<uint32_t>(va), n, begin_bit, end_bit, P0<void>(tmp), cur_stream(),
-                          &passes);
+                          &passes, skip_trivial);
     return {ko, vo, passes};
   }
   const uint64_t* k = P0<uint64_t>(keys);

@@ -217,7 +217,7 @@ bool GroupIndex::finish(KMV* out, ConvertStats* st) {
     return t;
   };
   // 1. groups in 64-bit hash order (convert's key order)
-  auto [gsorted, order, p1] = radix_sort_pairs(ghash_.narrow(0, 0, m), iota(m), 0, 64);
+  auto [gsorted, order, p1] = radix_sort_pairs(ghash_.narrow(0, 0, m), iota(m), 0, 64, false);
   at::Tensor rank = at::empty({m}, opt(dev_, at::kInt)), heads = at::empty({m}, opt(dev_, at::kInt));
   at::Tensor key = at::empty({n}, opt(dev_, at::kLong));
   if (cuda) {
@@ -239,7 +239,7 @@ bool GroupIndex::finish(KMV* out, ConvertStats* st) {
   // 2. pairs by group rank: stable, so values keep their append order
   int bits = 1;
   while (bits < 63 && (int64_t(1) << bits) < m) ++bits;
-  auto [sk, perm, p2] = radix_sort_pairs(key, iota(n), 0, bits);
+  auto [sk, perm, p2] = radix_sort_pairs(key, iota(n), 0, bits, false);
   at::Tensor seg = at::empty({m + 1}, opt(dev_, at::kLong));
   if (cuda) {
     k::grp_seg(P0<uint64_t>(sk), n, m, P0<int64_t>(seg), cur());

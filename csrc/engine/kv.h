@@ -65,10 +65,12 @@ at::Tensor fixed_offsets(int64_t n, int w, at::Device dev);
 // ------------------------------------------------------------------ primitives
 // exclusive scan returning n+1 entries (int64 result for int32/int64 input, uint32 for uint32)
 at::Tensor exclusive_scan(const at::Tensor& x);
-// stable sort of (u64 key, u32 val); returns (keys_sorted, vals_sorted, passes)
+// stable sort of (u64 key, u32 val); returns (keys_sorted, vals_sorted, passes).
+// skip_trivial: skip digit passes that are constant over all keys (costs one
+// host sync); pass false when every digit in [begin_bit, end_bit) varies
 std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& keys,
                                                               const at::Tensor& vals, int begin_bit,
-                                                              int end_bit);
+                                                              int end_bit, bool skip_trivial = true);
 at::Tensor hash32_keys(const KV& kv, uint32_t seed);   // lookup3 hashlittle
 at::Tensor hash64_keys(const KV& kv);                  // lookup3 hashlittle2
 // rows gathered by u32 permutation

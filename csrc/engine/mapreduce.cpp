@@ -2,6 +2,7 @@
 // method as src/mapreduce.cpp:<lines>.
 #include "mapreduce.h"
 #include "guard.h"
+#include "guardalloc.h"
 #include "ooc.h"
 
 #include <c10/hip/HIPCachingAllocator.h>
@@ -54,6 +55,7 @@ void device_sync(const MapReduce* mr) {
 struct OpTrace {
   OpTrace(const char* name, MapReduce* mr) : mr_(mr), name_(name) {
     roctxRangePushA(name);
+    if (g_op_depth == 0) guard::set_current_op(name);
     if (guard::trace_enabled()) {
       device_sync(mr);
       t0_ = Comm::wtime();
@@ -87,6 +89,11 @@ struct OpTrace {
     if (mr_->set.freepage && mr_->budget() > 0 && g_op_depth == 0 && mr_->device().is_cuda() &&
         std::uncaught_exceptions() == 0)
       c10::hip::HIPCachingAllocator::emptyCache();
+    // MRH_GUARD: every live block's canaries at the end of each top-level op
+    if (g_op_depth == 0 && guard::alloc_guard_active()) {
+      guard::check_all_blocks(name_);
+      guard::set_current_op(nullptr);
+    }
     if (mr_->set.outofcore == 1 && std::uncaught_exceptions() == 0) {
       try {
         mr_->spill_disk();
@@ -303,6 +310,16 @@ MapReduce::~MapReduce() {
 // or spill-on-OOM) comes back to HBM before the op touches it
 void MapReduce::enter(const char* op, bool ooc_ok) {
   guard::fault_point(op, comm_->rank());
+  if (guard::alloc_guard_active()) {  // an overrun found at the end of an earlier op fails the next one
+    static size_t raised = 0;
+    const auto reps = guard::guard_reports();
+    if (reps.size() > raised) {
+      const guard::GuardReport& r = reps[raised];
+      raised = reps.size();
+      throw std::runtime_error("mrhip guard: out-of-bounds device write into a " + std::to_string(r.size) +
+                               "-byte block allocated in " + r.alloc_op + ", detected " + r.found_op);
+    }
+  }
   if (!started_) {
     started_ = true;
     // minpage (reference allocate(), src/mapreduce.cpp:3318-3357): pages

@@ -44,7 +44,10 @@ __global__ __launch_bounds__(NT) void k_grp_insert(const uint64_t* __restrict__ 
     const unsigned long long hv = nz(h[i]);
     uint64_t s = home(hv, mask);
     for (;;) {
-      unsigned long long v = __hip_atomic_load(&slots[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // plain load: a slot only ever goes 0 -> hash once, so a stale 0 just
+      // costs the CAS below (which returns the live value) and a non-zero
+      // value is final; hot keys then hit in the CU's L1 instead of L2
+      unsigned long long v = slots[s];
       if (v == 0) {
         v = atomicCAS(&slots[s], 0ull, hv);
         if (v == 0) {

@@ -27,14 +27,16 @@ void lengths_to_offsets(const int32_t* len, int64_t* off, int64_t n, void* temp,
 
 // ---------------------------------------------------------------- radix.hip
 // Stable LSD radix sort of (uint64 key, uint32 value) pairs over digits
-// [begin_bit, end_bit). Passes whose digit is constant over all keys are
-// skipped using a single up-front global histogram. Result ends in keys_out/vals_out.
+// [begin_bit, end_bit), one one-sweep (decoupled look-back) kernel per 8-bit
+// pass. skip_trivial: passes whose digit is constant over all keys are
+// skipped using the up-front global histogram (one host sync); false = no
+// host sync at all. Result ends in keys_out/vals_out.
 // temp must hold radix_temp_bytes(n) bytes. All buffers have n entries.
 size_t radix_temp_bytes(int64_t n);
 void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64_t* keys_out,
                         uint32_t* vals_out, uint64_t* keys_alt, uint32_t* vals_alt, int64_t n,
                         int begin_bit, int end_bit, void* temp, hipStream_t s,
-                        int* passes_run = nullptr);
+                        int* passes_run = nullptr, bool skip_trivial = true);
 
 // ---------------------------------------------------------------- hash.hip
 // lookup3 hashlittle(key, len, seed) (bit-exact with Bob Jenkins' reference) per key.

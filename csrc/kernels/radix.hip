@@ -1,20 +1,37 @@
-// Stable LSD radix sort of (uint64 key, uint32 value) pairs for CDNA4.
+// Stable LSD radix sort of (uint64 key, uint32 value) pairs for CDNA4:
+// one-sweep passes with decoupled look-back (Adinets & Merrill, "Onesweep",
+// 2022), re-built for 64-lane wavefronts.
 //
 // Replaces MR-MPI's qsort()+2-way spool merge (reference src/mapreduce.cpp:2462-2633)
 // and the hash-table group-by of KeyMultiValue::convert (src/keymultivalue.cpp:645-789).
 //
-// Per 8-bit digit pass:
-//   upsweep   : per-block digit histogram in LDS -> hist[digit][block]
-//   scan      : device exclusive scan over the digit-major histogram
-//   downsweep : wave64 multi-split ranking (8 x __ballot match + popcount, one
-//               LDS counter row per wave), block-local reorder through LDS,
-//               then coalesced-by-digit-run scatter to global memory.
-// A single global histogram of all 8 digit positions (one read of the keys)
-// lets the host skip passes whose digit is constant (e.g. the zero high bits of
-// vertex ids), so a 2^26-vertex key costs 4 passes, not 8.
+//   k_global_hist : one read of the keys -> the digit histograms of all eight
+//                   8-bit digit positions (LDS atomics, one global atomic per bin)
+//   k_digit_base  : per digit position, the exclusive scan of its 256 counts =
+//                   the global start of every digit (no host round trip)
+//   k_onesweep    : one kernel per pass. A workgroup takes the next 4096-pair
+//                   tile from an atomic ticket (so every earlier tile is already
+//                   resident: the look-back below always makes progress), ranks
+//                   its pairs with the wave64 multi-split (8 ballots + popcount
+//                   per pair, one LDS counter row per wave), publishes its
+//                   per-digit counts, looks back over earlier tiles for its
+//                   exclusive prefix (stopping at the first tile that already
+//                   published an inclusive one), publishes that, reorders the
+//                   tile through LDS and scatters coalesced runs per digit.
+// Keys are read once per pass (the upsweep/scan/downsweep design read them
+// twice and needed three launches per pass).
+//
+// Look-back words (u64, one per tile and digit): bits 0-47 count, 48-55 the
+// pass epoch (1..8), 56-57 state (1 tile aggregate, 2 inclusive prefix). The
+// epoch lets all passes of one sort share one status array, zeroed once.
+//
+// Passes whose digit is constant over all keys can be skipped (skip_trivial):
+// that needs the histogram on the host (one sync); callers that know every
+// digit varies (hashes, dense ranks) sort without any host synchronisation.
 #include "common.h"
 #include "launch.h"
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -25,10 +42,14 @@ namespace {
 constexpr int RX_NT = 256;
 constexpr int RX_NW = RX_NT / MRH_WAVE;
 constexpr int RX_IT = 8;
-constexpr int RX_TILE = RX_NT * RX_IT;   // 2048 pairs per block
+constexpr int RX_TILE = RX_NT * RX_IT;   // smallest tile (2048 pairs): sizes the look-back array
 constexpr int RX_BINS = 256;
+constexpr uint64_t LB_COUNT = (1ull << 48) - 1;
+constexpr uint64_t LB_AGG = 1ull << 56, LB_PRE = 2ull << 56;
 
-__global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restrict__ keys, int64_t n,
+// digit positions [p0, p1) only: positions outside the sorted bit range are
+// constant-heavy (zero high bytes) and would serialise on one LDS bin
+__global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restrict__ keys, int64_t n, int p0, int p1,
                                                       uint32_t* __restrict__ counts /*[8][256]*/) {
   __shared__ uint32_t h[8][RX_BINS];
   for (int i = threadIdx.x; i < 8 * RX_BINS; i += RX_NT) (&h[0][0])[i] = 0;
@@ -36,7 +57,8 @@ __global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restric
   for (int64_t i = (int64_t)blockIdx.x * RX_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * RX_NT) {
     uint64_t k = keys[i];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(k >> (8 * p)) & 255], 1u);
+    for (int p = 0; p < 8; ++p)
+      if (p >= p0 && p < p1) atomicAdd(&h[p][(k >> (8 * p)) & 255], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 8 * RX_BINS; i += RX_NT) {
@@ -45,40 +67,40 @@ __global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restric
   }
 }
 
-__global__ __launch_bounds__(RX_NT) void k_upsweep(const uint64_t* __restrict__ keys, int64_t n, int shift,
-                                                  uint32_t* __restrict__ hist, int nb) {
-  __shared__ uint32_t cnt[RX_BINS];
-  cnt[threadIdx.x] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * RX_TILE;
-#pragma unroll
-  for (int i = 0; i < RX_IT; ++i) {
-    int64_t j = base + (int64_t)i * RX_NT + threadIdx.x;
-    if (j < n) atomicAdd(&cnt[(keys[j] >> shift) & 255], 1u);
-  }
-  __syncthreads();
-  hist[(int64_t)threadIdx.x * nb + blockIdx.x] = cnt[threadIdx.x];
+// block p: base[p][d] = sum of counts[p][0..d)
+__global__ __launch_bounds__(RX_BINS) void k_digit_base(const uint32_t* __restrict__ counts,
+                                                       uint64_t* __restrict__ base) {
+  __shared__ uint64_t sh[RX_BINS / MRH_WAVE + 1];
+  const int p = blockIdx.x, t = threadIdx.x;
+  uint64_t total;
+  const uint64_t ex = dev::block_excl_scan<uint64_t, RX_BINS>((uint64_t)counts[p * RX_BINS + t], sh, &total);
+  base[p * RX_BINS + t] = ex;
 }
 
-__global__ __launch_bounds__(RX_NT) void k_downsweep(const uint64_t* __restrict__ kin,
-                                                    const uint32_t* __restrict__ vin,
-                                                    uint64_t* __restrict__ kout,
-                                                    uint32_t* __restrict__ vout, int64_t n, int shift,
-                                                    const uint32_t* __restrict__ hist_scan, int nb) {
+template <int RX_IT>
+__global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                   uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                   int64_t n, int shift, const uint64_t* __restrict__ dbase,
+                                                   unsigned long long* __restrict__ status, uint64_t epoch,
+                                                   unsigned int* __restrict__ ticket) {
+  constexpr int RX_TILE = RX_NT * RX_IT;
   __shared__ uint64_t skeys[RX_TILE];
   __shared__ uint32_t svals[RX_TILE];
   __shared__ uint32_t wcnt[RX_NW][RX_BINS];
   __shared__ uint32_t bdig[RX_BINS];
-  __shared__ uint32_t gofs[RX_BINS];
+  __shared__ uint64_t gofs[RX_BINS];
   __shared__ uint32_t scan_sh[RX_NW + 1];
+  __shared__ uint32_t s_tile;
 
+  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  for (int i = threadIdx.x; i < RX_NW * RX_BINS; i += RX_NT) (&wcnt[0][0])[i] = 0;
+  __syncthreads();
+  const int64_t tile = s_tile;
   const int lane = dev::lane_id();
   const int w = dev::wave_id();
-  const int64_t base = (int64_t)blockIdx.x * RX_TILE;
+  const int64_t base = tile * RX_TILE;
   const int64_t wbase = base + (int64_t)w * (MRH_WAVE * RX_IT);
   const int tilecount = (int)((n - base) < RX_TILE ? (n - base) : RX_TILE);
-
-  for (int i = threadIdx.x; i < RX_NW * RX_BINS; i += RX_NT) (&wcnt[0][0])[i] = 0;
 
   uint64_t kk[RX_IT];
   uint32_t vv[RX_IT];
@@ -90,8 +112,8 @@ __global__ __launch_bounds__(RX_NT) void k_downsweep(const uint64_t* __restrict_
     kk[j] = valid ? kin[idx] : 0ull;
     vv[j] = valid ? vin[idx] : 0u;
   }
-  __syncthreads();
 
+  // wave multi-split: rank of each pair among equal digits of its wave
   const uint64_t lt = dev::lanemask_lt();
 #pragma unroll
   for (int j = 0; j < RX_IT; ++j) {
@@ -113,7 +135,7 @@ __global__ __launch_bounds__(RX_NT) void k_downsweep(const uint64_t* __restrict_
   }
   __syncthreads();
 
-  {  // digit t = threadIdx.x : wave prefixes, block-local digit offsets, global offsets
+  {  // digit t = threadIdx.x: wave prefixes, block-local digit offsets, tile count
     const int t = threadIdx.x;
     uint32_t run = 0;
 #pragma unroll
@@ -123,9 +145,30 @@ __global__ __launch_bounds__(RX_NT) void k_downsweep(const uint64_t* __restrict_
       run += c;
     }
     uint32_t total;
-    uint32_t ex = dev::block_excl_scan<uint32_t, RX_NT>(run, scan_sh, &total);
-    bdig[t] = ex;
-    gofs[t] = hist_scan[(int64_t)t * nb + blockIdx.x];
+    bdig[t] = dev::block_excl_scan<uint32_t, RX_NT>(run, scan_sh, &total);
+    // decoupled look-back for digit t
+    unsigned long long* st = status + tile * RX_BINS + t;
+    uint64_t excl = 0;
+    if (tile == 0) {
+      __hip_atomic_store(st, (unsigned long long)(LB_PRE | (epoch << 48) | run), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(st, (unsigned long long)(LB_AGG | (epoch << 48) | run), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      for (int64_t p = tile - 1; p >= 0;) {
+        const uint64_t v = __hip_atomic_load(status + p * RX_BINS + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (((v >> 48) & 255) != epoch) {  // tile p has not published yet (it is resident: spin)
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += v & LB_COUNT;
+        if (v & LB_PRE) break;
+        --p;
+      }
+      __hip_atomic_store(st, (unsigned long long)(LB_PRE | (epoch << 48) | (excl + run)), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    gofs[t] = dbase[t] + excl;
   }
   __syncthreads();
 
@@ -144,59 +187,87 @@ __global__ __launch_bounds__(RX_NT) void k_downsweep(const uint64_t* __restrict_
   for (int i = threadIdx.x; i < tilecount; i += RX_NT) {
     uint64_t key = skeys[i];
     uint32_t d = (uint32_t)(key >> shift) & 255u;
-    uint32_t g = gofs[d] + (uint32_t)i - bdig[d];
+    uint64_t g = gofs[d] + (uint64_t)i - bdig[d];
     kout[g] = key;
     vout[g] = svals[i];
   }
 }
 
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// pairs per thread of a one-sweep tile: 16 (4096-pair tiles) by default —
+// on MI355X it beats 8 at every size (half the look-back chain, 16-key runs
+// per digit in the scatter: 5.4 M keys 90 -> 78 us/pass, 200 M keys
+// 2.74 -> 2.22 ms/pass, profiles/r2_radix_onesweep_bench.txt); MRH_RX_IT=8
+// selects 2048-pair tiles
+int rx_items() {
+  static const int it = [] {
+    const char* v = std::getenv("MRH_RX_IT");
+    return (v && std::atoi(v) == 8) ? 8 : 16;
+  }();
+  return it;
+}
+
 }  // namespace
 
 size_t radix_temp_bytes(int64_t n) {
-  int64_t nb = (n + RX_TILE - 1) / RX_TILE;
-  size_t hist = ((size_t)RX_BINS * nb + 1) * sizeof(uint32_t);
-  size_t a = (hist + 255) & ~size_t(255);
-  return 2 * a + scan_temp_bytes((int64_t)RX_BINS * nb) + 8 * RX_BINS * 4 + 1024;
+  const int64_t nb = (n + RX_TILE - 1) / RX_TILE;
+  return align256((size_t)nb * RX_BINS * 8) + align256(8 * RX_BINS * 8) + align256(8 * RX_BINS * 4) + 256 + 256;
 }
 
 void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64_t* keys_out,
                         uint32_t* vals_out, uint64_t* keys_alt, uint32_t* vals_alt, int64_t n,
-                        int begin_bit, int end_bit, void* temp, hipStream_t s, int* passes_run) {
+                        int begin_bit, int end_bit, void* temp, hipStream_t s, int* passes_run, bool skip_trivial) {
   if (passes_run) *passes_run = 0;
   if (n <= 0) return;
   check_arg(n <= 0xFFFFFFFFll, "radix sort: more than 2^32-1 pairs per call (the out-of-core sort splits larger inputs)");
-  const int64_t nb = (n + RX_TILE - 1) / RX_TILE;
+  const int64_t nb = (n + RX_TILE - 1) / RX_TILE;  // status rows sized for the smallest tile
+  const int items = rx_items();
+  const int64_t ntile = (n + (int64_t)RX_NT * items - 1) / ((int64_t)RX_NT * items);
   char* t = reinterpret_cast<char*>(temp);
-  size_t hist_bytes = ((((size_t)RX_BINS * nb + 1) * sizeof(uint32_t)) + 255) & ~size_t(255);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(t);
-  uint32_t* hist_scan = reinterpret_cast<uint32_t*>(t + hist_bytes);
-  uint32_t* gcounts = reinterpret_cast<uint32_t*>(t + 2 * hist_bytes);
-  char* scan_tmp = t + 2 * hist_bytes + 8 * RX_BINS * 4 + 256;
-  scan_tmp = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(scan_tmp) + 255) & ~uintptr_t(255));
+  t = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(t) + 255) & ~uintptr_t(255));
+  const size_t st_bytes = align256((size_t)nb * RX_BINS * 8);
+  unsigned long long* status = reinterpret_cast<unsigned long long*>(t);
+  uint64_t* dbase = reinterpret_cast<uint64_t*>(t + st_bytes);
+  uint32_t* gcounts = reinterpret_cast<uint32_t*>(t + st_bytes + align256(8 * RX_BINS * 8));
+  unsigned int* tickets = reinterpret_cast<unsigned int*>(t + st_bytes + align256(8 * RX_BINS * 8) +
+                                                          align256(8 * RX_BINS * 4));
 
-  // which digit positions actually vary?
-  hipMemsetAsync(gcounts, 0, 8 * RX_BINS * 4, s);
+  // zero the look-back words, the histogram and the 8 tickets in one memset
+  // (they are contiguous apart from dbase, which k_digit_base overwrites)
+  (void)hipMemsetAsync(status, 0, st_bytes, s);
+  (void)hipMemsetAsync(gcounts, 0, align256(8 * RX_BINS * 4) + 8 * sizeof(unsigned int), s);
   int ghist_blocks = (int)((n + RX_NT - 1) / RX_NT);
   if (ghist_blocks > 2048) ghist_blocks = 2048;
-  hipLaunchKernelGGL(k_global_hist, dim3(ghist_blocks), dim3(RX_NT), 0, s, keys_in, n, gcounts);
+  const int p0 = begin_bit / 8, p1 = std::min(8, (end_bit + 7) / 8);
+  hipLaunchKernelGGL(k_global_hist, dim3(ghist_blocks), dim3(RX_NT), 0, s, keys_in, n, p0, p1, gcounts);
   MRH_CHECK_LAUNCH();
-  std::vector<uint32_t> hc(8 * RX_BINS);
-  hipMemcpyAsync(hc.data(), gcounts, 8 * RX_BINS * 4, hipMemcpyDeviceToHost, s);
-  hipStreamSynchronize(s);
   std::vector<int> passes;
-  for (int p = begin_bit / 8; p * 8 < end_bit && p < 8; ++p) {
-    bool trivial = false;
-    for (int b = 0; b < RX_BINS; ++b)
-      if (hc[p * RX_BINS + b] == (uint32_t)n) { trivial = true; break; }
-    if (!trivial) passes.push_back(p);
+  if (skip_trivial) {  // which digit positions actually vary? (one host sync)
+    std::vector<uint32_t> hc(8 * RX_BINS);
+    (void)hipMemcpyAsync(hc.data(), gcounts, 8 * RX_BINS * 4, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    for (int p = begin_bit / 8; p * 8 < end_bit && p < 8; ++p) {
+      bool trivial = false;
+      for (int b = 0; b < RX_BINS; ++b)
+        if (hc[p * RX_BINS + b] == (uint32_t)n) {
+          trivial = true;
+          break;
+        }
+      if (!trivial) passes.push_back(p);
+    }
+  } else {
+    for (int p = begin_bit / 8; p * 8 < end_bit && p < 8; ++p) passes.push_back(p);
   }
   const int np = (int)passes.size();
   if (passes_run) *passes_run = np;
   if (np == 0) {
-    hipMemcpyAsync(keys_out, keys_in, n * 8, hipMemcpyDeviceToDevice, s);
-    hipMemcpyAsync(vals_out, vals_in, n * 4, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(keys_out, keys_in, n * 8, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(vals_out, vals_in, n * 4, hipMemcpyDeviceToDevice, s);
     return;
   }
+  hipLaunchKernelGGL(k_digit_base, dim3(8), dim3(RX_BINS), 0, s, (const uint32_t*)gcounts, dbase);
+  MRH_CHECK_LAUNCH();
   const uint64_t* ki = keys_in;
   const uint32_t* vi = vals_in;
   for (int q = 0; q < np; ++q) {
@@ -204,12 +275,13 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
     bool to_out = ((np - 1 - q) % 2) == 0;
     uint64_t* ko = to_out ? keys_out : keys_alt;
     uint32_t* vo = to_out ? vals_out : vals_alt;
-    int shift = passes[q] * 8;
-    hipLaunchKernelGGL(k_upsweep, dim3(nb), dim3(RX_NT), 0, s, ki, n, shift, hist, (int)nb);
-    MRH_CHECK_LAUNCH();
-    exclusive_scan_u32(hist, hist_scan, (int64_t)RX_BINS * nb, scan_tmp, s);
-    hipLaunchKernelGGL(k_downsweep, dim3(nb), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, shift,
-                       (const uint32_t*)hist_scan, (int)nb);
+    const int p = passes[q];
+    if (items == 16)
+      hipLaunchKernelGGL(k_onesweep<16>, dim3((unsigned)ntile), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, p * 8,
+                         (const uint64_t*)(dbase + p * RX_BINS), status, (uint64_t)(q + 1), tickets + q);
+    else
+      hipLaunchKernelGGL(k_onesweep<RX_IT>, dim3((unsigned)ntile), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, p * 8,
+                         (const uint64_t*)(dbase + p * RX_BINS), status, (uint64_t)(q + 1), tickets + q);
     MRH_CHECK_LAUNCH();
     ki = ko;
     vi = vo;

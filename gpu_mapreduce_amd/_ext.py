@@ -24,6 +24,12 @@ def _load():
 
 C = _load()
 
+# MRH_GUARD=1: the guarded (canaried) HBM allocator replaces ATen's caching
+# allocator before anything in this process allocates device memory
+# (csrc/engine/guardalloc.h)
+if os.environ.get("MRH_GUARD", "0") not in ("", "0"):
+    C.install_alloc_guard()
+
 
 def so_path():
     """Path of the loaded native library (used by tests / smoke to prove the

@@ -69,6 +69,25 @@ def test_radix_sort_stable(n, bits):
     assert torch.equal(vg.cpu(), vc)
 
 
+@pytest.mark.parametrize("n,bits,skip", [(2047, 64, False), (2049, 20, False), (5_000_000, 64, False),
+                                         (40_000_000, 40, True), (40_000_000, 64, False)])
+def test_radix_onesweep_large_vs_torch(n, bits, skip):
+    """one-sweep passes (decoupled look-back across ~20 K tiles) at bench
+    sizes, with and without the host-side trivial-pass skip; oracle: torch's
+    stable sort of the same keys on the device"""
+    g = torch.Generator(device=DEV).manual_seed(n + bits)
+    k = torch.randint(0, 2 ** 62, (n,), generator=g, dtype=torch.int64, device=DEV)
+    if bits < 64:
+        k &= (1 << bits) - 1
+    k[: n // 5] = k[n // 2]
+    v = torch.arange(n, dtype=torch.int32, device=DEV)
+    kg, vg, passes = C.radix_sort_pairs(k, v, 0, bits, skip)
+    ks, order = torch.sort(k, stable=True)
+    assert torch.equal(kg, ks)
+    assert torch.equal(vg.long(), order)
+    assert passes == (bits + 7) // 8
+
+
 def test_hashlittle_device_matches_host():
     keys = [b"", b"a", b"Four score and seven years ago", bytes(range(200))] + \
            [np.random.default_rng(1).bytes(i) for i in range(1, 40)]
