@@ -255,6 +255,130 @@ __global__ __launch_bounds__(RNT) void k_kmeans_reg(const float* __restrict__ pt
     }
 }
 
+// ---------------------------------------------------------------- matrix-core kernel (D > 8)
+// Higher dimensions score on the matrix cores: x.c is a [points x D] x
+// [D x centroids] product, computed per wave on 16-point x 16-centroid tiles
+// with v_mfma_f32_16x16x4_f32 (exact f32: one fmaf per product, k-ordered,
+// the same numerics as the VALU path) and consumed in registers — the score
+// matrix never exists in memory (the hipBLASLt GEMM + argmin it replaces
+// wrote and re-read N x K floats). Per wave step:
+//   A (points): lane l holds dims 4kk + (l>>4) of point (l&15), kk < DP/4,
+//               loaded once per 16 points;
+//   B (centroids, LDS): lane l reads c[j][4kk + (l>>4)] of centroid j = l&15
+//               of the tile; two centroid tiles in flight (independent
+//               accumulators cover the 40-cycle MFMA latency);
+//   D: lane l holds x.c for points 4(l>>4)+r (r < 4) against centroid l&15;
+//   score = |c|^2 - 2 x.c, running argmin per (point, lane column), then a
+//   16-lane butterfly (ties -> lower centroid index: first-minimum, as argmin).
+// The winning centroid of each point goes through LDS back to the lanes that
+// hold its coordinates, which add them into the workgroup's LDS partials.
+constexpr int MNT = 256, MNW = MNT / MRH_WAVE;
+template <int DP>
+__global__ __launch_bounds__(MNT) void k_kmeans_mfma(const float* __restrict__ pts, int64_t n, int D,
+                                                    const float* __restrict__ cen, int K, int KP,
+                                                    double* __restrict__ acc) {
+  extern __shared__ float sh[];
+  float* cs = sh;                   // [KP][DP] centroids, zero padded
+  float* cn = cs + (size_t)KP * DP;  // [KP] |c|^2 (padding centroids: +inf)
+  float* part = cn + KP;            // [K][D+1] workgroup partial sums / counts
+  __shared__ int bestk[MNW][16];
+  for (int i = threadIdx.x; i < KP * DP; i += MNT) {
+    const int j = i / DP, d = i % DP;
+    cs[i] = (j < K && d < D) ? cen[(size_t)j * D + d] : 0.f;
+  }
+  for (int j = threadIdx.x; j < KP; j += MNT) {
+    float v = 0.f;
+    if (j < K)
+      for (int d = 0; d < D; ++d) v = fmaf(cen[(size_t)j * D + d], cen[(size_t)j * D + d], v);
+    cn[j] = j < K ? v : FLT_MAX;
+  }
+  for (int i = threadIdx.x; i < K * (D + 1); i += MNT) part[i] = 0.f;
+  __syncthreads();
+  const int l = dev::lane_id(), w = dev::wave_id();
+  const int row = l & 15, kq = l >> 4;  // A: point row, k lane-quarter; D: column = row, rows 4kq..4kq+3
+  constexpr int KK = DP / 4;
+  for (int64_t p0 = ((int64_t)blockIdx.x * MNW + w) * 16; p0 < n; p0 += (int64_t)gridDim.x * MNW * 16) {
+    const int64_t pr = p0 + row;
+    float a[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int d = 4 * kk + kq;
+      a[kk] = (pr < n && d < D) ? pts[pr * D + d] : 0.f;
+    }
+    float bv[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+    int bk[4] = {0, 0, 0, 0};
+    for (int jt = 0; jt < KP; jt += 32) {  // two 16-centroid tiles per trip
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      f4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+      const float* b0 = cs + (size_t)(jt + row) * DP + kq;
+      const float* b1 = b0 + 16 * DP;
+      const bool two = jt + 16 < KP;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], b0[4 * kk], c0, 0, 0, 0);
+        if (two) c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], b1[4 * kk], c1, 0, 0, 0);
+      }
+      const float n0 = cn[jt + row], n1 = two ? cn[jt + 16 + row] : FLT_MAX;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s0 = fmaf(-2.f, c0[r], n0);
+        if (s0 < bv[r]) { bv[r] = s0; bk[r] = jt + row; }
+        const float s1 = fmaf(-2.f, c1[r], n1);
+        if (two && s1 < bv[r]) { bv[r] = s1; bk[r] = jt + 16 + row; }
+      }
+    }
+    // argmin across the 16 lanes (centroid columns) of each lane quarter
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float ov = __shfl_xor(bv[r], o, MRH_WAVE);
+        const int ok = __shfl_xor(bk[r], o, MRH_WAVE);
+        if (ov < bv[r] || (ov == bv[r] && ok < bk[r])) { bv[r] = ov; bk[r] = ok; }
+      }
+      if (row == 0) bestk[w][4 * kq + r] = bk[r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (pr < n) {
+      const int k = bestk[w][row];
+      float* dst = part + (size_t)k * (D + 1);
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int d = 4 * kk + kq;
+        if (d < D) atomicAdd(dst + d, a[kk]);
+      }
+      if (kq == 0) atomicAdd(dst + D, 1.f);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < K * (D + 1); i += MNT)
+    if (part[i] != 0.f) atomicAdd(&acc[i], (double)part[i]);
+}
+
+int mfma_dp(int D) { return D <= 16 ? 16 : D <= 32 ? 32 : D <= 64 ? 64 : D <= 128 ? 128 : 0; }
+size_t mfma_lds(int D, int K) {
+  const int DP = mfma_dp(D), KP = (K + 15) & ~15;
+  return sizeof(float) * ((size_t)KP * DP + KP + (size_t)K * (D + 1));
+}
+constexpr size_t kMfmaLds = 120 * 1024;
+
+void launch_mfma(const float* pts, int64_t n, int D, const float* cen, int K, double* acc, hipStream_t s) {
+  const int KP = (K + 15) & ~15;
+  const size_t lds = mfma_lds(D, K);
+  int64_t nb = (n + MNW * 16 - 1) / (MNW * 16);
+  if (nb > 2048) nb = 2048;  // each workgroup walks ~16 K points before flushing its partials
+  switch (mfma_dp(D)) {
+    case 16: hipLaunchKernelGGL((k_kmeans_mfma<16>), dim3((unsigned)nb), dim3(MNT), lds, s, pts, n, D, cen, K, KP, acc); break;
+    case 32: hipLaunchKernelGGL((k_kmeans_mfma<32>), dim3((unsigned)nb), dim3(MNT), lds, s, pts, n, D, cen, K, KP, acc); break;
+    case 64: hipLaunchKernelGGL((k_kmeans_mfma<64>), dim3((unsigned)nb), dim3(MNT), lds, s, pts, n, D, cen, K, KP, acc); break;
+    default: hipLaunchKernelGGL((k_kmeans_mfma<128>), dim3((unsigned)nb), dim3(MNT), lds, s, pts, n, D, cen, K, KP, acc); break;
+  }
+  MRH_CHECK_LAUNCH();
+}
+
 template <int D>
 void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, hipStream_t s) {
   static const int variant = [] {
@@ -301,20 +425,25 @@ void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, h
 // so per-cluster counts are exact and sums lose no more than fp32 rounding of
 // 2048 terms before the fp64 global accumulation.
 bool kmeans_supported(int D, int K) {
-  return (D == 1 || D == 2 || D == 3 || D == 4 || D == 8) && K >= 1 && (size_t)K * (2 * D + 1) * 4 <= 64 * 1024;
+  if (K < 1 || D < 1) return false;
+  if ((D == 1 || D == 2 || D == 3 || D == 4 || D == 8) && (size_t)K * (2 * D + 1) * 4 <= 64 * 1024) return true;
+  return mfma_dp(D) && mfma_lds(D, K) <= kMfmaLds;  // matrix-core kernel
 }
 // (the private-accumulator kernel uses < 62 KB of LDS: K*(D+1) <= 120 rows x 128 lanes + centroids)
 
 void kmeans_assign_accumulate(const float* pts, int64_t n, int D, const float* cen, int K, double* acc,
                               hipStream_t s) {
   if (n <= 0) return;
-  switch (D) {
+  const bool small = (size_t)K * (2 * D + 1) * 4 <= 64 * 1024;
+  switch (small ? D : 0) {
     case 1: launch<1>(pts, n, cen, K, acc, s); break;
     case 2: launch<2>(pts, n, cen, K, acc, s); break;
     case 3: launch<3>(pts, n, cen, K, acc, s); break;
     case 4: launch<4>(pts, n, cen, K, acc, s); break;
     case 8: launch<8>(pts, n, cen, K, acc, s); break;
-    default: check_arg(false, "kmeans: unsupported dimension D");
+    default:
+      check_arg(mfma_dp(D) && mfma_lds(D, K) <= kMfmaLds, "kmeans: unsupported (dimension, clusters)");
+      launch_mfma(pts, n, D, cen, K, acc, s);
   }
 }
 

@@ -47,11 +47,13 @@ def test_kmeans_job_matches_lloyd():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,K", [(2, 32), (3, 5), (8, 64), (16, 10)])
+@pytest.mark.parametrize("D,K", [(2, 32), (3, 5), (8, 64), (16, 10), (5, 7), (32, 64), (64, 128), (100, 40),
+                                 (128, 16), (160, 8)])
 def test_kmeans_map_gpu(D, K):
-    """fused assign + LDS combine kernel (D <= 8) and the GEMM path (D = 16)
-    against the float64 oracle; a point equidistant to two centroids may go
-    either way, so compare with a tolerance on the counts too"""
+    """fused assign + LDS combine kernel (D <= 8), the matrix-core kernel
+    (D <= 128, any K that fits LDS) and the GEMM fallback (D = 160) against
+    the float64 oracle; a point equidistant to two centroids may go either
+    way, so compare with a tolerance on the counts too"""
     p = blobs(300_000, D, K, seed=5, device="cuda")
     c = blobs(K, D, K, seed=6, device="cuda")
     got = _kv_vals(C.kmeans_map(p, c))
