@@ -37,10 +37,15 @@ KV kmeans_map(const at::Tensor& points, const at::Tensor& centroids) {
                                 acc.data_ptr<double>(), at::hip::getCurrentHIPStream());
   } else if (N > 0) {
     at::Tensor score = (c * c).sum(1).unsqueeze(0) - 2.0 * at::matmul(p, c.t());  // [N, K]
-    at::Tensor idx = score.argmin(1);
-    at::Tensor sums = at::zeros({K, D}, acc.options()).index_add_(0, idx, p.to(at::kDouble));
-    at::Tensor cnt = bincount_dev(idx, K).to(at::kDouble).unsqueeze(1);
-    acc = at::cat({sums, cnt}, 1).reshape({-1});
+    at::Tensor idx = score.argmin(1).contiguous();
+    if (dev.is_cuda()) {
+      k::kmeans_accumulate(p.data_ptr<float>(), N, (int)D, idx.data_ptr<int64_t>(), (int)K, acc.data_ptr<double>(),
+                           at::hip::getCurrentHIPStream());
+    } else {
+      at::Tensor sums = at::zeros({K, D}, acc.options()).index_add_(0, idx, p.to(at::kDouble));
+      at::Tensor cnt = bincount_dev(idx, K).to(at::kDouble).unsqueeze(1);
+      acc = at::cat({sums, cnt}, 1).reshape({-1});
+    }
   }
   KV kv;
   kv.n = K * (D + 1);

@@ -3,6 +3,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "../kernels/launch.h"
@@ -97,6 +98,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
   return {rowptr, col, okeys, perm};
 }
 
+// hub bitmap size: MRH_TRI_HUB vertices (0 = off), default 65536 (a 512 MB
+// bitmap), a multiple of 64 and at most nvert rounded down to one
+int64_t tri_hub_size(int64_t nvert) {
+  static const int64_t want = [] {
+    const char* e = std::getenv("MRH_TRI_HUB");
+    return e ? std::atoll(e) : int64_t(65536);
+  }();
+  int64_t K = std::min<int64_t>(std::max<int64_t>(want, 0), 262144);
+  K = std::min<int64_t>(K, nvert) / 64 * 64;
+  return K;
+}
+
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1) {
   e1 = std::min<int64_t>(e1, okeys.numel());
   if (e1 <= e0) return 0;
@@ -107,10 +120,21 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
     const int64_t u0 = e0 == 0 ? 0 : src(e0 - 1) + 1;
     const int64_t u1 = e1 == m ? nvert : src(e1 - 1) + 1;
     at::Tensor tot = at::zeros({1}, opt(okeys.device(), at::kLong));
-    at::Tensor big = at::empty({2 * std::max<int64_t>(u1 - u0, 1)}, opt(okeys.device(), at::kInt));
-    at::Tensor nbig = at::zeros({2}, opt(okeys.device(), at::kInt));
-    k::tri_count_hash(P0<int64_t>(rowptr), P0<uint32_t>(col), u0, u1, P0<uint32_t>(big), P0<uint32_t>(nbig),
-                      P0<unsigned long long>(tot), cur());
+    // the top-K ranks (hubs) go to the bitmap kernel, the rest to the hash kernels
+    const int64_t K = tri_hub_size(nvert);
+    const int64_t hb = nvert - K;
+    const int64_t uh = K ? std::max(u0, std::min(u1, hb)) : u1;
+    if (K && u1 > hb) {
+      at::Tensor H = at::empty({K * (K / 64)}, opt(okeys.device(), at::kLong));
+      k::tri_hub_count(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, std::max(u0, hb), u1, P0<uint64_t>(H),
+                       P0<unsigned long long>(tot), cur());
+    }
+    if (uh > u0) {
+      at::Tensor big = at::empty({2 * std::max<int64_t>(uh - u0, 1)}, opt(okeys.device(), at::kInt));
+      at::Tensor nbig = at::zeros({2}, opt(okeys.device(), at::kInt));
+      k::tri_count_hash(P0<int64_t>(rowptr), P0<uint32_t>(col), u0, uh, P0<uint32_t>(big), P0<uint32_t>(nbig),
+                        P0<unsigned long long>(tot), cur());
+    }
     return tot.item<int64_t>();
   }
   const int64_t* rp = P0<int64_t>(rowptr);

@@ -358,6 +358,33 @@ __global__ __launch_bounds__(MNT) void k_kmeans_mfma(const float* __restrict__ p
     if (part[i] != 0.f) atomicAdd(&acc[i], (double)part[i]);
 }
 
+// combine of the library-GEMM path (D > 128): points with their argmin
+// cluster -> LDS partial sums (or fp64 global atomics when K*(D+1) floats
+// exceed LDS), one fp64 atomic per partial per workgroup
+__global__ __launch_bounds__(MNT) void k_kmeans_accum(const float* __restrict__ pts, int64_t n, int D,
+                                                     const int64_t* __restrict__ idx, int K, bool lds_part,
+                                                     double* __restrict__ acc) {
+  extern __shared__ float part[];
+  const int R = K * (D + 1);
+  if (lds_part) {
+    for (int i = threadIdx.x; i < R; i += MNT) part[i] = 0.f;
+    __syncthreads();
+  }
+  const int l = dev::lane_id();
+  for (int64_t p = (int64_t)blockIdx.x * MNW + dev::wave_id(); p < n; p += (int64_t)gridDim.x * MNW) {
+    const int64_t k = idx[p];
+    for (int d = l; d <= D; d += MRH_WAVE) {
+      const float v = d < D ? pts[p * D + d] : 1.f;
+      if (lds_part) atomicAdd(&part[k * (D + 1) + d], v);
+      else atomicAdd(&acc[k * (D + 1) + d], (double)v);
+    }
+  }
+  if (!lds_part) return;
+  __syncthreads();
+  for (int i = threadIdx.x; i < R; i += MNT)
+    if (part[i] != 0.f) atomicAdd(&acc[i], (double)part[i]);
+}
+
 int mfma_dp(int D) { return D <= 16 ? 16 : D <= 32 ? 32 : D <= 64 ? 64 : D <= 128 ? 128 : 0; }
 size_t mfma_lds(int D, int K) {
   const int DP = mfma_dp(D), KP = (K + 15) & ~15;
@@ -424,6 +451,17 @@ void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, h
 // fp32 LDS partials hold at most NT*PTS_PER_THREAD = 2048 points per workgroup,
 // so per-cluster counts are exact and sums lose no more than fp32 rounding of
 // 2048 terms before the fp64 global accumulation.
+void kmeans_accumulate(const float* pts, int64_t n, int D, const int64_t* idx, int K, double* acc, hipStream_t s) {
+  if (n <= 0) return;
+  const size_t lds = sizeof(float) * (size_t)K * (D + 1);
+  const bool lds_part = lds <= 64 * 1024;
+  int64_t nb = (n + MNW - 1) / MNW;
+  if (nb > 2048) nb = 2048;
+  hipLaunchKernelGGL(k_kmeans_accum, dim3((unsigned)nb), dim3(MNT), lds_part ? lds : 0, s, pts, n, D, idx, K, lds_part,
+                     acc);
+  MRH_CHECK_LAUNCH();
+}
+
 bool kmeans_supported(int D, int K) {
   if (K < 1 || D < 1) return false;
   if ((D == 1 || D == 2 || D == 3 || D == 4 || D == 8) && (size_t)K * (2 * D + 1) * 4 <= 64 * 1024) return true;

@@ -207,6 +207,11 @@ void tri_count(const int64_t* rowptr, const uint32_t* col, const uint64_t* okeys
 // vertex-centric LDS-hash count over vertices [u0,u1); big: scratch u32[2*(u1-u0)], nbig: zeroed u32[2]
 void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int64_t u1, uint32_t* big,
                     uint32_t* nbig, unsigned long long* total, hipStream_t s);
+// triangles whose lowest vertex is a hub (rank >= hb = nvert - K) among the
+// vertices [u0, u1), by AND/popcount of hub adjacency bitmaps; H: scratch of
+// K * K / 8 bytes (K a multiple of 64, <= 262144)
+void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64_t K, int64_t u0, int64_t u1,
+                   uint64_t* H, unsigned long long* total, hipStream_t s);
 // CSR row pointers of sorted oriented keys
 void tri_rowptr(const uint64_t* okeys, int64_t m, int64_t nvert, int64_t* rowptr, hipStream_t s);
 // triangles (u,v,w) as 3 u64 at off[e-e0] (off: exclusive scan of cnt, n+1 entries)
@@ -272,5 +277,7 @@ bool kmeans_supported(int D, int K);
 // acc[K*(D+1)] (fp64, zeroed by the caller) += per-cluster coordinate sums and counts
 void kmeans_assign_accumulate(const float* pts, int64_t n, int D, const float* cen, int K, double* acc,
                               hipStream_t s);
+// acc[K*(D+1)] += coordinate sums and counts of points already assigned (idx[n] in [0, K))
+void kmeans_accumulate(const float* pts, int64_t n, int D, const int64_t* idx, int K, double* acc, hipStream_t s);
 }  // namespace k
 }  // namespace mrh

@@ -62,7 +62,10 @@ def test_kmeans_map_gpu(D, K):
     counts_got, counts_ref = got.reshape(K, D + 1)[:, D], ref.reshape(K, D + 1)[:, D]
     assert counts_got.sum() == 300_000
     assert np.abs(counts_got - counts_ref).max() <= 3
-    np.testing.assert_allclose(got, ref, rtol=1e-3, atol=0.5)
+    # each point that went to the other of two (near-)equidistant centroids
+    # moves its coordinates (< 1.5 in the unit-cube blobs) between two sums
+    moved = max(1.0, np.abs(counts_got - counts_ref).sum() / 2)
+    np.testing.assert_allclose(got, ref, rtol=1e-3, atol=1.5 * moved)
 
 
 @pytest.mark.gpu

@@ -111,3 +111,33 @@ def test_distributed_triangles_match_replicated(world):
         assert not (tris & set(lst)), "a triangle listed on two ranks"
         tris |= set(lst)
     assert tris == want
+
+
+TRI_HUB_CHILD = r'''
+import sys, torch
+from gpu_mapreduce_amd import Comm, C
+from gpu_mapreduce_amd.models.triangles import TriangleGraph
+from tests.test_triangles import _rmat
+e = _rmat(17, 16, 3)
+gpu = TriangleGraph(Comm(device="cuda"), e.cuda())
+print(C.tri_hub_size(gpu.nvert), gpu.count())
+'''
+
+
+@pytest.mark.gpu
+def test_gpu_hub_bitmap_split_matches_cpu():
+    """the same RMAT-17 count with the hub bitmap path off (hash kernels
+    only), on a 4096-vertex hub set (both paths) and on the default 65536
+    (most of the graph in bitmaps) — each must equal the CPU merge count"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    want = TriangleGraph(Comm(device="cpu"), _rmat(17, 16, 3)).count()
+    for hub, K in (("0", 0), ("4096", 4096), ("65536", 65536)):
+        env = dict(os.environ, MRH_TRI_HUB=hub, PYTHONPATH=root)
+        r = subprocess.run([sys.executable, "-c", TRI_HUB_CHILD], env=env, cwd=root, capture_output=True, text=True,
+                           timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        k, n = map(int, r.stdout.split())
+        assert k == K and n == want, (hub, k, n, want)
