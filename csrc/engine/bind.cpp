@@ -231,6 +231,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property("fpath", [](MR& r) { return r.set.fpath; }, [](MR& r, const std::string& v) { r.set.fpath = v; })
       .def_property("chunk_bytes", [](MR& r) { return r.set.chunk_bytes; },
                     [](MR& r, int64_t v) { r.set.chunk_bytes = v; })
+      .def_property("pipeline", [](MR& r) { return r.set.pipeline; }, [](MR& r, int v) { r.set.pipeline = v; })
       .def_property("hbm_budget", [](MR& r) { return r.set.hbm_budget; },
                     [](MR& r, int64_t v) { r.set.hbm_budget = v; })
       .def_property("host_budget", [](MR& r) { return r.set.host_budget; },

@@ -58,7 +58,7 @@ GroupIndex::GroupIndex(at::Device dev) : dev_(dev) {
 }
 
 bool GroupIndex::accepts(const KV& p) const {
-  if (kw_ == -2) return !(p.kfixed() && p.kw <= 8);  // fixed keys <= 8 B: convert's exact raw-key path
+  if (kw_ == -2) return true;
   return p.kw == kw_ && p.vw == vw_;
 }
 
@@ -194,8 +194,12 @@ KV GroupIndex::kv() const {
 }
 
 bool GroupIndex::describes(const KV& kv) const {
-  return kw_ != -2 && n_ > 0 && kv.n == n_ && kv.kw == kw_ && kv.vw == vw_ && kv.kdata.defined() &&
-         kv.kdata.data_ptr() == kd_.data_ptr() && kv.vdata.defined() && kv.vdata.data_ptr() == vd_.data_ptr();
+  // same arena storage (data_ptr() of an empty view is null: zero-width values)
+  auto same = [](const at::Tensor& t, const at::Tensor& a) {
+    return t.defined() && a.defined() && t.has_storage() && t.storage().data() == a.storage().data();
+  };
+  return kw_ != -2 && n_ > 0 && kv.n == n_ && kv.kw == kw_ && kv.vw == vw_ && same(kv.kdata, kd_) &&
+         same(kv.vdata, vd_);
 }
 
 bool GroupIndex::finish(KMV* out, ConvertStats* st) {
@@ -216,8 +220,31 @@ bool GroupIndex::finish(KMV* out, ConvertStats* st) {
     }
     return t;
   };
-  // 1. groups in 64-bit hash order (convert's key order)
-  auto [gsorted, order, p1] = radix_sort_pairs(ghash_.narrow(0, 0, m), iota(m), 0, 64, false);
+  // 1. groups in convert's key order: fixed keys of <= 8 bytes by their raw
+  // little-endian value (exact), all others by 64-bit hash
+  at::Tensor gkey;
+  int gbits = 64;
+  if (kw_ >= 0 && kw_ <= 8) {
+    gbits = std::max(8, 8 * kw_);
+    at::Tensor rep32 = rep_.narrow(0, 0, m).to(at::kInt);
+    at::Tensor uk = gather_rows(kd_, at::Tensor(), kw_, rep32, nullptr);
+    gkey = at::empty({m}, opt(dev_, at::kLong));
+    if (cuda) {
+      at::Tensor scratch_idx = at::empty({m}, opt(dev_, at::kInt));
+      k::make_sortkeys_fixed(P0<uint8_t>(uk), kw_, m, 0, false, P0<uint64_t>(gkey), P0<uint32_t>(scratch_idx), cur());
+    } else {
+      const uint8_t* d = P0<uint8_t>(uk);
+      uint64_t* g = P0<uint64_t>(gkey);
+      for (int64_t j = 0; j < m; ++j) {
+        uint64_t raw = 0;
+        for (int b = 0; b < kw_; ++b) raw |= (uint64_t)d[j * kw_ + b] << (8 * b);
+        g[j] = raw;
+      }
+    }
+  } else {
+    gkey = ghash_.narrow(0, 0, m);
+  }
+  auto [gsorted, order, p1] = radix_sort_pairs(gkey, iota(m), 0, gbits, false);
   at::Tensor rank = at::empty({m}, opt(dev_, at::kInt)), heads = at::empty({m}, opt(dev_, at::kInt));
   at::Tensor key = at::empty({n}, opt(dev_, at::kLong));
   if (cuda) {

@@ -10,14 +10,14 @@
 //              keys (lookup3 hashlittle2), claim / find each hash in an HBM
 //              hash table, check every key's bytes against its group's first
 //              key (exact);
-//   finish()   the KMV in convert()'s order — unique keys by 64-bit hash,
-//              values in append order — from two short sorts (the groups by
-//              hash, the pairs by group rank), no full-KV hash sort and no
-//              key verification pass left for after the map.
+//   finish()   the KMV in convert()'s order — unique keys by 64-bit hash
+//              (fixed keys of <= 8 bytes: by raw value), values in append
+//              order — from two short sorts (the groups by key order, the
+//              pairs by group rank), no full-KV sort and no key
+//              verification pass left for after the map.
 // A 64-bit hash collision between different keys is detected by the byte
 // check; finish() then reports failure and the caller runs the ordinary
-// convert (exact regrouping) on kv(). Keys of fixed width <= 8 bytes are not
-// grouped here (convert orders them by raw value, exactly, already).
+// convert (exact regrouping) on kv().
 #pragma once
 #include <memory>
 

@@ -20,6 +20,7 @@
 #pragma once
 #include <ATen/ATen.h>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -129,6 +130,13 @@ struct ExchangeOpts {
   // 311-363): P pairwise steps per round, step j sends to me+j and receives
   // from me-j, one peer link busy at a time
   int all2all = 1;
+  // pipelined consumer (collate): every round's received pairs are handed to
+  // round_sink as a KV (views of a device staging buffer, valid until the
+  // sink's work queued on the current stream has run; the sink must copy what
+  // it keeps) while the next round is on the wire. exchange() then returns an
+  // empty KV. Pairs reach the sink round by round, each round source-rank
+  // major (with one round: exactly the order exchange() would return)
+  std::function<void(const KV&)> round_sink;
 };
 // destination rank per pair: hashlittle(key, kb, P) % P (MR-MPI default)
 at::Tensor partition_dest(const KV& kv, int P, at::Tensor* counts);

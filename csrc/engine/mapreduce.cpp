@@ -2,6 +2,7 @@
 // method as src/mapreduce.cpp:<lines>.
 #include "mapreduce.h"
 #include "guard.h"
+#include "grouper.h"
 #include "guardalloc.h"
 #include "ooc.h"
 
@@ -824,6 +825,44 @@ uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
   OpTrace tr_(__func__, this);
   enter(__func__);
   need_kv("collate");
+  // pipelined collate: the hash-partition exchange hands every received round
+  // to a GroupIndex, which groups it on the compute stream while the next
+  // round is on the wire (alltoallv k || group k-1); the
+  // group-by is done when the last round lands. MRH_PIPELINE_COLLATE=0 turns
+  // it off; out-of-core data (an HBM budget in force) keeps aggregate+convert.
+  static const bool pipeline_env = [] {
+    const char* e = std::getenv("MRH_PIPELINE_COLLATE");
+    return !(e && *e == '0');
+  }();
+  const bool pipeline = set.pipeline < 0 ? pipeline_env : set.pipeline != 0;
+  if (pipeline && !hash && comm_->distributed() && budget() == 0) {
+    ShuffleStats st;
+    GroupIndex g(device());
+    ExchangeOpts o = xopts();
+    o.round_sink = [&](const KV& r) { g.add(r); };
+    KV rest = exchange(std::move(*kv), at::Tensor(), *comm_, o, &st);
+    note_shuffle(st);
+    last_convert = ConvertStats();
+    if (g.size() == 0) {
+      kv = rest;
+      kmv = mrh::convert(*kv, &last_convert);
+    } else {
+      kv = g.kv();
+      KMV m;
+      if (g.finish(&m, &last_convert)) {
+        kmv = std::move(m);
+        last_convert.grouped = 1;
+      } else {
+        last_convert = ConvertStats();
+        kmv = mrh::convert(*kv, &last_convert, 64);
+        last_convert.grouped = 2;
+      }
+    }
+    kv.reset();
+    grouped_.reset();
+    stats("Collate", 1);
+    return count(kmv->nkey);
+  }
   const int v = set.verbosity, t = set.timer;
   set.verbosity = set.timer = 0;
   aggregate(hash);

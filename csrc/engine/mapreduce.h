@@ -70,6 +70,10 @@ struct Settings {
   int64_t host_budget = 0;
   // HIP streams the pipelined apps overlap (H2D copy / compute / shuffle)
   int streams = 2;
+  // collate() groups each received shuffle round while the next one is on
+  // the wire (1, default) or runs aggregate then convert (0); the env
+  // MRH_PIPELINE_COLLATE=0 sets the default to 0
+  int pipeline = -1;
 };
 
 class MapReduce {

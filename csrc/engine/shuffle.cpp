@@ -339,21 +339,23 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
   };
 
   // ---- 5. output
-  const bool host_sink =
-      cuda && (o.host_sink || (o.hbm_budget > 0 && rkb_tot + rvb_tot + nrecv * (lenb + 8) > o.hbm_budget));
+  const bool round_sink = (bool)o.round_sink;
+  const bool host_sink = !round_sink && cuda &&
+                         (o.host_sink || (o.hbm_budget > 0 && rkb_tot + rvb_tot + nrecv * (lenb + 8) > o.hbm_budget));
   const at::Device odev = host_sink ? at::Device(at::kCPU) : dev;
   auto oopt = [&](at::ScalarType t) {
     auto x = opt(odev, t);
     return host_sink ? x.pinned_memory(true) : x;
   };
   KV out;
-  out.n = nrecv;
+  const int64_t nout = round_sink ? 0 : nrecv;  // a round sink gets the pairs instead
+  out.n = nout;
   out.kw = kw;
   out.vw = vw;
-  out.kdata = at::empty({kvar ? rkb_tot : nrecv * std::max(kw, 0)}, oopt(at::kByte));
-  out.vdata = at::empty({vvar ? rvb_tot : nrecv * std::max(vw, 0)}, oopt(at::kByte));
-  at::Tensor rklen = kvar ? at::empty({nrecv}, oopt(at::kInt)) : at::Tensor();
-  at::Tensor rvlen = vvar ? at::empty({nrecv}, oopt(at::kInt)) : at::Tensor();
+  out.kdata = at::empty({round_sink ? 0 : kvar ? rkb_tot : nrecv * std::max(kw, 0)}, oopt(at::kByte));
+  out.vdata = at::empty({round_sink ? 0 : vvar ? rvb_tot : nrecv * std::max(vw, 0)}, oopt(at::kByte));
+  at::Tensor rklen = kvar ? at::empty({nout}, oopt(at::kInt)) : at::Tensor();
+  at::Tensor rvlen = vvar ? at::empty({nout}, oopt(at::kInt)) : at::Tensor();
 
   // per-column send bases (bytes) of bucket d, piece k; receive bases of (src, k)
   // columns: 0 key bytes, 1 value bytes, 2 key lengths, 3 value lengths
@@ -392,6 +394,70 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
     return cols[ci].lens ? pairs_of(src, d, k) * 4 : bytes_of(src, d, cols[ci].c, k);
   };
 
+  // ---- 6a. pipelined rounds into a consumer: round k lands in device staging
+  // buffer k%2 on the communication stream while the compute stream hands
+  // round k-1 to the sink (two rounds in flight); a staging buffer is posted
+  // again only behind the sink's work on it (the RCCL fence on the compute
+  // stream orders it)
+  if (round_sink) {
+    int64_t stage_bytes = 1;
+    for (int k = 0; k < R; ++k) {
+      int64_t b = 0;
+      for (int ci = 0; ci < 4; ++ci)
+        if (cols[ci].on)
+          for (int src = 0; src < P; ++src) b += piece_col_bytes(ci, src, me, k);
+      stage_bytes = std::max(stage_bytes, b + 4 * 16);  // each column starts 16-byte aligned
+    }
+    at::Tensor stage[2] = {at::empty({stage_bytes}, opt(dev, at::kByte)), at::empty({stage_bytes}, opt(dev, at::kByte))};
+    struct RoundLayout {
+      int64_t start[4] = {0, 0, 0, 0}, bytes[4] = {0, 0, 0, 0}, n = 0;
+      hipEvent_t landed = nullptr;
+    } lay[2];
+    auto post = [&](int k) {
+      guard::fault_point("exchange_round", me);
+      RoundLayout& L = lay[k % 2];
+      L = RoundLayout();
+      std::vector<Xfer> xs, xr;
+      int64_t sbuf = 0;
+      for (int src = 0; src < P; ++src) L.n += pairs_of(src, me, k);
+      for (int ci = 0; ci < 4; ++ci) {
+        if (!cols[ci].on) continue;
+        sbuf = (sbuf + 15) & ~int64_t(15);  // the int32 length columns are viewed in place
+        L.start[ci] = sbuf;
+        for (int p = 0; p < P; ++p) {
+          const int64_t sb = piece_col_bytes(ci, me, p, k);
+          xs.push_back({p, cols[ci].send + soff[ci][p], sb});
+          soff[ci][p] += sb;
+          const int64_t rb = piece_col_bytes(ci, p, me, k);
+          xr.push_back({p, P0<uint8_t>(stage[k % 2]) + sbuf, rb});
+          sbuf += rb;
+        }
+        L.bytes[ci] = sbuf - L.start[ci];
+      }
+      if (comm.uses_rccl()) L.landed = comm.rccl()->sendrecv_async(xs, xr, s);
+      else comm.sendrecv(xs, xr);
+    };
+    post(0);
+    if (R > 1) post(1);
+    for (int k = 0; k < R; ++k) {
+      RoundLayout& L = lay[k % 2];
+      if (L.landed) (void)hipStreamWaitEvent(s, L.landed, 0);
+      if (L.n > 0) {
+        KV r;
+        r.n = L.n;
+        r.kw = kw;
+        r.vw = vw;
+        r.kdata = stage[k % 2].narrow(0, L.start[0], L.bytes[0]);
+        r.vdata = stage[k % 2].narrow(0, L.start[1], L.bytes[1]);
+        if (kvar) r.koff = exclusive_scan(stage[k % 2].narrow(0, L.start[2], L.bytes[2]).view(at::kInt));
+        if (vvar) r.voff = exclusive_scan(stage[k % 2].narrow(0, L.start[3], L.bytes[3]).view(at::kInt));
+        o.round_sink(r);
+      }
+      if (k + 2 < R) post(k + 2);
+    }
+    for (auto& L : lay) L.landed = nullptr;  // events belong to the communicator's ring
+  }
+
   // ---- 6. rounds
   const hipStream_t cs_ = s;
   at::Tensor stage[2];
@@ -410,7 +476,7 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
     copy_stream = c10::hip::getStreamFromPool(false, dev.index());
     for (auto& e : drained) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   }
-  for (int k = 0; k < R; ++k) {
+  for (int k = 0; k < R && !round_sink; ++k) {
     guard::fault_point("exchange_round", me);
     std::vector<Xfer> xs, xr;
     struct Drain {
@@ -478,8 +544,8 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
   }
 
   // ---- 7. offsets of variable columns
-  if (kvar) out.koff = exclusive_scan(rklen);
-  if (vvar) out.voff = exclusive_scan(rvlen);
+  if (kvar) out.koff = round_sink ? at::zeros({1}, opt(dev, at::kLong)) : exclusive_scan(rklen);
+  if (vvar) out.voff = round_sink ? at::zeros({1}, opt(dev, at::kLong)) : exclusive_scan(rvlen);
   if (st) {
     st->send_pairs += sent_pairs;
     st->recv_pairs += nrecv;

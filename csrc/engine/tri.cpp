@@ -98,14 +98,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
   return {rowptr, col, okeys, perm};
 }
 
-// hub bitmap size: MRH_TRI_HUB vertices (0 = off), default 65536 (a 512 MB
-// bitmap), a multiple of 64 and at most nvert rounded down to one
+// hub bitmap size: MRH_TRI_HUB vertices (0 = off); default nvert / 64 capped
+// at 262144 (an 8 GB bitmap) — the best of a sweep on RMAT-24 (16.8 M
+// vertices): 0 / 32 K / 64 K / 128 K / 256 K / 384 K / 512 K hubs = 1566 /
+// 1332 / 999 / 867 / 673 / 812 / 811 ms (profiles/r2_trifind_hub_sweep.txt);
+// a multiple of 64, at most nvert
 int64_t tri_hub_size(int64_t nvert) {
-  static const int64_t want = [] {
+  static const int64_t env = [] {
     const char* e = std::getenv("MRH_TRI_HUB");
-    return e ? std::atoll(e) : int64_t(65536);
+    return e ? std::atoll(e) : int64_t(-1);
   }();
-  int64_t K = std::min<int64_t>(std::max<int64_t>(want, 0), 262144);
+  const int64_t want = env >= 0 ? env : std::min<int64_t>(nvert / 64, 262144);
+  int64_t K = std::min<int64_t>(std::max<int64_t>(want, 0), 524288);
   K = std::min<int64_t>(K, nvert) / 64 * 64;
   return K;
 }

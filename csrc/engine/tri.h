@@ -11,8 +11,8 @@ namespace mrh {
 // [nvert+1], col int32 [m], okeys int64 [m] = src<<32|dst sorted) and perm
 // (int64 [nvert], perm[rank] = original id).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq, int64_t nvert);
-// vertices of the hub bitmap path of tri_count (MRH_TRI_HUB, default 65536;
-// 0 = hash kernels only)
+// vertices of the hub bitmap path of tri_count (MRH_TRI_HUB, default
+// nvert/64 up to 262144; 0 = hash kernels only)
 int64_t tri_hub_size(int64_t nvert);
 // number of triangles whose first oriented edge lies in [e0, e1)
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1);

@@ -209,7 +209,7 @@ void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int6
                     uint32_t* nbig, unsigned long long* total, hipStream_t s);
 // triangles whose lowest vertex is a hub (rank >= hb = nvert - K) among the
 // vertices [u0, u1), by AND/popcount of hub adjacency bitmaps; H: scratch of
-// K * K / 8 bytes (K a multiple of 64, <= 262144)
+// K * K / 8 bytes (K a multiple of 64, <= 524288)
 void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64_t K, int64_t u0, int64_t u1,
                    uint64_t* H, unsigned long long* total, hipStream_t s);
 // CSR row pointers of sorted oriented keys

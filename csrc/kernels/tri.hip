@@ -436,7 +436,7 @@ void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int6
 
 void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64_t K, int64_t u0, int64_t u1,
                    uint64_t* H, unsigned long long* total, hipStream_t s) {
-  check_arg(K > 0 && K % 64 == 0 && K <= HUB_NT * 64 * 16, "tri_hub_count: K must be a multiple of 64, <= 262144");
+  check_arg(K > 0 && K % 64 == 0 && K <= HUB_NT * 64 * 32, "tri_hub_count: K must be a multiple of 64, <= 524288");
   const int64_t r0 = std::max<int64_t>(u0 - hb, 0), r1 = std::min<int64_t>(u1 - hb, K);
   if (r1 <= r0) return;
   (void)hipMemsetAsync(H, 0, (size_t)K * (K / 64) * 8, s);
@@ -452,8 +452,10 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
     hipLaunchKernelGGL(k_tri_hub_count<4>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
   else if (W <= HUB_NT * 8)
     hipLaunchKernelGGL(k_tri_hub_count<8>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
-  else
+  else if (W <= HUB_NT * 16)
     hipLaunchKernelGGL(k_tri_hub_count<16>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
+  else
+    hipLaunchKernelGGL(k_tri_hub_count<32>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
   MRH_CHECK_LAUNCH();
 }
 

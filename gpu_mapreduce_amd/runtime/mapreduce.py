@@ -34,7 +34,7 @@ _SETTINGS = ("mapstyle", "all2all", "verbosity", "timer", "memsize", "minpage", 
              "outofcore", "zeropage", "keyalign", "valuealign", "fpath",
              # MI355X-native settings (mapreduce.h): shuffle receive cap, HBM /
              # pinned-host budgets of the out-of-core tiers, pipelined streams
-             "chunk_bytes", "hbm_budget", "host_budget", "streams")
+             "chunk_bytes", "hbm_budget", "host_budget", "streams", "pipeline")
 
 
 def _arity(fn):

@@ -39,7 +39,7 @@ def test_dead_rank_is_detected_not_hung(tmp_path):
     t0 = time.time()
     for r in range(2):
         env = dict(ENV0, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HIP_VISIBLE_DEVICES="", MRH_FAULT="abort:aggregate:1")
+                   MASTER_PORT=str(port), HIP_VISIBLE_DEVICES="", MRH_FAULT="abort:exchange_round:1")
         procs.append(subprocess.Popen([exe, "docs"], cwd=tmp_path, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     try:
@@ -49,7 +49,8 @@ def test_dead_rank_is_detected_not_hung(tmp_path):
             if p.poll() is None:
                 p.kill()
     elapsed = time.time() - t0
-    assert procs[1].returncode == 3 and "rank 1 aborts at aggregate" in res[1][1]
+    # rank 1 dies inside the shuffle (a round of the collate exchange)
+    assert procs[1].returncode == 3 and "rank 1 aborts at exchange_round" in res[1][1]
     assert procs[0].returncode != 0, "the surviving rank must fail, not report success"
     assert elapsed < 30, f"failure took {elapsed:.0f} s to surface (MRH_COMM_TIMEOUT left at 600 s)"
 
@@ -171,11 +172,12 @@ def test_op_trace_two_ranks(tmp_path):
     recs = ts.load(str(tmp_path / "trace"))
     assert {r["rank"] for r in recs} == {0, 1}
     ops = {r["op"] for r in recs}
-    assert {"map_file", "collate", "aggregate", "convert", "reduce", "gather", "sort_values"} <= ops
-    # collate is traced with its nested aggregate + convert one level deeper
+    assert {"map_file", "collate", "reduce", "gather", "sort_values"} <= ops
+    # the pipelined collate is one leaf op (shuffle rounds + per-round group-by);
+    # with MRH_PIPELINE_COLLATE=0 it nests aggregate + convert one level deeper
     col = [r for r in recs if r["op"] == "collate" and r["rank"] == 0][0]
-    assert any(r["op"] == "aggregate" and r["depth"] == col["depth"] + 1 for r in recs)
-    assert sum(r["sent"] for r in recs if r["op"] == "aggregate") > 0
+    assert "aggregate" not in ops or any(r["op"] == "aggregate" and r["depth"] == col["depth"] + 1 for r in recs)
+    assert sum(r["sent"] for r in recs if r["op"] in ("aggregate", "collate")) > 0
     s = ts.summarise(recs)
     assert {"Map", "Network I/O", "Sort/Hash", "Reduce"} <= set(s["stages_ms"])
 

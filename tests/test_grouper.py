@@ -95,17 +95,24 @@ def test_layout_change_falls_back_to_chunks():
     assert a[2] == b[2]
 
 
-def test_small_fixed_keys_not_grouped():
-    mr = MapReduce(g.Comm(device="cpu"))
-    seen = {}
+def _small_parts(dev):
+    rng = random.Random(11)
+    out = []
+    for p in range(4):
+        ks = [rng.randrange(0, 300) * (1 if p % 2 else 1 << 33) for _ in range(500)]
+        out.append(C.make_kv(torch.tensor(ks, dtype=torch.int64).view(torch.uint8), None,
+                             torch.tensor([p * 1000 + i for i in range(500)], dtype=torch.int32).view(torch.uint8),
+                             None, 500, dev))
+    return out
 
-    def fn(itask, kv):
-        kv.enable_grouping()
-        kv.add_tensors(torch.tensor([3, 1, 3, 2], dtype=torch.int64), torch.tensor([1, 2, 3, 4], dtype=torch.int32))
-        seen["g"] = kv.grouping
-    mr.map(1, fn)
-    assert not seen["g"]  # int64 keys take convert's exact raw-key path
-    assert mr.convert() == 3
+
+def test_small_fixed_keys_grouped_in_raw_key_order():
+    """int64 keys: convert orders groups by raw key value (exact path); the
+    grouped convert must produce the same KMV"""
+    a = _run("cpu", _small_parts, False)
+    b = _run("cpu", _small_parts, True)
+    assert a[1] == b[1] and a[2] == b[2]
+    assert b[3].grouped == 1 and a[3].exact
 
 
 def test_forced_collisions_exact_fallback():
@@ -145,6 +152,13 @@ def test_grouped_convert_gpu_matches_cpu(seed):
     assert a[0] == b[0] and a[1] == b[1]
     assert a[2] == b[2]
     assert b[3].collisions == 0
+
+
+@pytest.mark.gpu
+def test_grouped_convert_gpu_small_fixed():
+    a = _run("cpu", _small_parts, False)
+    b = _run("cuda", _small_parts, True)
+    assert a[2] == b[2] and b[3].grouped == 1
 
 
 @pytest.mark.gpu

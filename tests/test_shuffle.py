@@ -155,3 +155,49 @@ def test_chunked_collate_via_settings():
         for k, c in a:
             total[k] += c
     assert sum(total.values()) == 4000
+
+
+def case_pipelined_collate(comm):
+    """collate with the pipelined exchange -> GroupIndex (pipeline=1) vs
+    aggregate + convert (pipeline=0): the same keys in the same order, the
+    same per-key value multisets; with one round the same value order too.
+    Skewed keys (one hot key), rank 2 maps nothing, var and int64 keys."""
+    import gpu_mapreduce_amd as g
+    out = {}
+    for layout in ("var", "i64"):
+        for chunk in (0, 200):
+            got = []
+            for pipe in (1, 0):
+                mr = g.MapReduce(comm)
+                mr.chunk_bytes = chunk
+                mr.pipeline = pipe
+
+                def fn(i, kv):
+                    if comm.rank == 2:
+                        return
+                    for j in range(1500):
+                        k = 7 if j % 3 == 0 else (i * 31 + j * 7) % 53
+                        key = (b"key%d\0" % k) if layout == "var" else struct.pack("<q", k * 1000003)
+                        kv.add(key, struct.pack("<i", comm.rank * 100000 + i * 10000 + j))
+                mr.map(6, fn)  # two tasks per rank; rank 2 emits nothing
+                nu = mr.collate()
+                conv = mr.last_convert.grouped
+                pairs = mr.kmv_pairs()
+                got.append((nu, conv, [k for k, _ in pairs], [list(v) for _, v in pairs]))
+            (n1, g1, k1, v1), (n0, g0, k0, v0) = got
+            assert n1 == n0 and k1 == k0, (layout, chunk)
+            assert [sorted(a) for a in v1] == [sorted(b) for b in v0], (layout, chunk)
+            if chunk == 0:
+                assert v1 == v0, (layout, chunk)
+            out[(layout, chunk)] = (n1, g1, g0, sum(len(v) for v in v1))
+    return out
+
+
+def test_pipelined_collate_matches_aggregate_convert():
+    out = run_world("test_shuffle:case_pipelined_collate", 3)
+    for r, res in out.items():
+        for (layout, chunk), (nu, g1, g0, nval) in res.items():
+            assert g1 == (1 if nval else 0) and g0 == 0, (r, layout, chunk, g1, g0)
+    # every pair arrived somewhere: 2 ranks x 2 tasks x 1500 per setting
+    for key in out[0]:
+        assert sum(out[r][key][3] for r in out) == 6000

@@ -127,15 +127,18 @@ print(C.tri_hub_size(gpu.nvert), gpu.count())
 @pytest.mark.gpu
 def test_gpu_hub_bitmap_split_matches_cpu():
     """the same RMAT-17 count with the hub bitmap path off (hash kernels
-    only), on a 4096-vertex hub set (both paths) and on the default 65536
-    (most of the graph in bitmaps) — each must equal the CPU merge count"""
+    only), on the default (nvert/64 = 2048 hubs), 4096 hubs, and 65536 (half
+    of the graph in bitmaps) — each must equal the CPU merge count"""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     want = TriangleGraph(Comm(device="cpu"), _rmat(17, 16, 3)).count()
-    for hub, K in (("0", 0), ("4096", 4096), ("65536", 65536)):
-        env = dict(os.environ, MRH_TRI_HUB=hub, PYTHONPATH=root)
+    for hub, K in (("0", 0), (None, 2048), ("4096", 4096), ("65536", 65536)):
+        env = dict(os.environ, PYTHONPATH=root)
+        env.pop("MRH_TRI_HUB", None)
+        if hub is not None:
+            env["MRH_TRI_HUB"] = hub
         r = subprocess.run([sys.executable, "-c", TRI_HUB_CHILD], env=env, cwd=root, capture_output=True, text=True,
                            timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]

@@ -18,6 +18,9 @@ STAGE = {
     "map_mr_batch": "Map", "map_chunks": "Map",
     "aggregate": "Network I/O", "aggregate_dest": "Network I/O", "gather": "Network I/O",
     "broadcast": "Network I/O",
+    # a pipelined collate is one leaf op: the shuffle rounds with the
+    # group-by of each round hidden under the next one
+    "collate": "Network I/O",
     "convert": "Sort/Hash", "clone": "Sort/Hash", "collapse": "Sort/Hash", "sort_keys": "Sort/Hash",
     "sort_values": "Sort/Hash", "sort_multivalues": "Sort/Hash",
     "reduce": "Reduce", "reduce_builtin": "Reduce", "reduce_batch": "Reduce", "compress": "Reduce",
