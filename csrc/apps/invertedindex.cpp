@@ -51,6 +51,7 @@ std::string part_name(int i) {
 struct App {
   std::string dir;
   int nfile = 0, first = 0, last = 0;  // this rank's files [first, last)
+  int nprocs = 1;
   int64_t in_bytes = 0;
 };
 
@@ -58,6 +59,9 @@ struct App {
 void map_files(App& app, KeyValue& kv, at::Device dev) {
   const int nf = app.last - app.first;
   if (nf <= 0) return;
+  // one rank: group each part file as it arrives (the aggregate that follows
+  // is the identity, so convert finds the group-by done; keyvalue.h)
+  if (app.nprocs == 1) kv.enable_grouping();
   std::vector<int64_t> sizes(nf);
   int64_t maxlen = 0;
   for (int i = 0; i < nf; ++i) {
@@ -144,6 +148,7 @@ int main(int argc, char** argv) {
   app.nfile = std::atoi(pos[1].c_str());
   app.first = (int)((int64_t)app.nfile * me / np);
   app.last = (int)((int64_t)app.nfile * (me + 1) / np);
+  app.nprocs = np;
   const std::string outdir = pos.size() > 2 ? pos[2] : "NULL";
   const at::Device dev = comm->device();
 

@@ -127,7 +127,7 @@ print(C.tri_hub_size(gpu.nvert), gpu.count())
 @pytest.mark.gpu
 def test_gpu_hub_bitmap_split_matches_cpu():
     """the same RMAT-17 count with the hub bitmap path off (hash kernels
-    only), on the default (nvert/64 = 2048 hubs), 4096 hubs, and 65536 (half
+    only), on the default (nvert/64 ~ 2048 hubs), 4096 hubs, and 65536 (half
     of the graph in bitmaps) — each must equal the CPU merge count"""
     import os
     import subprocess
@@ -143,4 +143,4 @@ def test_gpu_hub_bitmap_split_matches_cpu():
                            timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         k, n = map(int, r.stdout.split())
-        assert k == K and n == want, (hub, k, n, want)
+        assert (k == K if hub is not None else 0 < k <= K and k % 64 == 0) and n == want, (hub, k, n, want)
