@@ -595,6 +595,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("ranks", &PageRankPlan::ranks)
       .def_readonly("N", &PageRankPlan::N)
       .def_readonly("nlocal", &PageRankPlan::nlocal)
+      .def_property_readonly("blocking", &PageRankPlan::blocking)
       .def_readonly("nedge", &PageRankPlan::nedge)
       .def_readonly("ndangling", &PageRankPlan::ndangling);
   py::class_<TriangleGraph>(m, "TriangleGraph")

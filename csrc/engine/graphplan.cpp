@@ -278,14 +278,94 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
   } else {
     vid_ = new_of_old.index_select(0, at::floor_divide(ujv, P)).contiguous();
   }
+  // one GPU, opt-in (MRH_PR_BLOCKING=1): propagation blocking (pbpr.hip).
+  // Measured on RMAT-26 at 8.9 ms per iteration (phase 1 3.5 + phase 2 5.4)
+  // vs 7.9 ms for the pull kernel, whose 60 % L2 hit rate on the
+  // degree-sorted gathers already beats two streaming passes
+  // (profiles/r2_pagerank_blocking.txt); kept for graphs without hub locality
+  {
+    const char* e = std::getenv("MRH_PR_BLOCKING");
+    const bool want = e && *e == '1';
+    if (want && !dist && dev.is_cuda() && nedge > 0 && nedge < (int64_t(1) << 31) && ngrp > 0)
+      build_blocking(vid_.index_select(0, segment_ids(seg_, ngrp, nedge)));
+  }
   at::Tensor deg_new = outdeg.index_select(0, order_);
   dangling_ = (deg_new == 0).to(at::kByte);
   invdeg_ = at::where(deg_new > 0, 1.0 / deg_new.clamp_min(1).to(at::kDouble), at::zeros_like(deg_new, at::kDouble))
                 .to(at::kFloat);
   ndangling = comm->allreduce(dangling_.sum().item<int64_t>(), Comm::SUM);
   acc_ = at::empty({nlocal}, opt(dev, at::kFloat));
-  if (ngrp > 0 && use_seg_index(dev)) six_ = seg_index(seg_, nedge);
+  if (ngrp > 0 && use_seg_index(dev) && !pb_) six_ = seg_index(seg_, nedge);
   reset();
+}
+
+// Static layout of the propagation-blocked iteration (pbpr.hip): phase-1
+// order = (source chunk of 2^18 sources, destination), phase-2 order = the
+// same edges stably re-sorted by destination bin of 2^14; work
+// units = bins cut into slices of <= 2^18 edges (hub bins get many slices).
+void PageRankPlan::build_blocking(const at::Tensor& dst_new) {
+  const int64_t m = nedge;
+  const int CS = 18, BS = 14;
+  if (k::pb_bin_size() != (1 << BS)) throw std::runtime_error("PageRank blocking: bin size mismatch");
+  int nb = 1;
+  while (nb < 32 && (int64_t(1) << nb) < nlocal) ++nb;
+  nb = std::max(nb, BS + 1);
+  const int cbits = std::max(nb - CS, 0), bbits = nb - BS;
+  // phase-1 key (source chunk, destination bin, source): a chunk's sources
+  // share a small window of c and a hub's out-edges into one bin are adjacent
+  // (broadcast gathers). Sorting each run by destination instead made the
+  // phase-2 atomics cheaper (5.4 -> 3.2 ms) but the gathers random (3.5 ->
+  // 9.0 ms) on RMAT-26.
+  at::Tensor s64 = src_.to(at::kLong), d64 = dst_new.to(at::kLong);
+  at::Tensor key1 = at::bitwise_or(
+      at::bitwise_or(at::bitwise_left_shift(at::bitwise_right_shift(s64, CS), (int64_t)(bbits + nb)),
+                     at::bitwise_left_shift(at::bitwise_right_shift(d64, BS), (int64_t)nb)),
+      s64);
+  s64 = d64 = at::Tensor();
+  auto [k1s, perm1] = sort_with_perm(key1, cbits + bbits + nb);
+  key1 = k1s = at::Tensor();
+  const at::Tensor p1 = perm1.to(at::kLong);
+  pb_src_ = src_.index_select(0, p1).contiguous();
+  at::Tensor dst1 = dst_new.index_select(0, p1).contiguous();
+  perm1 = at::Tensor();
+  at::Tensor bin1 = at::bitwise_right_shift(dst1.to(at::kLong), BS);
+  auto [bins, perm2] = sort_with_perm(bin1, std::max(bbits, 1));
+  bin1 = at::Tensor();
+  pb_out_ = at::empty({m}, opt(dev, at::kInt));
+  pb_dst_ = at::empty({m}, opt(dev, at::kShort));
+  k::pb_layout(perm2.data_ptr<int32_t>(), dst1.data_ptr<int32_t>(), m, pb_out_.data_ptr<int32_t>(),
+               reinterpret_cast<uint16_t*>(pb_dst_.data_ptr()), at::hip::getCurrentHIPStream());
+  perm2 = dst1 = at::Tensor();
+  // work units from the bin boundaries (one host copy of ~nlocal/2^14 entries)
+  at::Tensor bseg = segments(bins);
+  const int64_t nbin = bseg.numel() - 1;
+  std::vector<int64_t> hs = to_vec(bseg);
+  std::vector<int64_t> hb = to_vec(bins.index_select(0, bseg.narrow(0, 0, nbin)));
+  bins = at::Tensor();
+  constexpr int64_t SL = int64_t(1) << 18;
+  std::vector<int32_t> ub;
+  std::vector<int64_t> e0, e1;
+  std::vector<uint8_t> ex;
+  for (int64_t i = 0; i < nbin; ++i) {
+    const int64_t a = hs[i], b = hs[i + 1], ns = (b - a + SL - 1) / SL;
+    for (int64_t j = 0; j < ns; ++j) {
+      ub.push_back((int32_t)hb[i]);
+      e0.push_back(a + (b - a) * j / ns);
+      e1.push_back(a + (b - a) * (j + 1) / ns);
+      ex.push_back(ns == 1 ? 1 : 0);
+    }
+  }
+  pb_nunit_ = (int64_t)ub.size();
+  auto up = [&](const void* p, int64_t n, at::ScalarType t) {
+    return at::from_blob(const_cast<void*>(p), {n}, opt(at::kCPU, t)).clone().to(dev);
+  };
+  pb_ub_ = up(ub.data(), pb_nunit_, at::kInt);
+  pb_ue0_ = up(e0.data(), pb_nunit_, at::kLong);
+  pb_ue1_ = up(e1.data(), pb_nunit_, at::kLong);
+  pb_uex_ = up(ex.data(), pb_nunit_, at::kByte);
+  pb_vals_ = at::empty({m}, opt(dev, at::kFloat));
+  src_ = at::Tensor();  // the pull layout is not needed any more
+  pb_ = true;
 }
 
 void PageRankPlan::reset() {
@@ -297,10 +377,21 @@ void PageRankPlan::reset() {
 }
 
 void PageRankPlan::step() {
-  if (six_.defined()) seg_gather_reduce(six_, src_, c_, at::Tensor(), 0, send_);
-  else if (send_.numel()) pr_contrib(seg_, src_, w_, c_, send_);
-  acc_.zero_();
-  if (comm->distributed()) {
+  if (pb_) {
+    const hipStream_t s = at::hip::getCurrentHIPStream();
+    k::pb_phase1(pb_src_.data_ptr<int32_t>(), pb_out_.data_ptr<int32_t>(), nedge, c_.data_ptr<float>(),
+                 pb_vals_.data_ptr<float>(), s);
+    acc_.zero_();
+    k::pb_phase2(pb_vals_.data_ptr<float>(), reinterpret_cast<const uint16_t*>(pb_dst_.data_ptr()),
+                 pb_ub_.data_ptr<int32_t>(), pb_ue0_.data_ptr<int64_t>(), pb_ue1_.data_ptr<int64_t>(),
+                 pb_uex_.data_ptr<uint8_t>(), pb_nunit_, nlocal, acc_.data_ptr<float>(), s);
+  } else {
+    if (six_.defined()) seg_gather_reduce(six_, src_, c_, at::Tensor(), 0, send_);
+    else if (send_.numel()) pr_contrib(seg_, src_, w_, c_, send_);
+    acc_.zero_();
+  }
+  if (pb_) {
+  } else if (comm->distributed()) {
     at::Tensor recv = comm->alltoallv(send_, send_splits_, recv_splits_);
     if (recv.numel()) pr_combine(rseg_, rperm_, recv, rvid_, acc_);
   } else if (send_.numel()) {

@@ -93,6 +93,15 @@ class PageRankPlan {
   at::Tensor r_, rn_, c_, dmass_, stats_;
   SegIndex six_;
   std::vector<int64_t> send_splits_, recv_splits_;
+  // propagation blocking (one GPU; pbpr.hip): phase-1 sources and slots,
+  // phase-2 16-bit destinations, contributions, work units
+  void build_blocking(const at::Tensor& dst_new);
+  bool pb_ = false;
+  at::Tensor pb_src_, pb_out_, pb_dst_, pb_vals_, pb_ub_, pb_ue0_, pb_ue1_, pb_uex_;
+  int64_t pb_nunit_ = 0;
+
+ public:
+  bool blocking() const { return pb_; }
 };
 
 // Triangle finder on a degree-oriented CSR (tri.cpp kernels). Multi-rank jobs

@@ -196,6 +196,17 @@ void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_
 void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
             int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);
 
+// ---------------------------------------------------------------- pbpr.hip
+// propagation-blocked PageRank (graphplan.cpp PageRankPlan, one GPU)
+int pb_bin_size();  // destinations per bin (16-bit offsets)
+// vals[out_pos[j]] = c[src[j]] over the phase-1 order
+void pb_phase1(const int32_t* src, const int32_t* out_pos, int64_t m, const float* c, float* vals, hipStream_t s);
+// per unit (bin, [e0, e1)): LDS sums of vals by 16-bit destination -> acc
+void pb_phase2(const float* vals, const uint16_t* dst, const int32_t* ub, const int64_t* ue0, const int64_t* ue1,
+               const uint8_t* uex, int64_t nunit, int64_t nv, float* acc, hipStream_t s);
+// out_pos[perm2[k]] = k ; dst2[k] = dst1[perm2[k]] & (bin - 1)
+void pb_layout(const int32_t* perm2, const int32_t* dst1, int64_t m, int32_t* out_pos, uint16_t* dst2, hipStream_t s);
+
 // ---------------------------------------------------------------- tri.hip
 // triangle enumeration on a degree-oriented CSR (packed u64 edges lo<<32|hi)
 void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);

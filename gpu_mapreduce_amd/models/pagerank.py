@@ -66,6 +66,8 @@ class PageRank:
         self.nedge = self._p.nedge
         self.nlocal = self._p.nlocal
         self.ndangling = self._p.ndangling
+        # one GPU: propagation-blocked iteration (csrc/kernels/pbpr.hip)
+        self.blocking = self._p.blocking
         return self
 
     def reset(self):

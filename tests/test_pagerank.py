@@ -44,3 +44,46 @@ def test_pagerank_gpu_matches_numpy():
     edges, r = _run("cuda", scale=14, ef=16)
     ref = reference_pagerank(edges, 1 << 14, iters=15)
     np.testing.assert_allclose(r, ref, rtol=2e-4, atol=1e-9)
+
+
+PB_CHILD = r"""
+import sys, numpy as np, torch
+import gpu_mapreduce_amd as g
+from gpu_mapreduce_amd.models.pagerank import PageRank, rmat_map
+comm = g.Comm(device="cuda")
+mr = g.MapReduce(comm)
+rmat_map(mr, 20, 16, seed=3)
+edges = mr.kv.kdata.view(torch.int64).view(-1, 2).cpu().numpy().copy()
+pr = PageRank(mr, 1 << 20).build()
+pr.run(15)
+ids, r = pr.ranks()
+out = np.zeros(1 << 20)
+out[ids.cpu().numpy()] = r.cpu().numpy()
+np.save(sys.argv[1], out)
+if sys.argv[2] == "1":
+    from gpu_mapreduce_amd.models.pagerank import reference_pagerank
+    np.testing.assert_allclose(out, reference_pagerank(edges, 1 << 20, iters=15), rtol=2e-4, atol=1e-9)
+print(int(pr.blocking))
+"""
+
+
+@pytest.mark.gpu
+def test_pagerank_blocking_matches_pull_and_numpy(tmp_path):
+    """RMAT-20 (64 destination bins, hub bins split over several slices):
+    the propagation-blocked iteration and the pull iteration
+    (MRH_PR_BLOCKING=0, the default) agree with each other and with the
+    float64 oracle"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for flag in ("1", "0"):
+        env = dict(os.environ, MRH_PR_BLOCKING=flag, PYTHONPATH=root)  # "0" = the default pull path
+        path = str(tmp_path / f"r{flag}.npy")
+        p = subprocess.run([sys.executable, "-c", PB_CHILD, path, flag], env=env, cwd=root, capture_output=True,
+                           text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-2000:]
+        assert p.stdout.strip() == flag
+        res[flag] = np.load(path)
+    np.testing.assert_allclose(res["1"], res["0"], rtol=1e-4, atol=1e-10)
