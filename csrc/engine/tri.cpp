@@ -1,6 +1,7 @@
 // Triangle enumeration engine ops (kernels: csrc/kernels/tri.hip) with CPU
 // twins of identical semantics.
 #include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -98,17 +99,20 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
   return {rowptr, col, okeys, perm};
 }
 
-// hub bitmap size: MRH_TRI_HUB vertices (0 = off); default nvert / 64 capped
-// at 262144 (an 8 GB bitmap) — the best of a sweep on RMAT-24 (16.8 M
-// vertices): 0 / 32 K / 64 K / 128 K / 256 K / 384 K / 512 K hubs = 1566 /
-// 1332 / 999 / 867 / 673 / 812 / 811 ms (profiles/r2_trifind_hub_sweep.txt);
-// a multiple of 64, at most nvert
+// hub bitmap size: MRH_TRI_HUB vertices (0 = off); default nvert / 32 capped
+// at 524288 (a 32 GB bitmap) and at a quarter of the free HBM — the best of
+// a sweep on RMAT-24 (16.8 M vertices) with sparse-row lists: 128 K / 256 K /
+// 384 K / 512 K hubs = 862 / 649 / 661 / 606 ms, 1566 ms without hubs
+// (profiles/r2_trifind_hub_sweep.txt); a multiple of 64, at most nvert
 int64_t tri_hub_size(int64_t nvert) {
   static const int64_t env = [] {
     const char* e = std::getenv("MRH_TRI_HUB");
     return e ? std::atoll(e) : int64_t(-1);
   }();
-  const int64_t want = env >= 0 ? env : std::min<int64_t>(nvert / 64, 262144);
+  int64_t want = env >= 0 ? env : std::min<int64_t>(nvert / 32, 524288);
+  size_t free_b = 0, total_b = 0;
+  if (env < 0 && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+    while (want > 64 && (size_t)want * (size_t)want / 8 > free_b / 4) want /= 2;
   int64_t K = std::min<int64_t>(std::max<int64_t>(want, 0), 524288);
   K = std::min<int64_t>(K, nvert) / 64 * 64;
   return K;

@@ -12,7 +12,7 @@ namespace mrh {
 // (int64 [nvert], perm[rank] = original id).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq, int64_t nvert);
 // vertices of the hub bitmap path of tri_count (MRH_TRI_HUB, default
-// nvert/64 up to 262144; 0 = hash kernels only)
+// nvert/32 up to 524288 and a quarter of free HBM; 0 = hash kernels only)
 int64_t tri_hub_size(int64_t nvert);
 // number of triangles whose first oriented edge lies in [e0, e1)
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1);

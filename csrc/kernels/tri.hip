@@ -338,24 +338,57 @@ __global__ __launch_bounds__(NT) void k_tri_hub_build(const int64_t* __restrict_
 // keeps HUB_WPT words of H[u] in registers and ANDs them with the same words
 // of H[v] for every v in N+(u) (coalesced row reads, words below v skipped)
 constexpr int HUB_NT = 256;
+constexpr int HUB_LIST = 2048;   // LDS list of a sparse hub row's non-zero words (24 KB)
+constexpr int HUB_SPARSE = 8;    // sparse when fewer than W / 8 words are non-zero
 template <int WPT>
 __global__ __launch_bounds__(HUB_NT) void k_tri_hub_count(const int64_t* __restrict__ rowptr,
                                                          const uint32_t* __restrict__ col, int64_t hb, int64_t K,
                                                          int64_t r0, int64_t r1,
                                                          const unsigned long long* __restrict__ H,
                                                          unsigned long long* __restrict__ total) {
+  __shared__ int s_scan[HUB_NT / MRH_WAVE + 1];
+  __shared__ int32_t s_idx[HUB_LIST];
+  __shared__ unsigned long long s_val[HUB_LIST];
   const int64_t W = K / 64;
   uint64_t cnt = 0;
   for (int64_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
     const int64_t u = hb + r;
     const int64_t a = rowptr[u], b = rowptr[u + 1];
-    if (b - a < 2) continue;
+    if (b - a < 2) continue;  // uniform over the block: no barrier is skipped unevenly
     const unsigned long long* hu = H + r * W;
     unsigned long long mine[WPT];
 #pragma unroll
     for (int j = 0; j < WPT; ++j) {
       const int64_t w = threadIdx.x + (int64_t)j * HUB_NT;
       mine[j] = w < W ? hu[w] : 0ull;
+    }
+    // sparse rows (the lower hubs: few of W words set) compact their
+    // non-zero words into LDS and AND only those against each H[v]: d+(u) x
+    // nnz word loads instead of d+(u) x W
+    int nz = 0;
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) nz += mine[j] != 0ull;
+    int total_nz;
+    const int base = dev::block_excl_scan<int, HUB_NT>(nz, s_scan, &total_nz);
+    if ((int64_t)total_nz * HUB_SPARSE < W && total_nz <= HUB_LIST) {
+      int o = base;
+#pragma unroll
+      for (int j = 0; j < WPT; ++j)
+        if (mine[j]) {
+          s_idx[o] = (int32_t)(threadIdx.x + j * HUB_NT);
+          s_val[o] = mine[j];
+          ++o;
+        }
+      __syncthreads();
+      const int64_t work = (b - a) * total_nz;
+      for (int64_t t = threadIdx.x; t < work; t += HUB_NT) {
+        const int64_t e = a + t / total_nz;
+        const int li = (int)(t % total_nz);
+        const int64_t vr = (int64_t)col[e] - hb, w = s_idx[li];
+        if (w >= (vr >> 6)) cnt += __popcll(s_val[li] & H[vr * W + w]);
+      }
+      __syncthreads();
+      continue;
     }
     for (int64_t e = a; e < b; ++e) {
       const int64_t vr = (int64_t)col[e] - hb;

@@ -127,14 +127,14 @@ print(C.tri_hub_size(gpu.nvert), gpu.count())
 @pytest.mark.gpu
 def test_gpu_hub_bitmap_split_matches_cpu():
     """the same RMAT-17 count with the hub bitmap path off (hash kernels
-    only), on the default (nvert/64 ~ 2048 hubs), 4096 hubs, and 65536 (half
+    only), on the default (nvert/32 ~ 4096 hubs), 4096 hubs, and 65536 (half
     of the graph in bitmaps) — each must equal the CPU merge count"""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     want = TriangleGraph(Comm(device="cpu"), _rmat(17, 16, 3)).count()
-    for hub, K in (("0", 0), (None, 2048), ("4096", 4096), ("65536", 65536)):
+    for hub, K in (("0", 0), (None, 4096), ("4096", 4096), ("65536", 65536)):
         env = dict(os.environ, PYTHONPATH=root)
         env.pop("MRH_TRI_HUB", None)
         if hub is not None:
