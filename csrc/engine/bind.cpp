@@ -619,6 +619,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tri_prepare", &mrh::tri_prepare);
   m.def("tri_count", &mrh::tri_count);
   m.def("tri_hub_size", &mrh::tri_hub_size);
+  m.def("tri_last_hub_size", &mrh::tri_last_hub_size);
   m.def("tri_list", &mrh::tri_list);
   m.def("kv_iter", &kv_iter);
   m.def("kmv_iter", &kmv_iter);

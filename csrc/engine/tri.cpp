@@ -1,6 +1,7 @@
 // Triangle enumeration engine ops (kernels: csrc/kernels/tri.hip) with CPU
 // twins of identical semantics.
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -104,6 +105,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
 // a sweep on RMAT-24 (16.8 M vertices) with sparse-row lists: 128 K / 256 K /
 // 384 K / 512 K hubs = 862 / 649 / 661 / 606 ms, 1566 ms without hubs
 // (profiles/r2_trifind_hub_sweep.txt); a multiple of 64, at most nvert
+static int64_t g_last_hub = 0;
+int64_t tri_last_hub_size() { return g_last_hub; }
+
 int64_t tri_hub_size(int64_t nvert) {
   static const int64_t env = [] {
     const char* e = std::getenv("MRH_TRI_HUB");
@@ -111,8 +115,13 @@ int64_t tri_hub_size(int64_t nvert) {
   }();
   int64_t want = env >= 0 ? env : std::min<int64_t>(nvert / 32, 524288);
   size_t free_b = 0, total_b = 0;
-  if (env < 0 && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+  if (env < 0 && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
+    if ((size_t)want * (size_t)want / 8 > free_b / 4) {  // blocks cached by the allocator count as free
+      c10::hip::HIPCachingAllocator::emptyCache();
+      (void)hipMemGetInfo(&free_b, &total_b);
+    }
     while (want > 64 && (size_t)want * (size_t)want / 8 > free_b / 4) want /= 2;
+  }
   int64_t K = std::min<int64_t>(std::max<int64_t>(want, 0), 524288);
   K = std::min<int64_t>(K, nvert) / 64 * 64;
   return K;
@@ -130,6 +139,7 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
     at::Tensor tot = at::zeros({1}, opt(okeys.device(), at::kLong));
     // the top-K ranks (hubs) go to the bitmap kernel, the rest to the hash kernels
     const int64_t K = tri_hub_size(nvert);
+    g_last_hub = K;
     const int64_t hb = nvert - K;
     const int64_t uh = K ? std::max(u0, std::min(u1, hb)) : u1;
     if (K && u1 > hb) {

@@ -14,6 +14,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
 // vertices of the hub bitmap path of tri_count (MRH_TRI_HUB, default
 // nvert/32 up to 524288 and a quarter of free HBM; 0 = hash kernels only)
 int64_t tri_hub_size(int64_t nvert);
+// hub vertices the last tri_count on this process used
+int64_t tri_last_hub_size();
 // number of triangles whose first oriented edge lies in [e0, e1)
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1);
 // number of triangles u < v < w (in the CSR's id order) over the rows u in

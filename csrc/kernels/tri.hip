@@ -26,12 +26,27 @@ namespace {
 
 constexpr int NT = 256;
 
+// the edges are sorted by their low endpoint: a wave counts each run of equal
+// low endpoints with one atomic (R-MAT hubs would otherwise serialise 64
+// lanes on one address); the high endpoints are scattered, one atomic each
 __global__ __launch_bounds__(NT) void k_tri_degree(const uint64_t* __restrict__ e, int64_t m,
                                                   uint32_t* __restrict__ deg) {
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (int64_t)gridDim.x * NT) {
-    const uint64_t x = e[i];
-    atomicAdd(deg + (uint32_t)(x >> 32), 1u);
-    atomicAdd(deg + (uint32_t)x, 1u);
+  const int lane = dev::lane_id();
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t base = (int64_t)blockIdx.x * NT + (threadIdx.x & ~(MRH_WAVE - 1)); base < m; base += stride) {
+    const int64_t i = base + lane;
+    const bool ok = i < m;
+    const uint64_t x = ok ? e[i] : ~0ull;
+    const uint32_t lo = (uint32_t)(x >> 32);
+    const uint32_t prev = __shfl_up(lo, 1, MRH_WAVE);
+    const uint64_t heads = __ballot(ok && (lane == 0 || lo != prev));
+    const uint64_t okm = __ballot(ok);
+    if (ok && ((heads >> lane) & 1ull)) {
+      const uint64_t above = heads & ~((2ull << lane) - 1ull);  // heads after this lane
+      const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll(okm);
+      atomicAdd(deg + lo, (uint32_t)(end - lane));
+    }
+    if (ok) atomicAdd(deg + (uint32_t)x, 1u);
   }
 }
 

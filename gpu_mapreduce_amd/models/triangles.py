@@ -103,4 +103,5 @@ def bench_trifind(comm, args):
         "config": {"model": "tri_find", "global_batch": ntotal, "seq_len": 1, "parallelism": f"dp{P}",
                    "scale": scale, "edgefactor": ef, "rmat": "graph500 a=.57 b=c=.19"},
         "triangles": ntri, "unique_edges": g.nedge, "scaling": "strong",
+        "hub_vertices": int(C.tri_last_hub_size()),
     }

@@ -42,7 +42,9 @@ class WordFreq:
         self.is_cuda = mr.device.startswith("cuda")
         maxlen = max((t.numel() for t in chunks), default=0)
         self.bufs = [pools.device_buffer(mr.device, maxlen + PAD, 8 + s) for s in range(2 if chunks else 0)]
-        self.copy_stream = torch.cuda.Stream() if self.is_cuda else None
+        # the process's persistent H2D stream (a new stream per job would be
+        # a new HIP queue each time)
+        self.copy_stream = pools.stream(mr.device, "h2d") if self.is_cuda else None
 
     def _map(self, itask, kv):
         self.local_words = 0
@@ -71,13 +73,14 @@ class WordFreq:
         main = torch.cuda.current_stream()
         cs = self.copy_stream
         ready = [torch.cuda.Event(), torch.cuda.Event()]
-        free = [torch.cuda.Event(), torch.cuda.Event()]
+        dev = self.mr.device
 
         def issue(i):
             b = i & 1
             with torch.cuda.stream(cs):
-                if i >= 2:
-                    cs.wait_event(free[b])
+                prev = pools.last_use(dev, 8 + b)  # the last kernel (any job) that read this buffer
+                if prev is not None:
+                    cs.wait_event(prev)
                 self.bufs[b][: self.chunks[i].numel()].copy_(self.chunks[i], non_blocking=True)
                 ready[b].record(cs)
 
@@ -88,7 +91,7 @@ class WordFreq:
             b = i & 1
             main.wait_event(ready[b])
             consume(self.bufs[b], self.chunks[i].numel())
-            free[b].record(main)
+            pools.mark_use(dev, 8 + b, main)
 
     def run(self):
         mr = self.mr

@@ -234,3 +234,30 @@ def test_gather_var_and_expand():
     kc, _ = C.convert(kv)
     kg, _ = C.convert(kv.to(DEV))
     assert _kv_rows(C.expand(kg)) == _kv_rows(C.expand(kc))
+
+
+def test_inverted_index_bench_scale_gpu():
+    """bench shape (128 MiB part files, the bench's URL density), 512 MiB:
+    the pipelined + grouped InvertedIndex output equals the Python oracle,
+    and a second job on the same files gives the same bytes (deterministic
+    order of keys and of each key's files)"""
+    import gpu_mapreduce_amd as g
+    from gpu_mapreduce_amd.models.inverted_index import InvertedIndex, reference_inverted_index
+    from gpu_mapreduce_amd.utils import synth
+    files = synth.html_corpus(512 << 20, file_bytes=128 << 20, seed=1, device=DEV, link_gap=200)
+    files = [(n, t.cpu().pin_memory()) for n, t in files]
+    comm = g.Comm(device="cuda")
+    outs = []
+    for _ in range(2):
+        mr = g.MapReduce(comm)
+        app = InvertedIndex(mr, files)
+        app.run()
+        assert mr.last_convert.grouped == 1
+        app.output_ready()
+        outs.append(bytes(app.output.numpy()))
+    assert outs[0] == outs[1]
+    got = {}
+    for line in outs[0].decode("utf-8", "replace").splitlines():
+        url, rest = line.split("\t")
+        got[url.encode()] = sorted(rest.split())
+    assert got == reference_inverted_index(files)
