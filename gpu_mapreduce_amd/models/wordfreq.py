@@ -41,7 +41,10 @@ class WordFreq:
         self.combiner = combiner
         self.is_cuda = mr.device.startswith("cuda")
         maxlen = max((t.numel() for t in chunks), default=0)
-        self.bufs = [pools.device_buffer(mr.device, maxlen + PAD, 8 + s) for s in range(2 if chunks else 0)]
+        # staging ring depth (MRH_WF_BUFS, default 2)
+        import os
+        self.nbuf = max(2, int(os.environ.get("MRH_WF_BUFS", "2")))
+        self.bufs = [pools.device_buffer(mr.device, maxlen + PAD, 8 + s) for s in range(self.nbuf if chunks else 0)]
         # the process's persistent H2D stream (a new stream per job would be
         # a new HIP queue each time)
         self.copy_stream = pools.stream(mr.device, "h2d") if self.is_cuda else None
@@ -72,11 +75,12 @@ class WordFreq:
     def _stream_chunks(self, consume):
         main = torch.cuda.current_stream()
         cs = self.copy_stream
-        ready = [torch.cuda.Event(), torch.cuda.Event()]
+        nb = self.nbuf
+        ready = [torch.cuda.Event() for _ in range(nb)]
         dev = self.mr.device
 
         def issue(i):
-            b = i & 1
+            b = i % nb
             with torch.cuda.stream(cs):
                 prev = pools.last_use(dev, 8 + b)  # the last kernel (any job) that read this buffer
                 if prev is not None:
@@ -84,11 +88,12 @@ class WordFreq:
                 self.bufs[b][: self.chunks[i].numel()].copy_(self.chunks[i], non_blocking=True)
                 ready[b].record(cs)
 
-        issue(0)
+        for i in range(min(nb - 1, len(self.chunks))):
+            issue(i)
         for i in range(len(self.chunks)):
-            if i + 1 < len(self.chunks):
-                issue(i + 1)
-            b = i & 1
+            if i + nb - 1 < len(self.chunks):
+                issue(i + nb - 1)
+            b = i % nb
             main.wait_event(ready[b])
             consume(self.bufs[b], self.chunks[i].numel())
             pools.mark_use(dev, 8 + b, main)
