@@ -41,9 +41,12 @@ class WordFreq:
         self.combiner = combiner
         self.is_cuda = mr.device.startswith("cuda")
         maxlen = max((t.numel() for t in chunks), default=0)
-        # staging ring depth (MRH_WF_BUFS, default 2)
+        # staging ring depth (MRH_WF_BUFS): 3 by default — with two buffers the
+        # copy of chunk i+2 waits for the count kernel of chunk i; 1 GiB step
+        # 29.0 / 24.5 / 25.3 ms with 2 / 3 / 4 buffers on one MI355X
+        # (profiles/r2_wordfreq_ring.txt)
         import os
-        self.nbuf = max(2, int(os.environ.get("MRH_WF_BUFS", "2")))
+        self.nbuf = max(2, int(os.environ.get("MRH_WF_BUFS", "3")))
         self.bufs = [pools.device_buffer(mr.device, maxlen + PAD, 8 + s) for s in range(self.nbuf if chunks else 0)]
         # the process's persistent H2D stream (a new stream per job would be
         # a new HIP queue each time)
