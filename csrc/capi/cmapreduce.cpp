@@ -272,6 +272,10 @@ void MR_set_zeropage(void* p, int v) { M(p)->set.zeropage = v; }
 void MR_set_keyalign(void* p, int v) { M(p)->set.keyalign = v; }
 void MR_set_valuealign(void* p, int v) { M(p)->set.valuealign = v; }
 void MR_set_fpath(void* p, char* s) { M(p)->set_fpath(s ? s : "."); }
+void MR_set_chunk_bytes(void* p, int64_t v) { M(p)->set.chunk_bytes = v; }
+void MR_set_hbm_budget(void* p, int64_t v) { M(p)->set.hbm_budget = v; }
+void MR_set_host_budget(void* p, int64_t v) { M(p)->set.host_budget = v; }
+void MR_set_pipeline(void* p, int v) { M(p)->set.pipeline = v; }
 
 void MR_kv_add(void* kv, char* k, int kb, char* v, int vb) { static_cast<KeyValue*>(kv)->add(k, kb, v, vb); }
 void MR_kv_add_multi_static(void* kv, int n, char* k, int kb, char* v, int vb) {

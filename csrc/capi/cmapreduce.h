@@ -114,6 +114,13 @@ void MR_set_zeropage(void *MRptr, int value);
 void MR_set_keyalign(void *MRptr, int value);
 void MR_set_valuealign(void *MRptr, int value);
 void MR_set_fpath(void *MRptr, char *str);
+/* MI355X-native settings (not in the reference): shuffle receive cap per
+ * round in bytes, HBM budget of the MR's data (out-of-core beyond it), pinned
+ * host bytes before the spill tier writes to disk, pipelined collate (1/0) */
+void MR_set_chunk_bytes(void *MRptr, int64_t value);
+void MR_set_hbm_budget(void *MRptr, int64_t value);
+void MR_set_host_budget(void *MRptr, int64_t value);
+void MR_set_pipeline(void *MRptr, int value);
 
 void MR_kv_add(void *KVptr, char *key, int keybytes, char *value, int valuebytes);
 void MR_kv_add_multi_static(void *KVptr, int n, char *key, int keybytes, char *value, int valuebytes);

@@ -220,6 +220,12 @@ void run_mr_method(Oink& o, int index, const Args& args) {
     else if (k == "zeropage") s.zeropage = ival(v);
     else if (k == "keyalign") s.keyalign = ival(v);
     else if (k == "valuealign") s.valuealign = ival(v);
+    // MI355X-native settings (mapreduce.h)
+    else if (k == "chunk_bytes") s.chunk_bytes = (int64_t)std::stoll(v);
+    else if (k == "hbm_budget") s.hbm_budget = (int64_t)std::stoll(v);
+    else if (k == "host_budget") s.host_budget = (int64_t)std::stoll(v);
+    else if (k == "streams") s.streams = ival(v);
+    else if (k == "pipeline") s.pipeline = ival(v);
     else throw Error("Illegal MR object set command");
   } else {
     throw Error("Illegal MR object command");

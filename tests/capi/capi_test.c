@@ -156,6 +156,9 @@ int main(int argc, char **argv) {
 
   /* built-in device reducers */
   void *c = MR_create(NULL);
+  MR_set_chunk_bytes(c, 4096); /* MI355X settings: tiny shuffle rounds, pipelined collate */
+  MR_set_pipeline(c, 1);
+  MR_set_hbm_budget(c, 0);
   MR_map(c, 4, gen, &n);
   CHECK(MR_collate(c, NULL) == 7);
   CHECK(MR_reduce_builtin(c, "count", "int32") == 7);
