@@ -142,16 +142,18 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
     g_last_hub = K;
     const int64_t hb = nvert - K;
     const int64_t uh = K ? std::max(u0, std::min(u1, hb)) : u1;
-    if (K && u1 > hb) {
-      at::Tensor H = at::empty({K * (K / 64)}, opt(okeys.device(), at::kLong));
-      k::tri_hub_count(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, std::max(u0, hb), u1, P0<uint64_t>(H),
-                       P0<unsigned long long>(tot), cur());
+    at::Tensor H;
+    if (K) {
+      // the bitmaps serve both the hub kernel and the hub probes of the hash kernels
+      H = at::empty({K * (K / 64)}, opt(okeys.device(), at::kLong));
+      k::tri_hub_count(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, std::max(u0, hb), std::max(u1, hb),
+                       P0<uint64_t>(H), P0<unsigned long long>(tot), cur());
     }
     if (uh > u0) {
       at::Tensor big = at::empty({2 * std::max<int64_t>(uh - u0, 1)}, opt(okeys.device(), at::kInt));
       at::Tensor nbig = at::zeros({2}, opt(okeys.device(), at::kInt));
       k::tri_count_hash(P0<int64_t>(rowptr), P0<uint32_t>(col), u0, uh, P0<uint32_t>(big), P0<uint32_t>(nbig),
-                        P0<unsigned long long>(tot), cur());
+                        P0<unsigned long long>(tot), cur(), K ? P0<uint64_t>(H) : nullptr, hb, K);
     }
     return tot.item<int64_t>();
   }

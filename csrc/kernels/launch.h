@@ -216,8 +216,11 @@ void tri_orient(const uint64_t* e, int64_t m, const uint32_t* rank, uint64_t* ou
 void tri_count(const int64_t* rowptr, const uint32_t* col, const uint64_t* okeys, int64_t e0, int64_t e1,
                uint32_t* cnt, unsigned long long* total, hipStream_t s);
 // vertex-centric LDS-hash count over vertices [u0,u1); big: scratch u32[2*(u1-u0)], nbig: zeroed u32[2]
+// H/hb/K: hub bitmaps built by tri_hub_count (H null: none) — probes of a hub
+// neighbour test bits of its row instead of walking its adjacency list
 void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int64_t u1, uint32_t* big,
-                    uint32_t* nbig, unsigned long long* total, hipStream_t s);
+                    uint32_t* nbig, unsigned long long* total, hipStream_t s, const uint64_t* H = nullptr,
+                    int64_t hb = 0, int64_t K = 0);
 // triangles whose lowest vertex is a hub (rank >= hb = nvert - K) among the
 // vertices [u0, u1), by AND/popcount of hub adjacency bitmaps; H: scratch of
 // K * K / 8 bytes (K a multiple of 64, <= 524288)

@@ -206,26 +206,44 @@ __device__ __forceinline__ bool tab_has(const uint32_t* tab, uint32_t mask, uint
   }
 }
 
+// hub bitmaps for the probe walk (k_tri_hub_count's H; H == null: none)
+struct Hubs {
+  const unsigned long long* H;
+  int64_t hb, W;
+};
+
 // one wave walks the v's of N+(u) in chunks of 64: returns the number of w ∈ N+(v) found in tab
 // rows hold rank ids in increasing order, so only the prefix of N+(v) up to
-// max N+(u) can match: cut each row there (binary search) before probing
+// max N+(u) can match: cut each row there (binary search) before probing.
+// A hub v (rank >= hb) has its out-neighbours in bitmap row H[v]: instead of
+// walking N+(v) (long for hubs) the wave tests the elements of N+(u) after v
+// (all hubs, since they rank above v) against that row — |N+(u)| - pos(v) - 1
+// bit tests
 __device__ __forceinline__ uint64_t probe_chunks(const int64_t* __restrict__ rowptr, const uint32_t* __restrict__ col,
                                                  int64_t c0, int64_t b, int64_t cstep, const uint32_t* tab,
-                                                 uint32_t mask, uint32_t maxu, int64_t* pre, int64_t* st) {
+                                                 uint32_t mask, uint32_t maxu, int64_t* pre, int64_t* st,
+                                                 int64_t* hv, const Hubs& hubs) {
   const int l = dev::lane_id();
   uint64_t cnt = 0;
   for (int64_t c = c0; c < b; c += cstep) {
-    int64_t len = 0, vs = 0;
+    int64_t len = 0, vs = 0, hrow = -1;
     if (c + l < b) {
       const uint32_t v = col[c + l];
-      vs = rowptr[v];
-      len = lower_bound(col, vs, rowptr[v + 1], maxu + 1u) - vs;
+      if (hubs.H && (int64_t)v >= hubs.hb) {
+        hrow = ((int64_t)v - hubs.hb) * hubs.W;
+        vs = c + l + 1;  // the rest of N+(u): hubs above v
+        len = b - vs;
+      } else {
+        vs = rowptr[v];
+        len = lower_bound(col, vs, rowptr[v + 1], maxu + 1u) - vs;
+      }
     }
     const int64_t inc = dev::wave_incl_scan(len);
     const int64_t tot = __shfl(inc, MRH_WAVE - 1, MRH_WAVE);
     pre[l + 1] = inc;
     if (l == 0) pre[0] = 0;
     st[l] = vs;
+    hv[l] = hrow;
     wave_sync();
     // lane l takes flat items l, l+64, ...: its owning v only moves forward, so
     // a short monotone walk replaces a binary search; two items per trip keep
@@ -234,14 +252,29 @@ __device__ __forceinline__ uint64_t probe_chunks(const int64_t* __restrict__ row
     for (int64_t t = l; t < tot; t += 2 * MRH_WAVE) {
       while (pre[j + 1] <= t) ++j;
       const uint32_t x0 = col[st[j] + (t - pre[j])];
+      const int64_t h0 = hv[j];
       const int64_t t1 = t + MRH_WAVE;
       uint32_t x1 = EMPTY;
+      int64_t h1 = -1;
       if (t1 < tot) {
         while (pre[j + 1] <= t1) ++j;
         x1 = col[st[j] + (t1 - pre[j])];
+        h1 = hv[j];
       }
-      cnt += tab_has(tab, mask, x0) ? 1u : 0u;
-      if (x1 != EMPTY) cnt += tab_has(tab, mask, x1) ? 1u : 0u;
+      if (h0 >= 0) {
+        const int64_t bit = (int64_t)x0 - hubs.hb;
+        cnt += (hubs.H[h0 + (bit >> 6)] >> (bit & 63)) & 1ull;
+      } else {
+        cnt += tab_has(tab, mask, x0) ? 1u : 0u;
+      }
+      if (x1 != EMPTY) {
+        if (h1 >= 0) {
+          const int64_t bit = (int64_t)x1 - hubs.hb;
+          cnt += (hubs.H[h1 + (bit >> 6)] >> (bit & 63)) & 1ull;
+        } else {
+          cnt += tab_has(tab, mask, x1) ? 1u : 0u;
+        }
+      }
     }
     wave_sync();
   }
@@ -259,10 +292,11 @@ __global__ __launch_bounds__(NT) void k_tri_hash_wave(const int64_t* __restrict_
                                                      const uint32_t* __restrict__ list,
                                                      const uint32_t* __restrict__ nlist,
                                                      uint32_t* __restrict__ next, uint32_t* __restrict__ nnext,
-                                                     unsigned long long* __restrict__ total) {
+                                                     unsigned long long* __restrict__ total, Hubs hubs) {
   __shared__ uint32_t tab[HASH_NW][TWN];
   __shared__ int64_t pre[HASH_NW][MRH_WAVE + 1];
   __shared__ int64_t st[HASH_NW][MRH_WAVE];
+  __shared__ int64_t hv[HASH_NW][MRH_WAVE];
   const int w = dev::wave_id(), l = dev::lane_id();
   uint64_t cnt = 0;
   const int64_t nw = (int64_t)gridDim.x * HASH_NW;
@@ -282,7 +316,7 @@ __global__ __launch_bounds__(NT) void k_tri_hash_wave(const int64_t* __restrict_
     wave_sync();
     for (int64_t i = a + l; i < b; i += MRH_WAVE) tab_insert(tab[w], mask, col[i]);
     wave_sync();
-    cnt += probe_chunks(rowptr, col, a, b, MRH_WAVE, tab[w], mask, col[b - 1], pre[w], st[w]);
+    cnt += probe_chunks(rowptr, col, a, b, MRH_WAVE, tab[w], mask, col[b - 1], pre[w], st[w], hv[w], hubs);
   }
   cnt = dev::wave_sum(cnt);
   if (l == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
@@ -293,10 +327,11 @@ __global__ __launch_bounds__(BIG_NT) void k_tri_hash_big(const int64_t* __restri
                                                         const uint32_t* __restrict__ col,
                                                         const uint32_t* __restrict__ big,
                                                         const uint32_t* __restrict__ nbig,
-                                                        unsigned long long* __restrict__ total) {
+                                                        unsigned long long* __restrict__ total, Hubs hubs) {
   __shared__ uint32_t tab[BIG_TAB];
   __shared__ int64_t pre[BIG_NT / MRH_WAVE][MRH_WAVE + 1];
   __shared__ int64_t st[BIG_NT / MRH_WAVE][MRH_WAVE];
+  __shared__ int64_t hv[BIG_NT / MRH_WAVE][MRH_WAVE];
   const int w = dev::wave_id(), l = dev::lane_id();
   const uint32_t n = *nbig;
   uint64_t cnt = 0;
@@ -318,7 +353,7 @@ __global__ __launch_bounds__(BIG_NT) void k_tri_hash_big(const int64_t* __restri
     for (int64_t j = a + threadIdx.x; j < b; j += BIG_NT) tab_insert(tab, mask, col[j]);
     __syncthreads();
     cnt += probe_chunks(rowptr, col, a + (int64_t)w * MRH_WAVE, b, (int64_t)BIG_NT, tab, mask, col[b - 1], pre[w],
-                        st[w]);
+                        st[w], hv[w], hubs);
     __syncthreads();
   }
   cnt = dev::wave_sum(cnt);
@@ -464,7 +499,9 @@ void tri_count(const int64_t* rowptr, const uint32_t* col, const uint64_t* okeys
 }
 
 void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int64_t u1, uint32_t* big,
-                    uint32_t* nbig, unsigned long long* total, hipStream_t s) {
+                    uint32_t* nbig, unsigned long long* total, hipStream_t s, const uint64_t* H, int64_t hb,
+                    int64_t K) {
+  const Hubs hubs{(const unsigned long long*)H, hb, K / 64};
   if (u1 <= u0) return;
   // scratch: big = [mid list | big list] each u1-u0 entries; nbig = [nmid, nbig]
   const int64_t nv = u1 - u0;
@@ -473,12 +510,12 @@ void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int6
   int64_t blocks = (nv + HASH_NW - 1) / HASH_NW;
   if (blocks > 16384) blocks = 16384;  // waves grid-stride over the vertices
   hipLaunchKernelGGL(k_tri_hash_wave<256>, dim3((unsigned)blocks), dim3(NT), 0, s, rowptr, col, u0, u1,
-                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, mid, nbig, total);
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, mid, nbig, total, hubs);
   MRH_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_tri_hash_wave<TW>, dim3(2048), dim3(NT), 0, s, rowptr, col, u0, u1, (const uint32_t*)mid,
-                     (const uint32_t*)nbig, bigl, nbig + 1, total);
+                     (const uint32_t*)nbig, bigl, nbig + 1, total, hubs);
   MRH_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_tri_hash_big, dim3(512), dim3(BIG_NT), 0, s, rowptr, col, bigl, nbig + 1, total);
+  hipLaunchKernelGGL(k_tri_hash_big, dim3(512), dim3(BIG_NT), 0, s, rowptr, col, bigl, nbig + 1, total, hubs);
   MRH_CHECK_LAUNCH();
 }
 
@@ -486,11 +523,12 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
                    uint64_t* H, unsigned long long* total, hipStream_t s) {
   check_arg(K > 0 && K % 64 == 0 && K <= HUB_NT * 64 * 32, "tri_hub_count: K must be a multiple of 64, <= 524288");
   const int64_t r0 = std::max<int64_t>(u0 - hb, 0), r1 = std::min<int64_t>(u1 - hb, K);
-  if (r1 <= r0) return;
+  // the bitmaps are always built: the hash kernels' hub probes read them too
   (void)hipMemsetAsync(H, 0, (size_t)K * (K / 64) * 8, s);
   hipLaunchKernelGGL(k_tri_hub_build, dim3((unsigned)std::min<int64_t>((K + HASH_NW - 1) / HASH_NW, 16384)), dim3(NT),
                      0, s, rowptr, col, hb, K, (unsigned long long*)H);
   MRH_CHECK_LAUNCH();
+  if (r1 <= r0) return;
   const int64_t W = K / 64;
   const unsigned grid = (unsigned)std::min<int64_t>(r1 - r0, 65536);
   const unsigned long long* Hc = (const unsigned long long*)H;
