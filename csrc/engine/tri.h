@@ -24,4 +24,18 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
 int64_t tri_count_rows(const at::Tensor& rowptr, const at::Tensor& col, int64_t u0, int64_t u1);
 // the triangles found on oriented edges [e0, e1) as [T,3] int64 rank ids
 at::Tensor tri_list(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1);
+
+// tri_find_mr callbacks (trimr.cpp; oink/tri_find.cpp:104-325)
+struct KV;
+struct KMV;
+// vertex -> neighbours KMV: per value, the edge (min, max) [nval,2] int64 and
+// {deg, 0} / {0, deg} [nval,2] int32 (deg in the key vertex's slot)
+std::pair<at::Tensor, at::Tensor> trimr_first_degree(const KMV& m);
+// edge -> its two degree records: {di, dj} per edge, [nkey,2] int32
+at::Tensor trimr_second_degree(const KMV& m);
+// KV(edge, {di, dj}) -> (lower-degree end, other end), int64 each
+std::pair<at::Tensor, at::Tensor> trimr_low_degree(const KV& kv);
+// edge -> {wedge centres (8 B), edge marker (0 B)}: closed triangles
+// (centre, e0, e1) as [T,3] int64
+at::Tensor trimr_emit(const KMV& m);
 }  // namespace mrh

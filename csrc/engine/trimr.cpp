@@ -1,0 +1,134 @@
+// tri_find_mr callback ops (kernels: csrc/kernels/trimr.hip) with CPU twins
+// of identical semantics. The OINK command tri_find_mr (commands.cpp) runs
+// the reference's 4-shuffle pipeline (oink/tri_find.cpp:43-82) with these
+// as its batch map/reduce callbacks.
+#include <ATen/hip/HIPContext.h>
+
+#include <cstring>
+#include <stdexcept>
+
+#include "../kernels/launch.h"
+#include "kv.h"
+#include "tri.h"
+
+namespace mrh {
+
+namespace {
+at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
+template <typename T>
+T* P0(const at::Tensor& t) {
+  return t.defined() ? reinterpret_cast<T*>(t.data_ptr()) : nullptr;
+}
+hipStream_t cur() { return at::hip::getCurrentHIPStream(); }
+void need(bool c, const char* m) {
+  if (!c) throw std::runtime_error(std::string("mrhip: ") + m);
+}
+}  // namespace
+
+std::pair<at::Tensor, at::Tensor> trimr_first_degree(const KMV& m) {
+  need(m.vw == 8 && m.keys.kw == 8, "tri_find_mr first degree: 8-byte vertex keys and values");
+  const at::Device dev = m.seg.device();
+  at::Tensor edge = at::empty({m.nval, 2}, opt(dev, at::kLong)), deg = at::empty({m.nval, 2}, opt(dev, at::kInt));
+  if (!m.nval) return {edge, deg};
+  const int64_t* seg = P0<int64_t>(m.seg);
+  const int64_t* key = P0<int64_t>(m.keys.kdata);
+  const int64_t* nbr = P0<int64_t>(m.vdata);
+  if (dev.is_cuda()) {
+    k::trimr_first_degree(seg, m.nkey, key, nbr, m.nval, P0<int64_t>(edge), P0<int32_t>(deg), cur());
+    return {edge, deg};
+  }
+  int64_t* e = P0<int64_t>(edge);
+  int32_t* d = P0<int32_t>(deg);
+  for (int64_t s = 0; s < m.nkey; ++s) {
+    const int32_t n = (int32_t)(seg[s + 1] - seg[s]);
+    for (int64_t j = seg[s]; j < seg[s + 1]; ++j) {
+      const int64_t vi = key[s], vj = nbr[j];
+      const bool lt = vi < vj;
+      e[2 * j] = lt ? vi : vj;
+      e[2 * j + 1] = lt ? vj : vi;
+      d[2 * j] = lt ? n : 0;
+      d[2 * j + 1] = lt ? 0 : n;
+    }
+  }
+  return {edge, deg};
+}
+
+at::Tensor trimr_second_degree(const KMV& m) {
+  need(m.vw == 8, "tri_find_mr second degree: {int, int} values");
+  const at::Device dev = m.seg.device();
+  at::Tensor out = at::empty({m.nkey, 2}, opt(dev, at::kInt));
+  if (!m.nkey) return out;
+  const int64_t* seg = P0<int64_t>(m.seg);
+  const int32_t* v = P0<int32_t>(m.vdata);
+  if (dev.is_cuda()) {
+    k::trimr_second_degree(seg, m.nkey, v, m.nval, P0<int32_t>(out), cur());
+    return out;
+  }
+  int32_t* o = P0<int32_t>(out);
+  for (int64_t s = 0; s < m.nkey; ++s) {
+    const int64_t h = seg[s], h2 = h + 1 < m.nval ? h + 1 : m.nval - 1;
+    const bool use1 = v[2 * h] != 0;
+    o[2 * s] = use1 ? v[2 * h] : v[2 * h2];
+    o[2 * s + 1] = use1 ? v[2 * h2 + 1] : v[2 * h + 1];
+  }
+  return out;
+}
+
+std::pair<at::Tensor, at::Tensor> trimr_low_degree(const KV& kv) {
+  need(kv.kw == 16 && kv.vw == 8, "tri_find_mr low degree: EDGE keys, {int, int} values");
+  const at::Device dev = kv.device();
+  at::Tensor key = at::empty({kv.n}, opt(dev, at::kLong)), val = at::empty({kv.n}, opt(dev, at::kLong));
+  if (!kv.n) return {key, val};
+  const int64_t* e = P0<int64_t>(kv.kdata);
+  const int32_t* dg = P0<int32_t>(kv.vdata);
+  if (dev.is_cuda()) {
+    k::trimr_low_degree(e, dg, kv.n, P0<int64_t>(key), P0<int64_t>(val), cur());
+    return {key, val};
+  }
+  int64_t* k = P0<int64_t>(key);
+  int64_t* v = P0<int64_t>(val);
+  for (int64_t i = 0; i < kv.n; ++i) {
+    const int64_t vi = e[2 * i], vj = e[2 * i + 1];
+    const int32_t di = dg[2 * i], dj = dg[2 * i + 1];
+    const bool fi = di < dj || (di == dj && vi < vj);
+    k[i] = fi ? vi : vj;
+    v[i] = fi ? vj : vi;
+  }
+  return {key, val};
+}
+
+at::Tensor trimr_emit(const KMV& m) {
+  const at::Device dev = m.seg.device();
+  // one value width for the whole KMV: only markers or only centres, so no
+  // segment can close a wedge
+  if (!m.nkey || m.vw >= 0) return at::empty({0, 3}, opt(dev, at::kLong));
+  need(m.keys.kw == 16, "tri_find_mr emit: EDGE keys");
+  const int64_t* seg = P0<int64_t>(m.seg);
+  const int64_t* voff = P0<int64_t>(m.voff);
+  const int64_t* ek = P0<int64_t>(m.keys.kdata);
+  if (dev.is_cuda()) {
+    at::Tensor cnt = at::empty({m.nkey}, opt(dev, at::kLong));
+    k::trimr_emit_count(seg, m.nkey, voff, P0<int64_t>(cnt), cur());
+    at::Tensor pos = exclusive_scan(cnt);
+    const int64_t T = pos[m.nkey].item<int64_t>();
+    at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
+    if (T) k::trimr_emit_write(seg, m.nkey, voff, P0<uint8_t>(m.vdata), ek, P0<int64_t>(pos), P0<int64_t>(out), cur());
+    return out;
+  }
+  const uint8_t* vd = P0<uint8_t>(m.vdata);
+  std::vector<int64_t> rows;
+  for (int64_t s = 0; s < m.nkey; ++s) {
+    bool marker = false;
+    for (int64_t j = seg[s]; j < seg[s + 1]; ++j) marker |= voff[j + 1] == voff[j];
+    if (!marker) continue;
+    for (int64_t j = seg[s]; j < seg[s + 1]; ++j) {
+      if (voff[j + 1] - voff[j] != 8) continue;
+      int64_t c;
+      std::memcpy(&c, vd + voff[j], 8);
+      rows.insert(rows.end(), {c, ek[2 * s], ek[2 * s + 1]});
+    }
+  }
+  return at::tensor(rows, opt(at::kCPU, at::kLong)).view({-1, 3});
+}
+
+}  // namespace mrh

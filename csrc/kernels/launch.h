@@ -226,6 +226,20 @@ void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int6
 // K * K / 8 bytes (K a multiple of 64, <= 524288)
 void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64_t K, int64_t u0, int64_t u1,
                    uint64_t* H, unsigned long long* total, hipStream_t s);
+// ---------------------------------------------------------------- trimr.hip
+// tri_find_mr callbacks (oink/tri_find.cpp:104-325); edge rows are int64
+// pairs, degree rows int32 pairs
+void trimr_first_degree(const int64_t* seg, int64_t nkey, const int64_t* key, const int64_t* nbr, int64_t nval,
+                        int64_t* edge, int32_t* deg, hipStream_t s);
+void trimr_second_degree(const int64_t* seg, int64_t nkey, const int32_t* v, int64_t nval, int32_t* out,
+                         hipStream_t s);
+void trimr_low_degree(const int64_t* e, const int32_t* dg, int64_t n, int64_t* key, int64_t* val, hipStream_t s);
+// cnt[s] = wedge centres of edge segment s if it holds the edge marker, else 0
+void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, int64_t* cnt, hipStream_t s);
+// rows (centre, e0, e1) at pos[s].. (pos = exclusive scan of cnt)
+void trimr_emit_write(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vdata,
+                      const int64_t* ekey, const int64_t* pos, int64_t* out, hipStream_t s);
+
 // CSR row pointers of sorted oriented keys
 void tri_rowptr(const uint64_t* okeys, int64_t m, int64_t nvert, int64_t* rowptr, hipStream_t s);
 // triangles (u,v,w) as 3 u64 at off[e-e0] (off: exclusive scan of cnt, n+1 entries)

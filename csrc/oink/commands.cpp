@@ -18,6 +18,7 @@
 
 #include "callbacks.h"
 #include "engine/graphplan.h"
+#include "engine/tri.h"
 #include "oink.h"
 
 namespace mrh {
@@ -511,31 +512,18 @@ class TriFindMR : public Command {
     mrt.collate();
     mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_first_degree
       if (!m.nval) return;
-      at::Tensor deg = kmv_lens(m).to(at::kInt), sid = kmv_sid(m);
-      at::Tensor vi = m.keys.kdata.view(at::kLong).index({sid}), vj = m.vdata.view(at::kLong);
-      at::Tensor d = deg.index({sid}), z = at::zeros_like(d);
-      at::Tensor lt = vi < vj;
-      add_tensors(kv, at::stack({at::where(lt, vi, vj), at::where(lt, vj, vi)}, 1),
-                  at::stack({at::where(lt, d, z), at::where(lt, z, d)}, 1));
+      auto [edge, deg] = trimr_first_degree(m);
+      add_tensors(kv, edge, deg);
     });
     mrt.collate();
     mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_second_degree
       if (!m.nkey) return;
-      at::Tensor v = m.vdata.view(at::kInt).view({-1, 2});
-      at::Tensor h = m.seg.narrow(0, 0, m.nkey);
-      at::Tensor one = v.index({h}), two = v.index({at::clamp_max(h + 1, m.nval - 1)});
-      at::Tensor use1 = one.select(1, 0) != 0;
-      at::Tensor dg = at::stack({at::where(use1, one.select(1, 0), two.select(1, 0)),
-                                 at::where(use1, two.select(1, 1), one.select(1, 1))},
-                                1);
-      add_tensors(kv, m.keys.kdata.view(at::kLong).view({-1, 2}), dg);
+      add_tensors(kv, m.keys.kdata.view(at::kLong).view({-1, 2}), trimr_second_degree(m));
     });
     mrt.map_mr_batch(mrt, [](const KV& src, KeyValue& kv) {  // map_low_degree
       if (!src.n) return;
-      at::Tensor e = edges_of(src), dg = src.vdata.view(at::kInt).view({-1, 2});
-      at::Tensor vi = e.select(1, 0), vj = e.select(1, 1), di = dg.select(1, 0), dj = dg.select(1, 1);
-      at::Tensor fi = at::logical_or(di < dj, at::logical_and(di == dj, vi < vj));
-      add_tensors(kv, at::where(fi, vi, vj), at::where(fi, vj, vi));
+      auto [key, val] = trimr_low_degree(src);
+      add_tensors(kv, key, val);
     });
     mrt.collate();
     mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_nsq_angles
@@ -546,15 +534,8 @@ class TriFindMR : public Command {
     mrt.add(mre);
     mrt.collate();
     const uint64_t ntri = mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_emit_triangles
-      if (!m.nval) return;
-      at::Tensor vl = kmv_vlens(m), vs = kmv_vstart(m), sid = kmv_sid(m);
-      at::Tensor has_edge = at::zeros({m.nkey}, opt(m.seg.device(), at::kInt));
-      has_edge.index_put_({sid.index({vl == 0})}, 1);
-      at::Tensor sel = at::logical_and(vl == 8, has_edge.index({sid}) > 0);
-      if (!sel.any().item<bool>()) return;
-      at::Tensor centre = gather_bytes(m.vdata, vs.index({sel}), 8).view(at::kLong).reshape({-1});
-      at::Tensor e = m.keys.kdata.view(at::kLong).view({-1, 2}).index({sid.index({sel})});
-      add_tensors(kv, at::stack({centre, e.select(1, 0), e.select(1, 1)}, 1));
+      at::Tensor tri = trimr_emit(m);
+      if (tri.size(0)) add_tensors(kv, tri);
     });
     obj.output(1, mrt, print_tri);
     message(fmt("Tri_find: %" PRIu64 " triangles", ntri));

@@ -50,21 +50,55 @@ def test_empty_and_tiny():
     assert TriangleGraph(c, k4).count() == 4
 
 
-def test_oink_tri_find_matches_mapreduce_pipeline(tmp_path, monkeypatch):
+def _oink_tri(tmp_path, comm=None, scale=9):
     import io
     from gpu_mapreduce_amd.oink.interp import OINK
-    monkeypatch.chdir(tmp_path)
     out = io.StringIO()
-    OINK(screen=out, logfile="none").file(text=(
-        "rmat 9 8 0.57 0.19 0.19 0.05 0.0 11 -o NULL mre\n"
+    OINK(comm, screen=out, logfile="none").file(text=(
+        f"rmat {scale} 8 0.57 0.19 0.19 0.05 0.0 11 -o NULL mre\n"
         "edge_upper -i mre -o NULL mre\n"     # the MR pipeline needs upper-triangular input (examples/in.tri)
-        "tri_find -i mre -o tmp.fast NULL\n"
-        "tri_find_mr -i mre -o tmp.mr NULL\n"))
-    msgs = [ln for ln in out.getvalue().splitlines() if ln.startswith("Tri_find")]
+        f"tri_find -i mre -o {tmp_path}/tmp.fast NULL\n"
+        f"tri_find_mr -i mre -o {tmp_path}/tmp.mr NULL\n"))
+    return [ln for ln in out.getvalue().splitlines() if ln.startswith("Tri_find")]
+
+
+def _tri_files(tmp_path, stem):
+    import glob
+    return {tuple(sorted(map(int, ln.split()))) for f in glob.glob(str(tmp_path / f"{stem}.*")) for ln in open(f)}
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_oink_tri_find_matches_mapreduce_pipeline(tmp_path, dev):
+    """tri_find_mr (the reference's 4-shuffle pipeline, callbacks as the
+    trimr kernels on cuda / their host twins on cpu) lists exactly the
+    triangles of tri_find (oriented CSR + LDS-hash kernels)"""
+    msgs = _oink_tri(tmp_path, Comm(device=dev), scale=9 if dev == "cpu" else 12)
     assert len(msgs) == 2 and msgs[0] == msgs[1]
-    fast = {tuple(sorted(map(int, ln.split()))) for ln in open(tmp_path / "tmp.fast.0")}
-    mr = {tuple(sorted(map(int, ln.split()))) for ln in open(tmp_path / "tmp.mr.0")}
-    assert fast == mr and len(fast) == int(msgs[0].split()[1])
+    fast, mr = _tri_files(tmp_path, "tmp.fast"), _tri_files(tmp_path, "tmp.mr")
+    assert fast == mr and len(fast) == int(msgs[0].split()[1]) > 0
+
+
+def case_oink_tri_mr(comm):
+    import tempfile
+    import pathlib
+    d = pathlib.Path(tempfile.mkdtemp(prefix=f"trimr{comm.rank}_"))
+    msgs = _oink_tri(d, comm)
+    return msgs, sorted(_tri_files(d, "tmp.fast")), sorted(_tri_files(d, "tmp.mr"))
+
+
+def test_oink_tri_find_mr_distributed():
+    """3 ranks: every rank's share of the MR pipeline's triangles, unioned,
+    equals tri_find's and the single-rank brute force"""
+    from test_distributed_cpu import run_world
+    out = run_world("test_triangles:case_oink_tri_mr", 3)
+    fast, mr = set(), set()
+    msgs = out[0][0]  # rank 0 writes the screen
+    assert len(msgs) == 2 and msgs[0] == msgs[1]
+    for _, f, m in out.values():
+        assert not (mr & set(map(tuple, m)))
+        fast |= set(map(tuple, f))
+        mr |= set(map(tuple, m))
+    assert fast == mr and len(mr) == int(msgs[0].split()[1]) > 0
 
 
 @pytest.mark.gpu
