@@ -3,8 +3,9 @@
 // code, which only runs IntCount-style jobs on MR-MPI).
 //
 // One pass over the points: each lane assigns its points to the nearest
-// centroid (centroids staged in LDS, D <= 8 dims in registers) and adds the
-// point to its workgroup's per-cluster LDS accumulators (fp32 sums + count);
+// centroid (centroids staged in LDS, D <= 8 dims in registers) and the
+// workgroup sums each cluster's points on chip (D <= 3: the transposed
+// reduction of k_kmeans_tr, no atomics; else per-cluster LDS accumulators);
 // the workgroup then flushes its K x (D+1) partials into a global fp64 array
 // with device atomics (global_atomic_add_f64). The map emits (cluster, sums,
 // count) KVs from that array — GPMR's "emit (cluster, point) then combine"
@@ -120,14 +121,21 @@ __global__ __launch_bounds__(PNT) void k_kmeans_priv(const float* __restrict__ p
 // centroids as ||c||^2 - 2 x.c from one 16-byte LDS broadcast read per
 // centroid ({-2c, ||c||^2}, D <= 3), and adds into per-workgroup LDS
 // partials with LDS float atomics.
-constexpr int BNT = 256, PB = 8;
+constexpr int BNT = 256, PB = 8, BCMAX = 16;
 template <int D>
 __global__ __launch_bounds__(BNT) void k_kmeans_batch(const float* __restrict__ pts, int64_t n,
-                                                     const float* __restrict__ cen, int K, double* __restrict__ acc) {
+                                                     const float* __restrict__ cen, int K, int BC,
+                                                     double* __restrict__ acc) {
   static_assert(D <= 3, "one float4 per centroid");
   extern __shared__ float sh[];
   float4* c4 = reinterpret_cast<float4*>(sh);      // K x {-2c0, -2c1, -2c2, |c|^2}
-  float* part = sh + 4 * K;                          // K*(D+1)
+  // BC copies of the K*(D+1) partials, one per lane group (lane & (BC-1)),
+  // rows at an odd stride RS so equal rows of different copies fall in
+  // different banks: lanes of one wave instruction collide on an address
+  // only when they share a copy AND a cluster
+  const int R = K * (D + 1), RS = R | 1;
+  float* part = sh + 4 * K;
+  float* mine = part + (threadIdx.x & (BC - 1)) * RS;  // BC: power of two
   for (int kk = threadIdx.x; kk < K; kk += BNT) {
     float v[4] = {0.f, 0.f, 0.f, 0.f};
     float cc = 0.f;
@@ -139,46 +147,184 @@ __global__ __launch_bounds__(BNT) void k_kmeans_batch(const float* __restrict__ 
     v[3] = cc;
     c4[kk] = make_float4(v[0], v[1], v[2], v[3]);
   }
-  for (int i = threadIdx.x; i < K * (D + 1); i += BNT) part[i] = 0.f;
+  for (int i = threadIdx.x; i < BC * RS; i += BNT) part[i] = 0.f;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * BNT * PB + threadIdx.x;
-  float x[PB][D];
-#pragma unroll
-  for (int r = 0; r < PB; ++r) {
-    const int64_t i = base + (int64_t)r * BNT;
-#pragma unroll
-    for (int d = 0; d < D; ++d) x[r][d] = (i < n) ? pts[i * D + d] : 0.f;
-  }
-  float best[PB];
-  int bk[PB];
-#pragma unroll
-  for (int r = 0; r < PB; ++r) {
-    best[r] = FLT_MAX;
-    bk[r] = 0;
-  }
-  for (int kk = 0; kk < K; ++kk) {
-    const float4 c = c4[kk];
+  // grid-stride over tiles of BNT * PB points: a capped grid keeps adding
+  // into the same LDS partials, so the fp64 global atomics on the K * (D+1)
+  // accumulators (one per partial per workgroup, all on a few hot addresses)
+  // shrink with the grid instead of growing with n
+  const int64_t ntiles = (n + (int64_t)BNT * PB - 1) / ((int64_t)BNT * PB);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t base = tile * BNT * PB + threadIdx.x;
+    float x[PB][D];
 #pragma unroll
     for (int r = 0; r < PB; ++r) {
-      float sc = c.w;
-      sc = fmaf(x[r][0], c.x, sc);
-      if (D > 1) sc = fmaf(x[r][1], c.y, sc);
-      if (D > 2) sc = fmaf(x[r][2], c.z, sc);
-      const bool lt = sc < best[r];
-      best[r] = lt ? sc : best[r];
-      bk[r] = lt ? kk : bk[r];
+      const int64_t i = base + (int64_t)r * BNT;
+#pragma unroll
+      for (int d = 0; d < D; ++d) x[r][d] = (i < n) ? pts[i * D + d] : 0.f;
+    }
+    float best[PB];
+    int bk[PB];
+#pragma unroll
+    for (int r = 0; r < PB; ++r) {
+      best[r] = FLT_MAX;
+      bk[r] = 0;
+    }
+    for (int kk = 0; kk < K; ++kk) {
+      const float4 c = c4[kk];
+#pragma unroll
+      for (int r = 0; r < PB; ++r) {
+        float sc = c.w;
+        sc = fmaf(x[r][0], c.x, sc);
+        if (D > 1) sc = fmaf(x[r][1], c.y, sc);
+        if (D > 2) sc = fmaf(x[r][2], c.z, sc);
+        const bool lt = sc < best[r];
+        best[r] = lt ? sc : best[r];
+        bk[r] = lt ? kk : bk[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < PB; ++r) {
+      if (base + (int64_t)r * BNT >= n) break;
+#pragma unroll
+      for (int d = 0; d < D; ++d) atomicAdd(&mine[bk[r] * (D + 1) + d], x[r][d]);
+      atomicAdd(&mine[bk[r] * (D + 1) + D], 1.f);
     }
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < R; i += BNT) {
+    double v = 0.0;
+    for (int c = 0; c < BC; ++c) v += (double)part[c * RS + i];
+    if (v != 0.0) atomicAdd(&acc[i], v);
+  }
+}
+
+// Transposed-reduction variant (default for D <= 3, K <= 256): no atomics
+// in the point loop. PMC on the LDS-atomic kernels (profiles/r2_kmeans_tr.txt)
+// showed the LDS array 92-93 % busy at ~200 LDS cycles per ds_add_f32 wave
+// instruction — with one shared copy of the partials AND with 16 lane-group
+// copies (no address collisions), i.e. LDS float atomics themselves run at
+// ~3 cycles per lane. Per tile of 2048 points a workgroup
+//   1. scores its points (8 per lane, {-2c, |c|^2} LDS broadcast) and
+//      writes (cluster, x) of the tile to LDS in SoA;
+//   2. transposes the reduction: lane l owns clusters l%32 (+32 g) and the
+//      half l/32 of its wave's 512 points, and walks them with broadcast LDS
+//      reads (4 points per ds_read_b128), adding the coordinates of the
+//      points whose cluster it owns into registers (compare + select + add).
+// Persistent grid; at the end the 8 owners of each (cluster, value) fold
+// through LDS and the workgroup issues one fp64 global atomic per value.
+constexpr int TNT = 256, TPB = 8, TTILE = TNT * TPB, TKG = 8;  // K <= 32 * TKG
+template <int D, int KG>  // KG cluster groups of 32 per lane: K <= 32 * KG
+__global__ __launch_bounds__(TNT) void k_kmeans_tr(const float* __restrict__ pts, int64_t n,
+                                                  const float* __restrict__ cen, int K, double* __restrict__ acc) {
+  static_assert(D <= 3, "one float4 per centroid");
+  extern __shared__ float sh[];
+  float4* c4 = reinterpret_cast<float4*>(sh);       // K x {-2c, |c|^2}
+  int* sbk = reinterpret_cast<int*>(sh + 4 * K);    // TTILE cluster ids
+  float* sx = sh + 4 * K + TTILE;                   // D x TTILE coordinates
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int kk = tid; kk < K; kk += TNT) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    float cc = 0.f;
+    for (int d = 0; d < D; ++d) {
+      const float cd = cen[kk * D + d];
+      v[d] = -2.f * cd;
+      cc = fmaf(cd, cd, cc);
+    }
+    v[3] = cc;
+    c4[kk] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  float s[KG][D];
+  int cnt[KG];
 #pragma unroll
-  for (int r = 0; r < PB; ++r) {
-    if (base + (int64_t)r * BNT >= n) break;
+  for (int g = 0; g < KG; ++g) {
+    cnt[g] = 0;
 #pragma unroll
-    for (int d = 0; d < D; ++d) atomicAdd(&part[bk[r] * (D + 1) + d], x[r][d]);
-    atomicAdd(&part[bk[r] * (D + 1) + D], 1.f);
+    for (int d = 0; d < D; ++d) s[g][d] = 0.f;
+  }
+  const int own = lane & 31;
+  const int j0 = w * (TTILE / 4) + (lane >> 5) * (TTILE / 8);  // this lane's 256 tile points
+  const int64_t ntiles = (n + TTILE - 1) / TTILE;
+  __syncthreads();
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t base = tile * TTILE;
+    float x[TPB][D];
+#pragma unroll
+    for (int r = 0; r < TPB; ++r) {
+      const int64_t i = std::min<int64_t>(base + r * TNT + tid, n - 1);
+#pragma unroll
+      for (int d = 0; d < D; ++d) x[r][d] = pts[i * D + d];
+    }
+    float best[TPB];
+    int bk[TPB];
+#pragma unroll
+    for (int r = 0; r < TPB; ++r) {
+      best[r] = FLT_MAX;
+      bk[r] = 0;
+    }
+    for (int kk = 0; kk < K; ++kk) {
+      const float4 c = c4[kk];
+#pragma unroll
+      for (int r = 0; r < TPB; ++r) {
+        float sc = c.w;
+        sc = fmaf(x[r][0], c.x, sc);
+        if (D > 1) sc = fmaf(x[r][1], c.y, sc);
+        if (D > 2) sc = fmaf(x[r][2], c.z, sc);
+        const bool lt = sc < best[r];
+        best[r] = lt ? sc : best[r];
+        bk[r] = lt ? kk : bk[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < TPB; ++r) {
+      const int j = r * TNT + tid;
+      sbk[j] = (base + j < n) ? bk[r] : -1;  // tail points belong to no cluster
+#pragma unroll
+      for (int d = 0; d < D; ++d) sx[d * TTILE + j] = x[r][d];
+    }
+    __syncthreads();
+    for (int j = j0; j < j0 + TTILE / 8; j += 4) {
+      const int4 b4 = *reinterpret_cast<const int4*>(sbk + j);
+      float4 x4[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) x4[d] = *reinterpret_cast<const float4*>(sx + d * TTILE + j);
+      const int bb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        const int c = g * 32 + own;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool m = bb[q] == c;
+          cnt[g] += m;
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            const float xv = q == 0 ? x4[d].x : q == 1 ? x4[d].y : q == 2 ? x4[d].z : x4[d].w;
+            s[g][d] += m ? xv : 0.f;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // fold the 8 owners (2 halves x 4 waves) of each (cluster, value) through
+  // LDS (the tile buffers are free now), then one global atomic per value
+  float* red = sx;  // [8 owners][K * (D+1)]
+  const int R = K * (D + 1), owner = w * 2 + (lane >> 5);
+  for (int g = 0; g < KG; ++g) {
+    const int c = g * 32 + own;
+    if (c < K) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) red[owner * R + c * (D + 1) + d] = s[g][d];
+      red[owner * R + c * (D + 1) + D] = (float)cnt[g];
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < K * (D + 1); i += BNT)
-    if (part[i] != 0.f) atomicAdd(&acc[i], (double)part[i]);
+  for (int i = tid; i < R; i += TNT) {
+    double v = 0.0;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) v += (double)red[o * R + i];
+    if (v != 0.0) atomicAdd(&acc[i], v);
+  }
 }
 
 // Register-accumulator variant (opt-in, MRH_KMEANS_KERNEL=4; K <= KM = 32,
@@ -406,6 +552,19 @@ void launch_mfma(const float* pts, int64_t n, int D, const float* cen, int K, do
   MRH_CHECK_LAUNCH();
 }
 
+inline size_t batch_lds(int D, int K, int bc) { return sizeof(float) * ((size_t)4 * K + (size_t)bc * ((K * (D + 1)) | 1)); }
+// centroids + one tile's (cluster, coordinates) SoA; the final fold reuses
+// the coordinate buffer for 8 x K*(D+1) partials
+inline size_t tr_lds(int D, int K) {
+  return sizeof(float) * ((size_t)4 * K + TTILE + std::max<size_t>((size_t)D * TTILE, (size_t)8 * K * (D + 1)));
+}
+// copies of the partials: as many (<= 16) as fit in 64 KB with the centroids
+inline int batch_copies(int D, int K) {
+  int bc = BCMAX;
+  while (bc > 1 && batch_lds(D, K, bc) > 64 * 1024) bc >>= 1;
+  return bc;
+}
+
 template <int D>
 void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, hipStream_t s) {
   static const int variant = [] {
@@ -416,7 +575,7 @@ void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, h
     // MRH_KMEANS_KERNEL=4: the register-accumulator kernel. Measured slower
     // (26.0 vs 15.8 ms per 20 iterations, profiles/r1_kmeans_variants.txt):
     // its 128 predicated FMAs per point cost more than the LDS-atomic waits
-    // they remove, so the batched kernel stays the default.
+    // they remove.
     if (variant == 4 && K <= 32) {
       int64_t nb = (n + RNT - 1) / RNT;
       if (nb > 1024) nb = 1024;  // ~128 points per lane at 32 M points
@@ -424,10 +583,36 @@ void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, h
       MRH_CHECK_LAUNCH();
       return;
     }
-    if (variant != 1 && (size_t)K * (4 + D + 1) * 4 <= 64 * 1024) {
-      const int64_t nb = (n + (int64_t)BNT * PB - 1) / ((int64_t)BNT * PB);
-      const size_t lds = sizeof(float) * (size_t)K * (4 + D + 1);
-      hipLaunchKernelGGL((k_kmeans_batch<D>), dim3((unsigned)nb), dim3(BNT), lds, s, pts, n, cen, K, acc);
+    // default: the transposed-reduction kernel; MRH_KMEANS_KERNEL=6 keeps
+    // the LDS-atomic batched kernel (5: with one shared partial copy)
+    if (variant == 0 && K <= 32 * TKG && tr_lds(D, K) <= 64 * 1024) {
+      static const int ncu = [] {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return std::max(1, c);
+      }();
+      int64_t nb = (n + TTILE - 1) / TTILE;
+      if (nb > (int64_t)ncu * 8) nb = (int64_t)ncu * 8;  // persistent: ~8 workgroups per CU
+      const size_t lds = tr_lds(D, K);
+      if (K <= 32) hipLaunchKernelGGL((k_kmeans_tr<D, 1>), dim3((unsigned)nb), dim3(TNT), lds, s, pts, n, cen, K, acc);
+      else if (K <= 64) hipLaunchKernelGGL((k_kmeans_tr<D, 2>), dim3((unsigned)nb), dim3(TNT), lds, s, pts, n, cen, K, acc);
+      else if (K <= 128) hipLaunchKernelGGL((k_kmeans_tr<D, 4>), dim3((unsigned)nb), dim3(TNT), lds, s, pts, n, cen, K, acc);
+      else hipLaunchKernelGGL((k_kmeans_tr<D, TKG>), dim3((unsigned)nb), dim3(TNT), lds, s, pts, n, cen, K, acc);
+      MRH_CHECK_LAUNCH();
+      return;
+    }
+    if (variant != 1 && batch_lds(D, K, 1) <= 64 * 1024) {
+      const int bc = variant == 5 ? 1 : batch_copies(D, K);  // 5: one shared copy (the r1 kernel)
+      // MRH_KMEANS_BLOCKS caps the grid (0 = one workgroup per tile)
+      static const int64_t cap = [] {
+        const char* e = std::getenv("MRH_KMEANS_BLOCKS");
+        return e ? std::atoll(e) : (int64_t)0;
+      }();
+      int64_t nb = (n + (int64_t)BNT * PB - 1) / ((int64_t)BNT * PB);
+      if (cap > 0 && nb > cap) nb = cap;
+      const size_t lds = batch_lds(D, K, bc);
+      hipLaunchKernelGGL((k_kmeans_batch<D>), dim3((unsigned)nb), dim3(BNT), lds, s, pts, n, cen, K, bc, acc);
       MRH_CHECK_LAUNCH();
       return;
     }

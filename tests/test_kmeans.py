@@ -47,10 +47,12 @@ def test_kmeans_job_matches_lloyd():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,K", [(2, 32), (3, 5), (8, 64), (16, 10), (5, 7), (32, 64), (64, 128), (100, 40),
+@pytest.mark.parametrize("D,K", [(2, 32), (3, 5), (1, 8), (3, 64), (8, 64), (16, 10), (5, 7), (32, 64), (64, 128), (100, 40),
                                  (128, 16), (160, 8)])
 def test_kmeans_map_gpu(D, K):
-    """fused assign + LDS combine kernel (D <= 8), the matrix-core kernel
+    """lane-private accumulator kernel (D <= 3, K * (D+1) <= 184; (3, 64)
+    falls back to the LDS-atomic batched kernel), fused assign + LDS combine
+    kernel (D <= 8), the matrix-core kernel
     (D <= 128, any K that fits LDS) and the GEMM fallback (D = 160) against
     the float64 oracle; a point equidistant to two centroids may go either
     way, so compare with a tolerance on the counts too"""
