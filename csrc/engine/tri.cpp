@@ -127,6 +127,48 @@ int64_t tri_hub_size(int64_t nvert) {
   return K;
 }
 
+// dense core size: MRH_TRI_CORE ranks (default 0 = off), a multiple of 64, <= the hub set.
+// Off by default: on RMAT-24 a core of 4 K-32 K ranks measured 351 / 350 /
+// 348 / 359 ms against 351 ms without (profiles/r2_trifind_core_mfma.txt) —
+// the hub kernel's time is in the sparse lower hub rows, not the dense core
+int64_t tri_core_size(int64_t K) {
+  static const int64_t env = [] {
+    const char* e = std::getenv("MRH_TRI_CORE");
+    return e ? std::atoll(e) : int64_t(0);
+  }();
+  return std::min<int64_t>(std::max<int64_t>(env, 0), K) / 64 * 64;
+}
+
+// triangles whose lowest vertex u is a core rank in [u0, u1): the core's
+// oriented adjacency A (int8 0/1, top T ranks) gives |N+(u) ∩ N+(v)| =
+// (A A^T)[u][v] for all core pairs at once on the matrix cores (hipBLASLt
+// int8 GEMM, int32 accumulation: exact); the count is sum(A .* (A A^T)) over
+// the rows, in row blocks that bound the int32 product
+static int64_t tri_core_count(const at::Tensor& rowptr, const at::Tensor& col, int64_t cb, int64_t T, int64_t u0,
+                              int64_t u1) {
+  const at::Device dev = rowptr.device();
+  at::Tensor A = at::empty({T, T}, opt(dev, at::kChar));
+  k::tri_core_build(P0<int64_t>(rowptr), P0<uint32_t>(col), cb, T, P0<int8_t>(A), cur());
+  const int64_t ra = std::max<int64_t>(u0 - cb, 0), rb = std::min<int64_t>(u1 - cb, T);
+  at::Tensor At = A.t();
+  at::Tensor tot = at::zeros({}, opt(dev, at::kLong));
+  const int64_t RB = std::max<int64_t>(64, ((int64_t)1 << 28) / T) / 64 * 64;  // <= 1 GiB of int32 per block
+  // rows in multiples of 64 (the GEMM's shape rules); rows outside [ra, rb) masked
+  for (int64_t r = ra / 64 * 64; r < rb; r += RB) {
+    const int64_t n = std::min<int64_t>(RB, T - r);
+    at::Tensor Ar = A.narrow(0, r, n);
+    at::Tensor C = at::_int_mm(Ar, At);
+    at::Tensor M = Ar;
+    if (r < ra || r + n > rb) {
+      M = Ar.clone();
+      if (r < ra) M.narrow(0, 0, ra - r).zero_();
+      if (r + n > rb) M.narrow(0, rb - r, r + n - rb).zero_();
+    }
+    tot += at::mul(C, M).sum(at::kLong);
+  }
+  return tot.item<int64_t>();
+}
+
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1) {
   e1 = std::min<int64_t>(e1, okeys.numel());
   if (e1 <= e0) return 0;
@@ -142,20 +184,24 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
     g_last_hub = K;
     const int64_t hb = nvert - K;
     const int64_t uh = K ? std::max(u0, std::min(u1, hb)) : u1;
+    // the top T of the hubs (the dense core) go to the matrix cores instead
+    const int64_t T = K ? tri_core_size(K) : 0, cb = nvert - T;
     at::Tensor H;
     if (K) {
       // the bitmaps serve both the hub kernel and the hub probes of the hash kernels
       H = at::empty({K * (K / 64)}, opt(okeys.device(), at::kLong));
-      k::tri_hub_count(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, std::max(u0, hb), std::max(u1, hb),
-                       P0<uint64_t>(H), P0<unsigned long long>(tot), cur());
+      k::tri_hub_count(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, std::max(u0, hb),
+                       std::max(std::min(u1, cb), hb), P0<uint64_t>(H), P0<unsigned long long>(tot), cur());
     }
+    int64_t ncore = 0;
+    if (T && u1 > cb) ncore = tri_core_count(rowptr, col, cb, T, std::max(u0, cb), u1);
     if (uh > u0) {
       at::Tensor big = at::empty({2 * std::max<int64_t>(uh - u0, 1)}, opt(okeys.device(), at::kInt));
       at::Tensor nbig = at::zeros({2}, opt(okeys.device(), at::kInt));
       k::tri_count_hash(P0<int64_t>(rowptr), P0<uint32_t>(col), u0, uh, P0<uint32_t>(big), P0<uint32_t>(nbig),
                         P0<unsigned long long>(tot), cur(), K ? P0<uint64_t>(H) : nullptr, hb, K);
     }
-    return tot.item<int64_t>();
+    return tot.item<int64_t>() + ncore;
   }
   const int64_t* rp = P0<int64_t>(rowptr);
   const int32_t* c = P0<int32_t>(col);

@@ -240,6 +240,8 @@ void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, int
 void trimr_emit_write(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vdata,
                       const int64_t* ekey, const int64_t* pos, int64_t* out, hipStream_t s);
 
+// dense 0/1 int8 adjacency of the top T ranks (cb = nvert - T), T x T, zeroed here
+void tri_core_build(const int64_t* rowptr, const uint32_t* col, int64_t cb, int64_t T, int8_t* A, hipStream_t s);
 // CSR row pointers of sorted oriented keys
 void tri_rowptr(const uint64_t* okeys, int64_t m, int64_t nvert, int64_t* rowptr, hipStream_t s);
 // triangles (u,v,w) as 3 u64 at off[e-e0] (off: exclusive scan of cnt, n+1 entries)

@@ -384,6 +384,20 @@ __global__ __launch_bounds__(NT) void k_tri_hub_build(const int64_t* __restrict_
   }
 }
 
+// dense core: the top T ranks as a 0/1 int8 matrix (row u - cb: 1 at w - cb
+// for w in N+(u)); the triangles whose lowest vertex is in the core are then
+// sum(A .* (A A^T)), an int8 matrix-core GEMM instead of AND/popcount walks
+__global__ __launch_bounds__(NT) void k_tri_core_build(const int64_t* __restrict__ rowptr,
+                                                      const uint32_t* __restrict__ col, int64_t cb, int64_t T,
+                                                      int8_t* __restrict__ A) {
+  const int64_t nw = (int64_t)gridDim.x * HASH_NW;
+  for (int64_t r = (int64_t)blockIdx.x * HASH_NW + dev::wave_id(); r < T; r += nw) {
+    const int64_t u = cb + r;
+    for (int64_t e = rowptr[u] + dev::lane_id(); e < rowptr[u + 1]; e += MRH_WAVE)
+      A[r * T + ((int64_t)col[e] - cb)] = 1;  // N+(u) holds higher ranks only: inside the core
+  }
+}
+
 // one workgroup per hub u in [r0, r1) (rows relative to hb); each thread
 // keeps HUB_WPT words of H[u] in registers and ANDs them with the same words
 // of H[v] for every v in N+(u) (coalesced row reads, words below v skipped)
@@ -542,6 +556,14 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
     hipLaunchKernelGGL(k_tri_hub_count<16>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
   else
     hipLaunchKernelGGL(k_tri_hub_count<32>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
+  MRH_CHECK_LAUNCH();
+}
+
+void tri_core_build(const int64_t* rowptr, const uint32_t* col, int64_t cb, int64_t T, int8_t* A, hipStream_t s) {
+  if (T <= 0) return;
+  (void)hipMemsetAsync(A, 0, (size_t)T * (size_t)T, s);
+  hipLaunchKernelGGL(k_tri_core_build, dim3((unsigned)std::min<int64_t>((T + HASH_NW - 1) / HASH_NW, 16384)), dim3(NT),
+                     0, s, rowptr, col, cb, T, A);
   MRH_CHECK_LAUNCH();
 }
 

@@ -162,19 +162,24 @@ print(C.tri_hub_size(gpu.nvert), gpu.count())
 def test_gpu_hub_bitmap_split_matches_cpu():
     """the same RMAT-17 count with the hub bitmap path off (hash kernels
     only), on the default (nvert/32 ~ 4096 hubs), 4096 hubs, and 65536 (half
-    of the graph in bitmaps) — each must equal the CPU merge count"""
+    of the graph in bitmaps), and with the top 1024 / 8192 / all 8192 hubs as
+    the dense int8 GEMM core — each must equal the CPU merge count"""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     want = TriangleGraph(Comm(device="cpu"), _rmat(17, 16, 3)).count()
-    for hub, K in (("0", 0), (None, 4096), ("4096", 4096), ("65536", 65536)):
+    for hub, K, core in (("0", 0, None), (None, 4096, None), ("4096", 4096, None), ("65536", 65536, None),
+                         ("4096", 4096, "1024"), ("65536", 65536, "8192"), ("8192", 8192, "8192")):
         env = dict(os.environ, PYTHONPATH=root)
         env.pop("MRH_TRI_HUB", None)
+        env.pop("MRH_TRI_CORE", None)
         if hub is not None:
             env["MRH_TRI_HUB"] = hub
+        if core is not None:  # the top ranks of the hubs counted by the int8 GEMM
+            env["MRH_TRI_CORE"] = core
         r = subprocess.run([sys.executable, "-c", TRI_HUB_CHILD], env=env, cwd=root, capture_output=True, text=True,
                            timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         k, n = map(int, r.stdout.split())
-        assert (k == K if hub is not None else 0 < k <= K and k % 64 == 0) and n == want, (hub, k, n, want)
+        assert (k == K if hub is not None else 0 < k <= K and k % 64 == 0) and n == want, (hub, core, k, n, want)
