@@ -202,8 +202,8 @@ def bench_pagerank_extra(comm, args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="invertedindex", choices=["invertedindex", "pagerank", "wordfreq", "trifind", "intcount", "kmeans"])
     ap.add_argument("--bytes-per-gpu", type=float, default=float(1 << 30))
     ap.add_argument("--file-bytes", type=int, default=128 << 20)
