@@ -861,6 +861,21 @@ at::Tensor bincount_dev(const at::Tensor& idx_in, int64_t K) {
   return c;
 }
 
+at::Tensor mask_indices(const at::Tensor& mask_in) {
+  const at::Device dev = mask_in.device();
+  at::Tensor m = mask_in.to(at::kBool).contiguous().view(at::kByte);
+  const int64_t n = m.numel();
+  if (!dev.is_cuda()) return at::nonzero(m).view({-1});
+  if (n == 0) return at::empty({0}, opt(dev, at::kLong));
+  at::Tensor f = at::empty({n}, opt(dev, at::kLong));
+  k::mask_flags(P0<uint8_t>(m), n, P0<int64_t>(f), cur_stream());
+  at::Tensor pos = exclusive_scan(f);
+  const int64_t cnt = pos[n].item<int64_t>();
+  at::Tensor out = at::empty({cnt}, opt(dev, at::kLong));
+  if (cnt) k::compact_mask(P0<uint8_t>(m), P0<int64_t>(pos), n, P0<int64_t>(out), cur_stream());
+  return out;
+}
+
 at::Tensor repeat_index(const at::Tensor& counts) {
   at::Tensor off = exclusive_scan(counts.to(at::kLong));
   const int64_t n = counts.numel();

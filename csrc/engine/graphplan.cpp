@@ -219,7 +219,8 @@ at::Tensor sssp_predecessors(const EdgePlan& plan, const at::Tensor& edges, cons
                                   at::isfinite(dist.index_select(0, lv)));
   // deterministic tie-break across equal-length paths: the smallest predecessor id
   at::Tensor pred = at::full({plan.nlocal}, std::numeric_limits<int64_t>::max(), at::TensorOptions().device(dev).dtype(at::kLong));
-  if (ok.any().item<bool>()) pred.scatter_reduce_(0, lv.index({ok}), cu.select(1, 1).index({ok}), "amin", true);
+  at::Tensor oki = mask_indices(ok);
+  if (oki.numel()) pred.scatter_reduce_(0, lv.index_select(0, oki), cu.select(1, 1).index_select(0, oki), "amin", true);
   pred.masked_fill_(pred == std::numeric_limits<int64_t>::max(), -1);
   if (source % P == plan.me) pred.index_put_({source / P}, 0);  // the source: DISTANCE() default, e.v = 0
   return pred;
@@ -474,9 +475,9 @@ TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : c
   const at::Device dev = comm->device();
   at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2});
   at::Tensor lo = at::minimum(e.select(1, 0), e.select(1, 1)), hi = at::maximum(e.select(1, 0), e.select(1, 1));
-  at::Tensor keep = lo != hi;
-  lo = lo.index({keep});
-  hi = hi.index({keep});
+  at::Tensor keep = mask_indices(lo != hi);  // no self loops
+  lo = lo.index_select(0, keep);
+  hi = hi.index_select(0, keep);
   if (nv < 0) nv = comm->allreduce(hi.numel() ? hi.max().item<int64_t>() : -1, Comm::MAX) + 1;
   nvert = nv;
   if (nvert >= (int64_t(1) << 31)) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^31");
@@ -552,7 +553,7 @@ void TriangleGraph::build_distributed(const at::Tensor& lo_in, const at::Tensor&
   at::Tensor own_rp = exclusive_scan(bincount_dev(lu, nlocal));
   // 5. halo rows: request N+(v) for remote targets
   at::Tensor remote = at::remainder(v, P) != me;
-  at::Tensor hids = unique_sorted(v.index({remote}));
+  at::Tensor hids = unique_sorted(v.index_select(0, mask_indices(remote)));
   at::Tensor req = route_rows(cm, at::stack({hids, at::full_like(hids, me)}, 1), at::remainder(hids, P), 2);
   at::Tensor rv = req.select(1, 0).contiguous(), rq = req.select(1, 1).contiguous();
   at::Tensor rrow = at::floor_divide(rv, P);
@@ -566,9 +567,10 @@ void TriangleGraph::build_distributed(const at::Tensor& lo_in, const at::Tensor&
   // keep only entries that are rows here (owned, or a requested halo id)
   at::Tensor hw_halo = lookup(hids, hw);
   at::Tensor keep = at::logical_or(at::remainder(hw, P) == me, hw_halo >= 0);
-  hv = hv.index({keep});
-  hw = hw.index({keep});
-  hw_halo = hw_halo.index({keep});
+  at::Tensor ki = mask_indices(keep);
+  hv = hv.index_select(0, ki);
+  hw = hw.index_select(0, ki);
+  hw_halo = hw_halo.index_select(0, ki);
   // 6. one local id space, rows sorted by local id
   const int64_t nh = hids.numel();
   nrows = nlocal + nh;
@@ -585,7 +587,7 @@ void TriangleGraph::build_distributed(const at::Tensor& lo_in, const at::Tensor&
   rowptr = exclusive_scan(bincount_dev(at::bitwise_right_shift(keys, 32), nrows));
   // owned oriented edges in the local space (row < nlocal), for counting and listing
   at::Tensor owned = at::bitwise_right_shift(keys, 32) < nlocal;
-  okeys = keys.index({owned}).contiguous();
+  okeys = keys.index_select(0, mask_indices(owned)).contiguous();
   e0 = 0;
   e1 = okeys.numel();
   // global id of every local row

@@ -198,6 +198,9 @@ std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor
 at::Tensor segment_ids(const at::Tensor& seg, int64_t nseg, int64_t nval);
 // counts of each bin in [0, K) of an integer index column (device histogram)
 at::Tensor bincount_dev(const at::Tensor& idx, int64_t K);
+// positions of the true elements of a bool mask, in order (int64; the
+// device path is flags + scan + scatter, not at::nonzero's rocPRIM partition)
+at::Tensor mask_indices(const at::Tensor& mask);
 // i repeated counts[i] times (the row index of every expanded element)
 at::Tensor repeat_index(const at::Tensor& counts);
 // segment boundaries of a sorted int64 key column: seg[nseg+1]

@@ -85,6 +85,9 @@ void histogram(const int64_t* idx, int64_t n, int64_t K, int64_t* counts, hipStr
 // f[i] = v[i] != 0 ; out[pos[i]] = i for non-zero v (pos = exclusive scan of f)
 void nz_flags(const uint64_t* v, int64_t n, int32_t* f, hipStream_t s);
 void compact_nz(const uint64_t* v, const int64_t* pos, int64_t n, int64_t* out, hipStream_t s);
+// bool-mask compaction: f[i] = m[i] != 0 (int64); out[pos[i]] = i for set m[i] (pos = exclusive scan of f)
+void mask_flags(const uint8_t* m, int64_t n, int64_t* f, hipStream_t s);
+void compact_mask(const uint8_t* m, const int64_t* pos, int64_t n, int64_t* out, hipStream_t s);
 // idx[j] = index of q[j] in sorted unique keys[0, n), or -1 (binary search per query)
 void lookup_sorted(const int64_t* keys, int64_t n, const int64_t* q, int64_t m, int64_t* idx, hipStream_t s);
 

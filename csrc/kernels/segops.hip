@@ -9,7 +9,10 @@
 //  k_histogram   counts[idx[i]]++ with one global atomic per element (for
 //                wide histograms; narrow ones use the LDS count_mod kernel);
 //  k_compact_nz  indices of the non-zero u64 slots of a hash table, in
-//                order, from the exclusive scan of the non-zero flags.
+//                order, from the exclusive scan of the non-zero flags;
+//  k_mask_flags / k_compact_mask  the same for a bool mask (the engine's
+//                boolean-mask selections: at::nonzero would run rocPRIM's
+//                partition kernel).
 #include <algorithm>
 
 #include "common.h"
@@ -64,7 +67,29 @@ __global__ __launch_bounds__(NT) void k_lookup_sorted(const int64_t* __restrict_
   }
 }
 
+__global__ __launch_bounds__(NT) void k_mask_flags(const uint8_t* __restrict__ m, int64_t n, int64_t* __restrict__ f) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) f[i] = m[i] != 0;
+}
+
+__global__ __launch_bounds__(NT) void k_compact_mask(const uint8_t* __restrict__ m, const int64_t* __restrict__ pos,
+                                                    int64_t n, int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+    if (m[i]) out[pos[i]] = i;
+}
+
 }  // namespace
+
+void mask_flags(const uint8_t* m, int64_t n, int64_t* f, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_mask_flags, dim3(blocks(n)), dim3(NT), 0, s, m, n, f);
+  MRH_CHECK_LAUNCH();
+}
+
+void compact_mask(const uint8_t* m, const int64_t* pos, int64_t n, int64_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_compact_mask, dim3(blocks(n)), dim3(NT), 0, s, m, pos, n, out);
+  MRH_CHECK_LAUNCH();
+}
 
 void lookup_sorted(const int64_t* keys, int64_t n, const int64_t* q, int64_t m, int64_t* idx, hipStream_t s) {
   if (m <= 0) return;
