@@ -8,6 +8,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--bytes-per-gpu", "4e6", "--file-bytes", "1000000", "--steps", "1", "--warmup", "1", "--phases", "0",
         "--pagerank-scale", "10", "--pagerank-steps", "1"]
@@ -43,3 +45,28 @@ def test_bench_rejects_world_size_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", *ARGS], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu():
+    """bench.py --gpus 2 on a 1-GPU box: both ranks share cuda:0 (RCCL refuses
+    two ranks on one device, so torch.distributed runs gloo and the engine its
+    store transport); every multi-rank engine path of the headline job runs
+    on the GPU — per-file exchange, grouped collate, GPU output formatting,
+    PageRank plan with owner exchange — and the global counts double"""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(MRH_DIST_BACKEND="gloo", MRH_TRANSPORT="pg", MRH_NUMA_BIND="0")
+    args = ["--bytes-per-gpu", "32e6", "--file-bytes", "8000000", "--steps", "2", "--warmup", "1", "--phases", "0",
+            "--pagerank-scale", "16", "--pagerank-steps", "1"]
+    out = {}
+    for n in (1, 2):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), *args], cwd=ROOT,
+                           env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        out[n] = json.loads(lines[0])
+    one, two = out[1], out[2]
+    assert two["n_gpus"] == two["rccl_ranks"] == 2 and two["backend"]["torch.distributed"] == "gloo"
+    assert two["kv_pairs_per_step"] == 2 * one["kv_pairs_per_step"]
+    assert two["pagerank_config"]["edges"] == one["pagerank_config"]["edges"]
