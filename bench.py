@@ -257,7 +257,14 @@ def main():
         from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
         res = bench_wordfreq(comm, args)
     if args.workload == "invertedindex" and args.pagerank_scale > 0:
-        res.update(bench_pagerank_extra(comm, args))
+        # the headline line is printed even if the PageRank extra fails (its
+        # peers fail fast through the engine's peer monitor); the error is
+        # reported in the record instead of the PageRank keys
+        try:
+            res.update(bench_pagerank_extra(comm, args))
+        except Exception as e:  # noqa: BLE001
+            res["pagerank_error"] = f"{type(e).__name__}: {e}"[:500]
+            print(f"bench.py rank {comm.rank}: PageRank extra failed: {e}", file=sys.stderr, flush=True)
     res["rccl_ranks"] = comm.size
     res["backend"] = {"torch.distributed": comm.backend or "none (world size 1)",
                       "engine_transport": comm.native.transport}
