@@ -91,6 +91,11 @@ at::Tensor pr_update(const at::Tensor& acc, const at::Tensor& r, at::Tensor& rn,
   const int64_t n = r.numel();
   const bool wc = invdeg.defined() && invdeg.numel() > 0;
   if (r.is_cuda()) {
+    // the kernel moves 16 bytes per access and zeroes acc behind its read
+    auto al = [](const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.is_contiguous(); };
+    need(acc.numel() >= n && rn.numel() >= n && dangling.numel() >= n && al(acc) && al(r) && al(rn) &&
+             reinterpret_cast<uintptr_t>(dangling.data_ptr()) % 4 == 0 && (!wc || (al(invdeg) && al(cout))),
+         "pr_update: contiguous 16-byte-aligned float columns of n entries (dangling 4-byte aligned)");
     int nb = k::pr_update_blocks(n);
     at::Tensor part = at::empty({nb, 2}, opt(r.device(), at::kDouble));
     k::pr_update(P0<float>(acc), P0<float>(r), P0<float>(rn), P0<uint8_t>(dangling), n, (float)base, (float)alpha,
@@ -106,8 +111,10 @@ at::Tensor pr_update(const at::Tensor& acc, const at::Tensor& r, at::Tensor& rn,
   float* co = wc ? P0<float>(cout) : nullptr;
   const float dterm = (float)(dmass.to(at::kCPU).item<double>() * invN);
   double d = 0, dm = 0;
+  float* az = P0<float>(acc);
   for (int64_t i = 0; i < n; ++i) {
     float x = (float)base + (float)alpha * (a[i] + dterm);
+    az[i] = 0.f;  // as the kernel: acc is zeroed behind its read
     o[i] = x;
     if (co) co[i] = x * idg[i];
     d += std::fabs((double)x - (double)rp[i]);

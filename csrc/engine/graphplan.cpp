@@ -375,6 +375,7 @@ void PageRankPlan::reset() {
   c_ = r_ * invdeg_;
   dmass_ = at::full({1}, (double)ndangling / (double)N, opt(dev, at::kDouble));
   stats_ = at::zeros({2}, opt(dev, at::kDouble));
+  acc_.zero_();
 }
 
 void PageRankPlan::step() {
@@ -387,9 +388,9 @@ void PageRankPlan::step() {
                  pb_ub_.data_ptr<int32_t>(), pb_ue0_.data_ptr<int64_t>(), pb_ue1_.data_ptr<int64_t>(),
                  pb_uex_.data_ptr<uint8_t>(), pb_nunit_, nlocal, acc_.data_ptr<float>(), s);
   } else {
+    // acc_ is zero here: reset() and every pr_update leave it so
     if (six_.defined()) seg_gather_reduce(six_, src_, c_, at::Tensor(), 0, send_);
     else if (send_.numel()) pr_contrib(seg_, src_, w_, c_, send_);
-    acc_.zero_();
   }
   if (pb_) {
   } else if (comm->distributed()) {

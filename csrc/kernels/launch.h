@@ -174,7 +174,7 @@ void pr_combine(const int64_t* seg, int64_t ngrp, int64_t nrecv, const int32_t* 
                 const int32_t* vid, float* grp, float* acc, void* scratch, hipStream_t s);
 void scatter_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s);
 int pr_update_blocks(int64_t n);
-void pr_update(const float* acc, const float* r, float* rn, const uint8_t* dangling, int64_t n, float base,
+void pr_update(float* acc, const float* r, float* rn, const uint8_t* dangling, int64_t n, float base,
                float alpha, const double* dmass, double invN, const float* invdeg, float* cout, double* partial,
                hipStream_t s);
 
