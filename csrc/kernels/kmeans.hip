@@ -206,7 +206,7 @@ __global__ __launch_bounds__(BNT) void k_kmeans_batch(const float* __restrict__ 
 // copies (no address collisions), i.e. LDS float atomics themselves run at
 // ~3 cycles per lane. Per tile of 2048 points a workgroup
 //   1. scores its points (8 per lane, {-2c, |c|^2} LDS broadcast) and
-//      writes (cluster, x) of the tile to LDS in SoA;
+//      writes the tile's clusters and coordinates (point-major) to LDS;
 //   2. transposes the reduction: lane l owns clusters l%32 (+32 g) and the
 //      half l/32 of its wave's 512 points, and walks them with broadcast LDS
 //      reads (4 points per ds_read_b128), adding the coordinates of the
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(TNT) void k_kmeans_tr(const float* __restrict__ pts
   extern __shared__ float sh[];
   float4* c4 = reinterpret_cast<float4*>(sh);       // K x {-2c, |c|^2}
   int* sbk = reinterpret_cast<int*>(sh + 4 * K);    // TTILE cluster ids
-  float* sx = sh + 4 * K + TTILE;                   // D x TTILE coordinates
+  float* sx = sh + 4 * K + TTILE;                   // TTILE x D coordinates
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int kk = tid; kk < K; kk += TNT) {
     float v[4] = {0.f, 0.f, 0.f, 0.f};
@@ -235,10 +235,10 @@ __global__ __launch_bounds__(TNT) void k_kmeans_tr(const float* __restrict__ pts
     c4[kk] = make_float4(v[0], v[1], v[2], v[3]);
   }
   float s[KG][D];
-  int cnt[KG];
+  float cnt[KG];
 #pragma unroll
   for (int g = 0; g < KG; ++g) {
-    cnt[g] = 0;
+    cnt[g] = 0.f;
 #pragma unroll
     for (int d = 0; d < D; ++d) s[g][d] = 0.f;
   }
@@ -280,27 +280,32 @@ __global__ __launch_bounds__(TNT) void k_kmeans_tr(const float* __restrict__ pts
       const int j = r * TNT + tid;
       sbk[j] = (base + j < n) ? bk[r] : -1;  // tail points belong to no cluster
 #pragma unroll
-      for (int d = 0; d < D; ++d) sx[d * TTILE + j] = x[r][d];
+      for (int d = 0; d < D; ++d) sx[j * D + d] = x[r][d];  // AoS: a point's coordinates adjacent
     }
     __syncthreads();
     for (int j = j0; j < j0 + TTILE / 8; j += 4) {
       const int4 b4 = *reinterpret_cast<const int4*>(sbk + j);
-      float4 x4[D];
+      float xs[4 * D];  // 4 points x D coordinates, D 16-byte broadcast reads
 #pragma unroll
-      for (int d = 0; d < D; ++d) x4[d] = *reinterpret_cast<const float4*>(sx + d * TTILE + j);
+      for (int v = 0; v < D; ++v) {
+        const float4 t = *reinterpret_cast<const float4*>(sx + j * D + 4 * v);
+        xs[4 * v] = t.x;
+        xs[4 * v + 1] = t.y;
+        xs[4 * v + 2] = t.z;
+        xs[4 * v + 3] = t.w;
+      }
       const int bb[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
       for (int g = 0; g < KG; ++g) {
         const int c = g * 32 + own;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const bool m = bb[q] == c;
+          // one select + D+1 FMAs per point: the count rides along as a float
+          // (exact: a lane adds at most ~n / (64 x grid) ones)
+          const float m = bb[q] == c ? 1.f : 0.f;
           cnt[g] += m;
 #pragma unroll
-          for (int d = 0; d < D; ++d) {
-            const float xv = q == 0 ? x4[d].x : q == 1 ? x4[d].y : q == 2 ? x4[d].z : x4[d].w;
-            s[g][d] += m ? xv : 0.f;
-          }
+          for (int d = 0; d < D; ++d) s[g][d] = fmaf(m, xs[q * D + d], s[g][d]);
         }
       }
     }
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(TNT) void k_kmeans_tr(const float* __restrict__ pts
     if (c < K) {
 #pragma unroll
       for (int d = 0; d < D; ++d) red[owner * R + c * (D + 1) + d] = s[g][d];
-      red[owner * R + c * (D + 1) + D] = (float)cnt[g];
+      red[owner * R + c * (D + 1) + D] = cnt[g];
     }
   }
   __syncthreads();
