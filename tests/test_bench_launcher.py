@@ -40,6 +40,16 @@ def test_bench_spawns_n_ranks():
         assert k in three
 
 
+def test_bench_eight_ranks():
+    """the driver's largest scaling point, N = 8 (one node), rehearsed on the
+    CPU engine: 8 ranks join, global counts are 8x, PageRank keeps its graph"""
+    one, eight = _bench(1), _bench(8)
+    assert eight["n_gpus"] == eight["rccl_ranks"] == 8 and eight["config"]["parallelism"] == "dp8"
+    assert eight["kv_pairs_per_step"] == 8 * one["kv_pairs_per_step"]
+    assert eight["pagerank_config"]["edges"] == one["pagerank_config"]["edges"]
+    assert "pagerank_error" not in eight
+
+
 def test_bench_rejects_world_size_mismatch():
     env = dict(os.environ, WORLD_SIZE="2", RANK="0", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", *ARGS], cwd=ROOT, env=env,
