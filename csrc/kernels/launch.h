@@ -229,6 +229,28 @@ void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int6
 // K * K / 8 bytes (K a multiple of 64, <= 524288)
 void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64_t K, int64_t u0, int64_t u1,
                    uint64_t* H, unsigned long long* total, hipStream_t s);
+// ---------------------------------------------------------------- ccmr.hip
+// cc_find_mr callbacks (oink/cc_find.cpp:119-330); zone keys carry the hot
+// bit 63 and the salting rank at pshift. Emitting steps take pos = exclusive
+// scan of their flags (ccmr_len_flags / _winner_flags / _hot_flags).
+void ccmr_len_flags(const int64_t* voff, int64_t nval, int64_t w, int64_t* f, hipStream_t s);
+void ccmr_edge_zone_of(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vd, int64_t nval,
+                       int64_t* zone_of, hipStream_t s);
+void ccmr_edge_zone_emit(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vd, int64_t nval,
+                         const int64_t* zone_of, const int64_t* pos, int64_t* edge, int64_t* zone, hipStream_t s);
+void ccmr_winner_flags(const int64_t* seg, int64_t nkey, const int64_t* z, int64_t nval, int64_t* f, hipStream_t s);
+void ccmr_winner_emit(const int64_t* seg, int64_t nkey, const int64_t* z, int64_t nval, const int64_t* pos,
+                      int64_t* big, int64_t* pad, hipStream_t s);
+void ccmr_invert(const int64_t* v, const int64_t* zn, int64_t n, int P, int pshift, uint64_t seed, int64_t* key,
+                 int64_t* val, hipStream_t s);
+void ccmr_hot_flags(const int64_t* zn, int64_t n, int64_t* f, hipStream_t s);
+void ccmr_zone_multi(const int64_t* zn, const int64_t* pad, int64_t n, int P, int pshift, const int64_t* pos,
+                     int64_t* key, int64_t* val, hipStream_t s);
+void ccmr_reassign_seg(const int64_t* seg, int64_t nkey, const int64_t* keys, const int64_t* voff, const uint8_t* vd,
+                       int64_t lmask, int64_t nthresh, int64_t* zone_out, hipStream_t s);
+void ccmr_reassign_emit(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vd, int64_t nval,
+                        const int64_t* zone_seg, const int64_t* pos, int64_t* v, int64_t* zone, hipStream_t s);
+
 // ---------------------------------------------------------------- trimr.hip
 // tri_find_mr callbacks (oink/tri_find.cpp:104-325); edge rows are int64
 // pairs, degree rows int32 pairs

@@ -17,6 +17,7 @@
 #include <ATen/CPUGeneratorImpl.h>
 
 #include "callbacks.h"
+#include "engine/ccmr.h"
 #include "engine/graphplan.h"
 #include "engine/tri.h"
 #include "oink.h"
@@ -606,7 +607,6 @@ class CCFindMR : public Command {
     while ((int64_t(1) << pbits) < P) ++pbits;
     const int pshift = 63 - pbits;                         // rank id sits just under the high bit
     const int64_t lmask = (int64_t)(~0ull >> (pbits + 1));  // strips the high bit and the rank id
-    at::Generator gen = at::make_generator<at::CPUGeneratorImpl>(123456789 + (uint64_t)me);
     MapReduce& mre = obj.input(1, rd(parse_edge), rc(parse_edge));
     MapReduce& mrv = obj.create_mr();
     MapReduce& mrz = obj.create_mr();
@@ -634,68 +634,35 @@ class CCFindMR : public Command {
       mrz.collate();
       mrz.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_edge_zone: (edge, zone of this end)
         if (!m.nval) return;
-        at::Tensor vl = kmv_vlens(m), vs = kmv_vstart(m), sid = kmv_sid(m);
-        at::Tensor is_zone = vl == 8, is_edge = vl == 16;
-        at::Tensor zone_of = at::zeros({m.nkey}, opt(m.seg.device(), at::kLong));
-        zone_of.index_put_({sid.index({is_zone})}, gather_bytes(m.vdata, vs.index({is_zone}), 8).view(at::kLong).reshape({-1}));
-        at::Tensor ed = gather_bytes(m.vdata, vs.index({is_edge}), 16).view(at::kLong).view({-1, 2});
-        if (ed.numel()) add_tensors(kv, ed, zone_of.index({sid.index({is_edge})}));
+        auto [ed, zn] = ccmr_edge_zone(m);
+        if (ed.numel()) add_tensors(kv, ed, zn);
       });
       mrz.collate();
       int64_t changed = 0;
       mrz.reduce_batch([&](const KMV& m, KeyValue& kv) {  // reduce_zone_winner
         if (!m.nkey) return;
-        at::Tensor z = m.vdata.view(at::kLong), h = m.seg.narrow(0, 0, m.nkey);
-        at::Tensor z0 = z.index({h}), z1 = z.index({at::clamp_max(h + 1, m.nval - 1)});
-        at::Tensor s0 = at::bitwise_and(z0, ~HIBIT), s1 = at::bitwise_and(z1, ~HIBIT);
-        at::Tensor diff = s0 != s1;
-        changed = diff.sum().item<int64_t>();
-        if (!changed) return;
-        at::Tensor big = at::where(s0 > s1, z0, z1).index({diff}), small = at::where(s0 > s1, z1, z0).index({diff});
-        // value = PAD {winner zone, pad}: 16 bytes tell it apart from an 8-byte vertex
-        add_tensors(kv, big, at::stack({small, at::zeros_like(small)}, 1));
+        auto [big, pad] = ccmr_winner(m);  // value = PAD {winner zone, 0}: 16 bytes tell it apart from a vertex
+        changed += big.numel();
+        if (big.numel()) add_tensors(kv, big, pad);
       });
       if (comm->allreduce(changed, Comm::SUM) == 0) break;
       // vertices of hot zones go to a random salted copy of their zone key
+      const uint64_t seed = 0x9E3779B97F4A7C15ull * (uint64_t)(niter + 1) ^ (123456789ull + (uint64_t)me);
       mrv.map_mr_batch(mrv, [&](const KV& src, KeyValue& kv) {  // map_invert_multi
         if (!src.n) return;
-        at::Tensor v = src.kdata.view(at::kLong), zn = src.vdata.view(at::kLong);
-        at::Tensor hot = zn < 0;
-        at::Tensor rp = at::randint(P, {src.n}, gen, at::TensorOptions().dtype(at::kLong)).to(zn.device());
-        add_tensors(kv, at::where(hot, at::bitwise_or(zn, at::bitwise_left_shift(rp, pshift)), zn), v);
+        auto [key, v] = ccmr_invert(src, (int)P, pshift, seed);
+        add_tensors(kv, key, v);
       });
       mrv.map_mr_batch(mrz, [&](const KV& src, KeyValue& kv) {  // map_zone_multi: replicate to every salted key
         if (!src.n) return;
-        at::Tensor zn = src.kdata.view(at::kLong), pad = src.vdata.view(at::kLong).view({-1, 2});
-        at::Tensor hot = zn < 0, strip = at::bitwise_and(zn, ~HIBIT);
-        add_tensors(kv, strip, pad);
-        if (!hot.any().item<bool>()) return;
-        at::Tensor hz = strip.index({hot}), hp = pad.index({hot});
-        for (int64_t r = 0; r < P; ++r)
-          add_tensors(kv, at::bitwise_or(at::bitwise_or(hz, r << pshift), HIBIT), hp);
+        auto [key, pad] = ccmr_zone_multi(src, (int)P, pshift);
+        add_tensors(kv, key, pad);
       }, 1);
       mrv.collate();
       mrv.reduce_batch([&](const KMV& m, KeyValue& kv) {  // reduce_zone_reassign
         if (!m.nkey) return;
-        at::Tensor key = m.keys.kdata.view(at::kLong);
-        at::Tensor vl = kmv_vlens(m), vs = kmv_vstart(m), sid = kmv_sid(m);
-        at::Tensor isv = vl == 8, isp = vl == 16;
-        at::Tensor zone = at::bitwise_and(key, lmask), hkey = key < 0;
-        at::Tensor hwin = at::zeros({m.nkey}, opt(m.seg.device(), at::kBool));
-        if (isp.any().item<bool>()) {
-          at::Tensor pz = gather_bytes(m.vdata, vs.index({isp}), 8).view(at::kLong).reshape({-1});
-          at::Tensor ps = sid.index({isp}), pzs = at::bitwise_and(pz, ~HIBIT);
-          at::Tensor best = zone.clone().scatter_reduce_(0, ps, pzs, "amin", true);
-          // the winner's high bit comes along when a strictly smaller zone wins
-          at::Tensor won = at::logical_and(pzs == best.index({ps}), pzs < zone.index({ps}));
-          hwin.index_put_({ps.index({at::logical_and(won, pz < 0)})}, true);
-          zone = best;
-        }
-        at::Tensor nvert = bincount_dev(sid.index({isv}), m.nkey);
-        at::Tensor hot = at::logical_or(at::logical_or(hkey, hwin), nvert > nthresh);
-        zone = at::where(hot, at::bitwise_or(zone, HIBIT), zone);
-        at::Tensor v = gather_bytes(m.vdata, vs.index({isv}), 8).view(at::kLong).reshape({-1});
-        if (v.numel()) add_tensors(kv, v, zone.index({sid.index({isv})}));
+        auto [v, zone] = ccmr_reassign(m, lmask, nthresh);
+        if (v.numel()) add_tensors(kv, v, zone);
       });
     }
     mrv.map_mr_batch(mrv, [&](const KV& src, KeyValue& kv) {  // map_strip

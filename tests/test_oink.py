@@ -13,10 +13,10 @@ from gpu_mapreduce_amd.oink.interp import OINK
 from gpu_mapreduce_amd.oink.variable import OinkError
 
 
-def run(script, tmp_path, monkeypatch, variables=None):
+def run(script, tmp_path, monkeypatch, variables=None, comm=None):
     monkeypatch.chdir(tmp_path)
     out = io.StringIO()
-    o = OINK(screen=out, logfile="log.oink", variables=variables)
+    o = OINK(comm, screen=out, logfile="log.oink", variables=variables)
     o.file(text=script)
     return o, out.getvalue()
 
@@ -105,17 +105,21 @@ def test_cc_find_stats(tmp_path, monkeypatch):
     assert f"CCStats: {ncc} components, {present.sum()} vertices" in text
 
 
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
 @pytest.mark.parametrize("nthresh", [1000000, 2])
-def test_cc_find_mr_zone_salting(tmp_path, monkeypatch, nthresh):
-    """cc_find_mr: the reference's zone pipeline (oink/cc_find.cpp:38-109).
-    With nthresh = 2 nearly every zone becomes 'hot' and its vertices are
-    salted over ranks; the components must not change."""
+def test_cc_find_mr_zone_salting(tmp_path, monkeypatch, nthresh, dev):
+    """cc_find_mr: the reference's zone pipeline (oink/cc_find.cpp:38-109),
+    callbacks as the ccmr kernels on cuda / their host twins on cpu. With
+    nthresh = 2 nearly every zone becomes 'hot' and its vertices are salted
+    over ranks; the components must not change."""
     from gpu_mapreduce_amd.models.graph import reference_cc
-    s = ("rmat 8 1 0.25 0.25 0.25 0.25 0.0 99 -o tmp.rmat mre\n"
+    from gpu_mapreduce_amd.parallel.comm import Comm
+    scale = 8 if dev == "cpu" else 12
+    s = (f"rmat {scale} 1 0.25 0.25 0.25 0.25 0.0 99 -o tmp.rmat mre\n"
          "edge_upper -i mre -o NULL mre\n"
          f"cc_find_mr {nthresh} -i mre -o tmp.ccmr mrc\n"
          "cc_stats -i mrc\n")
-    o, text = run(s, tmp_path, monkeypatch)
+    o, text = run(s, tmp_path, monkeypatch, comm=Comm(device=dev))
     e = _upper(load_edges(tmp_path / "tmp.rmat.0"))
     n = int(e.max()) + 1
     lab = reference_cc(e, n)
