@@ -149,10 +149,7 @@ __global__ __launch_bounds__(BNT) void k_kmeans_batch(const float* __restrict__ 
   }
   for (int i = threadIdx.x; i < BC * RS; i += BNT) part[i] = 0.f;
   __syncthreads();
-  // grid-stride over tiles of BNT * PB points: a capped grid keeps adding
-  // into the same LDS partials, so the fp64 global atomics on the K * (D+1)
-  // accumulators (one per partial per workgroup, all on a few hot addresses)
-  // shrink with the grid instead of growing with n
+  // grid-stride over tiles of BNT * PB points (any grid size is correct)
   const int64_t ntiles = (n + (int64_t)BNT * PB - 1) / ((int64_t)BNT * PB);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t base = tile * BNT * PB + threadIdx.x;
@@ -609,13 +606,9 @@ void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, h
     }
     if (variant != 1 && batch_lds(D, K, 1) <= 64 * 1024) {
       const int bc = variant == 5 ? 1 : batch_copies(D, K);  // 5: one shared copy (the r1 kernel)
-      // MRH_KMEANS_BLOCKS caps the grid (0 = one workgroup per tile)
-      static const int64_t cap = [] {
-        const char* e = std::getenv("MRH_KMEANS_BLOCKS");
-        return e ? std::atoll(e) : (int64_t)0;
-      }();
-      int64_t nb = (n + (int64_t)BNT * PB - 1) / ((int64_t)BNT * PB);
-      if (cap > 0 && nb > cap) nb = cap;
+      // one workgroup per tile: capping the grid (fewer fp64 flush atomics)
+      // measured no faster (profiles/r2_kmeans_tr.txt)
+      const int64_t nb = (n + (int64_t)BNT * PB - 1) / ((int64_t)BNT * PB);
       const size_t lds = batch_lds(D, K, bc);
       hipLaunchKernelGGL((k_kmeans_batch<D>), dim3((unsigned)nb), dim3(BNT), lds, s, pts, n, cen, K, bc, acc);
       MRH_CHECK_LAUNCH();

@@ -6,7 +6,8 @@
 // and the hash-table group-by of KeyMultiValue::convert (src/keymultivalue.cpp:645-789).
 //
 //   k_global_hist : one read of the keys -> the digit histograms of all eight
-//                   8-bit digit positions (LDS atomics, one global atomic per bin)
+//                   8-bit digit positions (LDS atomics, one per wave for a
+//                   digit uniform over the wave; one global atomic per bin)
 //   k_digit_base  : per digit position, the exclusive scan of its 256 counts =
 //                   the global start of every digit (no host round trip)
 //   k_onesweep    : one kernel per pass. A workgroup takes the next 4096-pair
@@ -54,11 +55,25 @@ __global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restric
   __shared__ uint32_t h[8][RX_BINS];
   for (int i = threadIdx.x; i < 8 * RX_BINS; i += RX_NT) (&h[0][0])[i] = 0;
   __syncthreads();
+  const int lane = dev::lane_id();
   for (int64_t i = (int64_t)blockIdx.x * RX_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * RX_NT) {
     uint64_t k = keys[i];
+    const uint64_t active = __ballot(1);
+    const int first = __ffsll((long long)active) - 1;
 #pragma unroll
     for (int p = 0; p < 8; ++p)
-      if (p >= p0 && p < p1) atomicAdd(&h[p][(k >> (8 * p)) & 255], 1u);
+      if (p >= p0 && p < p1) {
+        // a digit that is the same on every active lane (the constant high
+        // bytes of small ids, or runs of sorted keys) is one add of the lane
+        // count: same-address LDS atomics from 64 lanes serialise
+        const uint32_t d = (uint32_t)(k >> (8 * p)) & 255u;
+        const uint32_t d0 = (uint32_t)__shfl((int)d, first, MRH_WAVE);
+        if (__ballot(d == d0) == active) {
+          if (lane == first) atomicAdd(&h[p][d0], (uint32_t)__popcll(active));
+        } else {
+          atomicAdd(&h[p][d], 1u);
+        }
+      }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 8 * RX_BINS; i += RX_NT) {
