@@ -224,7 +224,10 @@ void plan_combine(int dtype, const int64_t* seg, int64_t ngrp, int64_t nrecv, co
 }
 int64_t ws_words(int64_t nval) { return dev::ws_head_words(nval); }
 int64_t ws_waves(int64_t nval) { return dev::ws_nwave(nval); }
-size_t ws_scratch_bytes(int64_t nval) { return (size_t)dev::ws_nwave(nval) * 2 * 16 + 64; }
+size_t ws_scratch_bytes(int64_t nval) {
+  const int64_t nc = dev::ws_nwave(nval) * 2, nc2 = 2 * ((nc + 63) / 64);
+  return (size_t)nc * 16 + (size_t)nc2 * 16 + 64;
+}
 
 void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64_t* wbase, hipStream_t s) {
   const int64_t nw = dev::ws_nwave(nval);
@@ -239,11 +242,16 @@ void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64
 template <typename T>
 static void ws_gr_t(const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src, const T* x, const T* w,
                     int op, T* out, void* scratch, hipStream_t s) {
-  int64_t* cs = reinterpret_cast<int64_t*>(scratch);
-  T* cv = reinterpret_cast<T*>(reinterpret_cast<char*>(scratch) + (size_t)dev::ws_nwave(nval) * 2 * sizeof(int64_t));
-  if (op == 0) dev::ws_gather_reduce<T, 0>(H, wbase, nval, src, x, w, out, cs, cv, s);
-  else if (op == 1) dev::ws_gather_reduce<T, 1>(H, wbase, nval, src, x, w, out, cs, cv, s);
-  else dev::ws_gather_reduce<T, 2>(H, wbase, nval, src, x, w, out, cs, cv, s);
+  // scratch: carry (2 nw) ids + values, then the level-2 carry (2 ceil(2 nw / 64)) ids + values
+  const int64_t nc = dev::ws_nwave(nval) * 2, nc2 = 2 * ((nc + 63) / 64);
+  char* p = reinterpret_cast<char*>(scratch);
+  int64_t* cs = reinterpret_cast<int64_t*>(p);
+  T* cv = reinterpret_cast<T*>(p + (size_t)nc * sizeof(int64_t));
+  int64_t* cs2 = reinterpret_cast<int64_t*>(p + (size_t)nc * 16);
+  T* cv2 = reinterpret_cast<T*>(p + (size_t)nc * 16 + (size_t)nc2 * sizeof(int64_t));
+  if (op == 0) dev::ws_gather_reduce<T, 0>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2);
+  else if (op == 1) dev::ws_gather_reduce<T, 1>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2);
+  else dev::ws_gather_reduce<T, 2>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2);
 }
 
 void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src,

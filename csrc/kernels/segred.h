@@ -187,6 +187,68 @@ __global__ __launch_bounds__(SR_NT) void k_segred_carry(const int64_t* __restric
   out[s] = acc;
 }
 
+// Two-level carry fold for long carry arrays (k_segred_carry folds a run of
+// equal segment ids serially in one thread, so one segment spanning
+// thousands of tiles — an R-MAT hub's in-edges — serialises the launch).
+// Level 1: one wave per 64 carry entries; invalid (-1) entries join the run
+// before them with the identity (valid ids are non-decreasing); a segmented
+// wave scan reduces every run in entry order; runs that start and end inside
+// the wave are final, the wave's first and last runs go to slots 0 / 1 of
+// the level-2 carry (cs2 = -1 initialised), which k_segred_carry folds.
+// The fold order is fixed: results are bitwise reproducible.
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void k_carry_fold(const int64_t* __restrict__ cs, const T* __restrict__ cv,
+                                                   int64_t nc, T* __restrict__ out, int64_t* __restrict__ cs2,
+                                                   T* __restrict__ cv2) {
+  using R = RedOp<T, OP>;
+  const int lane = threadIdx.x & 63;
+  const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t j = wv * 64 + lane;
+  int64_t s = -1;
+  T v = R::ident();
+  if (j < nc) {
+    s = cs[j];
+    if (s >= 0) v = cv[j];
+  }
+  const uint64_t valid = __ballot(s >= 0);
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(s, d, 64);
+    if (lane >= d && y > s) s = y;
+  }
+  const int64_t sp = __shfl_up(s, 1, 64), sn = __shfl_down(s, 1, 64);
+  const bool head = lane == 0 || s != sp;
+  const uint64_t heads = __ballot(head);
+  T S = v;
+  int F = head;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T ys = __shfl_up(S, d, 64);
+    const int yf = __shfl_up(F, d, 64);
+    if (lane >= d) {
+      if (!F) S = R::f(ys, S);
+      F |= yf;
+    }
+  }
+  const bool tail = lane == 63 || s != sn;
+  if (!tail || s < 0) return;
+  // the wave's first run is the one holding its first valid entry fv (it may
+  // continue a run of the previous wave across invalid entries): no head in
+  // lanes (fv, lane]; the last run reaches lane 63
+  const int fv = __ffsll((long long)valid) - 1;  // valid != 0: a tail with s >= 0 exists
+  const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  const uint64_t after_fv = ~((2ull << fv) - 1ull);
+  const bool first = (heads & upto & after_fv) == 0ull;
+  const bool last = lane == 63;
+  if (first || last) {
+    const int slot = first ? 0 : 1;
+    cs2[2 * wv + slot] = s;
+    cv2[2 * wv + slot] = S;
+  } else {
+    out[s] = S;
+  }
+}
+
 // host launcher: carry buffers need 2*nblocks entries each
 template <typename T, int OP, typename G>
 inline void segred_launch(G get, const int64_t* seg, int64_t nseg, int64_t nval, T* out, int64_t* carry_seg,

@@ -168,7 +168,8 @@ __global__ __launch_bounds__(WS_NT) void k_ws_gather_reduce(const uint32_t* __re
 // launcher; carry buffers need 2*ws_nwave(nval) entries each
 template <typename T, int OP>
 inline void ws_gather_reduce(const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src, const T* x,
-                             const T* w, T* out, int64_t* carry_seg, T* carry_val, hipStream_t s) {
+                             const T* w, T* out, int64_t* carry_seg, T* carry_val, hipStream_t s,
+                             int64_t* carry2_seg = nullptr, T* carry2_val = nullptr) {
   if (nval <= 0) return;
   const int64_t nw = ws_nwave(nval);
   hipMemsetAsync(carry_seg, 0xff, sizeof(int64_t) * 2 * nw, s);
@@ -177,6 +178,17 @@ inline void ws_gather_reduce(const uint32_t* H, const int64_t* wbase, int64_t nv
                      out, carry_seg, carry_val);
   MRH_CHECK_LAUNCH();
   const int64_t nc = 2 * nw;
+  if (carry2_seg && nc > 4096) {  // two-level fold (k_carry_fold): long runs in parallel
+    const int64_t nw1 = (nc + 63) / 64;
+    hipMemsetAsync(carry2_seg, 0xff, sizeof(int64_t) * 2 * nw1, s);
+    hipLaunchKernelGGL((k_carry_fold<T, OP>), dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, carry_seg,
+                       carry_val, nc, out, carry2_seg, carry2_val);
+    MRH_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_segred_carry<T, OP>), dim3((unsigned)((2 * nw1 + SR_NT - 1) / SR_NT)), dim3(SR_NT), 0, s,
+                       carry2_seg, carry2_val, 2 * nw1, out);
+    MRH_CHECK_LAUNCH();
+    return;
+  }
   hipLaunchKernelGGL((k_segred_carry<T, OP>), dim3((unsigned)((nc + SR_NT - 1) / SR_NT)), dim3(SR_NT), 0, s, carry_seg,
                      carry_val, nc, out);
   MRH_CHECK_LAUNCH();

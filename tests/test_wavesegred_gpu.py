@@ -63,3 +63,30 @@ def test_ws_gather_reduce(kind, n, dtype, op):
     else:
         tol = 1e-4 if dtype == torch.float32 else 1e-10
         np.testing.assert_allclose(g, ref, rtol=tol, atol=tol * 10)
+
+
+@pytest.mark.parametrize("kind", ["ones", "hub", "long", "mixed"])
+@pytest.mark.parametrize("dtype,op", [(torch.float64, 0), (torch.int64, 2), (torch.int64, 1)])
+def test_ws_gather_reduce_two_level_carry(kind, dtype, op):
+    """5 M values = 4883 wave tiles: the carry array (2 per tile) is folded in
+    two levels (k_carry_fold + k_segred_carry); a hub segment spans half of
+    all tiles"""
+    n = 5_000_000
+    rng = np.random.default_rng(17 + op)
+    seg = _layout(kind, n, rng)
+    ne = int(seg[-1])
+    nx = 100_000
+    src = rng.integers(0, nx, size=ne).astype(np.int32)
+    if dtype == torch.int64:
+        x = rng.integers(-10**9, 10**9, size=nx).astype(np.int64)
+    else:
+        x = rng.standard_normal(nx)
+    got = C.seg_gather_reduce(torch.from_numpy(seg).to(DEV), torch.from_numpy(src).to(DEV),
+                              torch.from_numpy(x).to(DEV), None, op).cpu().numpy()
+    v = x[src]
+    red = {0: np.add, 1: np.minimum, 2: np.maximum}[op]
+    ref = red.reduceat(v, seg[:-1])
+    if dtype == torch.int64:
+        assert np.array_equal(got, ref)
+    else:
+        np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-9)
