@@ -260,12 +260,30 @@ inline void segred_launch(G get, const int64_t* seg, int64_t nseg, int64_t nval,
                      carry_seg, carry_val);
   MRH_CHECK_LAUNCH();
   int64_t nc = 2 * nb;
+  if (nc > 4096) {  // two-level fold; the level-2 carry sits behind the first (segred_carry_entries)
+    const int64_t nw1 = (nc + 63) / 64;
+    int64_t* cs2 = carry_seg + nc;
+    T* cv2 = carry_val + nc;
+    hipMemsetAsync(cs2, 0xff, sizeof(int64_t) * 2 * nw1, s);
+    hipLaunchKernelGGL((k_carry_fold<T, OP>), dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, carry_seg,
+                       carry_val, nc, out, cs2, cv2);
+    MRH_CHECK_LAUNCH();
+    hipLaunchKernelGGL((k_segred_carry<T, OP>), dim3((unsigned)((2 * nw1 + SR_NT - 1) / SR_NT)), dim3(SR_NT), 0, s,
+                       cs2, cv2, 2 * nw1, out);
+    MRH_CHECK_LAUNCH();
+    return;
+  }
   hipLaunchKernelGGL((k_segred_carry<T, OP>), dim3((unsigned)((nc + SR_NT - 1) / SR_NT)), dim3(SR_NT), 0, s,
                      carry_seg, carry_val, nc, out);
   MRH_CHECK_LAUNCH();
 }
 
-inline size_t segred_carry_entries(int64_t nval) { return 2 * (size_t)((nval + SR_TILE - 1) / SR_TILE) + 2; }
+// carry entries a segred_launch needs per array: 2 per tile, plus the
+// level-2 carry of the two-level fold (2 per 64 first-level entries)
+inline size_t segred_carry_entries(int64_t nval) {
+  const size_t nc = 2 * (size_t)((nval + SR_TILE - 1) / SR_TILE);
+  return nc + 2 * ((nc + 63) / 64) + 2;
+}
 
 }  // namespace dev
 }  // namespace mrh

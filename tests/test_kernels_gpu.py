@@ -261,3 +261,27 @@ def test_inverted_index_bench_scale_gpu():
         url, rest = line.split("\t")
         got[url.encode()] = sorted(rest.split())
     assert got == reference_inverted_index(files)
+
+
+@pytest.mark.parametrize("dtype,np_t", [("int64", np.int64), ("float64", np.float64)])
+@pytest.mark.parametrize("op", ["sum", "max"])
+def test_reduce_builtin_hub_two_level_carry(dtype, np_t, op):
+    """12 M values, one key holding 8 M of them: the segmented reduce spans
+    2900 tiles, whose carries are folded in two levels (k_carry_fold)"""
+    rng = np.random.default_rng(5)
+    n, hub = 12_000_000, 8_000_000
+    k = np.concatenate([rng.integers(0, 500_000, n - hub), np.full(hub, 123_456)]).astype(np.int64)
+    v = rng.integers(-1000, 1000, n).astype(np_t)
+    kv = C.make_kv(torch.from_numpy(k), None, torch.from_numpy(v), None, n, DEV)
+    kg, _ = C.convert(kv)
+    rg = C.reduce_builtin(kg, op, dtype)
+    keys = np.frombuffer(bytes(rg.kdata.cpu().numpy()), dtype=np.int64)
+    got = np.frombuffer(bytes(rg.vdata.cpu().numpy()), dtype=np_t)
+    order = np.argsort(k, kind="stable")
+    ks, vs = k[order], v[order]
+    heads = np.concatenate([[0], np.nonzero(np.diff(ks))[0] + 1])
+    ref = (np.add if op == "sum" else np.maximum).reduceat(vs, heads)
+    ref_keys = ks[heads]
+    pos = np.argsort(keys)
+    assert np.array_equal(keys[pos], ref_keys)
+    assert np.array_equal(got[pos], ref)  # integer-valued: exact in float64 too
