@@ -33,8 +33,11 @@ class KMeans:
         self.centroids = centroids.to(points.device, torch.float32).contiguous()
         self.K, self.D = self.centroids.shape
 
-    def iterate(self):
-        """one Lloyd iteration; returns the global point count"""
+    def iterate(self, sync=True):
+        """one Lloyd iteration; returns the global point count (sync=False:
+        returns None and leaves the shift / count on the device, read through
+        the `shift` / `npoints` properties — no host round trip per
+        iteration)"""
         K, D = self.K, self.D
         mr = MapReduce(self.comm)
         mr.map(mr.nprocs, lambda itask, kv: kv.add_kv(C.kmeans_map(self.points, self.centroids)))
@@ -50,11 +53,21 @@ class KMeans:
         acc = acc.view(K, D + 1)
         cnt = acc[:, D:]
         new = torch.where(cnt > 0, acc[:, :D] / cnt.clamp_min(1), self.centroids.double())
-        self.shift = float((new - self.centroids.double()).norm(dim=1).max())
+        self._shift = (new - self.centroids.double()).norm(dim=1).max()
         self.centroids = new.float().contiguous()
         self.counts = cnt.squeeze(1).long()
-        self.npoints = int(self.counts.sum())
-        return self.npoints
+        self._npoints = self.counts.sum()
+        return self.npoints if sync else None
+
+    @property
+    def shift(self):
+        """largest centroid move of the last iteration"""
+        return float(self._shift)
+
+    @property
+    def npoints(self):
+        """points assigned in the last iteration (all ranks)"""
+        return int(self._npoints)
 
 
 def blobs(n, D, K, seed, device, spread=0.05):
@@ -92,7 +105,7 @@ def bench_kmeans(comm, args):
     def step():
         km = KMeans(comm, pts, init)
         for _ in range(iters):
-            km.iterate()
+            km.iterate(sync=False)
         return km
 
     for _ in range(args.warmup):
