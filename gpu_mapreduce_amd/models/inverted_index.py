@@ -62,15 +62,8 @@ class InvertedIndex:
         dev = mr.device
         self.dev = dev
         self.is_cuda = dev.startswith("cuda")
-        if self.is_cuda:
-            # pinned + non-blocking: a pageable copy would make the host wait
-            # for the device queue — the previous job's reduce tail — before
-            # this job can issue its first file's H2D, idling the PCIe link
-            self.names_dev = self.names.pin_memory().to(dev, non_blocking=True)
-            self.name_off_dev = self.name_off.pin_memory().to(dev, non_blocking=True)
-        else:
-            self.names_dev = self.names.to(dev)
-            self.name_off_dev = self.name_off.to(dev)
+        self.names_dev = self.names.to(dev)
+        self.name_off_dev = self.name_off.to(dev)
         maxlen = max((t.numel() for _, t in files), default=0)
         # two persistent staging buffers (double-buffered H2D); the PAD bytes
         # past each file are read by the 16-byte scan windows but never matched
