@@ -211,6 +211,49 @@ def bench_pagerank_extra(comm, args):
     return out
 
 
+def rccl_record(comm):
+    """What RCCL itself reports about the job's communicator, from every rank:
+    ncclCommCount (must equal N on every rank), ncclCommCuDevice, the GPU's
+    PCI bus id (N distinct GPUs must have joined) and how many RCCL
+    communicators each process holds (exactly one). At N=1 the engine runs the
+    local transport, so a one-rank probe communicator answers instead."""
+    from gpu_mapreduce_amd._ext import C
+    rec = {"engine_transport": comm.native.transport}
+    if not comm.is_cuda:
+        return rec
+    dev = torch.device(comm.device).index or 0
+    if comm.native.transport == "rccl":
+        info, probe = comm.rccl_info(), False
+    else:
+        info, probe = dict(C.rccl_self_probe(dev)), True
+        info["live_comms"] = C.live_rccl_comms()
+    mine = {"comm_count": info["comm_count"], "cu_device": info["cu_device"], "user_rank": info["user_rank"],
+            "live_comms": info["live_comms"], "pci": C.gpu_pci_bus_id(dev)}
+    allr = comm.allgather_object(mine)
+    rec.update({
+        "rccl_comm_count": allr[0]["comm_count"],
+        "rccl_cu_devices": [r["cu_device"] for r in allr],
+        "rccl_user_ranks": [r["user_rank"] for r in allr],
+        "rccl_live_comms_per_rank": [r["live_comms"] for r in allr],
+        "gpu_pci_bus_ids": [r["pci"] for r in allr],
+    })
+    if probe:
+        rec["rccl_note"] = "engine transport is not RCCL at this N (local/pg); counts from a one-rank probe communicator"
+        return rec
+    bad = []
+    if any(r["comm_count"] != comm.size for r in allr):
+        bad.append(f"ncclCommCount {[r['comm_count'] for r in allr]} != {comm.size}")
+    if sorted(r["user_rank"] for r in allr) != list(range(comm.size)):
+        bad.append(f"ncclCommUserRank {[r['user_rank'] for r in allr]}")
+    if len(set(r["pci"] for r in allr)) != comm.size:
+        bad.append(f"{len(set(r['pci'] for r in allr))} distinct GPUs for {comm.size} ranks")
+    if any(r["live_comms"] != 1 for r in allr):
+        bad.append(f"RCCL communicators per process {[r['live_comms'] for r in allr]} (expected 1)")
+    if bad:
+        raise SystemExit("bench.py: RCCL communicator check failed: " + "; ".join(bad))
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,6 +311,8 @@ def main():
     else:
         from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
         res = bench_wordfreq(comm, args)
+    # before the extras: a failing extra poisons (aborts) the communicator
+    rrec = rccl_record(comm)
     if args.workload == "invertedindex" and args.pagerank_scale > 0:
         # the headline line is printed even if the PageRank extra fails (its
         # peers fail fast through the engine's peer monitor); the error is
@@ -277,9 +322,10 @@ def main():
         except Exception as e:  # noqa: BLE001
             res["pagerank_error"] = f"{type(e).__name__}: {e}"[:500]
             print(f"bench.py rank {comm.rank}: PageRank extra failed: {e}", file=sys.stderr, flush=True)
-    res["rccl_ranks"] = comm.size
-    res["backend"] = {"torch.distributed": comm.backend or "none (world size 1)",
-                      "engine_transport": comm.native.transport}
+    res.update(rrec)
+    res["ranks_joined"] = comm.size
+    res["backend"] = {"torch.distributed": (comm.backend or "none (world size 1)") + " (host objects/scalars only)",
+                      "engine_transport": rrec["engine_transport"]}
     out = {
         "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": comm.size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],

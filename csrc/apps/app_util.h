@@ -32,7 +32,8 @@ inline int64_t file_size(const std::string& p) {
 // teardown (the same policy as the C API, csrc/capi/cmapreduce.cpp).
 [[noreturn]] inline void finish(const CommPtr& comm, int rc) {
   std::fflush(nullptr);
-  comm->shutdown();
+  if (rc != 0) comm->poison("exited with status " + std::to_string(rc));
+  else comm->shutdown();
   if (comm->device().is_cuda()) {
     hipDeviceSynchronize();
     std::_Exit(rc);

@@ -42,7 +42,12 @@ std::shared_ptr<mrh::Comm> world() {
     if (g_world->device().is_cuda()) on_exit(finish_process, nullptr);
     // registered last so it runs first: rank 0 (the rendezvous server) waits
     // for every rank to be done with the store before the process ends
-    if (g_world->size() > 1) on_exit([](int, void*) { g_world->shutdown(); }, nullptr);
+    // (a non-zero exit status is a failure: peers are told, not released)
+    if (g_world->size() > 1)
+      on_exit([](int st, void*) {
+        if (st != 0) g_world->poison("process exited with status " + std::to_string(st));
+        else g_world->shutdown();
+      }, nullptr);
   }
   return g_world;
 }

@@ -11,6 +11,7 @@
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 
 #include <cstring>
+#include <random>
 #include <string>
 
 #include "kv.h"
@@ -34,6 +35,21 @@ namespace {
 PG as_pg(py::object o) {
   if (o.is_none()) return PG();
   return o.cast<PG>();
+}
+
+// Run a collective native op (graph plans, their iterations); if it throws on
+// a multi-rank communicator, poison the job before the error reaches Python,
+// so peers blocked in the same collective fail within seconds instead of
+// waiting on a rank that has moved on (MapReduce ops do this in OpTrace).
+template <typename F>
+auto poisoning(const CommPtr& c, const char* what, F&& f) -> decltype(f()) {
+  try {
+    return f();
+  } catch (const std::exception& e) {
+    if (c && c->size() > 1) c->poison(std::string(what) + " raised an error on rank " + std::to_string(c->rank()) +
+                                      ": " + e.what());
+    throw;
+  }
 }
 
 // ---------------------------------------------------------------- host iteration helpers
@@ -188,22 +204,49 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("device", [](const KeyValue& kv) { return kv.device().str(); });
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "NativeComm")
-      .def(py::init([](py::object pg, const std::string& dev, py::object store, const std::string& transport) {
+      .def(py::init([](py::object pg, const std::string& dev, py::object store, const std::string& transport,
+                       std::vector<int> members, int world_rank, int world_size) {
              c10::intrusive_ptr<c10d::Store> st;
              if (!store.is_none()) st = store.cast<c10::intrusive_ptr<c10d::Store>>();
              PG p = as_pg(pg);
              py::gil_scoped_release nogil;  // RCCL bootstrap blocks until every rank arrives
              if (!p) return std::make_shared<Comm>(at::Device(dev));
-             return std::make_shared<Comm>(p, at::Device(dev), st, transport);
+             return std::make_shared<Comm>(p, at::Device(dev), st, transport, members, world_rank, world_size);
            }),
-           py::arg("pg"), py::arg("device"), py::arg("store") = py::none(), py::arg("transport") = "")
+           py::arg("pg"), py::arg("device"), py::arg("store") = py::none(), py::arg("transport") = "",
+           py::arg("members") = std::vector<int>{}, py::arg("world_rank") = -1, py::arg("world_size") = -1)
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("size", &Comm::size)
+      .def_property_readonly("members", &Comm::members)
       .def_property_readonly("transport", &Comm::transport)
       .def_property_readonly("distributed", &Comm::distributed)
+      .def_property_readonly("failed", [](const Comm& c) { return c.monitor() && c.monitor()->failed(); })
+      .def("rccl_info",
+           [](const Comm& c) {
+             RcclInfo i = c.rccl_info();
+             py::dict d;
+             d["comm_count"] = i.comm_count;
+             d["cu_device"] = i.cu_device;
+             d["user_rank"] = i.user_rank;
+             d["live_comms"] = i.live_comms;
+             d["id_key"] = i.id_key;
+             return d;
+           })
       .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>())
       .def("allreduce", [](const Comm& c, std::vector<int64_t> v, int op) { return c.allreduce(v, (Comm::Op)op); },
            py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_f64",
+           [](const Comm& c, std::vector<double> v, int op) { return c.allreduce_f64(v, (Comm::Op)op); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("bcast",
+           [](const Comm& c, const std::string& s, int root) {
+             std::string r;
+             {
+               py::gil_scoped_release nogil;
+               r = c.bcast(s, root);
+             }
+             return py::bytes(r);
+           })
       .def("alltoall_counts", &Comm::alltoall_counts, py::call_guard<py::gil_scoped_release>())
       .def("alltoallv", &Comm::alltoallv, py::call_guard<py::gil_scoped_release>())
       .def("allgather_var", &Comm::allgather_var, py::call_guard<py::gil_scoped_release>())
@@ -498,7 +541,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       [xo](const KV& kv, c10::optional<at::Tensor> dest, std::shared_ptr<Comm> c, int64_t chunk, bool host_sink,
            int all2all) {
         ShuffleStats st;
-        KV r = exchange(kv, dest ? *dest : at::Tensor(), *c, xo(chunk, host_sink, all2all), &st);
+        KV r = poisoning(c, "exchange", [&] { return exchange(kv, dest ? *dest : at::Tensor(), *c, xo(chunk, host_sink, all2all), &st); });
         return std::make_pair(r, st);
       },
       py::arg("kv"), py::arg("dest"), py::arg("comm"), py::arg("chunk_bytes") = 0, py::arg("host_sink") = false,
@@ -507,7 +550,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       "aggregate",
       [xo](const KV& kv, std::shared_ptr<Comm> c, int64_t chunk, bool host_sink, int all2all) {
         ShuffleStats st;
-        KV r = mrh::aggregate(kv, *c, xo(chunk, host_sink, all2all), &st);
+        KV r = poisoning(c, "aggregate", [&] { return mrh::aggregate(kv, *c, xo(chunk, host_sink, all2all), &st); });
         return std::make_pair(r, st);
       },
       py::arg("kv"), py::arg("comm"), py::arg("chunk_bytes") = 0, py::arg("host_sink") = false,
@@ -516,12 +559,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       "gather_to",
       [](const KV& kv, int nprocs, std::shared_ptr<Comm> c) {
         ShuffleStats st;
-        KV r = gather_to(kv, nprocs, *c, ExchangeOpts(), &st);
+        KV r = poisoning(c, "gather_to", [&] { return gather_to(kv, nprocs, *c, ExchangeOpts(), &st); });
         return std::make_pair(r, st);
       },
       py::call_guard<py::gil_scoped_release>());
   m.def(
-      "broadcast", [](const KV& kv, int root, std::shared_ptr<Comm> c) { return mrh::broadcast(kv, root, *c); },
+      "broadcast",
+      [](const KV& kv, int root, std::shared_ptr<Comm> c) {
+        return poisoning(c, "broadcast", [&] { return mrh::broadcast(kv, root, *c); });
+      },
       py::call_guard<py::gil_scoped_release>());
   m.def("map_urls", &map_urls);
   m.def("kmeans_map", &kmeans_map);
@@ -554,12 +600,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                        bool symmetric) {
              std::optional<at::Tensor> ww = w ? std::optional<at::Tensor>(*w) : std::nullopt;
              py::gil_scoped_release nogil;
-             return new EdgePlan(c, e, nvert, ww, symmetric);
+             return poisoning(c, "EdgePlan", [&] { return new EdgePlan(c, e, nvert, ww, symmetric); });
            }),
            py::arg("comm"), py::arg("edges"), py::arg("nvert"), py::arg("weights") = py::none(),
            py::arg("symmetric") = false)
-      .def("propagate", &EdgePlan::propagate, py::call_guard<py::gil_scoped_release>())
-      .def("count_global", &EdgePlan::count_global, py::call_guard<py::gil_scoped_release>())
+      .def("propagate",
+           [](const EdgePlan& p, const at::Tensor& x, int op, double identity, bool use_weights) {
+             return poisoning(p.comm, "EdgePlan.propagate", [&] { return p.propagate(x, op, identity, use_weights); });
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("count_global",
+           [](const EdgePlan& p, const at::Tensor& mask) {
+             return poisoning(p.comm, "EdgePlan.count_global", [&] { return p.count_global(mask); });
+           },
+           py::call_guard<py::gil_scoped_release>())
       .def_readonly("N", &EdgePlan::N)
       .def_readonly("nlocal", &EdgePlan::nlocal)
       .def_readonly("nedge", &EdgePlan::nedge)
@@ -570,27 +624,38 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("local_ids", &EdgePlan::local_ids)
       .def_readonly("P", &EdgePlan::P)
       .def_readonly("me", &EdgePlan::me);
-  m.def("connected_components", [](const EdgePlan& p, int mx) { return connected_components(p, mx); },
+  m.def("connected_components",
+        [](const EdgePlan& p, int mx) {
+          return poisoning(p.comm, "connected_components", [&] { return connected_components(p, mx); });
+        },
         py::arg("plan"), py::arg("max_iter") = 100000, py::call_guard<py::gil_scoped_release>());
   m.def(
       "luby_mis",
       [](const EdgePlan& p, int64_t seed, c10::optional<at::Tensor> act, int mx) {
         std::optional<at::Tensor> a = act ? std::optional<at::Tensor>(*act) : std::nullopt;
         py::gil_scoped_release nogil;
-        return luby_mis(p, seed, a, mx);
+        return poisoning(p.comm, "luby_mis", [&] { return luby_mis(p, seed, a, mx); });
       },
       py::arg("plan"), py::arg("seed"), py::arg("active") = py::none(), py::arg("max_iter") = 100000);
-  m.def("sssp", [](const EdgePlan& p, int64_t s, int mx) { return sssp(p, s, mx); }, py::arg("plan"),
-        py::arg("source"), py::arg("max_iter") = 1000000, py::call_guard<py::gil_scoped_release>());
+  m.def("sssp",
+        [](const EdgePlan& p, int64_t s, int mx) { return poisoning(p.comm, "sssp", [&] { return sssp(p, s, mx); }); },
+        py::arg("plan"), py::arg("source"), py::arg("max_iter") = 1000000, py::call_guard<py::gil_scoped_release>());
   py::class_<PageRankPlan>(m, "PageRankPlan")
       .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t n, double a) {
         py::gil_scoped_release nogil;
-        return new PageRankPlan(c, e, n, a);
+        return poisoning(c, "PageRankPlan", [&] { return new PageRankPlan(c, e, n, a); });
       }))
-      .def("reset", &PageRankPlan::reset, py::call_guard<py::gil_scoped_release>())
-      .def("step", &PageRankPlan::step, py::call_guard<py::gil_scoped_release>())
-      .def("run", &PageRankPlan::run, py::call_guard<py::gil_scoped_release>())
-      .def("delta", &PageRankPlan::delta, py::call_guard<py::gil_scoped_release>())
+      .def("reset", [](PageRankPlan& p) { poisoning(p.comm, "PageRankPlan.reset", [&] { p.reset(); }); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("step", [](PageRankPlan& p) { poisoning(p.comm, "PageRankPlan.step", [&] { p.step(); }); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("run",
+           [](PageRankPlan& p, int maxiter, double tol) {
+             return poisoning(p.comm, "PageRankPlan.run", [&] { return p.run(maxiter, tol); });
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("delta", [](const PageRankPlan& p) { return poisoning(p.comm, "PageRankPlan.delta", [&] { return p.delta(); }); },
+           py::call_guard<py::gil_scoped_release>())
       .def("ids", &PageRankPlan::ids)
       .def("ranks", &PageRankPlan::ranks)
       .def_readonly("N", &PageRankPlan::N)
@@ -601,11 +666,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<TriangleGraph>(m, "TriangleGraph")
       .def(py::init([](std::shared_ptr<Comm> c, at::Tensor e, int64_t n) {
              py::gil_scoped_release nogil;
-             return new TriangleGraph(c, e, n);
+             return poisoning(c, "TriangleGraph", [&] { return new TriangleGraph(c, e, n); });
            }),
            py::arg("comm"), py::arg("edges"), py::arg("nvert") = -1)
-      .def("count", &TriangleGraph::count, py::call_guard<py::gil_scoped_release>())
-      .def("triangles", &TriangleGraph::triangles, py::call_guard<py::gil_scoped_release>())
+      .def("count", [](const TriangleGraph& g) { return poisoning(g.comm, "TriangleGraph.count", [&] { return g.count(); }); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("triangles",
+           [](const TriangleGraph& g) {
+             return poisoning(g.comm, "TriangleGraph.triangles", [&] { return g.triangles(); });
+           },
+           py::call_guard<py::gil_scoped_release>())
       .def_readonly("nvert", &TriangleGraph::nvert)
       .def_readonly("nedge", &TriangleGraph::nedge)
       .def_readonly("rowptr", &TriangleGraph::rowptr)
@@ -669,6 +739,41 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("oink_main", [](std::shared_ptr<Comm> u, std::vector<std::string> argv) {
     py::gil_scoped_release nogil;
     return mrh::oink::main_args(u, argv);
+  });
+  // The RCCL unique-id rendezvous with a fake (random) id instead of
+  // ncclGetUniqueId, so CPU multi-process tests drive the exact key protocol
+  // of Rccl's constructor: returns (key, id bytes); rank 0 then waits for the
+  // acknowledgements and deletes the key, as after ncclCommInitRank.
+  m.def(
+      "rccl_rendezvous_probe",
+      [](py::object store, const std::string& tag, std::vector<int> members, int rank) {
+        auto st = store.cast<c10::intrusive_ptr<c10d::Store>>();
+        IdRendezvous r;
+        {
+          py::gil_scoped_release nogil;
+          r = rendezvous_id(st, tag, members, rank, [] {
+            std::vector<uint8_t> id(128);
+            std::random_device rd;
+            for (auto& b : id) b = (uint8_t)rd();
+            return id;
+          }, nullptr);
+          if (rank == 0) rendezvous_release(st, r, (int)members.size(), nullptr);
+        }
+        return std::make_pair(r.key, py::bytes((const char*)r.id.data(), r.id.size()));
+      },
+      py::arg("store"), py::arg("tag"), py::arg("members"), py::arg("rank"));
+  m.def("live_rccl_comms", &mrh::live_rccl_comms);
+  // world size 1 runs the local transport (no communicator); this builds a
+  // one-rank RCCL communicator on `device` and returns what RCCL reports
+  m.def("rccl_self_probe", [](int device) {
+    py::dict d;
+    {
+      Rccl r(0, 1, device, c10::intrusive_ptr<c10d::Store>(), "probe");
+      d["comm_count"] = r.comm_count();
+      d["cu_device"] = r.cu_device();
+      d["user_rank"] = r.user_rank();
+    }
+    return d;
   });
   m.def("hip_compiled", []() { return true; });
   // PCI bus id of a visible GPU ("" if none), for NUMA-local CPU/memory binding

@@ -91,14 +91,21 @@ Comm::Comm(at::Device dev) : dev_(dev) {
   if (dev_.is_cuda() && force_rccl()) init_transport("", "self");
 }
 
-Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const std::string& transport)
+Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const std::string& transport,
+           std::vector<int> members, int world_rank, int world_size)
     : dev_(dev), pg_(std::move(pg)), store_(std::move(store)) {
   if (dev_.is_cuda()) guard::install_alloc_guard();
   if (pg_) {
     rank_ = pg_->getRank();
     size_ = pg_->getSize();
   }
-  if (size_ > 1 && store_) mon_ = shared_monitor(store_, rank_, size_);
+  if (members.empty())
+    for (int r = 0; r < size_; ++r) members.push_back(r);
+  if ((int)members.size() != size_) throw std::runtime_error("mrhip: member list does not match the group size");
+  members_ = std::move(members);
+  if (world_rank < 0) world_rank = members_[rank_];
+  if (world_size < 0) world_size = size_;
+  if (world_size > 1 && store_) mon_ = shared_monitor(store_, world_rank, world_size);
   if (size_ == 1) pg_.reset();
   init_transport(transport, "world");
 }
@@ -110,7 +117,9 @@ void Comm::init_transport(const std::string& transport, const std::string& tag) 
     if (pg_) return;  // no store to bootstrap from: keep the process group
     throw std::runtime_error("mrhip: multi-rank RCCL communicator needs a rendezvous store");
   }
-  rccl_ = std::make_shared<Rccl>(rank_, size_, dev_.index(), store_, tag);
+  // one RCCL communicator per (member set, device) per process, shared by
+  // every Comm over the same ranks
+  rccl_ = shared_rccl(rank_, size_, dev_.index(), store_, tag, members_, mon_.get());
 }
 
 Comm::~Comm() = default;
@@ -181,10 +190,17 @@ void Comm::host_wait() const {
     ~Drop() { (void)hipEventDestroy(e); }
   } drop{ev};
   if (hipEventRecord(ev, cur(dev_)) != hipSuccess) throw std::runtime_error("mrhip: hipEventRecord failed");
+  // the deadline replaces the watchdog of a c10d RCCL group: a collective
+  // whose peer never posts its half cannot block this rank forever
+  const bool bounded = distributed() && size_ > 1;
+  const double t0 = bounded ? wtime() : 0.0, limit = guard::comm_timeout_seconds();
   for (int spin = 0;; ++spin) {
     const hipError_t q = hipEventQuery(ev);
     if (q == hipSuccess) return;
     if (q != hipErrorNotReady) throw std::runtime_error(std::string("mrhip: device error: ") + hipGetErrorString(q));
+    if (bounded && (spin & 255) == 0 && wtime() - t0 > limit)
+      fail_now("mrhip: device work did not complete within MRH_COMM_TIMEOUT=" + std::to_string((int)limit) +
+               " s (a collective whose peers never joined?)");
     if (rccl_) {
       const ncclResult_t r = rccl_->async_error();
       if (r != ncclSuccess && r != ncclInProgress)
@@ -207,14 +223,12 @@ std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
   if (v.empty() || !distributed()) return v;
   trace_coll(rank_, "allreduce_i64", (int64_t)v.size(), op);
   at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kLong));
-  if (rccl_) {
+  if (host_scalars()) {
+    pg_allreduce(pg_, t, op);
+  } else if (rccl_) {
     t = t.to(dev_);
     rccl_->allreduce(t.data_ptr(), v.size(), ncclInt64, nred(op), cur(dev_));
     host_wait();
-    t = t.to(at::kCPU);
-  } else {
-    t = t.to(dev_);
-    pg_allreduce(pg_, t, op);
     t = t.to(at::kCPU);
   }
   std::memcpy(v.data(), t.data_ptr<int64_t>(), v.size() * sizeof(int64_t));
@@ -225,14 +239,12 @@ std::vector<double> Comm::allreduce_f64(std::vector<double> v, Op op) const {
   if (v.empty() || !distributed()) return v;
   trace_coll(rank_, "allreduce_f64", (int64_t)v.size(), op);
   at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kDouble));
-  if (rccl_) {
+  if (host_scalars()) {
+    pg_allreduce(pg_, t, op);
+  } else if (rccl_) {
     t = t.to(dev_);
     rccl_->allreduce(t.data_ptr(), v.size(), ncclFloat64, nred(op), cur(dev_));
     host_wait();
-    t = t.to(at::kCPU);
-  } else {
-    t = t.to(dev_);
-    pg_allreduce(pg_, t, op);
     t = t.to(at::kCPU);
   }
   std::memcpy(v.data(), t.data_ptr<double>(), v.size() * sizeof(double));
@@ -251,10 +263,18 @@ std::string Comm::bcast(const std::string& s, int root) const {
   n = allreduce(n, SUM);
   at::Tensor t = at::zeros({std::max<int64_t>(n, 1)}, at::TensorOptions().dtype(at::kByte));
   if (rank_ == root && n) std::memcpy(t.data_ptr(), s.data(), n);
-  t = t.to(dev_);
-  broadcast_tensor(t, root);
-  if (rccl_) host_wait();
-  t = t.to(at::kCPU);
+  if (host_scalars()) {
+    std::vector<at::Tensor> v{t};
+    c10d::BroadcastOptions bo;
+    bo.rootRank = root;
+    pg_->broadcast(v, bo)->wait();
+    t = v[0];
+  } else {
+    t = t.to(dev_);
+    broadcast_tensor(t, root);
+    if (rccl_) host_wait();
+    t = t.to(at::kCPU);
+  }
   return std::string((const char*)t.data_ptr(), (size_t)n);
 }
 
@@ -436,31 +456,34 @@ std::shared_ptr<Comm> Comm::split(int color) const {
   const int id = nsplit++;  // every rank splits in the same sequence
   std::vector<double> colors = allgather_f64((double)color);
   int newrank = 0, newsize = 0;
+  std::vector<int> members;
   for (int r = 0; r < size_; ++r)
     if (colors[r] == (double)color) {
       if (r == rank_) newrank = newsize;
+      members.push_back(members_[r]);
       ++newsize;
     }
   if (newsize == 1) return std::make_shared<Comm>(dev_);
   if (!store_) throw std::runtime_error("mrhip: Comm::split needs the rendezvous store");
+  // the subgroup's host transport gets its own key space; its RCCL id goes
+  // through the root store under a key naming the member list
   auto pst = c10::make_intrusive<c10d::PrefixStore>("mrh_split_" + std::to_string(id) + "_" + std::to_string(color),
                                                     store_);
   auto c = std::make_shared<Comm>(dev_);
   c->rank_ = newrank;
   c->size_ = newsize;
-  c->store_ = pst;
+  c->members_ = members;
+  c->store_ = store_;
   c->mon_ = mon_;  // failure detection stays job-wide
   c->rccl_.reset();
-  if (rccl_) {
-    c->rccl_ = std::make_shared<Rccl>(newrank, newsize, dev_.index(), pst, "split");
-  } else {
-    c->pg_ = make_host_pg(pst, newrank, newsize, mon_);
-  }
+  c->pg_ = make_host_pg(pst, newrank, newsize, mon_);
+  if (rccl_) c->rccl_ = shared_rccl(newrank, newsize, dev_.index(), store_, "split", members, mon_.get());
   return c;
 }
 
 void Comm::shutdown() const {
   if (!store_ || size_ == 1) return;
+  if (mon_ && mon_->failed()) return;  // a failed job has no orderly end
   if (mon_) mon_->retire();
   try {
     store_->add("mrh_shutdown", 1);
@@ -476,7 +499,21 @@ void Comm::shutdown() const {
 int64_t Comm::next_task(const std::string& key) const {
   if (!store_) throw std::runtime_error("mrhip: mapstyle 2 needs a c10d store");
   check_peers();
-  return store_->add(key, 1) - 1;
+  // scoped by the member list: concurrent worlds of one job share the root store
+  std::string k = key + "@";
+  for (int m : members_) k += std::to_string(m) + ",";
+  return store_->add(k, 1) - 1;
+}
+
+RcclInfo Comm::rccl_info() const {
+  RcclInfo i;
+  i.live_comms = live_rccl_comms();
+  if (!rccl_) return i;
+  i.comm_count = rccl_->comm_count();
+  i.cu_device = rccl_->cu_device();
+  i.user_rank = rccl_->user_rank();
+  i.id_key = rccl_->id_key();
+  return i;
 }
 
 }  // namespace mrh

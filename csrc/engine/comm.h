@@ -36,15 +36,27 @@ namespace mrh {
 
 using PG = c10::intrusive_ptr<c10d::ProcessGroup>;
 
+struct RcclInfo {
+  int comm_count = -1;   // ncclCommCount
+  int cu_device = -1;    // ncclCommCuDevice
+  int user_rank = -1;    // ncclCommUserRank
+  int live_comms = 0;    // RCCL communicators this process holds
+  std::string id_key;    // store key of the unique-id rendezvous
+};
+
 class Comm {
  public:
   enum Op { SUM = 0, MAX = 1, MIN = 2 };
 
   // world size 1 on `dev` (an RCCL loopback communicator if MRH_FORCE_RCCL=1)
   explicit Comm(at::Device dev = at::Device(at::kCPU));
-  // an existing process group (e.g. created by torch.distributed) + its store;
-  // transport "" = automatic (RCCL for a GPU device), "pg" = stay on the group
-  Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store = {}, const std::string& transport = "");
+  // an existing process group (e.g. created by torch.distributed) + the job's
+  // root store; transport "" = automatic (RCCL for a GPU device), "pg" = stay
+  // on the group. members = the group's ranks in world numbering (empty: the
+  // group is the world); world_rank/world_size = this process in the world
+  // (-1: the group's), for the job-wide peer monitor
+  Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store = {}, const std::string& transport = "",
+       std::vector<int> members = {}, int world_rank = -1, int world_size = -1);
   ~Comm();
 
   // Bootstrap from torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK,
@@ -69,7 +81,14 @@ class Comm {
   const std::shared_ptr<Rccl>& rccl() const { return rccl_; }
   const std::shared_ptr<Monitor>& monitor() const { return mon_; }
   const c10::intrusive_ptr<c10d::Store>& store() const { return store_; }
+  // this communicator's ranks in world numbering
+  const std::vector<int>& members() const { return members_; }
 
+  // Host scalars (counts, stats, flags, the file list) travel over the host
+  // process group when the communicator has one (gloo / the store transport):
+  // no H2D/D2H staging and, above all, no device synchronisation, which an
+  // RCCL scalar collective would force on every op's return value. Without a
+  // host group they go through RCCL.
   std::vector<int64_t> allreduce(std::vector<int64_t> v, Op op) const;
   int64_t allreduce(int64_t v, Op op) const { return allreduce(std::vector<int64_t>{v}, op)[0]; }
   std::vector<double> allreduce_f64(std::vector<double> v, Op op) const;
@@ -92,6 +111,9 @@ class Comm {
   // mapstyle 2 work queue: next global task index from a store counter
   int64_t next_task(const std::string& key) const;
 
+  // what RCCL reports about this communicator (all -1 without RCCL)
+  RcclInfo rccl_info() const;
+
   // ---------------------------------------------------------------- data plane
   // One grouped round of point-to-point byte transfers between this rank and
   // any peers (self included): RCCL send/recv on the comm stream fenced
@@ -113,7 +135,8 @@ class Comm {
 
   // Block the host until the work queued so far on the current stream is
   // done, polling for peer failure and RCCL async errors (throws PeerFailure
-  // after aborting the communicator). Every host read of data that depends on
+  // after aborting the communicator; on a multi-rank communicator also after
+  // MRH_COMM_TIMEOUT seconds). Every host read of data that depends on
   // communication goes through here first.
   void host_wait() const;
   // fatal error on this rank: tell every peer and abort the communicator
@@ -124,9 +147,11 @@ class Comm {
  private:
   void init_transport(const std::string& transport, const std::string& tag);
   void fail_now(const std::string& why) const;
+  bool host_scalars() const { return pg_ && size_ > 1; }
 
   int rank_ = 0, size_ = 1;
   at::Device dev_;
+  std::vector<int> members_{0};
   PG pg_;
   c10::intrusive_ptr<c10d::Store> store_;
   std::shared_ptr<Rccl> rccl_;

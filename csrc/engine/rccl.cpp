@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 
 #include "guard.h"
 
@@ -38,8 +39,10 @@ Monitor::Monitor(c10::intrusive_ptr<c10d::Store> root, int rank, int size)
   thread_ = std::thread([this] { beat_loop(); });
 }
 
+// No retire() here: a process that tears its communicator down without the
+// end-of-job handshake (an exception that escaped, exit() from an error path)
+// must look like a crash to its peers, not like a clean exit.
 Monitor::~Monitor() {
-  if (!failed_) retire();  // orderly teardown is not a crash
   stop_ = true;
   if (thread_.joinable()) thread_.join();
 }
@@ -58,7 +61,7 @@ void Monitor::beat_loop() {
 }
 
 void Monitor::retire() {
-  if (retired_.exchange(true)) return;
+  if (poisoned_ || retired_.exchange(true)) return;
   try {
     store_->set("mrh/bye/" + std::to_string(rank_), std::vector<uint8_t>{1});
   } catch (const std::exception&) {
@@ -125,6 +128,74 @@ void Monitor::check() {
   }
 }
 
+// ====================================================================== id rendezvous
+
+namespace {
+std::string members_tag(const std::vector<int>& members) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over the member list
+  for (int m : members) {
+    h ^= (uint64_t)(uint32_t)m;
+    h *= 1099511628211ull;
+  }
+  char buf[48];
+  std::snprintf(buf, sizeof(buf), "n%zu-%016llx", members.size(), (unsigned long long)h);
+  return buf;
+}
+
+// wait (polling, bounded) until `key` exists in the store
+void wait_key(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, Monitor* mon, const char* what) {
+  const double t0 = now_s(), limit = guard::comm_timeout_seconds();
+  int sleep_us = 50;
+  while (!store->check({key})) {
+    if (mon) mon->check();
+    if (now_s() - t0 > limit)
+      throw PeerFailure(std::string("mrhip rccl: timed out after ") + std::to_string((int)limit) + " s waiting for " +
+                        what + " (" + key + ")");
+    std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
+    sleep_us = std::min(sleep_us * 2, 5000);
+  }
+}
+}  // namespace
+
+IdRendezvous rendezvous_id(const c10::intrusive_ptr<c10d::Store>& store, const std::string& tag,
+                           const std::vector<int>& members, int rank,
+                           const std::function<std::vector<uint8_t>()>& make_id, Monitor* mon) {
+  if (!store) throw std::runtime_error("mrhip rccl: multi-rank communicator needs the rendezvous store");
+  // the n-th communicator this process creates over this member set; every
+  // member creates the same communicators in the same order, so the numbers agree
+  static std::mutex mu;
+  static std::map<std::string, int64_t> seq;
+  const std::string base = "mrh/rccl_id/" + tag + "/" + members_tag(members);
+  int64_t n;
+  {
+    std::lock_guard<std::mutex> l(mu);
+    n = seq[base]++;
+  }
+  IdRendezvous r;
+  r.key = base + "/" + std::to_string(n);
+  if (rank == 0) {
+    r.id = make_id();
+    store->set(r.key, r.id);
+  } else {
+    wait_key(store, r.key, mon, "the communicator's unique id");
+    r.id = store->get(r.key);
+    store->add(r.key + "/ack", 1);
+  }
+  return r;
+}
+
+void rendezvous_release(const c10::intrusive_ptr<c10d::Store>& store, const IdRendezvous& r, int nmembers,
+                        Monitor* mon) {
+  const double t0 = now_s(), limit = guard::comm_timeout_seconds();
+  while (store->add(r.key + "/ack", 0) < nmembers - 1) {
+    if (mon) mon->check();
+    if (now_s() - t0 > limit) throw PeerFailure("mrhip rccl: timed out waiting for unique-id acknowledgements");
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  store->deleteKey(r.key);
+  store->deleteKey(r.key + "/ack");
+}
+
 // ====================================================================== Rccl
 
 void Rccl::check(ncclResult_t r, const char* what) {
@@ -137,25 +208,31 @@ void Rccl::check(ncclResult_t r, const char* what) {
   throw std::runtime_error(msg);
 }
 
-Rccl::Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>& store, const std::string& tag)
+Rccl::Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>& store, const std::string& tag,
+           const std::vector<int>& members_in, Monitor* mon)
     : rank_(rank), size_(size) {
   hip_ok(hipSetDevice(device), "hipSetDevice");
   ncclUniqueId id;
+  IdRendezvous rv;
   if (size == 1) {
     check(ncclGetUniqueId(&id), "ncclGetUniqueId");
   } else {
-    if (!store) throw std::runtime_error("mrhip rccl: multi-rank communicator needs the rendezvous store");
-    const std::string key = "mrh/rccl_id/" + tag;
-    if (rank == 0) {
-      check(ncclGetUniqueId(&id), "ncclGetUniqueId");
-      store->set(key, std::vector<uint8_t>((uint8_t*)&id, (uint8_t*)&id + sizeof(id)));
-    } else {
-      auto b = store->get(key);  // bounded by the store timeout (MRH_COMM_TIMEOUT)
-      if (b.size() != sizeof(id)) throw std::runtime_error("mrhip rccl: bad unique id in store");
-      std::memcpy(&id, b.data(), sizeof(id));
-    }
+    std::vector<int> members = members_in;
+    if (members.empty())
+      for (int r = 0; r < size; ++r) members.push_back(r);
+    if ((int)members.size() != size) throw std::runtime_error("mrhip rccl: member list does not match the size");
+    rv = rendezvous_id(store, tag, members, rank, [&] {
+      ncclUniqueId u;
+      check(ncclGetUniqueId(&u), "ncclGetUniqueId");
+      return std::vector<uint8_t>((uint8_t*)&u, (uint8_t*)&u + sizeof(u));
+    }, mon);
+    if (rv.id.size() != sizeof(id)) throw std::runtime_error("mrhip rccl: bad unique id in store");
+    std::memcpy(&id, rv.id.data(), sizeof(id));
+    id_key_ = rv.key;
   }
   check(ncclCommInitRank(&comm_, size, id, rank), "ncclCommInitRank");
+  // ncclCommInitRank returns once every member joined, so every reader is done
+  if (size > 1 && rank == 0) rendezvous_release(store, rv, size, mon);
   int lo = 0, hi = 0;
   hip_ok(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
   hip_ok(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
@@ -226,6 +303,47 @@ void Rccl::broadcast(void* buf, size_t bytes, int root, hipStream_t s) {
   fence_in(s);
   check(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
   hip_ok(hipStreamWaitEvent(s, fence_out(), 0), "hipStreamWaitEvent");
+}
+
+int Rccl::comm_count() {
+  int n = 0;
+  check(ncclCommCount(comm_, &n), "ncclCommCount");
+  return n;
+}
+int Rccl::cu_device() {
+  int d = -1;
+  check(ncclCommCuDevice(comm_, &d), "ncclCommCuDevice");
+  return d;
+}
+int Rccl::user_rank() {
+  int r = -1;
+  check(ncclCommUserRank(comm_, &r), "ncclCommUserRank");
+  return r;
+}
+
+namespace {
+std::mutex g_rccl_mu;
+std::map<std::string, std::weak_ptr<Rccl>> g_rccl;
+}  // namespace
+
+std::shared_ptr<Rccl> shared_rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>& store,
+                                  const std::string& tag, const std::vector<int>& members, Monitor* mon) {
+  std::string k = std::to_string((uintptr_t)store.get()) + "|" + tag + "|" + std::to_string(device) + "|" +
+                  std::to_string(size) + "|" + std::to_string(rank);
+  for (int m : members) k += "," + std::to_string(m);
+  std::lock_guard<std::mutex> l(g_rccl_mu);
+  auto& w = g_rccl[k];
+  if (auto r = w.lock()) return r;
+  auto r = std::make_shared<Rccl>(rank, size, device, store, tag, members, mon);
+  w = r;
+  return r;
+}
+
+int live_rccl_comms() {
+  std::lock_guard<std::mutex> l(g_rccl_mu);
+  int n = 0;
+  for (auto& kv : g_rccl) n += kv.second.expired() ? 0 : 1;
+  return n;
 }
 
 ncclResult_t Rccl::async_error() {

@@ -22,7 +22,14 @@
 //
 // Bootstrap without MPI: rank 0 creates the ncclUniqueId and publishes it in
 // the job's rendezvous store (the c10d TCPStore that torchrun / the native
-// launcher already run); the other ranks read it and ncclCommInitRank.
+// launcher already run); the other ranks read it and ncclCommInitRank. The
+// store key names the communicator: its tag, a hash of its member list (world
+// ranks) and a per-process sequence number of communicators created for that
+// member set, so two communicators of one job never share a key (a second
+// world communicator, MPI_Comm_split-style subgroups of different colours).
+// Readers acknowledge; rank 0 deletes the key once every member has read it.
+// A process keeps ONE RCCL communicator per member set and device: every
+// Comm built over the same ranks shares it (shared_rccl).
 //
 // Monitor: each rank of a multi-rank job runs a heartbeat thread that adds 1
 // to its store counter every MRH_HEARTBEAT_MS (default 250 ms). Any wait that
@@ -37,6 +44,7 @@
 #include <torch/csrc/distributed/c10d/Store.hpp>
 
 #include <atomic>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -66,7 +74,8 @@ class Monitor {
   // tell every peer this rank hit a fatal error (idempotent)
   void poison(const std::string& why);
   bool failed() const { return failed_.load(); }
-  // clean exit: peers stop treating this rank's silent counter as a crash
+  // clean exit (Comm::shutdown only — never implied by teardown): peers stop
+  // treating this rank's silent counter as a crash; no-op after poison()
   void retire();
   int rank() const { return rank_; }
   int size() const { return size_; }
@@ -93,10 +102,29 @@ struct Xfer {
   int64_t bytes;
 };
 
+// ---- unique-id rendezvous (store only; the CPU tests drive it with fake ids)
+struct IdRendezvous {
+  std::string key;          // store key the id was published under
+  std::vector<uint8_t> id;  // the id every member got
+};
+// Rank `rank` (0-based within `members`, the communicator's world ranks in
+// order) obtains the id of the next communicator over `members`: rank 0 calls
+// make_id() and publishes it, the others wait for it (polling `mon` for peer
+// failure, bounded by MRH_COMM_TIMEOUT) and acknowledge.
+IdRendezvous rendezvous_id(const c10::intrusive_ptr<c10d::Store>& store, const std::string& tag,
+                           const std::vector<int>& members, int rank,
+                           const std::function<std::vector<uint8_t>()>& make_id, Monitor* mon);
+// rank 0, after the communicator is up: wait for every reader's
+// acknowledgement, then delete the key (no stale id left for a later reader)
+void rendezvous_release(const c10::intrusive_ptr<c10d::Store>& store, const IdRendezvous& r, int nmembers,
+                        Monitor* mon);
+
 class Rccl {
  public:
-  // store may be null when size == 1 (the id is created locally)
-  Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>& store, const std::string& tag);
+  // store may be null when size == 1 (the id is created locally); members =
+  // the communicator's ranks in world numbering (empty = 0..size-1)
+  Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>& store, const std::string& tag,
+       const std::vector<int>& members = {}, Monitor* mon = nullptr);
   ~Rccl();
   Rccl(const Rccl&) = delete;
   Rccl& operator=(const Rccl&) = delete;
@@ -117,6 +145,13 @@ class Rccl {
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s);
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s);
 
+  // what RCCL itself reports (ncclCommCount / ncclCommCuDevice / ncclCommUserRank)
+  int comm_count();
+  int cu_device();
+  int user_rank();
+  // the store key the id came through ("" for a local id)
+  const std::string& id_key() const { return id_key_; }
+
   // nccl async error (ncclSuccess / ncclInProgress when healthy)
   ncclResult_t async_error();
   // tear the communicator down (unblocks kernels waiting on a dead peer)
@@ -134,6 +169,15 @@ class Rccl {
   std::vector<hipEvent_t> ev_;  // ring of fence events
   size_t ev_next_ = 0;
   bool aborted_ = false;
+  std::string id_key_;
 };
+
+// The process's communicator over (store, tag, members, device): an existing
+// live one is shared, otherwise a new one is bootstrapped (collectively: every
+// member must ask in the same order).
+std::shared_ptr<Rccl> shared_rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>& store,
+                                  const std::string& tag, const std::vector<int>& members, Monitor* mon);
+// number of live RCCL communicators this process holds (tests / bench record)
+int live_rccl_comms();
 
 }  // namespace mrh

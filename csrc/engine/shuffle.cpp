@@ -25,7 +25,10 @@
 //     (every column of every peer in one RCCL group): piece k of every bucket
 //     is sent from where it lies and received straight into its final place in
 //     the output (sender-major, then piece order — the same order as a single
-//     round, so the result does not depend on the cap). With a host sink
+//     round, so the aggregate result does not depend on the cap. The
+//     pipelined collate (pipeline=1) groups each round as it lands, so there
+//     the order of the values inside a key is (round, sender) and DOES change
+//     with chunk_bytes once R > 1; the groups themselves do not). With a host sink
 //     (out-of-core aggregate) a round lands in one of two HBM staging buffers
 //     and drains to pinned host memory on a copy stream while the next round
 //     is on the wire: HBM holds the send buffer + 2 rounds, never the output.

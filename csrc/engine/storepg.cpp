@@ -6,6 +6,7 @@
 #include <chrono>
 #include <thread>
 
+#include "guard.h"
 #include "rccl.h"
 
 #include <cstdio>
@@ -51,10 +52,18 @@ StoreBackend::StoreBackend(c10::intrusive_ptr<c10d::Store> store, int rank, int 
 // blocking read of a peer's blob; with a monitor it polls (check + backoff up
 // to 5 ms) so a peer that died before publishing fails the read in seconds
 std::vector<uint8_t> StoreBackend::get(const std::string& k) {
-  if (!mon_) return store_->get(k);
+  if (!mon_) return store_->get(k);  // bounded by the store's own timeout
+  const auto t0 = std::chrono::steady_clock::now();
+  const int limit = guard::comm_timeout_seconds();
   int sleep_us = 50;
   while (!store_->check({k})) {
     mon_->check();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(limit)) {
+      const std::string why = "mrh_store: no peer data for " + k + " within MRH_COMM_TIMEOUT=" +
+                              std::to_string(limit) + " s";
+      mon_->poison(why);
+      throw PeerFailure(why);
+    }
     std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
     sleep_us = std::min(sleep_us * 2, 5000);
   }

@@ -17,6 +17,9 @@ int main(int argc, char** argv) {
     return mrh::oink::main_args(mrh::capi_world(), a);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "ERROR: %s\n", e.what());
+    // peers must see a failure, not an orderly exit (the exit handler's
+    // shutdown handshake is skipped on a poisoned communicator)
+    mrh::capi_world()->poison(e.what());
     return 1;
   }
 }

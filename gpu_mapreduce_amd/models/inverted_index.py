@@ -28,6 +28,11 @@ MI355X design, pipelined per part file:
             duplex: the drain overlaps the next job's input stream); the
             output is complete once `output_ready()` (or any device sync).
             Optionally written to `out_dir/InvertedIndex-P-me`.
+
+`output` lives in a pinned host buffer of a two-slot pool (no
+hipHostMalloc per job): it stays valid until two more InvertedIndex jobs
+have run in this process. `output_lines()` / `output_bytes()` refuse to read
+an overwritten slot; pass `own_output=True` to get a private buffer.
 """
 from __future__ import annotations
 
@@ -43,13 +48,16 @@ PAD = 64
 
 
 class InvertedIndex:
-    def __init__(self, mr: MapReduce, files, out_dir=None, pipelined=True):
+    def __init__(self, mr: MapReduce, files, out_dir=None, pipelined=True, own_output=False):
         """files: list of (name, uint8 tensor) for THIS rank (host tensors —
         ideally pinned — or device tensors)."""
         self.mr = mr
         self.files = files
         self.out_dir = out_dir
         self.pipelined = pipelined
+        self.own_output = own_output
+        self._gen = None
+        self._mapped = False
         # doc ids are global (rank-major) so a value means the same file name on
         # every rank after the shuffle; the reference ships the name string itself
         all_names = mr.comm.allgather_object([n for n, _ in files])
@@ -84,6 +92,9 @@ class InvertedIndex:
         kv.add_kv(part)
 
     def _map(self, itask, kv):
+        if self._mapped:
+            raise RuntimeError("InvertedIndex: a rank was given two map tasks (its files are mapped once)")
+        self._mapped = True
         files = self.files
         if self.pipelined:
             kv.enable_grouping()
@@ -130,7 +141,11 @@ class InvertedIndex:
     def _reduce(self, kmv, kv):
         text = C.inverted_index_format(kmv, self.names_dev, self.name_off_dev)
         if self.is_cuda:
-            host = pools.pinned_buffer(text.numel(), slot=100 + pools.next_slot("ii_out"))
+            if self.own_output:
+                host = torch.empty(text.numel(), dtype=torch.uint8, pin_memory=True)
+            else:
+                host = pools.pinned_buffer(text.numel(), slot=100 + pools.next_slot("ii_out"))
+                self._gen = pools.generation("ii_out")
             d2h = pools.stream(self.dev, "d2h")
             d2h.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(d2h):
@@ -161,8 +176,18 @@ class InvertedIndex:
         map the per-file shuffle runs inside Map (Network I/O = 0)."""
         mr = self.mr
         tick = _Ticker(phases, mr.comm)
-        # one map task per rank, each maps its own files (reference :175, :278-284)
-        self.nurls = mr.map(mr.nprocs, self._map)
+        # one map task per rank, each maps its own files (reference :175,
+        # :278-284). The files are rank-local and the per-file exchange inside
+        # the callback is lock-step across ranks, so the task of rank r must
+        # run on rank r: mapstyle 2 (dynamic assignment: a rank could get none
+        # or two) is overridden for this map
+        ms = mr.mapstyle
+        if ms not in (0, 1):
+            mr.mapstyle = 0
+        try:
+            self.nurls = mr.map(mr.nprocs, self._map)
+        finally:
+            mr.mapstyle = ms
         tick("Map")
         if not self.exchanged:
             mr.aggregate()
@@ -175,11 +200,17 @@ class InvertedIndex:
         tick("Reduce")
         return self.nurls
 
-    def output_lines(self):
+    def output_bytes(self) -> bytes:
         if self.output is None:
-            return []
+            return b""
+        if self._gen is not None and pools.generation("ii_out") - self._gen >= 2:
+            raise RuntimeError("InvertedIndex.output was overwritten by a later job (two-slot pinned pool); "
+                               "read it sooner or construct with own_output=True")
         self.output_ready()
-        return bytes(self.output.cpu().numpy()).decode("utf-8", "replace").splitlines()
+        return bytes(self.output.cpu().numpy())
+
+    def output_lines(self):
+        return self.output_bytes().decode("utf-8", "replace").splitlines()
 
 
 class _Ticker:

@@ -1,29 +1,98 @@
-"""Communicator: one process per MI355X, torch.distributed over RCCL/xGMI.
+"""Communicator: one process per MI355X; RCCL over xGMI for the data plane.
 
 Replaces MR-MPI's MPI_Comm plumbing (reference src/mapreduce.cpp:93-161) and
 the serial `mpistubs/` fake MPI (mpistubs/mpi.cpp:57-67): with no process
 group (world size 1) every collective is the identity.
 
-Backend choice is not a dispatch layer: device tensors go through the "nccl"
-backend (which IS RCCL on ROCm); the CPU engine path (tests, no GPU) uses
-"gloo". The native shuffle calls the c10d ProcessGroup directly from C++.
+Exactly ONE RCCL communicator per process (per member set): the native
+engine's (csrc/engine/rccl.h), created by `Comm.native` and shared by every
+Comm over the same ranks. torch.distributed runs the **gloo** backend and only
+carries host objects and host scalars (the global pair counts every op returns,
+file lists, pickled objects) — so an op's return value never forces a device
+round trip, and no second (c10d) RCCL communicator competes for the xGMI links.
+The engine's device data (shuffle rounds, allgathers, PageRank/graph
+exchanges) goes through the native RCCL communicator.
+
+Engine transport "pg" (several ranks sharing one GPU, where RCCL cannot run —
+the multi-rank rehearsal on a 1-GPU box — or MRH_TRANSPORT=pg) keeps the
+engine's collectives on the gloo group instead.
 """
 from __future__ import annotations
 
+import atexit
 import datetime
 import os
+import sys
 import time
 
 import torch
 import torch.distributed as dist
 
 _WORLD = None
+_NATIVE = {}          # (group key, device, transport) -> NativeComm: one per member set
+_HOOKS = [False]
+
+
+def _shares_devices(size: int) -> bool:
+    """True when more local ranks than visible GPUs: ranks share a device,
+    which RCCL refuses (two ranks of one communicator on one GPU). Without
+    LOCAL_WORLD_SIZE (a single-node launcher) every rank is local."""
+    try:
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(size)))
+        return torch.cuda.is_available() and lws > torch.cuda.device_count()
+    except (ValueError, RuntimeError):
+        return False
+
+
+def _engine_transport(device: str, size: int) -> str:
+    if not device.startswith("cuda"):
+        return "pg"
+    if os.environ.get("MRH_TRANSPORT") == "pg" or _shares_devices(size):
+        return "pg"
+    return ""
+
+
+def _install_exit_hooks():
+    """A multi-rank job must end one of two ways for its peers: an orderly
+    shutdown handshake (atexit, after a clean run), or a poisoned communicator
+    (an exception escaped: peers fail within seconds instead of waiting on a
+    rank that is gone). Teardown alone never counts as a clean exit."""
+    if _HOOKS[0]:
+        return
+    _HOOKS[0] = True
+    prev = sys.excepthook
+
+    def hook(tp, val, tb):
+        for n in list(_NATIVE.values()):
+            try:
+                if n.size > 1:
+                    n.poison(f"uncaught {tp.__name__} on rank {dist.get_rank() if dist.is_initialized() else '?'}: {val}")
+            except Exception:  # noqa: BLE001
+                pass
+        prev(tp, val, tb)
+
+    sys.excepthook = hook
+
+    def retire():
+        done = set()
+        for n in list(_NATIVE.values()):
+            try:
+                key = tuple(n.members)
+                if n.size > 1 and not n.failed and key not in done and \
+                        (not dist.is_initialized() or n.size == dist.get_world_size()):
+                    done.add(key)
+                    n.shutdown()
+            except Exception:  # noqa: BLE001
+                pass
+
+    atexit.register(retire)
 
 
 class Comm:
-    """Thin host-side view of a c10d process group plus the engine device."""
+    """Host-side view of a process group (gloo), the engine device and the
+    engine's native communicator (RCCL for device engines)."""
 
-    def __init__(self, group=None, device=None):
+    def __init__(self, group=None, device=None, transport=None):
         if group is None and dist.is_available() and dist.is_initialized():
             group = dist.group.WORLD
         self.group = group
@@ -31,43 +100,56 @@ class Comm:
             self.rank = dist.get_rank(group)
             self.size = dist.get_world_size(group)
             backend = dist.get_backend(group)
+            self.members = list(dist.get_process_group_ranks(group))
         else:
             self.rank, self.size, backend = 0, 1, None
+            self.members = [0]
         self.backend = backend
         if device is None:
-            if backend == "gloo" or not torch.cuda.is_available():
-                device = "cpu"
-            else:
-                device = f"cuda:{torch.cuda.current_device()}"
+            device = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
         self.device = str(device)
         self.is_cuda = self.device.startswith("cuda")
-        # the c10d ProcessGroup handed to the native shuffle (None when P == 1)
+        # engine transport: "" = native RCCL for device engines, "pg" = the group
+        self.transport = _engine_transport(self.device, self.size) if transport is None else transport
+        # the c10d ProcessGroup handed to the native engine (None when P == 1)
         self.pg = group if (group is not None and self.size > 1) else None
-        self._native = None
+        # host scalars on the host group; device tensors only if the group is
+        # an explicit (non-default) nccl group
+        self._sdev = self.device if (backend == "nccl") else "cpu"
 
     @property
     def native(self):
-        """The C++ communicator (csrc/engine/comm.h) the native MapReduce uses:
-        same process group, plus the rendezvous store for mapstyle 2."""
-        if self._native is None:
+        """The C++ communicator (csrc/engine/comm.h) the native engine uses:
+        this group for host scalars, the root store for the RCCL id
+        rendezvous and mapstyle 2, and the process's RCCL communicator over
+        these members (shared with every other Comm over them)."""
+        key = (tuple(self.members) if self.size > 1 else ("self", id(self)), self.device, self.transport)
+        n = _NATIVE.get(key)
+        if n is None:
             from .._ext import C
             store = None
+            wr, ws = -1, -1
             if self.size > 1:
-                try:
-                    store = dist.distributed_c10d._get_default_store()
-                except Exception:
-                    store = None
-            # RCCL (native communicator over xGMI) for device engines whose
-            # group is the nccl backend or that run alone; a gloo group (CPU
-            # engine, or the MRH_DIST_BACKEND=gloo rehearsal of several ranks
-            # on one GPU) keeps its process group as the transport
-            transport = "pg" if self.backend == "gloo" else ""
-            self._native = C.NativeComm(self.pg, self.device, store, transport)
-        return self._native
+                store = dist.distributed_c10d._get_default_store()
+                wr, ws = dist.get_rank(), dist.get_world_size()
+            n = C.NativeComm(self.pg, self.device, store, self.transport,
+                             self.members if self.size > 1 else [], wr, ws)
+            if self.size > 1:
+                _NATIVE[key] = n
+                _install_exit_hooks()
+            else:
+                self.__dict__["_native1"] = n
+        return n if self.size > 1 else self.__dict__["_native1"]
+
+    def rccl_info(self):
+        """What RCCL itself reports for this communicator (ncclCommCount,
+        ncclCommCuDevice, ncclCommUserRank) plus the number of RCCL
+        communicators this process holds."""
+        return dict(self.native.rccl_info())
 
     # ---- scalar collectives (every MR op returns a global count) ----------
     def _t(self, vals, dtype):
-        return torch.tensor(vals, dtype=dtype, device=self.device)
+        return torch.tensor(vals, dtype=dtype, device=self._sdev)
 
     def allreduce(self, vals, op="sum", dtype=torch.int64):
         scalar = not isinstance(vals, (list, tuple))
@@ -96,9 +178,10 @@ class Comm:
         return out
 
     def barrier(self):
+        """Host barrier (MPI_Barrier): every rank has reached this point; it
+        does not wait for queued device work (torch.cuda.synchronize does)."""
         if self.size > 1:
-            if self.is_cuda:
-                # a 1-element allreduce on the device is the RCCL barrier
+            if self.backend == "nccl":
                 self.allreduce(0)
             else:
                 dist.barrier(group=self.group)
@@ -108,7 +191,7 @@ class Comm:
             return obj
         lst = [obj]
         dist.broadcast_object_list(lst, src=root, group=self.group,
-                                   device=torch.device(self.device) if self.is_cuda else None)
+                                   device=torch.device(self.device) if self.backend == "nccl" else None)
         return lst[0]
 
     def wtime(self):
@@ -117,16 +200,18 @@ class Comm:
         return time.perf_counter()
 
     def split(self, color, key=0):
-        """MPI_Comm_split analog (OINK -partition worlds): new group per color."""
+        """MPI_Comm_split analog (OINK -partition worlds): new group per color.
+        Its native communicator gets its own RCCL id key (tag + member list +
+        sequence), so colours never read each other's id."""
         if self.size == 1:
             return self
         colors = self.allgather(float(color))
         members = sorted(r for r, c in enumerate(colors) if c == float(color))
         groups = {}
         for c in sorted(set(colors)):
-            ranks = [r for r, cc in enumerate(colors) if cc == c]
+            ranks = [self.members[r] for r, cc in enumerate(colors) if cc == c]
             groups[c] = dist.new_group(ranks, backend=self.backend)
-        return Comm(groups[float(color)], device=self.device) if members else None
+        return Comm(groups[float(color)], device=self.device, transport=self.transport) if members else None
 
 
 def init(backend=None, timeout_s=None):
@@ -139,12 +224,13 @@ def init(backend=None, timeout_s=None):
     if timeout_s is None:
         timeout_s = int(os.environ.get("MRH_COMM_TIMEOUT", "600"))
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    # MRH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a
-    # device, LOCAL_RANK modulo the device count); production is "nccl" = RCCL
-    backend = backend or os.environ.get("MRH_DIST_BACKEND") or None
+    # torch.distributed is the HOST group (gloo): host objects and scalars.
+    # The device data plane is the engine's own RCCL communicator (one per
+    # process). MRH_DIST_BACKEND=nccl is honoured but adds a second RCCL
+    # communicator per process; ranks may share GPUs (LOCAL_RANK modulo the
+    # device count: the rehearsal on a 1-GPU box, engine transport "pg").
+    backend = backend or os.environ.get("MRH_DIST_BACKEND") or "gloo"
     if ws > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
         if torch.cuda.is_available():
             local = int(os.environ.get("LOCAL_RANK", "0"))
             torch.cuda.set_device(local % max(1, torch.cuda.device_count()))

@@ -61,6 +61,11 @@ def next_slot(name: str, n: int = 2) -> int:
     return i % n
 
 
+def generation(name: str) -> int:
+    """How many slots of ring `name` have been handed out so far."""
+    return _ring.get(name, 0)
+
+
 def clear():
     _dev.clear()
     _host.clear()

@@ -1,5 +1,5 @@
 """bench.py's own multi-rank launcher (`--gpus N` without torchrun): it must
-spawn N ranks that really join one job (n_gpus / rccl_ranks = N, global
+spawn N ranks that really join one job (n_gpus / ranks_joined = N, global
 counts = N x the 1-rank counts for this weak-scaling workload) and keep the
 single-rank path unchanged. CPU engine, gloo; the driver runs the same script
 under torchrun on an 8-GPU node."""
@@ -28,8 +28,8 @@ def _bench(n):
 
 def test_bench_spawns_n_ranks():
     one, three = _bench(1), _bench(3)
-    assert one["n_gpus"] == 1 and one["rccl_ranks"] == 1
-    assert three["n_gpus"] == 3 and three["rccl_ranks"] == 3
+    assert one["n_gpus"] == 1 and one["ranks_joined"] == 1
+    assert three["n_gpus"] == 3 and three["ranks_joined"] == 3
     assert three["config"]["parallelism"] == "dp3"
     assert three["kv_pairs_per_step"] == 3 * one["kv_pairs_per_step"]
     assert three["config"]["global_batch"] == 3 * one["config"]["global_batch"]
@@ -44,7 +44,7 @@ def test_bench_eight_ranks():
     """the driver's largest scaling point, N = 8 (one node), rehearsed on the
     CPU engine: 8 ranks join, global counts are 8x, PageRank keeps its graph"""
     one, eight = _bench(1), _bench(8)
-    assert eight["n_gpus"] == eight["rccl_ranks"] == 8 and eight["config"]["parallelism"] == "dp8"
+    assert eight["n_gpus"] == eight["ranks_joined"] == 8 and eight["config"]["parallelism"] == "dp8"
     assert eight["kv_pairs_per_step"] == 8 * one["kv_pairs_per_step"]
     assert eight["pagerank_config"]["edges"] == one["pagerank_config"]["edges"]
     assert "pagerank_error" not in eight
@@ -77,6 +77,9 @@ def test_bench_two_ranks_on_one_gpu():
         assert len(lines) == 1, r.stdout
         out[n] = json.loads(lines[0])
     one, two = out[1], out[2]
-    assert two["n_gpus"] == two["rccl_ranks"] == 2 and two["backend"]["torch.distributed"] == "gloo"
+    assert two["n_gpus"] == two["ranks_joined"] == 2 and two["backend"]["torch.distributed"].startswith("gloo")
+    # ranks share the GPU: the engine runs the pg transport; the RCCL facts come
+    # from a one-rank probe communicator per rank
+    assert two["engine_transport"].startswith("pg") and two["rccl_comm_count"] == 1
     assert two["kv_pairs_per_step"] == 2 * one["kv_pairs_per_step"]
     assert two["pagerank_config"]["edges"] == one["pagerank_config"]["edges"]
