@@ -211,6 +211,31 @@ def bench_pagerank_extra(comm, args):
     return out
 
 
+def _extra(comm, prefix, fn, args, **over):
+    """Run another BASELINE workload inside the headline invocation and report
+    it under prefixed keys; a failure is recorded, not fatal (the failing
+    rank's native op poisons the job, so its peers fail fast too)."""
+    import copy
+    a = copy.copy(args)
+    for k, v in over.items():
+        setattr(a, k, v)
+    try:
+        r = fn(comm, a)
+    except Exception as e:  # noqa: BLE001
+        print(f"bench.py rank {comm.rank}: {prefix} extra failed: {e}", file=sys.stderr, flush=True)
+        return {f"{prefix}_error": f"{type(e).__name__}: {e}"[:500]}
+    finally:
+        if comm.is_cuda:
+            torch.cuda.empty_cache()
+    out = {f"{prefix}_kvps": r["value"], f"{prefix}_ms": r["ms_per_step"], f"{prefix}_setup_ms": r.get("setup_ms"),
+           f"{prefix}_config": dict(r["config"], steps=a.steps, warmup=a.warmup, scaling=r.get("scaling", "weak"),
+                                    metric=r["metric"])}
+    for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices"):
+        if k in r:
+            out[f"{prefix}_{k}"] = r[k]
+    return out
+
+
 def rccl_record(comm):
     """What RCCL itself reports about the job's communicator, from every rank:
     ncclCommCount (must equal N on every rank), ncclCommCuDevice, the GPU's
@@ -277,6 +302,12 @@ def main():
                     help="RMAT scale of the PageRank extra (26 on GPU, 14 on CPU; 0 = skip)")
     ap.add_argument("--pagerank-steps", type=int, default=3, help="timed 20-iteration PageRank runs")
     ap.add_argument("--pagerank-warmup", type=int, default=1)
+    ap.add_argument("--trifind-scale", type=int, default=None,
+                    help="RMAT scale of the tri_find extra (BASELINE config 5: 24 on GPU, 12 on CPU; 0 = skip)")
+    ap.add_argument("--wordfreq-bytes", type=float, default=None,
+                    help="text bytes per GPU of the wordfreq extra (BASELINE config 3: 1 GiB per GPU = 8 GiB on "
+                         "8 GPUs; 4e6 on CPU; 0 = skip)")
+    ap.add_argument("--extra-steps", type=int, default=3, help="timed steps of the tri_find / wordfreq extras")
     args = ap.parse_args()
     if args.scale is None:
         args.scale = 24 if args.workload == "trifind" else 26
@@ -294,6 +325,10 @@ def main():
         raise SystemExit(f"bench.py: {comm.size} ranks joined, expected {args.gpus}")
     if args.pagerank_scale is None:
         args.pagerank_scale = 26 if comm.is_cuda else 14
+    if args.trifind_scale is None:
+        args.trifind_scale = 24 if comm.is_cuda else 12
+    if args.wordfreq_bytes is None:
+        args.wordfreq_bytes = float(1 << 30) if comm.is_cuda else 4e6
     if args.workload == "invertedindex":
         res = bench_inverted_index(comm, args)
     elif args.workload == "pagerank":
@@ -322,6 +357,17 @@ def main():
         except Exception as e:  # noqa: BLE001
             res["pagerank_error"] = f"{type(e).__name__}: {e}"[:500]
             print(f"bench.py rank {comm.rank}: PageRank extra failed: {e}", file=sys.stderr, flush=True)
+    if args.workload == "invertedindex":
+        # BASELINE configs 5 and 3 in the same driver-measured record
+        if args.trifind_scale > 0:
+            from gpu_mapreduce_amd.models.triangles import bench_trifind
+            res.update(_extra(comm, "trifind", bench_trifind, args, scale=args.trifind_scale,
+                              steps=args.extra_steps, warmup=1))
+        if args.wordfreq_bytes > 0:
+            from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
+            res.update(_extra(comm, "wordfreq", bench_wordfreq, args, bytes_per_gpu=args.wordfreq_bytes,
+                              file_bytes=min(args.file_bytes, int(args.wordfreq_bytes)),
+                              steps=args.extra_steps, warmup=1))
     res.update(rrec)
     res["ranks_joined"] = comm.size
     res["backend"] = {"torch.distributed": (comm.backend or "none (world size 1)") + " (host objects/scalars only)",

@@ -75,9 +75,13 @@ def bench_trifind(comm, args):
     ntotal = (1 << scale) * ef
     P, me = comm.size, comm.rank
     lo, hi = me * ntotal // P, (me + 1) * ntotal // P
+    ts = time.perf_counter()
     kv = C.map_rmat(hi - lo, scale, *GRAPH500, 0.0, args.seed, lo, comm.device)
     edges = kv.kdata.view(torch.int64).view(-1, 2)
     del kv
+    if comm.is_cuda:
+        torch.cuda.synchronize()
+    setup = comm.allreduce(time.perf_counter() - ts, "max", dtype=torch.float64)
 
     def sync():
         if comm.is_cuda:
@@ -102,6 +106,6 @@ def bench_trifind(comm, args):
         "baseline_note": "reference publishes no tri_find number",
         "config": {"model": "tri_find", "global_batch": ntotal, "seq_len": 1, "parallelism": f"dp{P}",
                    "scale": scale, "edgefactor": ef, "rmat": "graph500 a=.57 b=c=.19"},
-        "triangles": ntri, "unique_edges": g.nedge, "scaling": "strong",
+        "triangles": ntri, "unique_edges": g.nedge, "scaling": "strong", "setup_ms": setup * 1e3,
         "hub_vertices": int(C.tri_last_hub_size()),
     }

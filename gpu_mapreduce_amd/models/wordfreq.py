@@ -134,6 +134,7 @@ def bench_wordfreq(comm, args):
     from ..utils import synth
     per_gpu = int(args.bytes_per_gpu)
     chunk = int(args.file_bytes)
+    ts = time.perf_counter()
     chunks = []
     left = per_gpu
     i = 0
@@ -145,6 +146,7 @@ def bench_wordfreq(comm, args):
         i += 1
     if comm.is_cuda:
         torch.cuda.empty_cache()
+    setup = comm.allreduce(time.perf_counter() - ts, "max", dtype=torch.float64)
 
     def step():
         app = WordFreq(MapReduce(comm), chunks)
@@ -175,6 +177,7 @@ def bench_wordfreq(comm, args):
         "words": app.nwords,
         "unique_words": app.nunique,
         "top3": app.top[:3],
+        "setup_ms": setup * 1e3,
         "config": {"model": "wordfreq", "global_batch": total, "seq_len": chunk,
                    "parallelism": f"dp{comm.size}", "bytes_per_gpu": per_gpu},
     }

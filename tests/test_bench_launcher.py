@@ -36,8 +36,13 @@ def test_bench_spawns_n_ranks():
     # the PageRank extra is strong scaling: same graph, same edge count
     assert three["pagerank_config"]["edges"] == one["pagerank_config"]["edges"] == 16 * 1024
     for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
-              "data", "pagerank_kvps", "pagerank_ms", "pagerank_setup_ms"):
-        assert k in three
+              "data", "pagerank_kvps", "pagerank_ms", "pagerank_setup_ms",
+              # BASELINE configs 5 and 3 ride in the same record
+              "trifind_kvps", "trifind_ms", "trifind_setup_ms", "trifind_triangles",
+              "wordfreq_kvps", "wordfreq_ms", "wordfreq_setup_ms", "wordfreq_words"):
+        assert k in three, k
+    assert three["trifind_triangles"] == one["trifind_triangles"] > 0   # strong scaling: same graph
+    assert three["wordfreq_words"] == 3 * one["wordfreq_words"]          # weak scaling: text per rank
 
 
 def test_bench_eight_ranks():

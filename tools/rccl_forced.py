@@ -22,6 +22,14 @@ def comm(force):
 rc, lc = comm(True), comm(False)
 assert rc.native.transport == "rccl", rc.native.transport
 assert lc.native.transport == "local"
+# what RCCL itself reports about the forced communicator and a probe one
+info = rc.rccl_info()
+assert (info["comm_count"], info["cu_device"], info["user_rank"]) == (1, 0, 0), info
+assert info["live_comms"] == 1, info          # exactly one RCCL communicator in this process
+assert lc.rccl_info()["comm_count"] == -1
+probe = C.rccl_self_probe(0)
+assert (probe["comm_count"], probe["cu_device"]) == (1, 0), probe
+assert C.live_rccl_comms() == 1               # the probe is gone again
 
 def var_kv(keys, vals):
     import itertools
