@@ -123,8 +123,10 @@ class Comm:
         this group for host scalars, the root store for the RCCL id
         rendezvous and mapstyle 2, and the process's RCCL communicator over
         these members (shared with every other Comm over them)."""
-        key = (tuple(self.members) if self.size > 1 else ("self", id(self)), self.device, self.transport)
-        n = _NATIVE.get(key)
+        if self.size == 1 and "_native1" in self.__dict__:
+            return self.__dict__["_native1"]
+        key = (tuple(self.members), self.device, self.transport)
+        n = _NATIVE.get(key) if self.size > 1 else None
         if n is None:
             from .._ext import C
             store = None
