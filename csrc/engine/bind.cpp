@@ -198,6 +198,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            })
       .def("add_kv", &KeyValue::add_kv, py::call_guard<py::gil_scoped_release>())
       .def("enable_grouping", &KeyValue::enable_grouping)
+      .def("reserve_grouping", &KeyValue::reserve_grouping)
       .def_property_readonly("grouping", &KeyValue::grouping)
       .def("size", &KeyValue::size)
       .def("finish", &KeyValue::finish)

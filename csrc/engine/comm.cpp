@@ -187,7 +187,7 @@ void Comm::host_wait() const {
     throw std::runtime_error("mrhip: hipEventCreate failed");
   struct Drop {
     hipEvent_t e;
-    ~Drop() { (void)hipEventDestroy(e); }
+    ~Drop() { (void)hipEventDestroy(e); }  // destructor: cannot throw
   } drop{ev};
   if (hipEventRecord(ev, cur(dev_)) != hipSuccess) throw std::runtime_error("mrhip: hipEventRecord failed");
   // the deadline replaces the watchdog of a c10d RCCL group: a collective

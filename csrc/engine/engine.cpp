@@ -271,6 +271,31 @@ std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& k
   return {ko, vo, (end_bit - begin_bit) / 8};
 }
 
+at::Tensor radix_sort_keys(const at::Tensor& keys_in, int begin_bit, int end_bit, bool skip_trivial) {
+  at::Tensor keys = keys_in.contiguous();
+  const int64_t n = keys.numel();
+  if (keys.scalar_type() != at::kLong) fail("radix_sort_keys: int64 keys");
+  begin_bit = (begin_bit / 8) * 8;
+  end_bit = std::min(64, ((end_bit + 7) / 8) * 8);
+  at::Tensor ko = at::empty_like(keys);
+  if (n == 0) return ko;
+  if (keys.is_cuda()) {
+    at::Tensor ka = at::empty_like(keys);
+    at::Tensor tmp = scratch(k::radix_temp_bytes(n), keys.device());
+    int passes = 0;
+    k::radix_sort_u64_u32(P0<uint64_t>(keys), nullptr, P0<uint64_t>(ko), nullptr, P0<uint64_t>(ka), nullptr, n,
+                          begin_bit, end_bit, P0<void>(tmp), cur_stream(), &passes, skip_trivial);
+    return ko;
+  }
+  uint64_t mask = 0;
+  for (int b = begin_bit; b < end_bit; ++b) mask |= (1ull << b);
+  const uint64_t* k = P0<uint64_t>(keys);
+  uint64_t* o = P0<uint64_t>(ko);
+  std::copy(k, k + n, o);
+  std::stable_sort(o, o + n, [&](uint64_t a, uint64_t b) { return (a & mask) < (b & mask); });
+  return ko;
+}
+
 at::Tensor hash32_keys(const KV& kv, uint32_t seed) {
   const at::Device dev = kv.device();
   at::Tensor out = at::empty({kv.n}, opt(dev, at::kInt));
@@ -484,6 +509,27 @@ void exact_regroup_host(const KV& kv, const at::Tensor& h64_sorted_dev, at::Tens
 at::Tensor seg_heads(const at::Tensor& seg, int64_t nseg) { return seg.narrow(0, 0, nseg); }
 
 }  // namespace
+
+at::Tensor segments_from_flags(const at::Tensor& flags_in) {
+  const at::Tensor flags = flags_in.contiguous();
+  const int64_t n = flags.numel();
+  const at::Device dev = flags.device();
+  if (n == 0) return at::zeros({1}, opt(dev, at::kLong));
+  at::Tensor pos = scan_u32(flags);
+  const int64_t nseg = (int64_t)(uint32_t)pos[n].item<int32_t>();
+  at::Tensor seg = at::empty({nseg + 1}, opt(dev, at::kLong));
+  if (dev.is_cuda()) {
+    k::compact_heads(P0<uint32_t>(flags), P0<uint32_t>(pos), n, P0<int64_t>(seg), cur_stream());
+  } else {
+    const uint32_t* f = P0<uint32_t>(flags);
+    const uint32_t* p = P0<uint32_t>(pos);
+    int64_t* sp = P0<int64_t>(seg);
+    for (int64_t i = 0; i < n; ++i)
+      if (f[i]) sp[p[i]] = i;
+    sp[nseg] = n;
+  }
+  return seg;
+}
 
 at::Tensor segments_sorted(const at::Tensor& sorted_keys) {
   at::Tensor flags, pos, seg;

@@ -235,7 +235,137 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
   at::Tensor none;
   to_source_owner(*comm, e, none);
   nedge = e.size(0);
-  // out-degree = group-by source (convert on u64 keys)
+  if (dev.is_cuda() && nedge < (int64_t(1) << 32) && N < (int64_t(1) << 31)) build_device(e.contiguous());
+  else build_host(e);
+  e = at::Tensor();
+  const int64_t ngrp = seg_.numel() - 1;
+  // one GPU, opt-in (MRH_PR_BLOCKING=1): propagation blocking (pbpr.hip).
+  // Measured on RMAT-26 at 8.9 ms per iteration (phase 1 3.5 + phase 2 5.4)
+  // vs 7.9 ms for the pull kernel, whose 60 % L2 hit rate on the
+  // degree-sorted gathers already beats two streaming passes
+  // (profiles/r2_pagerank_blocking.txt); kept for graphs without hub locality
+  {
+    const char* env = std::getenv("MRH_PR_BLOCKING");
+    const bool want = env && *env == '1';
+    if (want && !comm->distributed() && dev.is_cuda() && nedge > 0 && nedge < (int64_t(1) << 31) && ngrp > 0)
+      build_blocking(vid_.index_select(0, segment_ids(seg_, ngrp, nedge)));
+  }
+  acc_ = at::empty({nlocal}, opt(dev, at::kFloat));
+  if (ngrp > 0 && use_seg_index(dev) && !pb_) six_ = seg_index(seg_, nedge);
+  reset();
+}
+
+// Device build: two keys-only sorts of packed edges, no group-by, no
+// payload arrays, no permutation gathers.
+//  1. edges packed as (local source << 32 | destination) and sorted on the
+//     source bits: every out-degree is a run length (a histogram of random
+//     global atomics ran 5x slower — they execute at the memory side);
+//  2. the nlocal vertices sorted by degree, descending and stable (R-MAT hubs
+//     are spread over ids with few 1-bits; clustering them keeps the hot part
+//     of the gathered rank array cache-resident); k_pr_relabel writes the new
+//     id of every vertex, the dangling flags and 1/outdeg in the same pass;
+//  3. the source-sorted edges repacked as (destination group << 32 | new
+//     source id) — the source ids are monotone, so the relabel is a
+//     sequential walk — and sorted on the destination bits;
+//  4. unpack: the int32 source stream + group head flags -> CSR segments.
+void PageRankPlan::build_device(const at::Tensor& e) {
+  const hipStream_t s = at::hip::getCurrentHIPStream();
+  const bool dist = comm->distributed();
+  const int64_t nlmax = (N + P - 1) / P;
+  auto chk = [](hipError_t r, const char* what) {
+    if (r != hipSuccess) throw std::runtime_error(std::string("PageRankPlan: ") + what + ": " + hipGetErrorString(r));
+  };
+  auto bits_for = [](int64_t maxval) {
+    int b = 1;
+    while (b < 31 && (int64_t(1) << b) <= maxval) ++b;
+    return b;
+  };
+  // 1. by source
+  at::Tensor su;
+  {
+    at::Tensor packed = at::empty({nedge}, opt(dev, at::kLong));
+    k::pr_pack_src(e.data_ptr<int64_t>(), nedge, P, reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
+    su = radix_sort_keys(packed, 32, 32 + bits_for(std::max<int64_t>(nlocal - 1, 0)), false);
+  }
+  at::Tensor deg = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
+  chk(hipMemsetAsync(deg.data_ptr(), 0, deg.numel() * 4, s), "hipMemsetAsync");
+  if (nedge > 0) {
+    at::Tensor flags = at::empty({nedge}, opt(dev, at::kInt));
+    k::pr_heads(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, reinterpret_cast<uint32_t*>(flags.data_ptr()),
+                s);
+    at::Tensor useg = segments_from_flags(flags);
+    flags = at::Tensor();
+    k::pr_run_degree(reinterpret_cast<const uint64_t*>(su.data_ptr()), useg.data_ptr<int64_t>(), useg.numel() - 1,
+                     reinterpret_cast<uint32_t*>(deg.data_ptr()), s);
+  }
+  // 2. vertices by degree
+  at::Tensor nid = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
+  order_ = at::empty({nlocal}, opt(dev, at::kLong));
+  dangling_ = at::empty({nlocal}, opt(dev, at::kByte));
+  invdeg_ = at::empty({nlocal}, opt(dev, at::kFloat));
+  at::Tensor nd = at::empty({1}, opt(dev, at::kLong));
+  chk(hipMemsetAsync(nd.data_ptr(), 0, 8, s), "hipMemsetAsync");
+  if (nlocal > 0) {
+    at::Tensor dkey = at::empty({nlocal}, opt(dev, at::kLong)), io = at::empty({nlocal}, opt(dev, at::kInt));
+    k::pr_degkey(reinterpret_cast<const uint32_t*>(deg.data_ptr()), nlocal, reinterpret_cast<uint64_t*>(dkey.data_ptr()),
+                 reinterpret_cast<uint32_t*>(io.data_ptr()), s);
+    // 32-bit key; constant high digits (every degree < 2^24) are skipped
+    at::Tensor ord = std::get<1>(radix_sort_pairs(dkey, io, 0, 32, true));
+    dkey = io = at::Tensor();
+    k::pr_relabel(reinterpret_cast<const uint32_t*>(ord.data_ptr()), reinterpret_cast<const uint32_t*>(deg.data_ptr()),
+                  nlocal, nid.data_ptr<int32_t>(), order_.data_ptr<int64_t>(), dangling_.data_ptr<uint8_t>(),
+                  invdeg_.data_ptr<float>(), reinterpret_cast<unsigned long long*>(nd.data_ptr()), s);
+  }
+  deg = at::Tensor();
+  // 3. by destination group, new source ids in the low word
+  const int64_t himax = !dist ? std::max<int64_t>(N - 1, 0) : P * nlmax - 1;
+  at::Tensor sorted;
+  {
+    at::Tensor packed = at::empty({nedge}, opt(dev, at::kLong));
+    k::pr_pack(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, P, nlmax, !dist, nid.data_ptr<int32_t>(),
+               reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
+    su = at::Tensor();
+    sorted = radix_sort_keys(packed, 32, 32 + bits_for(himax), false);
+  }
+  // 4. unpack
+  src_ = at::empty({nedge}, opt(dev, at::kInt));
+  {
+    at::Tensor flags = at::empty({nedge}, opt(dev, at::kInt));
+    k::pr_unpack(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), nedge, src_.data_ptr<int32_t>(),
+                 reinterpret_cast<uint32_t*>(flags.data_ptr()), s);
+    seg_ = segments_from_flags(flags);
+  }
+  const int64_t ngrp = seg_.numel() - 1;
+  at::Tensor hi = at::empty({ngrp}, opt(dev, at::kLong));
+  k::pr_group_hi(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), seg_.data_ptr<int64_t>(), ngrp,
+                 hi.data_ptr<int64_t>(), s);
+  sorted = at::Tensor();
+  w_ = at::empty({0}, opt(dev, at::kFloat));  // weights folded into c = r / outdeg
+  send_ = at::empty({ngrp}, opt(dev, at::kFloat));
+  if (dist) {
+    // hi = owner * nlmax + local id at the owner -> global destination id
+    at::Tensor ujv = at::remainder(hi, nlmax) * P + at::floor_divide(hi, nlmax);
+    build_exchange(ujv, nid.narrow(0, 0, nlocal));
+  } else {
+    vid_ = at::empty({ngrp}, opt(dev, at::kInt));  // the group's destination, as a new id
+    k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nid.data_ptr<int32_t>(), vid_.data_ptr<int32_t>(), s);
+  }
+  ndangling = comm->allreduce(nd.item<int64_t>(), Comm::SUM);
+}
+
+void PageRankPlan::build_exchange(const at::Tensor& ujv, const at::Tensor& new_of_old) {
+  send_splits_ = to_vec(owner_counts(ujv, P));
+  recv_splits_ = comm->alltoall_counts(send_splits_);
+  at::Tensor rids = comm->alltoallv(ujv.contiguous(), send_splits_, recv_splits_);
+  auto [rs, rperm] = sort_with_perm(at::floor_divide(rids, P));
+  rseg_ = segments(rs);
+  rperm_ = rperm;
+  rvid_ = new_of_old.index_select(0, rs.index_select(0, rseg_.narrow(0, 0, rseg_.numel() - 1))).contiguous();
+  recv_ = at::empty({rids.numel()}, opt(dev, at::kFloat));
+}
+
+// CPU engine: the same plan from tensor ops (group-by source for the degrees)
+void PageRankPlan::build_host(const at::Tensor& e) {
   KV kv = make_kv(e.select(1, 0).contiguous().view(at::kByte), std::nullopt, e.select(1, 1).contiguous().view(at::kByte),
                   std::nullopt, nedge, dev);
   at::Tensor vi, deg, vj;
@@ -249,9 +379,6 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
   }
   at::Tensor outdeg = at::zeros({nlocal}, opt(dev, at::kLong));
   if (vi.numel()) outdeg.index_put_({at::floor_divide(vi, P)}, deg);
-  // relabel local vertices by out-degree (descending, stable): R-MAT hubs are
-  // spread over ids with few 1-bits; clustering them keeps the hot part of the
-  // gathered rank array cache-resident
   at::Tensor dkey = (int64_t(1) << 40) - outdeg;
   order_ = sort_with_perm(dkey, 48).second.to(at::kLong);
   at::Tensor new_of_old = at::empty({nlocal}, opt(dev, at::kInt));
@@ -262,42 +389,18 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
   at::Tensor key = dist ? at::bitwise_or(at::bitwise_left_shift(at::remainder(vj, P), 40), vj) : vj.clone();
   auto [ks, perm] = sort_with_perm(key);
   src_ = src_local.index_select(0, perm.to(at::kLong)).contiguous();
-  w_ = at::empty({0}, opt(dev, at::kFloat));  // weights folded into c = r / outdeg
+  w_ = at::empty({0}, opt(dev, at::kFloat));
   seg_ = segments(ks);
   const int64_t ngrp = seg_.numel() - 1;
-  at::Tensor ujv = at::bitwise_and(ks.index_select(0, seg_.narrow(0, 0, ngrp)), VMASK);
+  at::Tensor gk = ks.index_select(0, seg_.narrow(0, 0, ngrp));
   send_ = at::empty({ngrp}, opt(dev, at::kFloat));
-  if (dist) {
-    send_splits_ = to_vec(owner_counts(ujv, P));
-    recv_splits_ = comm->alltoall_counts(send_splits_);
-    at::Tensor rids = comm->alltoallv(ujv.contiguous(), send_splits_, recv_splits_);
-    auto [rs, rperm] = sort_with_perm(at::floor_divide(rids, P));
-    rseg_ = segments(rs);
-    rperm_ = rperm;
-    rvid_ = new_of_old.index_select(0, rs.index_select(0, rseg_.narrow(0, 0, rseg_.numel() - 1))).contiguous();
-    recv_ = at::empty({rids.numel()}, opt(dev, at::kFloat));
-  } else {
-    vid_ = new_of_old.index_select(0, at::floor_divide(ujv, P)).contiguous();
-  }
-  // one GPU, opt-in (MRH_PR_BLOCKING=1): propagation blocking (pbpr.hip).
-  // Measured on RMAT-26 at 8.9 ms per iteration (phase 1 3.5 + phase 2 5.4)
-  // vs 7.9 ms for the pull kernel, whose 60 % L2 hit rate on the
-  // degree-sorted gathers already beats two streaming passes
-  // (profiles/r2_pagerank_blocking.txt); kept for graphs without hub locality
-  {
-    const char* e = std::getenv("MRH_PR_BLOCKING");
-    const bool want = e && *e == '1';
-    if (want && !dist && dev.is_cuda() && nedge > 0 && nedge < (int64_t(1) << 31) && ngrp > 0)
-      build_blocking(vid_.index_select(0, segment_ids(seg_, ngrp, nedge)));
-  }
+  if (dist) build_exchange(at::bitwise_and(gk, VMASK), new_of_old);
+  else vid_ = new_of_old.index_select(0, at::floor_divide(gk, P)).contiguous();
   at::Tensor deg_new = outdeg.index_select(0, order_);
   dangling_ = (deg_new == 0).to(at::kByte);
   invdeg_ = at::where(deg_new > 0, 1.0 / deg_new.clamp_min(1).to(at::kDouble), at::zeros_like(deg_new, at::kDouble))
                 .to(at::kFloat);
   ndangling = comm->allreduce(dangling_.sum().item<int64_t>(), Comm::SUM);
-  acc_ = at::empty({nlocal}, opt(dev, at::kFloat));
-  if (ngrp > 0 && use_seg_index(dev) && !pb_) six_ = seg_index(seg_, nedge);
-  reset();
 }
 
 // Static layout of the propagation-blocked iteration (pbpr.hip): phase-1

@@ -93,6 +93,13 @@ class PageRankPlan {
   at::Tensor r_, rn_, c_, dmass_, stats_;
   SegIndex six_;
   std::vector<int64_t> send_splits_, recv_splits_;
+  // the plan from this rank's edges (source-owned): device kernels, or the
+  // tensor-op twin on the CPU engine
+  void build_device(const at::Tensor& e);
+  void build_host(const at::Tensor& e);
+  // several ranks: the destination-owner side of the exchange from the
+  // group destinations ujv (global ids) and the new id of every old local id
+  void build_exchange(const at::Tensor& ujv, const at::Tensor& new_of_old);
   // propagation blocking (one GPU; pbpr.hip): phase-1 sources and slots,
   // phase-2 16-bit destinations, contributions, work units
   void build_blocking(const at::Tensor& dst_new);

@@ -99,6 +99,23 @@ void GroupIndex::reserve_table(int64_t groups) {
   cap_ = cap;
 }
 
+void GroupIndex::reserve(int64_t rows, int64_t key_bytes, int64_t value_bytes) {
+  if (rows <= 0) return;
+  reserve_rows(rows);
+  reserve_table(rows);
+  auto col = [&](int w, int64_t bytes, at::Tensor* ad, at::Tensor* aoff, int64_t used) {
+    if (w == -2) return;  // layout unknown until the first part
+    if (w >= 0) {
+      grow(ad, std::max<int64_t>(rows * w, 1), n_ * w, at::kByte, dev_);
+    } else {
+      grow(ad, std::max<int64_t>(bytes, 1), used, at::kByte, dev_);
+      grow(aoff, rows + 1, n_ + 1, at::kLong, dev_);
+    }
+  };
+  col(kw_, key_bytes, &kd_, &koff_, kbytes_);
+  col(vw_, value_bytes, &vd_, &voff_, vbytes_);
+}
+
 void GroupIndex::append_col(const at::Tensor& pd, const at::Tensor& poff, int w, int64_t n, at::Tensor* ad,
                             at::Tensor* aoff, int64_t* bytes) {
   const bool cuda = dev_.is_cuda();

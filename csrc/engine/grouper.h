@@ -31,6 +31,11 @@ class GroupIndex {
   // can `part` be appended (same fixed widths / variable-ness as the parts so far)?
   bool accepts(const KV& part) const;
   void add(const KV& part);
+  // capacity hint before (or between) adds: rows, key bytes and value bytes
+  // the whole index will hold, so the arenas, the per-row arrays and the hash
+  // table are sized once (no x1.5 regrow copies, no rehash) — the producer
+  // knows its input size (InvertedIndex: part-file bytes)
+  void reserve(int64_t rows, int64_t key_bytes, int64_t value_bytes);
   int64_t size() const { return n_; }
   // the appended KV (views of the arenas)
   KV kv() const;

@@ -40,8 +40,8 @@ Fault parse_fault() {
   std::string tok;
   std::vector<std::string> p;
   while (std::getline(ss, tok, ':')) p.push_back(tok);
-  if (p.size() < 3 || (p[0] != "abort" && p[0] != "throw" && p[0] != "oom"))
-    throw std::runtime_error("MRH_FAULT must be kind:op:rank[:nth] with kind abort|throw|oom, got '" +
+  if (p.size() < 3 || (p[0] != "abort" && p[0] != "throw" && p[0] != "oom" && p[0] != "hip"))
+    throw std::runtime_error("MRH_FAULT must be kind:op:rank[:nth] with kind abort|throw|oom|hip, got '" +
                              std::string(s) + "'");
   f.kind = p[0];
   f.op = p[1];
@@ -123,6 +123,16 @@ void fault_point(const char* op, int rank) {
     std::_Exit(3);
   }
   if (due(op, rank, "throw")) throw std::runtime_error(std::string("MRH_FAULT: injected failure in ") + op);
+}
+
+void hip_check(hipError_t e, const char* site, int rank) {
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    if (e == hipSuccess && due(site, rank, "hip")) e = hipErrorUnknown;  // injected (MRH_FAULT=hip:site:rank)
+  }
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string("mrhip: HIP error at ") + site + " on rank " + std::to_string(rank) + ": " +
+                             hipGetErrorString(e));
 }
 
 bool fault_oom(const char* op, int rank) {

@@ -19,12 +19,18 @@
 //    nth (default 1st) entry of MapReduce op `op` on rank `rank` (-1 = every
 //    rank): kind "abort" ends the process (exit status 3, no cleanup, like a
 //    crashed rank), "throw" raises an error, "oom" raises a HIP OOM inside the
-//    op's oom_retry (exercising the spill-and-retry path);
+//    op's oom_retry (exercising the spill-and-retry path), "hip" makes the
+//    checked HIP call at site `op` (hip_check) fail with hipErrorUnknown;
+//  * checked HIP calls: every HIP call on a data path goes through
+//    hip_check(call, site, rank) — a failed copy, event or stream wait is an
+//    exception (which poisons the job's communicator on the way out), never a
+//    silently ignored status and garbage output;
 //  * check mode: MRH_CHECK=1 validates the KV/KMV invariants (offset arrays
 //    monotone and consistent with the arenas, segment array covering every
 //    value, widths) after every op, naming the op that broke them.
 #pragma once
 #include <c10/util/Exception.h>
+#include <hip/hip_runtime.h>
 
 #include <functional>
 #include <string>
@@ -42,6 +48,9 @@ int comm_timeout_seconds();
 
 // fault injection hook at op entry ("abort" / "throw" kinds)
 void fault_point(const char* op, int rank);
+// throws (naming `site` and the rank) unless e == hipSuccess; an armed
+// MRH_FAULT=hip:site:rank turns a success into hipErrorUnknown
+void hip_check(hipError_t e, const char* site, int rank);
 // true if an injected OOM is due for this op on this rank (consumed)
 bool fault_oom(const char* op, int rank);
 

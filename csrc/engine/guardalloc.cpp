@@ -68,22 +68,34 @@ void report(void* user, const Block& b, int64_t front, int64_t back, const std::
   reports().push_back(r);
 }
 
+// allocator callbacks cannot throw through ATen: a failed runtime call is
+// printed and turned into "no memory" (alloc) or a logged error (free)
+bool ok_or_log(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  std::fprintf(stderr, "mrhip guard: %s failed: %s\n", what, hipGetErrorString(e));
+  return false;
+}
+
 void* g_alloc(size_t size, int device, hipStream_t) {
   if (size == 0) return nullptr;
-  (void)hipSetDevice(device);
+  if (!ok_or_log(hipSetDevice(device), "hipSetDevice")) return nullptr;
   Block b;
   b.size = size;
   b.padded = pad256(size);
   const size_t total = kGuard + b.padded + kGuard;
   if (hipMalloc(&b.base, total) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;  // ATen reports it as out of memory
+    (void)hipGetLastError();  // clear the sticky OOM status; ATen reports it as out of memory
+    return nullptr;
   }
   uint8_t* user = b.base + kGuard;
-  (void)hipMemset(b.base, kCanary, kGuard);
-  (void)hipMemset(user, kPoison, size);
-  (void)hipMemset(user + size, kCanary, b.padded - size + kGuard);
-  (void)hipDeviceSynchronize();
+  const bool ok = ok_or_log(hipMemset(b.base, kCanary, kGuard), "hipMemset (front canary)") &&
+                  ok_or_log(hipMemset(user, kPoison, size), "hipMemset (poison)") &&
+                  ok_or_log(hipMemset(user + size, kCanary, b.padded - size + kGuard), "hipMemset (back canary)") &&
+                  ok_or_log(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  if (!ok) {
+    ok_or_log(hipFree(b.base), "hipFree");
+    return nullptr;
+  }
   b.op = t_op;
   std::lock_guard<std::mutex> lk(g_mu);
   blocks()[user] = std::move(b);
@@ -100,15 +112,16 @@ void g_free(void* ptr, size_t, int device, hipStream_t) {
     b = std::move(it->second);
     blocks().erase(it);
   }
-  (void)hipSetDevice(device);
-  (void)hipDeviceSynchronize();  // every kernel that may still write the block has finished
+  ok_or_log(hipSetDevice(device), "hipSetDevice");
+  // every kernel that may still write the block has finished
+  ok_or_log(hipDeviceSynchronize(), "hipDeviceSynchronize (free)");
   int64_t f = 0, k = 0;
   scan(b, &f, &k);
   if (f || k) {
     std::lock_guard<std::mutex> lk(g_mu);
     report(ptr, b, f, k, "when the block was freed (during " + t_op + ")");
   }
-  (void)hipFree(b.base);
+  ok_or_log(hipFree(b.base), "hipFree");
 }
 
 }  // namespace
@@ -146,7 +159,10 @@ void set_current_op(const char* op) { t_op = op ? op : "(outside any MapReduce o
 
 int check_all_blocks(const char* op) {
   if (!g_active) return 0;
-  (void)hipDeviceSynchronize();
+  auto must = [](hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("mrhip guard: ") + what + ": " + hipGetErrorString(e));
+  };
+  must(hipDeviceSynchronize(), "hipDeviceSynchronize");
   std::lock_guard<std::mutex> lk(g_mu);
   int bad = 0;
   for (auto& [user, b] : blocks()) {
@@ -156,10 +172,10 @@ int check_all_blocks(const char* op) {
     ++bad;
     report(user, b, f, k, std::string("at the end of ") + (op ? op : "a check"));
     // re-arm the canaries so one overrun is reported once
-    (void)hipMemset(b.base, kCanary, kGuard);
-    (void)hipMemset(b.base + kGuard + b.size, kCanary, b.padded - b.size + kGuard);
+    must(hipMemset(b.base, kCanary, kGuard), "hipMemset (re-arm)");
+    must(hipMemset(b.base + kGuard + b.size, kCanary, b.padded - b.size + kGuard), "hipMemset (re-arm)");
   }
-  (void)hipDeviceSynchronize();
+  must(hipDeviceSynchronize(), "hipDeviceSynchronize");
   return bad;
 }
 

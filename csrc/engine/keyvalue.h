@@ -56,6 +56,10 @@ class KeyValue {
     if (!grp_ && chunks_.empty() && nh_ == 0) grp_ = std::make_shared<GroupIndex>(dev_);
   }
   bool grouping() const { return grp_ != nullptr; }
+  // capacity hint for the grouped arenas (GroupIndex::reserve); no-op without grouping
+  void reserve_grouping(int64_t rows, int64_t key_bytes, int64_t value_bytes) {
+    if (grp_) grp_->reserve(rows, key_bytes, value_bytes);
+  }
   // the index of the KV the last finish() returned (null if not grouped)
   std::shared_ptr<GroupIndex> take_group() { return std::move(done_); }
   int64_t size() const {

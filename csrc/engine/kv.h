@@ -72,6 +72,9 @@ at::Tensor exclusive_scan(const at::Tensor& x);
 std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& keys,
                                                               const at::Tensor& vals, int begin_bit,
                                                               int end_bit, bool skip_trivial = true);
+// keys-only stable sort of int64 keys on bits [begin_bit, end_bit) (bits below
+// begin_bit ride along as payload)
+at::Tensor radix_sort_keys(const at::Tensor& keys, int begin_bit, int end_bit, bool skip_trivial = true);
 at::Tensor hash32_keys(const KV& kv, uint32_t seed);   // lookup3 hashlittle
 at::Tensor hash64_keys(const KV& kv);                  // lookup3 hashlittle2
 // rows gathered by u32 permutation
@@ -205,6 +208,8 @@ at::Tensor mask_indices(const at::Tensor& mask);
 at::Tensor repeat_index(const at::Tensor& counts);
 // segment boundaries of a sorted int64 key column: seg[nseg+1]
 at::Tensor segments_sorted(const at::Tensor& sorted_keys);
+// segment boundaries from u32 head flags (1 where a segment starts): seg[nseg+1]
+at::Tensor segments_from_flags(const at::Tensor& flags);
 
 // K-means map with in-mapper combining (kmeans.cpp): KV(int32 cluster*(D+1)+j, double)
 KV kmeans_map(const at::Tensor& points, const at::Tensor& centroids);

@@ -51,7 +51,7 @@ namespace {
 // bytes, and the bytes this rank sent/received in shuffles during the op.
 thread_local int g_op_depth = 0;
 void device_sync(const MapReduce* mr) {
-  if (mr->device().is_cuda()) (void)hipDeviceSynchronize();
+  if (mr->device().is_cuda()) guard::hip_check(hipDeviceSynchronize(), "trace_sync", mr->comm()->rank());
 }
 struct OpTrace {
   OpTrace(const char* name, MapReduce* mr) : mr_(mr), name_(name) {

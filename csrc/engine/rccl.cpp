@@ -240,6 +240,8 @@ Rccl::Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>
   for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
 }
 
+// teardown cannot throw: statuses here are deliberately ignored (an aborted
+// communicator's stream may report the abort)
 Rccl::~Rccl() {
   if (stream_) {
     if (!aborted_) (void)hipStreamSynchronize(stream_);

@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <exception>
 #include <stdexcept>
 
 #include "../kernels/hashfn.h"
@@ -444,7 +445,7 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
     if (R > 1) post(1);
     for (int k = 0; k < R; ++k) {
       RoundLayout& L = lay[k % 2];
-      if (L.landed) (void)hipStreamWaitEvent(s, L.landed, 0);
+      if (L.landed) guard::hip_check(hipStreamWaitEvent(s, L.landed, 0), "round_wait", me);
       if (L.n > 0) {
         KV r;
         r.n = L.n;
@@ -477,8 +478,16 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
     }
     for (auto& t : stage) t = at::empty({std::max<int64_t>(stage_bytes, 1)}, opt(dev, at::kByte));
     copy_stream = c10::hip::getStreamFromPool(false, dev.index());
-    for (auto& e : drained) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    for (auto& e : drained) guard::hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "drain_event", me);
   }
+  // an exception out of the rounds (a failed drain, a peer failure) must not
+  // unwind while drain copies still write into the output being freed
+  struct DrainFence {
+    c10::optional<c10::hip::HIPStream>* cs;
+    ~DrainFence() {
+      if (std::uncaught_exceptions() > 0 && cs->has_value()) (void)hipStreamSynchronize((*cs)->stream());
+    }
+  } drain_fence{&copy_stream};
   for (int k = 0; k < R && !round_sink; ++k) {
     guard::fault_point("exchange_round", me);
     std::vector<Xfer> xs, xr;
@@ -522,28 +531,29 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
       continue;
     }
     // staging buffer k%2 is free once the drain of round k-2 finished
-    if (k >= 2) (void)hipStreamWaitEvent(cs_, drained[k % 2], 0);
+    if (k >= 2) guard::hip_check(hipStreamWaitEvent(cs_, drained[k % 2], 0), "drain_wait", me);
     hipEvent_t landed = nullptr;
     if (comm.uses_rccl()) {
       landed = comm.rccl()->sendrecv_async(xs, xr, cs_);
     } else {
       comm.sendrecv(xs, xr);
-      (void)hipEventCreateWithFlags(&landed, hipEventDisableTiming);
-      (void)hipEventRecord(landed, cs_);
+      guard::hip_check(hipEventCreateWithFlags(&landed, hipEventDisableTiming), "landed_event", me);
+      guard::hip_check(hipEventRecord(landed, cs_), "landed_event", me);
     }
     const hipStream_t cp = copy_stream->stream();
-    (void)hipStreamWaitEvent(cp, landed, 0);
+    guard::hip_check(hipStreamWaitEvent(cp, landed, 0), "drain_wait", me);
     for (const Drain& d : drains)
       if (d.bytes)
-        (void)hipMemcpyAsync(d.dst, P0<uint8_t>(stage[k % 2]) + d.stage_off, (size_t)d.bytes, hipMemcpyDeviceToHost,
-                             cp);
-    (void)hipEventRecord(drained[k % 2], cp);
-    if (!comm.uses_rccl()) (void)hipEventDestroy(landed);
+        guard::hip_check(hipMemcpyAsync(d.dst, P0<uint8_t>(stage[k % 2]) + d.stage_off, (size_t)d.bytes,
+                                        hipMemcpyDeviceToHost, cp),
+                         "drain_copy", me);
+    guard::hip_check(hipEventRecord(drained[k % 2], cp), "drain_event", me);
+    if (!comm.uses_rccl()) guard::hip_check(hipEventDestroy(landed), "landed_event", me);
   }
   if (host_sink) {
-    for (int k = std::max(0, R - 2); k < R; ++k) (void)hipStreamWaitEvent(cs_, drained[k % 2], 0);
+    for (int k = std::max(0, R - 2); k < R; ++k) guard::hip_check(hipStreamWaitEvent(cs_, drained[k % 2], 0), "drain_wait", me);
     comm.host_wait();  // pinned host output complete before the host reads it
-    for (auto& e : drained) (void)hipEventDestroy(e);
+    for (auto& e : drained) guard::hip_check(hipEventDestroy(e), "drain_event", me);
   }
 
   // ---- 7. offsets of variable columns

@@ -118,7 +118,7 @@ int64_t tri_hub_size(int64_t nvert) {
   if (env < 0 && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
     if ((size_t)want * (size_t)want / 8 > free_b / 4) {  // blocks cached by the allocator count as free
       c10::hip::HIPCachingAllocator::emptyCache();
-      (void)hipMemGetInfo(&free_b, &total_b);
+      if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;  // then the hub budget stays as set above
     }
     while (want > 64 && (size_t)want * (size_t)want / 8 > free_b / 4) want /= 2;
   }

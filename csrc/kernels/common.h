@@ -41,6 +41,13 @@ inline void check_launch(const char* file, int line) {
     throw KernelError(buf);
   }
 }
+// a runtime call of a launcher (memset, copy, sync): a failure is a KernelError
+inline void hip_call(hipError_t e, const char* what, const char* file, int line) {
+  if (e == hipSuccess) return;
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), "mrhip: %s failed: %s at %s:%d", what, hipGetErrorString(e), file, line);
+  throw KernelError(buf);
+}
 // host-side precondition of a launcher (shapes, limits): std::invalid_argument
 inline void check_arg(bool ok, const char* what) {
   if (!ok) throw std::invalid_argument(std::string("mrhip: ") + what);
@@ -49,6 +56,7 @@ inline void check_arg(bool ok, const char* what) {
 }  // namespace mrh
 
 #define MRH_CHECK_LAUNCH() ::mrh::k::check_launch(__FILE__, __LINE__)
+#define MRH_HIP(call) ::mrh::k::hip_call((call), #call, __FILE__, __LINE__)
 
 namespace mrh {
 namespace dev {

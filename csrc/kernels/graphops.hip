@@ -38,6 +38,111 @@ struct ContribGetC {
   __device__ __forceinline__ float operator()(int64_t i) const { return c[__builtin_nontemporal_load(src + i)]; }
 };
 
+// ---------------------------------------------------------------- plan build
+// The PageRank plan of one rank built without a group-by or a payload array:
+// the edges are sorted twice as packed u64 keys (by source: out-degrees are
+// run lengths; then by destination group with the new source id in the low
+// word), the degree relabel sorts the nlocal vertices.
+
+// packed (local source << 32 | destination) of every edge: sorting it on
+// the source bits makes the out-degrees segment lengths (random-address
+// global atomics run at the memory side, ~17x below their coalesced rate:
+// a degree histogram by atomics cost 98 ms on RMAT-26, this sort ~20)
+__global__ __launch_bounds__(NT) void k_pr_pack_src(const int64_t* __restrict__ e, int64_t n, int P,
+                                                    uint64_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
+    const int64_t u = __builtin_nontemporal_load(e + 2 * i), v = __builtin_nontemporal_load(e + 2 * i + 1);
+    out[i] = ((uint64_t)(P == 1 ? u : u / P) << 32) | (uint32_t)v;
+  }
+}
+
+// head flag of every run of equal high words in a sorted packed array
+__global__ __launch_bounds__(NT) void k_pr_heads(const uint64_t* __restrict__ s, int64_t n,
+                                                 uint32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i < n) flags[i] = (i == 0 || (s[i - 1] >> 32) != (s[i] >> 32)) ? 1u : 0u;
+}
+
+// deg[source of run g] = length of run g (deg zeroed before)
+__global__ __launch_bounds__(NT) void k_pr_run_degree(const uint64_t* __restrict__ s, const int64_t* __restrict__ seg,
+                                                      int64_t nrun, uint32_t* __restrict__ deg) {
+  const int64_t g = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (g < nrun) deg[s[seg[g]] >> 32] = (uint32_t)(seg[g + 1] - seg[g]);
+}
+
+// vertex sort key: descending degree, ties by id (stable sort of ~deg)
+__global__ __launch_bounds__(NT) void k_pr_degkey(const uint32_t* __restrict__ deg, int64_t n,
+                                                  uint64_t* __restrict__ key, uint32_t* __restrict__ iota) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i < n) {
+    key[i] = (uint64_t)(0xFFFFFFFFu - deg[i]);
+    iota[i] = (uint32_t)i;
+  }
+}
+
+// new id i of old vertex order[i]: nid[order[i]] = i; the per-new-id
+// dangling flag and 1/outdeg; the dangling count (one atomic per wave)
+__global__ __launch_bounds__(NT) void k_pr_relabel(const uint32_t* __restrict__ order, const uint32_t* __restrict__ deg,
+                                                   int64_t n, int32_t* __restrict__ nid, int64_t* __restrict__ order64,
+                                                   uint8_t* __restrict__ dangling, float* __restrict__ invdeg,
+                                                   unsigned long long* __restrict__ ndangling) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  bool dg = false;
+  if (i < n) {
+    const uint32_t o = order[i];
+    nid[o] = (int32_t)i;
+    order64[i] = o;
+    const uint32_t d = deg[o];
+    dg = d == 0;
+    dangling[i] = dg ? 1 : 0;
+    invdeg[i] = dg ? 0.f : (float)(1.0 / (double)d);
+  }
+  const uint64_t b = __ballot(dg);
+  if (dev::lane_id() == 0 && b) atomicAdd(ndangling, (unsigned long long)__popcll(b));
+}
+
+// the gather's sort key of every source-sorted edge (u << 32 | v): hi =
+// destination group (one rank, no exchange: v; otherwise (v % P) * nlmax +
+// v / P, owner-major), lo = new id of u (u is monotone here: the nid reads
+// are a sequential walk)
+__global__ __launch_bounds__(NT) void k_pr_pack(const uint64_t* __restrict__ su, int64_t n, int P, int64_t nlmax,
+                                                int local, const int32_t* __restrict__ nid,
+                                                uint64_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
+    const uint64_t x = __builtin_nontemporal_load(su + i);
+    const int64_t v = (int64_t)(uint32_t)x;
+    const uint64_t hi = local ? (uint64_t)v : (uint64_t)((v % P) * nlmax + v / P);
+    out[i] = (hi << 32) | (uint32_t)nid[x >> 32];
+  }
+}
+
+// sorted packed keys -> the int32 source stream of the gather and the u32
+// head flag of every destination group
+__global__ __launch_bounds__(NT) void k_pr_unpack(const uint64_t* __restrict__ s, int64_t n, int32_t* __restrict__ src,
+                                                  uint32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = s[i];
+  src[i] = (int32_t)(uint32_t)k;
+  flags[i] = (i == 0 || (s[i - 1] >> 32) != (k >> 32)) ? 1u : 0u;
+}
+
+// per destination group: its hi word (the group's destination)
+__global__ __launch_bounds__(NT) void k_pr_group_hi(const uint64_t* __restrict__ s, const int64_t* __restrict__ seg,
+                                                    int64_t ngrp, int64_t* __restrict__ hi) {
+  const int64_t g = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (g < ngrp) hi[g] = (int64_t)(s[seg[g]] >> 32);
+}
+
+// target row of group g: nid[hi] (hi an old id), or hi itself (nid == null)
+__global__ __launch_bounds__(NT) void k_pr_group_vid(const int64_t* __restrict__ hi, int64_t ngrp,
+                                                     const int32_t* __restrict__ nid, int32_t* __restrict__ vid) {
+  const int64_t g = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (g < ngrp) vid[g] = nid ? nid[hi[g]] : (int32_t)hi[g];
+}
+
 struct PermGet {
   const int32_t* perm;
   const float* v;
@@ -231,7 +336,7 @@ size_t ws_scratch_bytes(int64_t nval) {
 
 void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64_t* wbase, hipStream_t s) {
   const int64_t nw = dev::ws_nwave(nval);
-  hipMemsetAsync(H, 0, sizeof(uint32_t) * dev::ws_head_words(nval), s);
+  MRH_HIP(hipMemsetAsync(H, 0, sizeof(uint32_t) * dev::ws_head_words(nval), s));
   if (nseg > 0)
     hipLaunchKernelGGL(dev::k_ws_heads, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, seg, nseg, H);
   if (nw > 0)
@@ -299,6 +404,64 @@ void pr_combine(const int64_t* seg, int64_t ngrp, int64_t nrecv, const int32_t* 
 void scatter_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_scatter_f32, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, v, idx, n, out);
+  MRH_CHECK_LAUNCH();
+}
+
+static unsigned pr_grid(int64_t n) {
+  const int64_t b = (n + NT - 1) / NT;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+static unsigned pr_grid_stride(int64_t n) {
+  const int64_t b = (n + NT - 1) / NT;
+  return (unsigned)(b < 1 ? 1 : (b > 65536 ? 65536 : b));
+}
+
+void pr_pack_src(const int64_t* e, int64_t n, int P, uint64_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_pack_src, dim3(pr_grid_stride(n)), dim3(NT), 0, s, e, n, P, out);
+  MRH_CHECK_LAUNCH();
+}
+void pr_heads(const uint64_t* sorted, int64_t n, uint32_t* flags, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_heads, dim3(pr_grid(n)), dim3(NT), 0, s, sorted, n, flags);
+  MRH_CHECK_LAUNCH();
+}
+void pr_run_degree(const uint64_t* sorted, const int64_t* seg, int64_t nrun, uint32_t* deg, hipStream_t s) {
+  if (nrun <= 0) return;
+  hipLaunchKernelGGL(k_pr_run_degree, dim3(pr_grid(nrun)), dim3(NT), 0, s, sorted, seg, nrun, deg);
+  MRH_CHECK_LAUNCH();
+}
+void pr_degkey(const uint32_t* deg, int64_t n, uint64_t* key, uint32_t* iota, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_degkey, dim3(pr_grid(n)), dim3(NT), 0, s, deg, n, key, iota);
+  MRH_CHECK_LAUNCH();
+}
+void pr_relabel(const uint32_t* order, const uint32_t* deg, int64_t n, int32_t* nid, int64_t* order64,
+                uint8_t* dangling, float* invdeg, unsigned long long* ndangling, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_relabel, dim3(pr_grid(n)), dim3(NT), 0, s, order, deg, n, nid, order64, dangling, invdeg,
+                     ndangling);
+  MRH_CHECK_LAUNCH();
+}
+void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, uint64_t* out,
+             hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, nlmax, local ? 1 : 0, nid, out);
+  MRH_CHECK_LAUNCH();
+}
+void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_unpack, dim3(pr_grid(n)), dim3(NT), 0, s, sorted, n, src, flags);
+  MRH_CHECK_LAUNCH();
+}
+void pr_group_hi(const uint64_t* sorted, const int64_t* seg, int64_t ngrp, int64_t* hi, hipStream_t s) {
+  if (ngrp <= 0) return;
+  hipLaunchKernelGGL(k_pr_group_hi, dim3(pr_grid(ngrp)), dim3(NT), 0, s, sorted, seg, ngrp, hi);
+  MRH_CHECK_LAUNCH();
+}
+void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int32_t* vid, hipStream_t s) {
+  if (ngrp <= 0) return;
+  hipLaunchKernelGGL(k_pr_group_vid, dim3(pr_grid(ngrp)), dim3(NT), 0, s, hi, ngrp, nid, vid);
   MRH_CHECK_LAUNCH();
 }
 

@@ -94,7 +94,7 @@ void hash64_var(const uint8_t* kdata, const int64_t* koff, int64_t n, uint64_t* 
   MRH_CHECK_LAUNCH();
 }
 void partition_dest(const uint32_t* h, int64_t n, int P, int32_t* dest, int64_t* counts, hipStream_t s) {
-  hipMemsetAsync(counts, 0, sizeof(int64_t) * P, s);
+  MRH_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * P, s));
   if (n <= 0) return;
   check_arg(P <= 1024, "partition: more than 1024 ranks unsupported");
   unsigned g = nblk(n);

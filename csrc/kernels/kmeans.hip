@@ -590,8 +590,8 @@ void launch(const float* pts, int64_t n, const float* cen, int K, double* acc, h
     if (variant == 0 && K <= 32 * TKG && tr_lds(D, K) <= 64 * 1024) {
       static const int ncu = [] {
         int dev = 0, c = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        MRH_HIP(hipGetDevice(&dev));
+        MRH_HIP(hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev));
         return std::max(1, c);
       }();
       int64_t nb = (n + TTILE - 1) / TTILE;

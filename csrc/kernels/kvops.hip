@@ -269,7 +269,7 @@ void verify_groups_fixed(const uint8_t* kdata, int kw, const uint32_t* perm, con
 }
 void dest_byte_counts(const int32_t* dest, const int64_t* off, int64_t n, int P, int64_t* bytes,
                       hipStream_t s) {
-  hipMemsetAsync(bytes, 0, sizeof(int64_t) * P, s);
+  MRH_HIP(hipMemsetAsync(bytes, 0, sizeof(int64_t) * P, s));
   if (n <= 0) return;
   unsigned g = nblk(n);
   if (g > 2048) g = 2048;

@@ -1,4 +1,5 @@
-// Stable LSD radix sort of (uint64 key, uint32 value) pairs for CDNA4:
+// Stable LSD radix sort of (uint64 key, uint32 value) pairs — or of uint64 keys
+// alone (vals_in == nullptr; payload bits packed below the sorted range) — for CDNA4:
 // one-sweep passes with decoupled look-back (Adinets & Merrill, "Onesweep",
 // 2022), re-built for 64-lane wavefronts.
 //
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
     int64_t idx = wbase + (int64_t)j * MRH_WAVE + lane;
     bool valid = idx < n;
     kk[j] = valid ? kin[idx] : 0ull;
-    vv[j] = valid ? vin[idx] : 0u;
+    vv[j] = (valid && vin) ? vin[idx] : 0u;  // vin == nullptr: keys-only sort
   }
 
   // wave multi-split: rank of each pair among equal digits of its wave
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
       uint32_t d = (uint32_t)(kk[j] >> shift) & 255u;
       uint32_t pos = bdig[d] + wcnt[w][d] + lr[j];
       skeys[pos] = kk[j];
-      svals[pos] = vv[j];
+      if (vin) svals[pos] = vv[j];
     }
   }
   __syncthreads();
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
     uint32_t d = (uint32_t)(key >> shift) & 255u;
     uint64_t g = gofs[d] + (uint64_t)i - bdig[d];
     kout[g] = key;
-    vout[g] = svals[i];
+    if (vout) vout[g] = svals[i];
   }
 }
 
@@ -250,8 +251,8 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
 
   // zero the look-back words, the histogram and the 8 tickets in one memset
   // (they are contiguous apart from dbase, which k_digit_base overwrites)
-  (void)hipMemsetAsync(status, 0, st_bytes, s);
-  (void)hipMemsetAsync(gcounts, 0, align256(8 * RX_BINS * 4) + 8 * sizeof(unsigned int), s);
+  MRH_HIP(hipMemsetAsync(status, 0, st_bytes, s));
+  MRH_HIP(hipMemsetAsync(gcounts, 0, align256(8 * RX_BINS * 4) + 8 * sizeof(unsigned int), s));
   int ghist_blocks = (int)((n + RX_NT - 1) / RX_NT);
   if (ghist_blocks > 2048) ghist_blocks = 2048;
   const int p0 = begin_bit / 8, p1 = std::min(8, (end_bit + 7) / 8);
@@ -260,8 +261,8 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
   std::vector<int> passes;
   if (skip_trivial) {  // which digit positions actually vary? (one host sync)
     std::vector<uint32_t> hc(8 * RX_BINS);
-    (void)hipMemcpyAsync(hc.data(), gcounts, 8 * RX_BINS * 4, hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
+    MRH_HIP(hipMemcpyAsync(hc.data(), gcounts, 8 * RX_BINS * 4, hipMemcpyDeviceToHost, s));
+    MRH_HIP(hipStreamSynchronize(s));
     for (int p = begin_bit / 8; p * 8 < end_bit && p < 8; ++p) {
       bool trivial = false;
       for (int b = 0; b < RX_BINS; ++b)
@@ -277,8 +278,8 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
   const int np = (int)passes.size();
   if (passes_run) *passes_run = np;
   if (np == 0) {
-    (void)hipMemcpyAsync(keys_out, keys_in, n * 8, hipMemcpyDeviceToDevice, s);
-    (void)hipMemcpyAsync(vals_out, vals_in, n * 4, hipMemcpyDeviceToDevice, s);
+    MRH_HIP(hipMemcpyAsync(keys_out, keys_in, n * 8, hipMemcpyDeviceToDevice, s));
+    if (vals_in) MRH_HIP(hipMemcpyAsync(vals_out, vals_in, n * 4, hipMemcpyDeviceToDevice, s));
     return;
   }
   hipLaunchKernelGGL(k_digit_base, dim3(8), dim3(RX_BINS), 0, s, (const uint32_t*)gcounts, dbase);
@@ -289,7 +290,7 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
     // ping-pong so that the final pass lands in *_out
     bool to_out = ((np - 1 - q) % 2) == 0;
     uint64_t* ko = to_out ? keys_out : keys_alt;
-    uint32_t* vo = to_out ? vals_out : vals_alt;
+    uint32_t* vo = vals_in ? (to_out ? vals_out : vals_alt) : nullptr;
     const int p = passes[q];
     if (items == 16)
       hipLaunchKernelGGL(k_onesweep<16>, dim3((unsigned)ntile), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, p * 8,

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(SCAN_NT) void k_tile_scan(const Tin* __restrict__ i
 template <typename Tin, typename Tacc>
 void scan_impl(const Tin* in, Tacc* out, int64_t n, char* temp, hipStream_t s) {
   if (n <= 0) {
-    hipMemsetAsync(out, 0, sizeof(Tacc), s);
+    MRH_HIP(hipMemsetAsync(out, 0, sizeof(Tacc), s));
     return;
   }
   int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;

@@ -98,14 +98,14 @@ void lookup_sorted(const int64_t* keys, int64_t n, const int64_t* q, int64_t m, 
 }
 
 void seg_marks(const int64_t* seg, int64_t nseg, int64_t nval, int64_t* marks, hipStream_t s) {
-  (void)hipMemsetAsync(marks, 0, sizeof(int64_t) * std::max<int64_t>(nval, 1), s);
+  MRH_HIP(hipMemsetAsync(marks, 0, sizeof(int64_t) * std::max<int64_t>(nval, 1), s));
   if (nseg <= 1 || nval <= 0) return;
   hipLaunchKernelGGL(k_seg_marks, dim3(blocks(nseg)), dim3(NT), 0, s, seg, nseg, nval, marks);
   MRH_CHECK_LAUNCH();
 }
 
 void histogram(const int64_t* idx, int64_t n, int64_t K, int64_t* counts, hipStream_t s) {
-  (void)hipMemsetAsync(counts, 0, sizeof(int64_t) * std::max<int64_t>(K, 1), s);
+  MRH_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * std::max<int64_t>(K, 1), s));
   if (n <= 0) return;
   hipLaunchKernelGGL(k_histogram, dim3(blocks(n)), dim3(NT), 0, s, idx, n, K, counts);
   MRH_CHECK_LAUNCH();

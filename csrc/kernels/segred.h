@@ -255,7 +255,7 @@ inline void segred_launch(G get, const int64_t* seg, int64_t nseg, int64_t nval,
                           T* carry_val, hipStream_t s) {
   if (nseg <= 0 || nval <= 0) return;
   int64_t nb = (nval + SR_TILE - 1) / SR_TILE;
-  hipMemsetAsync(carry_seg, 0xff, sizeof(int64_t) * 2 * nb, s);  // -1
+  MRH_HIP(hipMemsetAsync(carry_seg, 0xff, sizeof(int64_t) * 2 * nb, s));  // -1
   hipLaunchKernelGGL((k_segred_tiles<T, OP, G>), dim3((unsigned)nb), dim3(SR_NT), 0, s, get, seg, nseg, nval, out,
                      carry_seg, carry_val);
   MRH_CHECK_LAUNCH();
@@ -264,7 +264,7 @@ inline void segred_launch(G get, const int64_t* seg, int64_t nseg, int64_t nval,
     const int64_t nw1 = (nc + 63) / 64;
     int64_t* cs2 = carry_seg + nc;
     T* cv2 = carry_val + nc;
-    hipMemsetAsync(cs2, 0xff, sizeof(int64_t) * 2 * nw1, s);
+    MRH_HIP(hipMemsetAsync(cs2, 0xff, sizeof(int64_t) * 2 * nw1, s));
     hipLaunchKernelGGL((k_carry_fold<T, OP>), dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, carry_seg,
                        carry_val, nc, out, cs2, cv2);
     MRH_CHECK_LAUNCH();

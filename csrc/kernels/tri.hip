@@ -538,7 +538,7 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
   check_arg(K > 0 && K % 64 == 0 && K <= HUB_NT * 64 * 32, "tri_hub_count: K must be a multiple of 64, <= 524288");
   const int64_t r0 = std::max<int64_t>(u0 - hb, 0), r1 = std::min<int64_t>(u1 - hb, K);
   // the bitmaps are always built: the hash kernels' hub probes read them too
-  (void)hipMemsetAsync(H, 0, (size_t)K * (K / 64) * 8, s);
+  MRH_HIP(hipMemsetAsync(H, 0, (size_t)K * (K / 64) * 8, s));
   hipLaunchKernelGGL(k_tri_hub_build, dim3((unsigned)std::min<int64_t>((K + HASH_NW - 1) / HASH_NW, 16384)), dim3(NT),
                      0, s, rowptr, col, hb, K, (unsigned long long*)H);
   MRH_CHECK_LAUNCH();
@@ -561,7 +561,7 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
 
 void tri_core_build(const int64_t* rowptr, const uint32_t* col, int64_t cb, int64_t T, int8_t* A, hipStream_t s) {
   if (T <= 0) return;
-  (void)hipMemsetAsync(A, 0, (size_t)T * (size_t)T, s);
+  MRH_HIP(hipMemsetAsync(A, 0, (size_t)T * (size_t)T, s));
   hipLaunchKernelGGL(k_tri_core_build, dim3((unsigned)std::min<int64_t>((T + HASH_NW - 1) / HASH_NW, 16384)), dim3(NT),
                      0, s, rowptr, col, cb, T, A);
   MRH_CHECK_LAUNCH();

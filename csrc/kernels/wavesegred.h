@@ -172,7 +172,7 @@ inline void ws_gather_reduce(const uint32_t* H, const int64_t* wbase, int64_t nv
                              int64_t* carry2_seg = nullptr, T* carry2_val = nullptr) {
   if (nval <= 0) return;
   const int64_t nw = ws_nwave(nval);
-  hipMemsetAsync(carry_seg, 0xff, sizeof(int64_t) * 2 * nw, s);
+  MRH_HIP(hipMemsetAsync(carry_seg, 0xff, sizeof(int64_t) * 2 * nw, s));
   const int64_t nb = (nw + (WS_NT / 64) - 1) / (WS_NT / 64);
   hipLaunchKernelGGL((k_ws_gather_reduce<T, OP>), dim3((unsigned)nb), dim3(WS_NT), 0, s, H, wbase, nval, nw, src, x, w,
                      out, carry_seg, carry_val);
@@ -180,7 +180,7 @@ inline void ws_gather_reduce(const uint32_t* H, const int64_t* wbase, int64_t nv
   const int64_t nc = 2 * nw;
   if (carry2_seg && nc > 4096) {  // two-level fold (k_carry_fold): long runs in parallel
     const int64_t nw1 = (nc + 63) / 64;
-    hipMemsetAsync(carry2_seg, 0xff, sizeof(int64_t) * 2 * nw1, s);
+    MRH_HIP(hipMemsetAsync(carry2_seg, 0xff, sizeof(int64_t) * 2 * nw1, s));
     hipLaunchKernelGGL((k_carry_fold<T, OP>), dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, carry_seg,
                        carry_val, nc, out, carry2_seg, carry2_val);
     MRH_CHECK_LAUNCH();

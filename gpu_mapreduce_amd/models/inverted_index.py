@@ -58,6 +58,7 @@ class InvertedIndex:
         self.own_output = own_output
         self._gen = None
         self._mapped = False
+        self._reserved = False
         # doc ids are global (rank-major) so a value means the same file name on
         # every rank after the shuffle; the reference ships the name string itself
         all_names = mr.comm.allgather_object([n for n, _ in files])
@@ -70,8 +71,8 @@ class InvertedIndex:
         dev = mr.device
         self.dev = dev
         self.is_cuda = dev.startswith("cuda")
-        self.names_dev = self.names.to(dev)
-        self.name_off_dev = self.name_off.to(dev)
+        self.names_dev = pools.device_constant(dev, self.names)
+        self.name_off_dev = pools.device_constant(dev, self.name_off)
         maxlen = max((t.numel() for _, t in files), default=0)
         # two persistent staging buffers (double-buffered H2D); the PAD bytes
         # past each file are read by the 16-byte scan windows but never matched
@@ -90,6 +91,13 @@ class InvertedIndex:
         if self.pipelined and mr.nprocs > 1:
             part, _ = C.aggregate(part, mr.comm.native, chunk_bytes=mr.chunk_bytes)
         kv.add_kv(part)
+        if self.pipelined and not self._reserved and part.n > 0:
+            # size the grouped arenas once for the whole job from the first
+            # part (+25 %): no x1.5 regrow copies or table rehash under the H2D
+            self._reserved = True
+            f = 1.25 * max(1, len(self.files), self.max_files)
+            kv.reserve_grouping(int(part.n * f) + 1024, int(part.kdata.numel() * f) + 4096,
+                                int(part.vdata.numel() * f) + 4096)
 
     def _map(self, itask, kv):
         if self._mapped:

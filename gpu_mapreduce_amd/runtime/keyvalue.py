@@ -98,6 +98,11 @@ class KeyValue:
         the device would otherwise idle between batches."""
         self._h.enable_grouping()
 
+    def reserve_grouping(self, rows: int, key_bytes: int, value_bytes: int):
+        """Capacity hint for the grouped arenas: sized once for the whole map
+        (no regrow copies or hash-table rehash while the input streams)."""
+        self._h.reserve_grouping(int(rows), int(key_bytes), int(value_bytes))
+
     @property
     def grouping(self) -> bool:
         return self._h.grouping

@@ -13,6 +13,7 @@ _host = {}
 _streams = {}
 _events = {}
 _ring = {}
+_const = {}
 
 
 def device_buffer(device: str, nbytes: int, slot: int = 0) -> torch.Tensor:
@@ -22,6 +23,22 @@ def device_buffer(device: str, nbytes: int, slot: int = 0) -> torch.Tensor:
         b = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
         _dev[key] = b
     return b
+
+
+def device_constant(device: str, t: torch.Tensor) -> torch.Tensor:
+    """A small host tensor uploaded once per (device, content) and reused:
+    job metadata that repeats between jobs (InvertedIndex's file-name table)
+    must not cost a pageable H2D copy per job — that copy waits for the
+    device queue, i.e. for the previous job's tail, before the next job can
+    issue its first input copy."""
+    key = (str(device), t.dtype, tuple(t.shape), t.numpy().tobytes())
+    d = _const.get(key)
+    if d is None:
+        if len(_const) > 64:
+            _const.clear()
+        d = t.to(device)
+        _const[key] = d
+    return d
 
 
 def pinned_buffer(nbytes: int, slot: int = 0) -> torch.Tensor:
@@ -72,3 +89,4 @@ def clear():
     _streams.clear()
     _events.clear()
     _ring.clear()
+    _const.clear()

@@ -229,3 +229,63 @@ def test_rank_failure_inside_shuffle_ends_job_fast(tmp_path, kind):
         assert ("stopped responding" in msg) if kind == "abort" else ("rank 1 failed" in msg), msg[-2000:]
     if kind == "abort":
         assert codes[1] == 3 and "rank 1 aborts at exchange_round" in res[1][1]
+
+
+DRAIN_SCRIPT = """
+import os, sys, time, torch
+sys.path.insert(0, os.environ["PYTHONPATH"])
+from gpu_mapreduce_amd.parallel import comm as pcomm
+from gpu_mapreduce_amd._ext import C
+comm = pcomm.init()
+assert comm.native.transport.startswith("pg"), comm.native.transport   # two ranks share the GPU
+n = 200000
+keys = torch.arange(n, dtype=torch.int64) * 2654435761 + comm.rank
+kv = C.make_kv(keys.view(torch.uint8), None, keys.view(torch.uint8), None, n, "cuda:0")
+t0 = time.time()
+try:
+    out, st = C.aggregate(kv, comm.native, chunk_bytes=1 << 16, host_sink=True)
+    torch.cuda.synchronize()
+    print("NO-ERROR", flush=True)
+except Exception as e:
+    print(f"RAISED after {time.time() - t0:.1f}s: {e}", flush=True)
+    os._exit(1)
+"""
+
+
+@pytest.mark.gpu
+def test_forced_drain_failure_ends_every_rank_fast(tmp_path):
+    """MRH_FAULT=hip:drain_copy:0 fails the first device->host drain copy of a
+    host-sink (out-of-core) aggregate on rank 0: the checked HIP call raises,
+    the job is poisoned, and BOTH ranks end with an error within seconds —
+    no rank reports success over garbage output, none hangs."""
+    port = _port()
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(ENV0, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT, MRH_NUMA_BIND="0",
+                   MRH_COMM_TIMEOUT="60", MRH_FAULT="hip:drain_copy:0")
+        procs.append(subprocess.Popen([sys.executable, "-c", DRAIN_SCRIPT], cwd=tmp_path, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    try:
+        res = [p.communicate(timeout=150) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.time() - t0
+    assert all(p.returncode != 0 for p in procs), res
+    assert "HIP error at drain_copy on rank 0" in res[0][0] + res[0][1], res[0]
+    assert "NO-ERROR" not in res[1][0], res[1]
+    assert elapsed < 60, f"failure took {elapsed:.0f} s to surface"
+
+
+def test_hip_fault_kind_is_accepted():
+    """kind 'hip' parses (it fires only at checked HIP call sites of device paths)"""
+    code = """
+    import gpu_mapreduce_amd as g
+    mr = g.MapReduce(g.Comm(device="cpu"))
+    print(mr.map(1, lambda i, kv: kv.add(b"k", b"v")))
+    """
+    r = _py(code, {"MRH_FAULT": "hip:drain_copy:0"})
+    assert r.returncode == 0 and r.stdout.strip() == "1", r.stderr
