@@ -1,0 +1,430 @@
+// Spool (spool.h): HBM -> pinned host -> memory-mapped disk file.
+#include "spool.h"
+
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <filesystem>
+#include <stdexcept>
+
+namespace mrh {
+
+namespace {
+
+at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
+[[noreturn]] void fail(const std::string& m) { throw std::runtime_error("mrhip spool: " + m); }
+
+std::atomic<int64_t> g_files_live{0};
+std::atomic<int64_t> g_counter{0};
+
+SpoolStats& totals() {
+  static SpoolStats s;
+  return s;
+}
+
+// one memory-mapped spool file; unmapped and deleted with the last view
+struct Mapping {
+  void* p = nullptr;
+  size_t len = 0;
+  std::string path;
+  ~Mapping() {
+    if (p && len) munmap(p, len);
+    if (!path.empty()) {
+      ::unlink(path.c_str());
+      g_files_live--;
+    }
+  }
+};
+
+constexpr size_t kAlign = 4096;
+size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// host int64 view of an offset column (device columns are copied)
+at::Tensor host_i64(const at::Tensor& t) { return t.to(at::kCPU).contiguous(); }
+
+// bytes used by a column of a part: fixed width -> n * w; variable -> off[n]
+int64_t col_bytes(const at::Tensor& off, int w, int64_t n, at::Tensor* hoff) {
+  if (w >= 0) return n * w;
+  *hoff = host_i64(off);
+  return hoff->data_ptr<int64_t>()[n] - hoff->data_ptr<int64_t>()[0];
+}
+
+struct Layout {
+  std::vector<size_t> off;  // byte offset of each column in the file
+  size_t total = 0;
+  size_t add(size_t bytes) {
+    off.push_back(total);
+    total = align_up(total + std::max<size_t>(bytes, 1));
+    return off.back();
+  }
+};
+
+std::shared_ptr<Mapping> create_mapping(const std::string& path, size_t len) {
+  const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
+  if (fd < 0) fail("cannot create " + path + ": " + std::strerror(errno));
+  auto m = std::make_shared<Mapping>();
+  m->path = path;
+  g_files_live++;
+  if (::ftruncate(fd, (off_t)len) != 0) {
+    const std::string e = std::strerror(errno);
+    ::close(fd);
+    fail("cannot size " + path + " to " + std::to_string(len) + " bytes: " + e);
+  }
+  void* p = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  ::close(fd);
+  if (p == MAP_FAILED) fail("cannot map " + path + ": " + std::strerror(errno));
+  m->p = p;
+  m->len = len;
+  return m;
+}
+
+// a host tensor viewing [off, off + numel * elem) of the mapping
+at::Tensor view(const std::shared_ptr<Mapping>& m, size_t off, int64_t numel, at::ScalarType dt) {
+  return at::from_blob(static_cast<char*>(m->p) + off, {numel}, [m](void*) {}, opt(at::kCPU, dt));
+}
+
+// concatenated byte column: parts' data [first .. first+bytes) packed
+void put_bytes(const std::shared_ptr<Mapping>& m, size_t off, const std::vector<at::Tensor>& data,
+               const std::vector<int64_t>& first, const std::vector<int64_t>& bytes) {
+  size_t at_ = off;
+  for (size_t i = 0; i < data.size(); ++i) {
+    if (bytes[i] <= 0) continue;
+    at::Tensor dst = view(m, at_, bytes[i], at::kByte);
+    dst.copy_(data[i].narrow(0, first[i], bytes[i]));
+    at_ += (size_t)bytes[i];
+  }
+}
+
+// concatenated offset column: part i's offsets rebased to the bytes before it
+void put_offsets(const std::shared_ptr<Mapping>& m, size_t off, const std::vector<at::Tensor>& hoff,
+                 const std::vector<int64_t>& ns) {
+  int64_t* d = reinterpret_cast<int64_t*>(static_cast<char*>(m->p) + off);
+  int64_t row = 0, base = 0;
+  d[0] = 0;
+  for (size_t i = 0; i < hoff.size(); ++i) {
+    const int64_t* s = hoff[i].data_ptr<int64_t>();
+    for (int64_t j = 1; j <= ns[i]; ++j) d[row + j] = s[j] - s[0] + base;
+    row += ns[i];
+    base = d[row];
+  }
+}
+
+struct Col {
+  bool fixed = true;
+  int w = 0;
+  std::vector<at::Tensor> data, hoff;
+  std::vector<int64_t> first, bytes, ns;
+  int64_t total_bytes = 0, n = 0;
+};
+
+// one KV column (keys or values) of `parts`
+Col gather_col(const std::vector<KV>& parts, bool keys) {
+  Col c;
+  for (auto& p : parts) {
+    const int w = keys ? p.kw : p.vw;
+    if (!c.data.empty() && (w < 0 || w != c.w)) c.fixed = false;
+    if (c.data.empty()) {
+      c.w = w;
+      c.fixed = w >= 0;
+    }
+    c.data.push_back(keys ? p.kdata : p.vdata);
+    c.ns.push_back(p.n);
+    c.n += p.n;
+  }
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const KV& p = parts[i];
+    const int w = keys ? p.kw : p.vw;
+    at::Tensor hoff;
+    int64_t b;
+    if (w >= 0) {
+      b = p.n * w;
+      if (!c.fixed) {  // mixed widths: synthesise offsets
+        hoff = at::arange(0, (p.n + 1) * (int64_t)w, std::max(w, 1), opt(at::kCPU, at::kLong));
+        if (w == 0) hoff = at::zeros({p.n + 1}, opt(at::kCPU, at::kLong));
+      }
+      c.first.push_back(0);
+    } else {
+      b = col_bytes(keys ? p.koff : p.voff, w, p.n, &hoff);
+      c.first.push_back(hoff.data_ptr<int64_t>()[0]);
+    }
+    c.hoff.push_back(hoff);
+    c.bytes.push_back(b);
+    c.total_bytes += b;
+  }
+  return c;
+}
+
+void place_col(Layout& L, const Col& c) {
+  L.add((size_t)c.total_bytes);
+  if (!c.fixed) L.add((size_t)(c.n + 1) * 8);
+}
+
+// write the column at layout slots [slot, slot+1] and return (data, off)
+std::pair<at::Tensor, at::Tensor> write_col(const std::shared_ptr<Mapping>& m, const Layout& L, size_t& slot,
+                                            const Col& c) {
+  const size_t doff = L.off[slot++];
+  put_bytes(m, doff, c.data, c.first, c.bytes);
+  at::Tensor data = view(m, doff, c.total_bytes, at::kByte), off;
+  if (!c.fixed) {
+    const size_t ooff = L.off[slot++];
+    put_offsets(m, ooff, c.hoff, c.ns);
+    off = view(m, ooff, c.n + 1, at::kLong);
+  }
+  return {data, off};
+}
+
+KV kv_of(const std::shared_ptr<Mapping>& m, const Layout& L, size_t& slot, const Col& k, const Col& v) {
+  KV o;
+  o.n = k.n;
+  o.kw = k.fixed ? k.w : -1;
+  o.vw = v.fixed ? v.w : -1;
+  auto [kd, ko] = write_col(m, L, slot, k);
+  auto [vd, vo] = write_col(m, L, slot, v);
+  o.kdata = kd;
+  o.koff = ko;
+  o.vdata = vd;
+  o.voff = vo;
+  return o;
+}
+
+}  // namespace
+
+SpoolStats& spool_totals() { return totals(); }
+int64_t spool_files_live() { return g_files_live.load(); }
+
+std::string spool_path(const std::string& dir, const std::string& kind, int instance, int rank) {
+  char name[128];
+  std::snprintf(name, sizeof(name), "mrmpi.%s.%d.%lld.%d", kind.c_str(), instance, (long long)++g_counter, rank);
+  return (std::filesystem::path(dir) / name).string();
+}
+
+KV kv_to_file(const std::vector<KV>& parts, const std::string& path) {
+  if (parts.empty()) fail("kv_to_file: no parts");
+  Col k = gather_col(parts, true), v = gather_col(parts, false);
+  Layout L;
+  place_col(L, k);
+  place_col(L, v);
+  auto m = create_mapping(path, L.total);
+  size_t slot = 0;
+  KV o = kv_of(m, L, slot, k, v);
+  totals().files++;
+  totals().disk_bytes += (int64_t)L.total;
+  return o;
+}
+
+KMV kmv_to_file(const std::vector<KMV>& parts, const std::string& path) {
+  if (parts.empty()) fail("kmv_to_file: no parts");
+  std::vector<KV> keys, vals;
+  for (auto& p : parts) {
+    keys.push_back(p.keys);
+    KV v;
+    v.n = p.nval;
+    v.kw = 0;
+    v.vw = p.vw;
+    v.kdata = at::empty({0}, opt(at::kCPU, at::kByte));
+    v.vdata = p.vdata;
+    v.voff = p.voff;
+    vals.push_back(v);
+  }
+  Col kk = gather_col(keys, true), kv0 = gather_col(keys, false), vk = gather_col(vals, true),
+      vv = gather_col(vals, false);
+  int64_t nkey = 0;
+  for (auto& p : parts) nkey += p.nkey;
+  Layout L;
+  place_col(L, kk);
+  place_col(L, kv0);
+  place_col(L, vk);
+  place_col(L, vv);
+  L.add((size_t)(nkey + 1) * 8);  // seg
+  auto m = create_mapping(path, L.total);
+  size_t slot = 0;
+  KMV o;
+  o.keys = kv_of(m, L, slot, kk, kv0);
+  KV vals_kv = kv_of(m, L, slot, vk, vv);
+  o.vdata = vals_kv.vdata;
+  o.voff = vals_kv.voff;
+  o.vw = vals_kv.vw;
+  o.nkey = nkey;
+  o.nval = vals_kv.n;
+  int64_t* sg = reinterpret_cast<int64_t*>(static_cast<char*>(m->p) + L.off[slot]);
+  int64_t row = 0, base = 0;
+  for (auto& p : parts) {
+    at::Tensor s = host_i64(p.seg);
+    const int64_t* sp = s.data_ptr<int64_t>();
+    for (int64_t j = 0; j < p.nkey; ++j) sg[row + j] = sp[j] - sp[0] + base;
+    row += p.nkey;
+    base += p.nval;
+  }
+  sg[nkey] = base;
+  o.seg = view(m, L.off[slot], nkey + 1, at::kLong);
+  totals().files++;
+  totals().disk_bytes += (int64_t)L.total;
+  return o;
+}
+
+Spool::Spool(at::Device dev, SpoolConfig cfg) : dev_(dev), cfg_(std::move(cfg)) {
+  if (!cfg_.budget) cfg_.budget = std::make_shared<SpoolBudget>();
+}
+
+Spool::~Spool() {
+  try {
+    clear();
+  } catch (...) {
+  }
+}
+
+void Spool::sync() {
+  for (hipEvent_t e : pending_) {
+    const hipError_t r = hipEventSynchronize(e);
+    (void)hipEventDestroy(e);
+    if (r != hipSuccess) {
+      for (hipEvent_t x : pending_) (void)hipEventQuery(x);
+      pending_.clear();
+      fail(std::string("asynchronous drain failed: ") + hipGetErrorString(r));
+    }
+  }
+  pending_.clear();
+}
+
+std::string Spool::next_path() const { return spool_path(cfg_.dir, cfg_.kind, cfg_.instance, cfg_.rank); }
+
+void Spool::release(const KV& piece, int tier) {
+  const int64_t b = piece.nbytes();
+  SpoolBudget& B = *cfg_.budget;
+  if (tier == 0 && B.hbm >= 0) B.hbm += b;
+  if (tier == 1 && B.host >= 0) B.host += b;
+}
+
+void Spool::add(const KV& piece, hipStream_t copy) {
+  if (piece.n == 0) return;
+  const int64_t b = piece.nbytes();
+  SpoolBudget& B = *cfg_.budget;
+  KV p;
+  int tier;
+  const bool cuda = dev_.is_cuda();
+  if (cuda && (B.hbm < 0 || B.hbm >= b)) {
+    p = piece.device() == dev_ ? piece : kv_to(piece, dev_);
+    if (B.hbm >= 0) B.hbm -= b;
+    tier = 0;
+    st_.hbm_bytes += b;
+  } else if (B.host < 0 || B.host >= b) {
+    // the host tier (pinned when a GPU will read it back); a device piece
+    // with a copy stream drains asynchronously behind the current stream
+    const bool async = copy && cuda && piece.device().is_cuda();
+    hipStream_t cs = async ? at::hip::getCurrentHIPStream().stream() : nullptr;
+    if (async) {
+      hipEvent_t e;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess || hipEventRecord(e, cs) != hipSuccess ||
+          hipStreamWaitEvent(copy, e, 0) != hipSuccess)
+        fail("drain fence failed");
+      (void)hipEventDestroy(e);
+    }
+    auto h = [&](const at::Tensor& t) {
+      if (!t.defined()) return t;
+      if (t.is_cpu() && (!cuda || t.is_pinned())) return t;
+      at::Tensor o = at::empty(t.sizes(), t.options().device(at::kCPU).pinned_memory(cuda));
+      if (async) {
+        at::Tensor src = t.contiguous();
+        const size_t nb = (size_t)src.numel() * src.element_size();
+        if (nb && hipMemcpyAsync(o.data_ptr(), src.data_ptr(), nb, hipMemcpyDeviceToHost, copy) != hipSuccess)
+          fail("asynchronous drain copy failed");
+        // the device source must outlive the copy on `copy`
+        c10::hip::HIPCachingAllocator::recordStream(src.storage().data_ptr(),
+                                                   c10::hip::getStreamFromExternal(copy, dev_.index()));
+      } else {
+        o.copy_(t);
+      }
+      return o;
+    };
+    p = piece;
+    p.kdata = h(piece.kdata);
+    p.vdata = h(piece.vdata);
+    p.koff = h(piece.koff);
+    p.voff = h(piece.voff);
+    if (B.host >= 0) B.host -= b;
+    tier = 1;
+    st_.host_bytes += b;
+    if (async) {
+      hipEvent_t done;
+      if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess || hipEventRecord(done, copy) != hipSuccess)
+        fail("drain event failed");
+      pending_.push_back(done);
+    }
+  } else {
+    p = kv_to_file({piece}, next_path());
+    tier = 2;
+    st_.disk_bytes += b;
+    st_.files++;
+  }
+  pieces_.push_back(p);
+  tier_.push_back(tier);
+  n_ += piece.n;
+  bytes_ += b;
+  st_.pieces++;
+  totals().pieces++;
+}
+
+void Spool::clear() {
+  sync();
+  for (size_t i = 0; i < pieces_.size(); ++i) release(pieces_[i], tier_[i]);
+  pieces_.clear();
+  tier_.clear();
+  n_ = bytes_ = 0;
+}
+
+KV Spool::gather_host() {
+  sync();
+  if (pieces_.empty()) {
+    clear();
+    return empty_kv(at::Device(at::kCPU), 0, 0);
+  }
+  std::vector<KV> parts = pieces_;
+  const int64_t total = bytes_;
+  clear();  // budget shares back before deciding where the whole goes
+  SpoolBudget& B = *cfg_.budget;
+  if (parts.size() == 1 && parts[0].device().is_cpu()) return parts[0];
+  if (B.host < 0 || B.host >= total) {
+    KV o = concat(parts, at::Device(at::kCPU));
+    if (dev_.is_cuda()) {
+      auto pin = [](const at::Tensor& t) { return t.defined() && !t.is_pinned() ? t.pin_memory() : t; };
+      o.kdata = pin(o.kdata);
+      o.vdata = pin(o.vdata);
+      o.koff = pin(o.koff);
+      o.voff = pin(o.voff);
+    }
+    return o;
+  }
+  st_.files++;
+  st_.disk_bytes += total;
+  return kv_to_file(parts, next_path());
+}
+
+KV Spool::gather() {
+  sync();
+  SpoolBudget& B = *cfg_.budget;
+  if (dev_.is_cuda()) {
+    // what the tiers would hold once this spool's own shares are returned
+    int64_t hbm_room = B.hbm;
+    if (hbm_room >= 0)
+      for (size_t i = 0; i < pieces_.size(); ++i)
+        if (tier_[i] == 0) hbm_room += pieces_[i].nbytes();
+    if (hbm_room < 0 || hbm_room >= bytes_) {
+      std::vector<KV> parts = pieces_;
+      clear();
+      return concat(parts, dev_);
+    }
+  } else if (B.host < 0) {
+    std::vector<KV> parts = pieces_;
+    clear();
+    return concat(parts, dev_);
+  }
+  return gather_host();
+}
+
+}  // namespace mrh
