@@ -282,6 +282,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                     [](MR& r, int64_t v) { r.set.host_budget = v; })
       .def_property("streams", [](MR& r) { return r.set.streams; }, [](MR& r, int v) { r.set.streams = v; })
       .def_readwrite("mapfilecount", &MR::mapfilecount)
+      .def_property_readonly("spool_stats",
+                             [](MR& r) {
+                               py::dict d;
+                               d["pieces"] = r.spool_stats.pieces;
+                               d["hbm_bytes"] = r.spool_stats.hbm_bytes;
+                               d["host_bytes"] = r.spool_stats.host_bytes;
+                               d["disk_bytes"] = r.spool_stats.disk_bytes;
+                               d["files"] = r.spool_stats.files;
+                               return d;
+                             })
       .def_property(
           "kv", [](MR& r) -> py::object {
             r.ensure_resident();
@@ -764,6 +774,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       },
       py::arg("store"), py::arg("tag"), py::arg("members"), py::arg("rank"));
   m.def("live_rccl_comms", &mrh::live_rccl_comms);
+  // spool files currently on disk in this process (disk tier, spool.h)
+  m.def("spool_files_live", &mrh::spool_files_live);
   // world size 1 runs the local transport (no communicator); this builds a
   // one-rank RCCL communicator on `device` and returns what RCCL reports
   m.def("rccl_self_probe", [](int device) {

@@ -18,11 +18,19 @@ void KeyValue::flush() {
     kv.koff = at::from_blob(koff_.data(), {(int64_t)koff_.size()}, at::TensorOptions().dtype(at::kLong)).clone();
   if (kv.vw < 0)
     kv.voff = at::from_blob(voff_.data(), {(int64_t)voff_.size()}, at::TensorOptions().dtype(at::kLong)).clone();
-  push(kv_to(kv, dev_));
   reset_host();
+  if (spool_) {
+    spool_->add(kv);  // the spool picks the tier (no detour through HBM)
+    return;
+  }
+  push(kv_to(kv, dev_));
 }
 
 void KeyValue::push(const KV& c) {
+  if (spool_) {
+    spool_->add(c);
+    return;
+  }
   if (grp_) {
     if (grp_->accepts(c)) {
       grp_->add(c);
@@ -38,6 +46,12 @@ void KeyValue::push(const KV& c) {
 KV KeyValue::finish() {
   flush();
   done_.reset();
+  if (spool_) {
+    KV out = spool_->n() ? spool_->gather() : empty_kv(dev_, kw_ >= 0 ? kw_ : 0, vw_ >= 0 ? vw_ : 0);
+    last_spool_ = spool_->stats();
+    spool_.reset();
+    return out;
+  }
   if (grp_) {
     KV out = grp_->size() ? grp_->kv() : empty_kv(dev_, 0, 0);
     if (grp_->size()) done_ = std::move(grp_);

@@ -8,6 +8,13 @@
 // emission order, so a callback can mix both without a host round trip for
 // device data. finish() uploads the host part once and concatenates.
 //
+// set_spool() (a MapReduce object with an HBM or host budget): the builder is
+// bounded — host-emitted pairs are flushed every SpoolConfig::piece_bytes and
+// every chunk goes to a Spool (spool.h: HBM while the budget lasts, then
+// pinned host, then memory-mapped files under fpath), and finish() returns
+// the KV on the tier it fits (the reference pages a KeyValue to disk while
+// the map is still emitting, src/keyvalue.cpp:359-380).
+//
 // enable_grouping() (before the first add): every chunk is instead appended
 // to a GroupIndex (grouper.h), which groups it by key as it arrives, so a
 // convert() right after the map finds the group-by already done; finish()
@@ -19,6 +26,7 @@
 
 #include "grouper.h"
 #include "kv.h"
+#include "spool.h"
 
 namespace mrh {
 
@@ -34,6 +42,7 @@ class KeyValue {
     koff_.push_back((int64_t)kd_.size());
     voff_.push_back((int64_t)vd_.size());
     ++nh_;
+    if (spool_ && (int64_t)(kd_.size() + vd_.size()) + 16 * nh_ >= piece_bytes_) flush();
   }
   // add(n, keys, keybytes, values, valuebytes): n fixed-size pairs, packed
   void add(int64_t n, const char* ks, int64_t kb, const char* vs, int64_t vb) {
@@ -53,8 +62,17 @@ class KeyValue {
     if (kv.n) push(kv);
   }
   void enable_grouping() {
-    if (!grp_ && chunks_.empty() && nh_ == 0) grp_ = std::make_shared<GroupIndex>(dev_);
+    // a bounded (spooled) builder does not group: the index keeps everything in HBM
+    if (!grp_ && !spool_ && chunks_.empty() && nh_ == 0) grp_ = std::make_shared<GroupIndex>(dev_);
   }
+  // bound this builder by the tiers of `cfg` (before the first add)
+  void set_spool(const SpoolConfig& cfg) {
+    if (spool_ || grp_ || !chunks_.empty() || nh_) return;
+    spool_ = std::make_unique<Spool>(dev_, cfg);
+    piece_bytes_ = std::max<int64_t>(cfg.piece_bytes, 4096);
+  }
+  // tiers the spooled pieces went to (empty stats without a spool)
+  SpoolStats spool_stats() const { return spool_ ? spool_->stats() : last_spool_; }
   bool grouping() const { return grp_ != nullptr; }
   // capacity hint for the grouped arenas (GroupIndex::reserve); no-op without grouping
   void reserve_grouping(int64_t rows, int64_t key_bytes, int64_t value_bytes) {
@@ -63,7 +81,7 @@ class KeyValue {
   // the index of the KV the last finish() returned (null if not grouped)
   std::shared_ptr<GroupIndex> take_group() { return std::move(done_); }
   int64_t size() const {
-    int64_t n = nh_ + (grp_ ? grp_->size() : 0);
+    int64_t n = nh_ + (grp_ ? grp_->size() : 0) + (spool_ ? spool_->n() : 0);
     for (auto& c : chunks_) n += c.n;
     return n;
   }
@@ -95,6 +113,9 @@ class KeyValue {
   int kw_ = -2, vw_ = -2;
   std::vector<KV> chunks_;
   std::shared_ptr<GroupIndex> grp_, done_;
+  std::unique_ptr<Spool> spool_;
+  int64_t piece_bytes_ = int64_t(64) << 20;
+  SpoolStats last_spool_;
 };
 
 }  // namespace mrh

@@ -341,6 +341,51 @@ void MapReduce::enter(const char* op, bool ooc_ok) {
   unspill();
 }
 
+// A map/reduce builder of an MR with an HBM or host budget is bounded: its
+// chunks go through a Spool (HBM share of the budget, then pinned host up to
+// host_budget, then files under fpath), pieces of memsize bytes at most
+void MapReduce::bound(KeyValue& b) {
+  if (budget() <= 0 && set.host_budget <= 0) return;
+  SpoolConfig c;
+  c.budget->hbm = budget() > 0 && device().is_cuda() ? budget() : -1;
+  c.budget->host = set.host_budget > 0 ? set.host_budget : -1;
+  c.dir = set.fpath;
+  c.kind = "kv";
+  c.instance = instance_me_;
+  c.rank = comm_->rank();
+  c.piece_bytes = block_bytes();
+  if (budget() > 0) c.piece_bytes = std::min<int64_t>(c.piece_bytes, std::max<int64_t>(budget() / 4, 4096));
+  b.set_spool(c);
+}
+
+OocEnv MapReduce::ooc_env() const {
+  OocEnv e;
+  e.hbm = budget();
+  e.host = set.host_budget > 0 ? set.host_budget : -1;
+  e.dir = set.fpath;
+  e.instance = instance_me_;
+  e.rank = comm_->rank();
+  return e;
+}
+
+// append b to a: on the device, or — for a bounded MR — through a Spool, so
+// an addflag map never concatenates past the budgets
+KV MapReduce::append_kv(const KV& a, const KV& b) {
+  if (budget() <= 0 && set.host_budget <= 0) return concat({a, b}, device());
+  KeyValue tmp(device());
+  bound(tmp);
+  tmp.add_kv(a);
+  tmp.add_kv(b);
+  KV o = tmp.finish();
+  note_spool(tmp);
+  return o;
+}
+
+void MapReduce::note_spool(const KeyValue& b) {
+  const SpoolStats s = b.spool_stats();
+  spool_stats.add(s);
+}
+
 int64_t MapReduce::data_bytes() const {
   int64_t b = 0;
   if (kv) b += kv->nbytes();
@@ -350,9 +395,11 @@ int64_t MapReduce::data_bytes() const {
 
 void MapReduce::note_ooc(const char* op, const OocStats& st) {
   pages_ = std::max<int64_t>(pages_, st.parts);
+  spool_stats.files += st.files;
+  spool_stats.disk_bytes += st.disk_bytes;
   if (set.verbosity > 0 && comm_->rank() == 0)
-    out(fmt("%s out of core: %" PRId64 " partitions, %" PRId64 " budget-sized chunks through HBM\n", op, st.parts,
-            st.chunks));
+    out(fmt("%s out of core: %" PRId64 " partitions, %" PRId64 " budget-sized chunks through HBM, %" PRId64
+            " spool files\n", op, st.parts, st.chunks, st.files));
 }
 
 std::unique_ptr<MapReduce> MapReduce::copy() const {
@@ -463,6 +510,7 @@ uint64_t MapReduce::add(MapReduce& other) {  // :348-374
 
 void MapReduce::open(int addflag) {  // :1648-1664
   open_ = std::make_unique<KeyValue>(device());
+  bound(*open_);
   open_add_ = addflag;
   kmv.reset();
 }
@@ -480,7 +528,7 @@ uint64_t MapReduce::close() {  // :658-672
   if (open_add_) ensure_resident();  // appending to data that was spilled to disk
   else drop_disk();                  // replacing it: the spilled copy must never be read back over n
   if (open_add_ && kv) {
-    kv = concat({*kv, n}, device());
+    kv = append_kv(*kv, n);
     grouped_.reset();
   } else {
     kv = n;
@@ -514,9 +562,10 @@ std::vector<int> MapReduce::my_tasks(int nmap) {  // :1102-1225
 
 uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) {
   KV n = kvb.finish();
+  note_spool(kvb);
   std::shared_ptr<GroupIndex> g = kvb.take_group();
   if (addflag && kv) {
-    kv = concat({*kv, n}, device());
+    kv = append_kv(*kv, n);
     grouped_.reset();
   } else {
     kv = n;
@@ -532,6 +581,7 @@ uint64_t MapReduce::map(int nmap, const MapTaskFn& fn, int addflag) {  // :1044-
   OpTrace tr_(__func__, this);
   enter(__func__);
   KeyValue kvb(device());
+  bound(kvb);
   for (int t : my_tasks(nmap)) fn(t, kvb);
   return finish_map(kvb, addflag);
 }
@@ -569,6 +619,7 @@ uint64_t MapReduce::map_file(const std::vector<std::string>& files, int selfflag
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
   KeyValue kvb(device());
+  bound(kvb);
   if (selfflag) {
     for (int i = 0; i < (int)fl.size(); ++i) fn(i, fl[i].c_str(), kvb);
   } else {
@@ -634,6 +685,7 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
       for (int j = 0; j < tpf[i]; ++j) plan.push_back({i, j, tpf[i], sizes[i]});
   }
   KeyValue kvb(device());
+  bound(kvb);
   std::vector<int> tasks;
   if (selfflag) {
     tasks.resize(plan.size());
@@ -681,9 +733,11 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
   align_col(k, s.n, src.set.keyalign, nullptr, 0, src.set.zeropage);
   align_col(v, s.n, src.set.valuealign, nullptr, 0, src.set.zeropage);
   KeyValue kvb(device());
+  bound(kvb);
   for (int64_t i = 0; i < s.n; ++i) fn((uint64_t)i, k.at(i), (int)k.len(i), v.at(i), (int)v.len(i), kvb);
   if (&src == this && addflag) {
     KV n = kvb.finish();
+    note_spool(kvb);
     kv = concat({s, n}, device());
     kmv.reset();
     stats("Map", 0);
@@ -700,9 +754,11 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   KeyValue kvb(device());
+  bound(kvb);
   fn(s, kvb);
   if (&src == this && addflag) {
     KV n = kvb.finish();
+    note_spool(kvb);
     kv = concat({s, n}, device());
     kmv.reset();
     stats("Map", 0);
@@ -797,7 +853,7 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
   last_convert = ConvertStats();
   if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
     OocStats os;
-    kmv = ooc_convert(*kv, budget(), device(), &os);  // hash-partitioned spools (src/keymultivalue.cpp:645-789)
+    kmv = ooc_convert(*kv, ooc_env(), device(), &os);  // hash-partitioned spools (src/keymultivalue.cpp:645-789)
     note_ooc("Convert", os);
   } else if (grouped_ && grouped_->describes(*kv) && !prehash.defined()) {
     // grouped while the map produced it: only the two short sorts are left
@@ -990,8 +1046,10 @@ uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
   enter(__func__, true);  // host callbacks read host-resident data in place
   need_kmv("reduce");
   KeyValue kvb(device());
+  bound(kvb);
   run_host_kmv(*kmv, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
   kv = kvb.finish();
+  note_spool(kvb);
   kmv.reset();
   stats("Reduce", 0);
   return count(kv->n);
@@ -1004,7 +1062,7 @@ uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dty
   need_kmv("reduce");
   if (needs_ooc(kmv->nbytes(), budget(), 2.0)) {  // values stream through HBM in budget-sized key ranges
     OocStats os;
-    kv = ooc_reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype, budget(), device(), &os);
+    kv = ooc_reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype, ooc_env(), device(), &os);
     note_ooc("Reduce", os);
   } else {
     kv = oom_retry(this, device(), my_proc(), "reduce_builtin",
@@ -1021,8 +1079,10 @@ uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
   enter(__func__);
   need_kmv("reduce");
   KeyValue kvb(device());
+  bound(kvb);
   fn(*kmv, kvb);
   kv = kvb.finish();
+  note_spool(kvb);
   kmv.reset();
   stats("Reduce", 0);
   return count(kv->n);
@@ -1035,8 +1095,10 @@ uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
   need_kv("compress");
   KMV m = mrh::convert(*kv, &last_convert);
   KeyValue kvb(device());
+  bound(kvb);
   run_host_kmv(m, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
   kv = kvb.finish();
+  note_spool(kvb);
   stats("Compress", 0);
   return count(kv->n);
 }
@@ -1097,7 +1159,7 @@ uint64_t MapReduce::sort_keys(int flag) {  // :2102-2126
   need_kv("sort_keys");
   if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
     OocStats os;
-    kv = ooc_sort(*kv, flag, false, budget(), device(), &os);  // sample sort over host spools
+    kv = ooc_sort(*kv, flag, false, ooc_env(), device(), &os);  // sample sort over host spools
     note_ooc("Sort_keys", os);
   } else {
     kv = oom_retry(this, device(), my_proc(), "sort_keys", [&] { return sort_kv(*kv, flag, false); });
@@ -1121,7 +1183,7 @@ uint64_t MapReduce::sort_values(int flag) {  // :2156-2180
   need_kv("sort_values");
   if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
     OocStats os;
-    kv = ooc_sort(*kv, flag, true, budget(), device(), &os);
+    kv = ooc_sort(*kv, flag, true, ooc_env(), device(), &os);
     note_ooc("Sort_values", os);
   } else {
     kv = oom_retry(this, device(), my_proc(), "sort_values", [&] { return sort_kv(*kv, flag, true); });

@@ -26,6 +26,7 @@
 #include "comm.h"
 #include "keyvalue.h"
 #include "kv.h"
+#include "ooc.h"
 
 namespace mrh {
 
@@ -66,7 +67,9 @@ struct Settings {
   // lands in pinned host memory, and convert / sort_keys / sort_values /
   // builtin reduces run out of core over host spools (ooc.cpp)
   int64_t hbm_budget = 0;
-  // pinned host bytes the spill tier may hold before it writes to disk (0 = unlimited)
+  // pinned host bytes the spill tier may hold before it writes to disk (0 =
+  // unlimited): map/reduce builders and the out-of-core spools put what
+  // exceeds it in memory-mapped files under fpath (spool.h)
   int64_t host_budget = 0;
   // HIP streams the pipelined apps overlap (H2D copy / compute / shuffle)
   int streams = 2;
@@ -152,6 +155,9 @@ class MapReduce {
   void cummulative_stats(int level, int reset);
   void set_fpath(const std::string& p) { set.fpath = p; }
 
+  // tiers the bounded builders of this MR's ops spooled to (spool.h), summed
+  SpoolStats spool_stats;
+
   // host spill tier: move the data to pinned host DRAM and back
   void spill();
   void unspill();
@@ -187,6 +193,13 @@ class MapReduce {
   void start();
   void enter(const char* op, bool ooc_ok = false);
   int64_t data_bytes() const;
+  void bound(KeyValue& b);
+  KV append_kv(const KV& a, const KV& b);
+ public:
+  // the tiers and names an out-of-core op of this MR may use
+  OocEnv ooc_env() const;
+ private:
+  void note_spool(const KeyValue& b);
   void note_ooc(const char* op, const OocStats& st);
   void stats(const char* heading, int which);
   void need_kv(const char* what) const;

@@ -23,17 +23,28 @@
 //           merge is needed, and stability holds end to end.
 //  reduce   builtin segmented reduces stream the KMV in key ranges whose values
 //           fit the budget.
-// Every result lives in pinned host memory; the MapReduce object brings it
+// Tiers (spool.h): the partition spools hold their pieces in pinned host
+// memory up to the host budget (Settings::host_budget) and in memory-mapped
+// files under fpath beyond it; results are pinned while they fit the host
+// budget, else one memory-mapped file. The MapReduce object brings a result
 // back to HBM on a later op when it fits.
+// Streaming: chunk k+1 is copied host -> HBM on a side stream while chunk k
+// is partitioned, and chunk k's buckets drain HBM -> host on a copy stream
+// (Spool::add with a stream) while chunk k+1 is partitioned.
 #include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
 
 #include <algorithm>
 #include <cstring>
 #include <limits>
 #include <stdexcept>
 
+#include "../kernels/launch.h"
 #include "kv.h"
 #include "ooc.h"
+#include "spool.h"
 
 namespace mrh {
 
@@ -136,30 +147,143 @@ std::vector<std::pair<int64_t, int64_t>> chunks(const KV& kv, const HostOff& h, 
   return out;
 }
 
-// spool the chunks of kv into M host buckets by a per-pair bucket id
-// produced on the device by `dest_of(chunk)`
+// a KV column set copied to `dev` on stream `side` (non-blocking from pinned
+// memory); the tensors are marked for use on `use` so the caching allocator
+// does not recycle them while `use` still reads them
+KV kv_to_async(const KV& kv, at::Device dev, const c10::hip::HIPStream& side, const c10::hip::HIPStream& use) {
+  c10::hip::HIPStreamGuard g(side);
+  auto one = [&](const at::Tensor& t) {
+    if (!t.defined()) return t;
+    at::Tensor d = t.to(dev, /*non_blocking=*/true);
+    if (d.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(d.storage().data_ptr(), use);
+    return d;
+  };
+  KV o = kv;
+  o.kdata = one(kv.kdata);
+  o.vdata = one(kv.vdata);
+  o.koff = one(kv.koff);
+  o.voff = one(kv.voff);
+  return o;
+}
+
+SpoolConfig spool_cfg(const OocEnv& env, const std::shared_ptr<SpoolBudget>& b, const char* kind) {
+  SpoolConfig c;
+  c.budget = b;
+  c.dir = env.dir;
+  c.kind = kind;
+  c.instance = env.instance;
+  c.rank = env.rank;
+  return c;
+}
+
+// spool the chunks of kv into M bucket spools by a per-pair bucket id
+// produced on the device by `dest_of(chunk)`; the spools share the host
+// budget and go to disk beyond it (HBM holds only the chunks in flight)
 template <typename F>
-std::vector<std::vector<KV>> spool(const KV& kv, int64_t cap, at::Device dev, int M, F&& dest_of, OocStats* st) {
-  std::vector<std::vector<KV>> parts((size_t)M);
+std::vector<Spool> spool(const KV& kv, int64_t cap, at::Device dev, int M, F&& dest_of, const OocEnv& env,
+                         OocStats* st) {
+  auto budget = std::make_shared<SpoolBudget>();
+  budget->hbm = 0;
+  budget->host = env.host;
+  std::vector<Spool> parts;
+  parts.reserve((size_t)M);
+  for (int d = 0; d < M; ++d) parts.emplace_back(dev, spool_cfg(env, budget, "part"));
   const HostOff h = host_off(kv);
-  for (auto [a, b] : chunks(kv, h, cap)) {
-    KV c = kv_to(kv_slice(kv, a, b, h.kp(), h.vp()), dev);
+  const auto ch = chunks(kv, h, cap);
+  const bool cuda = dev.is_cuda() && kv.device().is_cpu();
+  c10::optional<c10::hip::HIPStream> side, drain, main;
+  if (cuda) {
+    main = c10::hip::getCurrentHIPStream(dev.index());
+    side = c10::hip::getStreamFromPool(false, dev.index());
+    drain = c10::hip::getStreamFromPool(false, dev.index());
+  }
+  auto load = [&](size_t i) {
+    const KV slice = kv_slice(kv, ch[i].first, ch[i].second, h.kp(), h.vp());
+    if (!cuda) return kv_to(slice, dev);
+    KV c = kv_to_async(slice, dev, *side, *main);
+    return c;
+  };
+  std::vector<hipEvent_t> ready(2, nullptr);
+  if (cuda)
+    for (auto& e : ready)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) throw std::runtime_error("ooc: event");
+  struct Ev {
+    std::vector<hipEvent_t>* v;
+    ~Ev() {
+      for (auto e : *v)
+        if (e) (void)hipEventDestroy(e);
+    }
+  } ev_guard{&ready};
+  KV next;
+  if (!ch.empty()) {
+    next = load(0);
+    if (cuda && hipEventRecord(ready[0], side->stream()) != hipSuccess) throw std::runtime_error("ooc: event");
+  }
+  for (size_t i = 0; i < ch.size(); ++i) {
+    KV c = next;
+    if (cuda && hipStreamWaitEvent(main->stream(), ready[i % 2], 0) != hipSuccess)
+      throw std::runtime_error("ooc: stream wait");
+    if (i + 1 < ch.size()) {  // chunk i+1 on the PCIe link while chunk i partitions
+      next = load(i + 1);
+      if (cuda && hipEventRecord(ready[(i + 1) % 2], side->stream()) != hipSuccess)
+        throw std::runtime_error("ooc: event");
+    }
     at::Tensor dest = dest_of(c);
     Buckets B = bucket_local(c, dest, M);
     const HostOff bh = host_off(B.kv);
     int64_t s = 0;
     for (int d = 0; d < M; ++d) {
       const int64_t e = s + B.count[d];
-      if (e > s) parts[d].push_back(kv_host(kv_slice(B.kv, s, e, bh.kp(), bh.vp())));
+      if (e > s) parts[d].add(kv_slice(B.kv, s, e, bh.kp(), bh.vp()), cuda ? drain->stream() : nullptr);
       s = e;
     }
     if (st) {
       st->chunks++;
-      st->bytes_staged += row_bytes(kv, h, a, b);
+      st->bytes_staged += row_bytes(kv, h, ch[i].first, ch[i].second);
     }
   }
+  for (auto& p : parts) p.sync();
+  if (st)
+    for (auto& p : parts) {
+      st->files += p.stats().files;
+      st->disk_bytes += p.stats().disk_bytes;
+    }
   return parts;
 }
+
+// results of the per-partition pass: pinned while the host budget lasts,
+// files beyond it; finish() = one pinned KV, or one memory-mapped file
+struct KVSink {
+  const OocEnv& env;
+  OocStats* st;
+  int64_t used = 0;
+  std::vector<KV> parts;
+  void add(const KV& x) {
+    const int64_t b = x.nbytes();
+    if (env.host < 0 || used + b <= env.host) {
+      parts.push_back(kv_host(x));
+      used += b;
+    } else {
+      parts.push_back(kv_to_file({x.device().is_cpu() ? x : kv_host(x)}, spool_path(env.dir, "sort", env.instance,
+                                                                                     env.rank)));
+      if (st) {
+        st->files++;
+        st->disk_bytes += b;
+      }
+    }
+  }
+  int64_t total() const {
+    int64_t t = 0;
+    for (auto& p : parts) t += p.nbytes();
+    return t;
+  }
+  KV finish(const KV& like) {
+    if (parts.empty()) return kv_host(empty_kv(at::Device(at::kCPU), like.kw, like.vw));
+    if (env.host < 0 || total() <= env.host) return kv_host(concat(parts, at::Device(at::kCPU)));
+    if (st) st->files++;
+    return kv_to_file(parts, spool_path(env.dir, "kv", env.instance, env.rank));
+  }
+};
 
 int parts_for(int64_t bytes, int64_t budget, double factor) {
   const int64_t per = std::max<int64_t>(1, (int64_t)(budget / factor));
@@ -201,7 +325,8 @@ KMV kmv_concat_host(const std::vector<KMV>& parts, const KV& like) {
 
 bool needs_ooc(int64_t bytes, int64_t budget, double factor) { return budget > 0 && bytes * factor > budget; }
 
-KMV ooc_convert(const KV& kv, int64_t budget, at::Device dev, OocStats* st) {
+KMV ooc_convert(const KV& kv, const OocEnv& env, at::Device dev, OocStats* st) {
+  const int64_t budget = env.hbm;
   const int M = parts_for(kv.nbytes(), budget, 4.0);
   if (st) st->parts = M;
   auto parts = spool(kv, std::max<int64_t>(budget / 4, 1), dev, M, [&](const KV& c) {
@@ -209,19 +334,37 @@ KMV ooc_convert(const KV& kv, int64_t budget, at::Device dev, OocStats* st) {
     // has the same owner hash mod P): bits 20.. of the 64-bit grouping hash
     at::Tensor h = hash64_keys(c);
     return at::remainder(at::bitwise_right_shift(h, 20).bitwise_and_((int64_t(1) << 40) - 1), M).to(at::kInt);
-  }, st);
+  }, env, st);
   std::vector<KMV> out;
+  int64_t used = 0;
   for (int d = 0; d < M; ++d) {
     if (parts[d].empty()) continue;
-    KV p = kv_to(concat(parts[d], at::Device(at::kCPU)), dev);
+    KV p = kv_to(parts[d].gather_host(), dev);
     parts[d].clear();
-    out.push_back(kmv_host(convert(p)));
+    KMV m = convert(p);
+    p = KV();
+    const int64_t b = m.nbytes();
+    if (env.host < 0 || used + b <= env.host) {
+      out.push_back(kmv_host(m));
+      used += b;
+    } else {  // the disk tier: one file per partition result
+      out.push_back(kmv_to_file({kmv_host(m)}, spool_path(env.dir, "kmv", env.instance, env.rank)));
+      if (st) {
+        st->files++;
+        st->disk_bytes += b;
+      }
+    }
   }
-  return kmv_concat_host(out, kv);
+  int64_t total = 0;
+  for (auto& m : out) total += m.nbytes();
+  if (env.host < 0 || total <= env.host || out.empty()) return kmv_concat_host(out, kv);
+  if (st) st->files++;
+  return kmv_to_file(out, spool_path(env.dir, "kmv", env.instance, env.rank));
 }
 
-KV ooc_sort(const KV& kv, int flag, bool by_value, int64_t budget, at::Device dev, OocStats* st) {
-  const int M = parts_for(kv.nbytes(), budget, 4.0);
+KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device dev, OocStats* st) {
+  const int64_t budget = env.hbm;
+  const int M = std::min(parts_for(kv.nbytes(), budget, 4.0), 4096);
   if (st) st->parts = M;
   const int64_t cap = std::max<int64_t>(budget / 4, 1);
   auto skeys = [&](const KV& c) {
@@ -242,35 +385,47 @@ KV ooc_sort(const KV& kv, int flag, bool by_value, int64_t budget, at::Device de
     sample.insert(sample.end(), p, p + smp.numel());
   }
   std::sort(sample.begin(), sample.end());
-  // M-1 splitters as sign-flipped int64 (signed order == unsigned order)
-  std::vector<int64_t> split;
+  // M-1 distinct splitters (unsigned radix-key order)
+  std::vector<uint64_t> split;
   for (int j = 1; j < M && !sample.empty(); ++j) {
     const uint64_t v = sample[std::min(sample.size() - 1, sample.size() * j / M)];
-    if (split.empty() || (int64_t)(v ^ (1ull << 63)) != split.back()) split.push_back((int64_t)(v ^ (1ull << 63)));
+    if (split.empty() || v != split.back()) split.push_back(v);
   }
   const int MB = (int)split.size() + 1;
-  at::Tensor sp = at::tensor(split, opt(at::kCPU, at::kLong)).to(dev);
-  // pass 2: range partition (bucket = number of splitters below the key)
+  at::Tensor sp = at::from_blob(split.data(), {(int64_t)split.size()}, opt(at::kCPU, at::kLong)).clone().to(dev);
+  // pass 2: range partition, bucket = number of splitters below the key
+  // (a binary search over the splitters in LDS, k_bucket_by_splitters)
   auto parts = spool(kv, cap, dev, MB, [&](const KV& c) {
-    at::Tensor k = at::bitwise_xor(skeys(c), std::numeric_limits<int64_t>::min());
-    if (split.empty()) return at::zeros({c.n}, opt(dev, at::kInt));
-    return (k.unsqueeze(1) > sp.unsqueeze(0)).sum(1).to(at::kInt);
-  }, st);
+    at::Tensor k = skeys(c).contiguous();
+    at::Tensor out = at::empty({c.n}, opt(dev, at::kInt));
+    if (c.n == 0) return out;
+    if (dev.is_cuda()) {
+      k::bucket_by_splitters(reinterpret_cast<const uint64_t*>(k.data_ptr()), c.n,
+                             reinterpret_cast<const uint64_t*>(sp.data_ptr()), (int)split.size(),
+                             out.data_ptr<int32_t>(), at::hip::getCurrentHIPStream());
+    } else {
+      const uint64_t* kp = reinterpret_cast<const uint64_t*>(k.data_ptr());
+      int32_t* o = out.data_ptr<int32_t>();
+      for (int64_t i = 0; i < c.n; ++i) o[i] = (int32_t)(std::lower_bound(split.begin(), split.end(), kp[i]) - split.begin());
+    }
+    return out;
+  }, env, st);
   if (st) st->parts = MB;
   // pass 3: sort each bucket in HBM, append in bucket (= key) order
-  std::vector<KV> out;
+  KVSink sink{env, st};
   for (int d = 0; d < MB; ++d) {
     if (parts[d].empty()) continue;
-    KV p = kv_to(concat(parts[d], at::Device(at::kCPU)), dev);
+    KV p = kv_to(parts[d].gather_host(), dev);
     parts[d].clear();
-    out.push_back(kv_host(sort_kv(p, flag, by_value)));
+    sink.add(sort_kv(p, flag, by_value));
   }
-  if (out.empty()) return kv_host(kv);
-  return kv_host(concat(out, at::Device(at::kCPU)));
+  if (sink.parts.empty()) return kv_host(kv);
+  return sink.finish(kv);
 }
 
-KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, int64_t budget, at::Device dev,
-                      OocStats* st) {
+KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, const OocEnv& env,
+                      at::Device dev, OocStats* st) {
+  const int64_t budget = env.hbm;
   at::Tensor seg = kmv.seg.to(at::kCPU).contiguous();
   const int64_t* s = seg.data_ptr<int64_t>();
   at::Tensor vo = kmv.vw < 0 ? kmv.voff.to(at::kCPU).contiguous() : at::Tensor();
@@ -281,7 +436,7 @@ KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& 
     return kmv.vw >= 0 ? (s[b] - s[a]) * kmv.vw : vop[s[b]] - vop[s[a]] + 8 * (s[b] - s[a]);
   };
   const int64_t cap = std::max<int64_t>(budget / 4, 1);
-  std::vector<KV> out;
+  KVSink sink{env, st};
   int64_t a = 0;
   while (a < kmv.nkey) {
     const int64_t b = grow(a, kmv.nkey, [&](int64_t e) { return vbytes(a, e) <= cap; });
@@ -302,12 +457,12 @@ KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& 
     md.vdata = m.vdata.to(dev);
     if (m.voff.defined()) md.voff = m.voff.to(dev);
     md.seg = m.seg.to(dev);
-    out.push_back(kv_host(reduce_builtin(md, op, dtype)));
+    sink.add(reduce_builtin(md, op, dtype));
     if (st) st->chunks++;
     a = b;
   }
-  if (out.empty()) return kv_host(reduce_builtin(kmv, op, dtype));
-  return kv_host(concat(out, at::Device(at::kCPU)));
+  if (sink.parts.empty()) return kv_host(reduce_builtin(kmv, op, dtype));
+  return sink.finish(sink.parts[0]);
 }
 
 }  // namespace mrh

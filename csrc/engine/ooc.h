@@ -11,14 +11,26 @@ struct OocStats {
   int64_t parts = 0;         // partitions (convert) / range buckets (sort)
   int64_t chunks = 0;        // budget-sized pieces streamed through HBM
   int64_t bytes_staged = 0;  // bytes moved host -> HBM in the partition pass
+  int64_t files = 0;         // spool / result files written under fpath (disk tier)
+  int64_t disk_bytes = 0;    // bytes those files held
+};
+
+// where an out-of-core op may put its data (MapReduce settings)
+struct OocEnv {
+  int64_t hbm = 0;    // HBM budget (bytes)
+  int64_t host = -1;  // pinned host bytes before the disk tier (< 0 unlimited)
+  std::string dir = ".";
+  int instance = 0, rank = 0;
 };
 
 // does an op whose HBM working set is `factor` x `bytes` exceed the budget?
 bool needs_ooc(int64_t bytes, int64_t budget, double factor);
-// results are host-resident (pinned); inputs may be on the host or the device
-KMV ooc_convert(const KV& kv, int64_t budget, at::Device dev, OocStats* st = nullptr);
-KV ooc_sort(const KV& kv, int flag, bool by_value, int64_t budget, at::Device dev, OocStats* st = nullptr);
-KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, int64_t budget, at::Device dev,
-                      OocStats* st = nullptr);
+// results are host-resident: pinned while they fit env.host, else one
+// memory-mapped file under env.dir; inputs may be on the host (pinned,
+// pageable or memory-mapped) or the device
+KMV ooc_convert(const KV& kv, const OocEnv& env, at::Device dev, OocStats* st = nullptr);
+KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device dev, OocStats* st = nullptr);
+KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, const OocEnv& env,
+                      at::Device dev, OocStats* st = nullptr);
 
 }  // namespace mrh

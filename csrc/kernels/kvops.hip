@@ -199,6 +199,30 @@ void gather_fixed_t(const uint8_t* src, int w, const I* idx, int64_t n, uint8_t*
   MRH_CHECK_LAUNCH();
 }
 
+
+// range bucket of every key: the number of splitters strictly below it
+// (lower_bound over the sorted unsigned splitters, staged in LDS; up to
+// 4096 splitters = 32 KiB) — the out-of-core sample sort's partition pass
+constexpr int SPLIT_MAX = 4096;
+__global__ __launch_bounds__(256) void k_bucket_by_splitters(const uint64_t* __restrict__ keys, int64_t n,
+                                                            const uint64_t* __restrict__ split, int ns,
+                                                            int32_t* __restrict__ out) {
+  __shared__ uint64_t sp[SPLIT_MAX];
+  for (int i = threadIdx.x; i < ns; i += 256) sp[i] = split[i];
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const uint64_t k = keys[i];
+    int lo = 0, hi = ns;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sp[mid] < k) lo = mid + 1;
+      else hi = mid;
+    }
+    out[i] = lo;
+  }
+}
+
 }  // namespace
 
 void make_sortkeys_fixed(const uint8_t* data, int w, int64_t n, int mode, bool descending, uint64_t* keys,
@@ -276,6 +300,16 @@ void dest_byte_counts(const int32_t* dest, const int64_t* off, int64_t n, int P,
   hipLaunchKernelGGL(k_dest_bytes, dim3(g), dim3(NT), 0, s, dest, off, n, P, bytes);
   MRH_CHECK_LAUNCH();
 }
+void bucket_by_splitters(const uint64_t* keys, int64_t n, const uint64_t* split, int nsplit, int32_t* out,
+                         hipStream_t s) {
+  check_arg(nsplit >= 0 && nsplit <= SPLIT_MAX, "bucket_by_splitters: at most 4096 splitters");
+  if (n <= 0) return;
+  int64_t g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(k_bucket_by_splitters, dim3((unsigned)g), dim3(256), 0, s, keys, n, split, nsplit, out);
+  MRH_CHECK_LAUNCH();
+}
+
 void offsets_to_lengths(const int64_t* off, int64_t n, int32_t* len, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_off_to_len, dim3(nblk(n)), dim3(NT), 0, s, off, n, len);

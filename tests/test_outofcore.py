@@ -78,3 +78,72 @@ def test_out_of_core_cpu():
 @pytest.mark.gpu
 def test_out_of_core_gpu():
     _run("cuda:0")
+
+
+def _tiered(comm, tmp_path, data_bytes):
+    """hbm_budget = 1/20 and host_budget = 1/4 of the data: the map's builder
+    spools past both budgets (pinned host, then files under fpath), convert and
+    sort partition into spools that also reach the disk tier"""
+    mr = MapReduce(comm)
+    mr.fpath = str(tmp_path)
+    mr.hbm_budget = data_bytes // 20
+    mr.host_budget = data_bytes // 4
+    mr.memsize = -16384
+    return mr
+
+
+def _tiered_run(dev, tmp_path):
+    comm = g.Comm(device=dev)
+    C = g._ext.C
+    ref = MapReduce(comm)
+    ref.map(3, lambda i, kv: [kv.add(w, struct.pack("<i", j)) for j, w in enumerate(WORDS[i::3])])
+    data = ref.kv.nbytes()
+    ref.convert()
+    ref.reduce("count")
+    want_counts = dict((k, struct.unpack("<i", v)[0]) for k, v in ref.kv_pairs())
+    live0 = C.spool_files_live()
+    files_seen = set()
+
+    def peek():
+        files_seen.update(p.name for p in tmp_path.iterdir() if p.name.startswith("mrmpi."))
+
+    mr = _tiered(comm, tmp_path, data)
+    mr.map(3, lambda i, kv: [kv.add(w, struct.pack("<i", j)) for j, w in enumerate(WORDS[i::3])])
+    peek()
+    st = mr.spool_stats
+    assert st["files"] > 0 and st["disk_bytes"] > 0, st          # the map reached the disk tier
+    assert st["host_bytes"] > 0, st                              # ... through the pinned host tier
+    assert mr.kv.n == len(WORDS)
+    nu = mr.convert()
+    peek()
+    mr.reduce("count")
+    assert nu == len(set(WORDS))
+    assert dict((k, struct.unpack("<i", v)[0]) for k, v in mr.kv_pairs()) == want_counts
+    assert mr.spool_stats["files"] > st["files"]                 # convert's partition spools went to disk too
+    # sort: range-partitioned spools, same order as in memory
+    vals = [(j * 2654435761) % 100003 - 50000 for j in range(40000)]
+    srt = _tiered(comm, tmp_path, data)
+    srt.map(1, lambda i, kv: [kv.add(WORDS[j], struct.pack("<i", v)) for j, v in enumerate(vals)])
+    srt.sort_values(-1)
+    peek()
+    mem = MapReduce(comm)
+    mem.map(1, lambda i, kv: [kv.add(WORDS[j], struct.pack("<i", v)) for j, v in enumerate(vals)])
+    mem.sort_values(-1)
+    assert list(srt.kv_pairs()) == list(mem.kv_pairs())
+    assert files_seen, "spool files must appear under fpath"
+    assert all(p.startswith("mrmpi.") for p in files_seen)
+    del mr, srt
+    import gc
+    gc.collect()
+    # every spool file is removed once nothing views it
+    assert C.spool_files_live() == live0
+    assert not [p for p in tmp_path.iterdir() if p.name.startswith("mrmpi.")]
+
+
+def test_tiers_hbm_host_disk_cpu(tmp_path):
+    _tiered_run("cpu", tmp_path)
+
+
+@pytest.mark.gpu
+def test_tiers_hbm_host_disk_gpu(tmp_path):
+    _tiered_run("cuda:0", tmp_path)
