@@ -770,6 +770,52 @@ int str_cmp(const uint8_t* a, int64_t la, const uint8_t* b, int64_t lb) {
   }
 }
 
+// Device tie-break of a string sort (flags +-5/+-6): `ks`/`perm` are sorted on
+// the first 8-byte window. While some group of equal windows is still tied
+// and none of its strings ended inside the window (a zero byte: equal windows
+// then mean equal strings), its elements are re-keyed on the next 8 bytes and
+// re-sorted inside the group — LSD: by the new window, then stably by group
+// id — so only tied elements move and the order is stable throughout. Nothing
+// but the tied-element count leaves the device (reference compare_str /
+// compare_strn driving sort_onepage, src/mapreduce.cpp:2462-2538, 2780-2803).
+at::Tensor str_tiebreak_device(at::Tensor ks, at::Tensor perm, const at::Tensor& data, const at::Tensor& off,
+                               int64_t n, bool desc) {
+  auto s = cur_stream();
+  const at::Device dev = ks.device();
+  at::Tensor head = at::empty({n}, opt(dev, at::kInt)), active = at::empty({n}, opt(dev, at::kInt));
+  k::str_groups(P0<uint64_t>(ks), nullptr, nullptr, n, desc, P0<uint32_t>(head), s);
+  at::Tensor alive;
+  for (int64_t start = 8;; start += 8) {
+    k::str_active(P0<uint64_t>(ks), alive.defined() ? P0<uint8_t>(alive) : nullptr, P0<uint32_t>(head), n, desc,
+                  P0<uint32_t>(active), s);
+    at::Tensor pos = scan_u32(active);
+    const int64_t m = (int64_t)(uint32_t)pos[n].item<int32_t>();
+    if (m == 0) break;
+    at::Tensor hscan = scan_u32(head);  // hscan[i + 1] = group id of position i (1-based)
+    const int64_t ngroups = (int64_t)(uint32_t)hscan[n].item<int32_t>();
+    at::Tensor where = at::empty({m}, opt(dev, at::kInt)), nk = at::empty({m}, opt(dev, at::kLong)),
+               gk = at::empty({m}, opt(dev, at::kLong));
+    k::str_refine(P0<uint32_t>(active), P0<uint32_t>(pos), P0<uint32_t>(hscan) + 1, P0<uint32_t>(perm), P0<uint8_t>(data),
+                  P0<int64_t>(off), n, start, desc, P0<int32_t>(where), P0<uint64_t>(nk), P0<uint64_t>(gk), s);
+    auto r1 = radix_sort_pairs(nk, iota_u32(m, dev), 0, 64);
+    at::Tensor o1 = std::get<1>(r1);
+    at::Tensor g1 = gk.index_select(0, o1.to(at::kLong));
+    int gbits = 1;
+    while (gbits < 63 && (int64_t(1) << gbits) <= ngroups) ++gbits;
+    at::Tensor o2 = std::get<1>(radix_sort_pairs(g1, o1, 0, gbits));
+    at::Tensor perm2 = perm.clone();
+    at::Tensor alive2 = at::zeros({n}, opt(dev, at::kByte));
+    k::str_apply(P0<uint32_t>(o2), P0<int32_t>(where), P0<uint64_t>(nk), m, P0<uint32_t>(perm), P0<uint32_t>(perm2),
+                 P0<uint64_t>(ks), P0<uint8_t>(alive2), s);
+    perm = perm2;
+    alive = alive2;
+    at::Tensor head2 = at::empty({n}, opt(dev, at::kInt));
+    k::str_groups(P0<uint64_t>(ks), P0<uint8_t>(alive), P0<uint32_t>(head), n, desc, P0<uint32_t>(head2), s);
+    head = head2;
+  }
+  return perm;
+}
+
 // permutation sorting a (data, off, w) column by flag
 at::Tensor sort_perm_column(const at::Tensor& data, const at::Tensor& off, int w, int64_t n, int flag) {
   const at::Device dev = data.device();
@@ -797,15 +843,21 @@ at::Tensor sort_perm_column(const at::Tensor& data, const at::Tensor& off, int w
     uint32_t* ip = P0<uint32_t>(idx);
     for (int64_t i = 0; i < n; ++i) {
       uint64_t kk = 0;
-      for (int j = 0; j < 8; ++j) kk = (kk << 8) | (op[i] + j < op[i + 1] ? d[op[i] + j] : 0);
+      bool ended = false;  // strcmp semantics: nothing after the first NUL counts
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t c = (!ended && op[i] + j < op[i + 1]) ? d[op[i] + j] : 0;
+        ended |= c == 0;
+        kk = (kk << 8) | c;
+      }
       kp[i] = desc ? ~kk : kk;
       ip[i] = (uint32_t)i;
     }
   }
   auto [ks, perm, passes] = radix_sort_pairs(sk, idx, 0, 64);
-  // ties beyond the 8-byte prefix: only possible where adjacent prefixes are
-  // equal; resolve those groups on the host with full strcmp semantics.
-  if (n < 2 || !at::any(ks.narrow(0, 1, n - 1) == ks.narrow(0, 0, n - 1)).item<bool>()) return perm;
+  if (n < 2) return perm;
+  if (dev.is_cuda()) return str_tiebreak_device(ks, perm, data, o, n, desc);
+  // CPU engine: ties beyond the 8-byte prefix resolved with full strcmp semantics
+  if (!at::any(ks.narrow(0, 1, n - 1) == ks.narrow(0, 0, n - 1)).item<bool>()) return perm;
   at::Tensor ksh = ks.to(at::kCPU), ph = perm.to(at::kCPU);
   at::Tensor dh = data.to(at::kCPU), oh = o.to(at::kCPU);
   const uint64_t* kk = P0<uint64_t>(ksh);
@@ -856,7 +908,12 @@ at::Tensor column_sort_keys(const at::Tensor& data, const at::Tensor& off, int w
     uint64_t* kp = P0<uint64_t>(sk);
     for (int64_t i = 0; i < n; ++i) {
       uint64_t kk = 0;
-      for (int j = 0; j < 8; ++j) kk = (kk << 8) | (op[i] + j < op[i + 1] ? d[op[i] + j] : 0);
+      bool ended = false;
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t c = (!ended && op[i] + j < op[i + 1]) ? d[op[i] + j] : 0;
+        ended |= c == 0;
+        kk = (kk << 8) | c;
+      }
       kp[i] = desc ? ~kk : kk;
     }
   }

@@ -43,12 +43,86 @@ __global__ __launch_bounds__(NT) void k_sortkeys_str(const uint8_t* __restrict__
   if (i >= n) return;
   int64_t a = off[i] + start, b = off[i + 1];
   uint64_t k = 0;
+  bool ended = false;  // strcmp semantics: nothing after the first NUL counts
   for (int j = 0; j < 8; ++j) {
-    uint64_t c = (a + j < b) ? d[a + j] : 0;
+    uint64_t c = (!ended && a + j < b) ? d[a + j] : 0;
+    ended |= c == 0;
     k = (k << 8) | c;
   }
   keys[i] = desc ? ~k : k;
   idx[i] = (uint32_t)i;
+}
+
+// ---- device tie-break of the string sort (flags +-5/+-6), one round per
+// 8-byte window: elements whose groups are still tied after the window at
+// `start` are re-keyed on the next window and re-sorted inside their group
+
+__device__ __forceinline__ bool window_ended(uint64_t k, bool desc) {
+  const uint64_t x = desc ? ~k : k;
+  // any zero byte: the string ended inside this window (equal windows = equal strings)
+  return ((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull) != 0;
+}
+
+// head / active flags after the round whose keys are ks (valid for alive elements)
+__global__ __launch_bounds__(NT) void k_str_groups(const uint64_t* __restrict__ ks, const uint8_t* __restrict__ alive,
+                                                   const uint32_t* __restrict__ head_in, int64_t n, bool desc,
+                                                   uint32_t* __restrict__ head_out) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  const bool al = alive ? alive[i] != 0 : true;
+  bool h = i == 0 || (head_in && head_in[i]);
+  if (!h && al) {
+    const bool prev_al = alive ? alive[i - 1] != 0 : true;
+    h = !prev_al || ks[i] != ks[i - 1];
+  }
+  if (!h && !al) h = true;  // a settled element is its own group
+  head_out[i] = h ? 1u : 0u;
+}
+__global__ __launch_bounds__(NT) void k_str_active(const uint64_t* __restrict__ ks, const uint8_t* __restrict__ alive,
+                                                   const uint32_t* __restrict__ head, int64_t n, bool desc,
+                                                   uint32_t* __restrict__ active) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  const bool al = alive ? alive[i] != 0 : true;
+  const bool multi = !head[i] || (i + 1 < n && !head[i + 1]);
+  active[i] = (al && multi && !window_ended(ks[i], desc)) ? 1u : 0u;
+}
+
+// compact the active elements: position, next-window key, group id
+__global__ __launch_bounds__(NT) void k_str_refine(const uint32_t* __restrict__ active, const uint32_t* __restrict__ pos,
+                                                   const uint32_t* __restrict__ gid_incl, const uint32_t* __restrict__ perm,
+                                                   const uint8_t* __restrict__ d, const int64_t* __restrict__ off,
+                                                   int64_t n, int64_t start, bool desc, int32_t* __restrict__ where,
+                                                   uint64_t* __restrict__ nk, uint64_t* __restrict__ gk) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n || !active[i]) return;
+  const uint32_t j = pos[i];
+  const uint32_t r = perm[i];
+  int64_t a = off[r] + start, b = off[r + 1];
+  uint64_t k = 0;
+  bool ended = false;
+  for (int q = 0; q < 8; ++q) {
+    uint64_t c = (!ended && a + q < b) ? d[a + q] : 0;
+    ended |= c == 0;
+    k = (k << 8) | c;
+  }
+  where[j] = (int32_t)i;
+  nk[j] = desc ? ~k : k;
+  gk[j] = gid_incl[i];
+}
+
+// apply the in-group order: element j of the sorted compact list takes the
+// j-th active position (groups are contiguous in both)
+__global__ __launch_bounds__(NT) void k_str_apply(const uint32_t* __restrict__ order, const int32_t* __restrict__ where,
+                                                  const uint64_t* __restrict__ nk, int64_t m,
+                                                  const uint32_t* __restrict__ perm_in, uint32_t* __restrict__ perm_out,
+                                                  uint64_t* __restrict__ ks, uint8_t* __restrict__ alive) {
+  int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (j >= m) return;
+  const int32_t dst = where[j], src = where[order[j]];
+  perm_out[dst] = perm_in[src];
+  ks[dst] = nk[order[j]];
+  alive[dst] = 1;
 }
 
 __global__ __launch_bounds__(NT) void k_iota(uint32_t* __restrict__ idx, int64_t n) {
@@ -237,6 +311,32 @@ void make_sortkeys_strprefix(const uint8_t* data, const int64_t* off, int64_t n,
   if (n <= 0) return;
   hipLaunchKernelGGL(k_sortkeys_str, dim3(nblk(n)), dim3(NT), 0, s, data, off, n, start, descending, keys,
                      idx);
+  MRH_CHECK_LAUNCH();
+}
+void str_groups(const uint64_t* ks, const uint8_t* alive, const uint32_t* head_in, int64_t n, bool desc,
+                uint32_t* head_out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_str_groups, dim3(nblk(n)), dim3(NT), 0, s, ks, alive, head_in, n, desc, head_out);
+  MRH_CHECK_LAUNCH();
+}
+void str_active(const uint64_t* ks, const uint8_t* alive, const uint32_t* head, int64_t n, bool desc, uint32_t* active,
+                hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_str_active, dim3(nblk(n)), dim3(NT), 0, s, ks, alive, head, n, desc, active);
+  MRH_CHECK_LAUNCH();
+}
+void str_refine(const uint32_t* active, const uint32_t* pos, const uint32_t* gid_incl, const uint32_t* perm,
+                const uint8_t* data, const int64_t* off, int64_t n, int64_t start, bool desc, int32_t* where,
+                uint64_t* nk, uint64_t* gk, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_str_refine, dim3(nblk(n)), dim3(NT), 0, s, active, pos, gid_incl, perm, data, off, n, start,
+                     desc, where, nk, gk);
+  MRH_CHECK_LAUNCH();
+}
+void str_apply(const uint32_t* order, const int32_t* where, const uint64_t* nk, int64_t m, const uint32_t* perm_in,
+               uint32_t* perm_out, uint64_t* ks, uint8_t* alive, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_str_apply, dim3(nblk(m)), dim3(NT), 0, s, order, where, nk, m, perm_in, perm_out, ks, alive);
   MRH_CHECK_LAUNCH();
 }
 void iota_u32(uint32_t* idx, int64_t n, hipStream_t s) {

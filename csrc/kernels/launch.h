@@ -103,6 +103,16 @@ void make_sortkeys_fixed(const uint8_t* data, int w, int64_t n, int mode, bool d
 void make_sortkeys_strprefix(const uint8_t* data, const int64_t* off, int64_t n, int64_t start,
                              bool descending, uint64_t* keys, uint32_t* idx, hipStream_t s);
 void iota_u32(uint32_t* idx, int64_t n, hipStream_t s);
+// device tie-break rounds of the string sort (kvops.hip; engine.cpp sort_perm_column)
+void str_groups(const uint64_t* ks, const uint8_t* alive, const uint32_t* head_in, int64_t n, bool desc,
+                uint32_t* head_out, hipStream_t s);
+void str_active(const uint64_t* ks, const uint8_t* alive, const uint32_t* head, int64_t n, bool desc, uint32_t* active,
+                hipStream_t s);
+void str_refine(const uint32_t* active, const uint32_t* pos, const uint32_t* gid_incl, const uint32_t* perm,
+                const uint8_t* data, const int64_t* off, int64_t n, int64_t start, bool desc, int32_t* where,
+                uint64_t* nk, uint64_t* gk, hipStream_t s);
+void str_apply(const uint32_t* order, const int32_t* where, const uint64_t* nk, int64_t m, const uint32_t* perm_in,
+               uint32_t* perm_out, uint64_t* ks, uint8_t* alive, hipStream_t s);
 // rows of width w gathered by idx
 void gather_fixed(const uint8_t* src, int w, const uint32_t* idx, int64_t n, uint8_t* dst, hipStream_t s);
 void gather_fixed_i64idx(const uint8_t* src, int w, const int64_t* idx, int64_t n, uint8_t* dst,

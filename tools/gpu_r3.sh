@@ -18,4 +18,6 @@ step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 200 --time
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 step bench 400 python bench.py || exit $?
 tail -1 gpurun_out/bench.log > gpurun_out/bench.json
+step strsort 300 python tools/strsort_bench.py 10000000 || exit $?
+step strsort_prof 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/prof_ss -o ss -- python3 tools/strsort_bench.py 10000000 || exit $?
 exit 0
