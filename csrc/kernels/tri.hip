@@ -19,6 +19,8 @@
 #include "common.h"
 #include "launch.h"
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 namespace mrh {
 namespace k {
@@ -469,6 +471,53 @@ __global__ __launch_bounds__(HUB_NT) void k_tri_hub_count(const int64_t* __restr
   if (dev::lane_id() == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
 }
 
+// LDS-bitmap hub kernel: one workgroup per hub u at a time; N+(u) (hub
+// ranks, relative to hb) is set as bits of a K-bit bitmap in LDS (64 KiB at
+// K = 524288), then every wave takes a v of N+(u) and its 64 lanes stream
+// N+(v) from the CSR column array — coalesced 4-byte reads — testing each w
+// against the LDS bitmap: |N+(u) ∩ N+(v)| costs d+(v) coalesced loads and LDS
+// bit tests instead of nnz(H[u]) scattered 8-byte loads of H[v] (the bitmap
+// kernel above, whose sparse lower-hub rows made it 67 % of tri_find). The
+// bits of N+(u) are cleared again behind the count (O(d+(u)), not O(K)).
+constexpr int HUBL_NT = 256;
+constexpr int HUBL_WORDS = 8192;  // K <= 524288
+__global__ __launch_bounds__(HUBL_NT) void k_tri_hub_lds(const int64_t* __restrict__ rowptr,
+                                                        const uint32_t* __restrict__ col, int64_t hb, int64_t r0,
+                                                        int64_t r1, unsigned long long* __restrict__ total) {
+  __shared__ unsigned long long bm[HUBL_WORDS];
+  for (int i = threadIdx.x; i < HUBL_WORDS; i += HUBL_NT) bm[i] = 0ull;
+  __syncthreads();
+  const int lane = dev::lane_id(), wv = dev::wave_id();
+  constexpr int NWV = HUBL_NT / MRH_WAVE;
+  uint64_t cnt = 0;
+  for (int64_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
+    const int64_t u = hb + r;
+    const int64_t a = rowptr[u], b = rowptr[u + 1];
+    if (b - a < 2) continue;  // uniform over the block
+    for (int64_t e = a + threadIdx.x; e < b; e += HUBL_NT) {
+      const uint32_t c = (uint32_t)((int64_t)col[e] - hb);
+      atomicOr(&bm[c >> 6], 1ull << (c & 63));
+    }
+    __syncthreads();
+    for (int64_t i = a + wv; i < b; i += NWV) {
+      const int64_t v = col[i];
+      const int64_t s0 = rowptr[v], s1 = rowptr[v + 1];
+      for (int64_t f = s0 + lane; f < s1; f += MRH_WAVE) {
+        const uint32_t w = (uint32_t)((int64_t)col[f] - hb);
+        cnt += (bm[w >> 6] >> (w & 63)) & 1ull;
+      }
+    }
+    __syncthreads();
+    for (int64_t e = a + threadIdx.x; e < b; e += HUBL_NT) {
+      const uint32_t c = (uint32_t)((int64_t)col[e] - hb);
+      bm[c >> 6] = 0ull;
+    }
+    __syncthreads();
+  }
+  cnt = dev::wave_sum(cnt);
+  if (lane == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
+}
+
 // rowptr[v] = first index of src v in the sorted oriented keys (rowptr[nvert] = m)
 // one thread per vertex: binary search (the top ranks have no out-edges, so a
 // per-edge gap fill would leave one thread walking millions of vertices)
@@ -544,8 +593,18 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
   MRH_CHECK_LAUNCH();
   if (r1 <= r0) return;
   const int64_t W = K / 64;
-  const unsigned grid = (unsigned)std::min<int64_t>(r1 - r0, 65536);
   const unsigned long long* Hc = (const unsigned long long*)H;
+  static const int hub_kernel = [] {  // MRH_TRI_HUB_KERNEL=bitmap|lds
+    const char* e = std::getenv("MRH_TRI_HUB_KERNEL");
+    return (e && std::string(e) == "bitmap") ? 0 : 1;
+  }();
+  if (hub_kernel == 1 && W <= HUBL_WORDS) {
+    const unsigned g = (unsigned)std::min<int64_t>(r1 - r0, 4096);
+    hipLaunchKernelGGL(k_tri_hub_lds, dim3(g), dim3(HUBL_NT), 0, s, rowptr, col, hb, r0, r1, total);
+    MRH_CHECK_LAUNCH();
+    return;
+  }
+  const unsigned grid = (unsigned)std::min<int64_t>(r1 - r0, 65536);
   if (W <= HUB_NT * 2)
     hipLaunchKernelGGL(k_tri_hub_count<2>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
   else if (W <= HUB_NT * 4)
