@@ -365,6 +365,7 @@ OocEnv MapReduce::ooc_env() const {
   e.dir = set.fpath;
   e.instance = instance_me_;
   e.rank = comm_->rank();
+  e.streams = set.streams;
   return e;
 }
 

@@ -71,8 +71,13 @@ struct Settings {
   // unlimited): map/reduce builders and the out-of-core spools put what
   // exceeds it in memory-mapped files under fpath (spool.h)
   int64_t host_budget = 0;
-  // HIP streams the pipelined apps overlap (H2D copy / compute / shuffle)
-  int streams = 2;
+  // depth of the host -> HBM staging pipelines: the streaming apps
+  // (InvertedIndex, wordfreq) keep streams - 1 input copies in flight on a
+  // side stream while a chunk computes, and the out-of-core passes overlap
+  // the next chunk's copy and the previous chunk's drain with compute
+  // (streams >= 2); 1 = copy and compute one chunk at a time, on one stream;
+  // 0 = each pipeline's tuned default (InvertedIndex 2, wordfreq 3, OOC 2)
+  int streams = 0;
   // collate() groups each received shuffle round while the next one is on
   // the wire (1, default) or runs aggregate then convert (0); the env
   // MRH_PIPELINE_COLLATE=0 sets the default to 0

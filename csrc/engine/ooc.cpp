@@ -190,7 +190,7 @@ std::vector<Spool> spool(const KV& kv, int64_t cap, at::Device dev, int M, F&& d
   for (int d = 0; d < M; ++d) parts.emplace_back(dev, spool_cfg(env, budget, "part"));
   const HostOff h = host_off(kv);
   const auto ch = chunks(kv, h, cap);
-  const bool cuda = dev.is_cuda() && kv.device().is_cpu();
+  const bool cuda = dev.is_cuda() && kv.device().is_cpu() && env.streams != 1;
   c10::optional<c10::hip::HIPStream> side, drain, main;
   if (cuda) {
     main = c10::hip::getCurrentHIPStream(dev.index());

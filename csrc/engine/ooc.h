@@ -21,6 +21,7 @@ struct OocEnv {
   int64_t host = -1;  // pinned host bytes before the disk tier (< 0 unlimited)
   std::string dir = ".";
   int instance = 0, rank = 0;
+  int streams = 0;  // 1: no copy/compute overlap (Settings::streams)
 };
 
 // does an op whose HBM working set is `factor` x `bytes` exceed the budget?

@@ -74,9 +74,14 @@ class InvertedIndex:
         self.names_dev = pools.device_constant(dev, self.names)
         self.name_off_dev = pools.device_constant(dev, self.name_off)
         maxlen = max((t.numel() for _, t in files), default=0)
-        # two persistent staging buffers (double-buffered H2D); the PAD bytes
-        # past each file are read by the 16-byte scan windows but never matched
-        self.bufs = [pools.device_buffer(dev, maxlen + PAD, slot) for slot in range(2 if files else 0)]
+        # persistent staging buffers: a ring of `streams` (0 = auto: 2, double
+        # buffered — a deeper ring gains nothing with 8 files, each copy is
+        # longer than its map) so streams - 1 file copies are in flight while
+        # one file maps; the PAD bytes past each file are read by the 16-byte
+        # scan windows but never matched
+        st = int(mr.streams)
+        self.nbuf = st if st > 0 else 2
+        self.bufs = [pools.device_buffer(dev, maxlen + PAD, slot) for slot in range(self.nbuf if files else 0)]
         self.copy_stream = pools.stream(dev, "h2d") if self.is_cuda else None
         self.output = None
         self._done = None
@@ -116,10 +121,11 @@ class InvertedIndex:
         else:
             main = torch.cuda.current_stream()
             cs = self.copy_stream
-            ready = [torch.cuda.Event(), torch.cuda.Event()]
+            nb = self.nbuf
+            ready = [torch.cuda.Event() for _ in range(nb)]
 
             def issue(i):
-                b = i & 1
+                b = i % nb
                 t = files[i][1]
                 with torch.cuda.stream(cs):
                     prev = pools.last_use(self.dev, b)  # the last kernel (any job) that read this buffer
@@ -128,12 +134,15 @@ class InvertedIndex:
                     self.bufs[b][: t.numel()].copy_(t, non_blocking=True)
                     ready[b].record(cs)
 
-            if files:
-                issue(0)
+            ahead = max(1, nb - 1)
+            for i in range(min(ahead, len(files))):
+                issue(i)
             for i in range(len(files)):
-                if i + 1 < len(files):
-                    issue(i + 1)
-                b = i & 1
+                if nb > 1 and i + ahead < len(files):
+                    issue(i + ahead)
+                elif nb == 1 and i > 0:
+                    issue(i)
+                b = i % nb
                 main.wait_event(ready[b])
                 n = files[i][1].numel()
                 part = C.map_urls(self.bufs[b], n, self.doc_base + i)

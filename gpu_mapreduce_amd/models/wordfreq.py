@@ -41,12 +41,14 @@ class WordFreq:
         self.combiner = combiner
         self.is_cuda = mr.device.startswith("cuda")
         maxlen = max((t.numel() for t in chunks), default=0)
-        # staging ring depth (MRH_WF_BUFS): 3 by default — with two buffers the
-        # copy of chunk i+2 waits for the count kernel of chunk i; 1 GiB step
-        # 29.0 / 24.5 / 25.3 ms with 2 / 3 / 4 buffers on one MI355X
-        # (profiles/r2_wordfreq_ring.txt)
+        # staging ring depth = the MR's `streams` setting (0 = auto: 3, or
+        # MRH_WF_BUFS) — with two buffers the copy of chunk i+2 waits for the
+        # count kernel of chunk i; 1 GiB step 29.0 / 24.5 / 25.3 ms with 2 / 3 /
+        # 4 buffers on one MI355X (profiles/r2_wordfreq_ring.txt); streams = 1
+        # copies and counts one chunk at a time
         import os
-        self.nbuf = max(2, int(os.environ.get("MRH_WF_BUFS", "3")))
+        st = int(mr.streams)
+        self.nbuf = st if st > 0 else max(2, int(os.environ.get("MRH_WF_BUFS", "3")))
         self.bufs = [pools.device_buffer(mr.device, maxlen + PAD, 8 + s) for s in range(self.nbuf if chunks else 0)]
         # the process's persistent H2D stream (a new stream per job would be
         # a new HIP queue each time)
@@ -91,11 +93,14 @@ class WordFreq:
                 self.bufs[b][: self.chunks[i].numel()].copy_(self.chunks[i], non_blocking=True)
                 ready[b].record(cs)
 
-        for i in range(min(nb - 1, len(self.chunks))):
+        ahead = max(1, nb - 1)
+        for i in range(min(ahead, len(self.chunks))):
             issue(i)
         for i in range(len(self.chunks)):
-            if i + nb - 1 < len(self.chunks):
-                issue(i + nb - 1)
+            if nb > 1 and i + ahead < len(self.chunks):
+                issue(i + ahead)
+            elif nb == 1 and i > 0:
+                issue(i)
             b = i % nb
             main.wait_event(ready[b])
             consume(self.bufs[b], self.chunks[i].numel())

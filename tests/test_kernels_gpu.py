@@ -211,14 +211,19 @@ def test_rmat_bit_exact():
     assert int(e.max()) < 2 ** 16
 
 
-def test_inverted_index_end_to_end_gpu():
+@pytest.mark.parametrize("streams", [0, 1, 3])
+def test_inverted_index_end_to_end_gpu(streams):
+    """the staging ring depth (MapReduce.streams: 0 auto, 1 serial, 3) never
+    changes the output bytes"""
     import gpu_mapreduce_amd as g
     from gpu_mapreduce_amd.models.inverted_index import InvertedIndex, reference_inverted_index
     from gpu_mapreduce_amd.utils import synth
     files = synth.html_corpus(4_000_000, file_bytes=1_000_000, seed=9, nurl=20_000)
     mr = g.MapReduce(g.Comm(device="cuda"))
+    mr.streams = streams
     app = InvertedIndex(mr, [(n, t.pin_memory()) for n, t in files])
     app.run()
+    assert app.nbuf == (streams or 2)
     got = {}
     for line in app.output_lines():
         url, rest = line.split("\t")
