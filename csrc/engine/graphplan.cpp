@@ -317,15 +317,30 @@ void PageRankPlan::build_device(const at::Tensor& e) {
                   invdeg_.data_ptr<float>(), reinterpret_cast<unsigned long long*>(nd.data_ptr()), s);
   }
   deg = at::Tensor();
-  // 3. by destination group, new source ids in the low word
+  // 3. by destination group, new source ids in the low word. One GPU, opt-in
+  // (MRH_PR_SRC_BLOCKS=S): groups are (source block, destination) with S
+  // blocks of consecutive new source ids, so the gather, which walks the
+  // groups in order, touches one block's slice of the rank vector at a time
+  // (a slice that fits the Infinity Cache); the S partial sums of a
+  // destination are added in block order
   const int64_t himax = !dist ? std::max<int64_t>(N - 1, 0) : P * nlmax - 1;
+  const int dbits = bits_for(himax);
+  int nblk = 1;
+  if (const char* e = std::getenv("MRH_PR_SRC_BLOCKS")) nblk = std::max(1, std::min(64, std::atoi(e)));
+  if (dist) nblk = 1;
+  // blocks split the sources that are gathered at all (out-degree > 0: new
+  // ids [0, nactive), degree-descending), not the dangling tail
+  const int64_t ndl = nd.item<int64_t>(), nactive = std::max<int64_t>(nlocal - ndl, 1);
+  const int64_t bspan = nblk > 1 ? (nactive + nblk - 1) / nblk : 0;
   at::Tensor sorted;
   {
     at::Tensor packed = at::empty({nedge}, opt(dev, at::kLong));
     k::pr_pack(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, P, nlmax, !dist, nid.data_ptr<int32_t>(),
-               reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
+               bspan, dbits, reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
     su = at::Tensor();
-    sorted = radix_sort_keys(packed, 32, 32 + bits_for(himax), false);
+    int bb = 0;
+    while ((1 << bb) < nblk) ++bb;
+    sorted = radix_sort_keys(packed, 32, 32 + dbits + bb, false);
   }
   // 4. unpack
   src_ = at::empty({nedge}, opt(dev, at::kInt));
@@ -348,9 +363,16 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     build_exchange(ujv, nid.narrow(0, 0, nlocal));
   } else {
     vid_ = at::empty({ngrp}, opt(dev, at::kInt));  // the group's destination, as a new id
-    k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nid.data_ptr<int32_t>(), vid_.data_ptr<int32_t>(), s);
+    k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nid.data_ptr<int32_t>(), (int64_t(1) << dbits) - 1,
+                    vid_.data_ptr<int32_t>(), s);
+    if (nblk > 1) {  // group ranges of the source blocks (for the ordered partial-sum adds)
+      at::Tensor blk = at::bitwise_right_shift(hi, dbits);
+      std::vector<int64_t> cnt = to_vec(bincount_dev(blk, nblk));
+      blk_off_.assign(1, 0);
+      for (int64_t c : cnt) blk_off_.push_back(blk_off_.back() + c);
+    }
   }
-  ndangling = comm->allreduce(nd.item<int64_t>(), Comm::SUM);
+  ndangling = comm->allreduce(ndl, Comm::SUM);
 }
 
 void PageRankPlan::build_exchange(const at::Tensor& ujv, const at::Tensor& new_of_old) {
@@ -499,6 +521,16 @@ void PageRankPlan::step() {
   } else if (comm->distributed()) {
     at::Tensor recv = comm->alltoallv(send_, send_splits_, recv_splits_);
     if (recv.numel()) pr_combine(rseg_, rperm_, recv, rvid_, acc_);
+  } else if (send_.numel() && blk_off_.size() > 2) {
+    // source blocks: block 0 stores, later blocks add, in block order (deterministic)
+    for (size_t b = 0; b + 1 < blk_off_.size(); ++b) {
+      const int64_t g0 = blk_off_[b], g1 = blk_off_[b + 1];
+      if (g1 <= g0) continue;
+      at::Tensor sv = send_.narrow(0, g0, g1 - g0), iv = vid_.narrow(0, g0, g1 - g0);
+      if (b == 0) scatter_f32(sv, iv, acc_);
+      else k::scatter_add_f32(sv.data_ptr<float>(), iv.data_ptr<int32_t>(), g1 - g0, acc_.data_ptr<float>(),
+                              at::hip::getCurrentHIPStream());
+    }
   } else if (send_.numel()) {
     scatter_f32(send_, vid_, acc_);
   }

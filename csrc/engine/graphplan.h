@@ -93,6 +93,7 @@ class PageRankPlan {
   at::Tensor r_, rn_, c_, dmass_, stats_;
   SegIndex six_;
   std::vector<int64_t> send_splits_, recv_splits_;
+  std::vector<int64_t> blk_off_;  // group ranges of the source blocks (MRH_PR_SRC_BLOCKS)
   // the plan from this rank's edges (source-owned): device kernels, or the
   // tensor-op twin on the CPU engine
   void build_device(const at::Tensor& e);

@@ -107,14 +107,18 @@ __global__ __launch_bounds__(NT) void k_pr_relabel(const uint32_t* __restrict__ 
 // v / P, owner-major), lo = new id of u (u is monotone here: the nid reads
 // are a sequential walk)
 __global__ __launch_bounds__(NT) void k_pr_pack(const uint64_t* __restrict__ su, int64_t n, int P, int64_t nlmax,
-                                                int local, const int32_t* __restrict__ nid,
-                                                uint64_t* __restrict__ out) {
+                                                int local, const int32_t* __restrict__ nid, int64_t bspan,
+                                                int dbits, uint64_t* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * NT;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const uint64_t x = __builtin_nontemporal_load(su + i);
     const int64_t v = (int64_t)(uint32_t)x;
-    const uint64_t hi = local ? (uint64_t)v : (uint64_t)((v % P) * nlmax + v / P);
-    out[i] = (hi << 32) | (uint32_t)nid[x >> 32];
+    uint64_t hi = local ? (uint64_t)v : (uint64_t)((v % P) * nlmax + v / P);
+    const uint32_t src = (uint32_t)nid[x >> 32];
+    // source-range blocking: the block of the new source id above the
+    // destination bits (groups = (block, destination))
+    if (bspan > 0) hi |= (uint64_t)(src / bspan) << dbits;
+    out[i] = (hi << 32) | src;
   }
 }
 
@@ -136,11 +140,23 @@ __global__ __launch_bounds__(NT) void k_pr_group_hi(const uint64_t* __restrict__
   if (g < ngrp) hi[g] = (int64_t)(s[seg[g]] >> 32);
 }
 
-// target row of group g: nid[hi] (hi an old id), or hi itself (nid == null)
+// target row of group g: nid[hi] (hi an old id), or hi itself (nid == null);
+// the bits at and above dmask's width are the source block
 __global__ __launch_bounds__(NT) void k_pr_group_vid(const int64_t* __restrict__ hi, int64_t ngrp,
-                                                     const int32_t* __restrict__ nid, int32_t* __restrict__ vid) {
+                                                     const int32_t* __restrict__ nid, int64_t dmask,
+                                                     int32_t* __restrict__ vid) {
   const int64_t g = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (g < ngrp) vid[g] = nid ? nid[hi[g]] : (int32_t)hi[g];
+  if (g < ngrp) {
+    const int64_t h = hi[g] & dmask;
+    vid[g] = nid ? nid[h] : (int32_t)h;
+  }
+}
+
+// acc[idx[i]] += v[i] (idx unique within one launch: one source block)
+__global__ __launch_bounds__(NT) void k_scatter_add_f32(const float* __restrict__ v, const int32_t* __restrict__ idx,
+                                                       int64_t n, float* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i < n) out[idx[i]] += v[i];
 }
 
 struct PermGet {
@@ -443,10 +459,11 @@ void pr_relabel(const uint32_t* order, const uint32_t* deg, int64_t n, int32_t* 
                      ndangling);
   MRH_CHECK_LAUNCH();
 }
-void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, uint64_t* out,
-             hipStream_t s) {
+void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, int64_t bspan,
+             int dbits, uint64_t* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_pr_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, nlmax, local ? 1 : 0, nid, out);
+  hipLaunchKernelGGL(k_pr_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, nlmax, local ? 1 : 0, nid, bspan,
+                     dbits, out);
   MRH_CHECK_LAUNCH();
 }
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s) {
@@ -459,9 +476,14 @@ void pr_group_hi(const uint64_t* sorted, const int64_t* seg, int64_t ngrp, int64
   hipLaunchKernelGGL(k_pr_group_hi, dim3(pr_grid(ngrp)), dim3(NT), 0, s, sorted, seg, ngrp, hi);
   MRH_CHECK_LAUNCH();
 }
-void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int32_t* vid, hipStream_t s) {
+void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int64_t dmask, int32_t* vid, hipStream_t s) {
   if (ngrp <= 0) return;
-  hipLaunchKernelGGL(k_pr_group_vid, dim3(pr_grid(ngrp)), dim3(NT), 0, s, hi, ngrp, nid, vid);
+  hipLaunchKernelGGL(k_pr_group_vid, dim3(pr_grid(ngrp)), dim3(NT), 0, s, hi, ngrp, nid, dmask, vid);
+  MRH_CHECK_LAUNCH();
+}
+void scatter_add_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_scatter_add_f32, dim3(pr_grid(n)), dim3(NT), 0, s, v, idx, n, out);
   MRH_CHECK_LAUNCH();
 }
 

@@ -196,11 +196,12 @@ void pr_run_degree(const uint64_t* sorted, const int64_t* seg, int64_t nrun, uin
 void pr_degkey(const uint32_t* deg, int64_t n, uint64_t* key, uint32_t* iota, hipStream_t s);
 void pr_relabel(const uint32_t* order, const uint32_t* deg, int64_t n, int32_t* nid, int64_t* order64,
                 uint8_t* dangling, float* invdeg, unsigned long long* ndangling, hipStream_t s);
-void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, uint64_t* out,
-             hipStream_t s);
+void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, int64_t bspan,
+             int dbits, uint64_t* out, hipStream_t s);
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s);
 void pr_group_hi(const uint64_t* sorted, const int64_t* seg, int64_t ngrp, int64_t* hi, hipStream_t s);
-void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int32_t* vid, hipStream_t s);
+void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int64_t dmask, int32_t* vid, hipStream_t s);
+void scatter_add_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s);
 void pr_update(float* acc, const float* r, float* rn, const uint8_t* dangling, int64_t n, float base,
                float alpha, const double* dmass, double invN, const float* invdeg, float* cout, double* partial,
                hipStream_t s);

@@ -499,12 +499,43 @@ __global__ __launch_bounds__(HUBL_NT) void k_tri_hub_lds(const int64_t* __restri
       atomicOr(&bm[c >> 6], 1ull << (c & 63));
     }
     __syncthreads();
-    for (int64_t i = a + wv; i < b; i += NWV) {
-      const int64_t v = col[i];
-      const int64_t s0 = rowptr[v], s1 = rowptr[v + 1];
-      for (int64_t f = s0 + lane; f < s1; f += MRH_WAVE) {
-        const uint32_t w = (uint32_t)((int64_t)col[f] - hb);
-        cnt += (bm[w >> 6] >> (w & 63)) & 1ull;
+    // each wave takes 64 v's of N+(u) at a time and flattens their N+(v)
+    // lists (wave prefix sum of d+(v)): lane l tests element s*64 + l of the
+    // concatenation, so all 64 lanes work whatever the d+(v) mix
+    for (int64_t i0 = a + (int64_t)wv * MRH_WAVE; i0 < b; i0 += (int64_t)NWV * MRH_WAVE) {
+      const int64_t i = i0 + lane;
+      int64_t s0 = 0;
+      int dv = 0;
+      if (i < b) {
+        const int64_t v = col[i];
+        s0 = rowptr[v];
+        dv = (int)(rowptr[v + 1] - s0);
+      }
+      int incl = dv;
+#pragma unroll
+      for (int o = 1; o < MRH_WAVE; o <<= 1) {
+        const int y = __shfl_up(incl, o, MRH_WAVE);
+        if (lane >= o) incl += y;
+      }
+      const int tot = __shfl(incl, MRH_WAVE - 1, MRH_WAVE);
+      for (int k0 = 0; k0 < tot; k0 += MRH_WAVE) {
+        const int k = k0 + lane;
+        // owner lane j of element k: the first lane whose inclusive sum > k
+        int lo = 0, hi = MRH_WAVE - 1;
+#pragma unroll
+        for (int st = 0; st < 6; ++st) {
+          const int mid = (lo + hi) >> 1;
+          const int im = __shfl(incl, mid, MRH_WAVE);
+          if (im > k) hi = mid;
+          else lo = mid + 1;
+        }
+        const int j = lo;
+        const int ex = __shfl(incl - dv, j, MRH_WAVE);
+        const int64_t sj = __shfl(s0, j, MRH_WAVE);
+        if (k < tot) {
+          const uint32_t w = (uint32_t)((int64_t)col[sj + (k - ex)] - hb);
+          cnt += (bm[w >> 6] >> (w & 63)) & 1ull;
+        }
       }
     }
     __syncthreads();

@@ -48,9 +48,18 @@ PAD = 64
 
 
 class InvertedIndex:
-    def __init__(self, mr: MapReduce, files, out_dir=None, pipelined=True, own_output=False):
+    def __init__(self, mr: MapReduce, files, out_dir=None, pipelined=True, own_output=False, prefetch_next=None):
         """files: list of (name, uint8 tensor) for THIS rank (host tensors —
-        ideally pinned — or device tensors)."""
+        ideally pinned — or device tensors).
+
+        prefetch_next: the (name, tensor) files of the job that will run next on
+        this rank (a job pipeline, e.g. a serving loop). While this job maps
+        its last file, the next job's first file is already copied into the
+        following staging slot, so the PCIe link does not idle during this
+        job's tail (its last file's map and group-by, the group ordering, the
+        output formatting); the next job finds that copy and does not repeat
+        it. Every job still copies all of its own files."""
+        self.prefetch_next = prefetch_next
         self.mr = mr
         self.files = files
         self.out_dir = out_dir
@@ -123,16 +132,27 @@ class InvertedIndex:
             cs = self.copy_stream
             nb = self.nbuf
             ready = [torch.cuda.Event() for _ in range(nb)]
+            # the staging ring continues across jobs: file i of this job lands
+            # in slot (base + i) % nb, so a job pipeline's prefetch of the next
+            # job's first file goes to the slot after this job's last one
+            base = pools.ring_cursor(self.dev, "ii") % nb
 
-            def issue(i):
-                b = i % nb
-                t = files[i][1]
+            def copy_into(b, t, ev):
                 with torch.cuda.stream(cs):
                     prev = pools.last_use(self.dev, b)  # the last kernel (any job) that read this buffer
                     if prev is not None:
                         cs.wait_event(prev)
                     self.bufs[b][: t.numel()].copy_(t, non_blocking=True)
-                    ready[b].record(cs)
+                    ev.record(cs)
+
+            def issue(i):
+                b = (base + i) % nb
+                t = files[i][1]
+                ev = pools.take_prefetch(self.dev, b, t)  # copied by the previous job of a pipeline
+                if ev is not None:
+                    ready[b] = ev
+                else:
+                    copy_into(b, t, ready[b])
 
             ahead = max(1, nb - 1)
             for i in range(min(ahead, len(files))):
@@ -142,12 +162,21 @@ class InvertedIndex:
                     issue(i + ahead)
                 elif nb == 1 and i > 0:
                     issue(i)
-                b = i % nb
+                if i == len(files) - 1 and nb > 1 and self.prefetch_next:
+                    # the next job's first file, behind this job's last copy
+                    nxt = self.prefetch_next[0][1]
+                    if nxt.numel() + PAD <= self.bufs[0].numel():
+                        slot = (base + len(files)) % nb
+                        ev = torch.cuda.Event()
+                        copy_into(slot, nxt, ev)
+                        pools.set_prefetch(self.dev, slot, nxt, ev)
+                b = (base + i) % nb
                 main.wait_event(ready[b])
                 n = files[i][1].numel()
                 part = C.map_urls(self.bufs[b], n, self.doc_base + i)
                 pools.mark_use(self.dev, b, main)
                 self._emit(kv, part)
+            pools.ring_cursor(self.dev, "ii", advance=len(files), n=nb)
         # lock-step exchanges: ranks with fewer files join with empty parts
         if self.pipelined and self.mr.nprocs > 1:
             for _ in range(len(files), self.max_files):

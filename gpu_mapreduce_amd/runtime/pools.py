@@ -14,6 +14,8 @@ _streams = {}
 _events = {}
 _ring = {}
 _const = {}
+_cursor = {}
+_prefetch = {}
 
 
 def device_buffer(device: str, nbytes: int, slot: int = 0) -> torch.Tensor:
@@ -71,6 +73,30 @@ def mark_use(device: str, slot: int, stream) -> None:
     _events[(str(device), slot)] = ev
 
 
+def ring_cursor(device: str, name: str, advance: int = 0, n: int = 1) -> int:
+    """Persistent position of a staging ring (which slot the next job's first
+    input lands in); advance moves it by the job's input count."""
+    key = (str(device), name)
+    c = _cursor.get(key, 0)
+    if advance:
+        _cursor[key] = (c + advance) % max(1, n)
+    return c
+
+
+def set_prefetch(device: str, slot: int, src: torch.Tensor, event) -> None:
+    """Record that `src` (a host tensor) is being copied into staging slot
+    `slot`, complete at `event` — issued by the previous job of a pipeline."""
+    _prefetch[(str(device), slot)] = (src.data_ptr(), src.numel(), event)
+
+
+def take_prefetch(device: str, slot: int, src: torch.Tensor):
+    """The copy event if `src` was prefetched into `slot` (consumed), else None."""
+    rec = _prefetch.pop((str(device), slot), None)
+    if rec is not None and rec[0] == src.data_ptr() and rec[1] == src.numel():
+        return rec[2]
+    return None
+
+
 def next_slot(name: str, n: int = 2) -> int:
     """Round-robin slot index for double-buffered outputs (job k uses slot k % n)."""
     i = _ring.get(name, 0)
@@ -90,3 +116,5 @@ def clear():
     _events.clear()
     _ring.clear()
     _const.clear()
+    _cursor.clear()
+    _prefetch.clear()

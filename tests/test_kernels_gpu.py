@@ -253,14 +253,16 @@ def test_inverted_index_bench_scale_gpu():
     files = [(n, t.cpu().pin_memory()) for n, t in files]
     comm = g.Comm(device="cuda")
     outs = []
-    for _ in range(2):
+    # jobs 0 and 1 prefetch the next job's first file (a job pipeline), job 2
+    # finds its first file already staged, job 3 runs alone
+    for j in range(4):
         mr = g.MapReduce(comm)
-        app = InvertedIndex(mr, files)
+        app = InvertedIndex(mr, files, prefetch_next=files if j < 2 else None)
         app.run()
         assert mr.last_convert.grouped == 1
         app.output_ready()
         outs.append(bytes(app.output.numpy()))
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2] == outs[3]
     got = {}
     for line in outs[0].decode("utf-8", "replace").splitlines():
         url, rest = line.split("\t")
