@@ -672,6 +672,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("N", &PageRankPlan::N)
       .def_readonly("nlocal", &PageRankPlan::nlocal)
       .def_property_readonly("blocking", &PageRankPlan::blocking)
+      .def_property_readonly("xcd_ranges", &PageRankPlan::xcd_ranges_count)
       .def_readonly("nedge", &PageRankPlan::nedge)
       .def_readonly("ndangling", &PageRankPlan::ndangling);
   py::class_<TriangleGraph>(m, "TriangleGraph")

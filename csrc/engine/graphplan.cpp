@@ -251,7 +251,13 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
       build_blocking(vid_.index_select(0, segment_ids(seg_, ngrp, nedge)));
   }
   acc_ = at::empty({nlocal}, opt(dev, at::kFloat));
-  if (ngrp > 0 && use_seg_index(dev) && !pb_) six_ = seg_index(seg_, nedge);
+  if (ngrp > 0 && use_seg_index(dev) && !pb_) {
+    six_ = seg_index(seg_, nedge);
+    if (xsched_.defined()) {
+      six_.sched = xsched_;
+      six_.slen = xslen_;
+    }
+  }
   reset();
 }
 
@@ -305,6 +311,11 @@ void PageRankPlan::build_device(const at::Tensor& e) {
   invdeg_ = at::empty({nlocal}, opt(dev, at::kFloat));
   at::Tensor nd = at::empty({1}, opt(dev, at::kLong));
   chk(hipMemsetAsync(nd.data_ptr(), 0, 8, s), "hipMemsetAsync");
+  // XCD source ranges (one GPU; MRH_PR_XCD=0 disables): see xcd_ranges()
+  const char* xenv = std::getenv("MRH_PR_XCD");
+  const char* benv = std::getenv("MRH_PR_BLOCKING");  // propagation blocking needs the plain layout
+  const bool want_xcd = !dist && !(xenv && *xenv == '0') && !(benv && *benv == '1');
+  at::Tensor degn;
   if (nlocal > 0) {
     at::Tensor dkey = at::empty({nlocal}, opt(dev, at::kLong)), io = at::empty({nlocal}, opt(dev, at::kInt));
     k::pr_degkey(reinterpret_cast<const uint32_t*>(deg.data_ptr()), nlocal, reinterpret_cast<uint64_t*>(dkey.data_ptr()),
@@ -312,35 +323,38 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     // 32-bit key; constant high digits (every degree < 2^24) are skipped
     at::Tensor ord = std::get<1>(radix_sort_pairs(dkey, io, 0, 32, true));
     dkey = io = at::Tensor();
+    if (want_xcd) degn = at::empty({nlocal}, opt(dev, at::kInt));
     k::pr_relabel(reinterpret_cast<const uint32_t*>(ord.data_ptr()), reinterpret_cast<const uint32_t*>(deg.data_ptr()),
                   nlocal, nid.data_ptr<int32_t>(), order_.data_ptr<int64_t>(), dangling_.data_ptr<uint8_t>(),
-                  invdeg_.data_ptr<float>(), reinterpret_cast<unsigned long long*>(nd.data_ptr()), s);
+                  invdeg_.data_ptr<float>(), reinterpret_cast<unsigned long long*>(nd.data_ptr()),
+                  degn.defined() ? degn.data_ptr<int32_t>() : nullptr, s);
   }
   deg = at::Tensor();
-  // 3. by destination group, new source ids in the low word. One GPU, opt-in
-  // (MRH_PR_SRC_BLOCKS=S): groups are (source block, destination) with S
-  // blocks of consecutive new source ids, so the gather, which walks the
-  // groups in order, touches one block's slice of the rank vector at a time
-  // (a slice that fits the Infinity Cache); the S partial sums of a
-  // destination are added in block order
+  const int64_t ndl = nd.item<int64_t>(), nactive = std::max<int64_t>(nlocal - ndl, 0);
+  // 3. by destination group, new source ids in the low word; with XCD source
+  // ranges the groups are (range, destination)
   const int64_t himax = !dist ? std::max<int64_t>(N - 1, 0) : P * nlmax - 1;
   const int dbits = bits_for(himax);
-  int nblk = 1;
-  if (const char* e = std::getenv("MRH_PR_SRC_BLOCKS")) nblk = std::max(1, std::min(64, std::atoi(e)));
-  if (dist) nblk = 1;
-  // blocks split the sources that are gathered at all (out-degree > 0: new
-  // ids [0, nactive), degree-descending), not the dangling tail
-  const int64_t ndl = nd.item<int64_t>(), nactive = std::max<int64_t>(nlocal - ndl, 1);
-  const int64_t bspan = nblk > 1 ? (nactive + nblk - 1) / nblk : 0;
+  std::vector<int64_t> rb, redge;  // hot range boundaries (new ids) and their first edges
+  if (degn.defined() && nactive > 0) xcd_ranges(degn, nactive, dbits, rb, redge);
+  degn = at::Tensor();
+  const int nhot = rb.empty() ? 0 : (int)rb.size() - 1;
+  at::Tensor rbd;
+  if (nhot > 0) {
+    std::vector<int32_t> rb32(rb.begin(), rb.end());
+    rbd = at::from_blob(rb32.data(), {(int64_t)rb32.size()}, opt(at::kCPU, at::kInt)).to(dev);
+  }
+  int rbits = 0;
+  while ((1 << rbits) < nhot + 1) ++rbits;
+  if (nhot == 0) rbits = 0;
   at::Tensor sorted;
   {
     at::Tensor packed = at::empty({nedge}, opt(dev, at::kLong));
     k::pr_pack(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, P, nlmax, !dist, nid.data_ptr<int32_t>(),
-               bspan, dbits, reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
+               nhot > 0 ? rbd.data_ptr<int32_t>() : nullptr, nhot, dbits, reinterpret_cast<uint64_t*>(packed.data_ptr()),
+               s);
     su = at::Tensor();
-    int bb = 0;
-    while ((1 << bb) < nblk) ++bb;
-    sorted = radix_sort_keys(packed, 32, 32 + dbits + bb, false);
+    sorted = radix_sort_keys(packed, 32, 32 + dbits + rbits, false);
   }
   // 4. unpack
   src_ = at::empty({nedge}, opt(dev, at::kInt));
@@ -361,18 +375,111 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     // hi = owner * nlmax + local id at the owner -> global destination id
     at::Tensor ujv = at::remainder(hi, nlmax) * P + at::floor_divide(hi, nlmax);
     build_exchange(ujv, nid.narrow(0, 0, nlocal));
+  } else if (nhot > 0 && ngrp > 0) {
+    // partial sums per (range, destination): the tiled combine reads each
+    // tile's R runs of (old destination, partial) and writes acc[nid[v]]
+    xr_ = nhot + 1;
+    xtile_ = (nlocal + (int64_t(1) << k::pr_tile_bits()) - 1) >> k::pr_tile_bits();
+    ghi_ = at::empty({ngrp}, opt(dev, at::kInt));
+    k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nullptr, (int64_t(1) << dbits) - 1, ghi_.data_ptr<int32_t>(), s);
+    xoff_ = at::empty({xr_ * (xtile_ + 1)}, opt(dev, at::kLong));
+    k::pr_range_offsets(hi.data_ptr<int64_t>(), ngrp, dbits, xr_, xtile_, xoff_.data_ptr<int64_t>(), s);
+    nid_ = nid.narrow(0, 0, nlocal);
+    xcd_schedule(redge);
   } else {
     vid_ = at::empty({ngrp}, opt(dev, at::kInt));  // the group's destination, as a new id
     k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nid.data_ptr<int32_t>(), (int64_t(1) << dbits) - 1,
                     vid_.data_ptr<int32_t>(), s);
-    if (nblk > 1) {  // group ranges of the source blocks (for the ordered partial-sum adds)
-      at::Tensor blk = at::bitwise_right_shift(hi, dbits);
-      std::vector<int64_t> cnt = to_vec(bincount_dev(blk, nblk));
-      blk_off_.assign(1, 0);
-      for (int64_t c : cnt) blk_off_.push_back(blk_off_.back() + c);
-    }
   }
   ndangling = comm->allreduce(ndl, Comm::SUM);
+}
+
+// XCD source ranges. Each XCD has its own 4 MiB L2; the pull gather reads
+// x[src] for every edge, and the degree-sorted new ids put the hot sources
+// first. The sources [0, T) are cut into layers of 8 ranges of equal edge
+// count whose widest range still fits one L2 (MRH_PR_L2_BYTES, 85 % of it);
+// range r of every layer runs on XCD slot r % 8 (xcd_schedule), so each XCD
+// streams its edges against an L2-resident slice of x. Layers are added until
+// less than 2 % of the edges are left (the cold tail, spread over all XCDs)
+// or the range ids run out of bits above the destination bits.
+// rb: the hot range boundaries (nhot + 1 new ids), redge: the first edge of
+// every range, hot and cold (nhot + 2 entries, redge.back() = nedge).
+void PageRankPlan::xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits, std::vector<int64_t>& rb,
+                              std::vector<int64_t>& redge) {
+  int64_t l2 = int64_t(4) << 20;
+  if (const char* e = std::getenv("MRH_PR_L2_BYTES")) l2 = std::max<int64_t>(4096, std::atoll(e));
+  const int64_t cap = l2 / 4 * 85 / 100;
+  if (nactive <= cap) return;  // the whole active rank vector fits one L2
+  const int maxr = std::min(64, 1 << std::max(0, std::min(6, 32 - dbits)));
+  int maxl = (maxr - 1) / 8;
+  if (const char* e = std::getenv("MRH_PR_XCD_LAYERS")) maxl = std::max(0, std::min(maxl, std::atoi(e)));
+  if (maxl <= 0) return;
+  // edges of the ids below i, sampled every `st` ids (boundaries are multiples
+  // of st, where the sample is exact)
+  at::Tensor cum = exclusive_scan(degn.narrow(0, 0, nactive));
+  const int64_t st = std::max<int64_t>(1, nactive >> 20);
+  const int64_t ns = nactive / st + 1;
+  at::Tensor smp = at::empty({ns}, opt(dev, at::kLong));
+  k::sample_i64(cum.data_ptr<int64_t>(), nactive + 1, st, ns, smp.data_ptr<int64_t>(),
+                at::hip::getCurrentHIPStream());
+  std::vector<int64_t> c = to_vec(smp);
+  const int64_t total = cum[nactive].item<int64_t>();
+  cum = smp = at::Tensor();
+  auto id_of = [&](int64_t k) { return std::min(k * st, nactive); };
+  // first sample k in [a, b] with c[k] >= v
+  auto first_ge = [&](int64_t a, int64_t b, int64_t v) {
+    return std::lower_bound(c.begin() + a, c.begin() + b + 1, v) - c.begin();
+  };
+  // width (ids) of the last of 8 equal-edge ranges of samples [a, b)
+  auto last_width = [&](int64_t a, int64_t b) {
+    const int64_t k7 = first_ge(a, b, c[a] + (c[b] - c[a]) * 7 / 8);
+    return id_of(b) - id_of(k7);
+  };
+  std::vector<int64_t> ks{0};
+  int64_t a = 0;
+  for (int l = 0; l < maxl; ++l) {
+    if (c[a] >= total - total / 50 || ns - 1 - a < 8) break;
+    int64_t lo = a + 8, hi = ns - 1;  // largest b with last_width(a, b) <= cap
+    if (last_width(a, lo) > cap) break;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) / 2;
+      if (last_width(a, mid) <= cap) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t b = lo;
+    for (int r = 1; r < 8; ++r) ks.push_back(first_ge(a, b, c[a] + (c[b] - c[a]) * r / 8));
+    ks.push_back(b);
+    a = b;
+  }
+  if (ks.size() < 9) return;
+  rb.clear();
+  redge.clear();
+  for (int64_t k : ks) {
+    rb.push_back(id_of(k));
+    redge.push_back(c[k]);
+  }
+  redge.push_back(total);
+}
+
+// the 8 x slen wave schedule of the gather: wave w (edges [1024 w, 1024 w +
+// 1024)) belongs to the range holding its first edge; hot range r runs on
+// slot r % 8 in layer order, the cold waves are dealt round-robin after them
+void PageRankPlan::xcd_schedule(const std::vector<int64_t>& redge) {
+  const int64_t T = 1024;  // wavesegred.h WS_TILE
+  const int64_t nw = (nedge + T - 1) / T;
+  const int nhot = (int)redge.size() - 2;
+  std::vector<std::vector<int32_t>> rows(8);
+  auto wave_of = [&](int64_t e) { return std::min(nw, (e + T - 1) / T); };
+  for (int r = 0; r < nhot; ++r)
+    for (int64_t w = wave_of(redge[r]); w < wave_of(redge[r + 1]); ++w) rows[r % 8].push_back((int32_t)w);
+  int64_t c = 0;
+  for (int64_t w = wave_of(redge[nhot]); w < nw; ++w, ++c) rows[c % 8].push_back((int32_t)w);
+  size_t slen = 0;
+  for (auto& r : rows) slen = std::max(slen, r.size());
+  std::vector<int32_t> flat(8 * slen, -1);
+  for (int x = 0; x < 8; ++x) std::copy(rows[x].begin(), rows[x].end(), flat.begin() + x * slen);
+  xsched_ = at::from_blob(flat.data(), {8, (int64_t)slen}, opt(at::kCPU, at::kInt)).to(dev);
+  xslen_ = (int64_t)slen;
 }
 
 void PageRankPlan::build_exchange(const at::Tensor& ujv, const at::Tensor& new_of_old) {
@@ -521,16 +628,9 @@ void PageRankPlan::step() {
   } else if (comm->distributed()) {
     at::Tensor recv = comm->alltoallv(send_, send_splits_, recv_splits_);
     if (recv.numel()) pr_combine(rseg_, rperm_, recv, rvid_, acc_);
-  } else if (send_.numel() && blk_off_.size() > 2) {
-    // source blocks: block 0 stores, later blocks add, in block order (deterministic)
-    for (size_t b = 0; b + 1 < blk_off_.size(); ++b) {
-      const int64_t g0 = blk_off_[b], g1 = blk_off_[b + 1];
-      if (g1 <= g0) continue;
-      at::Tensor sv = send_.narrow(0, g0, g1 - g0), iv = vid_.narrow(0, g0, g1 - g0);
-      if (b == 0) scatter_f32(sv, iv, acc_);
-      else k::scatter_add_f32(sv.data_ptr<float>(), iv.data_ptr<int32_t>(), g1 - g0, acc_.data_ptr<float>(),
-                              at::hip::getCurrentHIPStream());
-    }
+  } else if (send_.numel() && xr_ > 0) {
+    k::pr_tile_combine(send_.data_ptr<float>(), ghi_.data_ptr<int32_t>(), xoff_.data_ptr<int64_t>(), (int)xr_, xtile_,
+                       nid_.data_ptr<int32_t>(), nlocal, acc_.data_ptr<float>(), at::hip::getCurrentHIPStream());
   } else if (send_.numel()) {
     scatter_f32(send_, vid_, acc_);
   }
@@ -595,7 +695,7 @@ at::Tensor lookup(const at::Tensor& keys, const at::Tensor& q) {
 // sorted unique values of an int64 column
 at::Tensor unique_sorted(const at::Tensor& x) {
   if (x.numel() == 0) return x.contiguous();
-  at::Tensor s = sort_with_perm(x.contiguous()).first;
+  at::Tensor s = x.is_cuda() && x.scalar_type() == at::kLong ? radix_sort_keys(x, 0, 64) : sort_with_perm(x.contiguous()).first;
   at::Tensor sg = segments(s);
   return s.index_select(0, sg.narrow(0, 0, sg.numel() - 1)).contiguous();
 }

@@ -93,7 +93,13 @@ class PageRankPlan {
   at::Tensor r_, rn_, c_, dmass_, stats_;
   SegIndex six_;
   std::vector<int64_t> send_splits_, recv_splits_;
-  std::vector<int64_t> blk_off_;  // group ranges of the source blocks (MRH_PR_SRC_BLOCKS)
+  // XCD source ranges (one GPU): R = xr_ ranges, combine tiles, (range, tile)
+  // group offsets, old destination per group, old -> new ids, gather schedule
+  int64_t xr_ = 0, xtile_ = 0, xslen_ = 0;
+  at::Tensor xoff_, ghi_, nid_, xsched_;
+  void xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits, std::vector<int64_t>& rb,
+                  std::vector<int64_t>& redge);
+  void xcd_schedule(const std::vector<int64_t>& redge);
   // the plan from this rank's edges (source-owned): device kernels, or the
   // tensor-op twin on the CPU engine
   void build_device(const at::Tensor& e);
@@ -110,6 +116,7 @@ class PageRankPlan {
 
  public:
   bool blocking() const { return pb_; }
+  int64_t xcd_ranges_count() const { return xr_; }
 };
 
 // Triangle finder on a degree-oriented CSR (tri.cpp kernels). Multi-rank jobs

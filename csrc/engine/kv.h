@@ -189,7 +189,8 @@ void plan_combine(const at::Tensor& seg, const at::Tensor& perm, const at::Tenso
 // csrc/kernels/wavesegred.h): per-iteration gather-reduce with no segment search
 struct SegIndex {
   at::Tensor H, wbase, scratch;
-  int64_t nval = 0;
+  at::Tensor sched;  // optional XCD-pinned wave schedule (int32 [8, slen], -1 = none)
+  int64_t nval = 0, slen = 0;
   bool defined() const { return H.defined(); }
 };
 SegIndex seg_index(const at::Tensor& seg, int64_t nval);

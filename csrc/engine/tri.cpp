@@ -64,8 +64,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
   }
   // rank = position in (degree, id) order; perm[rank] = original id
   at::Tensor ids = at::arange(nvert, opt(dev, at::kLong));
-  at::Tensor dkey = at::bitwise_or(at::bitwise_left_shift(deg.to(at::kLong), 32), ids);
-  at::Tensor perm = std::get<1>(radix_sort_pairs(dkey, ids.to(at::kInt), 0, 64)).to(at::kLong);
+  // the LSD radix sort is stable: sorting the degrees alone keeps equal
+  // degrees in id order, i.e. (degree, id) order
+  at::Tensor perm = std::get<1>(radix_sort_pairs(deg.to(at::kLong), ids.to(at::kInt), 0, 32)).to(at::kLong);
   at::Tensor rank = at::empty({nvert}, opt(dev, at::kInt));
   rank.index_put_({perm}, ids.to(at::kInt));
   at::Tensor oriented = at::empty({m}, opt(dev, at::kLong));
@@ -80,13 +81,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
       o[i] = ra < rb ? (ra << 32 | rb) : (rb << 32 | ra);
     }
   }
-  at::Tensor okeys;
-  if (m) {
-    auto r = radix_sort_pairs(oriented, at::arange(m, opt(dev, at::kInt)), 0, 64);
-    okeys = std::get<0>(r);
-  } else {
-    okeys = oriented;
-  }
+  // keys-only: the oriented edges carry no payload
+  at::Tensor okeys = m ? radix_sort_keys(oriented, 0, 64) : oriented;
   at::Tensor col = at::bitwise_and(okeys, (int64_t)0xffffffff).to(at::kInt);
   at::Tensor rowptr;
   if (okeys.is_cuda()) {

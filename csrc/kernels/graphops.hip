@@ -82,11 +82,13 @@ __global__ __launch_bounds__(NT) void k_pr_degkey(const uint32_t* __restrict__ d
 }
 
 // new id i of old vertex order[i]: nid[order[i]] = i; the per-new-id
-// dangling flag and 1/outdeg; the dangling count (one atomic per wave)
+// dangling flag and 1/outdeg; the dangling count (one atomic per wave);
+// degn (nullable): the out-degree of every new id (degree-descending)
 __global__ __launch_bounds__(NT) void k_pr_relabel(const uint32_t* __restrict__ order, const uint32_t* __restrict__ deg,
                                                    int64_t n, int32_t* __restrict__ nid, int64_t* __restrict__ order64,
                                                    uint8_t* __restrict__ dangling, float* __restrict__ invdeg,
-                                                   unsigned long long* __restrict__ ndangling) {
+                                                   unsigned long long* __restrict__ ndangling,
+                                                   int32_t* __restrict__ degn) {
   const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
   bool dg = false;
   if (i < n) {
@@ -97,9 +99,29 @@ __global__ __launch_bounds__(NT) void k_pr_relabel(const uint32_t* __restrict__ 
     dg = d == 0;
     dangling[i] = dg ? 1 : 0;
     invdeg[i] = dg ? 0.f : (float)(1.0 / (double)d);
+    if (degn) degn[i] = (int32_t)d;
   }
   const uint64_t b = __ballot(dg);
   if (dev::lane_id() == 0 && b) atomicAdd(ndangling, (unsigned long long)__popcll(b));
+}
+
+// out[k] = in[min(k * stride, n - 1)], k < ns (a host-sized sample of a scan)
+__global__ __launch_bounds__(NT) void k_sample_i64(const int64_t* __restrict__ in, int64_t n, int64_t stride,
+                                                   int64_t ns, int64_t* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (k < ns) out[k] = in[k * stride < n ? k * stride : n - 1];
+}
+
+// source range of a new source id: hot ranges [rb[r], rb[r+1]) for r < nr,
+// every id >= rb[nr] is the cold range nr
+__device__ __forceinline__ uint32_t pr_range_of(uint32_t src, const int32_t* __restrict__ rb, int nr) {
+  int lo = 0, hi = nr;  // number of rb[1..nr] <= src
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((uint32_t)rb[mid] <= src) lo = mid;
+    else hi = mid - 1;
+  }
+  return (uint32_t)lo;
 }
 
 // the gather's sort key of every source-sorted edge (u << 32 | v): hi =
@@ -107,17 +129,18 @@ __global__ __launch_bounds__(NT) void k_pr_relabel(const uint32_t* __restrict__ 
 // v / P, owner-major), lo = new id of u (u is monotone here: the nid reads
 // are a sequential walk)
 __global__ __launch_bounds__(NT) void k_pr_pack(const uint64_t* __restrict__ su, int64_t n, int P, int64_t nlmax,
-                                                int local, const int32_t* __restrict__ nid, int64_t bspan,
-                                                int dbits, uint64_t* __restrict__ out) {
+                                                int local, const int32_t* __restrict__ nid,
+                                                const int32_t* __restrict__ rb, int nr, int dbits,
+                                                uint64_t* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * NT;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const uint64_t x = __builtin_nontemporal_load(su + i);
     const int64_t v = (int64_t)(uint32_t)x;
     uint64_t hi = local ? (uint64_t)v : (uint64_t)((v % P) * nlmax + v / P);
     const uint32_t src = (uint32_t)nid[x >> 32];
-    // source-range blocking: the block of the new source id above the
-    // destination bits (groups = (block, destination))
-    if (bspan > 0) hi |= (uint64_t)(src / bspan) << dbits;
+    // XCD source ranges: the range of the new source id above the
+    // destination bits (groups = (range, destination))
+    if (rb) hi |= (uint64_t)pr_range_of(src, rb, nr) << dbits;
     out[i] = (hi << 32) | src;
   }
 }
@@ -152,11 +175,84 @@ __global__ __launch_bounds__(NT) void k_pr_group_vid(const int64_t* __restrict__
   }
 }
 
-// acc[idx[i]] += v[i] (idx unique within one launch: one source block)
-__global__ __launch_bounds__(NT) void k_scatter_add_f32(const float* __restrict__ v, const int32_t* __restrict__ idx,
-                                                       int64_t n, float* __restrict__ out) {
-  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (i < n) out[idx[i]] += v[i];
+// first group of every (range r, destination tile t) of the (range,
+// destination)-sorted group keys hi: off[r * (ntile + 1) + t]; t == ntile is
+// the end of range r
+__global__ __launch_bounds__(NT) void k_pr_range_offsets(const int64_t* __restrict__ hi, int64_t ngrp, int dbits,
+                                                         int R, int64_t ntile, int tile_bits,
+                                                         int64_t* __restrict__ off) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= (int64_t)R * (ntile + 1)) return;
+  const int64_t r = i / (ntile + 1), t = i - r * (ntile + 1);
+  const int64_t key = t < ntile ? (r << dbits) + (t << tile_bits) : ((r + 1) << dbits);
+  int64_t lo = 0, h = ngrp;
+  while (lo < h) {
+    const int64_t mid = (lo + h) >> 1;
+    if (hi[mid] < key) lo = mid + 1;
+    else h = mid;
+  }
+  off[i] = lo;
+}
+
+// acc[nid[v]] = sum over the source ranges of the partial sum of v's group
+// in that range. One workgroup per tile of 2^PR_TILE_BITS destinations (old
+// ids): the tile's R runs of (old destination, partial) are read as one
+// flattened index space (no per-range barrier, no dependent load chain) and
+// added into LDS as 62-bit fixed point with integer atomics — integer adds
+// commute, so the result does not depend on their order (bitwise
+// reproducible) — then each touched destination is written once. Every
+// partial is in [0, 1] (r sums to 1 and c = r / outdeg), so 2^62 * sum fits
+// int64; values >= 2^-39 convert exactly.
+constexpr int PR_TILE_BITS = 12;
+constexpr int PR_MAX_RANGES = 64;
+__global__ __launch_bounds__(NT) void k_pr_tile_combine(const float* __restrict__ send, const int32_t* __restrict__ ghi,
+                                                        const int64_t* __restrict__ off, int R, int64_t ntile,
+                                                        const int32_t* __restrict__ nid, int64_t ndst,
+                                                        float* __restrict__ acc) {
+  constexpr int TILE = 1 << PR_TILE_BITS;
+  __shared__ unsigned long long sum[TILE];
+  __shared__ int64_t s_b[PR_MAX_RANGES];
+  __shared__ int s_pre[PR_MAX_RANGES + 1];
+  const int64_t t = blockIdx.x;
+  const int64_t d0 = t << PR_TILE_BITS;
+  for (int i = threadIdx.x; i < TILE; i += NT) sum[i] = 0ull;
+  if (threadIdx.x < MRH_WAVE) {  // range starts and a wave scan of the run lengths (R <= 64)
+    const int r = threadIdx.x;
+    int64_t g0 = 0, g1 = 0;
+    if (r < R) {
+      g0 = off[(int64_t)r * (ntile + 1) + t];
+      g1 = off[(int64_t)r * (ntile + 1) + t + 1];
+      s_b[r] = g0;
+    }
+    int len = (int)(g1 - g0), incl = len;
+#pragma unroll
+    for (int d = 1; d < MRH_WAVE; d <<= 1) {
+      const int y = __shfl_up(incl, d, MRH_WAVE);
+      if (r >= d) incl += y;
+    }
+    if (r < R) s_pre[r] = incl - len;
+    if (r == R - 1) s_pre[R] = incl;
+  }
+  __syncthreads();
+  const int total = s_pre[R];
+  for (int j = threadIdx.x; j < total; j += NT) {
+    int lo = 0, hi = R - 1;  // the range holding flattened pair j: last r with s_pre[r] <= j
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= j) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t g = s_b[lo] + (j - s_pre[lo]);
+    const int d = (int)(ghi[g] - d0);
+    atomicAdd(&sum[d], (unsigned long long)(long long)((double)send[g] * 0x1p62));
+  }
+  __syncthreads();
+  const int64_t nd = ndst - d0 < TILE ? ndst - d0 : TILE;
+  for (int i = threadIdx.x; i < nd; i += NT) {
+    const unsigned long long v = sum[i];
+    // untouched destinations keep acc == 0 (pr_update leaves it zeroed)
+    if (v) acc[nid[d0 + i]] = (float)((double)(long long)v * 0x1p-62);
+  }
 }
 
 struct PermGet {
@@ -362,7 +458,7 @@ void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64
 
 template <typename T>
 static void ws_gr_t(const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src, const T* x, const T* w,
-                    int op, T* out, void* scratch, hipStream_t s) {
+                    int op, T* out, void* scratch, hipStream_t s, const int32_t* sched, int64_t slen) {
   // scratch: carry (2 nw) ids + values, then the level-2 carry (2 ceil(2 nw / 64)) ids + values
   const int64_t nc = dev::ws_nwave(nval) * 2, nc2 = 2 * ((nc + 63) / 64);
   char* p = reinterpret_cast<char*>(scratch);
@@ -370,18 +466,19 @@ static void ws_gr_t(const uint32_t* H, const int64_t* wbase, int64_t nval, const
   T* cv = reinterpret_cast<T*>(p + (size_t)nc * sizeof(int64_t));
   int64_t* cs2 = reinterpret_cast<int64_t*>(p + (size_t)nc * 16);
   T* cv2 = reinterpret_cast<T*>(p + (size_t)nc * 16 + (size_t)nc2 * sizeof(int64_t));
-  if (op == 0) dev::ws_gather_reduce<T, 0>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2);
-  else if (op == 1) dev::ws_gather_reduce<T, 1>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2);
-  else dev::ws_gather_reduce<T, 2>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2);
+  if (op == 0) dev::ws_gather_reduce<T, 0>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen);
+  else if (op == 1) dev::ws_gather_reduce<T, 1>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen);
+  else dev::ws_gather_reduce<T, 2>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen);
 }
 
 void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src,
-                      const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s) {
+                      const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s,
+                      const int32_t* sched, int64_t slen) {
   if (nval <= 0) return;
   switch (dtype) {
-    case 1: ws_gr_t<int64_t>(H, wbase, nval, src, (const int64_t*)x, (const int64_t*)w, op, (int64_t*)out, scratch, s); break;
-    case 2: ws_gr_t<float>(H, wbase, nval, src, (const float*)x, (const float*)w, op, (float*)out, scratch, s); break;
-    default: ws_gr_t<double>(H, wbase, nval, src, (const double*)x, (const double*)w, op, (double*)out, scratch, s); break;
+    case 1: ws_gr_t<int64_t>(H, wbase, nval, src, (const int64_t*)x, (const int64_t*)w, op, (int64_t*)out, scratch, s, sched, slen); break;
+    case 2: ws_gr_t<float>(H, wbase, nval, src, (const float*)x, (const float*)w, op, (float*)out, scratch, s, sched, slen); break;
+    default: ws_gr_t<double>(H, wbase, nval, src, (const double*)x, (const double*)w, op, (double*)out, scratch, s, sched, slen); break;
   }
 }
 
@@ -453,16 +550,21 @@ void pr_degkey(const uint32_t* deg, int64_t n, uint64_t* key, uint32_t* iota, hi
   MRH_CHECK_LAUNCH();
 }
 void pr_relabel(const uint32_t* order, const uint32_t* deg, int64_t n, int32_t* nid, int64_t* order64,
-                uint8_t* dangling, float* invdeg, unsigned long long* ndangling, hipStream_t s) {
+                uint8_t* dangling, float* invdeg, unsigned long long* ndangling, int32_t* degn, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_pr_relabel, dim3(pr_grid(n)), dim3(NT), 0, s, order, deg, n, nid, order64, dangling, invdeg,
-                     ndangling);
+                     ndangling, degn);
   MRH_CHECK_LAUNCH();
 }
-void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, int64_t bspan,
-             int dbits, uint64_t* out, hipStream_t s) {
+void sample_i64(const int64_t* in, int64_t n, int64_t stride, int64_t ns, int64_t* out, hipStream_t s) {
+  if (ns <= 0 || n <= 0) return;
+  hipLaunchKernelGGL(k_sample_i64, dim3(pr_grid(ns)), dim3(NT), 0, s, in, n, stride, ns, out);
+  MRH_CHECK_LAUNCH();
+}
+void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, const int32_t* rb,
+             int nr, int dbits, uint64_t* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_pr_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, nlmax, local ? 1 : 0, nid, bspan,
+  hipLaunchKernelGGL(k_pr_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, nlmax, local ? 1 : 0, nid, rb, nr,
                      dbits, out);
   MRH_CHECK_LAUNCH();
 }
@@ -481,9 +583,19 @@ void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int64_t d
   hipLaunchKernelGGL(k_pr_group_vid, dim3(pr_grid(ngrp)), dim3(NT), 0, s, hi, ngrp, nid, dmask, vid);
   MRH_CHECK_LAUNCH();
 }
-void scatter_add_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s) {
+int pr_tile_bits() { return PR_TILE_BITS; }
+void pr_range_offsets(const int64_t* hi, int64_t ngrp, int dbits, int R, int64_t ntile, int64_t* off, hipStream_t s) {
+  const int64_t n = (int64_t)R * (ntile + 1);
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_scatter_add_f32, dim3(pr_grid(n)), dim3(NT), 0, s, v, idx, n, out);
+  hipLaunchKernelGGL(k_pr_range_offsets, dim3(pr_grid(n)), dim3(NT), 0, s, hi, ngrp, dbits, R, ntile, PR_TILE_BITS,
+                     off);
+  MRH_CHECK_LAUNCH();
+}
+void pr_tile_combine(const float* send, const int32_t* ghi, const int64_t* off, int R, int64_t ntile, const int32_t* nid,
+                     int64_t ndst, float* acc, hipStream_t s) {
+  if (ntile <= 0) return;
+  check_arg(R >= 1 && R <= PR_MAX_RANGES, "pr_tile_combine: 1 <= R <= 64 source ranges");
+  hipLaunchKernelGGL(k_pr_tile_combine, dim3((unsigned)ntile), dim3(NT), 0, s, send, ghi, off, R, ntile, nid, ndst, acc);
   MRH_CHECK_LAUNCH();
 }
 

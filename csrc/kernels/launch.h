@@ -195,13 +195,22 @@ void pr_heads(const uint64_t* sorted, int64_t n, uint32_t* flags, hipStream_t s)
 void pr_run_degree(const uint64_t* sorted, const int64_t* seg, int64_t nrun, uint32_t* deg, hipStream_t s);
 void pr_degkey(const uint32_t* deg, int64_t n, uint64_t* key, uint32_t* iota, hipStream_t s);
 void pr_relabel(const uint32_t* order, const uint32_t* deg, int64_t n, int32_t* nid, int64_t* order64,
-                uint8_t* dangling, float* invdeg, unsigned long long* ndangling, hipStream_t s);
-void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, int64_t bspan,
-             int dbits, uint64_t* out, hipStream_t s);
+                uint8_t* dangling, float* invdeg, unsigned long long* ndangling, int32_t* degn, hipStream_t s);
+// out[k] = in[min(k * stride, n - 1)] for k < ns
+void sample_i64(const int64_t* in, int64_t n, int64_t stride, int64_t ns, int64_t* out, hipStream_t s);
+// rb (nullable, nr + 1 entries): hot source ranges [rb[r], rb[r+1]), ids >=
+// rb[nr] form range nr; the range goes above the dbits destination bits
+void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, const int32_t* rb,
+             int nr, int dbits, uint64_t* out, hipStream_t s);
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s);
 void pr_group_hi(const uint64_t* sorted, const int64_t* seg, int64_t ngrp, int64_t* hi, hipStream_t s);
 void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int64_t dmask, int32_t* vid, hipStream_t s);
-void scatter_add_f32(const float* v, const int32_t* idx, int64_t n, float* out, hipStream_t s);
+// XCD source ranges: destinations per combine tile (log2); first group of
+// every (range, tile) (R * (ntile + 1) int64); the tiled partial-sum combine
+int pr_tile_bits();
+void pr_range_offsets(const int64_t* hi, int64_t ngrp, int dbits, int R, int64_t ntile, int64_t* off, hipStream_t s);
+void pr_tile_combine(const float* send, const int32_t* ghi, const int64_t* off, int R, int64_t ntile, const int32_t* nid,
+                     int64_t ndst, float* acc, hipStream_t s);
 void pr_update(float* acc, const float* r, float* rn, const uint8_t* dangling, int64_t n, float base,
                float alpha, const double* dmass, double invN, const float* invdeg, float* cout, double* partial,
                hipStream_t s);
@@ -221,8 +230,11 @@ void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64
 // out[s] = OP_{e in seg s} x[src[e]] (+ w[e]); dtype/op as plan_gather_reduce;
 // scratch: ws_scratch_bytes(nval)
 size_t ws_scratch_bytes(int64_t nval);
+// sched (nullable): 8 x slen wave ids (-1 = none); blocks b and b + 8 share an
+// XCD, so slot b % 8 runs the waves of row b % 8 (an XCD-pinned schedule)
 void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src,
-                      const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s);
+                      const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s,
+                      const int32_t* sched = nullptr, int64_t slen = 0);
 // tri_find wedges: all pairs of each neighbour group
 void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
             int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);

@@ -446,12 +446,22 @@ __global__ __launch_bounds__(HUB_NT) void k_tri_hub_count(const int64_t* __restr
           ++o;
         }
       __syncthreads();
-      const int64_t work = (b - a) * total_nz;
-      for (int64_t t = threadIdx.x; t < work; t += HUB_NT) {
-        const int64_t e = a + t / total_nz;
-        const int li = (int)(t % total_nz);
+      // pair t = (edge t / nz, word t % nz), t = threadIdx.x + k * HUB_NT:
+      // both advance by a constant per step (one division per row, none per
+      // pair: the 64-bit div/mod per pair dominated this loop)
+      const uint32_t nzu = (uint32_t)total_nz;
+      const uint32_t de = HUB_NT / nzu, dl = HUB_NT % nzu;
+      int64_t e = a + threadIdx.x / nzu;
+      uint32_t li = threadIdx.x % nzu;
+      while (e < b) {
         const int64_t vr = (int64_t)col[e] - hb, w = s_idx[li];
         if (w >= (vr >> 6)) cnt += __popcll(s_val[li] & H[vr * W + w]);
+        e += de;
+        li += dl;
+        if (li >= nzu) {
+          li -= nzu;
+          ++e;
+        }
       }
       __syncthreads();
       continue;
@@ -625,9 +635,12 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
   if (r1 <= r0) return;
   const int64_t W = K / 64;
   const unsigned long long* Hc = (const unsigned long long*)H;
-  static const int hub_kernel = [] {  // MRH_TRI_HUB_KERNEL=bitmap|lds
+  // MRH_TRI_HUB_KERNEL=lds selects the LDS-bitmap kernel: on RMAT-24 it ran
+  // 1081 ms per tri_find against 350 with the global bitmap rows
+  // (profiles/r3_trifind_hub_kernels.txt), so the bitmap kernel is the default
+  static const int hub_kernel = [] {
     const char* e = std::getenv("MRH_TRI_HUB_KERNEL");
-    return (e && std::string(e) == "bitmap") ? 0 : 1;
+    return (e && std::string(e) == "lds") ? 1 : 0;
   }();
   if (hub_kernel == 1 && W <= HUBL_WORDS) {
     const unsigned g = (unsigned)std::min<int64_t>(r1 - r0, 4096);
@@ -635,18 +648,28 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
     MRH_CHECK_LAUNCH();
     return;
   }
-  const unsigned grid = (unsigned)std::min<int64_t>(r1 - r0, 65536);
-  if (W <= HUB_NT * 2)
-    hipLaunchKernelGGL(k_tri_hub_count<2>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
-  else if (W <= HUB_NT * 4)
-    hipLaunchKernelGGL(k_tri_hub_count<4>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
-  else if (W <= HUB_NT * 8)
-    hipLaunchKernelGGL(k_tri_hub_count<8>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
-  else if (W <= HUB_NT * 16)
-    hipLaunchKernelGGL(k_tri_hub_count<16>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
-  else
-    hipLaunchKernelGGL(k_tri_hub_count<32>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, r0, r1, Hc, total);
-  MRH_CHECK_LAUNCH();
+  // MRH_TRI_HUB_CHUNKS=n: n dispatches over equal row ranges (a per-range
+  // kernel trace of the hub work; one dispatch by default)
+  static const int chunks = [] {
+    const char* e = std::getenv("MRH_TRI_HUB_CHUNKS");
+    return e ? std::max(1, std::min(64, std::atoi(e))) : 1;
+  }();
+  for (int c = 0; c < chunks; ++c) {
+    const int64_t c0 = r0 + (r1 - r0) * c / chunks, c1 = r0 + (r1 - r0) * (c + 1) / chunks;
+    if (c1 <= c0) continue;
+    const unsigned grid = (unsigned)std::min<int64_t>(c1 - c0, 65536);
+    if (W <= HUB_NT * 2)
+      hipLaunchKernelGGL(k_tri_hub_count<2>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, c0, c1, Hc, total);
+    else if (W <= HUB_NT * 4)
+      hipLaunchKernelGGL(k_tri_hub_count<4>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, c0, c1, Hc, total);
+    else if (W <= HUB_NT * 8)
+      hipLaunchKernelGGL(k_tri_hub_count<8>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, c0, c1, Hc, total);
+    else if (W <= HUB_NT * 16)
+      hipLaunchKernelGGL(k_tri_hub_count<16>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, c0, c1, Hc, total);
+    else
+      hipLaunchKernelGGL(k_tri_hub_count<32>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, c0, c1, Hc, total);
+    MRH_CHECK_LAUNCH();
+  }
 }
 
 void tri_core_build(const int64_t* rowptr, const uint32_t* col, int64_t cb, int64_t T, int8_t* A, hipStream_t s) {

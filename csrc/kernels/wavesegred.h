@@ -61,10 +61,20 @@ __global__ __launch_bounds__(WS_NT) void k_ws_gather_reduce(const uint32_t* __re
                                                             int64_t nwave, const int32_t* __restrict__ src,
                                                             const T* __restrict__ x, const T* __restrict__ w,
                                                             T* __restrict__ out, int64_t* __restrict__ carry_seg,
-                                                            T* __restrict__ carry_val) {
+                                                            T* __restrict__ carry_val,
+                                                            const int32_t* __restrict__ sched, int64_t slen) {
   using R = RedOp<T, OP>;
   const int lane = threadIdx.x & 63;
-  const int64_t wv = (int64_t)blockIdx.x * (WS_NT / 64) + (threadIdx.x >> 6);
+  int64_t wv = (int64_t)blockIdx.x * (WS_NT / 64) + (threadIdx.x >> 6);
+  if (sched) {
+    // XCD-pinned schedule: blocks b and b + 8 run on one XCD, so slot b % 8
+    // walks row b % 8 of the schedule (its own source ranges: their slice of
+    // x stays in that XCD's L2)
+    const int64_t lw = (int64_t)(blockIdx.x >> 3) * (WS_NT / 64) + (threadIdx.x >> 6);
+    if (lw >= slen) return;
+    wv = sched[(int64_t)(blockIdx.x & 7) * slen + lw];
+    if (wv < 0) return;
+  }
   if (wv >= nwave) return;  // uniform per wave
   const int64_t E0 = wv * WS_TILE;
   const int64_t L0 = E0 + (int64_t)lane * WS_IT;
@@ -169,13 +179,14 @@ __global__ __launch_bounds__(WS_NT) void k_ws_gather_reduce(const uint32_t* __re
 template <typename T, int OP>
 inline void ws_gather_reduce(const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src, const T* x,
                              const T* w, T* out, int64_t* carry_seg, T* carry_val, hipStream_t s,
-                             int64_t* carry2_seg = nullptr, T* carry2_val = nullptr) {
+                             int64_t* carry2_seg = nullptr, T* carry2_val = nullptr,
+                             const int32_t* sched = nullptr, int64_t slen = 0) {
   if (nval <= 0) return;
   const int64_t nw = ws_nwave(nval);
   MRH_HIP(hipMemsetAsync(carry_seg, 0xff, sizeof(int64_t) * 2 * nw, s));
-  const int64_t nb = (nw + (WS_NT / 64) - 1) / (WS_NT / 64);
+  const int64_t nb = sched ? 8 * ((slen + (WS_NT / 64) - 1) / (WS_NT / 64)) : (nw + (WS_NT / 64) - 1) / (WS_NT / 64);
   hipLaunchKernelGGL((k_ws_gather_reduce<T, OP>), dim3((unsigned)nb), dim3(WS_NT), 0, s, H, wbase, nval, nw, src, x, w,
-                     out, carry_seg, carry_val);
+                     out, carry_seg, carry_val, sched, slen);
   MRH_CHECK_LAUNCH();
   const int64_t nc = 2 * nw;
   if (carry2_seg && nc > 4096) {  // two-level fold (k_carry_fold): long runs in parallel

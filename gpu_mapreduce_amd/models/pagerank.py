@@ -68,6 +68,8 @@ class PageRank:
         self.ndangling = self._p.ndangling
         # one GPU: propagation-blocked iteration (csrc/kernels/pbpr.hip)
         self.blocking = self._p.blocking
+        # source ranges pinned to XCDs (0 = plain pull gather)
+        self.xcd_ranges = self._p.xcd_ranges
         return self
 
     def reset(self):
