@@ -250,7 +250,8 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
     if (want && !comm->distributed() && dev.is_cuda() && nedge > 0 && nedge < (int64_t(1) << 31) && ngrp > 0)
       build_blocking(vid_.index_select(0, segment_ids(seg_, ngrp, nedge)));
   }
-  acc_ = at::empty({nlocal}, opt(dev, at::kFloat));
+  // the fused tile step (XCD ranges) needs no accumulator array
+  acc_ = at::empty({xr_ > 0 ? 0 : nlocal}, opt(dev, at::kFloat));
   if (ngrp > 0 && use_seg_index(dev) && !pb_) {
     six_ = seg_index(seg_, nedge);
     if (xsched_.defined()) {
@@ -376,20 +377,18 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     at::Tensor ujv = at::remainder(hi, nlmax) * P + at::floor_divide(hi, nlmax);
     build_exchange(ujv, nid.narrow(0, 0, nlocal));
   } else if (nhot > 0 && ngrp > 0) {
-    // partial sums per (range, destination): the tiled combine reads each
-    // tile's R runs of (old destination, partial) and writes acc[nid[v]]
+    // partial sums per (range, destination): the fused tile step reads each
+    // tile's R runs of (new destination id, partial) and updates the tile's ranks
     xr_ = nhot + 1;
     xtile_ = (nlocal + (int64_t(1) << k::pr_tile_bits()) - 1) >> k::pr_tile_bits();
     ghi_ = at::empty({ngrp}, opt(dev, at::kInt));
     k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nullptr, (int64_t(1) << dbits) - 1, ghi_.data_ptr<int32_t>(), s);
     xoff_ = at::empty({xr_ * (xtile_ + 1)}, opt(dev, at::kLong));
     k::pr_range_offsets(hi.data_ptr<int64_t>(), ngrp, dbits, xr_, xtile_, xoff_.data_ptr<int64_t>(), s);
-    nid_ = nid.narrow(0, 0, nlocal);
     xcd_schedule(redge);
   } else {
-    vid_ = at::empty({ngrp}, opt(dev, at::kInt));  // the group's destination, as a new id
-    k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nid.data_ptr<int32_t>(), (int64_t(1) << dbits) - 1,
-                    vid_.data_ptr<int32_t>(), s);
+    vid_ = at::empty({ngrp}, opt(dev, at::kInt));  // the group's destination (packed as its new id)
+    k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nullptr, (int64_t(1) << dbits) - 1, vid_.data_ptr<int32_t>(), s);
   }
   ndangling = comm->allreduce(ndl, Comm::SUM);
 }
@@ -629,8 +628,18 @@ void PageRankPlan::step() {
     at::Tensor recv = comm->alltoallv(send_, send_splits_, recv_splits_);
     if (recv.numel()) pr_combine(rseg_, rperm_, recv, rvid_, acc_);
   } else if (send_.numel() && xr_ > 0) {
-    k::pr_tile_combine(send_.data_ptr<float>(), ghi_.data_ptr<int32_t>(), xoff_.data_ptr<int64_t>(), (int)xr_, xtile_,
-                       nid_.data_ptr<int32_t>(), nlocal, acc_.data_ptr<float>(), at::hip::getCurrentHIPStream());
+    // combine and update fused per destination tile (no acc round trip)
+    const double base = (1.0 - alpha) / (double)N;
+    at::Tensor part = at::empty({xtile_, 2}, opt(dev, at::kDouble));
+    k::pr_tile_step(send_.data_ptr<float>(), ghi_.data_ptr<int32_t>(), xoff_.data_ptr<int64_t>(), (int)xr_, xtile_,
+                    nlocal, r_.data_ptr<float>(), rn_.data_ptr<float>(), dangling_.data_ptr<uint8_t>(), (float)base,
+                    (float)alpha, dmass_.data_ptr<double>(), 1.0 / (double)N, invdeg_.data_ptr<float>(),
+                    c_.data_ptr<float>(), part.data_ptr<double>(), at::hip::getCurrentHIPStream());
+    at::Tensor st = part.sum(0);
+    dmass_ = st.narrow(0, 1, 1);
+    stats_ = st;
+    std::swap(r_, rn_);
+    return;
   } else if (send_.numel()) {
     scatter_f32(send_, vid_, acc_);
   }

@@ -94,9 +94,9 @@ class PageRankPlan {
   SegIndex six_;
   std::vector<int64_t> send_splits_, recv_splits_;
   // XCD source ranges (one GPU): R = xr_ ranges, combine tiles, (range, tile)
-  // group offsets, old destination per group, old -> new ids, gather schedule
+  // group offsets, destination (new id) per group, gather schedule
   int64_t xr_ = 0, xtile_ = 0, xslen_ = 0;
-  at::Tensor xoff_, ghi_, nid_, xsched_;
+  at::Tensor xoff_, ghi_, xsched_;
   void xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits, std::vector<int64_t>& rb,
                   std::vector<int64_t>& redge);
   void xcd_schedule(const std::vector<int64_t>& redge);

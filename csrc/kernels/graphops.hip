@@ -136,7 +136,10 @@ __global__ __launch_bounds__(NT) void k_pr_pack(const uint64_t* __restrict__ su,
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const uint64_t x = __builtin_nontemporal_load(su + i);
     const int64_t v = (int64_t)(uint32_t)x;
-    uint64_t hi = local ? (uint64_t)v : (uint64_t)((v % P) * nlmax + v / P);
+    // one GPU: the destination as its NEW id (the relabelled id space of the
+    // rank vector), so the combine writes each tile of new ids contiguously;
+    // P > 1: the owner-major global destination
+    uint64_t hi = local ? (uint64_t)(uint32_t)nid[v] : (uint64_t)((v % P) * nlmax + v / P);
     const uint32_t src = (uint32_t)nid[x >> 32];
     // XCD source ranges: the range of the new source id above the
     // destination bits (groups = (range, destination))
@@ -194,49 +197,66 @@ __global__ __launch_bounds__(NT) void k_pr_range_offsets(const int64_t* __restri
   off[i] = lo;
 }
 
-// acc[nid[v]] = sum over the source ranges of the partial sum of v's group
-// in that range. One workgroup per tile of 2^PR_TILE_BITS destinations (old
-// ids): the tile's R runs of (old destination, partial) are read as one
-// flattened index space (no per-range barrier, no dependent load chain) and
-// added into LDS as 62-bit fixed point with integer atomics — integer adds
-// commute, so the result does not depend on their order (bitwise
-// reproducible) — then each touched destination is written once. Every
-// partial is in [0, 1] (r sums to 1 and c = r / outdeg), so 2^62 * sum fits
-// int64; values >= 2^-39 convert exactly.
+// One PageRank step's combine + update per tile of 2^PR_TILE_BITS
+// destinations (new ids d0 .. d0 + TILE): the sum over the source ranges of
+// the partial sums of each destination, then r_new = base + alpha * (sum +
+// dangling / N), c = r_new / outdeg, and the block's L1 delta and dangling
+// mass as fp64 partials — the rank vector is read and written once per
+// iteration, no acc array round trip. The tile's R runs of (destination,
+// partial) are read as one flattened index space (no per-range barrier, no
+// dependent load chain) and added into LDS as 62-bit fixed point with integer
+// atomics — integer adds commute, so the result does not depend on their
+// order (bitwise reproducible). Every partial is in [0, 1] (r sums to 1 and
+// c = r / outdeg), so 2^62 * sum fits int64; values >= 2^-39 convert exactly.
 constexpr int PR_TILE_BITS = 12;
 constexpr int PR_MAX_RANGES = 64;
-__global__ __launch_bounds__(NT) void k_pr_tile_combine(const float* __restrict__ send, const int32_t* __restrict__ ghi,
-                                                        const int64_t* __restrict__ off, int R, int64_t ntile,
-                                                        const int32_t* __restrict__ nid, int64_t ndst,
-                                                        float* __restrict__ acc) {
+
+__device__ __forceinline__ void pr_one(float a, float rv, float idg, bool dg, float base, float alpha, float dterm,
+                                       float& x, float& c, double& d, double& dm) {
+  x = base + alpha * (a + dterm);
+  c = x * idg;
+  d += fabs((double)x - (double)rv);
+  if (dg) dm += x;
+}
+
+__device__ __forceinline__ float fx_to_f(unsigned long long v) { return (float)((double)(long long)v * 0x1p-62); }
+
+__global__ __launch_bounds__(NT) void k_pr_tile_step(const float* __restrict__ send, const int32_t* __restrict__ ghi,
+                                                     const int64_t* __restrict__ off, int R, int64_t ntile,
+                                                     int64_t ndst, const float* __restrict__ r,
+                                                     float* __restrict__ rn, const uint8_t* __restrict__ dangling,
+                                                     float base, float alpha, const double* __restrict__ dmass,
+                                                     double invN, const float* __restrict__ invdeg,
+                                                     float* __restrict__ cout, double* __restrict__ partial) {
   constexpr int TILE = 1 << PR_TILE_BITS;
   __shared__ unsigned long long sum[TILE];
   __shared__ int64_t s_b[PR_MAX_RANGES];
   __shared__ int s_pre[PR_MAX_RANGES + 1];
+  __shared__ double sh[2][NT / MRH_WAVE];
   const int64_t t = blockIdx.x;
   const int64_t d0 = t << PR_TILE_BITS;
   for (int i = threadIdx.x; i < TILE; i += NT) sum[i] = 0ull;
   if (threadIdx.x < MRH_WAVE) {  // range starts and a wave scan of the run lengths (R <= 64)
-    const int r = threadIdx.x;
+    const int q = threadIdx.x;
     int64_t g0 = 0, g1 = 0;
-    if (r < R) {
-      g0 = off[(int64_t)r * (ntile + 1) + t];
-      g1 = off[(int64_t)r * (ntile + 1) + t + 1];
-      s_b[r] = g0;
+    if (q < R) {
+      g0 = off[(int64_t)q * (ntile + 1) + t];
+      g1 = off[(int64_t)q * (ntile + 1) + t + 1];
+      s_b[q] = g0;
     }
     int len = (int)(g1 - g0), incl = len;
 #pragma unroll
     for (int d = 1; d < MRH_WAVE; d <<= 1) {
       const int y = __shfl_up(incl, d, MRH_WAVE);
-      if (r >= d) incl += y;
+      if (q >= d) incl += y;
     }
-    if (r < R) s_pre[r] = incl - len;
-    if (r == R - 1) s_pre[R] = incl;
+    if (q < R) s_pre[q] = incl - len;
+    if (q == R - 1) s_pre[R] = incl;
   }
   __syncthreads();
   const int total = s_pre[R];
   for (int j = threadIdx.x; j < total; j += NT) {
-    int lo = 0, hi = R - 1;  // the range holding flattened pair j: last r with s_pre[r] <= j
+    int lo = 0, hi = R - 1;  // the range holding flattened pair j: last range with s_pre <= j
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (s_pre[mid] <= j) lo = mid;
@@ -247,11 +267,49 @@ __global__ __launch_bounds__(NT) void k_pr_tile_combine(const float* __restrict_
     atomicAdd(&sum[d], (unsigned long long)(long long)((double)send[g] * 0x1p62));
   }
   __syncthreads();
+  const float dterm = (float)(dmass[0] * invN);
+  double dd = 0.0, dm = 0.0;
   const int64_t nd = ndst - d0 < TILE ? ndst - d0 : TILE;
-  for (int i = threadIdx.x; i < nd; i += NT) {
-    const unsigned long long v = sum[i];
-    // untouched destinations keep acc == 0 (pr_update leaves it zeroed)
-    if (v) acc[nid[d0 + i]] = (float)((double)(long long)v * 0x1p-62);
+  if (nd == TILE) {  // full tile: 16-byte accesses (d0 is a multiple of TILE)
+    for (int q = threadIdx.x; q < TILE / 4; q += NT) {
+      const int64_t v4 = (d0 >> 2) + q;
+      const float4 rv = reinterpret_cast<const float4*>(r)[v4];
+      const float4 ig = reinterpret_cast<const float4*>(invdeg)[v4];
+      const uint32_t dg = reinterpret_cast<const uint32_t*>(dangling)[v4];
+      float4 x, c;
+      pr_one(fx_to_f(sum[4 * q]), rv.x, ig.x, dg & 0xffu, base, alpha, dterm, x.x, c.x, dd, dm);
+      pr_one(fx_to_f(sum[4 * q + 1]), rv.y, ig.y, (dg >> 8) & 0xffu, base, alpha, dterm, x.y, c.y, dd, dm);
+      pr_one(fx_to_f(sum[4 * q + 2]), rv.z, ig.z, (dg >> 16) & 0xffu, base, alpha, dterm, x.z, c.z, dd, dm);
+      pr_one(fx_to_f(sum[4 * q + 3]), rv.w, ig.w, dg >> 24, base, alpha, dterm, x.w, c.w, dd, dm);
+      reinterpret_cast<float4*>(rn)[v4] = x;
+      reinterpret_cast<float4*>(cout)[v4] = c;
+    }
+  } else {
+    for (int i = threadIdx.x; i < nd; i += NT) {
+      const int64_t v = d0 + i;
+      float x, c;
+      pr_one(fx_to_f(sum[i]), r[v], invdeg[v], dangling[v] != 0, base, alpha, dterm, x, c, dd, dm);
+      rn[v] = x;
+      cout[v] = c;
+    }
+  }
+  for (int o = MRH_WAVE / 2; o > 0; o >>= 1) {
+    dd += __shfl_xor(dd, o, MRH_WAVE);
+    dm += __shfl_xor(dm, o, MRH_WAVE);
+  }
+  if (dev::lane_id() == 0) {
+    sh[0][dev::wave_id()] = dd;
+    sh[1][dev::wave_id()] = dm;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0, b = 0;
+    for (int w = 0; w < NT / MRH_WAVE; ++w) {
+      a += sh[0][w];
+      b += sh[1][w];
+    }
+    partial[2 * t] = a;
+    partial[2 * t + 1] = b;
   }
 }
 
@@ -272,14 +330,6 @@ __global__ __launch_bounds__(NT) void k_scatter_f32(const float* __restrict__ v,
 // one u32), plus the L1 delta and the dangling mass as fp64 block partials.
 // acc is zeroed behind its read, so the next iteration's combine starts
 // from a clean array without a separate fill pass.
-__device__ __forceinline__ void pr_one(float a, float rv, float idg, bool dg, float base, float alpha, float dterm,
-                                       float& x, float& c, double& d, double& dm) {
-  x = base + alpha * (a + dterm);
-  c = x * idg;
-  d += fabs((double)x - (double)rv);
-  if (dg) dm += x;
-}
-
 __global__ __launch_bounds__(NT) void k_pr_update(float* __restrict__ acc, const float* __restrict__ r,
                                                  float* __restrict__ rn, const uint8_t* __restrict__ dangling,
                                                  int64_t n, float base, float alpha,
@@ -591,11 +641,16 @@ void pr_range_offsets(const int64_t* hi, int64_t ngrp, int dbits, int R, int64_t
                      off);
   MRH_CHECK_LAUNCH();
 }
-void pr_tile_combine(const float* send, const int32_t* ghi, const int64_t* off, int R, int64_t ntile, const int32_t* nid,
-                     int64_t ndst, float* acc, hipStream_t s) {
+void pr_tile_step(const float* send, const int32_t* ghi, const int64_t* off, int R, int64_t ntile, int64_t ndst,
+                  const float* r, float* rn, const uint8_t* dangling, float base, float alpha, const double* dmass,
+                  double invN, const float* invdeg, float* cout, double* partial, hipStream_t s) {
   if (ntile <= 0) return;
-  check_arg(R >= 1 && R <= PR_MAX_RANGES, "pr_tile_combine: 1 <= R <= 64 source ranges");
-  hipLaunchKernelGGL(k_pr_tile_combine, dim3((unsigned)ntile), dim3(NT), 0, s, send, ghi, off, R, ntile, nid, ndst, acc);
+  check_arg(R >= 1 && R <= PR_MAX_RANGES, "pr_tile_step: 1 <= R <= 64 source ranges");
+  check_arg(ntile == (ndst + (1 << PR_TILE_BITS) - 1) >> PR_TILE_BITS, "pr_tile_step: ntile must cover ndst");
+  check_arg(((uintptr_t)r | (uintptr_t)rn | (uintptr_t)invdeg | (uintptr_t)cout) % 16 == 0 && (uintptr_t)dangling % 4 == 0,
+            "pr_tile_step: 16-byte aligned float columns, 4-byte aligned dangling flags");
+  hipLaunchKernelGGL(k_pr_tile_step, dim3((unsigned)ntile), dim3(NT), 0, s, send, ghi, off, R, ntile, ndst, r, rn,
+                     dangling, base, alpha, dmass, invN, invdeg, cout, partial);
   MRH_CHECK_LAUNCH();
 }
 

@@ -209,8 +209,12 @@ void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int64_t d
 // every (range, tile) (R * (ntile + 1) int64); the tiled partial-sum combine
 int pr_tile_bits();
 void pr_range_offsets(const int64_t* hi, int64_t ngrp, int dbits, int R, int64_t ntile, int64_t* off, hipStream_t s);
-void pr_tile_combine(const float* send, const int32_t* ghi, const int64_t* off, int R, int64_t ntile, const int32_t* nid,
-                     int64_t ndst, float* acc, hipStream_t s);
+// one step's combine + update per tile of destinations (new ids): partial
+// sums -> r_new, c = r_new / outdeg, per-tile (L1 delta, dangling mass)
+// partials (2 * ntile doubles)
+void pr_tile_step(const float* send, const int32_t* ghi, const int64_t* off, int R, int64_t ntile, int64_t ndst,
+                  const float* r, float* rn, const uint8_t* dangling, float base, float alpha, const double* dmass,
+                  double invN, const float* invdeg, float* cout, double* partial, hipStream_t s);
 void pr_update(float* acc, const float* r, float* rn, const uint8_t* dangling, int64_t n, float base,
                float alpha, const double* dmass, double invN, const float* invdeg, float* cout, double* partial,
                hipStream_t s);
