@@ -17,6 +17,7 @@
 #include "kv.h"
 #include "graphplan.h"
 #include "guardalloc.h"
+#include "hbmpool.h"
 #include "kernels/launch.h"
 #include "mapreduce.h"
 #include "tri.h"
@@ -488,6 +489,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("to_var_keys", &to_var_keys);
   m.def("to_var_values", &to_var_values);
   m.def("exclusive_scan", &exclusive_scan);
+  // HBM page pool (hbmpool.h): the engine's device allocator with a hard cap
+  m.def("hbm_pool_install", &hbm::install);
+  m.def("hbm_pool_installed", &hbm::installed);
+  m.def("hbm_pool_stats", [](int dev) {
+    const hbm::PoolStats s = hbm::stats(dev);
+    py::dict d;
+    d["in_use"] = s.in_use;
+    d["peak"] = s.peak;
+    d["reserved"] = s.reserved;
+    d["cap"] = s.cap;
+    d["allocs"] = s.allocs;
+    d["frees"] = s.frees;
+    d["failures"] = s.failures;
+    return d;
+  });
+  m.def("hbm_pool_reset_peak", &hbm::reset_peak);
+  m.def("hbm_pool_set_cap", &hbm::set_cap);
+  m.def("hbm_pool_trim", &hbm::trim, py::call_guard<py::gil_scoped_release>());
   // MRH_GUARD device bounds-check mode (guardalloc.h)
   m.def("install_alloc_guard", &guard::install_alloc_guard);
   m.def("alloc_guard_active", &guard::alloc_guard_active);

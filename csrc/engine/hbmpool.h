@@ -1,0 +1,61 @@
+// HBM page pool: the engine's own device allocator (SURVEY.md §7.2 "page pool
+// (mem_request...) -> HbmPool"), the MI355X-side counterpart of the
+// reference's page pool (src/mapreduce.cpp:3318-3547: memsize pages, capped by
+// maxpage, freed per op with freepage, hi-water stats).
+//
+// When installed (MRH_HBM_POOL=1 before the first device allocation, or
+// gpu_mapreduce_amd.hbm_pool.install()), every device allocation of the
+// process — engine arenas, kernel scratch, ATen temporaries — comes from a
+// per-device stream-ordered HIP memory pool (hipMallocFromPoolAsync /
+// hipFreeAsync) instead of the ATen caching allocator:
+//  * stream order: a block freed on stream s is reusable by later work on s
+//    at once; blocks used on other streams (record_stream) are freed only
+//    behind an event of each of those streams;
+//  * hard cap: bytes in use never exceed the cap; an allocation past it fails
+//    with a c10::OutOfMemoryError naming the cap ("Cannot allocate page"), the
+//    reference's behaviour when maxpage pages are taken. MapReduce ops with a
+//    page budget B (maxpage x memsize, or hbm_budget) run under a cap of
+//    (bytes in use at op entry) + 2B (output plus working set);
+//  * freepage: trim() returns the pool's cached free memory to the driver;
+//  * stats: bytes in use, hi-water mark, reserved bytes, counts.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mrh::hbm {
+
+struct PoolStats {
+  int64_t in_use = 0;    // bytes of live allocations (512-byte granules)
+  int64_t peak = 0;      // hi-water mark of in_use since the last reset_peak
+  int64_t reserved = 0;  // bytes the HIP pool holds from the driver
+  int64_t cap = 0;       // hard cap on in_use (0: none)
+  int64_t allocs = 0, frees = 0, failures = 0;
+};
+
+// make the pool the process's device allocator; false (and no change) if the
+// current allocator has already been initialised by a device allocation
+bool install();
+bool installed();
+PoolStats stats(int device);
+void reset_peak(int device);
+// set the hard cap on bytes in use (0 = none); returns the previous cap
+int64_t set_cap(int device, int64_t cap);
+// release cached free memory of the pool down to keep_bytes
+void trim(int device, int64_t keep_bytes);
+
+// RAII: a MapReduce op's cap (in use at entry + extra bytes), restored on exit
+class OpCap {
+ public:
+  OpCap(int device, int64_t extra);
+  ~OpCap();
+  OpCap(const OpCap&) = delete;
+  OpCap& operator=(const OpCap&) = delete;
+
+ private:
+  int dev_ = -1;
+  int64_t prev_ = 0;
+  bool on_ = false;
+};
+
+}  // namespace mrh::hbm

@@ -2,6 +2,7 @@
 // method as src/mapreduce.cpp:<lines>.
 #include "mapreduce.h"
 #include "guard.h"
+#include "hbmpool.h"
 #include "grouper.h"
 #include "guardalloc.h"
 #include "ooc.h"
@@ -20,6 +21,7 @@
 #include <filesystem>
 #include <fstream>
 #include <numeric>
+#include <optional>
 #include <sstream>
 #include <stdexcept>
 
@@ -57,6 +59,11 @@ struct OpTrace {
   OpTrace(const char* name, MapReduce* mr) : mr_(mr), name_(name) {
     roctxRangePushA(name);
     if (g_op_depth == 0) guard::set_current_op(name);
+    // page pool installed + a page budget B: the op may hold at most 2B of
+    // new device memory (output + working set); past it an allocation fails
+    // with "Cannot allocate page" (reference mem_request at maxpage)
+    if (g_op_depth == 0 && hbm::installed() && mr->device().is_cuda() && mr->budget() > 0)
+      cap_.emplace(mr->device().index() < 0 ? 0 : mr->device().index(), 2 * mr->budget());
     if (guard::trace_enabled()) {
       device_sync(mr);
       t0_ = Comm::wtime();
@@ -108,6 +115,7 @@ struct OpTrace {
   const char* name_;
   double t0_ = 0;
   int64_t s0_ = 0, r0_ = 0;
+  std::optional<hbm::OpCap> cap_;
 };
 
 [[noreturn]] void fail(const std::string& m) { throw std::runtime_error(m); }
@@ -1356,6 +1364,13 @@ void MapReduce::cummulative_stats(int level, int reset) {  // :3007-3066
   }
   std::vector<int64_t> io = comm_->allreduce({rsize.load(), wsize.load()}, Comm::SUM);
   if ((io[0] || io[1]) && me == 0) out(fmt("Cummulative I/O = %.3g Mb read, %.3g Mb write\n", io[0] / mb, io[1] / mb));
+  if (hbm::installed() && device().is_cuda()) {  // the page pool's hi-water mark (reference hiwater())
+    const hbm::PoolStats ps = hbm::stats(device().index() < 0 ? 0 : device().index());
+    const int64_t hp = comm_->allreduce(ps.peak, Comm::MAX);
+    if (me == 0)
+      out(fmt("HBM page pool: hi-water %.3g Mb any proc, %.3g Mb in use, %.3g Mb reserved, %lld failed requests\n",
+              hp / mb, ps.in_use / mb, ps.reserved / mb, (long long)ps.failures));
+  }
   if (reset) rsize = wsize = cssize = crsize = 0;
 }
 

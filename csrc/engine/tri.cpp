@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "../kernels/launch.h"
 #include "kv.h"
@@ -165,6 +166,52 @@ static int64_t tri_core_count(const at::Tensor& rowptr, const at::Tensor& col, i
   return tot.item<int64_t>();
 }
 
+// hub-row kernel (MRH_TRI_HUB_KERNEL): "bitmap" (default; AND/popcount of
+// bitmap rows), "pull" (rows grouped by the middle vertex, streamed row tails
+// against an LDS table of N+(v): 40 G element tests on RMAT-24, 364 ms vs
+// 231 ms, profiles/r3_trifind_pull.txt) or "lds" (LDS bitmap of N+(u),
+// streamed N+(v))
+static int tri_hub_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("MRH_TRI_HUB_KERNEL");
+    if (e && std::string(e) == "pull") return 0;
+    if (!e || !*e || std::string(e) == "bitmap" || std::string(e) == "lds") return 1;  // tri_hub_count picks
+    throw std::runtime_error("MRH_TRI_HUB_KERNEL must be pull, bitmap or lds");
+  }();
+  return m;
+}
+
+// the hub rows [ua, ub) counted v-major (tri.hip k_tri_hub_pull): their edges
+// sorted by destination give every hub v its in-edges (u, v); each in-edge's
+// row tail past v is streamed against N+(v)
+static void tri_hub_pull_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t hb,
+                               int64_t K, int64_t ua, int64_t ub, const at::Tensor& H, at::Tensor& tot) {
+  if (ub <= ua || K <= 0) return;
+  const at::Device dev = rowptr.device();
+  const hipStream_t s = cur();
+  const int64_t ea = rowptr[ua].item<int64_t>(), n = rowptr[ub].item<int64_t>() - ea;
+  if (n <= 0) return;
+  at::Tensor tk = at::empty({n}, opt(dev, at::kLong));
+  at::Tensor endx = at::empty({n}, opt(dev, at::kInt));
+  k::tri_hub_pull_prep(P0<uint32_t>(col), P0<uint64_t>(okeys), P0<int64_t>(rowptr), hb, ea, n, P0<uint64_t>(tk),
+                       P0<uint32_t>(endx), s);
+  int kb = 1;
+  while ((int64_t(1) << kb) < K) ++kb;
+  at::Tensor tks = radix_sort_keys(tk, 32, 32 + kb);  // keys-only: the edge index rides in the low word
+  tk = at::Tensor();
+  at::Tensor tptr = at::empty({K + 1}, opt(dev, at::kLong));
+  k::tri_rowptr(P0<uint64_t>(tks), n, K, P0<int64_t>(tptr), s);
+  at::Tensor np = at::empty({K}, opt(dev, at::kLong));
+  k::tri_hub_pull_npieces(P0<int64_t>(tptr), P0<int64_t>(rowptr), hb, K, P0<int64_t>(np), s);
+  at::Tensor off = exclusive_scan(np).to(at::kLong).contiguous();  // K + 1 entries, off[K] = item count
+  const int64_t cap = k::tri_hub_pull_max_items(n, K);
+  at::Tensor items = at::empty({cap}, opt(dev, at::kLong)), big = at::empty({cap}, opt(dev, at::kLong));
+  at::Tensor nbig = at::empty({1}, opt(dev, at::kInt));
+  k::tri_hub_pull(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, ea, P0<uint64_t>(tks), P0<int64_t>(tptr),
+                  P0<uint32_t>(endx), P0<int64_t>(off), P0<uint64_t>(items), P0<uint64_t>(big), P0<unsigned int>(nbig),
+                  P0<uint64_t>(H), P0<unsigned long long>(tot), s);
+}
+
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1) {
   e1 = std::min<int64_t>(e1, okeys.numel());
   if (e1 <= e0) return 0;
@@ -186,8 +233,12 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
     if (K) {
       // the bitmaps serve both the hub kernel and the hub probes of the hash kernels
       H = at::empty({K * (K / 64)}, opt(okeys.device(), at::kLong));
-      k::tri_hub_count(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, std::max(u0, hb),
-                       std::max(std::min(u1, cb), hb), P0<uint64_t>(H), P0<unsigned long long>(tot), cur());
+      const int64_t ua = std::max(u0, hb), ub = std::max(std::min(u1, cb), hb);
+      const bool pull = tri_hub_mode() == 0;
+      // pull: tri_hub_count only builds the bitmaps (an empty row range)
+      k::tri_hub_count(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, ua, pull ? ua : ub, P0<uint64_t>(H),
+                       P0<unsigned long long>(tot), cur());
+      if (pull) tri_hub_pull_count(rowptr, col, okeys, hb, K, ua, ub, H, tot);
     }
     int64_t ncore = 0;
     if (T && u1 > cb) ncore = tri_core_count(rowptr, col, cb, T, std::max(u0, cb), u1);

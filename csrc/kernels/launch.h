@@ -271,6 +271,18 @@ void tri_count_hash(const int64_t* rowptr, const uint32_t* col, int64_t u0, int6
 // triangles whose lowest vertex is a hub (rank >= hb = nvert - K) among the
 // vertices [u0, u1), by AND/popcount of hub adjacency bitmaps; H: scratch of
 // K * K / 8 bytes (K a multiple of 64, <= 524288)
+// hub rows grouped by the middle vertex v (tri.hip "pull"): prep packs the
+// hub edges [ea, ea + n) as (v - hb) << 32 | (e - ea) and the end of every
+// edge's source row; after the keys-only sort (tks) and tptr (first item of
+// every v, K + 1), npieces -> exclusive scan off (K + 1) -> tri_hub_pull
+void tri_hub_pull_prep(const uint32_t* col, const uint64_t* okeys, const int64_t* rowptr, int64_t hb, int64_t ea,
+                       int64_t n, uint64_t* tk, uint32_t* endx, hipStream_t s);
+void tri_hub_pull_npieces(const int64_t* tptr, const int64_t* rowptr, int64_t hb, int64_t K, int64_t* np,
+                          hipStream_t s);
+int64_t tri_hub_pull_max_items(int64_t n, int64_t K);
+void tri_hub_pull(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64_t K, int64_t ea, const uint64_t* tks,
+                  const int64_t* tptr, const uint32_t* endx, const int64_t* off, uint64_t* items, uint64_t* big,
+                  unsigned int* nbig, const uint64_t* H, unsigned long long* total, hipStream_t s);
 void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64_t K, int64_t u0, int64_t u1,
                    uint64_t* H, unsigned long long* total, hipStream_t s);
 // ---------------------------------------------------------------- ccmr.hip

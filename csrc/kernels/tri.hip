@@ -412,10 +412,15 @@ __global__ __launch_bounds__(HUB_NT) void k_tri_hub_count(const int64_t* __restr
                                                          int64_t r0, int64_t r1,
                                                          const unsigned long long* __restrict__ H,
                                                          unsigned long long* __restrict__ total) {
+  constexpr int NWV = HUB_NT / MRH_WAVE;
   __shared__ int s_scan[HUB_NT / MRH_WAVE + 1];
   __shared__ int32_t s_idx[HUB_LIST];
   __shared__ unsigned long long s_val[HUB_LIST];
+  __shared__ int s_jw[WPT * NWV + 1];          // non-zero words per (register j, wave), then their offsets
+  __shared__ int s_vr[HUB_NT], s_lb[HUB_NT], s_off[HUB_NT + 1];
   const int64_t W = K / 64;
+  const int wv = dev::wave_id(), ln = dev::lane_id();
+  const uint64_t lt = dev::lanemask_lt();
   uint64_t cnt = 0;
   for (int64_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
     const int64_t u = hb + r;
@@ -428,42 +433,92 @@ __global__ __launch_bounds__(HUB_NT) void k_tri_hub_count(const int64_t* __restr
       const int64_t w = threadIdx.x + (int64_t)j * HUB_NT;
       mine[j] = w < W ? hu[w] : 0ull;
     }
-    // sparse rows (the lower hubs: few of W words set) compact their
-    // non-zero words into LDS and AND only those against each H[v]: d+(u) x
-    // nnz word loads instead of d+(u) x W
-    int nz = 0;
+    // the row's non-zero words in ascending word order (word = j * HUB_NT +
+    // thread, i.e. (j, wave, lane) order): per-(j, wave) ballot counts, one
+    // scan over them, then every thread places its words
 #pragma unroll
-    for (int j = 0; j < WPT; ++j) nz += mine[j] != 0ull;
-    int total_nz;
-    const int base = dev::block_excl_scan<int, HUB_NT>(nz, s_scan, &total_nz);
+    for (int j = 0; j < WPT; ++j) {
+      const uint64_t bm = __ballot(mine[j] != 0ull);
+      if (ln == 0) s_jw[j * NWV + wv] = __popcll(bm);
+    }
+    __syncthreads();
+    if (threadIdx.x < MRH_WAVE) {  // exclusive scan of the WPT * NWV (<= 128) counts, two per lane
+      const int i0 = 2 * ln, i1 = 2 * ln + 1;
+      const int x0 = i0 < WPT * NWV ? s_jw[i0] : 0, x1 = i1 < WPT * NWV ? s_jw[i1] : 0;
+      const int incl = dev::wave_incl_scan(x0 + x1);
+      if (i0 < WPT * NWV) s_jw[i0] = incl - x0 - x1;
+      if (i1 < WPT * NWV) s_jw[i1] = incl - x1;
+      if (ln == MRH_WAVE - 1) s_jw[WPT * NWV] = incl;
+    }
+    __syncthreads();
+    const int total_nz = s_jw[WPT * NWV];
+    // sparse rows (the lower hubs: few of W words set) AND only their
+    // non-zero words against each H[v]: d+(u) x nnz word loads instead of
+    // d+(u) x W, and only the words at or above v's own column (H[v] has no
+    // bits below it): with the words sorted, each edge's valid words are a
+    // suffix [lb, nz), and the (edge, word) pairs of 256 edges at a time are
+    // flattened over the block — every lane loads a word that can match
     if ((int64_t)total_nz * HUB_SPARSE < W && total_nz <= HUB_LIST) {
-      int o = base;
 #pragma unroll
-      for (int j = 0; j < WPT; ++j)
+      for (int j = 0; j < WPT; ++j) {
+        const uint64_t bm = __ballot(mine[j] != 0ull);
         if (mine[j]) {
+          const int o = s_jw[j * NWV + wv] + __popcll(bm & lt);
           s_idx[o] = (int32_t)(threadIdx.x + j * HUB_NT);
           s_val[o] = mine[j];
-          ++o;
-        }
-      __syncthreads();
-      // pair t = (edge t / nz, word t % nz), t = threadIdx.x + k * HUB_NT:
-      // both advance by a constant per step (one division per row, none per
-      // pair: the 64-bit div/mod per pair dominated this loop)
-      const uint32_t nzu = (uint32_t)total_nz;
-      const uint32_t de = HUB_NT / nzu, dl = HUB_NT % nzu;
-      int64_t e = a + threadIdx.x / nzu;
-      uint32_t li = threadIdx.x % nzu;
-      while (e < b) {
-        const int64_t vr = (int64_t)col[e] - hb, w = s_idx[li];
-        if (w >= (vr >> 6)) cnt += __popcll(s_val[li] & H[vr * W + w]);
-        e += de;
-        li += dl;
-        if (li >= nzu) {
-          li -= nzu;
-          ++e;
         }
       }
       __syncthreads();
+      const int nz = total_nz;
+      for (int64_t eb = a; eb < b; eb += HUB_NT) {
+        const int64_t e = eb + threadIdx.x;
+        int c = 0, vr = 0, lb = 0;
+        if (e < b) {
+          vr = (int)((int64_t)col[e] - hb);
+          const int w0 = vr >> 6;
+          int lo = 0, hi = nz;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_idx[mid] < w0) lo = mid + 1;
+            else hi = mid;
+          }
+          lb = lo;
+          c = nz - lo;
+        }
+        int tot;
+        const int off = dev::block_excl_scan<int, HUB_NT>(c, s_scan, &tot);
+        s_vr[threadIdx.x] = vr;
+        s_lb[threadIdx.x] = lb;
+        s_off[threadIdx.x] = off;
+        if (threadIdx.x == 0) s_off[HUB_NT] = tot;
+        __syncthreads();
+        // pair p = (edge j, word s_lb[j] + p - s_off[j]); a thread's pairs
+        // are HUB_NT apart, so its edge index only moves forward; four pairs
+        // per trip keep four independent loads of H in flight
+        int j = 0;
+        for (int p = threadIdx.x; p < tot; p += 4 * HUB_NT) {
+          int64_t addr[4];
+          unsigned long long mv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int q = p + k * HUB_NT;
+            addr[k] = -1;
+            mv[k] = 0ull;
+            if (q < tot) {
+              while (s_off[j + 1] <= q) ++j;
+              const int li = s_lb[j] + (q - s_off[j]);
+              addr[k] = (int64_t)s_vr[j] * W + s_idx[li];
+              mv[k] = s_val[li];
+            }
+          }
+          unsigned long long hv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) hv[k] = addr[k] >= 0 ? H[addr[k]] : 0ull;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) cnt += __popcll(mv[k] & hv[k]);
+        }
+        __syncthreads();
+      }
       continue;
     }
     for (int64_t e = a; e < b; ++e) {
@@ -557,6 +612,188 @@ __global__ __launch_bounds__(HUBL_NT) void k_tri_hub_lds(const int64_t* __restri
   }
   cnt = dev::wave_sum(cnt);
   if (lane == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
+}
+
+// ---------------------------------------------------------------- hub rows, v-major ("pull")
+// The hub rows counted grouped by the MIDDLE vertex v instead of the low
+// vertex u: every hub edge (u, v) contributes |N+(u) ∩ N+(v)|, and the
+// candidates w are the elements of N+(u) after v (rows are sorted). Grouped by
+// v, one wave (or block) holds N+(v) in an LDS hash table and streams, for
+// every in-edge (u, v), the tail of u's row past v — coalesced 4-byte reads of
+// the CSR column array, each tested in LDS — so the bitmap kernel's d+(u) x
+// nnz(H[u]) scattered 8-byte loads of other hubs' bitmap rows (3.9 G L2
+// misses on RMAT-24, profiles/r3_trifind_pmc.txt) become streaming reads plus
+// LDS probes. The in-edges of v are the hub edges sorted by destination
+// (keys-only radix sort of (v - hb) << 32 | edge index); a hub with many
+// in-edges is cut into pieces of PULL_PIECE in-edges (each piece rebuilds the
+// small table of N+(v)), so the top hubs do not serialise on one wave.
+constexpr int64_t PULL_PIECE = 2048;
+
+__global__ __launch_bounds__(NT) void k_tri_tpack(const uint32_t* __restrict__ col, int64_t ea, int64_t n, int64_t hb,
+                                                 uint64_t* __restrict__ tk) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+    tk[i] = ((uint64_t)((int64_t)col[ea + i] - hb) << 32) | (uint64_t)i;
+}
+
+// endx[i] = end of the row of edge ea + i's source, relative to ea
+__global__ __launch_bounds__(NT) void k_tri_hub_end(const uint64_t* __restrict__ okeys,
+                                                   const int64_t* __restrict__ rowptr, int64_t ea, int64_t n,
+                                                   uint32_t* __restrict__ endx) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+    endx[i] = (uint32_t)(rowptr[(int64_t)(okeys[ea + i] >> 32) + 1] - ea);
+}
+
+// pieces per hub v: ceil(in-edges / PULL_PIECE), none when N+(v) is empty
+__global__ __launch_bounds__(NT) void k_tri_pull_npieces(const int64_t* __restrict__ tptr,
+                                                        const int64_t* __restrict__ rowptr, int64_t hb, int64_t K,
+                                                        int64_t* __restrict__ np) {
+  for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < K; r += (int64_t)gridDim.x * NT) {
+    const int64_t din = tptr[r + 1] - tptr[r], dout = rowptr[hb + r + 1] - rowptr[hb + r];
+    np[r] = (din > 0 && dout > 0) ? (din + PULL_PIECE - 1) / PULL_PIECE : 0;
+  }
+}
+
+// work items (r << 32 | piece) at the exclusive-scan offsets off
+__global__ __launch_bounds__(NT) void k_tri_pull_items(const int64_t* __restrict__ off, int64_t K,
+                                                      uint64_t* __restrict__ items) {
+  for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < K; r += (int64_t)gridDim.x * NT)
+    for (int64_t p = off[r]; p < off[r + 1]; ++p) items[p] = ((uint64_t)r << 32) | (uint64_t)(p - off[r]);
+}
+
+struct TabTest {
+  const uint32_t* tab;
+  uint32_t mask;
+  __device__ __forceinline__ bool operator()(uint32_t x) const { return tab_has(tab, mask, x); }
+};
+// N+(v) too long for an LDS table: its bitmap row in H
+struct RowTest {
+  const unsigned long long* row;
+  int64_t hb;
+  __device__ __forceinline__ bool operator()(uint32_t x) const {
+    const int64_t b = (int64_t)x - hb;
+    return (row[b >> 6] >> (b & 63)) & 1ull;
+  }
+};
+
+// one wave streams the row tails of in-edge items [c0, p1) (step cstep, 64 at
+// a time): item x = edge ea + x = (u, v), tail = col[ea + x + 1, ea + endx[x])
+// cut at max N+(v); every element is tested against N+(v)
+template <class Test>
+__device__ __forceinline__ uint64_t pull_chunks(const uint32_t* __restrict__ col, int64_t ea,
+                                                const uint64_t* __restrict__ tks, const uint32_t* __restrict__ endx,
+                                                int64_t c0, int64_t p1, int64_t cstep, const Test& test, uint32_t maxv,
+                                                int64_t* pre, int64_t* st) {
+  const int l = dev::lane_id();
+  uint64_t cnt = 0;
+  for (int64_t c = c0; c < p1; c += cstep) {
+    int64_t len = 0, vs = 0;
+    if (c + l < p1) {
+      const uint32_t x = (uint32_t)tks[c + l];
+      vs = ea + (int64_t)x + 1;
+      len = lower_bound(col, vs, ea + (int64_t)endx[x], maxv + 1u) - vs;
+    }
+    const int64_t inc = dev::wave_incl_scan(len);
+    const int64_t tot = __shfl(inc, MRH_WAVE - 1, MRH_WAVE);
+    pre[l + 1] = inc;
+    if (l == 0) pre[0] = 0;
+    st[l] = vs;
+    wave_sync();
+    int j = 0;
+    for (int64_t t = l; t < tot; t += 2 * MRH_WAVE) {
+      while (pre[j + 1] <= t) ++j;
+      const uint32_t x0 = col[st[j] + (t - pre[j])];
+      const int64_t t1 = t + MRH_WAVE;
+      uint32_t x1 = 0;
+      const bool has1 = t1 < tot;
+      if (has1) {
+        while (pre[j + 1] <= t1) ++j;
+        x1 = col[st[j] + (t1 - pre[j])];
+      }
+      cnt += test(x0) ? 1u : 0u;
+      if (has1) cnt += test(x1) ? 1u : 0u;
+    }
+    wave_sync();
+  }
+  return cnt;
+}
+
+template <int TWN>
+__global__ __launch_bounds__(NT) void k_tri_hub_pull(const int64_t* __restrict__ rowptr,
+                                                    const uint32_t* __restrict__ col, int64_t hb, int64_t ea,
+                                                    const uint64_t* __restrict__ tks, const int64_t* __restrict__ tptr,
+                                                    const uint32_t* __restrict__ endx,
+                                                    const uint64_t* __restrict__ items,
+                                                    const int64_t* __restrict__ nitems, uint64_t* __restrict__ big,
+                                                    unsigned int* __restrict__ nbig,
+                                                    unsigned long long* __restrict__ total) {
+  __shared__ uint32_t tab[HASH_NW][TWN];
+  __shared__ int64_t pre[HASH_NW][MRH_WAVE + 1];
+  __shared__ int64_t st[HASH_NW][MRH_WAVE];
+  const int w = dev::wave_id(), l = dev::lane_id();
+  uint64_t cnt = 0;
+  const int64_t nw = (int64_t)gridDim.x * HASH_NW, ni = *nitems;
+  for (int64_t it = (int64_t)blockIdx.x * HASH_NW + w; it < ni; it += nw) {
+    const uint64_t item = items[it];
+    const int64_t r = (int64_t)(item >> 32), piece = (int64_t)(uint32_t)item;
+    const int64_t a = rowptr[hb + r], b = rowptr[hb + r + 1], d = b - a;
+    if (d > TWN / 2) {
+      if (l == 0) big[atomicAdd(nbig, 1u)] = item;
+      continue;
+    }
+    uint32_t size = 64;
+    while (size < 2 * d) size <<= 1;
+    const uint32_t mask = size - 1;
+    for (uint32_t i = l; i < size; i += MRH_WAVE) tab[w][i] = EMPTY;
+    wave_sync();
+    for (int64_t i = a + l; i < b; i += MRH_WAVE) tab_insert(tab[w], mask, col[i]);
+    wave_sync();
+    const int64_t p0 = tptr[r] + piece * PULL_PIECE, p1 = tptr[r + 1] < p0 + PULL_PIECE ? tptr[r + 1] : p0 + PULL_PIECE;
+    cnt += pull_chunks(col, ea, tks, endx, p0, p1, MRH_WAVE, TabTest{tab[w], mask}, col[b - 1], pre[w], st[w]);
+  }
+  cnt = dev::wave_sum(cnt);
+  if (l == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
+}
+
+// one block per big item (N+(v) beyond the wave table): a 32768-slot LDS
+// table, or v's bitmap row in H when N+(v) is longer still
+__global__ __launch_bounds__(BIG_NT) void k_tri_hub_pull_big(const int64_t* __restrict__ rowptr,
+                                                            const uint32_t* __restrict__ col, int64_t hb, int64_t ea,
+                                                            const uint64_t* __restrict__ tks,
+                                                            const int64_t* __restrict__ tptr,
+                                                            const uint32_t* __restrict__ endx,
+                                                            const uint64_t* __restrict__ big,
+                                                            const unsigned int* __restrict__ nbig,
+                                                            const unsigned long long* __restrict__ H, int64_t W,
+                                                            unsigned long long* __restrict__ total) {
+  __shared__ uint32_t tab[BIG_TAB];
+  __shared__ int64_t pre[BIG_NT / MRH_WAVE][MRH_WAVE + 1];
+  __shared__ int64_t st[BIG_NT / MRH_WAVE][MRH_WAVE];
+  const int w = dev::wave_id(), l = dev::lane_id();
+  const unsigned int n = *nbig;
+  uint64_t cnt = 0;
+  for (unsigned int i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint64_t item = big[i];
+    const int64_t r = (int64_t)(item >> 32), piece = (int64_t)(uint32_t)item;
+    const int64_t a = rowptr[hb + r], b = rowptr[hb + r + 1], d = b - a;
+    const int64_t p0 = tptr[r] + piece * PULL_PIECE, p1 = tptr[r + 1] < p0 + PULL_PIECE ? tptr[r + 1] : p0 + PULL_PIECE;
+    const int64_t c0 = p0 + (int64_t)w * MRH_WAVE;
+    if (2 * d > BIG_TAB) {  // uniform over the block
+      cnt += pull_chunks(col, ea, tks, endx, c0, p1, (int64_t)BIG_NT, RowTest{H + r * W, hb}, col[b - 1], pre[w], st[w]);
+      __syncthreads();
+      continue;
+    }
+    uint32_t size = 64;
+    while (size < 2 * d) size <<= 1;
+    const uint32_t mask = size - 1;
+    for (uint32_t j = threadIdx.x; j < size; j += BIG_NT) tab[j] = EMPTY;
+    __syncthreads();
+    for (int64_t j = a + threadIdx.x; j < b; j += BIG_NT) tab_insert(tab, mask, col[j]);
+    __syncthreads();
+    cnt += pull_chunks(col, ea, tks, endx, c0, p1, (int64_t)BIG_NT, TabTest{tab, mask}, col[b - 1], pre[w], st[w]);
+    __syncthreads();
+  }
+  cnt = dev::wave_sum(cnt);
+  if (l == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
 }
 
 // rowptr[v] = first index of src v in the sorted oriented keys (rowptr[nvert] = m)
@@ -670,6 +907,41 @@ void tri_hub_count(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64
       hipLaunchKernelGGL(k_tri_hub_count<32>, dim3(grid), dim3(HUB_NT), 0, s, rowptr, col, hb, K, c0, c1, Hc, total);
     MRH_CHECK_LAUNCH();
   }
+}
+
+void tri_hub_pull_prep(const uint32_t* col, const uint64_t* okeys, const int64_t* rowptr, int64_t hb, int64_t ea,
+                       int64_t n, uint64_t* tk, uint32_t* endx, hipStream_t s) {
+  if (n <= 0) return;
+  check_arg(n < (int64_t(1) << 32), "tri_hub_pull: more than 2^32 hub edges on one rank");
+  hipLaunchKernelGGL(k_tri_tpack, dim3(grid_for(n)), dim3(NT), 0, s, col, ea, n, hb, tk);
+  MRH_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_tri_hub_end, dim3(grid_for(n)), dim3(NT), 0, s, okeys, rowptr, ea, n, endx);
+  MRH_CHECK_LAUNCH();
+}
+
+void tri_hub_pull_npieces(const int64_t* tptr, const int64_t* rowptr, int64_t hb, int64_t K, int64_t* np,
+                          hipStream_t s) {
+  if (K <= 0) return;
+  hipLaunchKernelGGL(k_tri_pull_npieces, dim3(grid_for(K)), dim3(NT), 0, s, tptr, rowptr, hb, K, np);
+  MRH_CHECK_LAUNCH();
+}
+
+int64_t tri_hub_pull_max_items(int64_t n, int64_t K) { return n / PULL_PIECE + K + 1; }
+
+void tri_hub_pull(const int64_t* rowptr, const uint32_t* col, int64_t hb, int64_t K, int64_t ea, const uint64_t* tks,
+                  const int64_t* tptr, const uint32_t* endx, const int64_t* off, uint64_t* items, uint64_t* big,
+                  unsigned int* nbig, const uint64_t* H, unsigned long long* total, hipStream_t s) {
+  if (K <= 0) return;
+  hipLaunchKernelGGL(k_tri_pull_items, dim3(grid_for(K)), dim3(NT), 0, s, off, K, items);
+  MRH_CHECK_LAUNCH();
+  MRH_HIP(hipMemsetAsync(nbig, 0, sizeof(unsigned int), s));
+  // off[K] = the item count, read on the device (no host round trip)
+  hipLaunchKernelGGL(k_tri_hub_pull<TW>, dim3(4096), dim3(NT), 0, s, rowptr, col, hb, ea, tks, tptr, endx,
+                     (const uint64_t*)items, off + K, big, nbig, total);
+  MRH_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_tri_hub_pull_big, dim3(512), dim3(BIG_NT), 0, s, rowptr, col, hb, ea, tks, tptr, endx,
+                     (const uint64_t*)big, (const unsigned int*)nbig, (const unsigned long long*)H, K / 64, total);
+  MRH_CHECK_LAUNCH();
 }
 
 void tri_core_build(const int64_t* rowptr, const uint32_t* col, int64_t cb, int64_t T, int8_t* A, hipStream_t s) {

@@ -29,6 +29,13 @@ C = _load()
 # (csrc/engine/guardalloc.h)
 if os.environ.get("MRH_GUARD", "0") not in ("", "0"):
     C.install_alloc_guard()
+# MRH_HBM_POOL=1: the engine's HBM page pool (csrc/engine/hbmpool.h) is the
+# device allocator — stream-ordered HIP memory pools with a hard cap that
+# MapReduce ops with a page budget (maxpage x memsize / hbm_budget) enforce
+elif os.environ.get("MRH_HBM_POOL", "0") not in ("", "0"):
+    if not C.hbm_pool_install():
+        raise RuntimeError("MRH_HBM_POOL=1: device memory was allocated before gpu_mapreduce_amd was imported; "
+                           "import it first so the page pool can become the device allocator")
 
 
 def so_path():

@@ -1,0 +1,111 @@
+"""HBM page pool (csrc/engine/hbmpool.h): the engine's device allocator with a
+hard cap (reference page pool, src/mapreduce.cpp:3318-3547).
+
+The pool must be installed before the process allocates device memory, so
+every GPU case runs in a child process with MRH_HBM_POOL=1."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _child(code, timeout=240):
+    env = dict(os.environ, PYTHONPATH=ROOT, MRH_HBM_POOL="1")
+    env.pop("MRH_GUARD", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def test_pool_stats_shape_cpu():
+    from gpu_mapreduce_amd.runtime import hbm_pool
+    s = hbm_pool.stats(0)
+    assert set(s) == {"in_use", "peak", "reserved", "cap", "allocs", "frees", "failures"}
+
+
+BASIC = r'''
+import torch
+import gpu_mapreduce_amd as g
+from gpu_mapreduce_amd.runtime import hbm_pool
+assert hbm_pool.installed()
+s0 = hbm_pool.stats(0)
+x = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+s1 = hbm_pool.stats(0)
+assert s1["in_use"] - s0["in_use"] >= 64 << 20, (s0, s1)
+# a block used on a side stream is freed behind that stream's work
+side = torch.cuda.Stream()
+y = torch.ones(1 << 24, device="cuda")
+with torch.cuda.stream(side):
+    z = y * 2
+y.record_stream(side)
+del y
+torch.cuda.synchronize()
+assert float(z.sum()) == 2.0 * (1 << 24)
+del x, z
+torch.cuda.synchronize()
+s2 = hbm_pool.stats(0)
+assert s2["in_use"] <= s0["in_use"] + 4096 and s2["peak"] >= s1["in_use"], (s0, s2)
+# an end-to-end job on pool memory, checked against the host oracle
+from gpu_mapreduce_amd.models.inverted_index import InvertedIndex, reference_inverted_index
+from gpu_mapreduce_amd.utils import synth
+files = synth.html_corpus(4 << 20, file_bytes=1 << 20, seed=3, nurl=3000, device="cuda")
+files = [(n, t.cpu().pin_memory()) for n, t in files]
+app = InvertedIndex(g.MapReduce(g.Comm(device="cuda")), files)
+app.run()
+got = {}
+for line in app.output_lines():
+    url, rest = line.split("\t")
+    got[url.encode()] = sorted(rest.split())
+assert got == reference_inverted_index(files)
+hbm_pool.trim(0)
+print("ok", hbm_pool.stats(0))
+'''
+
+CAP = r'''
+import torch
+import gpu_mapreduce_amd as g
+from gpu_mapreduce_amd import C
+from gpu_mapreduce_amd.runtime import hbm_pool
+comm = g.Comm(device="cuda")
+# hard cap: a tensor past it fails with the page-pool error
+hbm_pool.set_cap(hbm_pool.stats(0)["in_use"] + (8 << 20), 0)
+try:
+    torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    raise SystemExit("allocation past the cap succeeded")
+except torch.OutOfMemoryError as e:
+    assert "Cannot allocate page" in str(e), e
+hbm_pool.set_cap(0, 0)
+assert hbm_pool.stats(0)["failures"] >= 1
+# a MapReduce op under a page budget: clone() of 64 MiB with a 4 MiB budget
+# needs 64 MiB of new device memory > 2 x 4 MiB -> Cannot allocate page
+n = 8 << 20
+mr = g.MapReduce(comm)
+mr.memsize = -(1 << 20)  # 1 MiB pages
+mr.maxpage = 4
+k = torch.arange(n, dtype=torch.int64, device="cuda")
+mr.map(1, lambda itask, kv: kv.add_kv(C.make_kv(k, None, k, None, n, "cuda")))
+try:
+    mr.clone()
+    raise SystemExit("clone past the page budget succeeded")
+except Exception as e:
+    assert "Cannot allocate page" in str(e), e
+# the same budget large enough: the op runs, and the pool saw the peak
+mr.maxpage = 256
+mr.clone()
+assert mr.kmv.nkey == n
+print("ok", hbm_pool.stats(0))
+'''
+
+
+@pytest.mark.gpu
+def test_pool_basic_and_stream_order_gpu():
+    assert _child(BASIC).startswith("ok")
+
+
+@pytest.mark.gpu
+def test_pool_cap_and_page_budget_gpu():
+    assert _child(CAP).startswith("ok")

@@ -169,11 +169,17 @@ def test_gpu_hub_bitmap_split_matches_cpu():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     want = TriangleGraph(Comm(device="cpu"), _rmat(17, 16, 3)).count()
-    for hub, K, core in (("0", 0, None), (None, 4096, None), ("4096", 4096, None), ("65536", 65536, None),
-                         ("4096", 4096, "1024"), ("65536", 65536, "8192"), ("8192", 8192, "8192")):
+    for hub, K, core, kern in (("0", 0, None, None), (None, 4096, None, None), ("4096", 4096, None, None),
+                               ("65536", 65536, None, None), ("4096", 4096, "1024", None),
+                               ("65536", 65536, "8192", None), ("8192", 8192, "8192", None),
+                               (None, 4096, None, "pull"), ("65536", 65536, None, "pull"),
+                               ("65536", 65536, None, "lds")):
         env = dict(os.environ, PYTHONPATH=root)
         env.pop("MRH_TRI_HUB", None)
         env.pop("MRH_TRI_CORE", None)
+        env.pop("MRH_TRI_HUB_KERNEL", None)
+        if kern is not None:  # hub rows by the v-major pull / LDS-bitmap kernels instead of the bitmap kernel
+            env["MRH_TRI_HUB_KERNEL"] = kern
         if hub is not None:
             env["MRH_TRI_HUB"] = hub
         if core is not None:  # the top ranks of the hubs counted by the int8 GEMM
@@ -182,4 +188,4 @@ def test_gpu_hub_bitmap_split_matches_cpu():
                            timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         k, n = map(int, r.stdout.split())
-        assert (k == K if hub is not None else 0 < k <= K and k % 64 == 0) and n == want, (hub, core, k, n, want)
+        assert (k == K if hub is not None else 0 < k <= K and k % 64 == 0) and n == want, (hub, core, kern, k, n, want)
