@@ -726,13 +726,28 @@ TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : c
   if (nv < 0) nv = comm->allreduce(hi.numel() ? hi.max().item<int64_t>() : -1, Comm::MAX) + 1;
   nvert = nv;
   if (nvert >= (int64_t(1) << 31)) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^31");
+  // MRH_TRI_REPLICATED=1 / 0 forces the replicated / distributed build; by
+  // default a GPU job replicates the graph when the whole edge list's build
+  // (~48 bytes per edge: packed copies, two sorts, CSR) takes under a quarter
+  // of the free HBM (RMAT-24: 13 GB of 288 GB) — every rank then runs the hub
+  // bitmap kernels on the full graph; larger graphs and CPU jobs keep the
+  // O(E/P + halo) distributed build
   const char* rep = std::getenv("MRH_TRI_REPLICATED");
-  if (comm->distributed() && !(rep && *rep == '1')) {
+  bool replicate = !comm->distributed() || (rep && *rep == '1');
+  if (comm->distributed() && !(rep && *rep)) {
+    const int64_t mall = comm->allreduce(lo.numel(), Comm::SUM);
+    size_t free_b = 0, total_b = 0;
+    int fits = 0;
+    if (dev.is_cuda() && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+      fits = (double)mall * 48.0 < (double)free_b / 4.0 ? 1 : 0;
+    replicate = comm->allreduce((int64_t)fits, Comm::MIN) == 1;  // every rank must take the same path
+  }
+  if (!replicate) {
     build_distributed(lo, hi);
     return;
   }
-  // replicated degree-oriented CSR (every rank holds the whole graph and
-  // counts a 1/P slice of its oriented edges)
+  // replicated degree-oriented CSR: every rank holds the whole graph and
+  // counts its share of the rows
   distributed = false;
   at::Tensor p = at::bitwise_or(at::bitwise_left_shift(lo, 32), hi).contiguous();
   if (comm->distributed()) p = comm->allgather_var(p);
@@ -740,8 +755,23 @@ TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : c
   nedge = uniq.numel();
   std::tie(rowptr, col, okeys, perm) = tri_prepare(uniq, std::max<int64_t>(nvert, 1));
   const int64_t m = okeys.numel(), P = comm->size(), me = comm->rank();
-  e0 = me * m / P;
-  e1 = (me + 1) * m / P;
+  e0 = 0;
+  e1 = m;
+  if (P > 1 && m > 0) {
+    // the shares are cut at row boundaries by estimated work, d+(u)^2 + d+(u)
+    // per row (the wedges the hash and hub-bitmap kernels walk), not by edge
+    // count: the top-ranked rows hold most of the work in few edges
+    const int64_t nr = rowptr.numel() - 1;
+    at::Tensor d = rowptr.narrow(0, 1, nr) - rowptr.narrow(0, 0, nr);
+    at::Tensor cost = exclusive_scan((d * d + d).contiguous());  // nr + 1 entries
+    const int64_t total = cost[nr].item<int64_t>();
+    at::Tensor targets = at::tensor({total / P * me + (total % P) * me / P, total / P * (me + 1) + (total % P) * (me + 1) / P},
+                                    at::TensorOptions().dtype(at::kLong)).to(rowptr.device());
+    at::Tensor ub = at::searchsorted(cost, targets).clamp(0, nr);
+    at::Tensor eb = rowptr.index_select(0, ub).to(at::kCPU);
+    e0 = me == 0 ? 0 : eb[0].item<int64_t>();
+    e1 = me == P - 1 ? m : eb[1].item<int64_t>();
+  }
 }
 
 // Distributed build (reference tri_find shuffles every edge 4 times,
