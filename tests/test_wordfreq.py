@@ -107,3 +107,18 @@ def test_wordfreq_gpu_combiner_matches_plain():
     assert [c for _, c in a.top] == [c for _, c in b.top] == [c for _, c in top]
     ref = {w.decode(): c for w, c in top}
     assert all(ref.get(w, c) == c for w, c in a.top)
+
+
+@pytest.mark.gpu
+def test_wordfreq_gpu_job_pipeline_prefetch():
+    """three jobs as a pipeline (each copies the next job's first chunk behind
+    its own last one, ring slots continuing across jobs): every job's counts
+    equal the oracle"""
+    chunks = [synth.zipf_text(1_000_000, seed=10 + s).pin_memory() for s in range(4)]
+    total, uniq, top = _oracle(chunks, 10)
+    comm = g.Comm(device="cuda")
+    for s in range(3):
+        app = WordFreq(g.MapReduce(comm), chunks, ntop=10, prefetch_next=chunks if s < 2 else None)
+        n = app.run()
+        assert n == total and app.nunique == uniq
+        assert [c for _, c in app.top] == [c for _, c in top]
