@@ -89,7 +89,7 @@ class InvertedIndex:
         # one file maps; the PAD bytes past each file are read by the 16-byte
         # scan windows but never matched
         st = int(mr.streams)
-        self.nbuf = st if st > 0 else 2
+        self.nbuf = st if st > 0 else max(1, int(os.environ.get("MRH_II_BUFS", "2")))
         self.bufs = [pools.device_buffer(dev, maxlen + PAD, slot) for slot in range(self.nbuf if files else 0)]
         self.copy_stream = pools.stream(dev, "h2d") if self.is_cuda else None
         self.output = None
