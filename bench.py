@@ -388,6 +388,11 @@ def main():
                               steps=args.extra_steps, warmup=1))
     res.update(rrec)
     res["ranks_joined"] = comm.size
+    from gpu_mapreduce_amd.runtime import hbm_pool
+    res["device_allocator"] = "mrhip HBM page pool (csrc/engine/hbmpool.cpp)" if hbm_pool.installed() else "ATen caching allocator"
+    if hbm_pool.installed() and comm.is_cuda:
+        st = hbm_pool.stats(torch.device(comm.device).index or 0)
+        res["hbm_pool_peak_bytes"] = st["peak"]
     res["backend"] = {"torch.distributed": (comm.backend or "none (world size 1)") + " (host objects/scalars only)",
                       "engine_transport": rrec["engine_transport"]}
     out = {

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <map>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -17,18 +18,36 @@ namespace mrh::hbm {
 namespace {
 
 constexpr int kMaxDev = 64;
-constexpr int64_t kGranule = 512;
+
+// size classes: 512 B granules up to 4 KiB, then 8 classes per power of two
+// (at most 12.5 % rounding) — a freed block is reused by any later request
+// of its class on its stream
+int64_t class_bytes(size_t size) {
+  if (size <= 4096) return (int64_t)((size + 511) / 512 * 512);
+  int b = 64 - __builtin_clzll((unsigned long long)(size - 1));  // 2^b >= size > 2^(b-1)
+  const int64_t step = std::max<int64_t>(512, (int64_t(1) << (b - 1)) / 8);
+  return ((int64_t)size + step - 1) / step * step;
+}
 
 struct Block {
-  int64_t bytes = 0;  // accounted size (granules)
+  int64_t bytes = 0;
   int dev = 0;
   hipStream_t stream = nullptr;
   std::vector<hipStream_t> used_on;  // other streams that touched the block (record_stream)
 };
 
+// a freed block that other streams used: reusable once their events complete
+struct Pending {
+  void* p = nullptr;
+  Block b;
+  std::vector<hipEvent_t> evs;
+};
+
 struct Dev {
   hipMemPool_t pool = nullptr;
-  int64_t in_use = 0, peak = 0, cap = 0, allocs = 0, frees = 0, failures = 0;
+  int64_t in_use = 0, peak = 0, cap = 0, cached = 0, allocs = 0, frees = 0, failures = 0;
+  std::map<std::pair<hipStream_t, int64_t>, std::vector<void*>> free;  // (stream, class) -> cached blocks
+  std::vector<Pending> pending;
 };
 
 std::mutex g_mu;
@@ -36,7 +55,9 @@ Dev g_dev[kMaxDev];
 std::unordered_map<void*, Block> g_blocks;
 std::atomic<bool> g_installed{false};
 
-std::string mib(int64_t b) { return std::to_string(b >> 20) + " MiB"; }
+std::string mib(int64_t b) {
+  return b >= (int64_t(1) << 20) ? std::to_string(b >> 20) + " MiB" : std::to_string(b >> 10) + " KiB";
+}
 
 hipMemPool_t pool_of(int dev) {  // g_mu held
   Dev& d = g_dev[dev];
@@ -56,10 +77,56 @@ hipMemPool_t pool_of(int dev) {  // g_mu held
   return d.pool;
 }
 
+// pending blocks whose other-stream work is done go to their stream's cache
+void reap(Dev& d) {  // g_mu held
+  for (size_t i = 0; i < d.pending.size();) {
+    Pending& q = d.pending[i];
+    bool done = true;
+    for (hipEvent_t e : q.evs) {
+      const hipError_t r = hipEventQuery(e);
+      if (r == hipErrorNotReady) {
+        done = false;
+        break;
+      }
+      if (r != hipSuccess) (void)hipGetLastError();
+    }
+    if (!done) {
+      ++i;
+      continue;
+    }
+    for (hipEvent_t e : q.evs) (void)hipEventDestroy(e);
+    d.free[{q.b.stream, q.b.bytes}].push_back(q.p);
+    q = std::move(d.pending.back());
+    d.pending.pop_back();
+  }
+}
+
+// every cached block back to the HIP pool (then the pool can hand the memory
+// to any stream, or trim it to the driver)
+void release_cached(Dev& d) {  // g_mu held
+  for (Pending& q : d.pending) {
+    for (hipEvent_t e : q.evs) {
+      (void)hipStreamWaitEvent(q.b.stream, e, 0);
+      (void)hipEventDestroy(e);
+    }
+    d.free[{q.b.stream, q.b.bytes}].push_back(q.p);
+  }
+  d.pending.clear();
+  for (auto& [k, v] : d.free)
+    for (void* p : v)
+      if (hipFreeAsync(p, k.first) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipDeviceSynchronize();
+        (void)hipFreeAsync(p, nullptr);
+      }
+  d.free.clear();
+  d.cached = 0;
+}
+
 void* pool_alloc(size_t size, int dev, hipStream_t stream) {
   if (size == 0) return nullptr;
   TORCH_CHECK(dev >= 0 && dev < kMaxDev, "mrhip page pool: device index out of range");
-  const int64_t bytes = ((int64_t)size + kGranule - 1) / kGranule * kGranule;
+  const int64_t bytes = class_bytes(size);
   hipMemPool_t pool;
   {
     std::lock_guard<std::mutex> l(g_mu);
@@ -70,20 +137,36 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
                        " requested with ", mib(d.in_use), " in use of a cap of ", mib(d.cap),
                        " (maxpage x memsize / hbm_budget) on device ", dev);
     }
+    if (!d.pending.empty()) reap(d);
+    auto it = d.free.find({stream, bytes});
+    if (it != d.free.end() && !it->second.empty()) {  // stream-ordered reuse: no HIP call
+      void* p = it->second.back();
+      it->second.pop_back();
+      d.cached -= bytes;
+      d.in_use += bytes;
+      d.peak = std::max(d.peak, d.in_use);
+      ++d.allocs;
+      g_blocks[p] = Block{bytes, dev, stream, {}};
+      return p;
+    }
     pool = pool_of(dev);
     d.in_use += bytes;  // reserved before the call so concurrent allocations see it
     d.peak = std::max(d.peak, d.in_use);
     ++d.allocs;
   }
   void* p = nullptr;
-  hipError_t e = hipMallocFromPoolAsync(&p, size, pool, stream);
+  hipError_t e = hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream);
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    // cached free memory of the pool that this stream cannot reuse yet: give
-    // it back to the driver and retry once
-    (void)hipStreamSynchronize(stream);
+    // memory held in the caches or freed on other streams: give it all back
+    // to the pool / driver and retry once
+    {
+      std::lock_guard<std::mutex> l(g_mu);
+      release_cached(g_dev[dev]);
+    }
+    (void)hipDeviceSynchronize();
     (void)hipMemPoolTrimTo(pool, 0);
-    e = hipMallocFromPoolAsync(&p, size, pool, stream);
+    e = hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream);
     if (e != hipSuccess) (void)hipGetLastError();
   }
   std::lock_guard<std::mutex> l(g_mu);
@@ -99,37 +182,34 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
 
 void pool_free(void* ptr, size_t /*size*/, int /*dev*/, hipStream_t /*stream*/) {
   if (!ptr) return;
-  Block b;
-  {
-    std::lock_guard<std::mutex> l(g_mu);
-    auto it = g_blocks.find(ptr);
-    if (it == g_blocks.end()) return;  // not ours (cannot happen once installed)
-    b = std::move(it->second);
-    g_blocks.erase(it);
-    g_dev[b.dev].in_use -= b.bytes;
-    ++g_dev[b.dev].frees;
+  std::lock_guard<std::mutex> l(g_mu);
+  auto it = g_blocks.find(ptr);
+  if (it == g_blocks.end()) return;  // not ours (cannot happen once installed)
+  Block b = std::move(it->second);
+  g_blocks.erase(it);
+  Dev& d = g_dev[b.dev];
+  d.in_use -= b.bytes;
+  d.cached += b.bytes;
+  ++d.frees;
+  if (b.used_on.empty()) {
+    // later work on the allocating stream runs after every earlier use
+    d.free[{b.stream, b.bytes}].push_back(ptr);
+    return;
   }
-  // the block may only be reused after the work of every stream that used it:
-  // the allocating stream waits for an event of each of the others, then frees
+  // used on other streams too: reusable after an event of each of them
+  Pending q;
+  q.p = ptr;
   for (hipStream_t s : b.used_on) {
     hipEvent_t ev;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, s) != hipSuccess) {
       (void)hipGetLastError();
       (void)hipStreamSynchronize(s);
       continue;
     }
-    if (hipEventRecord(ev, s) != hipSuccess || hipStreamWaitEvent(b.stream, ev, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      (void)hipStreamSynchronize(s);
-    }
-    (void)hipEventDestroy(ev);
+    q.evs.push_back(ev);
   }
-  if (hipFreeAsync(ptr, b.stream) != hipSuccess) {
-    // the allocating stream is gone: order against the whole device instead
-    (void)hipGetLastError();
-    (void)hipDeviceSynchronize();
-    (void)hipFreeAsync(ptr, nullptr);
-  }
+  q.b = std::move(b);
+  d.pending.push_back(std::move(q));
 }
 
 void pool_record_stream(void* ptr, hipStream_t s) {
@@ -201,6 +281,7 @@ void trim(int device, int64_t keep_bytes) {
   {
     std::lock_guard<std::mutex> l(g_mu);
     p = g_dev[device].pool;
+    if (p) release_cached(g_dev[device]);
   }
   if (!p) return;
   // freed blocks are returned to the pool in stream order: let the device

@@ -15,7 +15,11 @@
 //    with a c10::OutOfMemoryError naming the cap ("Cannot allocate page"), the
 //    reference's behaviour when maxpage pages are taken. MapReduce ops with a
 //    page budget B (maxpage x memsize, or hbm_budget) run under a cap of
-//    (bytes in use at op entry) + 2B (output plus working set);
+//    (bytes in use at op entry) + 2B (output plus working set) + 16 MiB of
+//    kernel scratch;
+//  * size classes: 512-byte granules to 4 KiB, then 8 classes per power of
+//    two; a freed block stays cached for later requests of its class on its
+//    stream (no HIP call on that path) until trim();
 //  * freepage: trim() returns the pool's cached free memory to the driver;
 //  * stats: bytes in use, hi-water mark, reserved bytes, counts.
 #pragma once

@@ -60,10 +60,12 @@ struct OpTrace {
     roctxRangePushA(name);
     if (g_op_depth == 0) guard::set_current_op(name);
     // page pool installed + a page budget B: the op may hold at most 2B of
-    // new device memory (output + working set); past it an allocation fails
-    // with "Cannot allocate page" (reference mem_request at maxpage)
+    // new device memory (output + working set) plus 16 MiB of kernel scratch
+    // (sort histograms, scan partials, size-class rounding); past it an
+    // allocation fails with "Cannot allocate page" (reference mem_request at
+    // maxpage)
     if (g_op_depth == 0 && hbm::installed() && mr->device().is_cuda() && mr->budget() > 0)
-      cap_.emplace(mr->device().index() < 0 ? 0 : mr->device().index(), 2 * mr->budget());
+      cap_.emplace(mr->device().index() < 0 ? 0 : mr->device().index(), 2 * mr->budget() + (int64_t(16) << 20));
     if (guard::trace_enabled()) {
       device_sync(mr);
       t0_ = Comm::wtime();

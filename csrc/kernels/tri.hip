@@ -52,52 +52,6 @@ __global__ __launch_bounds__(NT) void k_tri_degree(const uint64_t* __restrict__ 
   }
 }
 
-// the same degrees with per-tile LDS aggregation: a tile of DEG_PER edges
-// inserts both endpoints into an LDS hash table of (vertex, count) and flushes
-// one global atomic per distinct vertex — an R-MAT hub that is the high
-// endpoint of many edges of the tile costs one atomic, not one per edge
-constexpr int DEG_TAB = 4096;
-constexpr int DEG_PER = 1536;
-__device__ __forceinline__ uint32_t deg_slot(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x85EBCA6Bu;
-  x ^= x >> 13;
-  return x & (DEG_TAB - 1);
-}
-__device__ __forceinline__ void deg_insert(uint32_t* key, uint32_t* cnt, uint32_t k, uint32_t* __restrict__ deg) {
-  uint32_t s = deg_slot(k);
-  for (int p = 0; p < 32; ++p) {
-    const uint32_t old = atomicCAS(key + s, 0xffffffffu, k);
-    if (old == 0xffffffffu || old == k) {
-      atomicAdd(cnt + s, 1u);
-      return;
-    }
-    s = (s + 1) & (DEG_TAB - 1);
-  }
-  atomicAdd(deg + k, 1u);  // table crowded: straight to memory
-}
-__global__ __launch_bounds__(NT) void k_tri_degree_lds(const uint64_t* __restrict__ e, int64_t m,
-                                                      uint32_t* __restrict__ deg) {
-  __shared__ uint32_t key[DEG_TAB], cnt[DEG_TAB];
-  for (int64_t t0 = (int64_t)blockIdx.x * DEG_PER; t0 < m; t0 += (int64_t)gridDim.x * DEG_PER) {
-    for (int i = threadIdx.x; i < DEG_TAB; i += NT) {
-      key[i] = 0xffffffffu;
-      cnt[i] = 0;
-    }
-    __syncthreads();
-    const int64_t t1 = t0 + DEG_PER < m ? t0 + DEG_PER : m;
-    for (int64_t i = t0 + threadIdx.x; i < t1; i += NT) {
-      const uint64_t x = e[i];
-      deg_insert(key, cnt, (uint32_t)(x >> 32), deg);
-      deg_insert(key, cnt, (uint32_t)x, deg);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < DEG_TAB; i += NT)
-      if (cnt[i]) atomicAdd(deg + key[i], cnt[i]);
-    __syncthreads();
-  }
-}
-
 // rank[v] = position of v in (degree, id) order; the edge points from the
 // lower to the higher rank and is stored in rank ids, so every row holds only
 // higher ids and sorted rows can be cut at any id bound
@@ -868,17 +822,7 @@ unsigned grid_for(int64_t n) {
 
 void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s) {
   if (m <= 0) return;
-  // MRH_TRI_DEG=lds: per-tile LDS aggregation of both endpoints
-  static const bool lds = [] {
-    const char* v = std::getenv("MRH_TRI_DEG");
-    return v && std::string(v) == "lds";
-  }();
-  if (lds) {
-    const int64_t tiles = (m + DEG_PER - 1) / DEG_PER;
-    hipLaunchKernelGGL(k_tri_degree_lds, dim3((unsigned)std::min<int64_t>(tiles, 8192)), dim3(NT), 0, s, e, m, deg);
-  } else {
-    hipLaunchKernelGGL(k_tri_degree, dim3(grid_for(m)), dim3(NT), 0, s, e, m, deg);
-  }
+  hipLaunchKernelGGL(k_tri_degree, dim3(grid_for(m)), dim3(NT), 0, s, e, m, deg);
   MRH_CHECK_LAUNCH();
 }
 

@@ -24,16 +24,23 @@ def _load():
 
 C = _load()
 
-# MRH_GUARD=1: the guarded (canaried) HBM allocator replaces ATen's caching
-# allocator before anything in this process allocates device memory
-# (csrc/engine/guardalloc.h)
+# Device allocator of the process, chosen before anything allocates device
+# memory:
+#  * MRH_GUARD=1: the guarded (canaried) allocator (csrc/engine/guardalloc.h);
+#  * default: the engine's HBM page pool (csrc/engine/hbmpool.h) — per-stream
+#    size-class caches over stream-ordered HIP memory pools, with the hard cap
+#    MapReduce ops with a page budget (maxpage x memsize / hbm_budget) run
+#    under. It needs this package imported before the first device allocation
+#    of the process; otherwise the ATen caching allocator stays (a requested
+#    MRH_HBM_POOL=1 then fails loudly). MRH_HBM_POOL=0 keeps the ATen
+#    caching allocator.
+_POOL = os.environ.get("MRH_HBM_POOL", "")
 if os.environ.get("MRH_GUARD", "0") not in ("", "0"):
     C.install_alloc_guard()
-# MRH_HBM_POOL=1: the engine's HBM page pool (csrc/engine/hbmpool.h) is the
-# device allocator — stream-ordered HIP memory pools with a hard cap that
-# MapReduce ops with a page budget (maxpage x memsize / hbm_budget) enforce
-elif os.environ.get("MRH_HBM_POOL", "0") not in ("", "0"):
-    if not C.hbm_pool_install():
+elif _POOL != "0":
+    import torch as _torch
+    # device_count() does not initialise the device allocator (is_available()-style probes may)
+    if _torch.cuda.device_count() > 0 and not C.hbm_pool_install() and _POOL == "1":
         raise RuntimeError("MRH_HBM_POOL=1: device memory was allocated before gpu_mapreduce_amd was imported; "
                            "import it first so the page pool can become the device allocator")
 

@@ -83,13 +83,14 @@ class InvertedIndex:
         self.names_dev = pools.device_constant(dev, self.names)
         self.name_off_dev = pools.device_constant(dev, self.name_off)
         maxlen = max((t.numel() for _, t in files), default=0)
-        # persistent staging buffers: a ring of `streams` (0 = auto: 2, double
-        # buffered — a deeper ring gains nothing with 8 files, each copy is
-        # longer than its map) so streams - 1 file copies are in flight while
-        # one file maps; the PAD bytes past each file are read by the 16-byte
-        # scan windows but never matched
+        # persistent staging buffers: a ring of `streams` (0 = auto: 3, or
+        # MRH_II_BUFS) so streams - 1 file copies are in flight while one file
+        # maps: with the cross-job prefetch 2 / 3 / 4 buffers measured 19.75 /
+        # 19.25 / 19.22 ms per 1 GiB job (profiles/r3_ii_ring_depth.txt); the
+        # PAD bytes past each file are read by the 16-byte scan windows but
+        # never matched
         st = int(mr.streams)
-        self.nbuf = st if st > 0 else max(1, int(os.environ.get("MRH_II_BUFS", "2")))
+        self.nbuf = st if st > 0 else max(1, int(os.environ.get("MRH_II_BUFS", "3")))
         self.bufs = [pools.device_buffer(dev, maxlen + PAD, slot) for slot in range(self.nbuf if files else 0)]
         self.copy_stream = pools.stream(dev, "h2d") if self.is_cuda else None
         self.output = None

@@ -223,7 +223,7 @@ def test_inverted_index_end_to_end_gpu(streams):
     mr.streams = streams
     app = InvertedIndex(mr, [(n, t.pin_memory()) for n, t in files])
     app.run()
-    assert app.nbuf == (streams or 2)
+    assert app.nbuf == (streams or 3)
     got = {}
     for line in app.output_lines():
         url, rest = line.split("\t")

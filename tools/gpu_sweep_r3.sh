@@ -21,4 +21,7 @@ step tri_deg_atomic 200 python bench.py --workload trifind --steps 3 --warmup 1 
 step tri_deg_lds 200 env MRH_TRI_DEG=lds python bench.py --workload trifind --steps 3 --warmup 1 || exit $?
 step wf 200 python bench.py --workload wordfreq --steps 10 --warmup 2 || exit $?
 step tri_tests 400 env MRH_TRI_DEG=lds python -u -m pytest tests/test_triangles.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider || exit $?
+step pool_tests 400 python -u -m pytest tests/test_hbm_pool.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider || exit $?
+step pool_suite 400 env MRH_HBM_POOL=1 python -u -m pytest tests/test_outofcore.py tests/test_kernels_gpu.py tests/test_wordfreq.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider || exit $?
+step ii_pool 200 env MRH_HBM_POOL=1 python bench.py $NOX || exit $?
 exit 0
