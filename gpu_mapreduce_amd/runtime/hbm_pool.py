@@ -1,8 +1,9 @@
 """Python face of the HBM page pool (csrc/engine/hbmpool.h).
 
-The pool replaces the ATen caching allocator for the whole process when
-installed — `MRH_HBM_POOL=1` in the environment before `import
-gpu_mapreduce_amd`, or `install()` before any device tensor exists. Every
+The pool replaces the ATen caching allocator for the whole process: it is
+installed when `gpu_mapreduce_amd` is imported before any device tensor
+exists (`MRH_HBM_POOL=0` opts out, `=1` fails loudly if it cannot install),
+or by `install()` under the same condition. Every
 device allocation then comes from per-device stream-ordered HIP memory pools
 with a hard cap; a MapReduce op whose object has a page budget B
 (`maxpage` x `memsize`, or `hbm_budget`) may hold at most 2B of new device

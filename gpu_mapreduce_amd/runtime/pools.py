@@ -2,8 +2,9 @@
 page pool, reference src/mapreduce.cpp:3318-3547): device staging buffers for
 streamed input and pinned host buffers for device->host output are allocated
 once per process and reused by every job, so no job pays hipMalloc /
-hipHostMalloc on its critical path. Device scratch of the engine itself goes
-through the ATen caching allocator (stream-ordered reuse)."""
+hipHostMalloc on its critical path. Every other device allocation goes through
+the engine's HBM page pool (csrc/engine/hbmpool.h), the process's device
+allocator."""
 from __future__ import annotations
 
 import torch
