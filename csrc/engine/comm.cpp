@@ -1,6 +1,7 @@
 // Native communicator (see comm.h).
 #include "comm.h"
 #include "guardalloc.h"
+#include "hbmpool.h"
 
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -86,15 +87,23 @@ void copy_bytes(void* dst, const void* src, int64_t n, at::Device dev) {
 }
 }  // namespace
 
+// the job's device allocator, before its first HBM allocation: MRH_GUARD's
+// canaried allocator, else the HBM page pool (hbmpool.h) unless MRH_HBM_POOL=0
+// (a no-op when the process already allocated device memory)
+static void install_allocator() {
+  guard::install_alloc_guard();
+  if (!guard::alloc_guard_active()) hbm::install_default();
+}
+
 Comm::Comm(at::Device dev) : dev_(dev) {
-  if (dev_.is_cuda()) guard::install_alloc_guard();  // MRH_GUARD: before the job's first HBM allocation
+  if (dev_.is_cuda()) install_allocator();
   if (dev_.is_cuda() && force_rccl()) init_transport("", "self");
 }
 
 Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const std::string& transport,
            std::vector<int> members, int world_rank, int world_size)
     : dev_(dev), pg_(std::move(pg)), store_(std::move(store)) {
-  if (dev_.is_cuda()) guard::install_alloc_guard();
+  if (dev_.is_cuda()) install_allocator();
   if (pg_) {
     rank_ = pg_->getRank();
     size_ = pg_->getSize();

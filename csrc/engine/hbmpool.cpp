@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
@@ -239,6 +240,12 @@ bool install() {
   torch::cuda::CUDAPluggableAllocator::changeCurrentAllocator(a);
   g_installed = true;
   return true;
+}
+
+bool install_default() {
+  const char* e = std::getenv("MRH_HBM_POOL");
+  if (e && std::string(e) == "0") return false;
+  return install();
 }
 
 bool installed() { return g_installed; }

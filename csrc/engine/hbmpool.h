@@ -40,6 +40,9 @@ struct PoolStats {
 // make the pool the process's device allocator; false (and no change) if the
 // current allocator has already been initialised by a device allocation
 bool install();
+// install() unless MRH_HBM_POOL=0 — what Comm construction does on a GPU
+// (native programs, C API); false when it did not install
+bool install_default();
 bool installed();
 PoolStats stats(int device);
 void reset_peak(int device);
