@@ -97,11 +97,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
   return {rowptr, col, okeys, perm};
 }
 
-// hub bitmap size: MRH_TRI_HUB vertices (0 = off); default nvert / 32 capped
+// hub bitmap size: MRH_TRI_HUB vertices (0 = off); default nvert / 64 capped
 // at 524288 (a 32 GB bitmap) and at a quarter of the free HBM — the best of
-// a sweep on RMAT-24 (16.8 M vertices) with sparse-row lists: 128 K / 256 K /
-// 384 K / 512 K hubs = 862 / 649 / 661 / 606 ms, 1566 ms without hubs
-// (profiles/r2_trifind_hub_sweep.txt); a multiple of 64, at most nvert
+// a sweep on RMAT-24 (16.8 M vertices) with the sorted-word sparse hub kernel:
+// 128 K / 192 K / 224 K / 256 K / 288 K / 320 K / 384 K / 512 K hubs = 214.8 /
+// 164.9 / 159.6 / 159.6-162.9 / 172.0 / 173.0 / 176.5 / 181.6 ms
+// (profiles/r3_trifind_hub_sweep.txt; nvert / 32 was best for the earlier
+// kernel, profiles/r2_trifind_hub_sweep.txt); a multiple of 64, at most nvert
 static int64_t g_last_hub = 0;
 int64_t tri_last_hub_size() { return g_last_hub; }
 
@@ -110,7 +112,7 @@ int64_t tri_hub_size(int64_t nvert) {
     const char* e = std::getenv("MRH_TRI_HUB");
     return e ? std::atoll(e) : int64_t(-1);
   }();
-  int64_t want = env >= 0 ? env : std::min<int64_t>(nvert / 32, 524288);
+  int64_t want = env >= 0 ? env : std::min<int64_t>(nvert / 64, 524288);
   size_t free_b = 0, total_b = 0;
   if (env < 0 && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0) {
     if ((size_t)want * (size_t)want / 8 > free_b / 4) {  // blocks cached by the allocator count as free
