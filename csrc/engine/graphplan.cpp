@@ -405,7 +405,10 @@ void PageRankPlan::build_device(const at::Tensor& e) {
 // every range, hot and cold (nhot + 2 entries, redge.back() = nedge).
 void PageRankPlan::xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits, std::vector<int64_t>& rb,
                               std::vector<int64_t>& redge) {
-  int64_t l2 = int64_t(4) << 20;
+  // the widest range's slice of x is 85 % of l2: 3 MiB of each XCD's 4 MiB L2
+  // measured best with the fused tile step — RMAT-26 x20 at 2 / 3 / 4 / 5 /
+  // 6 MiB: 124.4 / 122.8 / 125.1 / 138.6 / 143.6 ms (profiles/r3_pagerank_sweep.txt)
+  int64_t l2 = int64_t(3) << 20;
   if (const char* e = std::getenv("MRH_PR_L2_BYTES")) l2 = std::max<int64_t>(4096, std::atoll(e));
   const int64_t cap = l2 / 4 * 85 / 100;
   if (nactive <= cap) return;  // the whole active rank vector fits one L2
