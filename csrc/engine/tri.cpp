@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
+#include <vector>
 #include <string>
 
 #include "../kernels/launch.h"
@@ -54,7 +55,46 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
   nvert = std::max<int64_t>(nvert, 1);
   at::Tensor deg = at::zeros({nvert}, opt(dev, at::kInt));
   if (uniq.is_cuda()) {
-    k::tri_degree(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), cur());
+    const int nb = k::tri_deg_buckets(nvert);
+    if (nb > 0 && m > 0) {
+      // partitioned count (tri.hip k_deg_*): no scattered atomic per edge
+      const hipStream_t s = cur();
+      const at::Device dev = uniq.device();
+      k::tri_deg_lo(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), s);
+      at::Tensor bcount = at::zeros({nb}, opt(dev, at::kInt));
+      k::tri_deg_count(P0<uint64_t>(uniq), m, nb, P0<unsigned int>(bcount), s);
+      at::Tensor bstart = exclusive_scan(bcount.to(at::kLong).contiguous()).contiguous();  // nb + 1
+      at::Tensor cursor = bstart.narrow(0, 0, nb).clone();
+      at::Tensor ids = at::empty({m}, opt(dev, at::kShort));
+      k::tri_deg_scatter(P0<uint64_t>(uniq), m, nb, P0<unsigned long long>(cursor), P0<uint16_t>(ids), s);
+      // (bucket, piece) items: a bucket up to 2 M endpoints is one block's
+      // (plain stores), a larger one (R-MAT hub ids) is split (atomic adds)
+      at::Tensor bc = bcount.to(at::kCPU);
+      const int32_t* bcp = bc.data_ptr<int32_t>();
+      constexpr int64_t PIECE = int64_t(1) << 21;
+      std::vector<int64_t> items;
+      std::vector<int32_t> ilen;
+      std::vector<uint8_t> whole;
+      for (int b = 0; b < nb; ++b) {
+        const int64_t c = (uint32_t)bcp[b];
+        if (c == 0) continue;
+        for (int64_t o = 0; o < c; o += PIECE) {
+          items.push_back((int64_t)(((uint64_t)b << 40) | (uint64_t)o));
+          ilen.push_back((int32_t)std::min<int64_t>(PIECE, c - o));
+          whole.push_back(c <= PIECE ? 1 : 0);
+        }
+      }
+      const int64_t ni = (int64_t)items.size();
+      if (ni > 0) {
+        at::Tensor ti = at::from_blob(items.data(), {ni}, opt(at::kCPU, at::kLong)).to(dev);
+        at::Tensor tl = at::from_blob(ilen.data(), {ni}, opt(at::kCPU, at::kInt)).to(dev);
+        at::Tensor tw = at::from_blob(whole.data(), {ni}, opt(at::kCPU, at::kByte)).to(dev);
+        k::tri_deg_hist(P0<uint16_t>(ids), P0<unsigned long long>(bstart), P0<uint64_t>(ti), P0<uint32_t>(tl),
+                        P0<uint8_t>(tw), ni, nvert, P0<uint32_t>(deg), s);
+      }
+    } else {
+      k::tri_degree(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), cur());
+    }
   } else {
     const uint64_t* e = P0<uint64_t>(uniq);
     int32_t* d = P0<int32_t>(deg);

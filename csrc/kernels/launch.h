@@ -257,6 +257,17 @@ void pb_layout(const int32_t* perm2, const int32_t* dst1, int64_t m, int32_t* ou
 // ---------------------------------------------------------------- tri.hip
 // triangle enumeration on a degree-oriented CSR (packed u64 edges lo<<32|hi)
 void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);
+// partitioned degree count (tri.hip): buckets of 2^tri_deg_bucket_bits()
+// vertices (-1: too many buckets, use tri_degree); lo runs; bucket counts;
+// scatter of the high endpoints as u16 into their buckets; per-(bucket,
+// piece) LDS histograms added to deg (plain stores where whole != 0)
+int tri_deg_buckets(int64_t nvert);
+int tri_deg_bucket_bits();
+void tri_deg_lo(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);
+void tri_deg_count(const uint64_t* e, int64_t m, int nb, unsigned int* bcount, hipStream_t s);
+void tri_deg_scatter(const uint64_t* e, int64_t m, int nb, unsigned long long* cursor, uint16_t* out, hipStream_t s);
+void tri_deg_hist(const uint16_t* ids, const unsigned long long* bstart, const uint64_t* items, const uint32_t* ilen,
+                  const uint8_t* whole, int64_t nitems, int64_t nvert, uint32_t* deg, hipStream_t s);
 // packed (a,b) -> rank ids (min<<32|max) with rank = (degree, id) order
 void tri_orient(const uint64_t* e, int64_t m, const uint32_t* rank, uint64_t* out, hipStream_t s);
 // per oriented edge in [e0,e1): cnt (nullable) and atomic total
