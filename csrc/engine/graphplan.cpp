@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -721,14 +722,7 @@ at::Tensor edge_owner(const at::Tensor& p, int P) {
 
 TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : comm(std::move(c)) {
   const at::Device dev = comm->device();
-  at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2});
-  at::Tensor lo = at::minimum(e.select(1, 0), e.select(1, 1)), hi = at::maximum(e.select(1, 0), e.select(1, 1));
-  at::Tensor keep = mask_indices(lo != hi);  // no self loops
-  lo = lo.index_select(0, keep);
-  hi = hi.index_select(0, keep);
-  if (nv < 0) nv = comm->allreduce(hi.numel() ? hi.max().item<int64_t>() : -1, Comm::MAX) + 1;
-  nvert = nv;
-  if (nvert >= (int64_t(1) << 31)) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^31");
+  at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2}).contiguous();
   // MRH_TRI_REPLICATED=1 / 0 forces the replicated / distributed build; by
   // default a GPU job replicates the graph when the whole edge list's build
   // (~48 bytes per edge: packed copies, two sorts, CSR) takes under a quarter
@@ -738,25 +732,60 @@ TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : c
   const char* rep = std::getenv("MRH_TRI_REPLICATED");
   bool replicate = !comm->distributed() || (rep && *rep == '1');
   if (comm->distributed() && !(rep && *rep)) {
-    const int64_t mall = comm->allreduce(lo.numel(), Comm::SUM);
+    const int64_t mall = comm->allreduce(e.size(0), Comm::SUM);
     size_t free_b = 0, total_b = 0;
     int fits = 0;
     if (dev.is_cuda() && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
       fits = (double)mall * 48.0 < (double)free_b / 4.0 ? 1 : 0;
     replicate = comm->allreduce((int64_t)fits, Comm::MIN) == 1;  // every rank must take the same path
   }
-  if (!replicate) {
-    build_distributed(lo, hi);
-    return;
+  at::Tensor p;
+  if (replicate && dev.is_cuda() && nv >= 0) {
+    // one pass: packed min << 32 | max, a self loop packed as edge (0, 0) —
+    // it sorts first, keeps every key byte that is constant over the real
+    // edges constant (the radix sort still skips those passes), and is
+    // dropped after the dedup
+    nvert = nv;
+    if (nvert >= (int64_t(1) << 31)) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^31");
+    p = at::empty({e.size(0)}, opt(dev, at::kLong));
+    at::Tensor bad = at::zeros({1}, opt(dev, at::kInt));
+    k::tri_pack(e.data_ptr<int64_t>(), e.size(0), nvert, reinterpret_cast<uint64_t*>(p.data_ptr()),
+                reinterpret_cast<unsigned int*>(bad.data_ptr()), at::hip::getCurrentHIPStream());
+    if (bad.item<int32_t>())
+      throw std::runtime_error("TriangleGraph: an edge has a vertex id outside [0, nvert = " + std::to_string(nvert) + ")");
+  } else {
+    at::Tensor lo = at::minimum(e.select(1, 0), e.select(1, 1)), hi = at::maximum(e.select(1, 0), e.select(1, 1));
+    at::Tensor keep = mask_indices(lo != hi);  // no self loops
+    lo = lo.index_select(0, keep);
+    hi = hi.index_select(0, keep);
+    if (nv < 0) nv = comm->allreduce(hi.numel() ? hi.max().item<int64_t>() : -1, Comm::MAX) + 1;
+    nvert = nv;
+    if (nvert >= (int64_t(1) << 31)) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^31");
+    if (!replicate) {
+      build_distributed(lo, hi);
+      return;
+    }
+    p = at::bitwise_or(at::bitwise_left_shift(lo, 32), hi).contiguous();
   }
   // replicated degree-oriented CSR: every rank holds the whole graph and
   // counts its share of the rows
+  static const bool dbg = std::getenv("MRH_TRI_DEBUG") != nullptr;
+  auto stage = [&](const char* what) {
+    if (!dbg) return;
+    if (dev.is_cuda()) (void)hipDeviceSynchronize();
+    std::fprintf(stderr, "mrhip TriangleGraph: %s done\n", what);
+  };
+  stage("pack");
   distributed = false;
-  at::Tensor p = at::bitwise_or(at::bitwise_left_shift(lo, 32), hi).contiguous();
   if (comm->distributed()) p = comm->allgather_var(p);
   at::Tensor uniq = unique_sorted(p);
+  stage("dedup");
+  p = at::Tensor();
+  if (uniq.numel() > 0 && uniq[0].item<int64_t>() == 0) uniq = uniq.narrow(0, 1, uniq.numel() - 1);  // (0, 0): self loops
+  stage("drop self loops");
   nedge = uniq.numel();
   std::tie(rowptr, col, okeys, perm) = tri_prepare(uniq, std::max<int64_t>(nvert, 1));
+  stage("CSR");
   const int64_t m = okeys.numel(), P = comm->size(), me = comm->rank();
   e0 = 0;
   e1 = m;

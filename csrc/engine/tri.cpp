@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <vector>
@@ -54,6 +55,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
   const int64_t m = uniq.numel();
   nvert = std::max<int64_t>(nvert, 1);
   at::Tensor deg = at::zeros({nvert}, opt(dev, at::kInt));
+  static const bool dbg = std::getenv("MRH_TRI_DEBUG") != nullptr;
+  auto stage = [&](const char* what) {
+    if (!dbg) return;
+    if (uniq.is_cuda()) (void)hipDeviceSynchronize();
+    std::fprintf(stderr, "mrhip tri_prepare: %s done\n", what);
+  };
   if (uniq.is_cuda()) {
     const int nb = k::tri_deg_buckets(nvert);
     if (nb > 0 && m > 0) {
@@ -61,12 +68,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
       const hipStream_t s = cur();
       const at::Device dev = uniq.device();
       k::tri_deg_lo(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), s);
+      stage("deg_lo");
       at::Tensor bcount = at::zeros({nb}, opt(dev, at::kInt));
       k::tri_deg_count(P0<uint64_t>(uniq), m, nb, P0<unsigned int>(bcount), s);
+      stage("deg_count");
       at::Tensor bstart = exclusive_scan(bcount.to(at::kLong).contiguous()).contiguous();  // nb + 1
       at::Tensor cursor = bstart.narrow(0, 0, nb).clone();
       at::Tensor ids = at::empty({m}, opt(dev, at::kShort));
       k::tri_deg_scatter(P0<uint64_t>(uniq), m, nb, P0<unsigned long long>(cursor), P0<uint16_t>(ids), s);
+      stage("deg_scatter");
       // (bucket, piece) items: a bucket up to 2 M endpoints is one block's
       // (plain stores), a larger one (R-MAT hub ids) is split (atomic adds)
       at::Tensor bc = bcount.to(at::kCPU);
@@ -103,13 +113,16 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
       d[(uint32_t)e[i]]++;
     }
   }
+  stage("degree");
   // rank = position in (degree, id) order; perm[rank] = original id
-  at::Tensor ids = at::arange(nvert, opt(dev, at::kLong));
   // the LSD radix sort is stable: sorting the degrees alone keeps equal
   // degrees in id order, i.e. (degree, id) order
-  at::Tensor perm = std::get<1>(radix_sort_pairs(deg.to(at::kLong), ids.to(at::kInt), 0, 32)).to(at::kLong);
+  at::Tensor perm32 = std::get<1>(radix_sort_pairs(deg.to(at::kLong), at::arange(nvert, opt(dev, at::kInt)), 0, 32));
+  at::Tensor perm = perm32.to(at::kLong);
   at::Tensor rank = at::empty({nvert}, opt(dev, at::kInt));
-  rank.index_put_({perm}, ids.to(at::kInt));
+  if (uniq.is_cuda()) k::tri_rank(P0<int32_t>(perm32), nvert, P0<int32_t>(rank), cur());
+  else rank.index_put_({perm}, at::arange(nvert, opt(dev, at::kInt)));
+  stage("rank");
   at::Tensor oriented = at::empty({m}, opt(dev, at::kLong));
   if (uniq.is_cuda()) {
     k::tri_orient(P0<uint64_t>(uniq), m, P0<uint32_t>(rank), P0<uint64_t>(oriented), cur());
@@ -122,9 +135,16 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
       o[i] = ra < rb ? (ra << 32 | rb) : (rb << 32 | ra);
     }
   }
+  stage("orient");
   // keys-only: the oriented edges carry no payload
   at::Tensor okeys = m ? radix_sort_keys(oriented, 0, 64) : oriented;
-  at::Tensor col = at::bitwise_and(okeys, (int64_t)0xffffffff).to(at::kInt);
+  at::Tensor col;
+  if (okeys.is_cuda()) {
+    col = at::empty({m}, opt(dev, at::kInt));
+    k::tri_col(P0<uint64_t>(okeys), m, P0<uint32_t>(col), cur());
+  } else {
+    col = at::bitwise_and(okeys, (int64_t)0xffffffff).to(at::kInt);
+  }
   at::Tensor rowptr;
   if (okeys.is_cuda()) {
     rowptr = at::empty({nvert + 1}, opt(dev, at::kLong));

@@ -256,6 +256,12 @@ void pb_layout(const int32_t* perm2, const int32_t* dst1, int64_t m, int32_t* ou
 
 // ---------------------------------------------------------------- tri.hip
 // triangle enumeration on a degree-oriented CSR (packed u64 edges lo<<32|hi)
+// [n, 2] int64 edges -> packed min << 32 | max (self loops -> 0, ids outside
+// [0, nvert) set *bad); col = low
+// words of the oriented keys; rank[perm[r]] = r
+void tri_pack(const int64_t* e, int64_t n, int64_t nvert, uint64_t* out, unsigned int* bad, hipStream_t s);
+void tri_col(const uint64_t* okeys, int64_t m, uint32_t* col, hipStream_t s);
+void tri_rank(const int32_t* perm, int64_t n, int32_t* rank, hipStream_t s);
 void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);
 // partitioned degree count (tri.hip): buckets of 2^tri_deg_bucket_bits()
 // vertices (-1: too many buckets, use tri_degree); lo runs; bucket counts;

@@ -154,6 +154,36 @@ __global__ __launch_bounds__(DEG_NT) void k_deg_hist(const uint16_t* __restrict_
   }
 }
 
+// [n, 2] int64 edges -> packed min << 32 | max; a self loop becomes edge
+// (0, 0), i.e. key 0 (sorts first, dropped after the dedup; any other
+// sentinel would make constant key bytes vary and cost radix passes) — one
+// pass instead of the minimum / maximum / mask / compaction / shift / or chain
+// an id outside [0, nvert) sets *bad (and packs as 0): the host checks it
+// before any kernel indexes a per-vertex array with the ids
+__global__ __launch_bounds__(NT) void k_tri_pack(const int64_t* __restrict__ e, int64_t n, int64_t nvert,
+                                                uint64_t* __restrict__ out, unsigned int* __restrict__ bad) {
+  bool oob = false;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const uint64_t a = (uint64_t)e[2 * i], b = (uint64_t)e[2 * i + 1];
+    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    const bool ok = hi < (uint64_t)nvert;  // unsigned: negative ids are huge
+    oob |= !ok;
+    out[i] = (!ok || lo == hi) ? 0ull : (lo << 32) | hi;
+  }
+  if (__ballot(oob) && dev::lane_id() == 0) atomicOr(bad, 1u);
+}
+
+// col[i] = low word of okeys[i]; rank[perm[r]] = r
+__global__ __launch_bounds__(NT) void k_tri_col(const uint64_t* __restrict__ okeys, int64_t m,
+                                               uint32_t* __restrict__ col) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (int64_t)gridDim.x * NT)
+    col[i] = (uint32_t)okeys[i];
+}
+__global__ __launch_bounds__(NT) void k_tri_rank(const int32_t* __restrict__ perm, int64_t n,
+                                                int32_t* __restrict__ rank) {
+  for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < n; r += (int64_t)gridDim.x * NT) rank[perm[r]] = (int32_t)r;
+}
+
 // rank[v] = position of v in (degree, id) order; the edge points from the
 // lower to the higher rank and is stored in rank ids, so every row holds only
 // higher ids and sorted rows can be cut at any id bound
@@ -960,6 +990,22 @@ void tri_deg_hist(const uint16_t* ids, const unsigned long long* bstart, const u
   if (nitems <= 0) return;
   hipLaunchKernelGGL(k_deg_hist, dim3((unsigned)std::min<int64_t>(nitems, 2048)), dim3(DEG_NT), 0, s, ids, bstart,
                      items, ilen, whole, nitems, nvert, deg);
+  MRH_CHECK_LAUNCH();
+}
+
+void tri_pack(const int64_t* e, int64_t n, int64_t nvert, uint64_t* out, unsigned int* bad, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_tri_pack, dim3(grid_for(n)), dim3(NT), 0, s, e, n, nvert, out, bad);
+  MRH_CHECK_LAUNCH();
+}
+void tri_col(const uint64_t* okeys, int64_t m, uint32_t* col, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_tri_col, dim3(grid_for(m)), dim3(NT), 0, s, okeys, m, col);
+  MRH_CHECK_LAUNCH();
+}
+void tri_rank(const int32_t* perm, int64_t n, int32_t* rank, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_tri_rank, dim3(grid_for(n)), dim3(NT), 0, s, perm, n, rank);
   MRH_CHECK_LAUNCH();
 }
 

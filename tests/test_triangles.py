@@ -189,3 +189,17 @@ def test_gpu_hub_bitmap_split_matches_cpu():
         assert r.returncode == 0, r.stderr[-2000:]
         k, n = map(int, r.stdout.split())
         assert (k == K if hub is not None else 0 < k <= K and k % 64 == 0) and n == want, (hub, core, kern, k, n, want)
+
+
+@pytest.mark.gpu
+def test_gpu_fast_build_with_nvert_matches_cpu():
+    """nvert given on one GPU: the one-pass pack (self loops packed as edge
+    (0, 0), dropped after the dedup) must build the CPU path's CSR; an id
+    outside [0, nvert) is an error, not an out-of-bounds write"""
+    e = _rmat(12, 16, 9)
+    cpu = TriangleGraph(Comm(device="cpu"), e, 1 << 12)
+    gpu = TriangleGraph(Comm(device="cuda"), e.cuda(), 1 << 12)
+    assert gpu.count() == cpu.count()
+    assert torch.equal(gpu.okeys.cpu(), cpu.okeys) and torch.equal(gpu.rowptr.cpu(), cpu.rowptr)
+    with pytest.raises(RuntimeError, match="outside"):
+        TriangleGraph(Comm(device="cuda"), e.cuda(), 100)
