@@ -216,6 +216,7 @@ def bench_pagerank_extra(comm, args):
         "pagerank_ms": dt * 1e3,
         "pagerank_setup_ms": setup * 1e3,
         "pagerank_kvps_incl_setup": nedge * iters / (dt + setup),
+        "pagerank_hip_graph_iterations": pr.graph_iterations,
         "pagerank_config": {"graph": f"RMAT-2^{scale}", "edgefactor": ef, "edges": nedge, "iters": iters,
                             "runs_timed": args.pagerank_steps, "alpha": 0.85, "scaling": "strong",
                             "rank_dtype": "fp32 ranks, fp64 L1/dangling reductions"},

@@ -10,6 +10,8 @@
 #include <stdexcept>
 
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
 
 #include "../kernels/launch.h"
 #include "tri.h"
@@ -251,8 +253,14 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
     if (want && !comm->distributed() && dev.is_cuda() && nedge > 0 && nedge < (int64_t(1) << 31) && ngrp > 0)
       build_blocking(vid_.index_select(0, segment_ids(seg_, ngrp, nedge)));
   }
-  // the fused tile step (XCD ranges) needs no accumulator array
+  // the fused tile step (XCD ranges) needs no accumulator array, only its
+  // per-tile partials
   acc_ = at::empty({xr_ > 0 ? 0 : nlocal}, opt(dev, at::kFloat));
+  if (xr_ > 0) part_ = at::empty({std::max<int64_t>(xtile_, 1), 2}, opt(dev, at::kDouble));
+  {
+    const char* g = std::getenv("MRH_PR_GRAPH");
+    use_graph = !(g && *g == '0');
+  }
   if (ngrp > 0 && use_seg_index(dev) && !pb_) {
     six_ = seg_index(seg_, nedge);
     if (xsched_.defined()) {
@@ -604,13 +612,98 @@ void PageRankPlan::build_blocking(const at::Tensor& dst_new) {
   pb_ = true;
 }
 
+// in place once the buffers exist: a captured iteration graph keeps its
+// pointers valid across runs
 void PageRankPlan::reset() {
-  r_ = at::full({nlocal}, 1.0 / (double)N, opt(dev, at::kFloat));
-  rn_ = at::empty_like(r_);
-  c_ = r_ * invdeg_;
-  dmass_ = at::full({1}, (double)ndangling / (double)N, opt(dev, at::kDouble));
-  stats_ = at::zeros({2}, opt(dev, at::kDouble));
+  if (!r_.defined() || r_.numel() != nlocal) {
+    r_ = at::empty({nlocal}, opt(dev, at::kFloat));
+    rn_ = at::empty_like(r_);
+    c_ = at::empty_like(r_);
+  }
+  r_.fill_(1.0 / (double)N);
+  at::mul_out(c_, r_, invdeg_);
+  if (!stats_.defined() || stats_.numel() != 2) stats_ = at::empty({2}, opt(dev, at::kDouble));
+  stats_.narrow(0, 0, 1).zero_();
+  stats_.narrow(0, 1, 1).fill_((double)ndangling / (double)N);
+  dmass_ = stats_.narrow(0, 1, 1);  // the dangling mass of the previous iteration
   acc_.zero_();
+}
+
+// one XCD-path iteration: gather + segmented reduce of c into send_, then
+// the fused tile step (combine, r -> rn, c = rn / outdeg, partials) and the
+// partials' sum into stats_ (stats_[1] is the next iteration's dmass)
+void PageRankPlan::launch_iter(const at::Tensor& r, at::Tensor& rn) {
+  seg_gather_reduce(six_, src_, c_, at::Tensor(), 0, send_);
+  const double base = (1.0 - alpha) / (double)N;
+  const hipStream_t s = at::hip::getCurrentHIPStream();
+  k::pr_tile_step(send_.data_ptr<float>(), ghi_.data_ptr<int32_t>(), xoff_.data_ptr<int64_t>(), (int)xr_, xtile_,
+                  nlocal, r.data_ptr<float>(), rn.data_ptr<float>(), dangling_.data_ptr<uint8_t>(), (float)base,
+                  (float)alpha, stats_.data_ptr<double>() + 1, 1.0 / (double)N, invdeg_.data_ptr<float>(),
+                  c_.data_ptr<float>(), part_.data_ptr<double>(), s);
+  k::pr_partials_sum(part_.data_ptr<double>(), xtile_, stats_.data_ptr<double>(), s);
+}
+
+PageRankPlan::~PageRankPlan() { graph_free(); }
+
+void PageRankPlan::graph_free() {
+  if (gexec_) (void)hipGraphExecDestroy(gexec_);
+  gexec_ = nullptr;
+  for (auto& e : gev_) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
+  if (gstream_) (void)hipStreamDestroy(gstream_);
+  gstream_ = nullptr;
+  gkey_.clear();
+}
+
+// graph replay: one GPU, the XCD tile-step path, a fixed iteration count, no
+// serialising diagnostic mode
+bool PageRankPlan::graph_ok() const {
+  static const bool sync = [] {
+    const char* v = std::getenv("MRH_SYNC");
+    return v && *v && *v != '0';
+  }();
+  return use_graph && !sync && dev.is_cuda() && !comm->distributed() && !pb_ && xr_ > 0 && six_.defined() &&
+         send_.numel() > 0;
+}
+
+// capture two iterations (r_ -> rn_, rn_ -> r_) on a private stream: every
+// launch of them becomes a graph node, so a 20-iteration run is 10 graph
+// launches instead of ~100 kernel / memset launches from the host
+void PageRankPlan::graph_build() {
+  graph_free();
+  auto chk = [](hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("PageRank graph: ") + what + ": " + hipGetErrorString(e));
+  };
+  chk(hipStreamCreateWithFlags(&gstream_, hipStreamNonBlocking), "hipStreamCreate");
+  for (auto& e : gev_) chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  // the buffers are ready when the caller's stream gets here
+  chk(hipEventRecord(gev_[0], at::hip::getCurrentHIPStream()), "hipEventRecord");
+  chk(hipStreamWaitEvent(gstream_, gev_[0], 0), "hipStreamWaitEvent");
+  hipGraph_t g = nullptr;
+  {
+    // the plan's device may be "cuda" without an index: the stream guard needs the real one
+    const c10::DeviceIndex di = dev.has_index() ? dev.index() : c10::hip::current_device();
+    c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(gstream_, di));
+    if (at::hip::getCurrentHIPStream().stream() != gstream_)
+      throw std::runtime_error("PageRank graph: the capture stream is not current");
+    chk(hipStreamBeginCapture(gstream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    try {
+      launch_iter(r_, rn_);
+      launch_iter(rn_, r_);
+    } catch (...) {
+      hipGraph_t bad = nullptr;
+      (void)hipStreamEndCapture(gstream_, &bad);
+      if (bad) (void)hipGraphDestroy(bad);
+      throw;
+    }
+    chk(hipStreamEndCapture(gstream_, &g), "hipStreamEndCapture");
+  }
+  const hipError_t e = hipGraphInstantiate(&gexec_, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  chk(e, "hipGraphInstantiate");
+  gkey_ = {r_.data_ptr(), rn_.data_ptr(), c_.data_ptr(), stats_.data_ptr(), send_.data_ptr(), part_.data_ptr()};
 }
 
 void PageRankPlan::step() {
@@ -632,16 +725,16 @@ void PageRankPlan::step() {
     at::Tensor recv = comm->alltoallv(send_, send_splits_, recv_splits_);
     if (recv.numel()) pr_combine(rseg_, rperm_, recv, rvid_, acc_);
   } else if (send_.numel() && xr_ > 0) {
-    // combine and update fused per destination tile (no acc round trip)
+    // combine and update fused per destination tile (no acc round trip);
+    // the gather above already ran: only the tile step and the partials here
     const double base = (1.0 - alpha) / (double)N;
-    at::Tensor part = at::empty({xtile_, 2}, opt(dev, at::kDouble));
+    const hipStream_t s = at::hip::getCurrentHIPStream();
     k::pr_tile_step(send_.data_ptr<float>(), ghi_.data_ptr<int32_t>(), xoff_.data_ptr<int64_t>(), (int)xr_, xtile_,
                     nlocal, r_.data_ptr<float>(), rn_.data_ptr<float>(), dangling_.data_ptr<uint8_t>(), (float)base,
-                    (float)alpha, dmass_.data_ptr<double>(), 1.0 / (double)N, invdeg_.data_ptr<float>(),
-                    c_.data_ptr<float>(), part.data_ptr<double>(), at::hip::getCurrentHIPStream());
-    at::Tensor st = part.sum(0);
-    dmass_ = st.narrow(0, 1, 1);
-    stats_ = st;
+                    (float)alpha, stats_.data_ptr<double>() + 1, 1.0 / (double)N, invdeg_.data_ptr<float>(),
+                    c_.data_ptr<float>(), part_.data_ptr<double>(), s);
+    k::pr_partials_sum(part_.data_ptr<double>(), xtile_, stats_.data_ptr<double>(), s);
+    dmass_ = stats_.narrow(0, 1, 1);
     std::swap(r_, rn_);
     return;
   } else if (send_.numel()) {
@@ -657,6 +750,24 @@ void PageRankPlan::step() {
 }
 
 int PageRankPlan::run(int maxiter, double tol) {
+  if (tol <= 0 && maxiter >= 2 && graph_ok()) {
+    const std::vector<const void*> key = {r_.data_ptr(), rn_.data_ptr(), c_.data_ptr(), stats_.data_ptr(),
+                                          send_.data_ptr(), part_.data_ptr()};
+    if (!gexec_ || key != gkey_) graph_build();
+    const hipStream_t cs = at::hip::getCurrentHIPStream();
+    auto chk = [](hipError_t e, const char* what) {
+      if (e != hipSuccess) throw std::runtime_error(std::string("PageRank graph: ") + what + ": " + hipGetErrorString(e));
+    };
+    chk(hipEventRecord(gev_[0], cs), "hipEventRecord");
+    chk(hipStreamWaitEvent(gstream_, gev_[0], 0), "hipStreamWaitEvent");
+    for (int p = 0; p < maxiter / 2; ++p) chk(hipGraphLaunch(gexec_, gstream_), "hipGraphLaunch");
+    chk(hipEventRecord(gev_[1], gstream_), "hipEventRecord");
+    chk(hipStreamWaitEvent(cs, gev_[1], 0), "hipStreamWaitEvent");
+    graph_iters_ += 2 * (maxiter / 2);
+    dmass_ = stats_.narrow(0, 1, 1);  // r_ holds the latest ranks after every pair
+    if (maxiter % 2) step();
+    return maxiter;
+  }
   int it = 0;
   for (it = 1; it <= maxiter; ++it) {
     step();

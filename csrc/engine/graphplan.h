@@ -14,6 +14,7 @@
 // reference re-shuffles every edge 2-4 times per iteration
 // (oink/cc_find.cpp:73-92, oink/sssp.cpp:49-184, oink/luby_find.cpp:53-97).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <ATen/ATen.h>
 
 #include <optional>
@@ -75,6 +76,9 @@ at::Tensor sssp_predecessors(const EdgePlan& plan, const at::Tensor& edges, cons
 class PageRankPlan {
  public:
   PageRankPlan(CommPtr comm, const at::Tensor& edges, int64_t nvert, double alpha);
+  ~PageRankPlan();
+  PageRankPlan(const PageRankPlan&) = delete;
+  PageRankPlan& operator=(const PageRankPlan&) = delete;
   void reset();
   void step();
   int run(int maxiter, double tol);
@@ -96,7 +100,19 @@ class PageRankPlan {
   // XCD source ranges (one GPU): R = xr_ ranges, combine tiles, (range, tile)
   // group offsets, destination (new id) per group, gather schedule
   int64_t xr_ = 0, xtile_ = 0, xslen_ = 0;
-  at::Tensor xoff_, ghi_, xsched_;
+  at::Tensor xoff_, ghi_, xsched_, part_;
+  // one XCD-path iteration from r into rn (no host work, no allocation)
+  void launch_iter(const at::Tensor& r, at::Tensor& rn);
+  // HIP graph of two iterations (r_ -> rn_ -> r_), replayed by run() for a
+  // fixed iteration count; rebuilt if the buffers it captured moved
+  bool graph_ok() const;
+  void graph_build();
+  void graph_free();
+  hipGraphExec_t gexec_ = nullptr;
+  hipStream_t gstream_ = nullptr;
+  hipEvent_t gev_[2] = {nullptr, nullptr};
+  std::vector<const void*> gkey_;
+  int64_t graph_iters_ = 0;
   void xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits, std::vector<int64_t>& rb,
                   std::vector<int64_t>& redge);
   void xcd_schedule(const std::vector<int64_t>& redge);
@@ -117,6 +133,9 @@ class PageRankPlan {
  public:
   bool blocking() const { return pb_; }
   int64_t xcd_ranges_count() const { return xr_; }
+  // fixed-count run() replays a captured HIP graph (MRH_PR_GRAPH=0: off)
+  bool use_graph = true;
+  int64_t graph_iterations() const { return graph_iters_; }
 };
 
 // Triangle finder on a degree-oriented CSR (tri.cpp kernels). Multi-rank jobs

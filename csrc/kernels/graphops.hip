@@ -313,6 +313,37 @@ __global__ __launch_bounds__(NT) void k_pr_tile_step(const float* __restrict__ s
   }
 }
 
+// stats[0..1] = the sums of the per-tile (L1 delta, dangling mass) partials
+// of k_pr_tile_step, in a fixed order (one block: bitwise reproducible, and
+// no allocation — the iteration can be replayed from a captured graph)
+__global__ __launch_bounds__(NT) void k_pr_partials_sum(const double* __restrict__ part, int64_t ntile,
+                                                        double* __restrict__ stats) {
+  __shared__ double sh[2][NT / MRH_WAVE];
+  double a = 0.0, b = 0.0;
+  for (int64_t t = threadIdx.x; t < ntile; t += NT) {
+    a += part[2 * t];
+    b += part[2 * t + 1];
+  }
+  for (int o = MRH_WAVE / 2; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, MRH_WAVE);
+    b += __shfl_xor(b, o, MRH_WAVE);
+  }
+  if (dev::lane_id() == 0) {
+    sh[0][dev::wave_id()] = a;
+    sh[1][dev::wave_id()] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double x = 0.0, y = 0.0;
+    for (int w = 0; w < NT / MRH_WAVE; ++w) {
+      x += sh[0][w];
+      y += sh[1][w];
+    }
+    stats[0] = x;
+    stats[1] = y;
+  }
+}
+
 struct PermGet {
   const int32_t* perm;
   const float* v;
@@ -651,6 +682,11 @@ void pr_tile_step(const float* send, const int32_t* ghi, const int64_t* off, int
             "pr_tile_step: 16-byte aligned float columns, 4-byte aligned dangling flags");
   hipLaunchKernelGGL(k_pr_tile_step, dim3((unsigned)ntile), dim3(NT), 0, s, send, ghi, off, R, ntile, ndst, r, rn,
                      dangling, base, alpha, dmass, invN, invdeg, cout, partial);
+  MRH_CHECK_LAUNCH();
+}
+
+void pr_partials_sum(const double* part, int64_t ntile, double* stats, hipStream_t s) {
+  hipLaunchKernelGGL(k_pr_partials_sum, dim3(1), dim3(NT), 0, s, part, ntile, stats);
   MRH_CHECK_LAUNCH();
 }
 

@@ -212,6 +212,8 @@ void pr_range_offsets(const int64_t* hi, int64_t ngrp, int dbits, int R, int64_t
 // one step's combine + update per tile of destinations (new ids): partial
 // sums -> r_new, c = r_new / outdeg, per-tile (L1 delta, dangling mass)
 // partials (2 * ntile doubles)
+// stats[0], stats[1] = sums of the tile step's (L1 delta, dangling mass) partials
+void pr_partials_sum(const double* part, int64_t ntile, double* stats, hipStream_t s);
 void pr_tile_step(const float* send, const int32_t* ghi, const int64_t* off, int R, int64_t ntile, int64_t ndst,
                   const float* r, float* rn, const uint8_t* dangling, float base, float alpha, const double* dmass,
                   double invN, const float* invdeg, float* cout, double* partial, hipStream_t s);

@@ -175,6 +175,19 @@ __global__ __launch_bounds__(WS_NT) void k_ws_gather_reduce(const uint32_t* __re
   }
 }
 
+// carry slots reset to -1 by a kernel, not hipMemsetAsync: the gather is
+// captured into PageRank's HIP graph, and kernel nodes are the graph node
+// type every ROCm release replays as launched
+__global__ __launch_bounds__(256) inline void k_ws_fill_neg1(int64_t* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = -1;
+}
+inline void ws_fill_neg1(int64_t* p, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t b = (n + 255) / 256;
+  hipLaunchKernelGGL(k_ws_fill_neg1, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, s, p, n);
+  MRH_CHECK_LAUNCH();
+}
+
 // launcher; carry buffers need 2*ws_nwave(nval) entries each
 template <typename T, int OP>
 inline void ws_gather_reduce(const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src, const T* x,
@@ -183,7 +196,7 @@ inline void ws_gather_reduce(const uint32_t* H, const int64_t* wbase, int64_t nv
                              const int32_t* sched = nullptr, int64_t slen = 0) {
   if (nval <= 0) return;
   const int64_t nw = ws_nwave(nval);
-  MRH_HIP(hipMemsetAsync(carry_seg, 0xff, sizeof(int64_t) * 2 * nw, s));
+  ws_fill_neg1(carry_seg, 2 * nw, s);
   const int64_t nb = sched ? 8 * ((slen + (WS_NT / 64) - 1) / (WS_NT / 64)) : (nw + (WS_NT / 64) - 1) / (WS_NT / 64);
   hipLaunchKernelGGL((k_ws_gather_reduce<T, OP>), dim3((unsigned)nb), dim3(WS_NT), 0, s, H, wbase, nval, nw, src, x, w,
                      out, carry_seg, carry_val, sched, slen);
@@ -191,7 +204,7 @@ inline void ws_gather_reduce(const uint32_t* H, const int64_t* wbase, int64_t nv
   const int64_t nc = 2 * nw;
   if (carry2_seg && nc > 4096) {  // two-level fold (k_carry_fold): long runs in parallel
     const int64_t nw1 = (nc + 63) / 64;
-    MRH_HIP(hipMemsetAsync(carry2_seg, 0xff, sizeof(int64_t) * 2 * nw1, s));
+    ws_fill_neg1(carry2_seg, 2 * nw1, s);
     hipLaunchKernelGGL((k_carry_fold<T, OP>), dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, carry_seg,
                        carry_val, nc, out, carry2_seg, carry2_val);
     MRH_CHECK_LAUNCH();

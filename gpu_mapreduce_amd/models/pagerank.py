@@ -84,6 +84,21 @@ class PageRank:
     def delta(self):
         return self._p.delta()
 
+    @property
+    def use_graph(self) -> bool:
+        """fixed-count run() replays a captured HIP graph of two iterations
+        (one GPU, XCD tile-step path; MRH_PR_GRAPH=0 turns it off)"""
+        return bool(self._p.use_graph)
+
+    @use_graph.setter
+    def use_graph(self, on: bool):
+        self._p.use_graph = bool(on)
+
+    @property
+    def graph_iterations(self) -> int:
+        """iterations run so far by graph replay"""
+        return int(self._p.graph_iterations)
+
     def ranks(self):
         """(global vertex ids, ranks) owned by this rank."""
         return self._p.ids(), self._p.ranks()
@@ -136,6 +151,7 @@ def bench_pagerank(comm, args):
         "edges": nedge,
         "setup_s": setup,
         "l1_delta_last": pr.delta(),
+        "hip_graph_iterations": pr.graph_iterations,
         "config": {"model": "PageRank", "global_batch": nedge, "seq_len": iters,
                    "parallelism": f"dp{comm.size}", "scale": scale, "edgefactor": ef, "alpha": 0.85},
         "scaling": "strong",

@@ -137,3 +137,35 @@ def test_pagerank_xcd_ranges_match_pull_and_numpy(tmp_path):
         res[name] = np.load(path)
     np.testing.assert_allclose(res["xcd"], res["pull"], rtol=1e-4, atol=1e-10)
     np.testing.assert_allclose(res["layer1"], res["pull"], rtol=1e-4, atol=1e-10)
+
+
+@pytest.mark.gpu
+def test_pagerank_hip_graph_replay_matches_plain_steps():
+    """a fixed-count run replays a captured HIP graph of two iterations; the
+    ranks must be bitwise those of the plain per-step launches (even and odd
+    counts, and again after reset(), which reuses the captured buffers)"""
+    import gpu_mapreduce_amd as g
+    from gpu_mapreduce_amd.models.pagerank import PageRank, rmat_map
+    import os
+    mr = g.MapReduce(g.Comm(device="cuda"))
+    rmat_map(mr, 18, 16, seed=3)
+    os.environ["MRH_PR_L2_BYTES"] = "65536"  # small ranges: RMAT-18 takes the XCD tile-step path
+    try:
+        pr = PageRank(mr, 1 << 18).build()
+    finally:
+        os.environ.pop("MRH_PR_L2_BYTES")
+    assert pr.xcd_ranges > 0
+    for iters in (20, 7):
+        pr.use_graph = False
+        pr.reset()
+        pr.run(iters)
+        _, plain = pr.ranks()
+        plain = plain.clone()
+        before = pr.graph_iterations
+        pr.use_graph = True
+        for _ in range(2):
+            pr.reset()
+            pr.run(iters)
+            _, got = pr.ranks()
+            assert torch.equal(got, plain), iters
+        assert pr.graph_iterations - before == 2 * 2 * (iters // 2)
