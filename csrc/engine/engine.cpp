@@ -242,6 +242,8 @@ std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& k
   const int64_t n = keys.numel();
   const at::Device dev = keys.device();
   if (keys.scalar_type() != at::kLong || vals.scalar_type() != at::kInt) fail("radix_sort_pairs: keys int64, vals int32");
+  if (vals.numel() != n || vals.device() != dev) fail("radix_sort_pairs: one int32 value per key, on the keys' device");
+  if (begin_bit < 0 || end_bit > 64 || begin_bit > end_bit) fail("radix_sort_pairs: need 0 <= begin_bit <= end_bit <= 64");
   begin_bit = (begin_bit / 8) * 8;
   end_bit = std::min(64, ((end_bit + 7) / 8) * 8);
   at::Tensor ko = at::empty_like(keys), vo = at::empty_like(vals);

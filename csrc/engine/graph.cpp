@@ -19,6 +19,16 @@ hipStream_t cur() { return at::hip::getCurrentHIPStream(); }
 void need(bool c, const char* m) {
   if (!c) throw std::runtime_error(std::string("mrhip: ") + m);
 }
+// a kernel operand: defined, contiguous, of dtype st, on device d (checked on
+// the host before any launch; the kernels reinterpret raw pointers)
+void operand(const at::Tensor& t, at::ScalarType st, const at::Device& d, const char* what) {
+  if (!t.defined() || t.scalar_type() != st || t.device() != d || !t.is_contiguous())
+    throw std::runtime_error(std::string("mrhip: ") + what + ": expected a contiguous " + c10::toString(st) +
+                             " tensor on " + d.str() +
+                             (t.defined() ? std::string(", got ") + c10::toString(t.scalar_type()) + " on " +
+                                                t.device().str() + (t.is_contiguous() ? "" : " (strided)")
+                                          : std::string(", got an undefined tensor")));
+}
 }  // namespace
 
 // out[g] = sum_{e in seg g} r[src[e]] * w[e]
@@ -52,6 +62,13 @@ void pr_contrib(const at::Tensor& seg, const at::Tensor& src, const at::Tensor& 
 void pr_combine(const at::Tensor& seg, const at::Tensor& perm, const at::Tensor& recv, const at::Tensor& vid,
                 at::Tensor& acc) {
   const int64_t ng = seg.numel() - 1, nr = perm.numel();
+  const at::Device d = seg.device();
+  operand(seg, at::kLong, d, "plan_combine seg");
+  operand(perm, at::kInt, d, "plan_combine perm");
+  operand(vid, at::kInt, d, "plan_combine vid");
+  operand(recv, recv.scalar_type(), d, "plan_combine recv");
+  operand(acc, recv.scalar_type(), d, "plan_combine acc (recv dtype)");
+  need(ng <= 0 || vid.numel() >= ng, "plan_combine: one vid per group");
   if (ng <= 0) return;
   if (seg.is_cuda()) {
     at::Tensor grp = at::empty({ng}, opt(seg.device(), at::kFloat));
@@ -143,8 +160,14 @@ void plan_gather_reduce(const at::Tensor& seg, const at::Tensor& src, const at::
                         int64_t op, at::Tensor& out) {
   const int64_t ng = seg.numel() - 1, ne = src.numel();
   const bool hw = w.defined() && w.numel() > 0;
-  need(!hw || w.scalar_type() == x.scalar_type(), "plan weights must match value dtype");
-  need(out.scalar_type() == x.scalar_type() && out.numel() >= ng, "plan out");
+  const at::Device d = seg.device();
+  operand(seg, at::kLong, d, "plan_gather_reduce seg");
+  operand(src, at::kInt, d, "plan_gather_reduce src");
+  operand(x, x.scalar_type(), d, "plan_gather_reduce x");
+  if (hw) operand(w, x.scalar_type(), d, "plan_gather_reduce weights (value dtype)");
+  need(!hw || w.numel() == ne, "plan_gather_reduce: one weight per source id");
+  operand(out, x.scalar_type(), d, "plan_gather_reduce out (value dtype)");
+  need(out.numel() >= ng, "plan_gather_reduce: out smaller than the group count");
   if (ng <= 0) return;
   if (seg.is_cuda()) {
     at::Tensor scratch = at::empty({(int64_t)k::plan_scratch_bytes(ne)}, opt(seg.device(), at::kByte));
@@ -220,6 +243,11 @@ void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tens
 // all neighbour pairs per group: returns (edges [W,2] int64 (min,max), centre [W])
 std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre) {
   const int64_t ng = seg.numel() - 1;
+  need(ng >= 0, "wedges: seg holds ngroups + 1 offsets");
+  operand(seg, at::kLong, seg.device(), "wedges seg");
+  operand(nb, at::kLong, seg.device(), "wedges neighbours");
+  operand(centre, at::kLong, seg.device(), "wedges centre");
+  need(centre.numel() >= ng, "wedges: one centre per group");
   at::Tensor d = seg.narrow(0, 1, ng) - seg.narrow(0, 0, ng);
   at::Tensor cnt = at::floor_divide(d * (d - 1), 2);
   at::Tensor wscan = exclusive_scan(cnt.contiguous());

@@ -14,7 +14,10 @@ import sys
 from .._ext import C
 from ..parallel.comm import Comm, world
 from ..runtime.mapreduce import MapReduce
-from .variable import OinkError  # noqa: F401
+
+# errors of the native interpreter (variables, evaluator, commands:
+# csrc/oink/variable.cpp, oink.cpp)
+OinkError = C.OinkError
 
 
 def _world_of(ucomm: Comm, partitions):

@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from gpu_mapreduce_amd.oink.interp import OINK
-from gpu_mapreduce_amd.oink.variable import OinkError
+from gpu_mapreduce_amd.oink.interp import OinkError
 
 
 def run(script, tmp_path, monkeypatch, variables=None, comm=None):
