@@ -170,10 +170,21 @@ def bench_wordfreq(comm, args):
     chunks = []
     left = per_gpu
     i = 0
+    # MRH_WF_INPUT=contig: the input chunks as views of one pinned allocation
+    # (default: one pinned allocation per chunk, as a reader of separate files
+    # would hold them)
+    import os
+    contig = comm.is_cuda and os.environ.get("MRH_WF_INPUT", "") == "contig"
+    host = torch.empty(per_gpu, dtype=torch.uint8, pin_memory=True) if contig else None
     while left > 0:
         n = min(chunk, left)
         t = synth.zipf_text(n, seed=args.seed * 7919 + comm.rank * 1000 + i, device=comm.device)
-        chunks.append(t.cpu().pin_memory() if comm.is_cuda else t)
+        if contig:
+            off = per_gpu - left
+            host[off:off + n].copy_(t)
+            chunks.append(host[off:off + n])
+        else:
+            chunks.append(t.cpu().pin_memory() if comm.is_cuda else t)
         left -= n
         i += 1
     if comm.is_cuda:
