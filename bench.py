@@ -163,17 +163,31 @@ def bench_inverted_index_files(comm, args):
     from gpu_mapreduce_amd import MapReduce
     from gpu_mapreduce_amd.models.inverted_index import InvertedIndex
     from gpu_mapreduce_amd.utils import synth
-    base = "/dev/shm" if os.path.isdir("/dev/shm") else None
-    root = tempfile.mkdtemp(prefix=f"mrh_ii_{comm.rank}_", dir=base)
+    # a RAM-backed directory with room for the part files and the output (on
+    # every rank: one rank without room would leave its peers waiting in the
+    # job's collectives, so all ranks agree before any of them starts)
+    need = 2 * int(args.bytes_per_gpu) + (256 << 20)
+    base = next((d for d in ("/dev/shm", tempfile.gettempdir())
+                 if os.path.isdir(d) and shutil.disk_usage(d).free >= need), None)
+    root = None
+    files_ok = 0
     try:
-        files = synth.html_corpus(int(args.bytes_per_gpu), file_bytes=args.file_bytes, seed=args.seed, rank=comm.rank,
-                                  device=comm.device, link_gap=args.link_gap)
-        paths = []
-        for name, t in files:
-            pth = os.path.join(root, name)
-            t.cpu().numpy().tofile(pth)
-            paths.append((name, pth, t.numel()))
-        del files
+        if base is not None:
+            root = tempfile.mkdtemp(prefix=f"mrh_ii_{comm.rank}_", dir=base)
+            files = synth.html_corpus(int(args.bytes_per_gpu), file_bytes=args.file_bytes, seed=args.seed,
+                                      rank=comm.rank, device=comm.device, link_gap=args.link_gap)
+            paths = []
+            for name, t in files:
+                pth = os.path.join(root, name)
+                t.cpu().numpy().tofile(pth)
+                paths.append((name, pth, t.numel()))
+            del files
+            files_ok = 1
+    except OSError as e:
+        print(f"bench.py rank {comm.rank}: with_file_io: {e}", file=sys.stderr, flush=True)
+    try:
+        if comm.allreduce(files_ok, "min") == 0:
+            return {"skipped": f"a rank had no directory with {need >> 20} MiB free for the part files"}
         bufs = [torch.empty(n, dtype=torch.uint8, pin_memory=comm.is_cuda) for _, _, n in paths]
         outdir = os.path.join(root, "out")
 
@@ -204,7 +218,8 @@ def bench_inverted_index_files(comm, args):
                 "note": "part files read from the page cache (RAM-backed directory) into pinned memory by 8 threads, "
                         "the index text written to a file; steps=%d" % args.steps}
     finally:
-        shutil.rmtree(root, ignore_errors=True)
+        if root is not None:
+            shutil.rmtree(root, ignore_errors=True)
 
 
 def _free_port():
