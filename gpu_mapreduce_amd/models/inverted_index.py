@@ -50,7 +50,12 @@ PAD = 64
 class InvertedIndex:
     def __init__(self, mr: MapReduce, files, out_dir=None, pipelined=True, own_output=False, prefetch_next=None):
         """files: list of (name, uint8 tensor) for THIS rank (host tensors —
-        ideally pinned — or device tensors).
+        ideally pinned — or device tensors), or (name, tensor, ready) where
+        ready.result() blocks until the tensor holds the file's bytes (e.g. the
+        future of a read into a pinned buffer): it is waited for right before
+        that file's copy is issued, so reading file i+1 overlaps the copy and
+        map of file i (the reference freads each part file in its map,
+        cuda/InvertedIndex.cu:170-190).
 
         prefetch_next: the (name, tensor) files of the job that will run next on
         this rank (a job pipeline, e.g. a serving loop). While this job maps
@@ -70,7 +75,7 @@ class InvertedIndex:
         self._reserved = False
         # doc ids are global (rank-major) so a value means the same file name on
         # every rank after the shuffle; the reference ships the name string itself
-        all_names = mr.comm.allgather_object([n for n, _ in files])
+        all_names = mr.comm.allgather_object([f[0] for f in files])
         self.doc_base = sum(len(x) for x in all_names[: mr.me])
         self.max_files = max(len(x) for x in all_names)
         names = [n.encode() for lst in all_names for n in lst]
@@ -82,7 +87,7 @@ class InvertedIndex:
         self.is_cuda = dev.startswith("cuda")
         self.names_dev = pools.device_constant(dev, self.names)
         self.name_off_dev = pools.device_constant(dev, self.name_off)
-        maxlen = max((t.numel() for _, t in files), default=0)
+        maxlen = max((f[1].numel() for f in files), default=0)
         # persistent staging buffers: a ring of `streams` (0 = auto: 3, or
         # MRH_II_BUFS) so streams - 1 file copies are in flight while one file
         # maps: with the cross-job prefetch 2 / 3 / 4 buffers measured 19.75 /
@@ -114,6 +119,11 @@ class InvertedIndex:
             kv.reserve_grouping(int(part.n * f) + 1024, int(part.kdata.numel() * f) + 4096,
                                 int(part.vdata.numel() * f) + 4096)
 
+    def _wait_read(self, i):
+        f = self.files[i]
+        if len(f) > 2 and f[2] is not None:
+            f[2].result()
+
     def _map(self, itask, kv):
         if self._mapped:
             raise RuntimeError("InvertedIndex: a rank was given two map tasks (its files are mapped once)")
@@ -123,7 +133,9 @@ class InvertedIndex:
             kv.enable_grouping()
         empty = lambda: C.map_urls(torch.zeros(PAD, dtype=torch.uint8, device=self.dev), 0, 0)
         if not self.is_cuda:
-            for fid, (_, t) in enumerate(files):
+            for fid, f in enumerate(files):
+                self._wait_read(fid)
+                t = f[1]
                 buf = self.bufs[0]
                 buf[: t.numel()].copy_(t)
                 buf[t.numel():t.numel() + PAD].zero_()
@@ -149,6 +161,7 @@ class InvertedIndex:
             def issue(i):
                 b = (base + i) % nb
                 t = files[i][1]
+                self._wait_read(i)
                 ev = pools.take_prefetch(self.dev, b, t)  # copied by the previous job of a pipeline
                 if ev is not None:
                     ready[b] = ev
