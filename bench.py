@@ -222,19 +222,26 @@ def bench_inverted_index_files(comm, args):
             futs = [pool.submit(read_piece, j) for j in jobs]
             ready = [_FileRead([f for f, j in zip(futs, jobs) if j[0] == i]) for i in range(len(paths))]
             files = [(paths[i][0], bufs[i], ready[i]) for i in range(len(paths))]
-            n = InvertedIndex(MapReduce(comm), files, out_dir=outdir).run()
+            app = InvertedIndex(MapReduce(comm), files, out_dir=outdir)
+            n = app.run()
             for r in ready:
                 r.result()
+            write_s.append(app.write_s)
+            out_bytes.append(app.output.numel() if app.output is not None else 0)
             return n
+
+        write_s, out_bytes = [], []
 
         for _ in range(args.warmup):
             step()
         _sync(comm)
+        write_s.clear()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
         _sync(comm)
         dt = comm.allreduce((time.perf_counter() - t0) / args.steps, "max", dtype=torch.float64)
+        wr = comm.allreduce(sum(write_s) / max(1, len(write_s)), "max", dtype=torch.float64)
         # the reads alone (untimed above: they overlap the job)
         t0 = time.perf_counter()
         list(pool.map(read_piece, jobs))
@@ -243,7 +250,8 @@ def bench_inverted_index_files(comm, args):
             os.close(fd)
         pool.shutdown()
         total_in = comm.allreduce(sum(n for _, _, n in paths), "sum")
-        return {"ms_per_step": dt * 1e3, "read_ms": rd * 1e3, "read_threads": nthr, "input_GBps": total_in / dt / 1e9,
+        return {"ms_per_step": dt * 1e3, "read_ms": rd * 1e3, "read_threads": nthr,
+                "write_ms": wr * 1e3, "output_bytes": out_bytes[-1] if out_bytes else 0, "input_GBps": total_in / dt / 1e9,
                 "vs_reference_end_to_end": total_in / dt / 1e9 / REF_GBPS,
                 "note": "part files read from the page cache (RAM-backed directory) into pinned memory (32 MiB pieces "
                         "over read_threads threads, file i+1 read while file i is copied and mapped; read_ms: the "
@@ -503,7 +511,8 @@ def main():
             from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
             res.update(_extra(comm, "wordfreq", bench_wordfreq, args, bytes_per_gpu=args.wordfreq_bytes,
                               file_bytes=min(args.file_bytes, int(args.wordfreq_bytes)),
-                              steps=args.extra_steps, warmup=1))
+                              steps=args.extra_steps, warmup=6))  # steady state after ~6 jobs:
+            # warmup 1 / 2 / 6 -> 27.1 / 24.7 / 22.8 ms (profiles/r3_wordfreq_input.txt)
     res.update(rrec)
     res["ranks_joined"] = comm.size
     from gpu_mapreduce_amd.runtime import hbm_pool

@@ -37,6 +37,7 @@ an overwritten slot; pass `own_output=True` to get a private buffer.
 from __future__ import annotations
 
 import os
+import time
 
 import torch
 
@@ -102,6 +103,7 @@ class InvertedIndex:
         self._done = None
         self.exchanged = False
         self.nurls = 0
+        self.write_s = 0.0
 
     # -------------------------------------------------------------- map
     def _emit(self, kv, part):
@@ -220,8 +222,10 @@ class InvertedIndex:
             self.output_ready()
             os.makedirs(self.out_dir, exist_ok=True)
             path = os.path.join(self.out_dir, f"InvertedIndex-{self.mr.nprocs}-{self.mr.me}")
+            t = time.perf_counter()
             with open(path, "wb") as f:
-                f.write(host.numpy().tobytes())
+                f.write(memoryview(host.numpy()))  # straight from the pinned buffer, no bytes copy
+            self.write_s = time.perf_counter() - t
             MapReduce.count_io(write=host.numel())
 
     def output_ready(self):
