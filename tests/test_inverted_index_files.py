@@ -45,12 +45,12 @@ def test_inverted_index_waits_for_file_reads(tmp_path, dev):
     assert got == reference_inverted_index(files)
 
 
-def test_parallel_output_write(tmp_path):
+def test_output_write_from_buffer(tmp_path):
     import numpy as np
 
-    from gpu_mapreduce_amd.models.inverted_index import _WRITE_PIECE, _write_parallel
-    for n in (0, 5, _WRITE_PIECE, 3 * _WRITE_PIECE + 7):
+    from gpu_mapreduce_amd.models.inverted_index import _write_file
+    for n in (0, 5, 1 << 20, (48 << 20) + 7):
         a = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
         p = tmp_path / f"out{n}"
-        _write_parallel(str(p), memoryview(a))
+        _write_file(str(p), memoryview(a))
         assert p.read_bytes() == a.tobytes()
