@@ -54,3 +54,8 @@ def test_output_write_from_buffer(tmp_path):
         p = tmp_path / f"out{n}"
         _write_file(str(p), memoryview(a))
         assert p.read_bytes() == a.tobytes()
+    # rewriting a path with less data leaves exactly the new bytes
+    p = tmp_path / "again"
+    _write_file(str(p), memoryview(np.full(1000, 7, dtype=np.uint8)))
+    _write_file(str(p), memoryview(np.full(10, 3, dtype=np.uint8)))
+    assert p.read_bytes() == bytes([3] * 10)
