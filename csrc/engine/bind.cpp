@@ -692,6 +692,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("nlocal", &PageRankPlan::nlocal)
       .def_property_readonly("blocking", &PageRankPlan::blocking)
       .def_property_readonly("xcd_ranges", &PageRankPlan::xcd_ranges_count)
+      .def_property_readonly("layout", &PageRankPlan::layout)
+      .def_property_readonly("c_slice", &PageRankPlan::c_slice)
       .def_readwrite("use_graph", &PageRankPlan::use_graph)
       .def_property_readonly("graph_iterations", &PageRankPlan::graph_iterations)
       .def_readonly("nedge", &PageRankPlan::nedge)

@@ -235,11 +235,20 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
     : comm(std::move(c)), P(comm->size()), me(comm->rank()), dev(comm->device()), N(nvert), alpha(a) {
   nlocal = std::max<int64_t>(0, (N - me + P - 1) / P);
   at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2});
-  at::Tensor none;
-  to_source_owner(*comm, e, none);
-  nedge = e.size(0);
-  if (dev.is_cuda() && nedge < (int64_t(1) << 32) && N < (int64_t(1) << 31)) build_device(e.contiguous());
-  else build_host(e);
+  // several GPUs (or the forced-RCCL rank): destination-owned edges and a
+  // replicated c vector (build_device_dist); MRH_PR_DIST=partials keeps the
+  // source-owned plan with an all-to-all of per-destination partial sums
+  const char* dmode = std::getenv("MRH_PR_DIST");
+  const bool partials = dmode && std::strcmp(dmode, "partials") == 0;
+  if (dev.is_cuda() && comm->distributed() && !partials && N < (int64_t(1) << 31)) {
+    build_device_dist(e.contiguous());
+  } else {
+    at::Tensor none;
+    to_source_owner(*comm, e, none);
+    nedge = e.size(0);
+    if (dev.is_cuda() && nedge < (int64_t(1) << 32) && N < (int64_t(1) << 31)) build_device(e.contiguous());
+    else build_host(e);
+  }
   e = at::Tensor();
   const int64_t ngrp = seg_.numel() - 1;
   // one GPU, opt-in (MRH_PR_BLOCKING=1): propagation blocking (pbpr.hip).
@@ -284,48 +293,55 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
 //     source id) — the source ids are monotone, so the relabel is a
 //     sequential walk — and sorted on the destination bits;
 //  4. unpack: the int32 source stream + group head flags -> CSR segments.
-void PageRankPlan::build_device(const at::Tensor& e) {
+namespace {
+void pr_chk(hipError_t r, const char* what) {
+  if (r != hipSuccess) throw std::runtime_error(std::string("PageRankPlan: ") + what + ": " + hipGetErrorString(r));
+}
+// smallest b >= 1 with maxval < 2^b (capped at 31)
+int pr_bits_for(int64_t maxval) {
+  int b = 1;
+  while (b < 31 && (int64_t(1) << b) <= maxval) ++b;
+  return b;
+}
+// route packed u64 keys to ranks `dest` (engine shuffle, fixed 8-byte keys)
+at::Tensor route_u64(const Comm& comm, const at::Tensor& keys, const at::Tensor& dest) {
+  KV kv;
+  kv.n = keys.numel();
+  kv.kw = 8;
+  kv.vw = 0;
+  kv.kdata = keys.contiguous().view(at::kByte).reshape({-1});
+  kv.vdata = at::empty({0}, opt(comm.device(), at::kByte));
+  kv = exchange(std::move(kv), dest, comm);
+  return kv.kdata.view(at::kLong).reshape({-1});
+}
+}  // namespace
+
+// Steps 1-2 of both device builds. su: this rank's out-edges packed as
+// (local source << 32 | destination), sorted on the source bits (the run
+// lengths are the out-degrees). Sorts the nlocal vertices by degree
+// (descending, stable) and writes the new id of every old local id (nid),
+// order_, dangling_, invdeg_; degn (if want_degn): the degree of every new id.
+// Returns the number of dangling (out-degree 0) local vertices.
+int64_t PageRankPlan::relabel_by_degree(const at::Tensor& su, bool want_degn, at::Tensor& nid, at::Tensor& degn) {
   const hipStream_t s = at::hip::getCurrentHIPStream();
-  const bool dist = comm->distributed();
-  const int64_t nlmax = (N + P - 1) / P;
-  auto chk = [](hipError_t r, const char* what) {
-    if (r != hipSuccess) throw std::runtime_error(std::string("PageRankPlan: ") + what + ": " + hipGetErrorString(r));
-  };
-  auto bits_for = [](int64_t maxval) {
-    int b = 1;
-    while (b < 31 && (int64_t(1) << b) <= maxval) ++b;
-    return b;
-  };
-  // 1. by source
-  at::Tensor su;
-  {
-    at::Tensor packed = at::empty({nedge}, opt(dev, at::kLong));
-    k::pr_pack_src(e.data_ptr<int64_t>(), nedge, P, reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
-    su = radix_sort_keys(packed, 32, 32 + bits_for(std::max<int64_t>(nlocal - 1, 0)), false);
-  }
+  const int64_t ne = su.numel();
   at::Tensor deg = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
-  chk(hipMemsetAsync(deg.data_ptr(), 0, deg.numel() * 4, s), "hipMemsetAsync");
-  if (nedge > 0) {
-    at::Tensor flags = at::empty({nedge}, opt(dev, at::kInt));
-    k::pr_heads(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, reinterpret_cast<uint32_t*>(flags.data_ptr()),
-                s);
+  pr_chk(hipMemsetAsync(deg.data_ptr(), 0, deg.numel() * 4, s), "hipMemsetAsync");
+  if (ne > 0) {
+    at::Tensor flags = at::empty({ne}, opt(dev, at::kInt));
+    k::pr_heads(reinterpret_cast<const uint64_t*>(su.data_ptr()), ne, reinterpret_cast<uint32_t*>(flags.data_ptr()), s);
     at::Tensor useg = segments_from_flags(flags);
     flags = at::Tensor();
     k::pr_run_degree(reinterpret_cast<const uint64_t*>(su.data_ptr()), useg.data_ptr<int64_t>(), useg.numel() - 1,
                      reinterpret_cast<uint32_t*>(deg.data_ptr()), s);
   }
-  // 2. vertices by degree
-  at::Tensor nid = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
+  nid = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
   order_ = at::empty({nlocal}, opt(dev, at::kLong));
   dangling_ = at::empty({nlocal}, opt(dev, at::kByte));
   invdeg_ = at::empty({nlocal}, opt(dev, at::kFloat));
   at::Tensor nd = at::empty({1}, opt(dev, at::kLong));
-  chk(hipMemsetAsync(nd.data_ptr(), 0, 8, s), "hipMemsetAsync");
-  // XCD source ranges (one GPU; MRH_PR_XCD=0 disables): see xcd_ranges()
-  const char* xenv = std::getenv("MRH_PR_XCD");
-  const char* benv = std::getenv("MRH_PR_BLOCKING");  // propagation blocking needs the plain layout
-  const bool want_xcd = !dist && !(xenv && *xenv == '0') && !(benv && *benv == '1');
-  at::Tensor degn;
+  pr_chk(hipMemsetAsync(nd.data_ptr(), 0, 8, s), "hipMemsetAsync");
+  degn = at::Tensor();
   if (nlocal > 0) {
     at::Tensor dkey = at::empty({nlocal}, opt(dev, at::kLong)), io = at::empty({nlocal}, opt(dev, at::kInt));
     k::pr_degkey(reinterpret_cast<const uint32_t*>(deg.data_ptr()), nlocal, reinterpret_cast<uint64_t*>(dkey.data_ptr()),
@@ -333,14 +349,35 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     // 32-bit key; constant high digits (every degree < 2^24) are skipped
     at::Tensor ord = std::get<1>(radix_sort_pairs(dkey, io, 0, 32, true));
     dkey = io = at::Tensor();
-    if (want_xcd) degn = at::empty({nlocal}, opt(dev, at::kInt));
+    if (want_degn) degn = at::empty({nlocal}, opt(dev, at::kInt));
     k::pr_relabel(reinterpret_cast<const uint32_t*>(ord.data_ptr()), reinterpret_cast<const uint32_t*>(deg.data_ptr()),
                   nlocal, nid.data_ptr<int32_t>(), order_.data_ptr<int64_t>(), dangling_.data_ptr<uint8_t>(),
                   invdeg_.data_ptr<float>(), reinterpret_cast<unsigned long long*>(nd.data_ptr()),
                   degn.defined() ? degn.data_ptr<int32_t>() : nullptr, s);
   }
-  deg = at::Tensor();
-  const int64_t ndl = nd.item<int64_t>(), nactive = std::max<int64_t>(nlocal - ndl, 0);
+  return nd.item<int64_t>();
+}
+
+void PageRankPlan::build_device(const at::Tensor& e) {
+  const hipStream_t s = at::hip::getCurrentHIPStream();
+  const bool dist = comm->distributed();
+  const int64_t nlmax = (N + P - 1) / P;
+  auto bits_for = pr_bits_for;
+  // 1. by source
+  at::Tensor su;
+  {
+    at::Tensor packed = at::empty({nedge}, opt(dev, at::kLong));
+    k::pr_pack_src(e.data_ptr<int64_t>(), nedge, P, reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
+    su = radix_sort_keys(packed, 32, 32 + bits_for(std::max<int64_t>(nlocal - 1, 0)), false);
+  }
+  // 2. vertices by degree; XCD source ranges (one GPU; MRH_PR_XCD=0
+  // disables): see xcd_ranges()
+  const char* xenv = std::getenv("MRH_PR_XCD");
+  const char* benv = std::getenv("MRH_PR_BLOCKING");  // propagation blocking needs the plain layout
+  const bool want_xcd = !dist && !(xenv && *xenv == '0') && !(benv && *benv == '1');
+  at::Tensor nid, degn;
+  const int64_t ndl = relabel_by_degree(su, want_xcd, nid, degn);
+  const int64_t nactive = std::max<int64_t>(nlocal - ndl, 0);
   // 3. by destination group, new source ids in the low word; with XCD source
   // ranges the groups are (range, destination)
   const int64_t himax = !dist ? std::max<int64_t>(N - 1, 0) : P * nlmax - 1;
@@ -400,6 +437,160 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nullptr, (int64_t(1) << dbits) - 1, vid_.data_ptr<int32_t>(), s);
   }
   ndangling = comm->allreduce(ndl, Comm::SUM);
+}
+
+// Multi-GPU device build: destination-owned edges, replicated c vector.
+// Every rank keeps the in-edges of the vertices it owns and gathers c = r /
+// outdeg of their sources from a full copy of c, which one in-place RCCL
+// all-gather of the ranks' c slices refreshes per iteration — the one
+// collective of an iteration besides the 16-byte (L1 delta, dangling mass)
+// allreduce. Each rank then runs exactly the one-GPU iteration: XCD source
+// ranges over the gathered vector, the fused tile step over its own
+// destinations, no combine of received partial sums. With 288 GB of HBM per
+// GPU the replicated vector costs nothing (RMAT-26: 256 MB), and the
+// all-gather moves only the active (out-degree > 0) sources: each rank's
+// slice is its first S new ids (degree-descending; the dangling ids are last
+// and contribute c = 0), S = the largest active count.
+//   1. edges -> the source owner, vertices owned by sigma(v) % P (vmix.h:
+//      balanced for R-MAT, whose v % P is not); out-degrees + degree relabel
+//      (relabel_by_degree);
+//   2. edges -> the destination owner as (sigma(v), slot of the source in c);
+//   3. XCD source ranges on the interleaved order gid = new id * P + rank
+//      (every rank's hot sources first), from the all-gathered degrees;
+//   4. sort by (range, new destination id); unpack as build_device.
+// One rank (the forced-RCCL mode) uses sigma = identity: the plan and its
+// results are then bitwise those of build_device.
+void PageRankPlan::build_device_dist(const at::Tensor& e) {
+  const hipStream_t s = at::hip::getCurrentHIPStream();
+  dist_dev_ = true;
+  mix_ = P > 1;
+  {
+    const char* m = std::getenv("MRH_PR_MIX");  // 0: owner = v % P (the edge plan's rule; for comparison)
+    if (m && *m == '0') mix_ = false;
+  }
+  const int64_t nlmax = (N + P - 1) / P;
+  // 1. to the source owner; out-degrees and relabel
+  at::Tensor su;
+  {
+    const int64_t n0 = e.size(0);
+    at::Tensor packed = at::empty({n0}, opt(dev, at::kLong)), dest = at::empty({n0}, opt(dev, at::kInt));
+    k::pr_mix_pack(e.data_ptr<int64_t>(), n0, P, N, mix_, reinterpret_cast<uint64_t*>(packed.data_ptr()),
+                   dest.data_ptr<int32_t>(), s);
+    packed = route_u64(*comm, packed, dest);
+    dest = at::Tensor();
+    k::pr_localize(reinterpret_cast<uint64_t*>(packed.data_ptr()), packed.numel(), P, s);
+    su = radix_sort_keys(packed, 32, 32 + pr_bits_for(std::max<int64_t>(nlocal - 1, 0)), false);
+  }
+  const char* xenv = std::getenv("MRH_PR_XCD");
+  const bool want_xcd = !(xenv && *xenv == '0');
+  at::Tensor nid, degn;
+  const int64_t ndl = relabel_by_degree(su, want_xcd, nid, degn);
+  const int64_t nactive = std::max<int64_t>(nlocal - ndl, 0);
+  ndangling = comm->allreduce(ndl, Comm::SUM);
+  // slice length: the largest active count, a multiple of 16 (64-byte aligned slices)
+  int64_t S = comm->allreduce(nactive, Comm::MAX);
+  S = (std::max<int64_t>(S, 1) + 15) / 16 * 16;
+  if (P * S >= (int64_t(1) << 31)) throw std::runtime_error("PageRankPlan: replicated c vector needs P * S < 2^31");
+  S_ = S;
+  // 2. to the destination owner
+  at::Tensor pk;
+  {
+    const int64_t n1 = su.numel();
+    pk = at::empty({n1}, opt(dev, at::kLong));
+    at::Tensor dest = at::empty({n1}, opt(dev, at::kInt));
+    k::pr_pack_dst(reinterpret_cast<const uint64_t*>(su.data_ptr()), n1, P, (int64_t)me * S, nid.data_ptr<int32_t>(),
+                   reinterpret_cast<uint64_t*>(pk.data_ptr()), dest.data_ptr<int32_t>(), s);
+    su = at::Tensor();
+    pk = route_u64(*comm, pk, dest);
+  }
+  nedge = pk.numel();
+  if (nedge >= (int64_t(1) << 32)) throw std::runtime_error("PageRankPlan: >= 2^32 in-edges on one rank");
+  // 3. XCD source ranges over the interleaved global order; the degree of
+  // every gid is the all-gathered degree array read column-major
+  const int dbits = pr_bits_for(std::max<int64_t>(nlocal - 1, 0));
+  std::vector<int64_t> rb, redge;
+  if (degn.defined()) {
+    at::Tensor dl = at::zeros({S}, opt(dev, at::kInt));
+    const int64_t k0 = std::min(S, nlocal);
+    if (k0 > 0) dl.narrow(0, 0, k0).copy_(degn.narrow(0, 0, k0));
+    at::Tensor dall = at::empty({P * S}, opt(dev, at::kInt));
+    comm->allgather_bytes(dl.data_ptr(), dall.data_ptr(), S * 4);
+    at::Tensor dg = dall.view({P, S}).t().contiguous().view({-1});
+    dl = dall = at::Tensor();
+    xcd_ranges(dg, P * S, dbits, rb, redge);
+  }
+  degn = at::Tensor();
+  const int nhot = rb.empty() ? 0 : (int)rb.size() - 1;
+  at::Tensor rbd;
+  if (nhot > 0) {
+    std::vector<int32_t> rb32(rb.begin(), rb.end());
+    rbd = at::from_blob(rb32.data(), {(int64_t)rb32.size()}, opt(at::kCPU, at::kInt)).to(dev);
+  }
+  int rbits = 0;
+  while ((1 << rbits) < nhot + 1) ++rbits;
+  if (nhot == 0) rbits = 0;
+  // 4. sort by (range, destination), unpack
+  at::Tensor sorted;
+  {
+    at::Tensor key = at::empty({nedge}, opt(dev, at::kLong));
+    k::pr_pack_gather(reinterpret_cast<const uint64_t*>(pk.data_ptr()), nedge, P, S, nid.data_ptr<int32_t>(),
+                      nhot > 0 ? rbd.data_ptr<int32_t>() : nullptr, nhot, dbits,
+                      reinterpret_cast<uint64_t*>(key.data_ptr()), s);
+    pk = at::Tensor();
+    sorted = radix_sort_keys(key, 32, 32 + dbits + rbits, false);
+  }
+  src_ = at::empty({nedge}, opt(dev, at::kInt));
+  {
+    at::Tensor flags = at::empty({nedge}, opt(dev, at::kInt));
+    k::pr_unpack(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), nedge, src_.data_ptr<int32_t>(),
+                 reinterpret_cast<uint32_t*>(flags.data_ptr()), s);
+    seg_ = nedge > 0 ? segments_from_flags(flags) : at::zeros({1}, opt(dev, at::kLong));
+  }
+  const int64_t ngrp = seg_.numel() - 1;
+  at::Tensor hi = at::empty({std::max<int64_t>(ngrp, 1)}, opt(dev, at::kLong));
+  k::pr_group_hi(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), seg_.data_ptr<int64_t>(), ngrp,
+                 hi.data_ptr<int64_t>(), s);
+  sorted = at::Tensor();
+  w_ = at::empty({0}, opt(dev, at::kFloat));
+  send_ = at::empty({ngrp}, opt(dev, at::kFloat));
+  // the fused tile step always (R = 1: no hot ranges)
+  xr_ = nhot + 1;
+  xtile_ = (nlocal + (int64_t(1) << k::pr_tile_bits()) - 1) >> k::pr_tile_bits();
+  ghi_ = at::empty({std::max<int64_t>(ngrp, 1)}, opt(dev, at::kInt));
+  k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nullptr, (int64_t(1) << dbits) - 1, ghi_.data_ptr<int32_t>(), s);
+  xoff_ = at::empty({xr_ * (xtile_ + 1)}, opt(dev, at::kLong));
+  k::pr_range_offsets(hi.data_ptr<int64_t>(), ngrp, dbits, xr_, xtile_, xoff_.data_ptr<int64_t>(), s);
+  if (nhot > 0 && ngrp > 0) {
+    // exact first edge of every range on this rank (the gather's wave
+    // schedule); the ranges themselves came from the global degrees
+    at::Tensor first = xoff_.view({xr_, xtile_ + 1}).select(1, 0).contiguous();
+    std::vector<int64_t> fg = to_vec(first), sg = to_vec(seg_);
+    redge.clear();
+    for (int64_t r = 0; r < xr_; ++r) redge.push_back(sg[std::min<int64_t>(fg[r], ngrp)]);
+    redge.push_back(nedge);
+    xcd_schedule(redge);
+  }
+  // the replicated c vector: P slices of S; the tile step writes this rank's
+  // nlocal entries at me * S (entries past S are dangling, c = 0, and land in
+  // the next slice, which the all-gather then overwrites), hence the slack
+  cfull_ = at::zeros({P * S + nlmax + 64}, opt(dev, at::kFloat));
+  c_ = cfull_.narrow(0, (int64_t)me * S, nlocal);
+}
+
+// one multi-GPU iteration from r into rn: gather from the replicated c,
+// fused tile step (writes this rank's c slice in place), (L1, dangling)
+// partials -> allreduce, in-place all-gather of the c slices
+void PageRankPlan::launch_iter_dist(const at::Tensor& r, at::Tensor& rn) {
+  if (six_.defined()) seg_gather_reduce(six_, src_, cfull_, at::Tensor(), 0, send_);
+  const double base = (1.0 - alpha) / (double)N;
+  const hipStream_t s = at::hip::getCurrentHIPStream();
+  k::pr_tile_step(send_.data_ptr<float>(), ghi_.data_ptr<int32_t>(), xoff_.data_ptr<int64_t>(), (int)xr_, xtile_,
+                  nlocal, r.data_ptr<float>(), rn.data_ptr<float>(), dangling_.data_ptr<uint8_t>(), (float)base,
+                  (float)alpha, stats_.data_ptr<double>() + 1, 1.0 / (double)N, invdeg_.data_ptr<float>(),
+                  c_.data_ptr<float>(), part_.data_ptr<double>(), s);
+  k::pr_partials_sum(part_.data_ptr<double>(), xtile_, stats_.data_ptr<double>(), s);
+  comm->allreduce_tensor(stats_, Comm::SUM);
+  comm->allgather_bytes(c_.data_ptr(), cfull_.data_ptr(), S_ * 4);
 }
 
 // XCD source ranges. Each XCD has its own 4 MiB L2; the pull gather reads
@@ -618,7 +809,7 @@ void PageRankPlan::reset() {
   if (!r_.defined() || r_.numel() != nlocal) {
     r_ = at::empty({nlocal}, opt(dev, at::kFloat));
     rn_ = at::empty_like(r_);
-    c_ = at::empty_like(r_);
+    if (!dist_dev_) c_ = at::empty_like(r_);  // dist: c_ is this rank's slice of cfull_
   }
   r_.fill_(1.0 / (double)N);
   at::mul_out(c_, r_, invdeg_);
@@ -627,6 +818,7 @@ void PageRankPlan::reset() {
   stats_.narrow(0, 1, 1).fill_((double)ndangling / (double)N);
   dmass_ = stats_.narrow(0, 1, 1);  // the dangling mass of the previous iteration
   acc_.zero_();
+  if (dist_dev_) comm->allgather_bytes(c_.data_ptr(), cfull_.data_ptr(), S_ * 4);
 }
 
 // one XCD-path iteration: gather + segmented reduce of c into send_, then
@@ -707,6 +899,12 @@ void PageRankPlan::graph_build() {
 }
 
 void PageRankPlan::step() {
+  if (dist_dev_) {
+    launch_iter_dist(r_, rn_);
+    dmass_ = stats_.narrow(0, 1, 1);
+    std::swap(r_, rn_);
+    return;
+  }
   if (pb_) {
     const hipStream_t s = at::hip::getCurrentHIPStream();
     k::pb_phase1(pb_src_.data_ptr<int32_t>(), pb_out_.data_ptr<int32_t>(), nedge, c_.data_ptr<float>(),
@@ -778,7 +976,13 @@ int PageRankPlan::run(int maxiter, double tol) {
 
 double PageRankPlan::delta() const { return stats_[0].item<double>(); }
 
-at::Tensor PageRankPlan::ids() const { return order_ * P + me; }
+at::Tensor PageRankPlan::ids() const {
+  if (!dist_dev_) return order_ * P + me;
+  at::Tensor out = at::empty({nlocal}, opt(dev, at::kLong));
+  k::pr_unmix_ids(order_.data_ptr<int64_t>(), nlocal, P, me, N, mix_, out.data_ptr<int64_t>(),
+                  at::hip::getCurrentHIPStream());
+  return out;
+}
 
 // ====================================================================== triangles
 

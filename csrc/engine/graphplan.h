@@ -120,6 +120,15 @@ class PageRankPlan {
   // tensor-op twin on the CPU engine
   void build_device(const at::Tensor& e);
   void build_host(const at::Tensor& e);
+  // out-degrees of source-sorted packed edges + the degree relabel (both
+  // device builds); returns the local dangling count
+  int64_t relabel_by_degree(const at::Tensor& su, bool want_degn, at::Tensor& nid, at::Tensor& degn);
+  // several GPUs: destination-owned edges, replicated c vector (graphplan.cpp)
+  void build_device_dist(const at::Tensor& e);
+  void launch_iter_dist(const at::Tensor& r, at::Tensor& rn);
+  bool dist_dev_ = false, mix_ = false;
+  int64_t S_ = 0;      // c slice length per rank
+  at::Tensor cfull_;   // the replicated c vector, P slices of S_ (+ slack)
   // several ranks: the destination-owner side of the exchange from the
   // group destinations ujv (global ids) and the new id of every old local id
   void build_exchange(const at::Tensor& ujv, const at::Tensor& new_of_old);
@@ -132,6 +141,10 @@ class PageRankPlan {
 
  public:
   bool blocking() const { return pb_; }
+  // "replicated" (multi-GPU: destination-owned edges + all-gathered c),
+  // "partials" (source-owned + all-to-all of partial sums), "local"
+  std::string layout() const { return dist_dev_ ? "replicated" : comm->distributed() ? "partials" : "local"; }
+  int64_t c_slice() const { return S_; }
   int64_t xcd_ranges_count() const { return xr_; }
   // fixed-count run() replays a captured HIP graph (MRH_PR_GRAPH=0: off)
   bool use_graph = true;

@@ -13,6 +13,7 @@
 #include "common.h"
 #include "launch.h"
 #include "segred.h"
+#include "vmix.h"
 #include "wavesegred.h"
 
 namespace mrh {
@@ -146,6 +147,83 @@ __global__ __launch_bounds__(NT) void k_pr_pack(const uint64_t* __restrict__ su,
     if (rb) hi |= (uint64_t)pr_range_of(src, rb, nr) << dbits;
     out[i] = (hi << 32) | src;
   }
+}
+
+// ---- multi-GPU plan (graphplan.cpp build_device_dist): vertex v is owned by
+// rank sigma(v) % P as local id sigma(v) / P (vmix.h; sigma = identity when
+// mix == 0). Edges move twice: to the source owner (out-degrees, relabel) and
+// to the destination owner, which gathers c = r / outdeg from the replicated
+// (all-gathered) c vector.
+
+// edge (u, v) -> packed (sigma(u) << 32 | sigma(v)), destination rank
+// sigma(u) % P
+__global__ __launch_bounds__(NT) void k_pr_mix_pack(const int64_t* __restrict__ e, int64_t n, int P, int64_t N, int b,
+                                                    int mix, uint64_t* __restrict__ out, int32_t* __restrict__ dest) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
+    uint64_t u = (uint64_t)__builtin_nontemporal_load(e + 2 * i), v = (uint64_t)__builtin_nontemporal_load(e + 2 * i + 1);
+    if (mix) {
+      u = dev::vmix(u, N, b);
+      v = dev::vmix(v, N, b);
+    }
+    out[i] = (u << 32) | v;
+    dest[i] = (int32_t)(u % (uint64_t)P);
+  }
+}
+
+// at the source owner: (su << 32 | sv) -> (su / P << 32 | sv), in place
+__global__ __launch_bounds__(NT) void k_pr_localize(uint64_t* __restrict__ p, int64_t n, int P) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
+    const uint64_t x = p[i];
+    p[i] = (((x >> 32) / (uint64_t)P) << 32) | (x & 0xffffffffull);
+  }
+}
+
+// source-sorted (lu << 32 | sv) -> (sv << 32 | pos), pos = me * S + nid[lu]:
+// the source's slot in the all-gathered c vector (rank-major slices of S
+// entries); destination rank sv % P
+__global__ __launch_bounds__(NT) void k_pr_pack_dst(const uint64_t* __restrict__ su, int64_t n, int P, int64_t base,
+                                                    const int32_t* __restrict__ nid, uint64_t* __restrict__ out,
+                                                    int32_t* __restrict__ dest) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
+    const uint64_t x = __builtin_nontemporal_load(su + i);
+    const uint64_t sv = x & 0xffffffffull;
+    const uint64_t pos = (uint64_t)(base + nid[x >> 32]);
+    out[i] = (sv << 32) | pos;
+    dest[i] = (int32_t)(sv % (uint64_t)P);
+  }
+}
+
+// at the destination owner: (sv << 32 | pos) -> the gather's sort key:
+// hi = (source range << dbits) | new destination id nid[sv / P], lo = pos.
+// The source range is found on the interleaved global order gid = (pos % S)
+// * P + pos / S (every rank's hottest sources first), so a range's sources
+// are P contiguous pieces of the c vector whose total fits one XCD's L2
+__global__ __launch_bounds__(NT) void k_pr_pack_gather(const uint64_t* __restrict__ in, int64_t n, int P, int64_t S,
+                                                       const int32_t* __restrict__ nid, const int32_t* __restrict__ rb,
+                                                       int nr, int dbits, uint64_t* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
+    const uint64_t x = __builtin_nontemporal_load(in + i);
+    const uint32_t pos = (uint32_t)x;
+    uint64_t hi = (uint64_t)(uint32_t)nid[(x >> 32) / (uint64_t)P];
+    if (rb) {
+      const uint32_t gid = (uint32_t)((pos % (uint64_t)S) * (uint64_t)P + pos / (uint64_t)S);
+      hi |= (uint64_t)pr_range_of(gid, rb, nr) << dbits;
+    }
+    out[i] = (hi << 32) | pos;
+  }
+}
+
+// global ids of the owned vertices: ids[i] = sigma^-1(order[i] * P + me)
+__global__ __launch_bounds__(NT) void k_pr_unmix_ids(const int64_t* __restrict__ order, int64_t n, int P, int me,
+                                                     int64_t N, int b, int mix, int64_t* __restrict__ ids) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t y = (uint64_t)order[i] * (uint64_t)P + (uint64_t)me;
+  ids[i] = (int64_t)(mix ? dev::vunmix(y, N, b) : y);
 }
 
 // sorted packed keys -> the int32 source stream of the gather and the u32
@@ -647,6 +725,36 @@ void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, co
   if (n <= 0) return;
   hipLaunchKernelGGL(k_pr_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, nlmax, local ? 1 : 0, nid, rb, nr,
                      dbits, out);
+  MRH_CHECK_LAUNCH();
+}
+void pr_mix_pack(const int64_t* e, int64_t n, int P, int64_t N, bool mix, uint64_t* out, int32_t* dest, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_mix_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, e, n, P, N, dev::vmix_bits(N), mix ? 1 : 0,
+                     out, dest);
+  MRH_CHECK_LAUNCH();
+}
+void pr_localize(uint64_t* p, int64_t n, int P, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_localize, dim3(pr_grid_stride(n)), dim3(NT), 0, s, p, n, P);
+  MRH_CHECK_LAUNCH();
+}
+void pr_pack_dst(const uint64_t* su, int64_t n, int P, int64_t base, const int32_t* nid, uint64_t* out, int32_t* dest,
+                 hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_pack_dst, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, base, nid, out, dest);
+  MRH_CHECK_LAUNCH();
+}
+void pr_pack_gather(const uint64_t* in, int64_t n, int P, int64_t S, const int32_t* nid, const int32_t* rb, int nr,
+                    int dbits, uint64_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  check_arg(S > 0 && P * S < (int64_t(1) << 31), "pr_pack_gather: 0 < P * S < 2^31");
+  hipLaunchKernelGGL(k_pr_pack_gather, dim3(pr_grid_stride(n)), dim3(NT), 0, s, in, n, P, S, nid, rb, nr, dbits, out);
+  MRH_CHECK_LAUNCH();
+}
+void pr_unmix_ids(const int64_t* order, int64_t n, int P, int me, int64_t N, bool mix, int64_t* ids, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_unmix_ids, dim3(pr_grid(n)), dim3(NT), 0, s, order, n, P, me, N, dev::vmix_bits(N),
+                     mix ? 1 : 0, ids);
   MRH_CHECK_LAUNCH();
 }
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s) {

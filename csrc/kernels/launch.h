@@ -202,6 +202,20 @@ void sample_i64(const int64_t* in, int64_t n, int64_t stride, int64_t ns, int64_
 // rb[nr] form range nr; the range goes above the dbits destination bits
 void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, const int32_t* rb,
              int nr, int dbits, uint64_t* out, hipStream_t s);
+// multi-GPU plan (owner of v = sigma(v) % P, vmix.h; mix false: sigma = id):
+// edges -> (sigma(u) << 32 | sigma(v)) + source owner; (su << 32 | sv) ->
+// (su / P << 32 | sv) in place; source-sorted (lu << 32 | sv) -> (sv << 32 |
+// base + nid[lu]) + destination owner; at the destination owner (sv << 32 |
+// pos) -> ((range << dbits | nid[sv / P]) << 32 | pos), the range of the
+// interleaved source id (pos % S) * P + pos / S; owned global ids
+// sigma^-1(order * P + me)
+void pr_mix_pack(const int64_t* e, int64_t n, int P, int64_t N, bool mix, uint64_t* out, int32_t* dest, hipStream_t s);
+void pr_localize(uint64_t* p, int64_t n, int P, hipStream_t s);
+void pr_pack_dst(const uint64_t* su, int64_t n, int P, int64_t base, const int32_t* nid, uint64_t* out, int32_t* dest,
+                 hipStream_t s);
+void pr_pack_gather(const uint64_t* in, int64_t n, int P, int64_t S, const int32_t* nid, const int32_t* rb, int nr,
+                    int dbits, uint64_t* out, hipStream_t s);
+void pr_unmix_ids(const int64_t* order, int64_t n, int P, int me, int64_t N, bool mix, int64_t* ids, hipStream_t s);
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s);
 void pr_group_hi(const uint64_t* sorted, const int64_t* seg, int64_t ngrp, int64_t* hi, hipStream_t s);
 void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int64_t dmask, int32_t* vid, hipStream_t s);

@@ -216,6 +216,23 @@ def case_pagerank(comm):
     return edges, ids.cpu().numpy(), r.cpu().numpy().copy()
 
 
+def case_pagerank_ranges(comm):
+    """RMAT-14 with the XCD source ranges forced on (tiny L2 budget): on
+    device engines the replicated-c multi-GPU plan (graphplan.cpp
+    build_device_dist) with several layers of ranges"""
+    import numpy as np
+    import gpu_mapreduce_amd as g
+    from gpu_mapreduce_amd.models.pagerank import PageRank, rmat_map
+    os.environ["MRH_PR_L2_BYTES"] = "4096"
+    mr = g.MapReduce(comm)
+    rmat_map(mr, 14, 16, seed=9)
+    edges = mr.kv.kdata.view(torch.int64).view(-1, 2).cpu().numpy().copy()
+    pr = PageRank(mr, 1 << 14).build()
+    pr.run(15)
+    ids, r = pr.ranks()
+    return edges, ids.cpu().numpy(), r.cpu().numpy().copy(), pr.layout, pr.xcd_ranges, pr.nedge
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_pagerank_distributed(world):
     import numpy as np

@@ -67,3 +67,25 @@ def test_shuffle_is_deterministic_gpu():
     assert all(same for same, _, _ in out.values()), out
     assert sum(n for _, n, _ in out.values()) == 2 * 3000
     assert sum(u for _, _, u in out.values()) == 211
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pagerank_replicated_plan_gpu(world):
+    """the multi-GPU PageRank plan (destination-owned edges, all-gathered c,
+    sigma-mixed vertex owners, XCD source ranges on the interleaved order)
+    against the float64 oracle; R-MAT in-edges spread evenly over the ranks"""
+    from gpu_mapreduce_amd.models.pagerank import reference_pagerank
+    out = run_world("case_pagerank_ranges", world, DEV)
+    edges = np.concatenate([out[r][0] for r in range(world)])
+    ref = reference_pagerank(edges, 1 << 14, iters=15)
+    got = np.full(1 << 14, np.nan)
+    for r in range(world):
+        _, ids, rk, layout, nranges, _ = out[r]
+        assert layout == "replicated"
+        assert nranges > 9  # several layers of 8 ranges + the cold range
+        got[ids] = rk
+    assert not np.isnan(got).any()  # every vertex owned exactly once
+    np.testing.assert_allclose(got, ref, rtol=2e-4, atol=1e-9)
+    ne = [out[r][5] for r in range(world)]
+    assert sum(ne) == len(edges)
+    assert max(ne) < 1.25 * sum(ne) / world, ne  # v % P would give rank 0 0.76^k of them

@@ -169,3 +169,50 @@ def test_pagerank_hip_graph_replay_matches_plain_steps():
             _, got = pr.ranks()
             assert torch.equal(got, plain), iters
         assert pr.graph_iterations - before == 2 * 2 * (iters // 2)
+
+
+FORCED_CHILD = r"""
+import os, sys, numpy as np, torch
+import gpu_mapreduce_amd as g
+from gpu_mapreduce_amd.models.pagerank import PageRank, rmat_map
+os.environ["MRH_PR_L2_BYTES"] = "65536"
+comm = g.Comm(device="cuda")
+mr = g.MapReduce(comm)
+rmat_map(mr, 18, 16, seed=7)
+pr = PageRank(mr, 1 << 18).build()
+for it in (20, 7):
+    pr.reset()
+    pr.run(it)
+ids, r = pr.ranks()
+out = np.zeros(1 << 18, dtype=np.float32)
+out[ids.cpu().numpy()] = r.cpu().numpy()
+np.save(sys.argv[1], out)
+print(pr.layout, pr.xcd_ranges, comm.native.transport)
+"""
+
+
+@pytest.mark.gpu
+def test_pagerank_forced_rccl_replicated_plan_is_bitwise_local(tmp_path):
+    """MRH_FORCE_RCCL=1: one rank runs the multi-GPU plan (edges through two
+    RCCL exchanges, c refreshed by an in-place all-gather, stats by an
+    allreduce every iteration); with sigma = identity at one rank its ranks
+    equal the local plan's (HIP-graph replay) bit for bit"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res, info = {}, {}
+    for flag in ("0", "1"):
+        env = dict(os.environ, MRH_FORCE_RCCL=flag, PYTHONPATH=root)
+        for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+            env.pop(k, None)
+        path = str(tmp_path / f"f{flag}.npy")
+        p = subprocess.run([sys.executable, "-c", FORCED_CHILD, path], env=env, cwd=root, capture_output=True,
+                           text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-3000:]
+        info[flag] = p.stdout.split()[-3:]
+        res[flag] = np.load(path)
+    assert info["0"][0] == "local" and info["0"][2] == "local", info
+    assert info["1"][0] == "replicated" and info["1"][2] == "rccl", info
+    assert info["0"][1] == info["1"][1] and int(info["1"][1]) > 9, info  # the same XCD ranges
+    assert np.array_equal(res["0"], res["1"])
