@@ -712,6 +712,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            },
            py::call_guard<py::gil_scoped_release>())
       .def_readonly("nvert", &TriangleGraph::nvert)
+      .def_readonly("split", &TriangleGraph::split)
+      .def_readonly("u0", &TriangleGraph::u0_)
+      .def_readonly("u1", &TriangleGraph::u1_)
       .def_readonly("nedge", &TriangleGraph::nedge)
       .def_readonly("rowptr", &TriangleGraph::rowptr)
       .def_readonly("col", &TriangleGraph::col)

@@ -1038,24 +1038,35 @@ at::Tensor edge_owner(const at::Tensor& p, int P) {
 TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : comm(std::move(c)) {
   const at::Device dev = comm->device();
   at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2}).contiguous();
-  // MRH_TRI_REPLICATED=1 / 0 forces the replicated / distributed build; by
-  // default a GPU job replicates the graph when the whole edge list's build
-  // (~48 bytes per edge: packed copies, two sorts, CSR) takes under a quarter
-  // of the free HBM (RMAT-24: 13 GB of 288 GB) — every rank then runs the hub
-  // bitmap kernels on the full graph; larger graphs and CPU jobs keep the
-  // O(E/P + halo) distributed build
-  const char* rep = std::getenv("MRH_TRI_REPLICATED");
-  bool replicate = !comm->distributed() || (rep && *rep == '1');
-  if (comm->distributed() && !(rep && *rep)) {
+  // Build modes for several ranks (MRH_TRI_BUILD = split | halo | replicated;
+  // the older MRH_TRI_REPLICATED=1 / 0 = replicated / halo):
+  //  * split (GPU default when the whole graph's CSR fits a quarter of the
+  //    free HBM — RMAT-24: ~13 GB of 288 GB): the edges are deduplicated,
+  //    degree-ranked and sorted by key-range and row-range owners (build_split),
+  //    only the finished column array is all-gathered; every rank holds the
+  //    CSR and counts its share of the rows (split by estimated work);
+  //  * halo (CPU default, and graphs too large to replicate): O(E/P + halo)
+  //    memory per rank (build_distributed);
+  //  * replicated: every rank all-gathers the raw edge list and builds the
+  //    whole CSR itself (the round-3 path, kept for comparison).
+  std::string mode = "split";
+  if (const char* bm = std::getenv("MRH_TRI_BUILD")) {
+    if (*bm) mode = bm;
+  } else if (const char* rep = std::getenv("MRH_TRI_REPLICATED")) {
+    if (*rep) mode = *rep == '1' ? "replicated" : "halo";
+  } else if (comm->distributed()) {
     const int64_t mall = comm->allreduce(e.size(0), Comm::SUM);
     size_t free_b = 0, total_b = 0;
     int fits = 0;
     if (dev.is_cuda() && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
       fits = (double)mall * 48.0 < (double)free_b / 4.0 ? 1 : 0;
-    replicate = comm->allreduce((int64_t)fits, Comm::MIN) == 1;  // every rank must take the same path
+    mode = comm->allreduce((int64_t)fits, Comm::MIN) == 1 ? "split" : "halo";  // every rank takes the same path
   }
+  if (mode != "split" && mode != "halo" && mode != "replicated")
+    throw std::runtime_error("MRH_TRI_BUILD must be split, halo or replicated");
+  if (!comm->distributed()) mode = "replicated";  // one rank: the whole graph is local anyway
   at::Tensor p;
-  if (replicate && dev.is_cuda() && nv >= 0) {
+  if (mode != "halo" && dev.is_cuda() && nv >= 0) {
     // one pass: packed min << 32 | max, a self loop packed as edge (0, 0) —
     // it sorts first, keeps every key byte that is constant over the real
     // edges constant (the radix sort still skips those passes), and is
@@ -1076,11 +1087,16 @@ TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : c
     if (nv < 0) nv = comm->allreduce(hi.numel() ? hi.max().item<int64_t>() : -1, Comm::MAX) + 1;
     nvert = nv;
     if (nvert >= (int64_t(1) << 31)) throw std::runtime_error("mrhip: triangle path needs vertex ids < 2^31");
-    if (!replicate) {
+    if (mode == "halo") {
       build_distributed(lo, hi);
       return;
     }
     p = at::bitwise_or(at::bitwise_left_shift(lo, 32), hi).contiguous();
+  }
+  e = at::Tensor();
+  if (mode == "split") {
+    build_split(p);
+    return;
   }
   // replicated degree-oriented CSR: every rank holds the whole graph and
   // counts its share of the rows
@@ -1105,20 +1121,119 @@ TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : c
   e0 = 0;
   e1 = m;
   if (P > 1 && m > 0) {
-    // the shares are cut at row boundaries by estimated work, d+(u)^2 + d+(u)
-    // per row (the wedges the hash and hub-bitmap kernels walk), not by edge
-    // count: the top-ranked rows hold most of the work in few edges
     const int64_t nr = rowptr.numel() - 1;
     at::Tensor d = rowptr.narrow(0, 1, nr) - rowptr.narrow(0, 0, nr);
-    at::Tensor cost = exclusive_scan((d * d + d).contiguous());  // nr + 1 entries
-    const int64_t total = cost[nr].item<int64_t>();
-    at::Tensor targets = at::tensor({total / P * me + (total % P) * me / P, total / P * (me + 1) + (total % P) * (me + 1) / P},
-                                    at::TensorOptions().dtype(at::kLong)).to(rowptr.device());
-    at::Tensor ub = at::searchsorted(cost, targets).clamp(0, nr);
-    at::Tensor eb = rowptr.index_select(0, ub).to(at::kCPU);
-    e0 = me == 0 ? 0 : eb[0].item<int64_t>();
-    e1 = me == P - 1 ? m : eb[1].item<int64_t>();
+    std::vector<int64_t> rb = work_split(d, P);
+    e0 = rowptr[rb[me]].item<int64_t>();
+    e1 = rowptr[rb[me + 1]].item<int64_t>();
   }
+}
+
+// row boundaries (P + 1, identical on every rank given the same d) cutting
+// the rows into P ranges of equal estimated work d+(u)^2 + d+(u) — the wedges
+// the hash and hub-bitmap kernels walk — not equal edge counts: the top-ranked
+// rows hold most of the work in few edges
+std::vector<int64_t> TriangleGraph::work_split(const at::Tensor& d_in, int64_t P) {
+  const int64_t nr = d_in.numel();
+  at::Tensor d = d_in.to(at::kLong);
+  at::Tensor cost = exclusive_scan((d * d + d).contiguous());  // nr + 1 entries
+  const int64_t total = cost[nr].item<int64_t>();
+  std::vector<int64_t> tg(P - 1);
+  for (int64_t r = 1; r < P; ++r) tg[r - 1] = total / P * r + (total % P) * r / P;
+  std::vector<int64_t> rb{0};
+  if (P > 1) {
+    at::Tensor targets = at::from_blob(tg.data(), {P - 1}, at::TensorOptions().dtype(at::kLong)).to(cost.device());
+    at::Tensor ub = at::searchsorted(cost, targets).clamp(0, nr).to(at::kCPU);
+    for (int64_t r = 0; r < P - 1; ++r) rb.push_back(ub[r].item<int64_t>());
+  }
+  rb.push_back(nr);
+  for (size_t i = 1; i < rb.size(); ++i) rb[i] = std::max(rb[i], rb[i - 1]);
+  return rb;
+}
+
+// Multi-rank build of the replicated CSR without replicating the work
+// (sample sort by key range, then by row range):
+//  1. every packed edge to the owner of its key range (splitters from an
+//     all-gathered sample), sort + dedup there: the ranks hold disjoint sets
+//     of unique edges;
+//  2. degrees: a partial count per rank, allreduced (nvert int32); every
+//     rank derives the same (degree, id) ranks;
+//  3. the local unique edges oriented to the higher rank and sorted; local
+//     out-degrees d+ from the sorted runs, allreduced -> the global rowptr
+//     and the row split by estimated work (work_split);
+//  4. the oriented edges to their row owner, merged there (another local
+//     sort of the P received sorted runs): this rank's rows, in order;
+//  5. the column arrays all-gathered in rank order = the global CSR order.
+// Per rank that is O(E/P) sorting, two all-to-alls of E/P keys and one
+// all-gather of the 4-byte columns, instead of the whole raw edge list
+// all-gathered and sorted on every rank.
+void TriangleGraph::build_split(const at::Tensor& p_in) {
+  const Comm& cm = *comm;
+  const int P = cm.size(), me = cm.rank();
+  const at::Device dev = cm.device();
+  auto L = at::TensorOptions().device(dev).dtype(at::kLong);
+  split = true;
+  distributed = false;
+  at::Tensor p = p_in.contiguous();
+  // 1. key-range owners from NS strided samples per rank
+  {
+    constexpr int64_t NS = 4096;
+    const int64_t n = p.numel();
+    at::Tensor smp = at::full({NS}, std::numeric_limits<int64_t>::max(), L);
+    if (n > 0) smp = p.index_select(0, at::floor_divide(at::arange(NS, L) * n, NS));
+    at::Tensor all = at::empty({P * NS}, L);
+    cm.allgather_bytes(smp.data_ptr(), all.data_ptr(), NS * 8);
+    at::Tensor srt = std::get<0>(at::sort(all));
+    at::Tensor spl = srt.index_select(0, at::arange(1, P, L) * NS).contiguous();  // P - 1 splitters
+    at::Tensor dest = P > 1 ? at::searchsorted(spl, p, /*out_int32=*/true, /*right=*/true)
+                            : at::zeros({n}, L.dtype(at::kInt));
+    p = route_u64(cm, p, dest);
+  }
+  at::Tensor uniq = unique_sorted(p);
+  p = at::Tensor();
+  if (uniq.numel() > 0 && uniq[0].item<int64_t>() == 0) uniq = uniq.narrow(0, 1, uniq.numel() - 1);  // self loops
+  nedge = cm.allreduce(uniq.numel(), Comm::SUM);
+  // 2. global degrees -> ranks
+  const int64_t nv = std::max<int64_t>(nvert, 1);
+  at::Tensor rank;
+  {
+    at::Tensor deg = tri_degrees(uniq, nv);
+    cm.allreduce_tensor(deg, Comm::SUM);
+    std::tie(rank, perm) = tri_rank_perm(deg);
+  }
+  // 3. oriented + sorted locally; d+ allreduced -> rowptr, row split
+  at::Tensor os = tri_orient_keys(uniq, rank);
+  uniq = rank = at::Tensor();
+  if (os.numel()) os = radix_sort_keys(os, 0, 64);
+  std::vector<int64_t> rb;
+  {
+    at::Tensor lrp = tri_rowptr_of(os, nv);
+    at::Tensor dp = (lrp.narrow(0, 1, nv) - lrp.narrow(0, 0, nv)).to(at::kInt).contiguous();
+    lrp = at::Tensor();
+    cm.allreduce_tensor(dp, Comm::SUM);
+    rowptr = exclusive_scan(dp.to(at::kLong).contiguous());
+    rb = work_split(dp, P);
+  }
+  u0_ = rb[me];
+  u1_ = rb[me + 1];
+  // 4. to the row owners; P sorted runs -> one
+  if (P > 1) {
+    std::vector<int64_t> bk;
+    for (int r = 1; r < P; ++r) bk.push_back(rb[r] << 32);
+    at::Tensor b = at::from_blob(bk.data(), {P - 1}, at::TensorOptions().dtype(at::kLong)).to(dev);
+    at::Tensor dest = at::searchsorted(b, os, /*out_int32=*/true, /*right=*/true);
+    os = route_u64(cm, os, dest);
+    if (os.numel()) os = radix_sort_keys(os, 0, 64);
+  }
+  okeys = os;
+  // 5. the columns of every rank's rows, in rank (= row) order
+  col = cm.allgather_var(tri_col_of(okeys));
+  const int64_t m = rowptr[nv].item<int64_t>();
+  if (col.numel() != m || m != nedge)
+    throw std::runtime_error("TriangleGraph split build: " + std::to_string(col.numel()) + " columns gathered, rowptr says " +
+                             std::to_string(m) + ", " + std::to_string(nedge) + " unique edges");
+  e0 = 0;
+  e1 = okeys.numel();
 }
 
 // Distributed build (reference tri_find shuffles every edge 4 times,
@@ -1217,6 +1332,7 @@ void TriangleGraph::build_distributed(const at::Tensor& lo_in, const at::Tensor&
 }
 
 int64_t TriangleGraph::count() const {
+  if (split) return comm->allreduce(tri_count_range(rowptr, col, u0_, u1_), Comm::SUM);
   if (!distributed) return comm->allreduce(tri_count(rowptr, col, okeys, e0, e1), Comm::SUM);
   return comm->allreduce(tri_count_rows(rowptr, col, 0, nlocal), Comm::SUM);
 }

@@ -165,9 +165,15 @@ class TriangleGraph {
   bool distributed = false;
   int64_t nlocal = 0, nrows = 0;  // distributed: owned rows, owned + halo rows
   at::Tensor rowptr, col, okeys, perm, row_gid;
+  // split build: the CSR is whole on every rank, okeys holds this rank's rows
+  // [u0_, u1_) only
+  bool split = false;
+  int64_t u0_ = 0, u1_ = 0;
 
  private:
   void build_distributed(const at::Tensor& lo, const at::Tensor& hi);
+  void build_split(const at::Tensor& packed);
+  static std::vector<int64_t> work_split(const at::Tensor& d, int64_t P);
 };
 
 }  // namespace mrh

@@ -47,10 +47,10 @@ int64_t intersect_host(const int64_t* rp, const int32_t* col, uint32_t u, uint32
 }
 }  // namespace
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq_in, int64_t nvert) {
+at::Tensor tri_degrees(const at::Tensor& uniq_in, int64_t nvert) {
   at::Tensor uniq = uniq_in.contiguous();
-  if (uniq.scalar_type() != at::kLong) throw std::runtime_error("tri_prepare: packed int64 edges expected");
-  if (nvert > (int64_t(1) << 32)) throw std::runtime_error("tri_prepare: vertex ids must fit in 32 bits");
+  if (uniq.scalar_type() != at::kLong) throw std::runtime_error("tri_degrees: packed int64 edges expected");
+  if (nvert > (int64_t(1) << 32)) throw std::runtime_error("tri_degrees: vertex ids must fit in 32 bits");
   const at::Device dev = uniq.device();
   const int64_t m = uniq.numel();
   nvert = std::max<int64_t>(nvert, 1);
@@ -59,14 +59,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
   auto stage = [&](const char* what) {
     if (!dbg) return;
     if (uniq.is_cuda()) (void)hipDeviceSynchronize();
-    std::fprintf(stderr, "mrhip tri_prepare: %s done\n", what);
+    std::fprintf(stderr, "mrhip tri_degrees: %s done\n", what);
   };
   if (uniq.is_cuda()) {
     const int nb = k::tri_deg_buckets(nvert);
     if (nb > 0 && m > 0) {
       // partitioned count (tri.hip k_deg_*): no scattered atomic per edge
       const hipStream_t s = cur();
-      const at::Device dev = uniq.device();
       k::tri_deg_lo(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), s);
       stage("deg_lo");
       at::Tensor bcount = at::zeros({nb}, opt(dev, at::kInt));
@@ -113,17 +112,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
       d[(uint32_t)e[i]]++;
     }
   }
-  stage("degree");
+  return deg;
+}
+
+std::pair<at::Tensor, at::Tensor> tri_rank_perm(const at::Tensor& deg) {
+  const at::Device dev = deg.device();
+  const int64_t nvert = deg.numel();
   // rank = position in (degree, id) order; perm[rank] = original id
   // the LSD radix sort is stable: sorting the degrees alone keeps equal
   // degrees in id order, i.e. (degree, id) order
   at::Tensor perm32 = std::get<1>(radix_sort_pairs(deg.to(at::kLong), at::arange(nvert, opt(dev, at::kInt)), 0, 32));
   at::Tensor perm = perm32.to(at::kLong);
   at::Tensor rank = at::empty({nvert}, opt(dev, at::kInt));
-  if (uniq.is_cuda()) k::tri_rank(P0<int32_t>(perm32), nvert, P0<int32_t>(rank), cur());
+  if (deg.is_cuda()) k::tri_rank(P0<int32_t>(perm32), nvert, P0<int32_t>(rank), cur());
   else rank.index_put_({perm}, at::arange(nvert, opt(dev, at::kInt)));
-  stage("rank");
-  at::Tensor oriented = at::empty({m}, opt(dev, at::kLong));
+  return {rank, perm};
+}
+
+at::Tensor tri_orient_keys(const at::Tensor& uniq_in, const at::Tensor& rank) {
+  at::Tensor uniq = uniq_in.contiguous();
+  const int64_t m = uniq.numel();
+  at::Tensor oriented = at::empty({m}, uniq.options());
+  if (m == 0) return oriented;
   if (uniq.is_cuda()) {
     k::tri_orient(P0<uint64_t>(uniq), m, P0<uint32_t>(rank), P0<uint64_t>(oriented), cur());
   } else {
@@ -135,26 +145,40 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
       o[i] = ra < rb ? (ra << 32 | rb) : (rb << 32 | ra);
     }
   }
-  stage("orient");
+  return oriented;
+}
+
+at::Tensor tri_col_of(const at::Tensor& okeys) {
+  const int64_t m = okeys.numel();
+  if (okeys.is_cuda()) {
+    at::Tensor col = at::empty({m}, opt(okeys.device(), at::kInt));
+    if (m) k::tri_col(P0<uint64_t>(okeys), m, P0<uint32_t>(col), cur());
+    return col;
+  }
+  return at::bitwise_and(okeys, (int64_t)0xffffffff).to(at::kInt);
+}
+
+at::Tensor tri_rowptr_of(const at::Tensor& okeys, int64_t nvert) {
+  if (okeys.is_cuda()) {
+    at::Tensor rowptr = at::empty({nvert + 1}, opt(okeys.device(), at::kLong));
+    k::tri_rowptr(P0<uint64_t>(okeys), okeys.numel(), nvert, P0<int64_t>(rowptr), cur());
+    return rowptr;
+  }
+  at::Tensor src = at::bitwise_right_shift(okeys, 32);
+  at::Tensor cnt = bincount_dev(src, nvert);
+  return exclusive_scan(cnt.to(at::kLong).contiguous());
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq_in, int64_t nvert) {
+  at::Tensor uniq = uniq_in.contiguous();
+  nvert = std::max<int64_t>(nvert, 1);
+  at::Tensor deg = tri_degrees(uniq, nvert);
+  auto [rank, perm] = tri_rank_perm(deg);
+  deg = at::Tensor();
+  at::Tensor oriented = tri_orient_keys(uniq, rank);
   // keys-only: the oriented edges carry no payload
-  at::Tensor okeys = m ? radix_sort_keys(oriented, 0, 64) : oriented;
-  at::Tensor col;
-  if (okeys.is_cuda()) {
-    col = at::empty({m}, opt(dev, at::kInt));
-    k::tri_col(P0<uint64_t>(okeys), m, P0<uint32_t>(col), cur());
-  } else {
-    col = at::bitwise_and(okeys, (int64_t)0xffffffff).to(at::kInt);
-  }
-  at::Tensor rowptr;
-  if (okeys.is_cuda()) {
-    rowptr = at::empty({nvert + 1}, opt(dev, at::kLong));
-    k::tri_rowptr(P0<uint64_t>(okeys), m, nvert, P0<int64_t>(rowptr), cur());
-  } else {
-    at::Tensor src = at::bitwise_right_shift(okeys, 32);
-    at::Tensor cnt = bincount_dev(src, nvert);
-    rowptr = exclusive_scan(cnt.to(at::kLong).contiguous());
-  }
-  return {rowptr, col, okeys, perm};
+  at::Tensor okeys = oriented.numel() ? radix_sort_keys(oriented, 0, 64) : oriented;
+  return {tri_rowptr_of(okeys, nvert), tri_col_of(okeys), okeys, perm};
 }
 
 // hub bitmap size: MRH_TRI_HUB vertices (0 = off); default nvert / 64 capped
@@ -283,7 +307,23 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
     auto src = [&](int64_t e) { return (int64_t)((uint64_t)okeys[e].item<int64_t>() >> 32); };
     const int64_t u0 = e0 == 0 ? 0 : src(e0 - 1) + 1;
     const int64_t u1 = e1 == m ? nvert : src(e1 - 1) + 1;
-    at::Tensor tot = at::zeros({1}, opt(okeys.device(), at::kLong));
+    return tri_count_range(rowptr, col, u0, u1, okeys);
+  }
+  const int64_t* rp = P0<int64_t>(rowptr);
+  const int32_t* c = P0<int32_t>(col);
+  const uint64_t* k = P0<uint64_t>(okeys);
+  int64_t n = 0;
+  for (int64_t e = e0; e < e1; ++e) n += intersect_host<false>(rp, c, (uint32_t)(k[e] >> 32), (uint32_t)k[e], nullptr);
+  return n;
+}
+
+int64_t tri_count_range(const at::Tensor& rowptr, const at::Tensor& col, int64_t u0, int64_t u1,
+                        const at::Tensor& okeys) {
+  if (u1 <= u0) return 0;
+  if (!rowptr.is_cuda()) return tri_count_rows(rowptr, col, u0, u1);
+  {
+    const int64_t nvert = rowptr.numel() - 1;
+    at::Tensor tot = at::zeros({1}, opt(rowptr.device(), at::kLong));
     // the top-K ranks (hubs) go to the bitmap kernel, the rest to the hash kernels
     const int64_t K = tri_hub_size(nvert);
     g_last_hub = K;
@@ -294,30 +334,26 @@ int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Ten
     at::Tensor H;
     if (K) {
       // the bitmaps serve both the hub kernel and the hub probes of the hash kernels
-      H = at::empty({K * (K / 64)}, opt(okeys.device(), at::kLong));
+      H = at::empty({K * (K / 64)}, opt(rowptr.device(), at::kLong));
       const int64_t ua = std::max(u0, hb), ub = std::max(std::min(u1, cb), hb);
       const bool pull = tri_hub_mode() == 0;
       // pull: tri_hub_count only builds the bitmaps (an empty row range)
       k::tri_hub_count(P0<int64_t>(rowptr), P0<uint32_t>(col), hb, K, ua, pull ? ua : ub, P0<uint64_t>(H),
                        P0<unsigned long long>(tot), cur());
+      if (pull && !okeys.defined())
+        throw std::runtime_error("MRH_TRI_HUB_KERNEL=pull needs the whole oriented edge list (one rank)");
       if (pull) tri_hub_pull_count(rowptr, col, okeys, hb, K, ua, ub, H, tot);
     }
     int64_t ncore = 0;
     if (T && u1 > cb) ncore = tri_core_count(rowptr, col, cb, T, std::max(u0, cb), u1);
     if (uh > u0) {
-      at::Tensor big = at::empty({2 * std::max<int64_t>(uh - u0, 1)}, opt(okeys.device(), at::kInt));
-      at::Tensor nbig = at::zeros({2}, opt(okeys.device(), at::kInt));
+      at::Tensor big = at::empty({2 * std::max<int64_t>(uh - u0, 1)}, opt(rowptr.device(), at::kInt));
+      at::Tensor nbig = at::zeros({2}, opt(rowptr.device(), at::kInt));
       k::tri_count_hash(P0<int64_t>(rowptr), P0<uint32_t>(col), u0, uh, P0<uint32_t>(big), P0<uint32_t>(nbig),
                         P0<unsigned long long>(tot), cur(), K ? P0<uint64_t>(H) : nullptr, hb, K);
     }
     return tot.item<int64_t>() + ncore;
   }
-  const int64_t* rp = P0<int64_t>(rowptr);
-  const int32_t* c = P0<int32_t>(col);
-  const uint64_t* k = P0<uint64_t>(okeys);
-  int64_t n = 0;
-  for (int64_t e = e0; e < e1; ++e) n += intersect_host<false>(rp, c, (uint32_t)(k[e] >> 32), (uint32_t)k[e], nullptr);
-  return n;
 }
 
 int64_t tri_count_rows(const at::Tensor& rowptr, const at::Tensor& col, int64_t u0, int64_t u1) {

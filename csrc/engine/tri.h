@@ -3,6 +3,7 @@
 #include <ATen/ATen.h>
 
 #include <tuple>
+#include <utility>
 
 namespace mrh {
 // uniq: sorted unique packed undirected edges (lo<<32|hi, lo<hi), ids < nvert < 2^32-1.
@@ -11,6 +12,15 @@ namespace mrh {
 // [nvert+1], col int32 [m], okeys int64 [m] = src<<32|dst sorted) and perm
 // (int64 [nvert], perm[rank] = original id).
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at::Tensor& uniq, int64_t nvert);
+// the pieces of tri_prepare (also the multi-GPU build, graphplan.cpp):
+// degree of every vertex over packed edges (int32 [nvert]); (rank, perm) of
+// the (degree, id) order; the edges oriented to the higher rank, packed
+// rank_lo << 32 | rank_hi (unsorted); col / rowptr of sorted oriented keys
+at::Tensor tri_degrees(const at::Tensor& uniq, int64_t nvert);
+std::pair<at::Tensor, at::Tensor> tri_rank_perm(const at::Tensor& deg);
+at::Tensor tri_orient_keys(const at::Tensor& uniq, const at::Tensor& rank);
+at::Tensor tri_col_of(const at::Tensor& okeys);
+at::Tensor tri_rowptr_of(const at::Tensor& okeys, int64_t nvert);
 // vertices of the hub bitmap path of tri_count (MRH_TRI_HUB, default
 // nvert/32 up to 524288 and a quarter of free HBM; 0 = hash kernels only)
 int64_t tri_hub_size(int64_t nvert);
@@ -18,6 +28,11 @@ int64_t tri_hub_size(int64_t nvert);
 int64_t tri_last_hub_size();
 // number of triangles whose first oriented edge lies in [e0, e1)
 int64_t tri_count(const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& okeys, int64_t e0, int64_t e1);
+// number of triangles whose lowest (rank) vertex is a row in [u0, u1): the
+// hub bitmap + hash kernels of tri_count over a row range (okeys, the whole
+// sorted oriented edge list, only for MRH_TRI_HUB_KERNEL=pull)
+int64_t tri_count_range(const at::Tensor& rowptr, const at::Tensor& col, int64_t u0, int64_t u1,
+                        const at::Tensor& okeys = {});
 // number of triangles u < v < w (in the CSR's id order) over the rows u in
 // [u0, u1): rows outside the range are only looked up (the distributed
 // graph's halo)

@@ -147,6 +147,59 @@ def test_distributed_triangles_match_replicated(world):
     assert tris == want
 
 
+def case_tri_split(comm):
+    """the split build (sample-sorted dedup, allreduced degrees and d+, rows
+    split by work, column arrays all-gathered): the whole CSR on every rank,
+    equal to the one-rank build; each rank counts / lists its rows only"""
+    import os
+    e = _rmat(11, 8, 7)
+    mine = e[comm.rank::comm.size]
+    os.environ["MRH_TRI_BUILD"] = "split"
+    try:
+        # on a device engine with nvert given: the one-pass device edge pack
+        g = TriangleGraph(comm, mine, (1 << 11) if comm.is_cuda else None)
+    finally:
+        os.environ.pop("MRH_TRI_BUILD")
+    return (g.count(), g._g.split, g._g.u0, g._g.u1, g.rowptr.cpu().numpy().copy(), g.col.cpu().numpy().copy(),
+            g.perm.cpu().numpy().copy(), [tuple(t) for t in g.triangles().tolist()])
+
+
+def _check_split(world, device):
+    import numpy as np
+    from test_distributed_cpu import run_world
+    import gpu_mapreduce_amd as gm
+    out = run_world("test_triangles:case_tri_split", world, device)
+    e = _rmat(11, 8, 7)
+    one = TriangleGraph(gm.Comm(device="cpu"), e)
+    want = _brute_list(e.numpy())
+    tris, rows = set(), []
+    for r in range(world):
+        cnt, split, u0, u1, rowptr, col, perm, lst = out[r]
+        assert split and cnt == len(want) == one.count()
+        np.testing.assert_array_equal(rowptr, one.rowptr.numpy())
+        np.testing.assert_array_equal(col, one.col.numpy())
+        np.testing.assert_array_equal(perm, one.perm.numpy())
+        rows.append((u0, u1))
+        assert not (tris & set(lst)), "a triangle listed on two ranks"
+        tris |= set(lst)
+    assert tris == want
+    assert rows[0][0] == 0 and rows[-1][1] == one.nvert
+    assert all(rows[i][1] == rows[i + 1][0] for i in range(world - 1))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_build_matches_single_rank(world):
+    _check_split(world, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_build_gpu_matches_single_rank(world):
+    """the split build on the device engine (ranks sharing the box's GPU over
+    the gloo transport): device pack, exchanges, dedup, degrees, d+, CSR"""
+    _check_split(world, "cuda:0")
+
+
 TRI_HUB_CHILD = r'''
 import sys, torch
 from gpu_mapreduce_amd import Comm, C
