@@ -4,6 +4,7 @@
 #include "hbmpool.h"
 
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPFunctions.h>
 #include <hip/hip_runtime.h>
 #include <torch/csrc/distributed/c10d/PrefixStore.hpp>
 #include <torch/csrc/distributed/c10d/TCPStore.hpp>
@@ -116,6 +117,15 @@ Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const s
   if (world_size < 0) world_size = size_;
   if (world_size > 1 && store_) mon_ = shared_monitor(store_, world_rank, world_size);
   if (size_ == 1) pg_.reset();
+  // host scalars need a CPU backend on the group (gloo / the store
+  // transport); an nccl-only group moves them as device tensors instead
+  if (pg_) {
+    try {
+      host_pg_ = (bool)pg_->getBackend(c10::DeviceType::CPU);
+    } catch (const std::exception&) {
+      host_pg_ = false;
+    }
+  }
   init_transport(transport, "world");
 }
 
@@ -128,10 +138,13 @@ void Comm::init_transport(const std::string& transport, const std::string& tag) 
   }
   // one RCCL communicator per (member set, device) per process, shared by
   // every Comm over the same ranks
-  rccl_ = shared_rccl(rank_, size_, dev_.index(), store_, tag, members_, mon_.get());
+  // a device without an index ("cuda") means the current one
+  rccl_ = shared_rccl(rank_, size_, rccl_device(), store_, tag, members_, mon_.get());
 }
 
 Comm::~Comm() = default;
+
+int Comm::rccl_device() const { return dev_.has_index() ? dev_.index() : (int)c10::hip::current_device(); }
 
 std::string Comm::transport() const {
   if (rccl_) return "rccl";
@@ -239,6 +252,10 @@ std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
     rccl_->allreduce(t.data_ptr(), v.size(), ncclInt64, nred(op), cur(dev_));
     host_wait();
     t = t.to(at::kCPU);
+  } else if (pg_) {  // a group without a CPU backend: device tensors through it
+    t = t.to(dev_);
+    pg_allreduce(pg_, t, op);
+    t = t.to(at::kCPU);
   }
   std::memcpy(v.data(), t.data_ptr<int64_t>(), v.size() * sizeof(int64_t));
   return v;
@@ -254,6 +271,10 @@ std::vector<double> Comm::allreduce_f64(std::vector<double> v, Op op) const {
     t = t.to(dev_);
     rccl_->allreduce(t.data_ptr(), v.size(), ncclFloat64, nred(op), cur(dev_));
     host_wait();
+    t = t.to(at::kCPU);
+  } else if (pg_) {
+    t = t.to(dev_);
+    pg_allreduce(pg_, t, op);
     t = t.to(at::kCPU);
   }
   std::memcpy(v.data(), t.data_ptr<double>(), v.size() * sizeof(double));
@@ -486,7 +507,8 @@ std::shared_ptr<Comm> Comm::split(int color) const {
   c->mon_ = mon_;  // failure detection stays job-wide
   c->rccl_.reset();
   c->pg_ = make_host_pg(pst, newrank, newsize, mon_);
-  if (rccl_) c->rccl_ = shared_rccl(newrank, newsize, dev_.index(), store_, "split", members, mon_.get());
+  c->host_pg_ = true;
+  if (rccl_) c->rccl_ = shared_rccl(newrank, newsize, rccl_device(), store_, "split", members, mon_.get());
   return c;
 }
 

@@ -147,7 +147,9 @@ class Comm {
  private:
   void init_transport(const std::string& transport, const std::string& tag);
   void fail_now(const std::string& why) const;
-  bool host_scalars() const { return pg_ && size_ > 1; }
+  bool host_scalars() const { return pg_ && host_pg_ && size_ > 1; }
+  bool host_pg_ = false;  // pg_ has a CPU backend
+  int rccl_device() const;  // the device index (the current one for "cuda")
 
   int rank_ = 0, size_ = 1;
   at::Device dev_;

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 
 #include "guard.h"
@@ -272,11 +273,23 @@ hipEvent_t Rccl::fence_out() {
 hipEvent_t Rccl::sendrecv_async(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
   if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
   fence_in(s);
+  // one transfer is posted as pieces of at most max_msg bytes (both ends cut
+  // the same byte count the same way): single RCCL point-to-point messages of
+  // 2 GiB and more came back incomplete on MI355X (tools/rccl_big.py)
+  static const int64_t max_msg = [] {
+    const char* e = std::getenv("MRH_RCCL_MAX_MSG");
+    const long long v = e && *e ? std::atoll(e) : (1LL << 30);
+    return v > 0 ? (int64_t)v : std::numeric_limits<int64_t>::max();
+  }();
   check(ncclGroupStart(), "ncclGroupStart");
   for (const Xfer& x : recvs)
-    if (x.bytes > 0) check(ncclRecv(x.ptr, (size_t)x.bytes, ncclUint8, x.peer, comm_, stream_), "ncclRecv");
+    for (int64_t o = 0; o < x.bytes; o += max_msg)
+      check(ncclRecv((uint8_t*)x.ptr + o, (size_t)std::min(max_msg, x.bytes - o), ncclUint8, x.peer, comm_, stream_),
+            "ncclRecv");
   for (const Xfer& x : sends)
-    if (x.bytes > 0) check(ncclSend(x.ptr, (size_t)x.bytes, ncclUint8, x.peer, comm_, stream_), "ncclSend");
+    for (int64_t o = 0; o < x.bytes; o += max_msg)
+      check(ncclSend((uint8_t*)x.ptr + o, (size_t)std::min(max_msg, x.bytes - o), ncclUint8, x.peer, comm_, stream_),
+            "ncclSend");
   check(ncclGroupEnd(), "ncclGroupEnd");
   return fence_out();
 }

@@ -70,6 +70,11 @@ class PageRank:
         self.blocking = self._p.blocking
         # source ranges pinned to XCDs (0 = plain pull gather)
         self.xcd_ranges = self._p.xcd_ranges
+        # "local" (one GPU), "replicated" (several GPUs: destination-owned
+        # edges + all-gathered c = r / outdeg), "partials" (source-owned edges +
+        # all-to-all of partial sums: CPU engine / MRH_PR_DIST=partials)
+        self.layout = self._p.layout
+        self.c_slice = self._p.c_slice
         return self
 
     def reset(self):

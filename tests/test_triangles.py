@@ -170,7 +170,7 @@ def _check_split(world, device):
     import gpu_mapreduce_amd as gm
     out = run_world("test_triangles:case_tri_split", world, device)
     e = _rmat(11, 8, 7)
-    one = TriangleGraph(gm.Comm(device="cpu"), e)
+    one = TriangleGraph(gm.Comm(device="cpu"), e, (1 << 11) if device.startswith("cuda") else None)
     want = _brute_list(e.numpy())
     tris, rows = set(), []
     for r in range(world):
