@@ -188,7 +188,10 @@ def bench_inverted_index_files(comm, args):
     try:
         if comm.allreduce(files_ok, "min") == 0:
             return {"skipped": f"a rank had no directory with {need >> 20} MiB free for the part files"}
-        bufs = [torch.empty(n, dtype=torch.uint8, pin_memory=comm.is_cuda) for _, _, n in paths]
+        # two sets of pinned read buffers: job s+1's files are read while job s
+        # copies and maps its own (a job pipeline, like the headline's)
+        bufsets = [[torch.empty(n, dtype=torch.uint8, pin_memory=comm.is_cuda) for _, _, n in paths]
+                   for _ in range(2)]
         outdir = os.path.join(root, "out")
 
         # reads in 32 MiB pieces (os.preadv releases the GIL), spread over
@@ -198,11 +201,11 @@ def bench_inverted_index_files(comm, args):
         nloc = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
         nthr = max(4, min(16, (os.cpu_count() or 8) // nloc))
         fds = [os.open(pth, os.O_RDONLY) for _, pth, _ in paths]
-        views = [memoryview(b.numpy()) for b in bufs]
+        views = [[memoryview(b.numpy()) for b in bs] for bs in bufsets]
 
-        def read_piece(job):
+        def read_piece(job, k=0):
             i, o, n = job
-            got = os.preadv(fds[i], [views[i][o:o + n]], o)
+            got = os.preadv(fds[i], [views[k][i][o:o + n]], o)
             if got != n:
                 raise OSError(f"short read of {paths[i][1]} at {o}: {got} of {n} bytes")
 
@@ -216,31 +219,39 @@ def bench_inverted_index_files(comm, args):
                 for f in self.futs:
                     f.result()
 
-        def step():
-            # all pieces queued in file order: file i+1 is read while file i
-            # is copied and mapped (the job waits per file)
-            futs = [pool.submit(read_piece, j) for j in jobs]
+        def reads(s):
+            """queue job s's reads (file order) into buffer set s % 2"""
+            k = s % 2
+            futs = [pool.submit(read_piece, j, k) for j in jobs]
             ready = [_FileRead([f for f, j in zip(futs, jobs) if j[0] == i]) for i in range(len(paths))]
-            files = [(paths[i][0], bufs[i], ready[i]) for i in range(len(paths))]
-            app = InvertedIndex(MapReduce(comm), files, out_dir=outdir)
-            n = app.run()
-            for r in ready:
-                r.result()
-            write_s.append(app.write_s)
-            out_bytes.append(app.output.numel() if app.output is not None else 0)
-            return n
+            return [(paths[i][0], bufsets[k][i], ready[i]) for i in range(len(paths))]
 
-        write_s, out_bytes = [], []
+        def window(k):
+            """k jobs back to back: job s's part files are read while job s-1
+            runs, job s copies job s+1's first file behind its own last one and
+            its index is written by the writer thread during job s+1; the
+            window ends when the last job's index is on disk"""
+            files = reads(0)
+            apps = []
+            for s in range(k):
+                nxt = reads(s + 1) if s < k - 1 else None
+                app = InvertedIndex(MapReduce(comm), files, out_dir=outdir, async_write=True,
+                                    prefetch_next=nxt)
+                app.run()
+                apps.append(app)
+                files = nxt
+            for app in apps:
+                app.wait_written()
+            return apps
 
-        for _ in range(args.warmup):
-            step()
+        window(max(1, args.warmup))
         _sync(comm)
-        write_s.clear()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
+        apps = window(args.steps)
         _sync(comm)
         dt = comm.allreduce((time.perf_counter() - t0) / args.steps, "max", dtype=torch.float64)
+        write_s = [a.write_s for a in apps]
+        out_bytes = [a.output.numel() if a.output is not None else 0 for a in apps]
         wr = comm.allreduce(sum(write_s) / max(1, len(write_s)), "max", dtype=torch.float64)
         # the reads alone (untimed above: they overlap the job)
         t0 = time.perf_counter()
@@ -254,9 +265,10 @@ def bench_inverted_index_files(comm, args):
                 "write_ms": wr * 1e3, "output_bytes": out_bytes[-1] if out_bytes else 0, "input_GBps": total_in / dt / 1e9,
                 "vs_reference_end_to_end": total_in / dt / 1e9 / REF_GBPS,
                 "note": "part files read from the page cache (RAM-backed directory) into pinned memory (32 MiB pieces "
-                        "over read_threads threads, file i+1 read while file i is copied and mapped; read_ms: the "
-                        "reads alone), "
-                        "the index text written to a file; steps=%d" % args.steps}
+                        "over read_threads threads; job s+1's files are read while job s copies and maps its own; "
+                        "read_ms: the reads alone), the index text written to a file by a writer thread during the "
+                        "next job (write_ms: one write); the window ends when the last index is written; "
+                        "steps=%d" % args.steps}
     finally:
         if root is not None:
             shutil.rmtree(root, ignore_errors=True)

@@ -53,11 +53,17 @@ def _write_file(path, data):
     from the buffer, no bytes copy. One writer: 16 MiB pieces pwritten by 8
     threads measured slower into a RAM-backed directory (27.8 vs 21.1 ms for
     the 98 MB index, profiles/r3_gpu_full_g.txt)"""
-    # overwrite in place and cut to size afterwards: a job writing the same
-    # path again reuses the file's cached pages instead of freeing them
-    # (O_TRUNC) and faulting in fresh zeroed ones
+    # overwrite in place: a job writing the same path again reuses the file's
+    # cached pages instead of freeing them (O_TRUNC) and faulting in fresh
+    # zeroed ones. A longer old file is cut first, so a write that dies
+    # midway leaves a file no longer than the new index (never stale lines
+    # past its end); an equal-size overwrite that dies midway leaves old bytes
+    # behind the new ones, which a reader cannot detect — write elsewhere and
+    # rename if that matters
     fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
     try:
+        if os.fstat(fd).st_size > len(data):
+            os.ftruncate(fd, len(data))
         done = 0
         while done < len(data):
             done += os.pwrite(fd, data[done:], done)
@@ -66,8 +72,21 @@ def _write_file(path, data):
         os.close(fd)
 
 
+_WRITER = []
+_SLOT_WRITE = {}  # pinned output slot -> the pending write of the job that filled it
+
+
+def _writer():
+    """the index writer thread (one: writes land in job order)"""
+    if not _WRITER:
+        from concurrent.futures import ThreadPoolExecutor
+        _WRITER.append(ThreadPoolExecutor(max_workers=1, thread_name_prefix="mrh-ii-write"))
+    return _WRITER[0]
+
+
 class InvertedIndex:
-    def __init__(self, mr: MapReduce, files, out_dir=None, pipelined=True, own_output=False, prefetch_next=None):
+    def __init__(self, mr: MapReduce, files, out_dir=None, pipelined=True, own_output=False, prefetch_next=None,
+                 async_write=False):
         """files: list of (name, uint8 tensor) for THIS rank (host tensors —
         ideally pinned — or device tensors), or (name, tensor, ready) where
         ready.result() blocks until the tensor holds the file's bytes (e.g. the
@@ -82,8 +101,17 @@ class InvertedIndex:
         following staging slot, so the PCIe link does not idle during this
         job's tail (its last file's map and group-by, the group ordering, the
         output formatting); the next job finds that copy and does not repeat
-        it. Every job still copies all of its own files."""
+        it. Every job still copies all of its own files. A (name, tensor,
+        ready) entry is waited for (ready.result()) before that copy.
+
+        async_write (with out_dir): the index file is written by a writer
+        thread once the output text has drained to host memory, so the write
+        overlaps the next job (the reference writes it inside its reduce,
+        cuda/InvertedIndex.cu:463-513); wait_written() blocks until it is on
+        disk. The pinned output slot is not reused before its write is done."""
         self.prefetch_next = prefetch_next
+        self.async_write = async_write
+        self._write = None
         self.mr = mr
         self.files = files
         self.out_dir = out_dir
@@ -182,7 +210,7 @@ class InvertedIndex:
                 b = (base + i) % nb
                 t = files[i][1]
                 self._wait_read(i)
-                ev = pools.take_prefetch(self.dev, b, t)  # copied by the previous job of a pipeline
+                ev = pools.take_prefetch(self.dev, b, t, self.bufs[b])  # copied by the previous job of a pipeline
                 if ev is not None:
                     ready[b] = ev
                 else:
@@ -198,12 +226,15 @@ class InvertedIndex:
                     issue(i)
                 if i == len(files) - 1 and nb > 1 and self.prefetch_next:
                     # the next job's first file, behind this job's last copy
-                    nxt = self.prefetch_next[0][1]
+                    first = self.prefetch_next[0]
+                    nxt = first[1]
                     if nxt.numel() + PAD <= self.bufs[0].numel():
+                        if len(first) > 2 and first[2] is not None:
+                            first[2].result()  # its bytes are read into the host buffer
                         slot = (base + len(files)) % nb
                         ev = torch.cuda.Event()
                         copy_into(slot, nxt, ev)
-                        pools.set_prefetch(self.dev, slot, nxt, ev)
+                        pools.set_prefetch(self.dev, slot, nxt, ev, self.bufs[slot])
                 b = (base + i) % nb
                 main.wait_event(ready[b])
                 n = files[i][1].numel()
@@ -221,10 +252,15 @@ class InvertedIndex:
     def _reduce(self, kmv, kv):
         text = C.inverted_index_format(kmv, self.names_dev, self.name_off_dev)
         if self.is_cuda:
+            slot = None
             if self.own_output:
                 host = torch.empty(text.numel(), dtype=torch.uint8, pin_memory=True)
             else:
-                host = pools.pinned_buffer(text.numel(), slot=100 + pools.next_slot("ii_out"))
+                slot = 100 + pools.next_slot("ii_out")
+                pending = _SLOT_WRITE.pop(slot, None)
+                if pending is not None:
+                    pending.result()  # an earlier job's index is still being written from this slot
+                host = pools.pinned_buffer(text.numel(), slot=slot)
                 self._gen = pools.generation("ii_out")
             d2h = pools.stream(self.dev, "d2h")
             d2h.wait_stream(torch.cuda.current_stream())
@@ -235,15 +271,34 @@ class InvertedIndex:
             self._done.record(d2h)
         else:
             host = text
+            slot = None
         self.output = host
         if self.out_dir is not None:
-            self.output_ready()
             os.makedirs(self.out_dir, exist_ok=True)
             path = os.path.join(self.out_dir, f"InvertedIndex-{self.mr.nprocs}-{self.mr.me}")
-            t = time.perf_counter()
-            _write_file(path, memoryview(host.numpy()))
-            self.write_s = time.perf_counter() - t
             MapReduce.count_io(write=host.numel())
+            done = self._done
+
+            def write():
+                if done is not None:
+                    done.synchronize()  # the D2H drain (releases the GIL)
+                t = time.perf_counter()
+                _write_file(path, memoryview(host.numpy()))
+                return time.perf_counter() - t
+            if self.async_write:
+                self._write = _writer().submit(write)
+                if slot is not None:
+                    _SLOT_WRITE[slot] = self._write
+            else:
+                self.write_s = write()
+
+    def wait_written(self):
+        """block until the index file is written (async_write); returns the
+        write's seconds"""
+        if self._write is not None:
+            self.write_s = self._write.result()
+            self._write = None
+        return self.write_s
 
     def output_ready(self):
         """block until the output text has drained to host memory"""

@@ -106,7 +106,7 @@ class WordFreq:
 
         def issue(i):
             b = (base + i) % nb
-            ev = pools.take_prefetch(dev, 8 + b, self.chunks[i])  # copied by the previous job of a pipeline
+            ev = pools.take_prefetch(dev, 8 + b, self.chunks[i], self.bufs[b])  # copied by the previous job of a pipeline
             if ev is not None:
                 ready[b] = ev
             else:
@@ -126,7 +126,7 @@ class WordFreq:
                     slot = (base + n) % nb
                     ev = torch.cuda.Event()
                     copy_into(slot, nxt, ev)
-                    pools.set_prefetch(dev, 8 + slot, nxt, ev)
+                    pools.set_prefetch(dev, 8 + slot, nxt, ev, self.bufs[slot])
             b = (base + i) % nb
             main.wait_event(ready[b])
             consume(self.bufs[b], self.chunks[i].numel())

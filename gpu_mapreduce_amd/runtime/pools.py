@@ -23,6 +23,12 @@ def device_buffer(device: str, nbytes: int, slot: int = 0) -> torch.Tensor:
     key = (str(device), slot)
     b = _dev.get(key)
     if b is None or b.numel() < nbytes:
+        if b is not None and str(device).startswith("cuda"):
+            # a copy (e.g. a previous job's prefetch) or a kernel may still use
+            # the old buffer: it is freed only after the device is idle, and a
+            # prefetch into it is void (take_prefetch also checks the buffer)
+            torch.cuda.synchronize(device)
+            _prefetch.pop(key, None)
         b = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
         _dev[key] = b
     return b
@@ -84,17 +90,20 @@ def ring_cursor(device: str, name: str, advance: int = 0, n: int = 1) -> int:
     return c
 
 
-def set_prefetch(device: str, slot: int, src: torch.Tensor, event) -> None:
-    """Record that `src` (a host tensor) is being copied into staging slot
-    `slot`, complete at `event` — issued by the previous job of a pipeline."""
-    _prefetch[(str(device), slot)] = (src.data_ptr(), src.numel(), event)
+def set_prefetch(device: str, slot: int, src: torch.Tensor, event, dst: torch.Tensor) -> None:
+    """Record that `src` (a host tensor) is being copied into staging buffer
+    `dst` (slot `slot`), complete at `event` — issued by the previous job of a
+    pipeline."""
+    _prefetch[(str(device), slot)] = (src.data_ptr(), src.numel(), dst.data_ptr(), dst.numel(), event)
 
 
-def take_prefetch(device: str, slot: int, src: torch.Tensor):
-    """The copy event if `src` was prefetched into `slot` (consumed), else None."""
+def take_prefetch(device: str, slot: int, src: torch.Tensor, dst: torch.Tensor):
+    """The copy event if `src` was prefetched into `dst`, the current buffer of
+    `slot` (consumed), else None — also None when the slot's buffer was
+    reallocated since (the copy went to the old one)."""
     rec = _prefetch.pop((str(device), slot), None)
-    if rec is not None and rec[0] == src.data_ptr() and rec[1] == src.numel():
-        return rec[2]
+    if rec is not None and rec[:4] == (src.data_ptr(), src.numel(), dst.data_ptr(), dst.numel()):
+        return rec[4]
     return None
 
 
