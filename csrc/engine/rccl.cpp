@@ -273,12 +273,15 @@ hipEvent_t Rccl::fence_out() {
 hipEvent_t Rccl::sendrecv_async(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
   if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
   fence_in(s);
-  // one transfer is posted as pieces of at most max_msg bytes (both ends cut
-  // the same byte count the same way): single RCCL point-to-point messages of
-  // 2 GiB and more came back incomplete on MI355X (tools/rccl_big.py)
+  // one transfer is posted as pieces of at most max_msg bytes (MRH_RCCL_MAX_MSG,
+  // default 256 MiB; both ends cut the same byte count the same way): on
+  // MI355X (RCCL 2.26.6) a single point-to-point message of 1 GiB + 40 bytes
+  // came back wrong from element 67141632 on (~512 MiB) while the same data in
+  // 1 GiB pieces arrived intact up to 4 GiB (tools/rccl_big.py,
+  // profiles/r4_rccl_big_messages.txt)
   static const int64_t max_msg = [] {
     const char* e = std::getenv("MRH_RCCL_MAX_MSG");
-    const long long v = e && *e ? std::atoll(e) : (1LL << 30);
+    const long long v = e && *e ? std::atoll(e) : (1LL << 28);
     return v > 0 ? (int64_t)v : std::numeric_limits<int64_t>::max();
   }();
   check(ncclGroupStart(), "ncclGroupStart");

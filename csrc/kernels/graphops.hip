@@ -155,11 +155,21 @@ __global__ __launch_bounds__(NT) void k_pr_pack(const uint64_t* __restrict__ su,
 // to the destination owner, which gathers c = r / outdeg from the replicated
 // (all-gathered) c vector.
 
+// q = x / d for x, d < 2^31 without an integer divide (none in hardware):
+// a double product (exact to well under one unit) and one correction step
+__device__ __forceinline__ uint32_t pr_udiv(uint32_t x, uint32_t d, double inv) {
+  uint32_t q = (uint32_t)((double)x * inv);
+  if (q * d > x) --q;
+  else if ((q + 1) * d <= x) ++q;
+  return q;
+}
+
 // edge (u, v) -> packed (sigma(u) << 32 | sigma(v)), destination rank
 // sigma(u) % P
 __global__ __launch_bounds__(NT) void k_pr_mix_pack(const int64_t* __restrict__ e, int64_t n, int P, int64_t N, int b,
                                                     int mix, uint64_t* __restrict__ out, int32_t* __restrict__ dest) {
   const int64_t stride = (int64_t)gridDim.x * NT;
+  const double invP = 1.0 / (double)P;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     uint64_t u = (uint64_t)__builtin_nontemporal_load(e + 2 * i), v = (uint64_t)__builtin_nontemporal_load(e + 2 * i + 1);
     if (mix) {
@@ -167,16 +177,17 @@ __global__ __launch_bounds__(NT) void k_pr_mix_pack(const int64_t* __restrict__ 
       v = dev::vmix(v, N, b);
     }
     out[i] = (u << 32) | v;
-    dest[i] = (int32_t)(u % (uint64_t)P);
+    dest[i] = (int32_t)((uint32_t)u - pr_udiv((uint32_t)u, (uint32_t)P, invP) * (uint32_t)P);
   }
 }
 
 // at the source owner: (su << 32 | sv) -> (su / P << 32 | sv), in place
 __global__ __launch_bounds__(NT) void k_pr_localize(uint64_t* __restrict__ p, int64_t n, int P) {
   const int64_t stride = (int64_t)gridDim.x * NT;
+  const double invP = 1.0 / (double)P;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const uint64_t x = p[i];
-    p[i] = (((x >> 32) / (uint64_t)P) << 32) | (x & 0xffffffffull);
+    p[i] = ((uint64_t)pr_udiv((uint32_t)(x >> 32), (uint32_t)P, invP) << 32) | (x & 0xffffffffull);
   }
 }
 
@@ -187,12 +198,13 @@ __global__ __launch_bounds__(NT) void k_pr_pack_dst(const uint64_t* __restrict__
                                                     const int32_t* __restrict__ nid, uint64_t* __restrict__ out,
                                                     int32_t* __restrict__ dest) {
   const int64_t stride = (int64_t)gridDim.x * NT;
+  const double invP = 1.0 / (double)P;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const uint64_t x = __builtin_nontemporal_load(su + i);
     const uint64_t sv = x & 0xffffffffull;
     const uint64_t pos = (uint64_t)(base + nid[x >> 32]);
     out[i] = (sv << 32) | pos;
-    dest[i] = (int32_t)(sv % (uint64_t)P);
+    dest[i] = (int32_t)((uint32_t)sv - pr_udiv((uint32_t)sv, (uint32_t)P, invP) * (uint32_t)P);
   }
 }
 
@@ -205,12 +217,14 @@ __global__ __launch_bounds__(NT) void k_pr_pack_gather(const uint64_t* __restric
                                                        const int32_t* __restrict__ nid, const int32_t* __restrict__ rb,
                                                        int nr, int dbits, uint64_t* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * NT;
+  const double invP = 1.0 / (double)P, invS = 1.0 / (double)S;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const uint64_t x = __builtin_nontemporal_load(in + i);
     const uint32_t pos = (uint32_t)x;
-    uint64_t hi = (uint64_t)(uint32_t)nid[(x >> 32) / (uint64_t)P];
+    uint64_t hi = (uint64_t)(uint32_t)nid[pr_udiv((uint32_t)(x >> 32), (uint32_t)P, invP)];
     if (rb) {
-      const uint32_t gid = (uint32_t)((pos % (uint64_t)S) * (uint64_t)P + pos / (uint64_t)S);
+      const uint32_t q = pr_udiv(pos, (uint32_t)S, invS);
+      const uint32_t gid = (pos - q * (uint32_t)S) * (uint32_t)P + q;
       hi |= (uint64_t)pr_range_of(gid, rb, nr) << dbits;
     }
     out[i] = (hi << 32) | pos;
