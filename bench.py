@@ -342,6 +342,7 @@ def bench_pagerank_extra(comm, args):
         "pagerank_setup_ms": setup * 1e3,
         "pagerank_kvps_incl_setup": nedge * iters / (dt + setup),
         "pagerank_hip_graph_iterations": pr.graph_iterations,
+        "pagerank_layout": pr.layout,
         "pagerank_config": {"graph": f"RMAT-2^{scale}", "edgefactor": ef, "edges": nedge, "iters": iters,
                             "runs_timed": args.pagerank_steps, "alpha": 0.85, "scaling": "strong",
                             "rank_dtype": "fp32 ranks, fp64 L1/dangling reductions"},
@@ -371,9 +372,130 @@ def _extra(comm, prefix, fn, args, **over):
     out = {f"{prefix}_kvps": r["value"], f"{prefix}_ms": r["ms_per_step"], f"{prefix}_setup_ms": r.get("setup_ms"),
            f"{prefix}_config": dict(r["config"], steps=a.steps, warmup=a.warmup, scaling=r.get("scaling", "weak"),
                                     metric=r["metric"])}
-    for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices"):
+    for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices", "build"):
         if k in r:
             out[f"{prefix}_{k}"] = r[k]
+    return out
+
+
+def bench_wordfreq_files(comm, args):
+    """wordfreq with its file reads (the reference maps files,
+    examples/wordfreq.cpp:64, 104-130): this rank's text as 128 MiB part files
+    in the page cache (a RAM-backed directory), streamed by a RingReader into
+    8 pinned buffers while the job copies and counts the earlier ones; the
+    next job's reads queue behind this job's. Part files are written once
+    before the timed steps (same synthetic text as the wordfreq extra)."""
+    import shutil
+    import tempfile
+
+    from gpu_mapreduce_amd import MapReduce
+    from gpu_mapreduce_amd.models.wordfreq import WordFreq
+    from gpu_mapreduce_amd.utils import synth
+    from gpu_mapreduce_amd.utils.fileio import RingReader
+    per_gpu = int(args.wordfreq_bytes)
+    chunk = min(int(args.file_bytes), per_gpu)
+    base = next((d for d in ("/dev/shm", tempfile.gettempdir())
+                 if os.path.isdir(d) and shutil.disk_usage(d).free >= per_gpu + (1 << 30)), None)
+    if comm.allreduce(0 if base is None else 1, "min") == 0:
+        return {"skipped": f"a rank had no directory with {(per_gpu >> 20) + 1024} MiB free for the part files"}
+    root = tempfile.mkdtemp(prefix=f"mrh_wf_{comm.rank}_", dir=base)
+    reader = None
+    try:
+        paths, left, i = [], per_gpu, 0
+        while left > 0:
+            n = min(chunk, left)
+            t = synth.zipf_text(n, seed=args.seed * 7919 + comm.rank * 1000 + i, device=comm.device)
+            pth = os.path.join(root, f"part-{i:05d}")
+            t.cpu().numpy().tofile(pth)
+            paths.append((pth, n))
+            left -= n
+            i += 1
+        del t
+        if comm.is_cuda:
+            torch.cuda.empty_cache()
+        nloc = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+        nthr = max(4, min(16, (os.cpu_count() or 8) // nloc))
+        reader = RingReader(paths, slots=8, threads=nthr, pin=comm.is_cuda)
+
+        def window(k):
+            nxt = reader.job()
+            app = None
+            for s in range(k):
+                entries, cb = nxt
+                if s < k - 1:
+                    nxt = reader.job()  # queued behind this job's reads
+                app = WordFreq(MapReduce(comm), entries, on_copied=cb)
+                app.run()
+            return app
+
+        window(2)
+        _sync(comm)
+        t0 = time.perf_counter()
+        app = window(args.extra_steps)
+        _sync(comm)
+        dt = comm.allreduce((time.perf_counter() - t0) / args.extra_steps, "max", dtype=torch.float64)
+        total = comm.allreduce(per_gpu, "sum")
+        return {"ms_per_step": dt * 1e3, "kvps": app.nwords / dt, "input_GBps": total / dt / 1e9,
+                "bytes_per_gpu": per_gpu, "part_file_bytes": chunk, "read_threads": nthr, "ring_slots": 8,
+                "words": app.nwords,
+                "steps": args.extra_steps,
+                "note": "part files read from the page cache into a ring of 8 pinned buffers (32 MiB pieces over "
+                        "read_threads threads) while the job copies and counts earlier files; the next job's reads "
+                        "queue behind; nothing cached between jobs"}
+    finally:
+        if reader is not None:
+            reader.close()
+        shutil.rmtree(root, ignore_errors=True)
+
+
+def _forced_rccl_comm(comm):
+    """A one-rank communicator on this rank's GPU that runs the native RCCL
+    transport (MRH_FORCE_RCCL=1, csrc/engine/comm.h): every multi-GPU code
+    path — the exchanges, the all-gathers and allreduces of the PageRank and
+    tri_find plans — runs through a real RCCL communicator on one GPU."""
+    from gpu_mapreduce_amd.parallel.comm import Comm
+    prev = os.environ.get("MRH_FORCE_RCCL")
+    os.environ["MRH_FORCE_RCCL"] = "1"
+    try:
+        c = Comm(group=None, device=comm.device)
+        c.__dict__["_force"] = True
+        if c.native.transport != "rccl":
+            raise RuntimeError(f"forced communicator has transport {c.native.transport}")
+    finally:
+        if prev is None:
+            os.environ.pop("MRH_FORCE_RCCL", None)
+        else:
+            os.environ["MRH_FORCE_RCCL"] = prev
+    return c
+
+
+def bench_dist_plans(comm, args):
+    """One GPU (N=1): PageRank RMAT-26 x20 and tri_find RMAT-24 again through
+    the multi-GPU plans on a forced one-rank RCCL communicator (the paths the
+    8-GPU BASELINE configs run), reported next to the local-path numbers"""
+    out = {}
+    fc = _forced_rccl_comm(comm)
+    try:
+        try:
+            r = bench_pagerank_extra(fc, args)
+            out.update({"pagerank_dist_ms": r["pagerank_ms"], "pagerank_dist_setup_ms": r["pagerank_setup_ms"],
+                        "pagerank_dist_layout": r.get("pagerank_layout")})
+        except Exception as e:  # noqa: BLE001
+            out["pagerank_dist_error"] = f"{type(e).__name__}: {e}"[:500]
+        if args.trifind_scale > 0:
+            from gpu_mapreduce_amd.models.triangles import bench_trifind
+            r = _extra(fc, "trifind_dist", bench_trifind, args, scale=args.trifind_scale, steps=args.extra_steps,
+                       warmup=1)
+            out.update({k: v for k, v in r.items() if k in ("trifind_dist_ms", "trifind_dist_triangles",
+                                                             "trifind_dist_error", "trifind_dist_build")})
+        out["dist_plans_note"] = ("MRH_FORCE_RCCL=1 one-rank RCCL communicator: the PageRank plan of several GPUs "
+                                  "(destination-owned edges, all-gathered c, per-iteration allreduce + all-gather) "
+                                  "and the tri_find split build (key-range exchange, allreduced degrees, row-range "
+                                  "exchange, column all-gather)")
+    finally:
+        del fc
+        if comm.is_cuda:
+            torch.cuda.empty_cache()
     return out
 
 
@@ -449,9 +571,12 @@ def main():
     ap.add_argument("--trifind-scale", type=int, default=None,
                     help="RMAT scale of the tri_find extra (BASELINE config 5: 24 on GPU, 12 on CPU; 0 = skip)")
     ap.add_argument("--wordfreq-bytes", type=float, default=None,
-                    help="text bytes per GPU of the wordfreq extra (BASELINE config 3: 1 GiB per GPU = 8 GiB on "
-                         "8 GPUs; 4e6 on CPU; 0 = skip)")
+                    help="text bytes per GPU of the wordfreq extra (BASELINE config 3: 64 GB over 8 GPUs = 8 GiB "
+                         "per GPU, the default on GPU; 4e6 on CPU; 0 = skip)")
     ap.add_argument("--extra-steps", type=int, default=3, help="timed steps of the tri_find / wordfreq extras")
+    ap.add_argument("--dist-extras", type=int, default=1,
+                    help="N=1: also time PageRank / tri_find through the multi-GPU plans on a forced one-rank RCCL "
+                         "communicator (pagerank_dist_* / trifind_dist_* keys)")
     ap.add_argument("--file-io-steps", type=int, default=3,
                     help="timed steps of the headline job with part-file reads and output write (0 = skip)")
     args = ap.parse_args()
@@ -474,7 +599,7 @@ def main():
     if args.trifind_scale is None:
         args.trifind_scale = 24 if comm.is_cuda else 12
     if args.wordfreq_bytes is None:
-        args.wordfreq_bytes = float(1 << 30) if comm.is_cuda else 4e6
+        args.wordfreq_bytes = float(8 << 30) if comm.is_cuda else 4e6
     if args.workload == "invertedindex":
         res = bench_inverted_index(comm, args)
     elif args.workload == "pagerank":
@@ -525,6 +650,13 @@ def main():
                               file_bytes=min(args.file_bytes, int(args.wordfreq_bytes)),
                               steps=args.extra_steps, warmup=6))  # steady state after ~6 jobs:
             # warmup 1 / 2 / 6 -> 27.1 / 24.7 / 22.8 ms (profiles/r3_wordfreq_input.txt)
+        if args.wordfreq_bytes > 0 and args.file_io_steps > 0:
+            try:
+                res["wordfreq_with_file_io"] = bench_wordfreq_files(comm, args)
+            except Exception as e:  # noqa: BLE001
+                res["wordfreq_with_file_io"] = {"error": f"{type(e).__name__}: {e}"[:500]}
+        if comm.size == 1 and comm.is_cuda and args.dist_extras:
+            res.update(bench_dist_plans(comm, args))
     res.update(rrec)
     res["ranks_joined"] = comm.size
     from gpu_mapreduce_amd.runtime import hbm_pool

@@ -108,4 +108,5 @@ def bench_trifind(comm, args):
                    "scale": scale, "edgefactor": ef, "rmat": "graph500 a=.57 b=c=.19"},
         "triangles": ntri, "unique_edges": g.nedge, "scaling": "strong", "setup_ms": setup * 1e3,
         "hub_vertices": int(C.tri_last_hub_size()),
+        "build": "split" if g._g.split else ("halo" if g._g.distributed else "replicated"),
     }

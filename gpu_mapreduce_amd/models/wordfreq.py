@@ -33,8 +33,15 @@ PAD = 64
 
 
 class WordFreq:
-    def __init__(self, mr: MapReduce, chunks, ntop=10, combiner=True, prefetch_next=None):
-        """chunks: list of uint8 text tensors for this rank (host, ideally pinned).
+    def __init__(self, mr: MapReduce, chunks, ntop=10, combiner=True, prefetch_next=None, on_copied=None):
+        """chunks: list of uint8 text tensors for this rank (host, ideally
+        pinned), or of (tensor, ready) pairs where ready.result() blocks until
+        the tensor holds the chunk (a file read in flight: it is waited for
+        right before that chunk's copy, so reading chunk i+1 overlaps the copy
+        and count of chunk i — the reference's fileread, examples/wordfreq.cpp:
+        104-130). on_copied(i, event): called once chunk i's host->HBM copy is
+        issued, event completing with it (a streaming reader reuses the host
+        buffer after that).
 
         prefetch_next: the chunks of the job that runs next on this rank (a job
         pipeline): the copy of its first chunk is issued behind this job's
@@ -42,7 +49,10 @@ class WordFreq:
         (collate, reduce, top-N); the next job finds that copy and does not
         repeat it."""
         self.prefetch_next = prefetch_next
+        self.on_copied = on_copied
         self.mr = mr
+        self.ready = [c[1] if isinstance(c, (tuple, list)) else None for c in chunks]
+        chunks = [c[0] if isinstance(c, (tuple, list)) else c for c in chunks]
         self.chunks = chunks
         self.ntop = ntop
         self.combiner = combiner
@@ -73,9 +83,13 @@ class WordFreq:
             else:
                 kv.add_kv(C.map_words(buf, n))
         if not self.is_cuda:
-            for t in self.chunks:
+            for i, t in enumerate(self.chunks):
+                if self.ready[i] is not None:
+                    self.ready[i].result()
                 b = self.bufs[0]
                 b[: t.numel()].copy_(t)
+                if self.on_copied is not None:
+                    self.on_copied(i, None)  # copied synchronously: the host buffer is free
                 b[t.numel():t.numel() + PAD].zero_()
                 consume(b, t.numel())
         else:
@@ -110,7 +124,12 @@ class WordFreq:
             if ev is not None:
                 ready[b] = ev
             else:
+                if self.ready[i] is not None:
+                    self.ready[i].result()  # the chunk's bytes are in its host buffer
+                ready[b] = torch.cuda.Event()  # one per copy: a reader may still wait on the previous one
                 copy_into(b, self.chunks[i], ready[b])
+            if self.on_copied is not None:
+                self.on_copied(i, ready[b])
 
         ahead = max(1, nb - 1)
         for i in range(min(ahead, n)):
