@@ -783,22 +783,24 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
 uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kv("aggregate");
-  if (comm_->distributed()) {
+  if (comm_->distributed() && ooc_shuffle()) {
+    // larger than the budget: budget-sized chunks in lock-step, received into
+    // host memory (ooc.h ooc_exchange); a custom hash runs on the host first
+    at::Tensor d;
+    if (hash) d = host_dest(hash);
+    ShuffleStats st;
+    OocStats os;
+    kv = ooc_exchange(*kv, d, *comm_, ooc_env(), device(), set.all2all, &os, &st);
+    note_shuffle(st);
+    note_ooc("Aggregate", os);
+  } else if (comm_->distributed()) {
     ShuffleStats st;
     if (!hash) {
       kv = oom_retry(this, device(), my_proc(), "aggregate", [&] { return mrh::aggregate(*kv, *comm_, xopts(), &st); });
     } else {
-      HostCol k = host_col(kv->kdata, kv->koff, kv->kw);
-      at::Tensor d = at::empty({kv->n}, at::TensorOptions().dtype(at::kInt));
-      int32_t* dp = d.data_ptr<int32_t>();
-      const int P = comm_->size();
-      for (int64_t i = 0; i < kv->n; ++i) {
-        int h = hash(k.at(i), (int)k.len(i));
-        dp[i] = (int32_t)(((int64_t)h % P + P) % P);
-      }
-      kv = exchange(std::move(*kv), d.to(device()), *comm_, xopts(), &st);
+      kv = exchange(std::move(*kv), host_dest(hash).to(device()), *comm_, xopts(), &st);
     }
     note_shuffle(st);
   }
@@ -806,10 +808,33 @@ uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
   return count(kv->n);
 }
 
+// owner rank of every pair by a user hash (MR-MPI's hash callback, run on the
+// host over the KV's bytes; src/mapreduce.cpp:469-472)
+at::Tensor MapReduce::host_dest(const HashFn& hash) const {
+  HostCol k = host_col(kv->kdata, kv->koff, kv->kw);
+  at::Tensor d = at::empty({kv->n}, at::TensorOptions().dtype(at::kInt));
+  int32_t* dp = d.data_ptr<int32_t>();
+  const int P = comm_->size();
+  for (int64_t i = 0; i < kv->n; ++i) {
+    int h = hash(k.at(i), (int)k.len(i));
+    dp[i] = (int32_t)(((int64_t)h % P + P) % P);
+  }
+  return d;
+}
+
+// a shuffle of more than half the HBM budget on any rank streams through
+// ooc_exchange on every rank (the paths' collectives differ, so the choice is
+// collective: one host allreduce, and only for an MR with a budget)
+bool MapReduce::ooc_shuffle() const {
+  if (budget() <= 0) return false;
+  const int64_t mine = kv && needs_ooc(kv->nbytes(), budget(), 2.0) ? 1 : 0;
+  return comm_->allreduce(mine, Comm::MAX) != 0;
+}
+
 uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kv("aggregate");
   if (comm_->distributed()) {
     ShuffleStats st;
@@ -820,7 +845,13 @@ uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
       if (std::get<0>(mm).item<int>() < 0 || std::get<1>(mm).item<int>() >= comm_->size())
         fail("aggregate: destination rank out of range");
     }
-    kv = exchange(std::move(*kv), d, *comm_, xopts(), &st);
+    if (ooc_shuffle()) {
+      OocStats os;
+      kv = ooc_exchange(*kv, d.to(at::kCPU), *comm_, ooc_env(), device(), set.all2all, &os, &st);
+      note_ooc("Aggregate", os);
+    } else {
+      kv = exchange(std::move(*kv), d, *comm_, xopts(), &st);
+    }
     note_shuffle(st);
   }
   stats("Aggregate", 0);
@@ -840,12 +871,19 @@ uint64_t MapReduce::broadcast(int root) {  // :569-623
 uint64_t MapReduce::gather(int nprocs) {  // :893-1036
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kv("gather");
   if (nprocs < 1 || nprocs > comm_->size()) fail("Invalid proc count for gather");
   if (comm_->distributed() && (nprocs < comm_->size() || comm_->uses_rccl())) {
     ShuffleStats st;
-    kv = gather_to(std::move(*kv), nprocs, *comm_, xopts(), &st);
+    if (ooc_shuffle()) {  // rank r's pairs to r % nprocs, budget-sized chunks into host memory
+      OocStats os;
+      at::Tensor d = at::full({kv->n}, comm_->rank() % nprocs, at::TensorOptions().dtype(at::kInt));
+      kv = ooc_exchange(*kv, d, *comm_, ooc_env(), device(), set.all2all, &os, &st);
+      note_ooc("Gather", os);
+    } else {
+      kv = gather_to(std::move(*kv), nprocs, *comm_, xopts(), &st);
+    }
     note_shuffle(st);
   }
   stats("Gather", 0);
@@ -890,7 +928,7 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
 uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);  // with a budget: aggregate and convert stream out-of-core data themselves
   need_kv("collate");
   // pipelined collate: the hash-partition exchange hands every received round
   // to a GroupIndex, which groups it on the compute stream while the next
@@ -940,10 +978,22 @@ uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
   return count(kmv->nkey);
 }
 
+// compress's local group-by: out of core (hash-partitioned spools) past the budget
+KMV MapReduce::local_groups(const char* heading) {
+  last_convert = ConvertStats();
+  if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
+    OocStats os;
+    KMV m = ooc_convert(*kv, ooc_env(), device(), &os);
+    note_ooc(heading, os);
+    return m;
+  }
+  return mrh::convert(*kv, &last_convert);
+}
+
 uint64_t MapReduce::clone() {  // :631-652
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);  // one value per key: a host-resident KV is cloned where it lives
   need_kv("clone");
   kmv = oom_retry(this, device(), my_proc(), "clone", [&] { return mrh::clone(*kv); });
   kv.reset();
@@ -1087,11 +1137,19 @@ uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dty
 uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kmv("reduce");
   KeyValue kvb(device());
   bound(kvb);
-  fn(*kmv, kvb);
+  if (needs_ooc(kmv->nbytes(), budget(), 2.0)) {
+    // key ranges whose values fit the budget go to HBM one at a time; the
+    // batch callback sees each as a KMV of its own (in key order)
+    OocStats os;
+    ooc_for_each_kmv_piece(*kmv, ooc_env(), device(), [&](const KMV& piece) { fn(piece, kvb); }, &os);
+    note_ooc("Reduce", os);
+  } else {
+    fn(*kmv, kvb);
+  }
   kv = kvb.finish();
   note_spool(kvb);
   kmv.reset();
@@ -1102,9 +1160,9 @@ uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
 uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);  // host callbacks read the (host-resident) groups in place
   need_kv("compress");
-  KMV m = mrh::convert(*kv, &last_convert);
+  KMV m = local_groups("Compress");
   KeyValue kvb(device());
   bound(kvb);
   run_host_kmv(m, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
@@ -1117,10 +1175,16 @@ uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
 uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& dtype) {
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);
   need_kv("compress");
-  KMV m = mrh::convert(*kv, &last_convert);
-  kv = mrh::reduce_builtin(m, op, dtype.empty() ? "int32" : dtype);
+  KMV m = local_groups("Compress");
+  if (needs_ooc(m.nbytes(), budget(), 2.0)) {
+    OocStats os;
+    kv = ooc_reduce_builtin(m, op, dtype.empty() ? "int32" : dtype, ooc_env(), device(), &os);
+    note_ooc("Compress", os);
+  } else {
+    kv = mrh::reduce_builtin(m, op, dtype.empty() ? "int32" : dtype);
+  }
   stats("Compress", 0);
   return count(kv->n);
 }

@@ -206,6 +206,11 @@ class MapReduce {
  private:
   void note_spool(const KeyValue& b);
   void note_ooc(const char* op, const OocStats& st);
+  // out-of-core helpers: a shuffle past the budget, a user hash's owner ranks
+  // (host), compress's group-by
+  bool ooc_shuffle() const;
+  at::Tensor host_dest(const HashFn& hash) const;
+  KMV local_groups(const char* heading);
   void stats(const char* heading, int which);
   void need_kv(const char* what) const;
   void need_kmv(const char* what) const;

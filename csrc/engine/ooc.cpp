@@ -43,6 +43,7 @@
 
 #include "../kernels/launch.h"
 #include "kv.h"
+#include "comm.h"
 #include "ooc.h"
 #include "spool.h"
 
@@ -423,8 +424,48 @@ KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device
   return sink.finish(kv);
 }
 
-KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, const OocEnv& env,
-                      at::Device dev, OocStats* st) {
+KV ooc_exchange(const KV& kv, const at::Tensor& dest_host, const Comm& comm, const OocEnv& env, at::Device dev,
+                int all2all, OocStats* st, ShuffleStats* sst) {
+  const int64_t cap = std::max<int64_t>(env.hbm / 4, 1);
+  const HostOff h = host_off(kv);
+  const auto ch = chunks(kv, h, cap);
+  // lock-step chunks: a rank with fewer (or none) joins with empty ones
+  const int64_t R = comm.allreduce((int64_t)ch.size(), Comm::MAX);
+  at::Tensor dh = dest_host.defined() ? dest_host.to(at::kCPU).to(at::kInt).contiguous() : at::Tensor();
+  if (dh.defined() && dh.numel() != kv.n) throw std::runtime_error("ooc_exchange: one destination per pair");
+  ExchangeOpts o;
+  o.chunk_bytes = cap;           // receive rounds of at most one chunk
+  o.host_sink = dev.is_cuda();   // received pairs land in pinned host memory, not HBM
+  o.all2all = all2all;
+  KVSink sink{env, st};
+  for (int64_t r = 0; r < R; ++r) {
+    const bool mine = r < (int64_t)ch.size();
+    KV c = mine ? kv_to(kv_slice(kv, ch[r].first, ch[r].second, h.kp(), h.vp()), dev) : empty_kv(dev, kv.kw, kv.vw);
+    at::Tensor d;
+    if (dh.defined())
+      d = (mine ? dh.narrow(0, ch[r].first, ch[r].second - ch[r].first) : at::empty({0}, opt(at::kCPU, at::kInt))).to(dev);
+    ShuffleStats s1;
+    KV out = exchange(std::move(c), d, comm, o, &s1);
+    if (sst) {
+      sst->send_bytes += s1.send_bytes;
+      sst->recv_bytes += s1.recv_bytes;
+      sst->send_pairs += s1.send_pairs;
+      sst->recv_pairs += s1.recv_pairs;
+      sst->rounds += s1.rounds;
+      sst->seconds += s1.seconds;
+    }
+    if (out.n) sink.add(out);
+    if (st) {
+      st->chunks++;
+      if (mine) st->bytes_staged += row_bytes(kv, h, ch[r].first, ch[r].second);
+    }
+  }
+  if (st) st->parts = R;
+  return sink.finish(kv);
+}
+
+void ooc_for_each_kmv_piece(const KMV& kmv, const OocEnv& env, at::Device dev, const std::function<void(const KMV&)>& fn,
+                            OocStats* st) {
   const int64_t budget = env.hbm;
   at::Tensor seg = kmv.seg.to(at::kCPU).contiguous();
   const int64_t* s = seg.data_ptr<int64_t>();
@@ -436,7 +477,6 @@ KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& 
     return kmv.vw >= 0 ? (s[b] - s[a]) * kmv.vw : vop[s[b]] - vop[s[a]] + 8 * (s[b] - s[a]);
   };
   const int64_t cap = std::max<int64_t>(budget / 4, 1);
-  KVSink sink{env, st};
   int64_t a = 0;
   while (a < kmv.nkey) {
     const int64_t b = grow(a, kmv.nkey, [&](int64_t e) { return vbytes(a, e) <= cap; });
@@ -457,10 +497,16 @@ KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& 
     md.vdata = m.vdata.to(dev);
     if (m.voff.defined()) md.voff = m.voff.to(dev);
     md.seg = m.seg.to(dev);
-    sink.add(reduce_builtin(md, op, dtype));
+    fn(md);
     if (st) st->chunks++;
     a = b;
   }
+}
+
+KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, const OocEnv& env,
+                      at::Device dev, OocStats* st) {
+  KVSink sink{env, st};
+  ooc_for_each_kmv_piece(kmv, env, dev, [&](const KMV& md) { sink.add(reduce_builtin(md, op, dtype)); }, st);
   if (sink.parts.empty()) return kv_host(reduce_builtin(kmv, op, dtype));
   return sink.finish(sink.parts[0]);
 }

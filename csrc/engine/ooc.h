@@ -1,6 +1,7 @@
 // Out-of-core convert / sort / builtin reduce (ooc.cpp): the KV or KMV lives
 // in pinned host memory and HBM holds one budget-sized piece at a time.
 #pragma once
+#include <functional>
 #include <string>
 
 #include "kv.h"
@@ -33,5 +34,18 @@ KMV ooc_convert(const KV& kv, const OocEnv& env, at::Device dev, OocStats* st = 
 KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device dev, OocStats* st = nullptr);
 KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, const OocEnv& env,
                       at::Device dev, OocStats* st = nullptr);
+// every key range of a (host-resident) KMV whose values fit a quarter of the
+// budget, as a device KMV, to fn in key order (the reduce-family ops)
+void ooc_for_each_kmv_piece(const KMV& kmv, const OocEnv& env, at::Device dev, const std::function<void(const KMV&)>& fn,
+                            OocStats* st = nullptr);
+// the shuffle of a KV larger than the budget (MR-MPI's paged aggregate,
+// src/mapreduce.cpp:385-563: pages in lock-step up to the global page count,
+// a two-page receive window): budget/4-byte chunks go to HBM one at a time,
+// every rank the same number of rounds; each chunk's exchange receives in
+// budget/4-byte rounds into pinned host memory, and the received pairs
+// collect in pinned host memory up to env.host, in files beyond it.
+// dest_host: one int32 destination per pair (undefined: hash partitioning)
+KV ooc_exchange(const KV& kv, const at::Tensor& dest_host, const Comm& comm, const OocEnv& env, at::Device dev,
+                int all2all = 1, OocStats* st = nullptr, ShuffleStats* sst = nullptr);
 
 }  // namespace mrh

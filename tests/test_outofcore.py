@@ -147,3 +147,97 @@ def test_tiers_hbm_host_disk_cpu(tmp_path):
 @pytest.mark.gpu
 def test_tiers_hbm_host_disk_gpu(tmp_path):
     _tiered_run("cuda:0", tmp_path)
+
+
+def case_ooc_pipeline(comm):
+    """map -> collate -> reduce("count"), -> collate -> host-callback reduce,
+    and compress / gather, with hbm_budget = 1/20 and host_budget = 1/4 of the
+    data: the shuffle streams budget-sized chunks into host memory
+    (ooc_exchange), convert / reduce partition into spools that reach the disk
+    tier. Returns what each rank ends with plus the spool evidence."""
+    import os
+    C = g._ext.C
+    d = os.path.join(os.environ["MRH_OOC_TEST_DIR"], f"r{comm.rank}")
+    os.makedirs(d, exist_ok=True)
+    P = comm.size
+
+    def task(i, kv):  # map task i: WORDS[i::P], whichever rank runs it
+        for j, w in enumerate(WORDS[i::P]):
+            kv.add(w, struct.pack("<i", j))
+    ref = MapReduce(comm)
+    ref.map(P, task)
+    data = comm.allreduce(ref.kv.nbytes(), "max")
+    del ref
+    live0 = C.spool_files_live()
+    seen = set()
+
+    def peek():
+        seen.update(p for p in os.listdir(d) if p.startswith("mrmpi."))
+
+    def tiered():
+        mr = MapReduce(comm)
+        mr.fpath = d
+        mr.hbm_budget = data // 20
+        mr.host_budget = data // 4
+        mr.memsize = -16384
+        mr.map(P, task)
+        return mr
+
+    mr = tiered()
+    nu = mr.collate()
+    peek()
+    mr.reduce("count")
+    counts = {k: struct.unpack("<i", v)[0] for k, v in mr.kv_pairs()}
+    st = dict(mr.spool_stats)
+    mr2 = tiered()
+    mr2.collate()
+    mr2.reduce(lambda k, mv, kv: kv.add(k, struct.pack("<q", sum(struct.unpack("<i", x)[0] for x in mv))))
+    sums = {k: struct.unpack("<q", v)[0] for k, v in mr2.kv_pairs()}
+    mr3 = tiered()
+    mr3.compress("count")              # local groups, out of core
+    mr3.gather(1)                      # every rank's pairs to rank 0, chunked into host memory
+    gathered = list(mr3.kv_pairs())
+    peek()
+    del mr, mr2, mr3
+    import gc
+    gc.collect()
+    left = [p for p in os.listdir(d) if p.startswith("mrmpi.")]
+    return nu, counts, sums, len(gathered), st, sorted(seen), left, C.spool_files_live() - live0
+
+
+def _ooc_world(world, device, tmp_path, monkeypatch):
+    from test_distributed_cpu import run_world
+    monkeypatch.setenv("MRH_OOC_TEST_DIR", str(tmp_path))
+    out = run_world("test_outofcore:case_ooc_pipeline", world, device)
+    want = collections.Counter(WORDS)
+    want_sums = collections.Counter()
+    # value sums: map task i numbers WORDS[i::world]
+    for i in range(world):
+        for j, w in enumerate(WORDS[i::world]):
+            want_sums[w] += j
+    counts, sums, gathered_total = {}, {}, 0
+    for r in range(world):
+        nu, c, s, ng, st, seen, left, live = out[r]
+        assert nu == len(want)
+        assert not (set(counts) & set(c)), "a key owned by two ranks"
+        counts.update(c)
+        sums.update(s)
+        gathered_total += ng
+        assert seen, "spool files must appear under fpath"
+        assert not left and live == 0, (left, live)      # every spool file removed again
+    assert counts == dict(want)
+    assert sums == dict(want_sums)
+    # compress("count") then gather(1): rank 0 holds every rank's local groups
+    assert out[0][3] == gathered_total and gathered_total >= len(want)
+
+
+def test_ooc_distributed_pipeline_cpu(tmp_path, monkeypatch):
+    _ooc_world(2, "cpu", tmp_path, monkeypatch)
+
+
+@pytest.mark.gpu
+def test_ooc_distributed_pipeline_gpu(tmp_path, monkeypatch):
+    """two ranks on the box's GPU (gloo transport): the device engine under an
+    HBM budget of 1/20 of the data and its pool cap (a chunk too large for
+    the cap fails with "Cannot allocate page")"""
+    _ooc_world(2, "cuda:0", tmp_path, monkeypatch)
