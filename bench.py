@@ -226,16 +226,29 @@ def bench_inverted_index_files(comm, args):
             ready = [_FileRead([f for f, j in zip(futs, jobs) if j[0] == i]) for i in range(len(paths))]
             return [(paths[i][0], bufsets[k][i], ready[i]) for i in range(len(paths))]
 
+        do_read = getattr(args, "fileio_read", True)    # probes (tools/ii_fileio_probe.py): drop one side
+        do_write = getattr(args, "fileio_write", True)
+        if not do_read:
+            for k in range(2):
+                for i in range(len(paths)):
+                    for j in jobs:
+                        if j[0] == i:
+                            read_piece(j, k)
+
         def window(k):
             """k jobs back to back: job s's part files are read while job s-1
             runs, job s copies job s+1's first file behind its own last one and
             its index is written by the writer thread during job s+1; the
             window ends when the last job's index is on disk"""
-            files = reads(0)
+            def get(s):
+                if do_read:
+                    return reads(s)
+                return [(paths[i][0], bufsets[s % 2][i]) for i in range(len(paths))]
+            files = get(0)
             apps = []
             for s in range(k):
-                nxt = reads(s + 1) if s < k - 1 else None
-                app = InvertedIndex(MapReduce(comm), files, out_dir=outdir, async_write=True,
+                nxt = get(s + 1) if s < k - 1 else None
+                app = InvertedIndex(MapReduce(comm), files, out_dir=outdir if do_write else None, async_write=True,
                                     prefetch_next=nxt)
                 app.run()
                 apps.append(app)

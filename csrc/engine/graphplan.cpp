@@ -22,6 +22,28 @@ namespace {
 constexpr int64_t VMASK = (int64_t(1) << 40) - 1;
 at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
 
+// MRH_PR_STAGES=1: device-synchronised wall time of every plan-build stage on
+// stderr (the setup breakdown of profiles/r4_pagerank_setup_stages.txt)
+struct StageClock {
+  bool on = false;
+  double t = 0;
+  StageClock() {
+    const char* e = std::getenv("MRH_PR_STAGES");
+    on = e && *e == '1';
+    if (on) {
+      (void)hipDeviceSynchronize();
+      t = Comm::wtime();
+    }
+  }
+  void operator()(const char* what) {
+    if (!on) return;
+    (void)hipDeviceSynchronize();
+    const double now = Comm::wtime();
+    std::fprintf(stderr, "mrhip PageRankPlan stage %-22s %8.2f ms\n", what, 1e3 * (now - t));
+    t = now;
+  }
+};
+
 at::Tensor iota32(int64_t n, at::Device d) { return at::arange(n, opt(d, at::kInt)); }
 
 // stable (keys, perm) sort; tolerates n == 0
@@ -234,7 +256,9 @@ at::Tensor sssp_predecessors(const EdgePlan& plan, const at::Tensor& edges, cons
 PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, double a)
     : comm(std::move(c)), P(comm->size()), me(comm->rank()), dev(comm->device()), N(nvert), alpha(a) {
   nlocal = std::max<int64_t>(0, (N - me + P - 1) / P);
+  StageClock clk;
   at::Tensor e = edges.to(dev).to(at::kLong).reshape({-1, 2});
+  clk("edges to device");
   // several GPUs (or the forced-RCCL rank): destination-owned edges and a
   // replicated c vector (build_device_dist); MRH_PR_DIST=partials keeps the
   // source-owned plan with an all-to-all of per-destination partial sums
@@ -249,6 +273,7 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
     if (dev.is_cuda() && nedge < (int64_t(1) << 32) && N < (int64_t(1) << 31)) build_device(e.contiguous());
     else build_host(e);
   }
+  clk("plan (total)");
   e = at::Tensor();
   const int64_t ngrp = seg_.numel() - 1;
   // one GPU, opt-in (MRH_PR_BLOCKING=1): propagation blocking (pbpr.hip).
@@ -277,7 +302,9 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
       six_.slen = xslen_;
     }
   }
+  clk("segment index");
   reset();
+  clk("reset");
 }
 
 // Device build: two keys-only sorts of packed edges, no group-by, no
@@ -359,6 +386,7 @@ int64_t PageRankPlan::relabel_by_degree(const at::Tensor& su, bool want_degn, at
 }
 
 void PageRankPlan::build_device(const at::Tensor& e) {
+  StageClock clk;
   const hipStream_t s = at::hip::getCurrentHIPStream();
   const bool dist = comm->distributed();
   const int64_t nlmax = (N + P - 1) / P;
@@ -370,6 +398,7 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     k::pr_pack_src(e.data_ptr<int64_t>(), nedge, P, reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
     su = radix_sort_keys(packed, 32, 32 + bits_for(std::max<int64_t>(nlocal - 1, 0)), false);
   }
+  clk("pack + sort by source");
   // 2. vertices by degree; XCD source ranges (one GPU; MRH_PR_XCD=0
   // disables): see xcd_ranges()
   const char* xenv = std::getenv("MRH_PR_XCD");
@@ -378,6 +407,7 @@ void PageRankPlan::build_device(const at::Tensor& e) {
   at::Tensor nid, degn;
   const int64_t ndl = relabel_by_degree(su, want_xcd, nid, degn);
   const int64_t nactive = std::max<int64_t>(nlocal - ndl, 0);
+  clk("degrees + relabel");
   // 3. by destination group, new source ids in the low word; with XCD source
   // ranges the groups are (range, destination)
   const int64_t himax = !dist ? std::max<int64_t>(N - 1, 0) : P * nlmax - 1;
@@ -400,9 +430,11 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     k::pr_pack(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, P, nlmax, !dist, nid.data_ptr<int32_t>(),
                nhot > 0 ? rbd.data_ptr<int32_t>() : nullptr, nhot, dbits, reinterpret_cast<uint64_t*>(packed.data_ptr()),
                s);
+    clk("xcd ranges + pack");
     su = at::Tensor();
     sorted = radix_sort_keys(packed, 32, 32 + dbits + rbits, false);
   }
+  clk("sort by destination");
   // 4. unpack
   src_ = at::empty({nedge}, opt(dev, at::kInt));
   {
@@ -437,6 +469,7 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nullptr, (int64_t(1) << dbits) - 1, vid_.data_ptr<int32_t>(), s);
   }
   ndangling = comm->allreduce(ndl, Comm::SUM);
+  clk("unpack + groups");
 }
 
 // Multi-GPU device build: destination-owned edges, replicated c vector.
@@ -461,6 +494,7 @@ void PageRankPlan::build_device(const at::Tensor& e) {
 // One rank (the forced-RCCL mode) uses sigma = identity: the plan and its
 // results are then bitwise those of build_device.
 void PageRankPlan::build_device_dist(const at::Tensor& e) {
+  StageClock clk;
   const hipStream_t s = at::hip::getCurrentHIPStream();
   dist_dev_ = true;
   mix_ = P > 1;
@@ -478,9 +512,11 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
                    dest.data_ptr<int32_t>(), s);
     packed = route_u64(*comm, packed, dest);
     dest = at::Tensor();
+    clk("exchange to source owner");
     k::pr_localize(reinterpret_cast<uint64_t*>(packed.data_ptr()), packed.numel(), P, s);
     su = radix_sort_keys(packed, 32, 32 + pr_bits_for(std::max<int64_t>(nlocal - 1, 0)), false);
   }
+  clk("sort by source");
   const char* xenv = std::getenv("MRH_PR_XCD");
   const bool want_xcd = !(xenv && *xenv == '0');
   at::Tensor nid, degn;
@@ -492,6 +528,7 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   S = (std::max<int64_t>(S, 1) + 15) / 16 * 16;
   if (P * S >= (int64_t(1) << 31)) throw std::runtime_error("PageRankPlan: replicated c vector needs P * S < 2^31");
   S_ = S;
+  clk("degrees + relabel");
   // 2. to the destination owner
   at::Tensor pk;
   {
@@ -505,6 +542,7 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   }
   nedge = pk.numel();
   if (nedge >= (int64_t(1) << 32)) throw std::runtime_error("PageRankPlan: >= 2^32 in-edges on one rank");
+  clk("exchange to dest owner");
   // 3. XCD source ranges over the interleaved global order; the degree of
   // every gid is the all-gathered degree array read column-major
   const int dbits = pr_bits_for(std::max<int64_t>(nlocal - 1, 0));
@@ -537,8 +575,10 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
                       nhot > 0 ? rbd.data_ptr<int32_t>() : nullptr, nhot, dbits,
                       reinterpret_cast<uint64_t*>(key.data_ptr()), s);
     pk = at::Tensor();
+    clk("xcd ranges + pack");
     sorted = radix_sort_keys(key, 32, 32 + dbits + rbits, false);
   }
+  clk("sort by destination");
   src_ = at::empty({nedge}, opt(dev, at::kInt));
   {
     at::Tensor flags = at::empty({nedge}, opt(dev, at::kInt));
@@ -575,6 +615,7 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   // the next slice, which the all-gather then overwrites), hence the slack
   cfull_ = at::zeros({P * S + nlmax + 64}, opt(dev, at::kFloat));
   c_ = cfull_.narrow(0, (int64_t)me * S, nlocal);
+  clk("unpack + groups");
 }
 
 // one multi-GPU iteration from r into rn: gather from the replicated c,
