@@ -590,7 +590,7 @@ def main():
     ap.add_argument("--dist-extras", type=int, default=1,
                     help="N=1: also time PageRank / tri_find through the multi-GPU plans on a forced one-rank RCCL "
                          "communicator (pagerank_dist_* / trifind_dist_* keys)")
-    ap.add_argument("--file-io-steps", type=int, default=3,
+    ap.add_argument("--file-io-steps", type=int, default=8,
                     help="timed steps of the headline job with part-file reads and output write (0 = skip)")
     args = ap.parse_args()
     if args.scale is None:

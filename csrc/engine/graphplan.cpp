@@ -343,25 +343,42 @@ at::Tensor route_u64(const Comm& comm, const at::Tensor& keys, const at::Tensor&
 }
 }  // namespace
 
-// Steps 1-2 of both device builds. su: this rank's out-edges packed as
-// (local source << 32 | destination), sorted on the source bits (the run
-// lengths are the out-degrees). Sorts the nlocal vertices by degree
+// out-degrees of this rank's out-edges, packed (destination << 32 | local
+// source) in any order (count_low_words: a partitioned LDS count) or — the
+// older build, MRH_PR_DEGREES=sort — (local source << 32 | destination)
+// sorted on the source bits, whose run lengths are the degrees
+at::Tensor PageRankPlan::out_degrees(const at::Tensor& packed, bool sorted_by_source) {
+  const hipStream_t s = at::hip::getCurrentHIPStream();
+  const int64_t ne = packed.numel();
+  at::Tensor deg = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
+  pr_chk(hipMemsetAsync(deg.data_ptr(), 0, deg.numel() * 4, s), "hipMemsetAsync");
+  if (ne == 0) return deg;
+  if (!sorted_by_source) {
+    count_low_words(packed, deg);
+    return deg;
+  }
+  at::Tensor flags = at::empty({ne}, opt(dev, at::kInt));
+  k::pr_heads(reinterpret_cast<const uint64_t*>(packed.data_ptr()), ne, reinterpret_cast<uint32_t*>(flags.data_ptr()),
+              s);
+  at::Tensor useg = segments_from_flags(flags);
+  flags = at::Tensor();
+  k::pr_run_degree(reinterpret_cast<const uint64_t*>(packed.data_ptr()), useg.data_ptr<int64_t>(), useg.numel() - 1,
+                   reinterpret_cast<uint32_t*>(deg.data_ptr()), s);
+  return deg;
+}
+
+bool PageRankPlan::degrees_by_sort() {
+  const char* e = std::getenv("MRH_PR_DEGREES");
+  return e && std::strcmp(e, "sort") == 0;
+}
+
+// Step 2 of both device builds: deg = out-degree of every local vertex (int32
+// [max(nlocal, 1)], out_degrees). Sorts the nlocal vertices by degree
 // (descending, stable) and writes the new id of every old local id (nid),
 // order_, dangling_, invdeg_; degn (if want_degn): the degree of every new id.
 // Returns the number of dangling (out-degree 0) local vertices.
-int64_t PageRankPlan::relabel_by_degree(const at::Tensor& su, bool want_degn, at::Tensor& nid, at::Tensor& degn) {
+int64_t PageRankPlan::relabel_by_degree(at::Tensor deg, bool want_degn, at::Tensor& nid, at::Tensor& degn) {
   const hipStream_t s = at::hip::getCurrentHIPStream();
-  const int64_t ne = su.numel();
-  at::Tensor deg = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
-  pr_chk(hipMemsetAsync(deg.data_ptr(), 0, deg.numel() * 4, s), "hipMemsetAsync");
-  if (ne > 0) {
-    at::Tensor flags = at::empty({ne}, opt(dev, at::kInt));
-    k::pr_heads(reinterpret_cast<const uint64_t*>(su.data_ptr()), ne, reinterpret_cast<uint32_t*>(flags.data_ptr()), s);
-    at::Tensor useg = segments_from_flags(flags);
-    flags = at::Tensor();
-    k::pr_run_degree(reinterpret_cast<const uint64_t*>(su.data_ptr()), useg.data_ptr<int64_t>(), useg.numel() - 1,
-                     reinterpret_cast<uint32_t*>(deg.data_ptr()), s);
-  }
   nid = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
   order_ = at::empty({nlocal}, opt(dev, at::kLong));
   dangling_ = at::empty({nlocal}, opt(dev, at::kByte));
@@ -391,23 +408,28 @@ void PageRankPlan::build_device(const at::Tensor& e) {
   const bool dist = comm->distributed();
   const int64_t nlmax = (N + P - 1) / P;
   auto bits_for = pr_bits_for;
-  // 1. by source
-  at::Tensor su;
+  // 1. out-degrees: a partitioned count over (destination << 32 | source)
+  // (MRH_PR_DEGREES=sort: sort (source << 32 | destination) on the source
+  // bits, degrees = run lengths — ~2x the time on RMAT-26)
+  const bool bysort = degrees_by_sort() || dist;
+  at::Tensor su, deg;
   {
     at::Tensor packed = at::empty({nedge}, opt(dev, at::kLong));
-    k::pr_pack_src(e.data_ptr<int64_t>(), nedge, P, reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
-    su = radix_sort_keys(packed, 32, 32 + bits_for(std::max<int64_t>(nlocal - 1, 0)), false);
+    k::pr_pack_src(e.data_ptr<int64_t>(), nedge, P, !bysort, reinterpret_cast<uint64_t*>(packed.data_ptr()), s);
+    su = bysort ? radix_sort_keys(packed, 32, 32 + bits_for(std::max<int64_t>(nlocal - 1, 0)), false) : packed;
+    deg = out_degrees(su, bysort);
   }
-  clk("pack + sort by source");
+  clk("pack + out-degrees");
   // 2. vertices by degree; XCD source ranges (one GPU; MRH_PR_XCD=0
   // disables): see xcd_ranges()
   const char* xenv = std::getenv("MRH_PR_XCD");
   const char* benv = std::getenv("MRH_PR_BLOCKING");  // propagation blocking needs the plain layout
   const bool want_xcd = !dist && !(xenv && *xenv == '0') && !(benv && *benv == '1');
   at::Tensor nid, degn;
-  const int64_t ndl = relabel_by_degree(su, want_xcd, nid, degn);
+  const int64_t ndl = relabel_by_degree(deg, want_xcd, nid, degn);
+  deg = at::Tensor();
   const int64_t nactive = std::max<int64_t>(nlocal - ndl, 0);
-  clk("degrees + relabel");
+  clk("relabel");
   // 3. by destination group, new source ids in the low word; with XCD source
   // ranges the groups are (range, destination)
   const int64_t himax = !dist ? std::max<int64_t>(N - 1, 0) : P * nlmax - 1;
@@ -427,7 +449,7 @@ void PageRankPlan::build_device(const at::Tensor& e) {
   at::Tensor sorted;
   {
     at::Tensor packed = at::empty({nedge}, opt(dev, at::kLong));
-    k::pr_pack(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, P, nlmax, !dist, nid.data_ptr<int32_t>(),
+    k::pr_pack(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, P, nlmax, !dist, !bysort, nid.data_ptr<int32_t>(),
                nhot > 0 ? rbd.data_ptr<int32_t>() : nullptr, nhot, dbits, reinterpret_cast<uint64_t*>(packed.data_ptr()),
                s);
     clk("xcd ranges + pack");
@@ -514,13 +536,15 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
     dest = at::Tensor();
     clk("exchange to source owner");
     k::pr_localize(reinterpret_cast<uint64_t*>(packed.data_ptr()), packed.numel(), P, s);
-    su = radix_sort_keys(packed, 32, 32 + pr_bits_for(std::max<int64_t>(nlocal - 1, 0)), false);
+    su = packed;  // (sv << 32 | local source), in arrival order
   }
-  clk("sort by source");
+  at::Tensor deg = out_degrees(su, false);
+  clk("out-degrees");
   const char* xenv = std::getenv("MRH_PR_XCD");
   const bool want_xcd = !(xenv && *xenv == '0');
   at::Tensor nid, degn;
-  const int64_t ndl = relabel_by_degree(su, want_xcd, nid, degn);
+  const int64_t ndl = relabel_by_degree(deg, want_xcd, nid, degn);
+  deg = at::Tensor();
   const int64_t nactive = std::max<int64_t>(nlocal - ndl, 0);
   ndangling = comm->allreduce(ndl, Comm::SUM);
   // slice length: the largest active count, a multiple of 16 (64-byte aligned slices)
@@ -603,10 +627,9 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   if (nhot > 0 && ngrp > 0) {
     // exact first edge of every range on this rank (the gather's wave
     // schedule); the ranges themselves came from the global degrees
-    at::Tensor first = xoff_.view({xr_, xtile_ + 1}).select(1, 0).contiguous();
-    std::vector<int64_t> fg = to_vec(first), sg = to_vec(seg_);
-    redge.clear();
-    for (int64_t r = 0; r < xr_; ++r) redge.push_back(sg[std::min<int64_t>(fg[r], ngrp)]);
+    at::Tensor first = xoff_.view({xr_, xtile_ + 1}).select(1, 0).clamp_max(ngrp).contiguous();
+    std::vector<int64_t> re = to_vec(seg_.index_select(0, first));  // xr_ entries, not the whole seg_
+    redge.assign(re.begin(), re.end());
     redge.push_back(nedge);
     xcd_schedule(redge);
   }

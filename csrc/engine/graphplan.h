@@ -120,9 +120,11 @@ class PageRankPlan {
   // tensor-op twin on the CPU engine
   void build_device(const at::Tensor& e);
   void build_host(const at::Tensor& e);
-  // out-degrees of source-sorted packed edges + the degree relabel (both
-  // device builds); returns the local dangling count
-  int64_t relabel_by_degree(const at::Tensor& su, bool want_degn, at::Tensor& nid, at::Tensor& degn);
+  // out-degrees (partitioned count, or run lengths of a source sort) and the
+  // degree relabel (both device builds); relabel returns the local dangling count
+  at::Tensor out_degrees(const at::Tensor& packed, bool sorted_by_source);
+  static bool degrees_by_sort();
+  int64_t relabel_by_degree(at::Tensor deg, bool want_degn, at::Tensor& nid, at::Tensor& degn);
   // several GPUs: destination-owned edges, replicated c vector (graphplan.cpp)
   void build_device_dist(const at::Tensor& e);
   void launch_iter_dist(const at::Tensor& r, at::Tensor& rn);

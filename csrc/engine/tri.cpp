@@ -65,9 +65,49 @@ at::Tensor tri_degrees(const at::Tensor& uniq_in, int64_t nvert) {
     const int nb = k::tri_deg_buckets(nvert);
     if (nb > 0 && m > 0) {
       // partitioned count (tri.hip k_deg_*): no scattered atomic per edge
-      const hipStream_t s = cur();
-      k::tri_deg_lo(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), s);
+      k::tri_deg_lo(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), cur());
       stage("deg_lo");
+      count_low_words(uniq, deg);
+    } else {
+      k::tri_degree(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), cur());
+    }
+  } else {
+    const uint64_t* e = P0<uint64_t>(uniq);
+    int32_t* d = P0<int32_t>(deg);
+    for (int64_t i = 0; i < m; ++i) {
+      d[e[i] >> 32]++;
+      d[(uint32_t)e[i]]++;
+    }
+  }
+  return deg;
+}
+
+void count_low_words(const at::Tensor& packed_in, at::Tensor& deg) {
+  at::Tensor packed = packed_in.contiguous();
+  const at::Device dev = packed.device();
+  const int64_t m = packed.numel(), nvert = deg.numel();
+  if (m == 0) return;
+  static const bool dbg = std::getenv("MRH_TRI_DEBUG") != nullptr;
+  auto stage = [&](const char* what) {
+    if (!dbg) return;
+    if (packed.is_cuda()) (void)hipDeviceSynchronize();
+    std::fprintf(stderr, "mrhip count_low_words: %s done\n", what);
+  };
+  if (!packed.is_cuda()) {
+    const uint64_t* e = P0<uint64_t>(packed);
+    int32_t* d = P0<int32_t>(deg);
+    for (int64_t i = 0; i < m; ++i) d[(uint32_t)e[i]]++;
+    return;
+  }
+  const hipStream_t s = cur();
+  const int nb = k::tri_deg_buckets(nvert);
+  if (nb <= 0) {
+    k::count_low_atomic(P0<uint64_t>(packed), m, P0<uint32_t>(deg), s);
+    return;
+  }
+  {
+    const at::Tensor& uniq = packed;
+    {
       at::Tensor bcount = at::zeros({nb}, opt(dev, at::kInt));
       k::tri_deg_count(P0<uint64_t>(uniq), m, nb, P0<unsigned int>(bcount), s);
       stage("deg_count");
@@ -101,18 +141,8 @@ at::Tensor tri_degrees(const at::Tensor& uniq_in, int64_t nvert) {
         k::tri_deg_hist(P0<uint16_t>(ids), P0<unsigned long long>(bstart), P0<uint64_t>(ti), P0<uint32_t>(tl),
                         P0<uint8_t>(tw), ni, nvert, P0<uint32_t>(deg), s);
       }
-    } else {
-      k::tri_degree(P0<uint64_t>(uniq), m, P0<uint32_t>(deg), cur());
-    }
-  } else {
-    const uint64_t* e = P0<uint64_t>(uniq);
-    int32_t* d = P0<int32_t>(deg);
-    for (int64_t i = 0; i < m; ++i) {
-      d[e[i] >> 32]++;
-      d[(uint32_t)e[i]]++;
     }
   }
-  return deg;
 }
 
 std::pair<at::Tensor, at::Tensor> tri_rank_perm(const at::Tensor& deg) {

@@ -17,6 +17,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tri_prepare(const at:
 // the (degree, id) order; the edges oriented to the higher rank, packed
 // rank_lo << 32 | rank_hi (unsorted); col / rowptr of sorted oriented keys
 at::Tensor tri_degrees(const at::Tensor& uniq, int64_t nvert);
+// deg[low 32 bits of packed[i]] += 1 over every element (deg: int32 bins, ids
+// < deg.numel()): a partitioned LDS count (bucket scatter of u16 ids + 32768-bin
+// block histograms), no scattered global atomic per element
+void count_low_words(const at::Tensor& packed, at::Tensor& deg);
 std::pair<at::Tensor, at::Tensor> tri_rank_perm(const at::Tensor& deg);
 at::Tensor tri_orient_keys(const at::Tensor& uniq, const at::Tensor& rank);
 at::Tensor tri_col_of(const at::Tensor& okeys);

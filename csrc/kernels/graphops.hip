@@ -49,12 +49,15 @@ struct ContribGetC {
 // the source bits makes the out-degrees segment lengths (random-address
 // global atomics run at the memory side, ~17x below their coalesced rate:
 // a degree histogram by atomics cost 98 ms on RMAT-26, this sort ~20)
-__global__ __launch_bounds__(NT) void k_pr_pack_src(const int64_t* __restrict__ e, int64_t n, int P,
+// swap: (destination << 32 | local source) instead — the out-degrees then
+// come from a partitioned count of the low words (count_low_words), no sort
+__global__ __launch_bounds__(NT) void k_pr_pack_src(const int64_t* __restrict__ e, int64_t n, int P, int swap,
                                                     uint64_t* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * NT;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const int64_t u = __builtin_nontemporal_load(e + 2 * i), v = __builtin_nontemporal_load(e + 2 * i + 1);
-    out[i] = ((uint64_t)(P == 1 ? u : u / P) << 32) | (uint32_t)v;
+    const uint64_t lu = (uint64_t)(P == 1 ? u : u / P);
+    out[i] = swap ? (((uint64_t)v << 32) | (uint32_t)lu) : ((lu << 32) | (uint32_t)v);
   }
 }
 
@@ -130,12 +133,13 @@ __device__ __forceinline__ uint32_t pr_range_of(uint32_t src, const int32_t* __r
 // v / P, owner-major), lo = new id of u (u is monotone here: the nid reads
 // are a sequential walk)
 __global__ __launch_bounds__(NT) void k_pr_pack(const uint64_t* __restrict__ su, int64_t n, int P, int64_t nlmax,
-                                                int local, const int32_t* __restrict__ nid,
+                                                int local, int swapped, const int32_t* __restrict__ nid,
                                                 const int32_t* __restrict__ rb, int nr, int dbits,
                                                 uint64_t* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * NT;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
-    const uint64_t x = __builtin_nontemporal_load(su + i);
+    uint64_t x = __builtin_nontemporal_load(su + i);
+    if (swapped) x = (x << 32) | (x >> 32);  // (v << 32 | u) input: unsorted, nid[u] is a random read
     const int64_t v = (int64_t)(uint32_t)x;
     // one GPU: the destination as its NEW id (the relabelled id space of the
     // rank vector), so the combine writes each tile of new ids contiguously;
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(NT) void k_pr_mix_pack(const int64_t* __restrict__ 
       u = dev::vmix(u, N, b);
       v = dev::vmix(v, N, b);
     }
-    out[i] = (u << 32) | v;
+    out[i] = (v << 32) | u;  // the source in the low word: out-degrees by count_low_words
     dest[i] = (int32_t)((uint32_t)u - pr_udiv((uint32_t)u, (uint32_t)P, invP) * (uint32_t)P);
   }
 }
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(NT) void k_pr_localize(uint64_t* __restrict__ p, in
   const double invP = 1.0 / (double)P;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const uint64_t x = p[i];
-    p[i] = ((uint64_t)pr_udiv((uint32_t)(x >> 32), (uint32_t)P, invP) << 32) | (x & 0xffffffffull);
+    p[i] = (x & 0xffffffff00000000ull) | (uint64_t)pr_udiv((uint32_t)x, (uint32_t)P, invP);
   }
 }
 
@@ -201,8 +205,8 @@ __global__ __launch_bounds__(NT) void k_pr_pack_dst(const uint64_t* __restrict__
   const double invP = 1.0 / (double)P;
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += stride) {
     const uint64_t x = __builtin_nontemporal_load(su + i);
-    const uint64_t sv = x & 0xffffffffull;
-    const uint64_t pos = (uint64_t)(base + nid[x >> 32]);
+    const uint64_t sv = x >> 32;
+    const uint64_t pos = (uint64_t)(base + nid[(uint32_t)x]);
     out[i] = (sv << 32) | pos;
     dest[i] = (int32_t)((uint32_t)sv - pr_udiv((uint32_t)sv, (uint32_t)P, invP) * (uint32_t)P);
   }
@@ -702,9 +706,9 @@ static unsigned pr_grid_stride(int64_t n) {
   return (unsigned)(b < 1 ? 1 : (b > 65536 ? 65536 : b));
 }
 
-void pr_pack_src(const int64_t* e, int64_t n, int P, uint64_t* out, hipStream_t s) {
+void pr_pack_src(const int64_t* e, int64_t n, int P, bool swap, uint64_t* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_pr_pack_src, dim3(pr_grid_stride(n)), dim3(NT), 0, s, e, n, P, out);
+  hipLaunchKernelGGL(k_pr_pack_src, dim3(pr_grid_stride(n)), dim3(NT), 0, s, e, n, P, swap ? 1 : 0, out);
   MRH_CHECK_LAUNCH();
 }
 void pr_heads(const uint64_t* sorted, int64_t n, uint32_t* flags, hipStream_t s) {
@@ -734,11 +738,11 @@ void sample_i64(const int64_t* in, int64_t n, int64_t stride, int64_t ns, int64_
   hipLaunchKernelGGL(k_sample_i64, dim3(pr_grid(ns)), dim3(NT), 0, s, in, n, stride, ns, out);
   MRH_CHECK_LAUNCH();
 }
-void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, const int32_t* rb,
-             int nr, int dbits, uint64_t* out, hipStream_t s) {
+void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, bool swapped, const int32_t* nid,
+             const int32_t* rb, int nr, int dbits, uint64_t* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_pr_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, nlmax, local ? 1 : 0, nid, rb, nr,
-                     dbits, out);
+  hipLaunchKernelGGL(k_pr_pack, dim3(pr_grid_stride(n)), dim3(NT), 0, s, su, n, P, nlmax, local ? 1 : 0,
+                     swapped ? 1 : 0, nid, rb, nr, dbits, out);
   MRH_CHECK_LAUNCH();
 }
 void pr_mix_pack(const int64_t* e, int64_t n, int P, int64_t N, bool mix, uint64_t* out, int32_t* dest, hipStream_t s) {

@@ -190,7 +190,7 @@ int pr_update_blocks(int64_t n);
 // PageRank plan build (graphops.hip): source-sorted packed edges -> run
 // degrees, degree relabel, packed (destination group << 32 | new source)
 // edge keys and their unpack
-void pr_pack_src(const int64_t* e, int64_t n, int P, uint64_t* out, hipStream_t s);
+void pr_pack_src(const int64_t* e, int64_t n, int P, bool swap, uint64_t* out, hipStream_t s);
 void pr_heads(const uint64_t* sorted, int64_t n, uint32_t* flags, hipStream_t s);
 void pr_run_degree(const uint64_t* sorted, const int64_t* seg, int64_t nrun, uint32_t* deg, hipStream_t s);
 void pr_degkey(const uint32_t* deg, int64_t n, uint64_t* key, uint32_t* iota, hipStream_t s);
@@ -200,12 +200,12 @@ void pr_relabel(const uint32_t* order, const uint32_t* deg, int64_t n, int32_t* 
 void sample_i64(const int64_t* in, int64_t n, int64_t stride, int64_t ns, int64_t* out, hipStream_t s);
 // rb (nullable, nr + 1 entries): hot source ranges [rb[r], rb[r+1]), ids >=
 // rb[nr] form range nr; the range goes above the dbits destination bits
-void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, const int32_t* nid, const int32_t* rb,
-             int nr, int dbits, uint64_t* out, hipStream_t s);
+void pr_pack(const uint64_t* su, int64_t n, int P, int64_t nlmax, bool local, bool swapped, const int32_t* nid,
+             const int32_t* rb, int nr, int dbits, uint64_t* out, hipStream_t s);
 // multi-GPU plan (owner of v = sigma(v) % P, vmix.h; mix false: sigma = id):
-// edges -> (sigma(u) << 32 | sigma(v)) + source owner; (su << 32 | sv) ->
-// (su / P << 32 | sv) in place; source-sorted (lu << 32 | sv) -> (sv << 32 |
-// base + nid[lu]) + destination owner; at the destination owner (sv << 32 |
+// edges -> (sigma(v) << 32 | sigma(u)) + source owner; (sv << 32 | su) ->
+// (sv << 32 | su / P) in place; (sv << 32 | lu) -> (sv << 32 | base +
+// nid[lu]) + destination owner; at the destination owner (sv << 32 |
 // pos) -> ((range << dbits | nid[sv / P]) << 32 | pos), the range of the
 // interleaved source id (pos % S) * P + pos / S; owned global ids
 // sigma^-1(order * P + me)
@@ -284,6 +284,9 @@ void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);
 // scatter of the high endpoints as u16 into their buckets; per-(bucket,
 // piece) LDS histograms added to deg (plain stores where whole != 0)
 int tri_deg_buckets(int64_t nvert);
+// deg[low word of e[i]] += 1 with one global atomic per element (the fallback
+// of the partitioned count for more than 2^27 bins)
+void count_low_atomic(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);
 int tri_deg_bucket_bits();
 void tri_deg_lo(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s);
 void tri_deg_count(const uint64_t* e, int64_t m, int nb, unsigned int* bcount, hipStream_t s);

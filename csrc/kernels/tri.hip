@@ -65,7 +65,8 @@ __global__ __launch_bounds__(NT) void k_tri_degree(const uint64_t* __restrict__ 
 //                   when the block holds the whole bucket.
 constexpr int DEG_RB = 15;
 constexpr int DEG_BINS = 1 << DEG_RB;
-constexpr int DEG_MAXB = 1024;   // buckets (nvert <= 2^25 on this path)
+constexpr int DEG_MAXB = 4096;   // buckets (nvert <= 2^27 on this path)
+constexpr int DEG_SMALLB = 1024; // the kernels' LDS tables for up to 2^25 vertices (higher occupancy)
 constexpr int DEG_NT = 1024;
 
 __global__ __launch_bounds__(NT) void k_deg_lo(const uint64_t* __restrict__ e, int64_t m, uint32_t* __restrict__ deg) {
@@ -86,9 +87,10 @@ __global__ __launch_bounds__(NT) void k_deg_lo(const uint64_t* __restrict__ e, i
   }
 }
 
+template <int MAXB>
 __global__ __launch_bounds__(NT) void k_deg_count(const uint64_t* __restrict__ e, int64_t m, int nb,
                                                  unsigned int* __restrict__ bcount) {
-  __shared__ uint32_t h[DEG_MAXB];
+  __shared__ uint32_t h[MAXB];
   for (int i = threadIdx.x; i < nb; i += NT) h[i] = 0;
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (int64_t)gridDim.x * NT)
@@ -101,11 +103,12 @@ __global__ __launch_bounds__(NT) void k_deg_count(const uint64_t* __restrict__ e
 // the same grid and element order as k_deg_count: every block counts its
 // elements per bucket again, reserves that many slots of each bucket, then
 // places its elements
+template <int MAXB>
 __global__ __launch_bounds__(NT) void k_deg_scatter(const uint64_t* __restrict__ e, int64_t m, int nb,
                                                    unsigned long long* __restrict__ cursor,
                                                    uint16_t* __restrict__ out) {
-  __shared__ uint32_t h[DEG_MAXB];
-  __shared__ unsigned long long base[DEG_MAXB];
+  __shared__ uint32_t h[MAXB];
+  __shared__ unsigned long long base[MAXB];
   for (int i = threadIdx.x; i < nb; i += NT) h[i] = 0;
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (int64_t)gridDim.x * NT)
@@ -958,6 +961,16 @@ void tri_degree(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s) {
   MRH_CHECK_LAUNCH();
 }
 
+__global__ __launch_bounds__(NT) void k_count_low(const uint64_t* __restrict__ e, int64_t m, uint32_t* __restrict__ deg) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (int64_t)gridDim.x * NT)
+    atomicAdd(deg + (uint32_t)e[i], 1u);
+}
+void count_low_atomic(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_count_low, dim3(grid_for(m)), dim3(NT), 0, s, e, m, deg);
+  MRH_CHECK_LAUNCH();
+}
+
 int tri_deg_buckets(int64_t nvert) {
   const int64_t nb = (nvert + DEG_BINS - 1) >> DEG_RB;
   return nb <= DEG_MAXB ? (int)nb : -1;
@@ -974,14 +987,20 @@ void tri_deg_lo(const uint64_t* e, int64_t m, uint32_t* deg, hipStream_t s) {
 void tri_deg_count(const uint64_t* e, int64_t m, int nb, unsigned int* bcount, hipStream_t s) {
   if (m <= 0) return;
   check_arg(nb >= 1 && nb <= DEG_MAXB, "tri_deg_count: bucket count out of range");
-  hipLaunchKernelGGL(k_deg_count, dim3(tri_deg_grid(m)), dim3(NT), 0, s, e, m, nb, bcount);
+  if (nb <= DEG_SMALLB)
+    hipLaunchKernelGGL(k_deg_count<DEG_SMALLB>, dim3(tri_deg_grid(m)), dim3(NT), 0, s, e, m, nb, bcount);
+  else
+    hipLaunchKernelGGL(k_deg_count<DEG_MAXB>, dim3(tri_deg_grid(m)), dim3(NT), 0, s, e, m, nb, bcount);
   MRH_CHECK_LAUNCH();
 }
 
 void tri_deg_scatter(const uint64_t* e, int64_t m, int nb, unsigned long long* cursor, uint16_t* out, hipStream_t s) {
   if (m <= 0) return;
   check_arg(nb >= 1 && nb <= DEG_MAXB, "tri_deg_scatter: bucket count out of range");
-  hipLaunchKernelGGL(k_deg_scatter, dim3(tri_deg_grid(m)), dim3(NT), 0, s, e, m, nb, cursor, out);
+  if (nb <= DEG_SMALLB)
+    hipLaunchKernelGGL(k_deg_scatter<DEG_SMALLB>, dim3(tri_deg_grid(m)), dim3(NT), 0, s, e, m, nb, cursor, out);
+  else
+    hipLaunchKernelGGL(k_deg_scatter<DEG_MAXB>, dim3(tri_deg_grid(m)), dim3(NT), 0, s, e, m, nb, cursor, out);
   MRH_CHECK_LAUNCH();
 }
 
