@@ -502,6 +502,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     d["allocs"] = s.allocs;
     d["frees"] = s.frees;
     d["failures"] = s.failures;
+    d["cached"] = s.cached;
+    d["cross_stream_reuse"] = s.cross_stream_reuse;
+    d["faulted"] = s.faulted;
     return d;
   });
   m.def("hbm_pool_reset_peak", &hbm::reset_peak);

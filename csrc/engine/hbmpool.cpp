@@ -6,13 +6,17 @@
 
 #include <algorithm>
 #include <atomic>
+#include <set>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
+
+#include "guard.h"
 
 namespace mrh::hbm {
 
@@ -46,10 +50,42 @@ struct Pending {
 
 struct Dev {
   hipMemPool_t pool = nullptr;
-  int64_t in_use = 0, peak = 0, cap = 0, cached = 0, allocs = 0, frees = 0, failures = 0;
+  int64_t in_use = 0, peak = 0, cap = 0, cached = 0, allocs = 0, frees = 0, failures = 0, cross = 0;
+  int64_t base_cap = 0;                   // set_cap's cap; cap = min(base_cap, active OpCaps)
+  std::multiset<int64_t> op_caps;         // caps of the ops running now (any thread)
   std::map<std::pair<hipStream_t, int64_t>, std::vector<void*>> free;  // (stream, class) -> cached blocks
+  std::vector<hipStream_t> streams;       // every stream with a cache entry
   std::vector<Pending> pending;
+  // sticky: an event or stream wait of the pool failed (a device fault), so
+  // no cached block can be trusted any more — every later allocation fails
+  std::string fault;
 };
+
+void recompute_cap(Dev& d) {  // g_mu held
+  int64_t c = d.base_cap;
+  if (!d.op_caps.empty()) c = c > 0 ? std::min(c, *d.op_caps.begin()) : *d.op_caps.begin();
+  d.cap = c;
+}
+
+// the pool cannot vouch for its blocks any more: record why (first fault
+// wins), and the caller keeps the block out of every cache (leaked)
+void set_fault(Dev& d, const std::string& why) {  // g_mu held
+  if (d.fault.empty()) d.fault = why;
+  ++d.failures;
+}
+
+void cache_put(Dev& d, hipStream_t s, int64_t bytes, void* p) {  // g_mu held
+  d.free[{s, bytes}].push_back(p);
+  if (std::find(d.streams.begin(), d.streams.end(), s) == d.streams.end()) d.streams.push_back(s);
+}
+
+int process_rank() {
+  static const int r = [] {
+    const char* e = std::getenv("RANK");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  return r;
+}
 
 std::mutex g_mu;
 Dev g_dev[kMaxDev];
@@ -78,25 +114,32 @@ hipMemPool_t pool_of(int dev) {  // g_mu held
   return d.pool;
 }
 
-// pending blocks whose other-stream work is done go to their stream's cache
+// pending blocks whose other-stream work is done go to their stream's cache;
+// an event that reports an error (not "not ready") faults the pool and its
+// block is never handed out again
 void reap(Dev& d) {  // g_mu held
   for (size_t i = 0; i < d.pending.size();) {
     Pending& q = d.pending[i];
-    bool done = true;
+    bool done = true, bad = false;
     for (hipEvent_t e : q.evs) {
       const hipError_t r = hipEventQuery(e);
       if (r == hipErrorNotReady) {
         done = false;
         break;
       }
-      if (r != hipSuccess) (void)hipGetLastError();
+      if (r != hipSuccess) {
+        (void)hipGetLastError();
+        set_fault(d, std::string("event of a block used on another stream: ") + hipGetErrorString(r));
+        bad = true;
+      }
     }
     if (!done) {
       ++i;
       continue;
     }
     for (hipEvent_t e : q.evs) (void)hipEventDestroy(e);
-    d.free[{q.b.stream, q.b.bytes}].push_back(q.p);
+    if (bad) d.cached -= q.b.bytes;  // leaked on purpose: other streams may still use it
+    else cache_put(d, q.b.stream, q.b.bytes, q.p);
     q = std::move(d.pending.back());
     d.pending.pop_back();
   }
@@ -106,32 +149,86 @@ void reap(Dev& d) {  // g_mu held
 // to any stream, or trim it to the driver)
 void release_cached(Dev& d) {  // g_mu held
   for (Pending& q : d.pending) {
+    bool ok = true;
     for (hipEvent_t e : q.evs) {
-      (void)hipStreamWaitEvent(q.b.stream, e, 0);
+      // the block goes back to the HIP pool on its own stream behind the other
+      // streams' events; a failed wait would free memory still in use
+      const hipError_t r = hipStreamWaitEvent(q.b.stream, e, 0);
+      if (r != hipSuccess) {
+        (void)hipGetLastError();
+        set_fault(d, std::string("stream wait before releasing a block: ") + hipGetErrorString(r));
+        ok = false;
+      }
       (void)hipEventDestroy(e);
     }
-    d.free[{q.b.stream, q.b.bytes}].push_back(q.p);
+    if (ok) cache_put(d, q.b.stream, q.b.bytes, q.p);
   }
   d.pending.clear();
   for (auto& [k, v] : d.free)
     for (void* p : v)
       if (hipFreeAsync(p, k.first) != hipSuccess) {
         (void)hipGetLastError();
-        (void)hipDeviceSynchronize();
+        const hipError_t r = hipDeviceSynchronize();
+        if (r != hipSuccess) {  // a sticky device fault: nothing can be freed safely
+          (void)hipGetLastError();
+          set_fault(d, std::string("device fault while releasing cached blocks: ") + hipGetErrorString(r));
+          continue;
+        }
         (void)hipFreeAsync(p, nullptr);
       }
   d.free.clear();
+  d.streams.clear();
   d.cached = 0;
+}
+
+// a cached block of this class on another stream, made safe for `stream` by
+// an event of the stream it was freed on (bounds the reserved memory: blocks
+// freed on the copy streams feed the compute stream and vice versa)
+void* take_other_stream(Dev& d, hipStream_t stream, int64_t bytes) {  // g_mu held
+  for (hipStream_t s : d.streams) {
+    if (s == stream) continue;
+    auto it = d.free.find({s, bytes});
+    if (it == d.free.end() || it->second.empty()) continue;
+    hipEvent_t ev = nullptr;
+    hipError_t r = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (r == hipSuccess) r = hipEventRecord(ev, s);
+    if (r == hipSuccess) r = hipStreamWaitEvent(stream, ev, 0);
+    if (ev) (void)hipEventDestroy(ev);  // released once the wait no longer needs it
+    if (r != hipSuccess) {
+      (void)hipGetLastError();
+      set_fault(d, std::string("cross-stream reuse event: ") + hipGetErrorString(r));
+      return nullptr;
+    }
+    void* p = it->second.back();
+    it->second.pop_back();
+    ++d.cross;
+    return p;
+  }
+  return nullptr;
 }
 
 void* pool_alloc(size_t size, int dev, hipStream_t stream) {
   if (size == 0) return nullptr;
   TORCH_CHECK(dev >= 0 && dev < kMaxDev, "mrhip page pool: device index out of range");
   const int64_t bytes = class_bytes(size);
+  static const bool fault_armed = [] {
+    const char* e = std::getenv("MRH_FAULT");
+    return e && std::strncmp(e, "hip:pool:", 9) == 0;
+  }();
   hipMemPool_t pool;
   {
     std::lock_guard<std::mutex> l(g_mu);
     Dev& d = g_dev[dev];
+    if (fault_armed) {  // MRH_FAULT=hip:pool:<rank>[:nth]: the nth allocation finds the pool faulted
+      try {
+        guard::hip_check(hipSuccess, "pool", process_rank());
+      } catch (const std::exception& ex) {
+        set_fault(d, ex.what());
+      }
+    }
+    if (!d.fault.empty())
+      TORCH_CHECK(false, "mrhip page pool: device ", dev, " is unusable after an earlier fault (", d.fault,
+                  "); no allocation is served");
     if (d.cap > 0 && d.in_use + bytes > d.cap) {
       ++d.failures;
       TORCH_CHECK_WITH(OutOfMemoryError, false, "mrhip page pool: Cannot allocate page: ", mib(bytes),
@@ -140,9 +237,16 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
     }
     if (!d.pending.empty()) reap(d);
     auto it = d.free.find({stream, bytes});
+    void* p = nullptr;
     if (it != d.free.end() && !it->second.empty()) {  // stream-ordered reuse: no HIP call
-      void* p = it->second.back();
+      p = it->second.back();
       it->second.pop_back();
+    } else {
+      p = take_other_stream(d, stream, bytes);
+      if (!d.fault.empty())
+        TORCH_CHECK(false, "mrhip page pool: device ", dev, " faulted: ", d.fault);
+    }
+    if (p) {
       d.cached -= bytes;
       d.in_use += bytes;
       d.peak = std::max(d.peak, d.in_use);
@@ -150,6 +254,9 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
       g_blocks[p] = Block{bytes, dev, stream, {}};
       return p;
     }
+    // much idle memory cached in other classes: hand it back to the HIP pool
+    // before growing it (the pool reuses freed memory across streams)
+    if (d.cached > (int64_t(1) << 30) && d.cached > d.in_use / 4) release_cached(d);
     pool = pool_of(dev);
     d.in_use += bytes;  // reserved before the call so concurrent allocations see it
     d.peak = std::max(d.peak, d.in_use);
@@ -165,7 +272,15 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
       std::lock_guard<std::mutex> l(g_mu);
       release_cached(g_dev[dev]);
     }
-    (void)hipDeviceSynchronize();
+    const hipError_t se = hipDeviceSynchronize();
+    if (se != hipSuccess) {  // not an out-of-memory: a device fault, which a retry must not hide
+      (void)hipGetLastError();
+      std::lock_guard<std::mutex> l(g_mu);
+      g_dev[dev].in_use -= bytes;
+      set_fault(g_dev[dev], std::string("device fault seen by an allocation retry: ") + hipGetErrorString(se));
+      TORCH_CHECK(false, "mrhip page pool: device error on device ", dev, " while retrying an allocation of ",
+                  mib(bytes), ": ", hipGetErrorString(se));
+    }
     (void)hipMemPoolTrimTo(pool, 0);
     e = hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream);
     if (e != hipSuccess) (void)hipGetLastError();
@@ -194,7 +309,7 @@ void pool_free(void* ptr, size_t /*size*/, int /*dev*/, hipStream_t /*stream*/) 
   ++d.frees;
   if (b.used_on.empty()) {
     // later work on the allocating stream runs after every earlier use
-    d.free[{b.stream, b.bytes}].push_back(ptr);
+    cache_put(d, b.stream, b.bytes, ptr);
     return;
   }
   // used on other streams too: reusable after an event of each of them
@@ -204,7 +319,13 @@ void pool_free(void* ptr, size_t /*size*/, int /*dev*/, hipStream_t /*stream*/) 
     hipEvent_t ev;
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, s) != hipSuccess) {
       (void)hipGetLastError();
-      (void)hipStreamSynchronize(s);
+      const hipError_t r = hipStreamSynchronize(s);
+      if (r != hipSuccess) {  // cannot tell when the other stream is done with it: never reuse
+        (void)hipGetLastError();
+        set_fault(d, std::string("freeing a block used on another stream: ") + hipGetErrorString(r));
+        d.cached -= b.bytes;
+        return;
+      }
       continue;
     }
     q.evs.push_back(ev);
@@ -261,6 +382,9 @@ PoolStats stats(int device) {
   s.allocs = d.allocs;
   s.frees = d.frees;
   s.failures = d.failures;
+  s.cached = d.cached;
+  s.cross_stream_reuse = d.cross;
+  s.faulted = !d.fault.empty();
   if (d.pool) {
     uint64_t r = 0;
     if (hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemCurrent, &r) == hipSuccess) s.reserved = (int64_t)r;
@@ -277,8 +401,10 @@ void reset_peak(int device) {
 int64_t set_cap(int device, int64_t cap) {
   if (device < 0 || device >= kMaxDev) return 0;
   std::lock_guard<std::mutex> l(g_mu);
-  const int64_t prev = g_dev[device].cap;
-  g_dev[device].cap = std::max<int64_t>(0, cap);
+  Dev& d = g_dev[device];
+  const int64_t prev = d.base_cap;
+  d.base_cap = std::max<int64_t>(0, cap);
+  recompute_cap(d);
   return prev;
 }
 
@@ -297,21 +423,27 @@ void trim(int device, int64_t keep_bytes) {
   if (hipMemPoolTrimTo(p, (size_t)std::max<int64_t>(0, keep_bytes)) != hipSuccess) (void)hipGetLastError();
 }
 
+// every running op's cap is kept (a multiset: ops on one device may run on
+// several threads, and their scopes need not nest); the cap in force is the
+// tightest of them and set_cap's, so no exit order can leave a stale cap
 OpCap::OpCap(int device, int64_t extra) {
   if (!g_installed || device < 0 || device >= kMaxDev || extra <= 0) return;
   std::lock_guard<std::mutex> l(g_mu);
   Dev& d = g_dev[device];
   dev_ = device;
-  prev_ = d.cap;
-  const int64_t want = d.in_use + extra;
-  d.cap = prev_ > 0 ? std::min(prev_, want) : want;  // never loosen an outer cap
+  prev_ = d.in_use + extra;
+  d.op_caps.insert(prev_);
+  recompute_cap(d);
   on_ = true;
 }
 
 OpCap::~OpCap() {
   if (!on_) return;
   std::lock_guard<std::mutex> l(g_mu);
-  g_dev[dev_].cap = prev_;
+  Dev& d = g_dev[dev_];
+  auto it = d.op_caps.find(prev_);
+  if (it != d.op_caps.end()) d.op_caps.erase(it);
+  recompute_cap(d);
 }
 
 }  // namespace mrh::hbm

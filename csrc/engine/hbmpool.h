@@ -19,7 +19,14 @@
 //    kernel scratch;
 //  * size classes: 512-byte granules to 4 KiB, then 8 classes per power of
 //    two; a freed block stays cached for later requests of its class on its
-//    stream (no HIP call on that path) until trim();
+//    stream (no HIP call on that path), or serves another stream's request of
+//    that class behind an event, until trim(); more than 1 GiB (and a quarter
+//    of the bytes in use) cached goes back to the HIP pool before it grows;
+//  * faults: an event query or stream wait of the pool that fails marks the
+//    device's pool faulted — the block in question is never reused and every
+//    later allocation throws (MRH_FAULT=hip:pool:<rank> injects it), so the
+//    op fails and poisons its communicator instead of handing out memory a
+//    faulted stream may still write;
 //  * freepage: trim() returns the pool's cached free memory to the driver;
 //  * stats: bytes in use, hi-water mark, reserved bytes, counts.
 #pragma once
@@ -35,6 +42,9 @@ struct PoolStats {
   int64_t reserved = 0;  // bytes the HIP pool holds from the driver
   int64_t cap = 0;       // hard cap on in_use (0: none)
   int64_t allocs = 0, frees = 0, failures = 0;
+  int64_t cached = 0;              // bytes of freed blocks held in the per-(stream, class) caches
+  int64_t cross_stream_reuse = 0;  // allocations served from another stream's cache behind an event
+  bool faulted = false;            // an event / stream wait of the pool failed: no allocation is served
 };
 
 // make the pool the process's device allocator; false (and no change) if the
@@ -51,7 +61,8 @@ int64_t set_cap(int device, int64_t cap);
 // release cached free memory of the pool down to keep_bytes
 void trim(int device, int64_t keep_bytes);
 
-// RAII: a MapReduce op's cap (in use at entry + extra bytes), restored on exit
+// RAII: a MapReduce op's cap (in use at entry + extra bytes) while it runs;
+// concurrent ops' caps combine (the tightest is in force)
 class OpCap {
  public:
   OpCap(int device, int64_t extra);
@@ -61,7 +72,7 @@ class OpCap {
 
  private:
   int dev_ = -1;
-  int64_t prev_ = 0;
+  int64_t prev_ = 0;  // this op's cap
   bool on_ = false;
 };
 

@@ -289,3 +289,52 @@ def test_hip_fault_kind_is_accepted():
     """
     r = _py(code, {"MRH_FAULT": "hip:drain_copy:0"})
     assert r.returncode == 0 and r.stdout.strip() == "1", r.stderr
+
+
+POOL_SCRIPT = """
+import os, sys, time, struct, torch
+sys.path.insert(0, os.environ["PYTHONPATH"])
+from gpu_mapreduce_amd.parallel import comm as pcomm
+import gpu_mapreduce_amd as g
+comm = pcomm.init()
+t0 = time.time()
+try:
+    for it in range(40):
+        mr = g.MapReduce(comm)
+        mr.map(2, lambda i, kv: [kv.add(b"w%d" % (j % 97), struct.pack("<i", j)) for j in range(2000)])
+        mr.collate()
+        mr.reduce("count")
+        torch.cuda.synchronize()
+    print("NO-ERROR", flush=True)
+except Exception as e:
+    print(f"RAISED after {time.time() - t0:.1f}s: {e}", flush=True)
+    os._exit(1)
+"""
+
+
+@pytest.mark.gpu
+def test_pool_fault_poisons_every_rank(tmp_path):
+    """MRH_FAULT=hip:pool:1:200: rank 1's page pool reports a failed event /
+    stream wait at its 200th allocation. The pool is then faulted for good
+    (the block is never reused, no later allocation is served), the op raises,
+    the job is poisoned and both ranks end with an error within seconds."""
+    port = _port()
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(ENV0, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT, MRH_NUMA_BIND="0",
+                   MRH_COMM_TIMEOUT="60", MRH_FAULT="hip:pool:1:200")
+        procs.append(subprocess.Popen([sys.executable, "-c", POOL_SCRIPT], cwd=tmp_path, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    try:
+        res = [p.communicate(timeout=150) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.time() - t0
+    assert all(p.returncode != 0 for p in procs), res
+    assert "page pool" in res[1][0] + res[1][1], res[1]
+    assert "NO-ERROR" not in res[0][0], res[0]
+    assert elapsed < 90, f"failure took {elapsed:.0f} s to surface"

@@ -24,7 +24,8 @@ def _child(code, timeout=240):
 def test_pool_stats_shape_cpu():
     from gpu_mapreduce_amd.runtime import hbm_pool
     s = hbm_pool.stats(0)
-    assert set(s) == {"in_use", "peak", "reserved", "cap", "allocs", "frees", "failures"}
+    assert set(s) == {"in_use", "peak", "reserved", "cap", "allocs", "frees", "failures", "cached",
+                      "cross_stream_reuse", "faulted"}
 
 
 BASIC = r'''
@@ -109,3 +110,48 @@ def test_pool_basic_and_stream_order_gpu():
 @pytest.mark.gpu
 def test_pool_cap_and_page_budget_gpu():
     assert _child(CAP).startswith("ok")
+
+
+CROSS = r'''
+import torch
+import gpu_mapreduce_amd as g
+from gpu_mapreduce_amd.runtime import hbm_pool
+assert hbm_pool.installed()
+side = torch.cuda.Stream()
+# blocks freed on the side stream serve the main stream's requests of their
+# class (behind an event) instead of growing the pool
+with torch.cuda.stream(side):
+    xs = [torch.full((1 << 22,), float(i), device="cuda") for i in range(8)]
+    ref = [float(x.sum()) for x in xs]
+with torch.cuda.stream(side):
+    del xs
+torch.cuda.synchronize()
+r0 = hbm_pool.stats(0)
+ys = [torch.ones(1 << 22, device="cuda") for _ in range(8)]
+torch.cuda.synchronize()
+r1 = hbm_pool.stats(0)
+assert r1["cross_stream_reuse"] - r0["cross_stream_reuse"] >= 8, (r0, r1)
+assert r1["reserved"] <= r0["reserved"], (r0, r1)   # no growth
+assert all(float(y.sum()) == float(1 << 22) for y in ys)
+# concurrent op caps never leave a stale cap behind (advisor r3)
+from gpu_mapreduce_amd import C
+import threading
+def op():
+    mr = g.MapReduce(g.Comm(device="cuda"))
+    mr.memsize = -(1 << 20)
+    mr.maxpage = 64
+    k = torch.arange(1 << 18, dtype=torch.int64, device="cuda")
+    for _ in range(5):
+        mr.map(1, lambda i, kv: kv.add_kv(C.make_kv(k, None, k, None, k.numel(), "cuda")))
+        mr.convert()
+ts = [threading.Thread(target=op) for _ in range(4)]
+[t.start() for t in ts]
+[t.join() for t in ts]
+assert hbm_pool.stats(0)["cap"] == 0, hbm_pool.stats(0)
+print("ok", hbm_pool.stats(0))
+'''
+
+
+@pytest.mark.gpu
+def test_pool_cross_stream_reuse_and_concurrent_caps_gpu():
+    assert _child(CROSS).startswith("ok")

@@ -7,3 +7,4 @@ bash tools/pr_setup_stages.sh &&
 timeout -k 10 200 python bench.py --workload pagerank --steps 3 --warmup 1 > $O/pr_local.json 2> $O/pr_local.err &&
 MRH_PR_DEGREES=sort timeout -k 10 200 python bench.py --workload pagerank --steps 3 --warmup 1 > $O/pr_sort.json 2> $O/pr_sort.err &&
 MRH_FORCE_RCCL=1 timeout -k 10 200 python bench.py --workload pagerank --steps 3 --warmup 1 > $O/pr_forced.json 2> $O/pr_forced.err
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_hbm_pool.py tests/test_faults.py tests/test_outofcore.py > $O/t_pool.log 2>&1
