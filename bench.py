@@ -385,7 +385,8 @@ def _extra(comm, prefix, fn, args, **over):
     out = {f"{prefix}_kvps": r["value"], f"{prefix}_ms": r["ms_per_step"], f"{prefix}_setup_ms": r.get("setup_ms"),
            f"{prefix}_config": dict(r["config"], steps=a.steps, warmup=a.warmup, scaling=r.get("scaling", "weak"),
                                     metric=r["metric"])}
-    for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices", "build"):
+    for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices", "build",
+              "triangles_check", "stages", "wedge_pairs", "ooc"):
         if k in r:
             out[f"{prefix}_{k}"] = r[k]
     return out
@@ -583,6 +584,11 @@ def main():
     ap.add_argument("--pagerank-warmup", type=int, default=1)
     ap.add_argument("--trifind-scale", type=int, default=None,
                     help="RMAT scale of the tri_find extra (BASELINE config 5: 24 on GPU, 12 on CPU; 0 = skip)")
+    ap.add_argument("--trifind-mr-scale", type=int, default=None,
+                    help="RMAT scale of the tri_find_mr extra (the 4-collate MapReduce pipeline: 20 on GPU, 10 on "
+                         "CPU; 0 = skip)")
+    ap.add_argument("--trifind-mr-ooc-scale", type=int, default=None,
+                    help="RMAT scale of its out-of-core run under a 256 MiB HBM budget (18 on GPU, 0 on CPU)")
     ap.add_argument("--wordfreq-bytes", type=float, default=None,
                     help="text bytes per GPU of the wordfreq extra (BASELINE config 3: 64 GB over 8 GPUs = 8 GiB "
                          "per GPU, the default on GPU; 4e6 on CPU; 0 = skip)")
@@ -611,6 +617,10 @@ def main():
         args.pagerank_scale = 26 if comm.is_cuda else 14
     if args.trifind_scale is None:
         args.trifind_scale = 24 if comm.is_cuda else 12
+    if args.trifind_mr_scale is None:
+        args.trifind_mr_scale = 20 if comm.is_cuda else 10
+    if args.trifind_mr_ooc_scale is None:
+        args.trifind_mr_ooc_scale = 18 if comm.is_cuda else 0
     if args.wordfreq_bytes is None:
         args.wordfreq_bytes = float(8 << 30) if comm.is_cuda else 4e6
     if args.workload == "invertedindex":
@@ -663,6 +673,11 @@ def main():
                               file_bytes=min(args.file_bytes, int(args.wordfreq_bytes)),
                               steps=args.extra_steps, warmup=6))  # steady state after ~6 jobs:
             # warmup 1 / 2 / 6 -> 27.1 / 24.7 / 22.8 ms (profiles/r3_wordfreq_input.txt)
+        if args.trifind_mr_scale > 0:
+            from gpu_mapreduce_amd.models.triangles import bench_trifind_mr
+            r = _extra(comm, "trifind_mr", bench_trifind_mr, args, scale=args.trifind_mr_scale, steps=1, warmup=1,
+                       mr_ooc_scale=args.trifind_mr_ooc_scale)
+            res.update(r)
         if args.wordfreq_bytes > 0 and args.file_io_steps > 0:
             try:
                 res["wordfreq_with_file_io"] = bench_wordfreq_files(comm, args)

@@ -22,7 +22,9 @@
 #include "mapreduce.h"
 #include "tri.h"
 #include "wordcount.h"
+#include "oink/callbacks.h"
 #include "oink/oink.h"
+#include "oink/trifind_mr.h"
 
 namespace py = pybind11;
 using namespace mrh;
@@ -618,6 +620,55 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_gather_reduce", &mrh::plan_gather_reduce);
   m.def("plan_combine", &mrh::plan_combine);
   m.def("wedges", &mrh::wedges);
+  // the reference's 4-collate tri_find over this rank's [n,2] int64 edges,
+  // each stage timed (oink/trifind_mr.h); budgets / fpath / memsize as the
+  // MapReduce settings of the pipeline's object (0 / "": defaults)
+  m.def(
+      "tri_find_mr",
+      [](std::shared_ptr<Comm> c, at::Tensor edges, int64_t hbm_budget, int64_t host_budget, std::string fpath,
+         int memsize, bool upper) {
+        oink::TriMRRun r;
+        int64_t spool_files = 0, spool_host = 0, spool_disk = 0;
+        {
+          py::gil_scoped_release nogil;
+          r = poisoning(c, "tri_find_mr", [&] {
+            MapReduce mre(c), mrt(c);
+            at::Tensor e = edges.to(c->device()).to(at::kLong).reshape({-1, 2}).contiguous();
+            mre.map(c->size(), [&](int, KeyValue& kv) {
+              if (e.size(0)) oink::add_tensors(kv, e);
+            });
+            for (MapReduce* m : {&mre, &mrt}) {
+              if (hbm_budget > 0) m->set.hbm_budget = hbm_budget;
+              if (host_budget > 0) m->set.host_budget = host_budget;
+              if (!fpath.empty()) m->set.fpath = fpath;
+              if (memsize != 0) m->set.memsize = memsize;
+            }
+            oink::TriMRRun out = oink::tri_find_mr(mre, mrt, upper);
+            spool_files = mrt.spool_stats.files + mre.spool_stats.files;
+            spool_host = mrt.spool_stats.host_bytes + mre.spool_stats.host_bytes;
+            spool_disk = mrt.spool_stats.disk_bytes + mre.spool_stats.disk_bytes;
+            return out;
+          });
+        }
+        py::list st;
+        for (const auto& s : r.stages) {
+          py::dict d;
+          d["op"] = s.op;
+          d["ms"] = s.seconds * 1e3;
+          d["pairs_in"] = s.pairs_in;
+          d["pairs_out"] = s.pairs_out;
+          st.append(d);
+        }
+        py::dict d;
+        d["triangles"] = r.triangles;
+        d["stages"] = st;
+        d["spool_files"] = spool_files;
+        d["spool_host_bytes"] = spool_host;
+        d["spool_disk_bytes"] = spool_disk;
+        return d;
+      },
+      py::arg("comm"), py::arg("edges"), py::arg("hbm_budget") = 0, py::arg("host_budget") = 0,
+      py::arg("fpath") = "", py::arg("memsize") = 0, py::arg("upper") = true);
   // one-shot static-segment gather-reduce (builds the index each call; tests)
   m.def("seg_gather_reduce", [](const at::Tensor& seg, const at::Tensor& src, const at::Tensor& x,
                                 c10::optional<at::Tensor> w, int64_t op) {

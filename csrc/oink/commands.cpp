@@ -21,6 +21,7 @@
 #include "engine/graphplan.h"
 #include "engine/tri.h"
 #include "oink.h"
+#include "trifind_mr.h"
 
 namespace mrh {
 namespace oink {
@@ -505,39 +506,7 @@ class TriFindMR : public Command {
   void run() override {
     MapReduce& mre = obj.input(1, rd(parse_edge), rc(parse_edge));
     MapReduce& mrt = obj.create_mr();
-    mrt.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {  // map_edge_vert
-      if (!src.n) return;
-      at::Tensor e = edges_of(src);
-      add_tensors(kv, at::cat({e.select(1, 0), e.select(1, 1)}), at::cat({e.select(1, 1), e.select(1, 0)}));
-    });
-    mrt.collate();
-    mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_first_degree
-      if (!m.nval) return;
-      auto [edge, deg] = trimr_first_degree(m);
-      add_tensors(kv, edge, deg);
-    });
-    mrt.collate();
-    mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_second_degree
-      if (!m.nkey) return;
-      add_tensors(kv, m.keys.kdata.view(at::kLong).view({-1, 2}), trimr_second_degree(m));
-    });
-    mrt.map_mr_batch(mrt, [](const KV& src, KeyValue& kv) {  // map_low_degree
-      if (!src.n) return;
-      auto [key, val] = trimr_low_degree(src);
-      add_tensors(kv, key, val);
-    });
-    mrt.collate();
-    mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_nsq_angles
-      if (!m.nkey) return;
-      auto r = wedges(m.seg, m.vdata.view(at::kLong), m.keys.kdata.view(at::kLong));
-      if (r.first.numel()) add_tensors(kv, r.first, r.second);
-    });
-    mrt.add(mre);
-    mrt.collate();
-    const uint64_t ntri = mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_emit_triangles
-      at::Tensor tri = trimr_emit(m);
-      if (tri.size(0)) add_tensors(kv, tri);
-    });
+    const uint64_t ntri = tri_find_mr(mre, mrt).triangles;
     obj.output(1, mrt, print_tri);
     message(fmt("Tri_find: %" PRIu64 " triangles", ntri));
     obj.cleanup();

@@ -110,3 +110,84 @@ def bench_trifind(comm, args):
         "hub_vertices": int(C.tri_last_hub_size()),
         "build": "split" if g._g.split else ("halo" if g._g.distributed else "replicated"),
     }
+
+
+def tri_find_mr(comm, edges: torch.Tensor, hbm_budget=0, host_budget=0, fpath="", memsize=0, upper=True):
+    """The reference's MapReduce tri_find (oink/tri_find.cpp:43-82): edge_upper
+    (map -> collate -> reduce cull) then 4 collates with the O(d^2) wedge
+    reduce, on the generic engine ops (csrc/oink/trifind_mr.cpp), every stage
+    device-synchronised and timed. edges: this rank's raw [n,2] int64 edges.
+    Returns {"triangles", "stages": [{op, ms, pairs_in, pairs_out}], spool stats}."""
+    return dict(C.tri_find_mr(comm.native, edges, int(hbm_budget), int(host_budget), str(fpath), int(memsize),
+                              bool(upper)))
+
+
+def bench_trifind_mr(comm, args):
+    """tri_find as the 4-collate MapReduce pipeline on an R-MAT graph: the
+    generic engine at large KV counts (RMAT-20: ~16 M edges -> ~1.3 G wedge
+    pairs through collate 4). Optional out-of-core run (args.mr_ooc_scale)
+    under an HBM budget that forces the spool tiers."""
+    import shutil
+    import tempfile
+    from .pagerank import GRAPH500
+    scale, ef = args.scale, args.edgefactor
+    ntotal = (1 << scale) * ef
+    P, me = comm.size, comm.rank
+
+    def edges_of(sc):
+        nt = (1 << sc) * ef
+        lo, hi = me * nt // P, (me + 1) * nt // P
+        kv = C.map_rmat(hi - lo, sc, *GRAPH500, 0.0, args.seed, lo, comm.device)
+        return kv.kdata.view(torch.int64).view(-1, 2)
+
+    def sync():
+        if comm.is_cuda:
+            torch.cuda.synchronize()
+        comm.barrier()
+
+    e = edges_of(scale)
+    want = TriangleGraph(comm, e, 1 << scale).count()  # the specialised path's count, for the check
+    for _ in range(args.warmup):
+        tri_find_mr(comm, e)
+    sync()
+    runs = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        r = tri_find_mr(comm, e)
+        sync()
+        runs.append(time.perf_counter() - t0)
+    dt = comm.allreduce(sum(runs) / len(runs), "max", dtype=torch.float64)
+    stages = [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"], "pairs_out": s["pairs_out"],
+               "Mkvps_in": round(s["pairs_in"] / max(s["ms"], 1e-9) / 1e3, 1)} for s in r["stages"]]
+    out = {
+        "metric": f"KV-pairs/sec (whole node), tri_find_mr raw edges through the 4-collate pipeline "
+                  f"(RMAT-2^{scale}, ef{ef})",
+        "value": ntotal / dt, "unit": "KV/s", "ms_per_step": dt * 1e3, "vs_baseline": None,
+        "config": {"model": "tri_find_mr", "global_batch": ntotal, "seq_len": 1, "parallelism": f"dp{P}",
+                   "scale": scale, "edgefactor": ef},
+        "triangles": int(r["triangles"]), "triangles_check": int(want),
+        "stages": stages, "scaling": "strong",
+        "wedge_pairs": max((s["pairs_out"] for s in r["stages"] if s["op"] == "reduce nsq_angles"), default=0),
+    }
+    oscale = getattr(args, "mr_ooc_scale", 0) or 0
+    if oscale > 0:
+        root = tempfile.mkdtemp(prefix=f"mrh_trimr_{me}_")
+        try:
+            e2 = edges_of(oscale)
+            want2 = TriangleGraph(comm, e2, 1 << oscale).count()
+            budget = int(getattr(args, "mr_ooc_hbm", 256 << 20))
+            host = int(getattr(args, "mr_ooc_host", 2 << 30))
+            sync()
+            t0 = time.perf_counter()
+            r2 = tri_find_mr(comm, e2, hbm_budget=budget, host_budget=host, fpath=root, memsize=-(16 << 20))
+            sync()
+            dt2 = comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
+            out["ooc"] = {"scale": oscale, "ms": dt2 * 1e3, "triangles": int(r2["triangles"]),
+                          "triangles_check": int(want2), "hbm_budget": budget, "host_budget": host,
+                          "spool_files": r2["spool_files"], "spool_host_bytes": r2["spool_host_bytes"],
+                          "spool_disk_bytes": r2["spool_disk_bytes"],
+                          "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"]}
+                                     for s in r2["stages"]]}
+        finally:
+            shutil.rmtree(root, ignore_errors=True)
+    return out

@@ -256,3 +256,25 @@ def test_gpu_fast_build_with_nvert_matches_cpu():
     assert torch.equal(gpu.okeys.cpu(), cpu.okeys) and torch.equal(gpu.rowptr.cpu(), cpu.rowptr)
     with pytest.raises(RuntimeError, match="outside"):
         TriangleGraph(Comm(device="cuda"), e.cuda(), 100)
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_tri_find_mr_pipeline_in_memory_and_out_of_core(dev, tmp_path):
+    """the reference's 4-collate pipeline (edge_upper first) on raw R-MAT
+    edges: the triangle count equals the brute-force oracle in memory and
+    under an HBM budget of ~1/50 of the wedge pairs (spooled collates and
+    reduces), with every stage timed"""
+    from gpu_mapreduce_amd.models.triangles import tri_find_mr
+    import gpu_mapreduce_amd as gm
+    e = _rmat(9, 8, 5)
+    want = brute_force_count(e.numpy())
+    comm = gm.Comm(device=dev)
+    r = tri_find_mr(comm, e)
+    assert r["triangles"] == want
+    ops = [s["op"] for s in r["stages"]]
+    assert ops[:3] == ["map edge_upper", "collate 0", "reduce cull"] and ops[-1] == "reduce emit_triangles"
+    wedges = next(s["pairs_out"] for s in r["stages"] if s["op"] == "reduce nsq_angles")
+    r2 = tri_find_mr(comm, e, hbm_budget=max(4096, wedges * 24 // 50), host_budget=wedges * 24 // 8,
+                     fpath=str(tmp_path), memsize=-65536)
+    assert r2["triangles"] == want
+    assert r2["spool_host_bytes"] > 0
