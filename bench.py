@@ -166,9 +166,11 @@ def bench_inverted_index_files(comm, args):
     # a RAM-backed directory with room for the part files and the output (on
     # every rank: one rank without room would leave its peers waiting in the
     # job's collectives, so all ranks agree before any of them starts)
+    # the node's ranks share the directory: room for all of them, with a margin
+    nloc = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     need = 2 * int(args.bytes_per_gpu) + (256 << 20)
     base = next((d for d in ("/dev/shm", tempfile.gettempdir())
-                 if os.path.isdir(d) and shutil.disk_usage(d).free >= need), None)
+                 if os.path.isdir(d) and shutil.disk_usage(d).free >= nloc * need + (4 << 30)), None)
     root = None
     files_ok = 0
     try:
@@ -408,10 +410,13 @@ def bench_wordfreq_files(comm, args):
     from gpu_mapreduce_amd.utils.fileio import RingReader
     per_gpu = int(args.wordfreq_bytes)
     chunk = min(int(args.file_bytes), per_gpu)
+    nloc = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))  # ranks of this node share the directory
     base = next((d for d in ("/dev/shm", tempfile.gettempdir())
-                 if os.path.isdir(d) and shutil.disk_usage(d).free >= per_gpu + (1 << 30)), None)
+                 if os.path.isdir(d) and shutil.disk_usage(d).free >= nloc * (per_gpu + (1 << 30)) + (4 << 30)),
+                None)
     if comm.allreduce(0 if base is None else 1, "min") == 0:
-        return {"skipped": f"a rank had no directory with {(per_gpu >> 20) + 1024} MiB free for the part files"}
+        return {"skipped": f"a rank had no directory with room for its node's part files "
+                           f"({nloc} x {(per_gpu >> 20) + 1024} MiB + 4 GiB)"}
     root = tempfile.mkdtemp(prefix=f"mrh_wf_{comm.rank}_", dir=base)
     reader = None
     try:

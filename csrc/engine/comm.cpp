@@ -242,7 +242,8 @@ void Comm::host_wait() const {
 // ---------------------------------------------------------------- scalars
 
 std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
-  if (v.empty() || !distributed()) return v;
+  // one rank (the forced-RCCL mode included): identity, no device round trip
+  if (v.empty() || !distributed() || size_ == 1) return v;
   trace_coll(rank_, "allreduce_i64", (int64_t)v.size(), op);
   at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kLong));
   if (host_scalars()) {
@@ -262,7 +263,7 @@ std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
 }
 
 std::vector<double> Comm::allreduce_f64(std::vector<double> v, Op op) const {
-  if (v.empty() || !distributed()) return v;
+  if (v.empty() || !distributed() || size_ == 1) return v;
   trace_coll(rank_, "allreduce_f64", (int64_t)v.size(), op);
   at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kDouble));
   if (host_scalars()) {
@@ -288,7 +289,7 @@ std::vector<double> Comm::allgather_f64(double x) const {
 }
 
 std::string Comm::bcast(const std::string& s, int root) const {
-  if (!distributed()) return s;
+  if (!distributed() || size_ == 1) return s;
   int64_t n = rank_ == root ? (int64_t)s.size() : 0;
   n = allreduce(n, SUM);
   at::Tensor t = at::zeros({std::max<int64_t>(n, 1)}, at::TensorOptions().dtype(at::kByte));
