@@ -331,14 +331,22 @@ def bench_pagerank_extra(comm, args):
     from gpu_mapreduce_amd import MapReduce
     from gpu_mapreduce_amd.models.pagerank import PageRank, rmat_map
     scale, ef, iters = args.pagerank_scale, args.edgefactor, args.iters
-    _sync(comm)
-    t0 = time.perf_counter()
-    mr = MapReduce(comm)
-    rmat_map(mr, scale, ef, seed=args.seed)
-    pr = PageRank(mr, 1 << scale).build()
-    del mr
-    _sync(comm)
-    setup = comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
+
+    def setup_once():
+        """R-MAT generation (map) + aggregate to the owners + plan build, timed"""
+        _sync(comm)
+        t0 = time.perf_counter()
+        mr = MapReduce(comm)
+        rmat_map(mr, scale, ef, seed=args.seed)
+        p = PageRank(mr, 1 << scale).build()
+        del mr
+        _sync(comm)
+        return p, comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
+    # the first setup of the process (cold: device memory grows, kernels load)
+    # is the record's pagerank_setup_ms; a second one shows the warm cost
+    pr, setup = setup_once()
+    del pr
+    pr, setup_warm = setup_once()
     nedge = comm.allreduce(pr.nedge, "sum")
     for _ in range(max(1, args.pagerank_warmup)):
         pr.reset()
@@ -355,6 +363,7 @@ def bench_pagerank_extra(comm, args):
         "pagerank_kvps": nedge * iters / dt,
         "pagerank_ms": dt * 1e3,
         "pagerank_setup_ms": setup * 1e3,
+        "pagerank_setup_warm_ms": setup_warm * 1e3,
         "pagerank_kvps_incl_setup": nedge * iters / (dt + setup),
         "pagerank_hip_graph_iterations": pr.graph_iterations,
         "pagerank_layout": pr.layout,
