@@ -620,6 +620,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("plan_gather_reduce", &mrh::plan_gather_reduce);
   m.def("plan_combine", &mrh::plan_combine);
   m.def("wedges", &mrh::wedges);
+  m.def("wedge_chunks", [](const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre, int64_t max_w) {
+    std::vector<std::pair<at::Tensor, at::Tensor>> out;
+    for_each_wedge_chunk(seg, nb, centre, max_w, [&](const at::Tensor& e, const at::Tensor& c) { out.emplace_back(e, c); });
+    return out;
+  });
   // the reference's 4-collate tri_find over this rank's [n,2] int64 edges,
   // each stage timed (oink/trifind_mr.h); budgets / fpath / memsize as the
   // MapReduce settings of the pipeline's object (0 / "": defaults)

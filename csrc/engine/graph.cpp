@@ -1,6 +1,7 @@
 // Graph-iteration engine ops (PageRank plan execution) with CPU twins.
 #include <ATen/hip/HIPContext.h>
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 
@@ -241,40 +242,76 @@ void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tens
 }
 
 // all neighbour pairs per group: returns (edges [W,2] int64 (min,max), centre [W])
-std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre) {
-  const int64_t ng = seg.numel() - 1;
-  need(ng >= 0, "wedges: seg holds ngroups + 1 offsets");
+namespace {
+struct WedgeScan {
+  at::Tensor wscan;  // exclusive scan of C(d,2) over the groups, ng + 1 entries
+  int64_t ng = 0, nw = 0;
+};
+WedgeScan wedge_scan(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre) {
+  WedgeScan w;
+  w.ng = seg.numel() - 1;
+  need(w.ng >= 0, "wedges: seg holds ngroups + 1 offsets");
   operand(seg, at::kLong, seg.device(), "wedges seg");
   operand(nb, at::kLong, seg.device(), "wedges neighbours");
   operand(centre, at::kLong, seg.device(), "wedges centre");
-  need(centre.numel() >= ng, "wedges: one centre per group");
-  at::Tensor d = seg.narrow(0, 1, ng) - seg.narrow(0, 0, ng);
-  at::Tensor cnt = at::floor_divide(d * (d - 1), 2);
-  at::Tensor wscan = exclusive_scan(cnt.contiguous());
-  const int64_t nw = ng > 0 ? wscan[ng].item<int64_t>() : 0;
-  at::Tensor oe = at::empty({nw, 2}, nb.options());
-  at::Tensor oc = at::empty({nw}, nb.options());
-  if (nw == 0) return {oe, oc};
+  need(centre.numel() >= w.ng, "wedges: one centre per group");
+  at::Tensor d = seg.narrow(0, 1, w.ng) - seg.narrow(0, 0, w.ng);
+  w.wscan = exclusive_scan(at::floor_divide(d * (d - 1), 2).contiguous());
+  w.nw = w.ng > 0 ? w.wscan[w.ng].item<int64_t>() : 0;
+  return w;
+}
+// wedges [w0, w1) of the scan
+std::pair<at::Tensor, at::Tensor> wedge_range(const at::Tensor& seg, const WedgeScan& ws, const at::Tensor& nb,
+                                              const at::Tensor& centre, int64_t w0, int64_t w1) {
+  const int64_t n = w1 - w0;
+  at::Tensor oe = at::empty({n, 2}, nb.options());
+  at::Tensor oc = at::empty({n}, nb.options());
+  if (n == 0) return {oe, oc};
   if (seg.is_cuda()) {
-    k::wedges(P0<int64_t>(seg), P0<int64_t>(wscan), ng, P0<int64_t>(nb), P0<int64_t>(centre), nw, P0<int64_t>(oe),
-              P0<int64_t>(oc), cur());
+    k::wedges(P0<int64_t>(seg), P0<int64_t>(ws.wscan), ws.ng, P0<int64_t>(nb), P0<int64_t>(centre), w0, n,
+              P0<int64_t>(oe), P0<int64_t>(oc), cur());
     return {oe, oc};
   }
   const int64_t* sg = P0<int64_t>(seg);
-  const int64_t* n = P0<int64_t>(nb);
+  const int64_t* sc = P0<int64_t>(ws.wscan);
+  const int64_t* nbp = P0<int64_t>(nb);
   const int64_t* c = P0<int64_t>(centre);
   int64_t* e = P0<int64_t>(oe);
   int64_t* co = P0<int64_t>(oc);
-  int64_t w = 0;
-  for (int64_t g = 0; g < ng; ++g)
-    for (int64_t j = sg[g]; j < sg[g + 1]; ++j)
-      for (int64_t k2 = j + 1; k2 < sg[g + 1]; ++k2) {
-        uint64_t a = (uint64_t)n[j], b = (uint64_t)n[k2];
-        e[2 * w] = (int64_t)(a < b ? a : b);
-        e[2 * w + 1] = (int64_t)(a < b ? b : a);
-        co[w++] = c[g];
-      }
+  // first wedge: its group, then (j, k) by walking the rows of its triangle
+  int64_t g = std::upper_bound(sc, sc + ws.ng, w0) - sc - 1, t = w0 - sc[g], j = 0;
+  int64_t d = sg[g + 1] - sg[g];
+  while (t >= d - 1 - j) t -= d - 1 - j++;
+  int64_t k2 = j + 1 + t;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t a = (uint64_t)nbp[sg[g] + j], b = (uint64_t)nbp[sg[g] + k2];
+    e[2 * i] = (int64_t)(a < b ? a : b);
+    e[2 * i + 1] = (int64_t)(a < b ? b : a);
+    co[i] = c[g];
+    if (++k2 < d) continue;
+    k2 = ++j + 1;
+    if (k2 < d) continue;
+    do d = ++g < ws.ng ? sg[g + 1] - sg[g] : 2;  // next group with a wedge
+    while (d < 2);
+    j = 0, k2 = 1;
+  }
   return {oe, oc};
+}
+}  // namespace
+
+std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre) {
+  const WedgeScan ws = wedge_scan(seg, nb, centre);
+  return wedge_range(seg, ws, nb, centre, 0, ws.nw);
+}
+
+void for_each_wedge_chunk(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre, int64_t max_w,
+                          const std::function<void(const at::Tensor&, const at::Tensor&)>& fn) {
+  const WedgeScan ws = wedge_scan(seg, nb, centre);
+  const int64_t step = max_w > 0 ? max_w : std::max<int64_t>(ws.nw, 1);
+  for (int64_t w0 = 0; w0 < ws.nw; w0 += step) {
+    auto r = wedge_range(seg, ws, nb, centre, w0, std::min(ws.nw, w0 + step));
+    fn(r.first, r.second);
+  }
 }
 
 }  // namespace mrh

@@ -156,6 +156,7 @@ bool install_alloc_guard() {
 bool alloc_guard_active() { return g_active; }
 
 void set_current_op(const char* op) { t_op = op ? op : "(outside any MapReduce op)"; }
+const char* current_op() { return t_op.c_str(); }
 
 int check_all_blocks(const char* op) {
   if (!g_active) return 0;

@@ -47,6 +47,7 @@ int check_all_blocks(const char* op);
 std::vector<GuardReport> guard_reports();
 // the op currently running on this thread (recorded with each allocation)
 void set_current_op(const char* op);
+const char* current_op();
 int64_t guarded_blocks_live();
 
 }  // namespace guard

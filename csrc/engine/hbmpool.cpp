@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "guard.h"
+#include "guardalloc.h"
 
 namespace mrh::hbm {
 
@@ -233,7 +234,7 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
       ++d.failures;
       TORCH_CHECK_WITH(OutOfMemoryError, false, "mrhip page pool: Cannot allocate page: ", mib(bytes),
                        " requested with ", mib(d.in_use), " in use of a cap of ", mib(d.cap),
-                       " (maxpage x memsize / hbm_budget) on device ", dev);
+                       " (maxpage x memsize / hbm_budget) on device ", dev, " in ", guard::current_op());
     }
     if (!d.pending.empty()) reap(d);
     auto it = d.free.find({stream, bytes});

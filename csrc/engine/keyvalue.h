@@ -73,6 +73,9 @@ class KeyValue {
   }
   // tiers the spooled pieces went to (empty stats without a spool)
   SpoolStats spool_stats() const { return spool_ ? spool_->stats() : last_spool_; }
+  // bytes per spooled piece of a bounded builder (0: unbounded) — a batch
+  // callback whose output can dwarf its input emits it in chunks of this size
+  int64_t piece_bytes() const { return spool_ ? piece_bytes_ : 0; }
   bool grouping() const { return grp_ != nullptr; }
   // capacity hint for the grouped arenas (GroupIndex::reserve); no-op without grouping
   void reserve_grouping(int64_t rows, int64_t key_bytes, int64_t value_bytes) {

@@ -198,6 +198,11 @@ SegIndex seg_index(const at::Tensor& seg, int64_t nval);
 void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tensor& x, const at::Tensor& w, int64_t op,
                        at::Tensor& out);
 std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre);
+// the same wedges in chunks of at most max_w (<= 0: one chunk), handed to fn
+// in wedge order: an emitter bounded by a page budget never holds the whole
+// O(d^2) set (a hub of degree 20k alone makes 2e8 wedges, 4.8 GB)
+void for_each_wedge_chunk(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre, int64_t max_w,
+                          const std::function<void(const at::Tensor& edges, const at::Tensor& centre)>& fn);
 // segment id of every value of a CSR segment array (seg[nseg+1], nval values)
 at::Tensor segment_ids(const at::Tensor& seg, int64_t nseg, int64_t nval);
 // counts of each bin in [0, K) of an integer index column (device histogram)

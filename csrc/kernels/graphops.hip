@@ -541,10 +541,11 @@ __global__ __launch_bounds__(NT) void k_scatter_t(const T* __restrict__ v, const
 // the degree skew.
 __global__ __launch_bounds__(NT) void k_wedges(const int64_t* __restrict__ seg, const int64_t* __restrict__ wscan,
                                               int64_t ngrp, const int64_t* __restrict__ nb,
-                                              const int64_t* __restrict__ centre, int64_t nwedge,
+                                              const int64_t* __restrict__ centre, int64_t w0, int64_t nwedge,
                                               int64_t* __restrict__ out_edge, int64_t* __restrict__ out_centre) {
-  int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (w >= nwedge) return;
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= nwedge) return;
+  const int64_t w = w0 + i;  // global wedge id; the chunk's output slot is i
   int64_t lo = 0, hi = ngrp - 1;
   while (lo < hi) {
     int64_t mid = (lo + hi + 1) >> 1;
@@ -563,9 +564,9 @@ __global__ __launch_bounds__(NT) void k_wedges(const int64_t* __restrict__ seg, 
   const int64_t k = j + 1 + (t - j * (2 * d - j - 1) / 2);
   const int64_t a = nb[seg[g] + j], b = nb[seg[g] + k];
   const bool lt = (uint64_t)a < (uint64_t)b;
-  out_edge[2 * w] = lt ? a : b;
-  out_edge[2 * w + 1] = lt ? b : a;
-  out_centre[w] = centre[g];
+  out_edge[2 * i] = lt ? a : b;
+  out_edge[2 * i + 1] = lt ? b : a;
+  out_centre[i] = centre[g];
 }
 
 }  // namespace
@@ -660,10 +661,10 @@ void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_
 }
 
 void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
-            int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s) {
+            int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s) {
   if (nwedge <= 0 || ngrp <= 0) return;
   hipLaunchKernelGGL(k_wedges, dim3((unsigned)((nwedge + NT - 1) / NT)), dim3(NT), 0, s, seg, wscan, ngrp, nb, centre,
-                     nwedge, out_edge, out_centre);
+                     w0, nwedge, out_edge, out_centre);
   MRH_CHECK_LAUNCH();
 }
 

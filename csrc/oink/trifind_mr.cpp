@@ -68,8 +68,10 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
   stage("reduce nsq_angles", mrt, [&] {
     mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // O(d^2) wedges, load-balanced kernel
       if (!m.nkey) return;
-      auto r = wedges(m.seg, m.vdata.view(at::kLong), m.keys.kdata.view(at::kLong));
-      if (r.first.numel()) add_tensors(kv, r.first, r.second);
+      // under a page budget the wedges go out in spool pieces (24 B a wedge)
+      const int64_t chunk = kv.piece_bytes() / 24;
+      for_each_wedge_chunk(m.seg, m.vdata.view(at::kLong), m.keys.kdata.view(at::kLong), chunk,
+                           [&](const at::Tensor& e, const at::Tensor& c) { add_tensors(kv, e, c); });
     });
   });
   stage("add edges", mrt, [&] { mrt.add(mre); });

@@ -81,23 +81,31 @@ except torch.OutOfMemoryError as e:
     assert "Cannot allocate page" in str(e), e
 hbm_pool.set_cap(0, 0)
 assert hbm_pool.stats(0)["failures"] >= 1
-# a MapReduce op under a page budget: clone() of 64 MiB with a 4 MiB budget
-# needs 64 MiB of new device memory > 2 x 4 MiB -> Cannot allocate page
+# a MapReduce op under a page budget (1 MiB pages, maxpage 4): the map's
+# 64 MiB of pairs are spooled to pinned host. clone() has an out-of-core
+# path and clones them where they live; collapse() has none and must bring
+# them back to HBM: 64 MiB of new device memory > 2 x 4 MiB + 16 MiB of
+# scratch -> Cannot allocate page
 n = 8 << 20
 mr = g.MapReduce(comm)
 mr.memsize = -(1 << 20)  # 1 MiB pages
 mr.maxpage = 4
 k = torch.arange(n, dtype=torch.int64, device="cuda")
-mr.map(1, lambda itask, kv: kv.add_kv(C.make_kv(k, None, k, None, n, "cuda")))
+emit = lambda itask, kv: kv.add_kv(C.make_kv(k, None, k, None, n, "cuda"))
+mr.map(1, emit)
+assert mr.clone() == n
+assert not mr.kmv.vdata.is_cuda
+mr.map(1, emit)
 try:
-    mr.clone()
-    raise SystemExit("clone past the page budget succeeded")
+    mr.collapse(b"all")
+    raise SystemExit("collapse past the page budget succeeded")
 except Exception as e:
     assert "Cannot allocate page" in str(e), e
-# the same budget large enough: the op runs, and the pool saw the peak
+# the same budget large enough: the op runs in HBM
 mr.maxpage = 256
+mr.map(1, emit)
 mr.clone()
-assert mr.kmv.nkey == n
+assert mr.kmv.nkey == n and mr.kmv.vdata.is_cuda
 print("ok", hbm_pool.stats(0))
 '''
 

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_mapreduce_amd import ops
+from gpu_mapreduce_amd import C, ops
 
 DEVS = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
 
@@ -131,6 +131,26 @@ def test_wedges_vs_combinations(dev):
         for a, b in itertools.combinations(nb[seg[gi]:seg[gi + 1]].tolist(), 2):
             ref.append(((min(a, b), max(a, b)), int(centre[gi])))
     assert got == sorted(ref)
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_wedge_chunks_concatenate_to_wedges(dev):
+    # bounded emission (tri_find_mr under a page budget): the chunks, in
+    # order, are the one-shot wedge set, whatever the chunk size and however
+    # many groups have no wedge (degree 0/1)
+    g = torch.Generator().manual_seed(11)
+    deg = torch.randint(0, 4, (300,), generator=g)
+    deg[[5, 120, 299]] = torch.tensor([40, 1, 25])
+    seg = torch.cat([torch.zeros(1, dtype=torch.int64), deg.cumsum(0)]).to(dev)
+    nb = torch.randint(0, 1 << 40, (int(deg.sum()),), generator=g).to(dev)
+    centre = torch.arange(300, dtype=torch.int64).to(dev) + 7
+    e, c = C.wedges(seg, nb, centre)
+    for step in (1, 7, 64, 1000, 0):
+        parts = C.wedge_chunks(seg, nb, centre, step)
+        if step:
+            assert all(p[1].numel() <= step for p in parts)
+        assert torch.equal(torch.cat([p[0] for p in parts]), e)
+        assert torch.equal(torch.cat([p[1] for p in parts]), c)
 
 
 @pytest.mark.parametrize("dev", DEVS)
