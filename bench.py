@@ -656,6 +656,16 @@ def main():
         res = bench_wordfreq(comm, args)
     # before the extras: a failing extra poisons (aborts) the communicator
     rrec = rccl_record(comm)
+    peaks = {}
+
+    def mark(part):
+        """hi-water of pool bytes in use during `part`, then a fresh mark"""
+        from gpu_mapreduce_amd.runtime import hbm_pool
+        if hbm_pool.installed() and comm.is_cuda:
+            dev = torch.device(comm.device).index or 0
+            peaks[part] = hbm_pool.stats(dev)["peak"]
+            hbm_pool.reset_peak(dev)
+    mark(args.workload)
     if args.workload == "invertedindex" and args.pagerank_scale > 0:
         # the headline line is printed even if the PageRank extra fails (its
         # peers fail fast through the engine's peer monitor); the error is
@@ -665,6 +675,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             res["pagerank_error"] = f"{type(e).__name__}: {e}"[:500]
             print(f"bench.py rank {comm.rank}: PageRank extra failed: {e}", file=sys.stderr, flush=True)
+        mark("pagerank")
     if args.workload == "invertedindex" and args.file_io_steps > 0:
         # the headline job again with its file reads and output write (the
         # reference's end-to-end scope), failure-isolated
@@ -675,37 +686,46 @@ def main():
             res["with_file_io"] = bench_inverted_index_files(comm, a)
         except Exception as e:  # noqa: BLE001
             res["with_file_io"] = {"error": f"{type(e).__name__}: {e}"[:500]}
+        mark("with_file_io")
     if args.workload == "invertedindex":
         # BASELINE configs 5 and 3 in the same driver-measured record
         if args.trifind_scale > 0:
             from gpu_mapreduce_amd.models.triangles import bench_trifind
             res.update(_extra(comm, "trifind", bench_trifind, args, scale=args.trifind_scale,
                               steps=args.extra_steps, warmup=1))
+            mark("trifind")
         if args.wordfreq_bytes > 0:
             from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
             res.update(_extra(comm, "wordfreq", bench_wordfreq, args, bytes_per_gpu=args.wordfreq_bytes,
                               file_bytes=min(args.file_bytes, int(args.wordfreq_bytes)),
                               steps=args.extra_steps, warmup=6))  # steady state after ~6 jobs:
             # warmup 1 / 2 / 6 -> 27.1 / 24.7 / 22.8 ms (profiles/r3_wordfreq_input.txt)
+            mark("wordfreq")
         if args.trifind_mr_scale > 0:
             from gpu_mapreduce_amd.models.triangles import bench_trifind_mr
             r = _extra(comm, "trifind_mr", bench_trifind_mr, args, scale=args.trifind_mr_scale, steps=1, warmup=1,
                        mr_ooc_scale=args.trifind_mr_ooc_scale)
             res.update(r)
+            mark("trifind_mr")
         if args.wordfreq_bytes > 0 and args.file_io_steps > 0:
             try:
                 res["wordfreq_with_file_io"] = bench_wordfreq_files(comm, args)
             except Exception as e:  # noqa: BLE001
                 res["wordfreq_with_file_io"] = {"error": f"{type(e).__name__}: {e}"[:500]}
+            mark("wordfreq_with_file_io")
         if comm.size == 1 and comm.is_cuda and args.dist_extras:
             res.update(bench_dist_plans(comm, args))
+            mark("dist_extras")
     res.update(rrec)
     res["ranks_joined"] = comm.size
     from gpu_mapreduce_amd.runtime import hbm_pool
     res["device_allocator"] = "mrhip HBM page pool (csrc/engine/hbmpool.cpp)" if hbm_pool.installed() else "ATen caching allocator"
     if hbm_pool.installed() and comm.is_cuda:
         st = hbm_pool.stats(torch.device(comm.device).index or 0)
-        res["hbm_pool_peak_bytes"] = st["peak"]
+        res["hbm_pool_peak_bytes"] = max([st["peak"], *peaks.values()])  # hi-water of bytes in use
+        res["hbm_pool_reserved_peak_bytes"] = st["reserved_peak"]  # hi-water of bytes held from the driver
+        res["hbm_pool_cross_stream_reuse"] = st["cross_stream_reuse"]
+        res["hbm_pool_peak_bytes_by_part"] = peaks  # the hi-water of each workload of the record
     res["backend"] = {"torch.distributed": (comm.backend or "none (world size 1)") + " (host objects/scalars only)",
                       "engine_transport": rrec["engine_transport"]}
     out = {

@@ -500,6 +500,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     d["in_use"] = s.in_use;
     d["peak"] = s.peak;
     d["reserved"] = s.reserved;
+    d["reserved_peak"] = s.reserved_peak;
     d["cap"] = s.cap;
     d["allocs"] = s.allocs;
     d["frees"] = s.frees;

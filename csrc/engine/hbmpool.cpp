@@ -389,6 +389,7 @@ PoolStats stats(int device) {
   if (d.pool) {
     uint64_t r = 0;
     if (hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemCurrent, &r) == hipSuccess) s.reserved = (int64_t)r;
+    if (hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemHigh, &r) == hipSuccess) s.reserved_peak = (int64_t)r;
   }
   return s;
 }

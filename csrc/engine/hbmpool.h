@@ -40,6 +40,7 @@ struct PoolStats {
   int64_t in_use = 0;    // bytes of live allocations (512-byte granules)
   int64_t peak = 0;      // hi-water mark of in_use since the last reset_peak
   int64_t reserved = 0;  // bytes the HIP pool holds from the driver
+  int64_t reserved_peak = 0;  // hi-water mark of reserved
   int64_t cap = 0;       // hard cap on in_use (0: none)
   int64_t allocs = 0, frees = 0, failures = 0;
   int64_t cached = 0;              // bytes of freed blocks held in the per-(stream, class) caches

@@ -26,7 +26,8 @@ def installed() -> bool:
 
 
 def stats(device: int = 0) -> dict:
-    """{in_use, peak, reserved, cap, allocs, frees, failures} in bytes / counts"""
+    """{in_use, peak, reserved, reserved_peak, cap, allocs, frees, failures,
+    cached, cross_stream_reuse, faulted} in bytes / counts"""
     return dict(C.hbm_pool_stats(int(device)))
 
 
