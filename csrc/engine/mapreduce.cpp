@@ -590,6 +590,7 @@ uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) 
 uint64_t MapReduce::map(int nmap, const MapTaskFn& fn, int addflag) {  // :1044-1051
   start();
   OpTrace tr_(__func__, this);
+  drop_for_map(addflag);
   enter(__func__);
   KeyValue kvb(device());
   bound(kvb);
@@ -626,6 +627,7 @@ uint64_t MapReduce::map_file(const std::vector<std::string>& files, int selfflag
                              const MapFileFn& fn, int addflag) {  // :1060-1092
   start();
   OpTrace tr_(__func__, this);
+  drop_for_map(addflag);
   enter(__func__);
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
@@ -658,6 +660,7 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
                                int addflag) {
   start();
   OpTrace tr_(__func__, this);
+  drop_for_map(addflag);
   enter(__func__);
   auto fl = find_files(*comm_, files, selfflag, recurse, readflag);
   mapfilecount = (int)fl.size();
@@ -736,6 +739,7 @@ uint64_t MapReduce::map_chunks(int nmap, const std::vector<std::string>& files, 
 uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  // :1560-1642
   start();
   OpTrace tr_(__func__, this);
+  drop_for_map(addflag, &src);
   enter(__func__);
   src.ensure_resident();
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
@@ -760,6 +764,7 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
 uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addflag) {
   start();
   OpTrace tr_(__func__, this);
+  drop_for_map(addflag, &src);
   enter(__func__);
   src.ensure_resident();
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
@@ -1631,6 +1636,15 @@ void MapReduce::ensure_resident() {
   disk_path_.clear();
   read_file(p);
   std::remove(p.c_str());
+}
+
+void MapReduce::drop_for_map(int addflag, const MapReduce* src) {
+  // the reference deletes kv/kmv at the start of a map too (src/mapreduce.cpp:1044-1051)
+  if (addflag || src == this) return;
+  drop_disk();
+  kv.reset();
+  kmv.reset();
+  grouped_.reset();
 }
 
 void MapReduce::drop_disk() {

@@ -236,6 +236,9 @@ class MapReduce {
   void write_file(const std::string& p) const;
   int64_t read_file(const std::string& p);
   void drop_disk();
+  // a map replacing the object's data (addflag 0, not reading its own KV)
+  // drops the old KV/KMV up front instead of bringing them back to HBM
+  void drop_for_map(int addflag, const MapReduce* src = nullptr);
 
   CommPtr comm_;
   std::string disk_path_;
