@@ -614,6 +614,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("inverted_index_format", &inverted_index_format);
   m.def("segments_sorted", &segments_sorted);
+  m.def("segments_from_bits", &segments_from_bits);
   m.def("pr_contrib", &mrh::pr_contrib);
   m.def("pr_combine", &mrh::pr_combine);
   m.def("scatter_f32", &mrh::scatter_f32);

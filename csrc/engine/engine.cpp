@@ -533,6 +533,30 @@ at::Tensor segments_from_flags(const at::Tensor& flags_in) {
   return seg;
 }
 
+at::Tensor segments_from_bits(const at::Tensor& heads, int64_t n) {
+  const at::Device dev = heads.device();
+  if (n == 0) return at::zeros({1}, opt(dev, at::kLong));
+  const int64_t nw = (n + 63) / 64;
+  if (heads.scalar_type() != at::kInt || !heads.is_contiguous() || heads.numel() < 2 * nw)
+    fail("segments_from_bits: int32 head words covering n bits");
+  if (!dev.is_cuda()) {
+    const uint32_t* h = P0<uint32_t>(heads);
+    std::vector<int64_t> v;
+    for (int64_t i = 0; i < n; ++i)
+      if (h[i >> 5] >> (i & 31) & 1u) v.push_back(i);
+    v.push_back(n);
+    return at::tensor(v, opt(at::kCPU, at::kLong));
+  }
+  at::Tensor cnt = at::empty({nw}, opt(dev, at::kInt));
+  const uint64_t* h64 = reinterpret_cast<const uint64_t*>(heads.data_ptr());
+  k::bits_count(h64, nw, P0<uint32_t>(cnt), cur_stream());
+  at::Tensor pos = scan_u32(cnt);
+  const int64_t nseg = (int64_t)(uint32_t)pos[nw].item<int32_t>();
+  at::Tensor seg = at::empty({nseg + 1}, opt(dev, at::kLong));
+  k::bits_compact(h64, nw, P0<uint32_t>(pos), n, P0<int64_t>(seg), cur_stream());
+  return seg;
+}
+
 at::Tensor segments_sorted(const at::Tensor& sorted_keys) {
   at::Tensor flags, pos, seg;
   int64_t nseg = 0;

@@ -228,6 +228,19 @@ SegIndex seg_index(const at::Tensor& seg, int64_t nval) {
   return ix;
 }
 
+SegIndex seg_index(const at::Tensor& seg, int64_t nval, const at::Tensor& heads) {
+  SegIndex ix;
+  need(seg.is_cuda() && heads.device() == seg.device(), "seg_index: device plans only");
+  need(heads.scalar_type() == at::kInt && heads.numel() == k::ws_words(nval), "seg_index: heads must be ws_words(nval) words");
+  const at::Device d = seg.device();
+  ix.nval = nval;
+  ix.H = heads;
+  ix.wbase = at::empty({std::max<int64_t>(k::ws_waves(nval), 1)}, opt(d, at::kLong));
+  ix.scratch = at::empty({(int64_t)k::ws_scratch_bytes(nval)}, opt(d, at::kByte));
+  k::ws_bases(P0<int64_t>(seg), seg.numel() - 1, nval, P0<int64_t>(ix.wbase), cur());
+  return ix;
+}
+
 void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tensor& x, const at::Tensor& w, int64_t op,
                        at::Tensor& out) {
   const bool hw = w.defined() && w.numel() > 0;

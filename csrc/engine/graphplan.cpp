@@ -296,7 +296,8 @@ PageRankPlan::PageRankPlan(CommPtr c, const at::Tensor& edges, int64_t nvert, do
     use_graph = !(g && *g == '0');
   }
   if (ngrp > 0 && use_seg_index(dev) && !pb_) {
-    six_ = seg_index(seg_, nedge);
+    six_ = heads_.defined() ? seg_index(seg_, nedge, heads_) : seg_index(seg_, nedge);
+    heads_ = at::Tensor();
     if (xsched_.defined()) {
       six_.sched = xsched_;
       six_.slen = xslen_;
@@ -365,6 +366,18 @@ at::Tensor PageRankPlan::out_degrees(const at::Tensor& packed, bool sorted_by_so
   k::pr_run_degree(reinterpret_cast<const uint64_t*>(packed.data_ptr()), useg.data_ptr<int64_t>(), useg.numel() - 1,
                    reinterpret_cast<uint32_t*>(deg.data_ptr()), s);
   return deg;
+}
+
+// sorted (group key << 32 | new source id) -> src_, the groups seg_ and
+// their head bitmap heads_ (the gather's segment index, no per-edge flags)
+void PageRankPlan::unpack_sorted(const at::Tensor& sorted) {
+  const hipStream_t s = at::hip::getCurrentHIPStream();
+  src_ = at::empty({nedge}, opt(dev, at::kInt));
+  heads_ = at::empty({k::ws_words(nedge)}, opt(dev, at::kInt));
+  pr_chk(hipMemsetAsync(heads_.data_ptr(), 0, heads_.numel() * 4, s), "hipMemsetAsync");
+  k::pr_unpack_bits(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), nedge, src_.data_ptr<int32_t>(),
+                    reinterpret_cast<uint32_t*>(heads_.data_ptr()), s);
+  seg_ = segments_from_bits(heads_, nedge);
 }
 
 bool PageRankPlan::degrees_by_sort() {
@@ -458,13 +471,7 @@ void PageRankPlan::build_device(const at::Tensor& e) {
   }
   clk("sort by destination");
   // 4. unpack
-  src_ = at::empty({nedge}, opt(dev, at::kInt));
-  {
-    at::Tensor flags = at::empty({nedge}, opt(dev, at::kInt));
-    k::pr_unpack(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), nedge, src_.data_ptr<int32_t>(),
-                 reinterpret_cast<uint32_t*>(flags.data_ptr()), s);
-    seg_ = segments_from_flags(flags);
-  }
+  unpack_sorted(sorted);
   const int64_t ngrp = seg_.numel() - 1;
   at::Tensor hi = at::empty({ngrp}, opt(dev, at::kLong));
   k::pr_group_hi(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), seg_.data_ptr<int64_t>(), ngrp,
@@ -603,13 +610,7 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
     sorted = radix_sort_keys(key, 32, 32 + dbits + rbits, false);
   }
   clk("sort by destination");
-  src_ = at::empty({nedge}, opt(dev, at::kInt));
-  {
-    at::Tensor flags = at::empty({nedge}, opt(dev, at::kInt));
-    k::pr_unpack(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), nedge, src_.data_ptr<int32_t>(),
-                 reinterpret_cast<uint32_t*>(flags.data_ptr()), s);
-    seg_ = nedge > 0 ? segments_from_flags(flags) : at::zeros({1}, opt(dev, at::kLong));
-  }
+  unpack_sorted(sorted);
   const int64_t ngrp = seg_.numel() - 1;
   at::Tensor hi = at::empty({std::max<int64_t>(ngrp, 1)}, opt(dev, at::kLong));
   k::pr_group_hi(reinterpret_cast<const uint64_t*>(sorted.data_ptr()), seg_.data_ptr<int64_t>(), ngrp,

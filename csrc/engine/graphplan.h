@@ -124,6 +124,9 @@ class PageRankPlan {
   // degree relabel (both device builds); relabel returns the local dangling count
   at::Tensor out_degrees(const at::Tensor& packed, bool sorted_by_source);
   static bool degrees_by_sort();
+  // sorted (group key << 32 | source) -> src_, seg_ and the head bitmap heads_
+  void unpack_sorted(const at::Tensor& sorted);
+  at::Tensor heads_;  // until the segment index takes it
   int64_t relabel_by_degree(at::Tensor deg, bool want_degn, at::Tensor& nid, at::Tensor& degn);
   // several GPUs: destination-owned edges, replicated c vector (graphplan.cpp)
   void build_device_dist(const at::Tensor& e);

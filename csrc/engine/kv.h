@@ -194,6 +194,9 @@ struct SegIndex {
   bool defined() const { return H.defined(); }
 };
 SegIndex seg_index(const at::Tensor& seg, int64_t nval);
+// the same over a head bitmap already built (k::ws_words(nval) words, e.g. by
+// the unpack of a sorted plan): only the per-wave bases are computed
+SegIndex seg_index(const at::Tensor& seg, int64_t nval, const at::Tensor& heads);
 // out[s] = OP_{e in seg s} (x[src[e]] (+ w[e])), op 0 sum / 1 min / 2 max
 void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tensor& x, const at::Tensor& w, int64_t op,
                        at::Tensor& out);
@@ -216,6 +219,9 @@ at::Tensor repeat_index(const at::Tensor& counts);
 at::Tensor segments_sorted(const at::Tensor& sorted_keys);
 // segment boundaries from u32 head flags (1 where a segment starts): seg[nseg+1]
 at::Tensor segments_from_flags(const at::Tensor& flags);
+// segment boundaries from a head bitmap over n values (int32 words, bit i of
+// word i / 32 set where a segment starts; words past n zero): seg[nseg+1]
+at::Tensor segments_from_bits(const at::Tensor& heads, int64_t n);
 
 // K-means map with in-mapper combining (kmeans.cpp): KV(int32 cluster*(D+1)+j, double)
 KV kmeans_map(const at::Tensor& points, const at::Tensor& centroids);

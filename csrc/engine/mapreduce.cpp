@@ -510,11 +510,12 @@ void MapReduce::note_shuffle(const ShuffleStats& st) {
 uint64_t MapReduce::add(MapReduce& other) {  // :348-374
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__);
+  enter(__func__, true);  // out-of-core data is appended where it lives (a bounded MR appends through a Spool)
   need_kv("add");
   other.ensure_resident();
   if (!other.kv) fail("MapReduce passed to add() does not have KeyValue pairs");
-  kv = concat({*kv, *other.kv}, device());
+  kv = append_kv(*kv, *other.kv);
+  grouped_.reset();
   stats("Add", 0);
   return count(kv->n);
 }

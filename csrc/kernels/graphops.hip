@@ -105,8 +105,12 @@ __global__ __launch_bounds__(NT) void k_pr_relabel(const uint32_t* __restrict__ 
     invdeg[i] = dg ? 0.f : (float)(1.0 / (double)d);
     if (degn) degn[i] = (int32_t)d;
   }
-  const uint64_t b = __ballot(dg);
-  if (dev::lane_id() == 0 && b) atomicAdd(ndangling, (unsigned long long)__popcll(b));
+  // degrees descend, so the dangling vertices are the tail: the first of
+  // them records the count (one store, no per-wave atomics on one word)
+  if (i < n && dg) {
+    const bool prev_dg = i > 0 && deg[order[i - 1]] == 0;
+    if (!prev_dg) *ndangling = (unsigned long long)(n - i);
+  }
 }
 
 // out[k] = in[min(k * stride, n - 1)], k < ns (a host-sized sample of a scan)
@@ -253,6 +257,23 @@ __global__ __launch_bounds__(NT) void k_pr_unpack(const uint64_t* __restrict__ s
   const uint64_t k = s[i];
   src[i] = (int32_t)(uint32_t)k;
   flags[i] = (i == 0 || (s[i - 1] >> 32) != (k >> 32)) ? 1u : 0u;
+}
+
+// the same split, the heads as a bitmap (bit i of u32 word i / 32; one
+// ballot per wave, written as one 8-byte store by lane 0 — waves start at
+// multiples of 64) instead of a u32 flag per edge: the gather's segment index
+// (wavesegred.h H) directly, 1/32 of the bytes; words past n stay as zeroed
+__global__ __launch_bounds__(NT) void k_pr_unpack_bits(const uint64_t* __restrict__ s, int64_t n,
+                                                       int32_t* __restrict__ src, uint2* __restrict__ H) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  bool head = false;
+  if (i < n) {
+    const uint64_t k = s[i];
+    src[i] = (int32_t)(uint32_t)k;
+    head = i == 0 || (s[i - 1] >> 32) != (k >> 32);
+  }
+  const uint64_t b = __ballot(head);
+  if (dev::lane_id() == 0 && i < n) H[i >> 6] = make_uint2((uint32_t)b, (uint32_t)(b >> 32));
 }
 
 // per destination group: its hi word (the group's destination)
@@ -624,6 +645,12 @@ size_t ws_scratch_bytes(int64_t nval) {
   return (size_t)nc * 16 + (size_t)nc2 * 16 + 64;
 }
 
+void ws_bases(const int64_t* seg, int64_t nseg, int64_t nval, int64_t* wbase, hipStream_t s) {
+  const int64_t nw = dev::ws_nwave(nval);
+  if (nw > 0)
+    hipLaunchKernelGGL(dev::k_ws_base, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, seg, nseg, nw, wbase);
+  MRH_CHECK_LAUNCH();
+}
 void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64_t* wbase, hipStream_t s) {
   const int64_t nw = dev::ws_nwave(nval);
   MRH_HIP(hipMemsetAsync(H, 0, sizeof(uint32_t) * dev::ws_head_words(nval), s));
@@ -779,6 +806,11 @@ void pr_unmix_ids(const int64_t* order, int64_t n, int P, int me, int64_t N, boo
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_pr_unpack, dim3(pr_grid(n)), dim3(NT), 0, s, sorted, n, src, flags);
+  MRH_CHECK_LAUNCH();
+}
+void pr_unpack_bits(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* H, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pr_unpack_bits, dim3(pr_grid(n)), dim3(NT), 0, s, sorted, n, src, reinterpret_cast<uint2*>(H));
   MRH_CHECK_LAUNCH();
 }
 void pr_group_hi(const uint64_t* sorted, const int64_t* seg, int64_t ngrp, int64_t* hi, hipStream_t s) {

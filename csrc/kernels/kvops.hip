@@ -184,6 +184,28 @@ __global__ __launch_bounds__(NT) void k_compact_heads(const uint32_t* __restrict
   if (i == 0) seg[pos[n]] = n;
 }
 
+// head bitmap (bit i of 64-bit word i / 64 set where a segment starts) ->
+// per-word counts, then the positions of the set bits (one word per thread)
+__global__ __launch_bounds__(NT) void k_bits_count(const uint64_t* __restrict__ H, int64_t nw,
+                                                  uint32_t* __restrict__ cnt) {
+  const int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (w < nw) cnt[w] = (uint32_t)__popcll(H[w]);
+}
+__global__ __launch_bounds__(NT) void k_bits_compact(const uint64_t* __restrict__ H, int64_t nw,
+                                                    const uint32_t* __restrict__ pos, int64_t n,
+                                                    int64_t* __restrict__ seg) {
+  const int64_t w = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (w < nw) {
+    uint64_t b = H[w];
+    int64_t o = pos[w];
+    while (b) {
+      seg[o++] = w * 64 + (__ffsll((long long)b) - 1);
+      b &= b - 1;
+    }
+  }
+  if (w == 0) seg[pos[nw]] = n;
+}
+
 // 16 lanes per pair: each group compares one non-head key with its sorted
 // predecessor (same segment, so equality along the chain = equality with the
 // head; the count is > 0 iff some segment mixes keys). The predecessor's perm
@@ -372,6 +394,15 @@ void head_flags_u64(const uint64_t* keys, int64_t n, uint32_t* flags, hipStream_
 }
 void compact_heads(const uint32_t* flags, const uint32_t* pos, int64_t n, int64_t* seg, hipStream_t s) {
   hipLaunchKernelGGL(k_compact_heads, dim3(n > 0 ? nblk(n) : 1), dim3(NT), 0, s, flags, pos, n, seg);
+  MRH_CHECK_LAUNCH();
+}
+void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s) {
+  if (nw <= 0) return;
+  hipLaunchKernelGGL(k_bits_count, dim3(nblk(nw)), dim3(NT), 0, s, H, nw, cnt);
+  MRH_CHECK_LAUNCH();
+}
+void bits_compact(const uint64_t* H, int64_t nw, const uint32_t* pos, int64_t n, int64_t* seg, hipStream_t s) {
+  hipLaunchKernelGGL(k_bits_compact, dim3(nw > 0 ? nblk(nw) : 1), dim3(NT), 0, s, H, nw, pos, n, seg);
   MRH_CHECK_LAUNCH();
 }
 void verify_groups_var(const uint8_t* kdata, const int64_t* koff, const uint32_t* perm, const uint32_t* flags,

@@ -126,6 +126,10 @@ void gather_var_copy(const uint8_t* src, const int64_t* src_off, const uint32_t*
 void head_flags_u64(const uint64_t* keys, int64_t n, uint32_t* flags, hipStream_t s);
 // head positions: seg[pos[i]] = i where flags[i]; seg[nseg] = n  (pos = exclusive scan of flags)
 void compact_heads(const uint32_t* flags, const uint32_t* pos, int64_t n, int64_t* seg, hipStream_t s);
+// head bitmap H (nw 64-bit words): cnt[w] = popcount; then seg[pos[w] + k] =
+// position of the k-th set bit of word w, seg[pos[nw]] = n
+void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s);
+void bits_compact(const uint64_t* H, int64_t nw, const uint32_t* pos, int64_t n, int64_t* seg, hipStream_t s);
 // after grouping by 64-bit hash: count elements whose key bytes differ from their group head
 void verify_groups_var(const uint8_t* kdata, const int64_t* koff, const uint32_t* perm,
                        const uint32_t* flags, const uint32_t* pos, const int64_t* seg, int64_t n,
@@ -217,6 +221,8 @@ void pr_pack_gather(const uint64_t* in, int64_t n, int P, int64_t S, const int32
                     int dbits, uint64_t* out, hipStream_t s);
 void pr_unmix_ids(const int64_t* order, int64_t n, int P, int me, int64_t N, bool mix, int64_t* ids, hipStream_t s);
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s);
+// the same with the heads as a bitmap H (ws_words(n) u32, zeroed by the caller)
+void pr_unpack_bits(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* H, hipStream_t s);
 void pr_group_hi(const uint64_t* sorted, const int64_t* seg, int64_t ngrp, int64_t* hi, hipStream_t s);
 void pr_group_vid(const int64_t* hi, int64_t ngrp, const int32_t* nid, int64_t dmask, int32_t* vid, hipStream_t s);
 // XCD source ranges: destinations per combine tile (log2); first group of
@@ -247,6 +253,8 @@ void plan_combine(int dtype, const int64_t* seg, int64_t ngrp, int64_t nrecv, co
 int64_t ws_words(int64_t nval);
 int64_t ws_waves(int64_t nval);
 void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64_t* wbase, hipStream_t s);
+// the per-wave segment bases only (H built elsewhere, e.g. pr_unpack_bits)
+void ws_bases(const int64_t* seg, int64_t nseg, int64_t nval, int64_t* wbase, hipStream_t s);
 // out[s] = OP_{e in seg s} x[src[e]] (+ w[e]); dtype/op as plan_gather_reduce;
 // scratch: ws_scratch_bytes(nval)
 size_t ws_scratch_bytes(int64_t nval);

@@ -154,6 +154,23 @@ def test_wedge_chunks_concatenate_to_wedges(dev):
 
 
 @pytest.mark.parametrize("dev", DEVS)
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 70_001])
+def test_segments_from_head_bitmap(dev, n):
+    # the PageRank plan's unpack emits segment heads as a bitmap (bit i of
+    # int32 word i / 32); its segments are the head positions + n
+    g = torch.Generator().manual_seed(n)
+    heads = torch.rand(n, generator=g) < 0.2
+    heads[0] = True
+    nw = (n + 63) // 64 * 2 + 3  # padded like the gather's index (words past n zero)
+    bits = np.zeros(nw * 32, dtype=np.uint8)
+    bits[:n] = heads.numpy()
+    words = np.packbits(bits.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").astype(np.uint32).reshape(-1)
+    H = torch.from_numpy(words.view(np.int32).copy()).to(dev)
+    seg = C.segments_from_bits(H, n).cpu().numpy()
+    assert np.array_equal(seg, np.concatenate([np.flatnonzero(heads.numpy()), [n]]))
+
+
+@pytest.mark.parametrize("dev", DEVS)
 def test_segments_sorted_vs_numpy(dev):
     k = torch.sort(torch.randint(0, 50, (3000,), dtype=torch.int64)).values
     seg = ops.segments_sorted(k.to(dev)).cpu().numpy()
