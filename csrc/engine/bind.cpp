@@ -541,6 +541,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       throw std::runtime_error("_guard_selftest_overrun: contiguous int32 HIP tensor, past in [4, 4096], multiple of 4");
     k::fill_i32(t.data_ptr<int32_t>(), t.numel() + past / 4, 7, at::hip::getCurrentHIPStream());
   });
+  m.def("radix_sort_keys", &radix_sort_keys, py::arg("keys"), py::arg("begin_bit"), py::arg("end_bit"),
+        py::arg("skip_trivial") = true);
   m.def("radix_sort_pairs", &radix_sort_pairs, py::arg("keys"), py::arg("vals"), py::arg("begin_bit"),
         py::arg("end_bit"), py::arg("skip_trivial") = true);
   m.def("hash32_keys", &hash32_keys);

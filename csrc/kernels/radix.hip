@@ -93,7 +93,7 @@ __global__ __launch_bounds__(RX_BINS) void k_digit_base(const uint32_t* __restri
   base[p * RX_BINS + t] = ex;
 }
 
-template <int RX_IT>
+template <int RX_IT, bool VALS>
 __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                    int64_t n, int shift, const uint64_t* __restrict__ dbase,
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
                                                    unsigned int* __restrict__ ticket) {
   constexpr int RX_TILE = RX_NT * RX_IT;
   __shared__ uint64_t skeys[RX_TILE];
-  __shared__ uint32_t svals[RX_TILE];
+  __shared__ uint32_t svals[VALS ? RX_TILE : 1];  // keys-only: the LDS goes to bigger tiles
   __shared__ uint32_t wcnt[RX_NW][RX_BINS];
   __shared__ uint32_t bdig[RX_BINS];
   __shared__ uint64_t gofs[RX_BINS];
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
     int64_t idx = wbase + (int64_t)j * MRH_WAVE + lane;
     bool valid = idx < n;
     kk[j] = valid ? kin[idx] : 0ull;
-    vv[j] = (valid && vin) ? vin[idx] : 0u;  // vin == nullptr: keys-only sort
+    vv[j] = (VALS && valid) ? vin[idx] : 0u;
   }
 
   // wave multi-split: rank of each pair among equal digits of its wave
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
       uint32_t d = (uint32_t)(kk[j] >> shift) & 255u;
       uint32_t pos = bdig[d] + wcnt[w][d] + lr[j];
       skeys[pos] = kk[j];
-      if (vin) svals[pos] = vv[j];
+      if (VALS) svals[pos] = vv[j];
     }
   }
   __syncthreads();
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
     uint32_t d = (uint32_t)(key >> shift) & 255u;
     uint64_t g = gofs[d] + (uint64_t)i - bdig[d];
     kout[g] = key;
-    if (vout) vout[g] = svals[i];
+    if (VALS) vout[g] = svals[i];
   }
 }
 
@@ -215,11 +215,20 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // on MI355X it beats 8 at every size (half the look-back chain, 16-key runs
 // per digit in the scatter: 5.4 M keys 90 -> 78 us/pass, 200 M keys
 // 2.74 -> 2.22 ms/pass, profiles/r2_radix_onesweep_bench.txt); MRH_RX_IT=8
-// selects 2048-pair tiles
+// selects 2048-pair tiles. Keys-only sorts have no value column in LDS and
+// take MRH_RX_KIT keys per thread (default 32: 8192-key tiles, 32-key runs)
 int rx_items() {
   static const int it = [] {
     const char* v = std::getenv("MRH_RX_IT");
     return (v && std::atoi(v) == 8) ? 8 : 16;
+  }();
+  return it;
+}
+int rx_key_items() {
+  static const int it = [] {
+    const char* v = std::getenv("MRH_RX_KIT");
+    const int k = v ? std::atoi(v) : 32;
+    return k == 8 || k == 16 || k == 24 ? k : 32;
   }();
   return it;
 }
@@ -238,7 +247,7 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
   if (n <= 0) return;
   check_arg(n <= 0xFFFFFFFFll, "radix sort: more than 2^32-1 pairs per call (the out-of-core sort splits larger inputs)");
   const int64_t nb = (n + RX_TILE - 1) / RX_TILE;  // status rows sized for the smallest tile
-  const int items = rx_items();
+  const int items = vals_in ? rx_items() : rx_key_items();
   const int64_t ntile = (n + (int64_t)RX_NT * items - 1) / ((int64_t)RX_NT * items);
   char* t = reinterpret_cast<char*>(temp);
   t = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(t) + 255) & ~uintptr_t(255));
@@ -292,12 +301,23 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
     uint64_t* ko = to_out ? keys_out : keys_alt;
     uint32_t* vo = vals_in ? (to_out ? vals_out : vals_alt) : nullptr;
     const int p = passes[q];
-    if (items == 16)
-      hipLaunchKernelGGL(k_onesweep<16>, dim3((unsigned)ntile), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, p * 8,
-                         (const uint64_t*)(dbase + p * RX_BINS), status, (uint64_t)(q + 1), tickets + q);
-    else
-      hipLaunchKernelGGL(k_onesweep<RX_IT>, dim3((unsigned)ntile), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, p * 8,
-                         (const uint64_t*)(dbase + p * RX_BINS), status, (uint64_t)(q + 1), tickets + q);
+    const uint64_t* db = dbase + p * RX_BINS;
+    const uint64_t ep = (uint64_t)(q + 1);
+#define MRH_ONESWEEP(IT, V)                                                                                   \
+  hipLaunchKernelGGL((k_onesweep<IT, V>), dim3((unsigned)ntile), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, p * 8, db, \
+                     status, ep, tickets + q)
+    if (vals_in) {
+      if (items == 16) MRH_ONESWEEP(16, true);
+      else MRH_ONESWEEP(8, true);
+    } else {
+      switch (items) {
+        case 8: MRH_ONESWEEP(8, false); break;
+        case 16: MRH_ONESWEEP(16, false); break;
+        case 24: MRH_ONESWEEP(24, false); break;
+        default: MRH_ONESWEEP(32, false); break;
+      }
+    }
+#undef MRH_ONESWEEP
     MRH_CHECK_LAUNCH();
     ki = ko;
     vi = vo;

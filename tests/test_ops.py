@@ -54,6 +54,19 @@ def test_radix_sort_pairs_is_stable(dev):
 
 
 @pytest.mark.parametrize("dev", DEVS)
+@pytest.mark.parametrize("n", [1, 8191, 8192, 300_001])
+def test_radix_sort_keys_vs_sorted(dev, n):
+    # keys-only sort (8192-key tiles on the GPU): stable on the sorted bits,
+    # the bits below ride along as payload
+    g = torch.Generator().manual_seed(n)
+    k = torch.randint(0, 1 << 62, (n,), generator=g, dtype=torch.int64)
+    k = (k & ((1 << 21) - 1)) << 32 | torch.arange(n, dtype=torch.int64)
+    got = C.radix_sort_keys(k.to(dev), 32, 53, False).cpu()
+    ref = sorted(k.tolist(), key=lambda x: x >> 32)  # Python sort is stable
+    assert got.tolist() == ref
+
+
+@pytest.mark.parametrize("dev", DEVS)
 def test_tokenize_vs_str_split(dev):
     rng = np.random.default_rng(5)
     words = ["w%d" % i for i in rng.integers(0, 500, 4000)]
