@@ -257,8 +257,10 @@ void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tens
 // all neighbour pairs per group: returns (edges [W,2] int64 (min,max), centre [W])
 namespace {
 struct WedgeScan {
-  at::Tensor wscan;  // exclusive scan of C(d,2) over the groups, ng + 1 entries
-  int64_t ng = 0, nw = 0;
+  // exclusive scan of C(d,2): over every group (ng + 1 entries) on the CPU;
+  // on the device over the groups with a wedge only (gidx, ngw + 1 entries)
+  at::Tensor wscan, gidx;
+  int64_t ng = 0, ngw = 0, nw = 0;
 };
 WedgeScan wedge_scan(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre) {
   WedgeScan w;
@@ -269,8 +271,15 @@ WedgeScan wedge_scan(const at::Tensor& seg, const at::Tensor& nb, const at::Tens
   operand(centre, at::kLong, seg.device(), "wedges centre");
   need(centre.numel() >= w.ng, "wedges: one centre per group");
   at::Tensor d = seg.narrow(0, 1, w.ng) - seg.narrow(0, 0, w.ng);
-  w.wscan = exclusive_scan(at::floor_divide(d * (d - 1), 2).contiguous());
-  w.nw = w.ng > 0 ? w.wscan[w.ng].item<int64_t>() : 0;
+  at::Tensor cnt = at::floor_divide(d * (d - 1), 2);
+  if (seg.is_cuda()) {
+    w.gidx = mask_indices(d >= 2);
+    w.ngw = w.gidx.numel();
+    cnt = cnt.index_select(0, w.gidx);
+  }
+  w.wscan = exclusive_scan(cnt.contiguous());
+  const int64_t nscan = seg.is_cuda() ? w.ngw : w.ng;
+  w.nw = nscan > 0 ? w.wscan[nscan].item<int64_t>() : 0;
   return w;
 }
 // wedges [w0, w1) of the scan
@@ -281,8 +290,8 @@ std::pair<at::Tensor, at::Tensor> wedge_range(const at::Tensor& seg, const Wedge
   at::Tensor oc = at::empty({n}, nb.options());
   if (n == 0) return {oe, oc};
   if (seg.is_cuda()) {
-    k::wedges(P0<int64_t>(seg), P0<int64_t>(ws.wscan), ws.ng, P0<int64_t>(nb), P0<int64_t>(centre), w0, n,
-              P0<int64_t>(oe), P0<int64_t>(oc), cur());
+    k::wedges(P0<int64_t>(seg), P0<int64_t>(ws.gidx), P0<int64_t>(ws.wscan), ws.ngw, P0<int64_t>(nb),
+              P0<int64_t>(centre), w0, n, P0<int64_t>(oe), P0<int64_t>(oc), cur());
     return {oe, oc};
   }
   const int64_t* sg = P0<int64_t>(seg);

@@ -556,38 +556,80 @@ __global__ __launch_bounds__(NT) void k_scatter_t(const T* __restrict__ v, const
 
 // Wedges of tri_find (reference oink/tri_find.cpp:207-276, O(d^2) per vertex):
 // for group g with neighbour list nb[seg[g]..seg[g+1]) emit every pair
-// (min, max) with value = centre key[g]. One thread per wedge: the wedge's
-// group is found by binary search over the exclusive scan of C(d,2), then the
-// pair (j, k) is decoded from the triangular index — load-balanced whatever
-// the degree skew.
-__global__ __launch_bounds__(NT) void k_wedges(const int64_t* __restrict__ seg, const int64_t* __restrict__ wscan,
-                                              int64_t ngrp, const int64_t* __restrict__ nb,
-                                              const int64_t* __restrict__ centre, int64_t w0, int64_t nwedge,
-                                              int64_t* __restrict__ out_edge, int64_t* __restrict__ out_centre) {
-  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (i >= nwedge) return;
-  const int64_t w = w0 + i;  // global wedge id; the chunk's output slot is i
-  int64_t lo = 0, hi = ngrp - 1;
+// (min, max) with value = centre key[g]. Only groups with a wedge (d >= 2)
+// take part: gidx lists them and wscan is the exclusive scan of their C(d,2).
+// One block per tile of WG_TILE consecutive wedge ids: lane 0 finds the
+// tile's first and last group by binary search in global memory, the block
+// stages their scan entries and ids in LDS (at most WG_TILE groups: each has
+// a wedge), and every wedge finds its group by a binary search in LDS — a
+// per-wedge search through global memory was latency-bound (1.2 G wedges of
+// RMAT-20: 4.2 s). The pair (j, k) comes from the triangular index;
+// thread t writes wedges t, t + NT, ... of the tile (coalesced stores).
+constexpr int WG_IT = 16;
+constexpr int WG_TILE = NT * WG_IT;
+
+__device__ __forceinline__ int64_t wg_upper(const int64_t* __restrict__ a, int64_t n, int64_t x) {
+  int64_t lo = 0, hi = n;  // first index with a[idx] > x
   while (lo < hi) {
-    int64_t mid = (lo + hi + 1) >> 1;
-    if (wscan[mid] <= w) lo = mid;
-    else hi = mid - 1;
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1;
+    else hi = mid;
   }
-  const int64_t g = lo;
-  const int64_t t = w - wscan[g];
-  const int64_t d = seg[g + 1] - seg[g];
-  // row j has (d-1-j) pairs; find j with S(j) <= t < S(j+1), S(j) = j*(2d-j-1)/2
-  double dd = (double)(2 * d - 1);
-  int64_t j = (int64_t)floor((dd - sqrt(dd * dd - 8.0 * (double)t)) * 0.5);
-  if (j < 0) j = 0;
-  while (j > 0 && j * (2 * d - j - 1) / 2 > t) --j;
-  while ((j + 1) * (2 * d - j - 2) / 2 <= t) ++j;
-  const int64_t k = j + 1 + (t - j * (2 * d - j - 1) / 2);
-  const int64_t a = nb[seg[g] + j], b = nb[seg[g] + k];
-  const bool lt = (uint64_t)a < (uint64_t)b;
-  out_edge[2 * i] = lt ? a : b;
-  out_edge[2 * i + 1] = lt ? b : a;
-  out_centre[i] = centre[g];
+  return lo;
+}
+
+__global__ __launch_bounds__(NT) void k_wedges(const int64_t* __restrict__ seg, const int64_t* __restrict__ gidx,
+                                              const int64_t* __restrict__ wscan, int64_t ngw,
+                                              const int64_t* __restrict__ nb, const int64_t* __restrict__ centre,
+                                              int64_t w0, int64_t nwedge, int64_t* __restrict__ out_edge,
+                                              int64_t* __restrict__ out_centre) {
+  __shared__ int64_t s_scan[WG_TILE + 1];
+  __shared__ int64_t s_gi[WG_TILE];
+  __shared__ int64_t s_g0;
+  __shared__ int s_n;
+  const int64_t t0 = (int64_t)blockIdx.x * WG_TILE;  // tile offset in this call's output
+  const int64_t tn = nwedge - t0 < WG_TILE ? nwedge - t0 : WG_TILE;
+  if (threadIdx.x == 0) {
+    const int64_t g0 = wg_upper(wscan, ngw, w0 + t0) - 1;
+    const int64_t g1 = wg_upper(wscan, ngw, w0 + t0 + tn - 1) - 1;
+    s_g0 = g0;
+    s_n = (int)(g1 - g0 + 1);
+  }
+  __syncthreads();
+  const int64_t g0 = s_g0;
+  const int ng = s_n;
+  for (int i = threadIdx.x; i <= ng; i += NT) {
+    s_scan[i] = wscan[g0 + i];
+    if (i < ng) s_gi[i] = gidx[g0 + i];
+  }
+  __syncthreads();
+  for (int it = 0; it < WG_IT; ++it) {
+    const int64_t o = (int64_t)it * NT + threadIdx.x;
+    if (o >= tn) break;
+    const int64_t w = w0 + t0 + o;
+    int lo = 0, hi = ng;  // last group with s_scan <= w
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (s_scan[mid] <= w) lo = mid;
+      else hi = mid;
+    }
+    const int64_t g = s_gi[lo];
+    const int64_t t = w - s_scan[lo];
+    const int64_t base = seg[g];
+    const int64_t d = seg[g + 1] - base;
+    // row j has (d-1-j) pairs; find j with S(j) <= t < S(j+1), S(j) = j*(2d-j-1)/2
+    const double dd = (double)(2 * d - 1);
+    int64_t j = (int64_t)floor((dd - sqrt(dd * dd - 8.0 * (double)t)) * 0.5);
+    if (j < 0) j = 0;
+    while (j > 0 && j * (2 * d - j - 1) / 2 > t) --j;
+    while ((j + 1) * (2 * d - j - 2) / 2 <= t) ++j;
+    const int64_t k = j + 1 + (t - j * (2 * d - j - 1) / 2);
+    const int64_t a = nb[base + j], b = nb[base + k];
+    const bool lt = (uint64_t)a < (uint64_t)b;
+    out_edge[2 * (t0 + o)] = lt ? a : b;
+    out_edge[2 * (t0 + o) + 1] = lt ? b : a;
+    out_centre[t0 + o] = centre[g];
+  }
 }
 
 }  // namespace
@@ -687,11 +729,11 @@ void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_
   }
 }
 
-void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
-            int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s) {
-  if (nwedge <= 0 || ngrp <= 0) return;
-  hipLaunchKernelGGL(k_wedges, dim3((unsigned)((nwedge + NT - 1) / NT)), dim3(NT), 0, s, seg, wscan, ngrp, nb, centre,
-                     w0, nwedge, out_edge, out_centre);
+void wedges(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
+            const int64_t* centre, int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s) {
+  if (nwedge <= 0 || ngw <= 0) return;
+  hipLaunchKernelGGL(k_wedges, dim3((unsigned)((nwedge + WG_TILE - 1) / WG_TILE)), dim3(NT), 0, s, seg, gidx, wscan,
+                     ngw, nb, centre, w0, nwedge, out_edge, out_centre);
   MRH_CHECK_LAUNCH();
 }
 

@@ -263,11 +263,12 @@ size_t ws_scratch_bytes(int64_t nval);
 void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src,
                       const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s,
                       const int32_t* sched = nullptr, int64_t slen = 0);
-// tri_find wedges: all pairs of each neighbour group
-// (wedge ids [w0, w0 + nwedge) of the exclusive scan wscan of C(d,2); output
-// slot i holds wedge w0 + i, so a huge group set is generated in bounded chunks)
-void wedges(const int64_t* seg, const int64_t* wscan, int64_t ngrp, const int64_t* nb, const int64_t* centre,
-            int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);
+// tri_find wedges: all pairs of each neighbour group with d >= 2 (gidx:
+// those groups, wscan: the exclusive scan of their C(d,2), ngw + 1 entries);
+// wedge ids [w0, w0 + nwedge), output slot i holds wedge w0 + i, so a huge
+// group set is generated in bounded chunks
+void wedges(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
+            const int64_t* centre, int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);
 
 // ---------------------------------------------------------------- pbpr.hip
 // propagation-blocked PageRank (graphplan.cpp PageRankPlan, one GPU)
