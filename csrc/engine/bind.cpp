@@ -508,6 +508,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     d["cached"] = s.cached;
     d["cross_stream_reuse"] = s.cross_stream_reuse;
     d["faulted"] = s.faulted;
+    d["grows"] = s.grows;
+    d["grow_ms"] = s.grow_ms;
+    d["releases"] = s.releases;
+    d["oom_retries"] = s.oom_retries;
     return d;
   });
   m.def("hbm_pool_reset_peak", &hbm::reset_peak);

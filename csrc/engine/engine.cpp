@@ -564,6 +564,53 @@ at::Tensor segments_sorted(const at::Tensor& sorted_keys) {
   return seg;
 }
 
+// Fixed keys of 2..8 8-byte words (edges, vertex pairs, small tuples) whose
+// words, read as unsigned integers, need <= 64 significant bits together
+// (an R-MAT-20 edge: 20 + 20) are grouped exactly on one packed u64: no
+// 64-bit hash, no verification gather of every key, and the radix sort runs
+// only over the packed bits. Returns the packed bit count (0: not narrow).
+int narrow_keys(const KV& kv, at::Tensor* keys, at::Tensor* idx) {
+  if (!kv.kfixed() || kv.kw <= 8 || kv.kw % 8 || kv.kw > 64 || kv.n == 0) return 0;
+  if (!kv.kdata.is_contiguous() || reinterpret_cast<uintptr_t>(kv.kdata.data_ptr()) % 8 ||
+      kv.kdata.numel() < kv.n * kv.kw)
+    return 0;
+  const int nw = kv.kw / 8;
+  at::Tensor words = kv.kdata.narrow(0, 0, kv.n * kv.kw).view(at::kLong).view({kv.n, nw});
+  // unsigned significance: a negative word (top bit set) needs all 64 bits
+  auto [mn, mx] = at::aminmax(words, 0);
+  at::Tensor both = at::stack({mn, mx}).to(at::kCPU);
+  const int64_t* b = P0<int64_t>(both);
+  k::PackShifts sh{};
+  sh.nw = nw;
+  int total = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int64_t lo = b[w], hi = b[nw + w];
+    const int bits = lo < 0 ? 64 : (hi == 0 ? 0 : 64 - __builtin_clzll((uint64_t)hi));
+    sh.s[w] = bits ? total : -1;
+    total += bits;
+  }
+  if (total > 64) return 0;
+  const at::Device dev = kv.device();
+  *keys = at::empty({kv.n}, opt(dev, at::kLong));
+  *idx = at::empty({kv.n}, opt(dev, at::kInt));
+  if (dev.is_cuda()) {
+    k::pack_words(reinterpret_cast<const uint64_t*>(kv.kdata.data_ptr()), kv.n, sh, P0<uint64_t>(*keys),
+                  P0<uint32_t>(*idx), cur_stream());
+  } else {
+    const uint64_t* kd = reinterpret_cast<const uint64_t*>(kv.kdata.data_ptr());
+    uint64_t* o = P0<uint64_t>(*keys);
+    uint32_t* ip = P0<uint32_t>(*idx);
+    for (int64_t i = 0; i < kv.n; ++i) {
+      uint64_t k = 0;
+      for (int w = 0; w < nw; ++w)
+        if (sh.s[w] >= 0) k |= kd[i * nw + w] << sh.s[w];
+      o[i] = k;
+      ip[i] = (uint32_t)i;
+    }
+  }
+  return std::max(total, 1);
+}
+
 KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tensor& prehash) {
   const at::Device dev = kv.device();
   KMV out;
@@ -585,6 +632,8 @@ KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tenso
   if (st->exact) {
     sk_in = raw_keys_u64(kv, 0, false, kv.kdata, kv.kw, &idx);
     end_bit = 8 * kv.kw;
+  } else if (force_hash_bits >= 64 && !prehash.defined() && (end_bit = narrow_keys(kv, &sk_in, &idx)) > 0) {
+    st->exact = true;  // wide fixed keys whose words carry <= 64 significant bits together (edges, tuples)
   } else {
     // the 64-bit grouping hash of every key, unless the producer already
     // computed it (the pipelined InvertedIndex map hashes each file's URLs

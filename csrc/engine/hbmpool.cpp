@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <set>
 #include <cstdio>
 #include <cstdlib>
@@ -52,6 +53,8 @@ struct Pending {
 struct Dev {
   hipMemPool_t pool = nullptr;
   int64_t in_use = 0, peak = 0, cap = 0, cached = 0, allocs = 0, frees = 0, failures = 0, cross = 0;
+  int64_t grows = 0, releases = 0, oom_retries = 0;
+  double grow_ms = 0;
   int64_t base_cap = 0;                   // set_cap's cap; cap = min(base_cap, active OpCaps)
   std::multiset<int64_t> op_caps;         // caps of the ops running now (any thread)
   std::map<std::pair<hipStream_t, int64_t>, std::vector<void*>> free;  // (stream, class) -> cached blocks
@@ -149,6 +152,7 @@ void reap(Dev& d) {  // g_mu held
 // every cached block back to the HIP pool (then the pool can hand the memory
 // to any stream, or trim it to the driver)
 void release_cached(Dev& d) {  // g_mu held
+  ++d.releases;
   for (Pending& q : d.pending) {
     bool ok = true;
     for (hipEvent_t e : q.evs) {
@@ -264,9 +268,14 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
     ++d.allocs;
   }
   void* p = nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream);
   if (e != hipSuccess) {
     (void)hipGetLastError();
+    {
+      std::lock_guard<std::mutex> l(g_mu);
+      ++g_dev[dev].oom_retries;
+    }
     // memory held in the caches or freed on other streams: give it all back
     // to the pool / driver and retry once
     {
@@ -287,6 +296,8 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
     if (e != hipSuccess) (void)hipGetLastError();
   }
   std::lock_guard<std::mutex> l(g_mu);
+  ++g_dev[dev].grows;
+  g_dev[dev].grow_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (e != hipSuccess || !p) {
     g_dev[dev].in_use -= bytes;
     ++g_dev[dev].failures;
@@ -386,6 +397,10 @@ PoolStats stats(int device) {
   s.cached = d.cached;
   s.cross_stream_reuse = d.cross;
   s.faulted = !d.fault.empty();
+  s.grows = d.grows;
+  s.grow_ms = d.grow_ms;
+  s.releases = d.releases;
+  s.oom_retries = d.oom_retries;
   if (d.pool) {
     uint64_t r = 0;
     if (hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemCurrent, &r) == hipSuccess) s.reserved = (int64_t)r;

@@ -46,6 +46,10 @@ struct PoolStats {
   int64_t cached = 0;              // bytes of freed blocks held in the per-(stream, class) caches
   int64_t cross_stream_reuse = 0;  // allocations served from another stream's cache behind an event
   bool faulted = false;            // an event / stream wait of the pool failed: no allocation is served
+  int64_t grows = 0;               // allocations the caches could not serve (hipMallocFromPoolAsync)
+  double grow_ms = 0;              // host time spent in those calls (a large fresh block maps pages)
+  int64_t releases = 0;            // times every cached block went back to the HIP pool
+  int64_t oom_retries = 0;         // HIP out-of-memory answers retried after a release + trim
 };
 
 // make the pool the process's device allocator; false (and no change) if the

@@ -184,6 +184,20 @@ __global__ __launch_bounds__(NT) void k_compact_heads(const uint32_t* __restrict
   if (i == 0) seg[pos[n]] = n;
 }
 
+// fixed keys of nw 8-byte words whose significant bits fit one u64 together:
+// key i -> OR of (word w << shift[w]) (an exact group key; words with no
+// significant bit have shift -1)
+__global__ __launch_bounds__(NT) void k_pack_words(const uint64_t* __restrict__ kd, int64_t n, PackShifts sh,
+                                                  uint64_t* __restrict__ out, uint32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = 0;
+  for (int w = 0; w < sh.nw; ++w)
+    if (sh.s[w] >= 0) k |= kd[i * sh.nw + w] << sh.s[w];
+  out[i] = k;
+  idx[i] = (uint32_t)i;
+}
+
 // head bitmap (bit i of 64-bit word i / 64 set where a segment starts) ->
 // per-word counts, then the positions of the set bits (one word per thread)
 __global__ __launch_bounds__(NT) void k_bits_count(const uint64_t* __restrict__ H, int64_t nw,
@@ -394,6 +408,11 @@ void head_flags_u64(const uint64_t* keys, int64_t n, uint32_t* flags, hipStream_
 }
 void compact_heads(const uint32_t* flags, const uint32_t* pos, int64_t n, int64_t* seg, hipStream_t s) {
   hipLaunchKernelGGL(k_compact_heads, dim3(n > 0 ? nblk(n) : 1), dim3(NT), 0, s, flags, pos, n, seg);
+  MRH_CHECK_LAUNCH();
+}
+void pack_words(const uint64_t* kd, int64_t n, const PackShifts& sh, uint64_t* out, uint32_t* idx, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pack_words, dim3(nblk(n)), dim3(NT), 0, s, kd, n, sh, out, idx);
   MRH_CHECK_LAUNCH();
 }
 void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s) {

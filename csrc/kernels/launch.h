@@ -126,6 +126,13 @@ void gather_var_copy(const uint8_t* src, const int64_t* src_off, const uint32_t*
 void head_flags_u64(const uint64_t* keys, int64_t n, uint32_t* flags, hipStream_t s);
 // head positions: seg[pos[i]] = i where flags[i]; seg[nseg] = n  (pos = exclusive scan of flags)
 void compact_heads(const uint32_t* flags, const uint32_t* pos, int64_t n, int64_t* seg, hipStream_t s);
+// exact narrow keys: fixed keys of nw (<= 8) 8-byte words -> out[i] = OR of
+// word w << s[w] (s[w] < 0: the word is zero in every key), idx[i] = i
+struct PackShifts {
+  int nw;
+  int s[8];
+};
+void pack_words(const uint64_t* kd, int64_t n, const PackShifts& sh, uint64_t* out, uint32_t* idx, hipStream_t s);
 // head bitmap H (nw 64-bit words): cnt[w] = popcount; then seg[pos[w] + k] =
 // position of the k-th set bit of word w, seg[pos[nw]] = n
 void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s);

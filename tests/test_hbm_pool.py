@@ -25,7 +25,7 @@ def test_pool_stats_shape_cpu():
     from gpu_mapreduce_amd.runtime import hbm_pool
     s = hbm_pool.stats(0)
     assert set(s) == {"in_use", "peak", "reserved", "reserved_peak", "cap", "allocs", "frees", "failures", "cached",
-                      "cross_stream_reuse", "faulted"}
+                      "cross_stream_reuse", "faulted", "grows", "grow_ms", "releases", "oom_retries"}
 
 
 BASIC = r'''

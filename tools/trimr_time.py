@@ -21,5 +21,8 @@ for rep in range(2):
         torch.cuda.synchronize()
     tot = sum(s["ms"] for s in r["stages"])
     print(f"rep {rep}: {tot:.1f} ms, {r['triangles']} triangles", flush=True)
+    if torch.cuda.is_available():
+        from gpu_mapreduce_amd.runtime import hbm_pool
+        print("   pool:", hbm_pool.stats(0), flush=True)
     for s in r["stages"]:
         print(f"   {s['op']:<24} {s['ms']:9.2f} ms  in {s['pairs_in']:>12}  out {s['pairs_out']:>12}", flush=True)
