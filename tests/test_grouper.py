@@ -177,4 +177,6 @@ def test_grouped_convert_gpu_fixed_wide():
     mk = lambda dev: [_fixed_part(k, v, dev) for k, v in parts]
     a = _run("cpu", mk, False)
     b = _run("cuda", mk, True)
-    assert a[2] == b[2]
+    assert a[1] == b[1]
+    # packed-word order (ordinary convert) vs hash order (incremental index)
+    assert sorted(a[2]) == sorted(b[2])
