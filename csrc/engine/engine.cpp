@@ -244,8 +244,6 @@ std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& k
   if (keys.scalar_type() != at::kLong || vals.scalar_type() != at::kInt) fail("radix_sort_pairs: keys int64, vals int32");
   if (vals.numel() != n || vals.device() != dev) fail("radix_sort_pairs: one int32 value per key, on the keys' device");
   if (begin_bit < 0 || end_bit > 64 || begin_bit > end_bit) fail("radix_sort_pairs: need 0 <= begin_bit <= end_bit <= 64");
-  begin_bit = (begin_bit / 8) * 8;
-  end_bit = std::min(64, ((end_bit + 7) / 8) * 8);
   at::Tensor ko = at::empty_like(keys), vo = at::empty_like(vals);
   int passes = 0;
   if (n == 0) return {ko, vo, 0};
@@ -270,15 +268,14 @@ std::tuple<at::Tensor, at::Tensor, int64_t> radix_sort_pairs(const at::Tensor& k
     kop[i] = k[idx[i]];
     vop[i] = v[idx[i]];
   }
-  return {ko, vo, (end_bit - begin_bit) / 8};
+  return {ko, vo, (end_bit - begin_bit + 7) / 8};
 }
 
 at::Tensor radix_sort_keys(const at::Tensor& keys_in, int begin_bit, int end_bit, bool skip_trivial) {
   at::Tensor keys = keys_in.contiguous();
   const int64_t n = keys.numel();
   if (keys.scalar_type() != at::kLong) fail("radix_sort_keys: int64 keys");
-  begin_bit = (begin_bit / 8) * 8;
-  end_bit = std::min(64, ((end_bit + 7) / 8) * 8);
+  if (begin_bit < 0 || end_bit > 64 || begin_bit > end_bit) fail("radix_sort_keys: need 0 <= begin_bit <= end_bit <= 64");
   at::Tensor ko = at::empty_like(keys);
   if (n == 0) return ko;
   if (keys.is_cuda()) {

@@ -344,18 +344,32 @@ at::Tensor route_u64(const Comm& comm, const at::Tensor& keys, const at::Tensor&
 }
 }  // namespace
 
-// out-degrees of this rank's out-edges, packed (destination << 32 | local
-// source) in any order (count_low_words: a partitioned LDS count) or — the
-// older build, MRH_PR_DEGREES=sort — (local source << 32 | destination)
-// sorted on the source bits, whose run lengths are the degrees
-at::Tensor PageRankPlan::out_degrees(const at::Tensor& packed, bool sorted_by_source) {
+// out-degrees of this rank's out-edges. packed (destination << 32 | local
+// source) in any order: by default it is sorted on the source bits above 10
+// (runs of 1024 sources contiguous: 2 passes at RMAT-26, packed is replaced
+// by the sorted array) and counted tile by tile in LDS windows — the
+// source-run order also turns the later new-id reads of the sources into
+// near-sequential ones; MRH_PR_DEGREES=partition counts the unsorted edges
+// (count_low_words: bucket scatter + LDS histograms). The older build,
+// MRH_PR_DEGREES=sort: (local source << 32 | destination) fully sorted on
+// the source bits, whose run lengths are the degrees.
+at::Tensor PageRankPlan::out_degrees(at::Tensor& packed, bool sorted_by_source) {
   const hipStream_t s = at::hip::getCurrentHIPStream();
   const int64_t ne = packed.numel();
   at::Tensor deg = at::empty({std::max<int64_t>(nlocal, 1)}, opt(dev, at::kInt));
   pr_chk(hipMemsetAsync(deg.data_ptr(), 0, deg.numel() * 4, s), "hipMemsetAsync");
   if (ne == 0) return deg;
   if (!sorted_by_source) {
-    count_low_words(packed, deg);
+    const char* e = std::getenv("MRH_PR_DEGREES");
+    if (e && std::strcmp(e, "partition") == 0) {
+      count_low_words(packed, deg);
+      return deg;
+    }
+    constexpr int kRun = 10;
+    const int sbits = pr_bits_for(std::max<int64_t>(nlocal - 1, 0));
+    if (sbits > kRun) packed = radix_sort_keys(packed, kRun, sbits, false);
+    k::pr_deg_window(reinterpret_cast<const uint64_t*>(packed.data_ptr()), ne, kRun,
+                     reinterpret_cast<uint32_t*>(deg.data_ptr()), s);
     return deg;
   }
   at::Tensor flags = at::empty({ne}, opt(dev, at::kInt));
@@ -421,9 +435,9 @@ void PageRankPlan::build_device(const at::Tensor& e) {
   const bool dist = comm->distributed();
   const int64_t nlmax = (N + P - 1) / P;
   auto bits_for = pr_bits_for;
-  // 1. out-degrees: a partitioned count over (destination << 32 | source)
-  // (MRH_PR_DEGREES=sort: sort (source << 32 | destination) on the source
-  // bits, degrees = run lengths — ~2x the time on RMAT-26)
+  // 1. out-degrees over (destination << 32 | source), su left in source-run
+  // order (out_degrees; MRH_PR_DEGREES=sort: sort (source << 32 |
+  // destination) on the source bits, degrees = run lengths)
   const bool bysort = degrees_by_sort() || dist;
   at::Tensor su, deg;
   {

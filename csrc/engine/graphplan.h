@@ -122,7 +122,7 @@ class PageRankPlan {
   void build_host(const at::Tensor& e);
   // out-degrees (partitioned count, or run lengths of a source sort) and the
   // degree relabel (both device builds); relabel returns the local dangling count
-  at::Tensor out_degrees(const at::Tensor& packed, bool sorted_by_source);
+  at::Tensor out_degrees(at::Tensor& packed, bool sorted_by_source);
   static bool degrees_by_sort();
   // sorted (group key << 32 | source) -> src_, seg_ and the head bitmap heads_
   void unpack_sorted(const at::Tensor& sorted);

@@ -61,6 +61,48 @@ __global__ __launch_bounds__(NT) void k_pr_pack_src(const int64_t* __restrict__ 
   }
 }
 
+// out-degrees from edges sorted on the source's bits above `shift` (the low
+// word is the source; runs of 2^shift sources are contiguous): one block per
+// tile of DW_TILE edges counts them in an LDS window of DW_BINS sources from
+// its first edge's run, then adds the window to deg (lane-contiguous atomics);
+// an edge past the window (a tile spanning more than DW_BINS sources, i.e.
+// average degree < 0.5 there) adds to deg directly
+constexpr int DW_TILE = 8192, DW_BINS = 16384;
+__global__ __launch_bounds__(NT) void k_pr_deg_window(const uint64_t* __restrict__ e, int64_t m, int shift,
+                                                      uint32_t* __restrict__ deg) {
+  __shared__ uint32_t h[DW_BINS];
+  const int64_t t0 = (int64_t)blockIdx.x * DW_TILE;
+  const int tn = (int)(m - t0 < DW_TILE ? m - t0 : DW_TILE);
+  const uint32_t vbase = ((uint32_t)e[t0] >> shift) << shift;
+  for (int i = threadIdx.x; i < DW_BINS; i += NT) h[i] = 0;
+  __syncthreads();
+  const int lane = dev::lane_id();
+  for (int i = threadIdx.x; i < DW_TILE; i += NT) {
+    const bool valid = i < tn;
+    const uint32_t v = valid ? (uint32_t)e[t0 + i] : 0u;
+    const uint64_t active = __ballot(valid);
+    if (!active) break;
+    // a hub's run: every lane on one source is one add (same-address LDS
+    // atomics from 64 lanes serialise)
+    const int first = __ffsll((long long)active) - 1;
+    const uint32_t v0 = (uint32_t)__shfl((int)v, first, MRH_WAVE);
+    if (__ballot(valid && v == v0) == active) {
+      if (lane == first) {
+        if (v0 - vbase < (uint32_t)DW_BINS) atomicAdd(&h[v0 - vbase], (uint32_t)__popcll(active));
+        else atomicAdd(deg + v0, (uint32_t)__popcll(active));
+      }
+    } else if (valid) {
+      if (v - vbase < (uint32_t)DW_BINS) atomicAdd(&h[v - vbase], 1u);
+      else atomicAdd(deg + v, 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < DW_BINS; i += NT) {
+    const uint32_t c = h[i];
+    if (c) atomicAdd(deg + vbase + i, c);
+  }
+}
+
 // head flag of every run of equal high words in a sorted packed array
 __global__ __launch_bounds__(NT) void k_pr_heads(const uint64_t* __restrict__ s, int64_t n,
                                                  uint32_t* __restrict__ flags) {
@@ -848,6 +890,11 @@ void pr_unmix_ids(const int64_t* order, int64_t n, int P, int me, int64_t N, boo
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_pr_unpack, dim3(pr_grid(n)), dim3(NT), 0, s, sorted, n, src, flags);
+  MRH_CHECK_LAUNCH();
+}
+void pr_deg_window(const uint64_t* e, int64_t m, int shift, uint32_t* deg, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_pr_deg_window, dim3((unsigned)((m + DW_TILE - 1) / DW_TILE)), dim3(NT), 0, s, e, m, shift, deg);
   MRH_CHECK_LAUNCH();
 }
 void pr_unpack_bits(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* H, hipStream_t s) {

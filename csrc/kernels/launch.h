@@ -228,6 +228,9 @@ void pr_pack_gather(const uint64_t* in, int64_t n, int P, int64_t S, const int32
                     int dbits, uint64_t* out, hipStream_t s);
 void pr_unmix_ids(const int64_t* order, int64_t n, int P, int me, int64_t N, bool mix, int64_t* ids, hipStream_t s);
 void pr_unpack(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* flags, hipStream_t s);
+// deg[v] += out-edges of v; e sorted on the source (low word) bits >= shift
+// (shift <= 10), deg zeroed by the caller
+void pr_deg_window(const uint64_t* e, int64_t m, int shift, uint32_t* deg, hipStream_t s);
 // the same with the heads as a bitmap H (ws_words(n) u32, zeroed by the caller)
 void pr_unpack_bits(const uint64_t* sorted, int64_t n, int32_t* src, uint32_t* H, hipStream_t s);
 void pr_group_hi(const uint64_t* sorted, const int64_t* seg, int64_t ngrp, int64_t* hi, hipStream_t s);

@@ -49,10 +49,11 @@ constexpr int RX_BINS = 256;
 constexpr uint64_t LB_COUNT = (1ull << 48) - 1;
 constexpr uint64_t LB_AGG = 1ull << 56, LB_PRE = 2ull << 56;
 
-// digit positions [p0, p1) only: positions outside the sorted bit range are
-// constant-heavy (zero high bytes) and would serialise on one LDS bin
-__global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restrict__ keys, int64_t n, int p0, int p1,
-                                                      uint32_t* __restrict__ counts /*[8][256]*/) {
+// the npos digits of the sorted bit range only (digit q at bit sh0 + 8q, the
+// last one lastbits wide): bits outside it are constant-heavy (zero high
+// bytes) and would serialise on one LDS bin
+__global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restrict__ keys, int64_t n, int sh0, int npos,
+                                                      int lastbits, uint32_t* __restrict__ counts /*[8][256]*/) {
   __shared__ uint32_t h[8][RX_BINS];
   for (int i = threadIdx.x; i < 8 * RX_BINS; i += RX_NT) (&h[0][0])[i] = 0;
   __syncthreads();
@@ -63,11 +64,11 @@ __global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restric
     const int first = __ffsll((long long)active) - 1;
 #pragma unroll
     for (int p = 0; p < 8; ++p)
-      if (p >= p0 && p < p1) {
+      if (p < npos) {
         // a digit that is the same on every active lane (the constant high
         // bytes of small ids, or runs of sorted keys) is one add of the lane
         // count: same-address LDS atomics from 64 lanes serialise
-        const uint32_t d = (uint32_t)(k >> (8 * p)) & 255u;
+        const uint32_t d = (uint32_t)(k >> (sh0 + 8 * p)) & (p == npos - 1 ? (1u << lastbits) - 1u : 255u);
         const uint32_t d0 = (uint32_t)__shfl((int)d, first, MRH_WAVE);
         if (__ballot(d == d0) == active) {
           if (lane == first) atomicAdd(&h[p][d0], (uint32_t)__popcll(active));
@@ -96,7 +97,8 @@ __global__ __launch_bounds__(RX_BINS) void k_digit_base(const uint32_t* __restri
 template <int RX_IT, bool VALS>
 __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                    uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                   int64_t n, int shift, const uint64_t* __restrict__ dbase,
+                                                   int64_t n, int shift, uint32_t dmask,
+                                                   const uint64_t* __restrict__ dbase,
                                                    unsigned long long* __restrict__ status, uint64_t epoch,
                                                    unsigned int* __restrict__ ticket) {
   constexpr int RX_TILE = RX_NT * RX_IT;
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
   for (int j = 0; j < RX_IT; ++j) {
     int64_t idx = wbase + (int64_t)j * MRH_WAVE + lane;
     bool valid = idx < n;
-    uint32_t d = (uint32_t)(kk[j] >> shift) & 255u;
+    uint32_t d = (uint32_t)(kk[j] >> shift) & dmask;
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
   for (int j = 0; j < RX_IT; ++j) {
     int64_t idx = wbase + (int64_t)j * MRH_WAVE + lane;
     if (idx < n) {
-      uint32_t d = (uint32_t)(kk[j] >> shift) & 255u;
+      uint32_t d = (uint32_t)(kk[j] >> shift) & dmask;
       uint32_t pos = bdig[d] + wcnt[w][d] + lr[j];
       skeys[pos] = kk[j];
       if (VALS) svals[pos] = vv[j];
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(RX_NT) void k_onesweep(const uint64_t* __restrict__
 
   for (int i = threadIdx.x; i < tilecount; i += RX_NT) {
     uint64_t key = skeys[i];
-    uint32_t d = (uint32_t)(key >> shift) & 255u;
+    uint32_t d = (uint32_t)(key >> shift) & dmask;
     uint64_t g = gofs[d] + (uint64_t)i - bdig[d];
     kout[g] = key;
     if (VALS) vout[g] = svals[i];
@@ -264,15 +266,19 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
   MRH_HIP(hipMemsetAsync(gcounts, 0, align256(8 * RX_BINS * 4) + 8 * sizeof(unsigned int), s));
   int ghist_blocks = (int)((n + RX_NT - 1) / RX_NT);
   if (ghist_blocks > 2048) ghist_blocks = 2048;
-  const int p0 = begin_bit / 8, p1 = std::min(8, (end_bit + 7) / 8);
-  hipLaunchKernelGGL(k_global_hist, dim3(ghist_blocks), dim3(RX_NT), 0, s, keys_in, n, p0, p1, gcounts);
+  // digits of at most 8 bits from begin_bit up (any bit offset; the last one
+  // narrower when the range is not a multiple of 8 bits)
+  const int npos = std::min(8, (end_bit - begin_bit + 7) / 8);
+  const int lastbits = end_bit - begin_bit - 8 * (npos - 1);
+  hipLaunchKernelGGL(k_global_hist, dim3(ghist_blocks), dim3(RX_NT), 0, s, keys_in, n, begin_bit, npos, lastbits,
+                     gcounts);
   MRH_CHECK_LAUNCH();
   std::vector<int> passes;
   if (skip_trivial) {  // which digit positions actually vary? (one host sync)
     std::vector<uint32_t> hc(8 * RX_BINS);
     MRH_HIP(hipMemcpyAsync(hc.data(), gcounts, 8 * RX_BINS * 4, hipMemcpyDeviceToHost, s));
     MRH_HIP(hipStreamSynchronize(s));
-    for (int p = begin_bit / 8; p * 8 < end_bit && p < 8; ++p) {
+    for (int p = 0; p < npos; ++p) {
       bool trivial = false;
       for (int b = 0; b < RX_BINS; ++b)
         if (hc[p * RX_BINS + b] == (uint32_t)n) {
@@ -282,7 +288,7 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
       if (!trivial) passes.push_back(p);
     }
   } else {
-    for (int p = begin_bit / 8; p * 8 < end_bit && p < 8; ++p) passes.push_back(p);
+    for (int p = 0; p < npos; ++p) passes.push_back(p);
   }
   const int np = (int)passes.size();
   if (passes_run) *passes_run = np;
@@ -303,9 +309,11 @@ void radix_sort_u64_u32(const uint64_t* keys_in, const uint32_t* vals_in, uint64
     const int p = passes[q];
     const uint64_t* db = dbase + p * RX_BINS;
     const uint64_t ep = (uint64_t)(q + 1);
-#define MRH_ONESWEEP(IT, V)                                                                                   \
-  hipLaunchKernelGGL((k_onesweep<IT, V>), dim3((unsigned)ntile), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, p * 8, db, \
-                     status, ep, tickets + q)
+    const int shift = begin_bit + 8 * p;
+    const uint32_t dmask = p == npos - 1 ? (1u << lastbits) - 1u : 255u;
+#define MRH_ONESWEEP(IT, V)                                                                                        \
+  hipLaunchKernelGGL((k_onesweep<IT, V>), dim3((unsigned)ntile), dim3(RX_NT), 0, s, ki, vi, ko, vo, n, shift, dmask, \
+                     db, status, ep, tickets + q)
     if (vals_in) {
       if (items == 16) MRH_ONESWEEP(16, true);
       else MRH_ONESWEEP(8, true);
