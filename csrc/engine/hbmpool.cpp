@@ -15,6 +15,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "guard.h"
@@ -55,6 +56,15 @@ struct Dev {
   int64_t in_use = 0, peak = 0, cap = 0, cached = 0, allocs = 0, frees = 0, failures = 0, cross = 0;
   int64_t grows = 0, releases = 0, oom_retries = 0;
   double grow_ms = 0;
+  // blocks of >= kBigBlock come from hipMalloc, not the HIP pool: re-growing
+  // the stream-ordered pool by tens of GB after its free memory came back in
+  // other sizes took seconds (a 30 GB concat of tri_find_mr: 4.5 s), a fresh
+  // hipMalloc of the same size ~0.1 s. They are cached like every block and
+  // hipFree'd (after a checked device sync) when the caches are released.
+  std::unordered_set<void*> big;
+  int64_t big_bytes = 0;     // held by big blocks (live + cached): part of reserved
+  int64_t big_peak = 0;
+  int64_t total_mem = 0;     // device memory (hipMemGetInfo at the first growth)
   int64_t base_cap = 0;                   // set_cap's cap; cap = min(base_cap, active OpCaps)
   std::multiset<int64_t> op_caps;         // caps of the ops running now (any thread)
   std::map<std::pair<hipStream_t, int64_t>, std::vector<void*>> free;  // (stream, class) -> cached blocks
@@ -151,8 +161,11 @@ void reap(Dev& d) {  // g_mu held
 
 // every cached block back to the HIP pool (then the pool can hand the memory
 // to any stream, or trim it to the driver)
+constexpr int64_t kBigBlock = int64_t(256) << 20;
+
 void release_cached(Dev& d) {  // g_mu held
   ++d.releases;
+  bool synced = false;
   for (Pending& q : d.pending) {
     bool ok = true;
     for (hipEvent_t e : q.evs) {
@@ -170,7 +183,24 @@ void release_cached(Dev& d) {  // g_mu held
   }
   d.pending.clear();
   for (auto& [k, v] : d.free)
-    for (void* p : v)
+    for (void* p : v) {
+      if (d.big.count(p)) {
+        // hipMalloc'd: free once the device has drained (its last users were
+        // stream-ordered before the free that cached it)
+        if (!synced) {
+          const hipError_t r = hipDeviceSynchronize();
+          if (r != hipSuccess) {
+            (void)hipGetLastError();
+            set_fault(d, std::string("device fault while releasing cached blocks: ") + hipGetErrorString(r));
+            return;
+          }
+          synced = true;
+        }
+        if (hipFree(p) != hipSuccess) (void)hipGetLastError();
+        d.big.erase(p);
+        d.big_bytes -= k.second;
+        continue;
+      }
       if (hipFreeAsync(p, k.first) != hipSuccess) {
         (void)hipGetLastError();
         const hipError_t r = hipDeviceSynchronize();
@@ -181,6 +211,7 @@ void release_cached(Dev& d) {  // g_mu held
         }
         (void)hipFreeAsync(p, nullptr);
       }
+    }
   d.free.clear();
   d.streams.clear();
   d.cached = 0;
@@ -259,9 +290,19 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
       g_blocks[p] = Block{bytes, dev, stream, {}};
       return p;
     }
-    // much idle memory cached in other classes: hand it back to the HIP pool
-    // before growing it (the pool reuses freed memory across streams)
-    if (d.cached > (int64_t(1) << 30) && d.cached > d.in_use / 4) release_cached(d);
+    // much idle memory cached in other classes and the device filling up:
+    // hand it back before growing (the HIP pool reuses freed memory across
+    // streams and sizes; big blocks go back to the driver)
+    if (d.total_mem == 0) {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) == hipSuccess) d.total_mem = (int64_t)tot;
+      else (void)hipGetLastError();
+    }
+    const int64_t held = d.in_use + d.cached;
+    if (d.cached > (int64_t(1) << 30) && d.cached > d.in_use / 4 &&
+        (d.total_mem == 0 || held + bytes > d.total_mem / 10 * 7))
+      release_cached(d);
+    if (!d.fault.empty()) TORCH_CHECK(false, "mrhip page pool: device ", dev, " faulted: ", d.fault);
     pool = pool_of(dev);
     d.in_use += bytes;  // reserved before the call so concurrent allocations see it
     d.peak = std::max(d.peak, d.in_use);
@@ -269,7 +310,11 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
   }
   void* p = nullptr;
   const auto t0 = std::chrono::steady_clock::now();
-  hipError_t e = hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream);
+  const bool is_big = bytes >= kBigBlock;
+  auto grow = [&] {
+    return is_big ? hipMalloc(&p, (size_t)bytes) : hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream);
+  };
+  hipError_t e = grow();
   if (e != hipSuccess) {
     (void)hipGetLastError();
     {
@@ -292,7 +337,7 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
                   mib(bytes), ": ", hipGetErrorString(se));
     }
     (void)hipMemPoolTrimTo(pool, 0);
-    e = hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream);
+    e = grow();
     if (e != hipSuccess) (void)hipGetLastError();
   }
   std::lock_guard<std::mutex> l(g_mu);
@@ -303,6 +348,11 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
     ++g_dev[dev].failures;
     TORCH_CHECK_WITH(OutOfMemoryError, false, "mrhip page pool: HIP out of memory allocating ", mib(bytes),
                      " on device ", dev, " (", mib(g_dev[dev].in_use), " in use): ", hipGetErrorString(e));
+  }
+  if (is_big) {
+    g_dev[dev].big.insert(p);
+    g_dev[dev].big_bytes += bytes;
+    g_dev[dev].big_peak = std::max(g_dev[dev].big_peak, g_dev[dev].big_bytes);
   }
   g_blocks[p] = Block{bytes, dev, stream, {}};
   return p;
@@ -406,6 +456,8 @@ PoolStats stats(int device) {
     if (hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemCurrent, &r) == hipSuccess) s.reserved = (int64_t)r;
     if (hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemHigh, &r) == hipSuccess) s.reserved_peak = (int64_t)r;
   }
+  s.reserved += d.big_bytes;
+  s.reserved_peak += d.big_peak;  // an upper bound: the two hi-water marks need not coincide
   return s;
 }
 
