@@ -464,6 +464,7 @@ void PageRankPlan::build_device(const at::Tensor& e) {
   std::vector<int64_t> rb, redge;  // hot range boundaries (new ids) and their first edges
   if (degn.defined() && nactive > 0) xcd_ranges(degn, nactive, dbits, rb, redge);
   degn = at::Tensor();
+  clk("xcd ranges");
   const int nhot = rb.empty() ? 0 : (int)rb.size() - 1;
   at::Tensor rbd;
   if (nhot > 0) {
@@ -479,7 +480,7 @@ void PageRankPlan::build_device(const at::Tensor& e) {
     k::pr_pack(reinterpret_cast<const uint64_t*>(su.data_ptr()), nedge, P, nlmax, !dist, !bysort, nid.data_ptr<int32_t>(),
                nhot > 0 ? rbd.data_ptr<int32_t>() : nullptr, nhot, dbits, reinterpret_cast<uint64_t*>(packed.data_ptr()),
                s);
-    clk("xcd ranges + pack");
+    clk("pack");
     su = at::Tensor();
     sorted = radix_sort_keys(packed, 32, 32 + dbits + rbits, false);
   }
