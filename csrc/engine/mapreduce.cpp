@@ -383,6 +383,25 @@ OocEnv MapReduce::ooc_env() const {
 // an addflag map never concatenates past the budgets
 KV MapReduce::append_kv(const KV& a, const KV& b) {
   if (budget() <= 0 && set.host_budget <= 0) return concat({a, b}, device());
+  if (!a.device().is_cuda() && device().is_cuda()) {
+    // a is already out of core (pinned host or a spool file): the result is
+    // written once where it fits — not spooled piece by piece and gathered
+    // into a second copy
+    const int64_t total = a.nbytes() + b.nbytes();
+    if (set.host_budget <= 0 || total <= set.host_budget) {
+      KV o = concat({a, b}, at::Device(at::kCPU));
+      auto pin = [](const at::Tensor& t) { return t.defined() && !t.is_pinned() ? t.pin_memory() : t; };
+      o.kdata = pin(o.kdata);
+      o.vdata = pin(o.vdata);
+      o.koff = pin(o.koff);
+      o.voff = pin(o.voff);
+      spool_stats.host_bytes += total;
+      return o;
+    }
+    spool_stats.files++;
+    spool_stats.disk_bytes += total;
+    return kv_to_file({a, b}, spool_path(set.fpath, "kv", instance_me_, comm_->rank()));
+  }
   KeyValue tmp(device());
   bound(tmp);
   tmp.add_kv(a);
