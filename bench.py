@@ -504,6 +504,8 @@ def bench_dist_plans(comm, args):
     the multi-GPU plans on a forced one-rank RCCL communicator (the paths the
     8-GPU BASELINE configs run), reported next to the local-path numbers"""
     out = {}
+    if comm.is_cuda:
+        torch.cuda.empty_cache()  # the previous extras' cached blocks back to the driver first
     fc = _forced_rccl_comm(comm)
     try:
         try:
