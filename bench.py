@@ -374,7 +374,7 @@ def bench_pagerank_extra(comm, args):
                             "rank_dtype": "fp32 ranks, fp64 L1/dangling reductions"},
     }
     del pr
-    if comm.is_cuda:
+    if comm.is_cuda and os.environ.get("MRH_BENCH_KEEP_CACHE") != "1":  # diagnostics: keep the pool's caches
         torch.cuda.empty_cache()
     return out
 
