@@ -373,9 +373,10 @@ def bench_pagerank_extra(comm, args):
                             "runs_timed": args.pagerank_steps, "alpha": 0.85, "scaling": "strong",
                             "rank_dtype": "fp32 ranks, fp64 L1/dangling reductions"},
     }
+    # the pool keeps its caches (it releases them itself when the device fills
+    # up): trimming 45 GB here and regrowing made the next job 7 ms slower per
+    # step (with_file_io 21.3 -> 28.5 ms, the same with the ATen allocator)
     del pr
-    if comm.is_cuda and os.environ.get("MRH_BENCH_KEEP_CACHE") != "1":  # diagnostics: keep the pool's caches
-        torch.cuda.empty_cache()
     return out
 
 
@@ -392,9 +393,6 @@ def _extra(comm, prefix, fn, args, **over):
     except Exception as e:  # noqa: BLE001
         print(f"bench.py rank {comm.rank}: {prefix} extra failed: {e}", file=sys.stderr, flush=True)
         return {f"{prefix}_error": f"{type(e).__name__}: {e}"[:500]}
-    finally:
-        if comm.is_cuda:
-            torch.cuda.empty_cache()
     out = {f"{prefix}_kvps": r["value"], f"{prefix}_ms": r["ms_per_step"], f"{prefix}_setup_ms": r.get("setup_ms"),
            f"{prefix}_config": dict(r["config"], steps=a.steps, warmup=a.warmup, scaling=r.get("scaling", "weak"),
                                     metric=r["metric"])}
@@ -504,8 +502,6 @@ def bench_dist_plans(comm, args):
     the multi-GPU plans on a forced one-rank RCCL communicator (the paths the
     8-GPU BASELINE configs run), reported next to the local-path numbers"""
     out = {}
-    if comm.is_cuda:
-        torch.cuda.empty_cache()  # the previous extras' cached blocks back to the driver first
     fc = _forced_rccl_comm(comm)
     try:
         try:
@@ -526,8 +522,6 @@ def bench_dist_plans(comm, args):
                                   "exchange, column all-gather)")
     finally:
         del fc
-        if comm.is_cuda:
-            torch.cuda.empty_cache()
     return out
 
 
