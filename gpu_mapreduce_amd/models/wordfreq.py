@@ -206,8 +206,6 @@ def bench_wordfreq(comm, args):
             chunks.append(t.cpu().pin_memory() if comm.is_cuda else t)
         left -= n
         i += 1
-    if comm.is_cuda:
-        torch.cuda.empty_cache()
     setup = comm.allreduce(time.perf_counter() - ts, "max", dtype=torch.float64)
 
     def steps(k, pipelined):
