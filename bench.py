@@ -516,7 +516,9 @@ def bench_dist_plans(comm, args):
         out["dist_plans_note"] = ("MRH_FORCE_RCCL=1 one-rank RCCL communicator: the PageRank plan of several GPUs "
                                   "(destination-owned edges, all-gathered c, per-iteration allreduce + all-gather) "
                                   "and the tri_find split build (key-range exchange, allreduced degrees, row-range "
-                                  "exchange, column all-gather)")
+                                  "exchange, column all-gather); at one rank the all-gathers, allreduces and broadcasts "
+                                  "of device tensors are the identity (no collective kernel), the exchanges go through "
+                                  "RCCL send/recv")
     finally:
         del fc
     return out

@@ -374,6 +374,10 @@ void Comm::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& rec
 
 void Comm::allgather_bytes(const void* send, void* recv, int64_t bytes) const {
   trace_coll(rank_, "allgather", bytes, 0);
+  if (size_ == 1) {  // one rank (the forced-RCCL mode): the identity, no collective kernel
+    if (send != recv) copy_bytes(recv, send, bytes, dev_);
+    return;
+  }
   if (rccl_) {
     rccl_->allgather(send, recv, (size_t)bytes, cur(dev_));
     return;
@@ -450,7 +454,7 @@ at::Tensor Comm::allgather_var(const at::Tensor& in) const {
 }
 
 void Comm::allreduce_tensor(at::Tensor& t, Op op) const {
-  if (!distributed()) return;
+  if (!distributed() || size_ == 1) return;
   trace_coll(rank_, "allreduce_tensor", t.numel(), op);
   if (rccl_) {
     if (!t.is_contiguous()) t = t.contiguous();
@@ -461,7 +465,7 @@ void Comm::allreduce_tensor(at::Tensor& t, Op op) const {
 }
 
 void Comm::broadcast_tensor(at::Tensor& t, int root) const {
-  if (!distributed()) return;
+  if (!distributed() || size_ == 1) return;
   trace_coll(rank_, "broadcast", t.numel(), root);
   if (rccl_) {
     if (!t.is_contiguous()) t = t.contiguous();
