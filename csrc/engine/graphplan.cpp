@@ -482,7 +482,12 @@ void PageRankPlan::build_device(const at::Tensor& e) {
                s);
     clk("pack");
     su = at::Tensor();
-    sorted = radix_sort_keys(packed, 32, 32 + dbits + rbits, false);
+    // MRH_PR_SRC_ORDER=1: the sources of every group in ascending new id too
+    // (the sort also runs over the low word: 4 more passes at RMAT-26) — an
+    // experiment on the gather's request rate
+    const char* so = std::getenv("MRH_PR_SRC_ORDER");
+    const int lo_bit = so && *so == '1' ? 0 : 32;
+    sorted = radix_sort_keys(packed, lo_bit, 32 + dbits + rbits, false);
   }
   clk("sort by destination");
   // 4. unpack
