@@ -487,8 +487,14 @@ void trim(int device, int64_t keep_bytes) {
   }
   if (!p) return;
   // freed blocks are returned to the pool in stream order: let the device
-  // drain so the trim sees them
-  (void)hipDeviceSynchronize();
+  // drain so the trim sees them; a device fault here is the pool's too
+  const hipError_t r = hipDeviceSynchronize();
+  if (r != hipSuccess) {
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> l(g_mu);
+    set_fault(g_dev[device], std::string("device fault seen by trim: ") + hipGetErrorString(r));
+    return;
+  }
   if (hipMemPoolTrimTo(p, (size_t)std::max<int64_t>(0, keep_bytes)) != hipSuccess) (void)hipGetLastError();
 }
 
