@@ -43,6 +43,11 @@ def test_bench_spawns_n_ranks():
         assert k in three, k
     assert three["trifind_triangles"] == one["trifind_triangles"] > 0   # strong scaling: same graph
     assert three["wordfreq_words"] == 3 * one["wordfreq_words"]          # weak scaling: text per rank
+    # every extra ran (a failing extra is recorded as <name>_error, not fatal)
+    for rec in (one, three):
+        assert not [k for k in rec if k.endswith("_error")], [k for k in rec if k.endswith("_error")]
+        assert rec["trifind_mr_triangles"] == rec["trifind_mr_triangles_check"] > 0
+        assert "ms_per_step" in rec["with_file_io"] and "ms_per_step" in rec["wordfreq_with_file_io"]
 
 
 def test_bench_eight_ranks():

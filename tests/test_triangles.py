@@ -278,3 +278,30 @@ def test_tri_find_mr_pipeline_in_memory_and_out_of_core(dev, tmp_path):
                      fpath=str(tmp_path), memsize=-65536)
     assert r2["triangles"] == want
     assert r2["spool_host_bytes"] > 0
+
+
+def case_tri_mr_ooc(comm):
+    """every rank maps its share of one R-MAT edge list; tri_find_mr in
+    memory and under HBM / host budgets (spooled shuffles, collates and
+    reduces at every rank, collective out-of-core decisions)"""
+    import tempfile
+    from gpu_mapreduce_amd.models.triangles import tri_find_mr
+    e = _rmat(9, 8, 7)
+    P, me = comm.size, comm.rank
+    mine = e[me * e.shape[0] // P:(me + 1) * e.shape[0] // P]
+    r = tri_find_mr(comm, mine)
+    wedges = comm.allreduce(next(s["pairs_out"] for s in r["stages"] if s["op"] == "reduce nsq_angles"), "max")
+    d = tempfile.mkdtemp(prefix=f"trimr_ooc{me}_")
+    r2 = tri_find_mr(comm, mine, hbm_budget=max(4096, wedges * 24 // 50), host_budget=wedges * 24 // 16, fpath=d,
+                     memsize=-65536)
+    return r["triangles"], r2["triangles"], r2["spool_host_bytes"] + r2["spool_disk_bytes"], brute_force_count(e.numpy())
+
+
+def test_tri_find_mr_out_of_core_three_ranks():
+    """3 gloo ranks: the 4-collate pipeline gives the brute-force count in
+    memory and out of core (no rank waits on a collective another skipped)"""
+    from test_distributed_cpu import run_world
+    out = run_world("test_triangles:case_tri_mr_ooc", 3)
+    for a, b, spooled, want in out.values():
+        assert a == b == want
+    assert sum(v[2] for v in out.values()) > 0
