@@ -1105,6 +1105,14 @@ at::Tensor lookup(const at::Tensor& keys, const at::Tensor& q) {
   return out;
 }
 
+// the triangle builds rank vertices by their degree counted over the raw
+// edges, duplicates included (MRH_TRI_ONESORT=0: over the unique edges, the
+// older two-sort one-rank build)
+bool tri_raw_degrees() {
+  const char* e = std::getenv("MRH_TRI_ONESORT");
+  return !(e && *e == '0');
+}
+
 // sorted unique values of an int64 column
 at::Tensor unique_sorted(const at::Tensor& x) {
   if (x.numel() == 0) return x.contiguous();
@@ -1194,14 +1202,43 @@ TriangleGraph::TriangleGraph(CommPtr c, const at::Tensor& edges, int64_t nv) : c
   stage("pack");
   distributed = false;
   if (comm->distributed()) p = comm->allgather_var(p);
-  at::Tensor uniq = unique_sorted(p);
-  stage("dedup");
-  p = at::Tensor();
-  if (uniq.numel() > 0 && uniq[0].item<int64_t>() == 0) uniq = uniq.narrow(0, 1, uniq.numel() - 1);  // (0, 0): self loops
-  stage("drop self loops");
-  nedge = uniq.numel();
-  std::tie(rowptr, col, okeys, perm) = tri_prepare(uniq, std::max<int64_t>(nvert, 1));
-  stage("CSR");
+  if (tri_raw_degrees()) {
+    // one sort instead of two: rank the vertices by their degree counted with
+    // the duplicate edges (any total order orients correctly; duplicates only
+    // nudge the order), orient the raw edges, sort once and drop the
+    // duplicates and self loops (packed (0, 0) -> equal halves) afterwards —
+    // the dedup sort of the raw edges before the orientation sort is gone
+    at::Tensor deg = tri_degrees(p, std::max<int64_t>(nvert, 1));
+    auto [rank, pm] = tri_rank_perm(deg);
+    deg = at::Tensor();
+    at::Tensor o = tri_orient_keys(p, rank);
+    p = at::Tensor();
+    rank = at::Tensor();
+    at::Tensor srt = o.numel() ? radix_sort_keys(o, 0, 64) : o;
+    o = at::Tensor();
+    stage("orient + sort");
+    const int64_t n = srt.numel();
+    if (n > 0) {
+      at::Tensor keep = at::ne(at::bitwise_right_shift(srt, 32), at::bitwise_and(srt, (int64_t)0xffffffff));
+      if (n > 1) keep.narrow(0, 1, n - 1).logical_and_(at::ne(srt.narrow(0, 1, n - 1), srt.narrow(0, 0, n - 1)));
+      srt = srt.index_select(0, mask_indices(keep)).contiguous();
+    }
+    okeys = srt;
+    nedge = okeys.numel();
+    rowptr = tri_rowptr_of(okeys, std::max<int64_t>(nvert, 1));
+    col = tri_col_of(okeys);
+    perm = pm;
+    stage("CSR");
+  } else {
+    at::Tensor uniq = unique_sorted(p);
+    stage("dedup");
+    p = at::Tensor();
+    if (uniq.numel() > 0 && uniq[0].item<int64_t>() == 0) uniq = uniq.narrow(0, 1, uniq.numel() - 1);  // (0, 0): self loops
+    stage("drop self loops");
+    nedge = uniq.numel();
+    std::tie(rowptr, col, okeys, perm) = tri_prepare(uniq, std::max<int64_t>(nvert, 1));
+    stage("CSR");
+  }
   const int64_t m = okeys.numel(), P = comm->size(), me = comm->rank();
   e0 = 0;
   e1 = m;
@@ -1260,6 +1297,11 @@ void TriangleGraph::build_split(const at::Tensor& p_in) {
   split = true;
   distributed = false;
   at::Tensor p = p_in.contiguous();
+  const int64_t nv = std::max<int64_t>(nvert, 1);
+  // the degree order: counted over the raw edges, duplicates included, like
+  // the one-rank build (tri_raw_degrees), so both orient and count alike
+  at::Tensor deg;
+  if (tri_raw_degrees()) deg = tri_degrees(p, nv);
   // 1. key-range owners from NS strided samples per rank
   {
     constexpr int64_t NS = 4096;
@@ -1279,12 +1321,12 @@ void TriangleGraph::build_split(const at::Tensor& p_in) {
   if (uniq.numel() > 0 && uniq[0].item<int64_t>() == 0) uniq = uniq.narrow(0, 1, uniq.numel() - 1);  // self loops
   nedge = cm.allreduce(uniq.numel(), Comm::SUM);
   // 2. global degrees -> ranks
-  const int64_t nv = std::max<int64_t>(nvert, 1);
   at::Tensor rank;
   {
-    at::Tensor deg = tri_degrees(uniq, nv);
+    if (!deg.defined()) deg = tri_degrees(uniq, nv);
     cm.allreduce_tensor(deg, Comm::SUM);
     std::tie(rank, perm) = tri_rank_perm(deg);
+    deg = at::Tensor();
   }
   // 3. oriented + sorted locally; d+ allreduced -> rowptr, row split
   at::Tensor os = tri_orient_keys(uniq, rank);
