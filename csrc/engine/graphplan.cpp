@@ -1105,12 +1105,15 @@ at::Tensor lookup(const at::Tensor& keys, const at::Tensor& q) {
   return out;
 }
 
-// the triangle builds rank vertices by their degree counted over the raw
-// edges, duplicates included (MRH_TRI_ONESORT=0: over the unique edges, the
-// older two-sort one-rank build)
+// MRH_TRI_ONESORT=1: rank vertices by their degree counted over the raw
+// edges, duplicates included, so the one-rank build sorts once (orient, sort,
+// then drop duplicates) instead of twice. Measured slower on RMAT-24: 157.9
+// vs 124.2 ms per step — the duplicate-inflated order makes the hub rows'
+// counting costlier than the saved sort (profiles/r4_trifind_onesort.txt);
+// the default ranks by the unique edges' degrees
 bool tri_raw_degrees() {
   const char* e = std::getenv("MRH_TRI_ONESORT");
-  return !(e && *e == '0');
+  return e && *e == '1';
 }
 
 // sorted unique values of an int64 column
