@@ -56,5 +56,7 @@ at::Tensor trimr_second_degree(const KMV& m);
 std::pair<at::Tensor, at::Tensor> trimr_low_degree(const KV& kv);
 // edge -> {wedge centres (8 B), edge marker (0 B)}: closed triangles
 // (centre, e0, e1) as [T,3] int64
+// the edge marker of fixed 8-byte values in tri_find_mr's last collate
+constexpr int64_t kTriEdgeMark = -1;
 at::Tensor trimr_emit(const KMV& m);
 }  // namespace mrh

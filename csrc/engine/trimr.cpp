@@ -97,18 +97,21 @@ std::pair<at::Tensor, at::Tensor> trimr_low_degree(const KV& kv) {
   return {key, val};
 }
 
+// Edge markers: an empty value (the reference's NULL) or, with fixed 8-byte
+// values, kTriEdgeMark — the pipeline marks its edges that way so that the
+// last collate moves one fixed-width value column (no per-pair offsets)
 at::Tensor trimr_emit(const KMV& m) {
   const at::Device dev = m.seg.device();
-  // one value width for the whole KMV: only markers or only centres, so no
-  // segment can close a wedge
-  if (!m.nkey || m.vw >= 0) return at::empty({0, 3}, opt(dev, at::kLong));
+  // fixed widths other than 8: only markers (0) or no marker at all
+  if (!m.nkey || (m.vw >= 0 && m.vw != 8)) return at::empty({0, 3}, opt(dev, at::kLong));
   need(m.keys.kw == 16, "tri_find_mr emit: EDGE keys");
+  const bool fixed = m.vw == 8;
   const int64_t* seg = P0<int64_t>(m.seg);
-  const int64_t* voff = P0<int64_t>(m.voff);
+  const int64_t* voff = fixed ? nullptr : P0<int64_t>(m.voff);
   const int64_t* ek = P0<int64_t>(m.keys.kdata);
   if (dev.is_cuda()) {
     at::Tensor cnt = at::empty({m.nkey}, opt(dev, at::kLong));
-    k::trimr_emit_count(seg, m.nkey, voff, P0<int64_t>(cnt), cur());
+    k::trimr_emit_count(seg, m.nkey, voff, fixed ? P0<int64_t>(m.vdata) : nullptr, P0<int64_t>(cnt), cur());
     at::Tensor pos = exclusive_scan(cnt);
     const int64_t T = pos[m.nkey].item<int64_t>();
     at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
@@ -117,16 +120,22 @@ at::Tensor trimr_emit(const KMV& m) {
   }
   const uint8_t* vd = P0<uint8_t>(m.vdata);
   std::vector<int64_t> rows;
+  auto value = [&](int64_t j, int64_t* c) {  // false: the edge marker
+    if (fixed) {
+      std::memcpy(c, vd + 8 * j, 8);
+      return *c != kTriEdgeMark;
+    }
+    if (voff[j + 1] - voff[j] != 8) return false;
+    std::memcpy(c, vd + voff[j], 8);
+    return true;
+  };
   for (int64_t s = 0; s < m.nkey; ++s) {
     bool marker = false;
-    for (int64_t j = seg[s]; j < seg[s + 1]; ++j) marker |= voff[j + 1] == voff[j];
+    int64_t c;
+    for (int64_t j = seg[s]; j < seg[s + 1]; ++j) marker |= !value(j, &c);
     if (!marker) continue;
-    for (int64_t j = seg[s]; j < seg[s + 1]; ++j) {
-      if (voff[j + 1] - voff[j] != 8) continue;
-      int64_t c;
-      std::memcpy(&c, vd + voff[j], 8);
-      rows.insert(rows.end(), {c, ek[2 * s], ek[2 * s + 1]});
-    }
+    for (int64_t j = seg[s]; j < seg[s + 1]; ++j)
+      if (value(j, &c)) rows.insert(rows.end(), {c, ek[2 * s], ek[2 * s + 1]});
   }
   return at::tensor(rows, opt(at::kCPU, at::kLong)).view({-1, 3});
 }

@@ -373,7 +373,10 @@ void trimr_second_degree(const int64_t* seg, int64_t nkey, const int32_t* v, int
                          hipStream_t s);
 void trimr_low_degree(const int64_t* e, const int32_t* dg, int64_t n, int64_t* key, int64_t* val, hipStream_t s);
 // cnt[s] = wedge centres of edge segment s if it holds the edge marker, else 0
-void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, int64_t* cnt, hipStream_t s);
+// (voff: variable-width values, the marker is empty; voff null: fixed 8-byte
+// values vals, the marker is -1)
+void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, const int64_t* vals, int64_t* cnt,
+                      hipStream_t s);
 // rows (centre, e0, e1) at pos[s].. (pos = exclusive scan of cnt)
 void trimr_emit_write(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vdata,
                       const int64_t* ekey, const int64_t* pos, int64_t* out, hipStream_t s);

@@ -76,12 +76,22 @@ __global__ __launch_bounds__(NT) void k_low_degree(const int64_t* __restrict__ e
   }
 }
 
+// the wedge centres of the EDGE keys that are also edges: a marker value is
+// either empty (voff given: variable-width values) or -1 (voff null: fixed
+// 8-byte values, vals)
 __global__ __launch_bounds__(NT) void k_emit_count(const int64_t* __restrict__ seg, int64_t nkey,
-                                                  const int64_t* __restrict__ voff, int64_t* __restrict__ cnt) {
+                                                  const int64_t* __restrict__ voff, const int64_t* __restrict__ vals,
+                                                  int64_t* __restrict__ cnt) {
   for (int64_t s = (int64_t)blockIdx.x * NT + threadIdx.x; s < nkey; s += (int64_t)gridDim.x * NT) {
     int64_t c = 0;
     bool marker = false;
     for (int64_t j = seg[s]; j < seg[s + 1]; ++j) {
+      if (!voff) {  // fixed 8-byte values: the edge marker is the value -1
+        const bool m = vals[j] == -1;
+        marker |= m;
+        c += !m;
+        continue;
+      }
       const int64_t l = voff[j + 1] - voff[j];
       marker |= l == 0;
       c += l == 8;
@@ -99,10 +109,15 @@ __global__ __launch_bounds__(NT) void k_emit_write(const int64_t* __restrict__ s
     if (pos[s + 1] == o) continue;
     const int64_t e0 = ekey[2 * s], e1 = ekey[2 * s + 1];
     for (int64_t j = seg[s]; j < seg[s + 1]; ++j) {
-      const int64_t b = voff[j];
-      if (voff[j + 1] - b != 8) continue;
       int64_t c;
-      __builtin_memcpy(&c, vdata + b, 8);
+      if (!voff) {
+        c = reinterpret_cast<const int64_t*>(vdata)[j];
+        if (c == -1) continue;
+      } else {
+        const int64_t b = voff[j];
+        if (voff[j + 1] - b != 8) continue;
+        __builtin_memcpy(&c, vdata + b, 8);
+      }
       out[3 * o] = c;
       out[3 * o + 1] = e0;
       out[3 * o + 2] = e1;
@@ -134,9 +149,10 @@ void trimr_low_degree(const int64_t* e, const int32_t* dg, int64_t n, int64_t* k
   MRH_CHECK_LAUNCH();
 }
 
-void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, int64_t* cnt, hipStream_t s) {
+void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, const int64_t* vals, int64_t* cnt,
+                      hipStream_t s) {
   if (nkey <= 0) return;
-  hipLaunchKernelGGL(k_emit_count, dim3(blocks(nkey)), dim3(NT), 0, s, seg, nkey, voff, cnt);
+  hipLaunchKernelGGL(k_emit_count, dim3(blocks(nkey)), dim3(NT), 0, s, seg, nkey, voff, vals, cnt);
   MRH_CHECK_LAUNCH();
 }
 

@@ -74,7 +74,14 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
                            [&](const at::Tensor& e, const at::Tensor& c) { add_tensors(kv, e, c); });
     });
   });
-  stage("add edges", mrt, [&] { mrt.add(mre); });
+  stage("add edges", mrt, [&] {
+    // the edges carry the marker kTriEdgeMark (not an empty value), so the
+    // pairs of collate 4 all have one 8-byte value (fixed-width gathers)
+    mre.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {
+      if (src.n) add_tensors(kv, edges_of(src), at::full({src.n}, kTriEdgeMark, src.kdata.options().dtype(at::kLong)));
+    });
+    mrt.add(mre);
+  });
   stage("collate 4", mrt, [&] { mrt.collate(); });
   stage("reduce emit_triangles", mrt, [&] {
     run.triangles = mrt.reduce_batch([](const KMV& m, KeyValue& kv) {
