@@ -109,6 +109,23 @@ at::Tensor trimr_emit(const KMV& m) {
   const int64_t* seg = P0<int64_t>(m.seg);
   const int64_t* voff = fixed ? nullptr : P0<int64_t>(m.voff);
   const int64_t* ek = P0<int64_t>(m.keys.kdata);
+  if (dev.is_cuda() && fixed) {
+    const int64_t nval = m.nval;
+    const int64_t* vals = P0<int64_t>(m.vdata);
+    at::Tensor marked = at::zeros({m.nkey}, opt(dev, at::kByte));
+    const int64_t nt = k::trimr_emit_tiles(nval);
+    at::Tensor tcount = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kLong));
+    k::trimr_emit_fixed(0, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, nullptr, ek, nullptr, cur());
+    k::trimr_emit_fixed(1, seg, m.nkey, nval, vals, P0<uint8_t>(marked), P0<int64_t>(tcount), nullptr, ek, nullptr,
+                        cur());
+    at::Tensor tbase = exclusive_scan(tcount.narrow(0, 0, nt).contiguous());
+    const int64_t T = nt > 0 ? tbase[nt].item<int64_t>() : 0;
+    at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
+    if (T)
+      k::trimr_emit_fixed(2, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, P0<int64_t>(tbase), ek,
+                          P0<int64_t>(out), cur());
+    return out;
+  }
   if (dev.is_cuda()) {
     at::Tensor cnt = at::empty({m.nkey}, opt(dev, at::kLong));
     k::trimr_emit_count(seg, m.nkey, voff, fixed ? P0<int64_t>(m.vdata) : nullptr, P0<int64_t>(cnt), cur());

@@ -372,6 +372,13 @@ void trimr_first_degree(const int64_t* seg, int64_t nkey, const int64_t* key, co
 void trimr_second_degree(const int64_t* seg, int64_t nkey, const int32_t* v, int64_t nval, int32_t* out,
                          hipStream_t s);
 void trimr_low_degree(const int64_t* e, const int32_t* dg, int64_t n, int64_t* key, int64_t* val, hipStream_t s);
+// fixed 8-byte values (marker -1), value-parallel in tiles: phase 0 sets
+// marked[key] (zeroed by the caller) for the keys holding a marker, phase 1
+// writes each tile's count of centres of marked keys to tcount[tile], phase 2
+// writes rows (centre, edge key) from tbase[tile] on
+int64_t trimr_emit_tiles(int64_t nval);
+void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval, const int64_t* vals, uint8_t* marked,
+                      int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, hipStream_t s);
 // cnt[s] = wedge centres of edge segment s if it holds the edge marker, else 0
 // (voff: variable-width values, the marker is empty; voff null: fixed 8-byte
 // values vals, the marker is -1)

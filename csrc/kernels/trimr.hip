@@ -126,7 +126,110 @@ __global__ __launch_bounds__(NT) void k_emit_write(const int64_t* __restrict__ s
   }
 }
 
+// Fixed 8-byte values (marker -1): value-parallel instead of a thread per key
+// (RMAT-20's last reduce: 1.24 G values over 190 M keys, hub pairs with 10^5
+// centres, and uncoalesced per-thread walks). One block per tile of ET_TILE
+// values stages the tile's segment starts in LDS (at most ET_TILE + 1:
+// every segment has a value) and finds each value's key by an LDS binary
+// search. PHASE 0 marks the keys holding a marker, PHASE 1 counts the
+// centres of marked keys per tile, PHASE 2 writes them at the tile's offset.
+constexpr int ET_IT = 16;
+constexpr int ET_TILE = NT * ET_IT;
+
+__device__ __forceinline__ int64_t et_upper(const int64_t* __restrict__ a, int64_t n, int64_t x) {
+  int64_t lo = 0, hi = n;  // first index with a[idx] > x
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <int PHASE>
+__global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ seg, int64_t nkey, int64_t nval,
+                                                   const int64_t* __restrict__ vals, uint8_t* __restrict__ marked,
+                                                   int64_t* __restrict__ tcount, const int64_t* __restrict__ tbase,
+                                                   const int64_t* __restrict__ ekey, int64_t* __restrict__ out) {
+  __shared__ int64_t s_seg[ET_TILE + 1];
+  __shared__ int64_t s_k0;
+  __shared__ int s_n;
+  __shared__ int64_t sh[NT / MRH_WAVE + 1];
+  const int64_t t0 = (int64_t)blockIdx.x * ET_TILE;
+  const int tn = (int)(nval - t0 < ET_TILE ? nval - t0 : ET_TILE);
+  if (threadIdx.x == 0) {
+    const int64_t k0 = et_upper(seg, nkey, t0) - 1;            // key of the tile's first value
+    const int64_t k1 = et_upper(seg, nkey, t0 + tn - 1) - 1;   // and of its last
+    s_k0 = k0;
+    s_n = (int)(k1 - k0 + 1);
+  }
+  __syncthreads();
+  const int64_t k0 = s_k0;
+  const int nk = s_n;
+  for (int i = threadIdx.x; i <= nk; i += NT) s_seg[i] = seg[k0 + i];
+  __syncthreads();
+  int64_t mine = 0;
+  int64_t c_[ET_IT];
+  int64_t key_[ET_IT];
+#pragma unroll
+  for (int it = 0; it < ET_IT; ++it) {
+    const int o = it * NT + threadIdx.x;
+    key_[it] = -1;
+    if (o >= tn) continue;
+    const int64_t j = t0 + o;
+    int lo = 0, hi = nk;  // last key with s_seg <= j
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (s_seg[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    const int64_t k = k0 + lo;
+    const int64_t c = vals[j];
+    if (PHASE == 0) {
+      if (c == -1) marked[k] = 1;  // every writer stores the same byte
+    } else if (c != -1 && marked[k]) {
+      c_[it] = c;
+      key_[it] = k;
+      ++mine;
+    }
+  }
+  if (PHASE == 0) return;
+  int64_t total;
+  const int64_t pre = dev::block_excl_scan<int64_t, NT>(mine, sh, &total);
+  if (PHASE == 1) {
+    if (threadIdx.x == 0) tcount[blockIdx.x] = total;
+    return;
+  }
+  int64_t o = tbase[blockIdx.x] + pre;
+#pragma unroll
+  for (int it = 0; it < ET_IT; ++it) {
+    if (key_[it] < 0) continue;
+    out[3 * o] = c_[it];
+    out[3 * o + 1] = ekey[2 * key_[it]];
+    out[3 * o + 2] = ekey[2 * key_[it] + 1];
+    ++o;
+  }
+}
+
 }  // namespace
+
+int64_t trimr_emit_tiles(int64_t nval) { return (nval + ET_TILE - 1) / ET_TILE; }
+
+void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval, const int64_t* vals, uint8_t* marked,
+                      int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, hipStream_t s) {
+  if (nval <= 0 || nkey <= 0) return;
+  const unsigned g = (unsigned)trimr_emit_tiles(nval);
+  if (phase == 0)
+    hipLaunchKernelGGL(k_emit_tiles<0>, dim3(g), dim3(NT), 0, s, seg, nkey, nval, vals, marked, tcount, tbase, ekey,
+                       out);
+  else if (phase == 1)
+    hipLaunchKernelGGL(k_emit_tiles<1>, dim3(g), dim3(NT), 0, s, seg, nkey, nval, vals, marked, tcount, tbase, ekey,
+                       out);
+  else
+    hipLaunchKernelGGL(k_emit_tiles<2>, dim3(g), dim3(NT), 0, s, seg, nkey, nval, vals, marked, tcount, tbase, ekey,
+                       out);
+  MRH_CHECK_LAUNCH();
+}
 
 void trimr_first_degree(const int64_t* seg, int64_t nkey, const int64_t* key, const int64_t* nbr, int64_t nval,
                         int64_t* edge, int32_t* deg, hipStream_t s) {
