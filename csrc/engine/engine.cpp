@@ -608,6 +608,100 @@ int narrow_keys(const KV& kv, at::Tensor* keys, at::Tensor* idx) {
   return std::max(total, 1);
 }
 
+// MRH_PACKED_PAIRS=0: group every pair through the key sort + index gathers
+bool packed_pairs_disabled() {
+  static const bool off = [] {
+    const char* e = std::getenv("MRH_PACKED_PAIRS");
+    return e && *e == '0';
+  }();
+  return off;
+}
+
+// Fixed keys of 8-byte words and fixed 8-byte values whose significant bits
+// fit one u64 together — the pairs of graph collates: (vertex, vertex),
+// (edge, vertex), ... — are grouped on (packed key << vbits | value): one
+// keys-only radix sort over the key bits (stable: every group keeps its
+// values in input order), no index column, no gather of keys or values
+// afterwards (the values are the low bits, the unique keys unpacked from
+// the heads). Returns false when the pairs are not that narrow.
+bool convert_packed_pairs(const KV& kv, KMV* out, ConvertStats* st) {
+  if (!kv.kfixed() || kv.kw < 8 || kv.kw % 8 || kv.kw > 64 || kv.vw != 8 || kv.n == 0) return false;
+  auto aligned = [&](const at::Tensor& t, int64_t bytes) {
+    return t.defined() && t.is_contiguous() && reinterpret_cast<uintptr_t>(t.data_ptr()) % 8 == 0 && t.numel() >= bytes;
+  };
+  if (!aligned(kv.kdata, kv.n * kv.kw) || !aligned(kv.vdata, kv.n * 8)) return false;
+  const at::Device dev = kv.device();
+  const int nw = kv.kw / 8;
+  at::Tensor kw = kv.kdata.narrow(0, 0, kv.n * kv.kw).view(at::kLong).view({kv.n, nw});
+  at::Tensor vv = kv.vdata.narrow(0, 0, kv.n * 8).view(at::kLong);
+  auto [kmn, kmx] = at::aminmax(kw, 0);
+  auto [vmn, vmx] = at::aminmax(vv);
+  at::Tensor b = at::cat({kmn, kmx, vmn.view({1}), vmx.view({1})}).to(at::kCPU);
+  const int64_t* bp = P0<int64_t>(b);
+  auto bits_of = [](int64_t lo, int64_t hi) { return lo < 0 ? 64 : (hi == 0 ? 0 : 64 - __builtin_clzll((uint64_t)hi)); };
+  const int vbits = std::max(1, bits_of(bp[2 * nw], bp[2 * nw + 1]));
+  if (vbits >= 64) return false;
+  k::PackShifts sh{};
+  sh.nw = nw;
+  std::vector<int> kwbits(nw);
+  int kbits = 0;
+  for (int w = 0; w < nw; ++w) {
+    kwbits[w] = bits_of(bp[w], bp[nw + w]);
+    sh.s[w] = kwbits[w] ? vbits + kbits : -1;
+    kbits += kwbits[w];
+  }
+  if (kbits + vbits > 64) return false;
+  at::Tensor packed = at::empty({kv.n}, opt(dev, at::kLong));
+  if (dev.is_cuda()) {
+    k::pack_kv(reinterpret_cast<const uint64_t*>(kv.kdata.data_ptr()), reinterpret_cast<const uint64_t*>(vv.data_ptr()),
+               kv.n, sh, P0<uint64_t>(packed), cur_stream());
+  } else {
+    const uint64_t* kd = reinterpret_cast<const uint64_t*>(kv.kdata.data_ptr());
+    const uint64_t* vd = reinterpret_cast<const uint64_t*>(vv.data_ptr());
+    uint64_t* o = P0<uint64_t>(packed);
+    for (int64_t i = 0; i < kv.n; ++i) {
+      uint64_t k = vd[i];
+      for (int w = 0; w < nw; ++w)
+        if (sh.s[w] >= 0) k |= kd[i * nw + w] << sh.s[w];
+      o[i] = k;
+    }
+  }
+  at::Tensor sk = kbits > 0 ? radix_sort_keys(packed, vbits, vbits + kbits, false) : packed;
+  packed = at::Tensor();
+  at::Tensor keyp = at::bitwise_right_shift(sk, vbits);
+  at::Tensor flags, pos, seg;
+  int64_t nseg = 0;
+  segments_from_sorted(keyp, &flags, &pos, &seg, &nseg);
+  flags = pos = at::Tensor();
+  at::Tensor heads = keyp.index_select(0, seg.narrow(0, 0, nseg));
+  keyp = at::Tensor();
+  std::vector<at::Tensor> cols;
+  int off = 0;
+  for (int w = 0; w < nw; ++w) {
+    if (!kwbits[w]) {
+      cols.push_back(at::zeros({nseg}, opt(dev, at::kLong)));
+      continue;
+    }
+    at::Tensor c = at::bitwise_right_shift(heads, off);
+    if (off + kwbits[w] < 64) c = at::bitwise_and(c, (int64_t)((1ull << kwbits[w]) - 1));
+    cols.push_back(c);
+    off += kwbits[w];
+  }
+  out->keys.n = nseg;
+  out->keys.kw = kv.kw;
+  out->keys.vw = 0;
+  out->keys.kdata = at::stack(cols, 1).contiguous().view(at::kByte).view({-1});
+  out->keys.vdata = at::empty({0}, opt(dev, at::kByte));
+  out->vw = 8;
+  out->vdata = at::bitwise_and(sk, (int64_t)((1ull << vbits) - 1)).contiguous().view(at::kByte).view({-1});
+  out->seg = seg;
+  out->nkey = nseg;
+  out->nval = kv.n;
+  st->exact = true;
+  st->passes = (kbits + 7) / 8;
+  return true;
+}
+
 KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tensor& prehash) {
   const at::Device dev = kv.device();
   KMV out;
@@ -623,6 +717,8 @@ KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tenso
   }
   const int64_t n = kv.n;
   if (n > 0xFFFFFFFFll) fail("convert: more than 2^32 pairs on one rank");
+  if (force_hash_bits >= 64 && !prehash.defined() && !packed_pairs_disabled() && convert_packed_pairs(kv, &out, st))
+    return out;
   at::Tensor sk_in, idx;
   int end_bit;
   st->exact = kv.kfixed() && kv.kw <= 8 && force_hash_bits >= 64;

@@ -56,7 +56,8 @@ at::Tensor trimr_second_degree(const KMV& m);
 std::pair<at::Tensor, at::Tensor> trimr_low_degree(const KV& kv);
 // edge -> {wedge centres (8 B), edge marker (0 B)}: closed triangles
 // (centre, e0, e1) as [T,3] int64
-// the edge marker of fixed 8-byte values in tri_find_mr's last collate
-constexpr int64_t kTriEdgeMark = -1;
+// tri_find_mr's last collate, fixed 8-byte values: an edge (vi, vj) carries
+// the value vi (a wedge's centre is never one of its key's endpoints), so
+// the pairs stay narrow (vertex-sized values) and group as packed words
 at::Tensor trimr_emit(const KMV& m);
 }  // namespace mrh

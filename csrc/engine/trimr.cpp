@@ -98,8 +98,8 @@ std::pair<at::Tensor, at::Tensor> trimr_low_degree(const KV& kv) {
 }
 
 // Edge markers: an empty value (the reference's NULL) or, with fixed 8-byte
-// values, kTriEdgeMark — the pipeline marks its edges that way so that the
-// last collate moves one fixed-width value column (no per-pair offsets)
+// values, the key's first vertex (tri.h) — the pipeline marks its edges
+// that way so that the last collate moves one narrow fixed-width value column
 at::Tensor trimr_emit(const KMV& m) {
   const at::Device dev = m.seg.device();
   // fixed widths other than 8: only markers (0) or no marker at all
@@ -128,7 +128,7 @@ at::Tensor trimr_emit(const KMV& m) {
   }
   if (dev.is_cuda()) {
     at::Tensor cnt = at::empty({m.nkey}, opt(dev, at::kLong));
-    k::trimr_emit_count(seg, m.nkey, voff, fixed ? P0<int64_t>(m.vdata) : nullptr, P0<int64_t>(cnt), cur());
+    k::trimr_emit_count(seg, m.nkey, voff, fixed ? P0<int64_t>(m.vdata) : nullptr, ek, P0<int64_t>(cnt), cur());
     at::Tensor pos = exclusive_scan(cnt);
     const int64_t T = pos[m.nkey].item<int64_t>();
     at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
@@ -137,16 +137,17 @@ at::Tensor trimr_emit(const KMV& m) {
   }
   const uint8_t* vd = P0<uint8_t>(m.vdata);
   std::vector<int64_t> rows;
+  int64_t s = 0;
   auto value = [&](int64_t j, int64_t* c) {  // false: the edge marker
     if (fixed) {
       std::memcpy(c, vd + 8 * j, 8);
-      return *c != kTriEdgeMark;
+      return *c != ek[2 * s];
     }
     if (voff[j + 1] - voff[j] != 8) return false;
     std::memcpy(c, vd + voff[j], 8);
     return true;
   };
-  for (int64_t s = 0; s < m.nkey; ++s) {
+  for (s = 0; s < m.nkey; ++s) {
     bool marker = false;
     int64_t c;
     for (int64_t j = seg[s]; j < seg[s + 1]; ++j) marker |= !value(j, &c);

@@ -198,6 +198,18 @@ __global__ __launch_bounds__(NT) void k_pack_words(const uint64_t* __restrict__ 
   idx[i] = (uint32_t)i;
 }
 
+// narrow keys with narrow 8-byte values: pair i -> (packed key words) | value
+// (key word w at shift s[w] >= vbits, the value below vbits)
+__global__ __launch_bounds__(NT) void k_pack_kv(const uint64_t* __restrict__ kd, const uint64_t* __restrict__ vd,
+                                               int64_t n, PackShifts sh, uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = vd[i];
+  for (int w = 0; w < sh.nw; ++w)
+    if (sh.s[w] >= 0) k |= kd[i * sh.nw + w] << sh.s[w];
+  out[i] = k;
+}
+
 // head bitmap (bit i of 64-bit word i / 64 set where a segment starts) ->
 // per-word counts, then the positions of the set bits (one word per thread)
 __global__ __launch_bounds__(NT) void k_bits_count(const uint64_t* __restrict__ H, int64_t nw,
@@ -413,6 +425,11 @@ void compact_heads(const uint32_t* flags, const uint32_t* pos, int64_t n, int64_
 void pack_words(const uint64_t* kd, int64_t n, const PackShifts& sh, uint64_t* out, uint32_t* idx, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_pack_words, dim3(nblk(n)), dim3(NT), 0, s, kd, n, sh, out, idx);
+  MRH_CHECK_LAUNCH();
+}
+void pack_kv(const uint64_t* kd, const uint64_t* vd, int64_t n, const PackShifts& sh, uint64_t* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pack_kv, dim3(nblk(n)), dim3(NT), 0, s, kd, vd, n, sh, out);
   MRH_CHECK_LAUNCH();
 }
 void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s) {

@@ -133,6 +133,8 @@ struct PackShifts {
   int s[8];
 };
 void pack_words(const uint64_t* kd, int64_t n, const PackShifts& sh, uint64_t* out, uint32_t* idx, hipStream_t s);
+// out[i] = vd[i] | OR of key word w << s[w] (narrow keys and values on one u64)
+void pack_kv(const uint64_t* kd, const uint64_t* vd, int64_t n, const PackShifts& sh, uint64_t* out, hipStream_t s);
 // head bitmap H (nw 64-bit words): cnt[w] = popcount; then seg[pos[w] + k] =
 // position of the k-th set bit of word w, seg[pos[nw]] = n
 void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s);
@@ -372,7 +374,7 @@ void trimr_first_degree(const int64_t* seg, int64_t nkey, const int64_t* key, co
 void trimr_second_degree(const int64_t* seg, int64_t nkey, const int32_t* v, int64_t nval, int32_t* out,
                          hipStream_t s);
 void trimr_low_degree(const int64_t* e, const int32_t* dg, int64_t n, int64_t* key, int64_t* val, hipStream_t s);
-// fixed 8-byte values (marker -1), value-parallel in tiles: phase 0 sets
+// fixed 8-byte values (marker: the key's first vertex), value-parallel in tiles: phase 0 sets
 // marked[key] (zeroed by the caller) for the keys holding a marker, phase 1
 // writes each tile's count of centres of marked keys to tcount[tile], phase 2
 // writes rows (centre, edge key) from tbase[tile] on
@@ -381,9 +383,9 @@ void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval,
                       int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, hipStream_t s);
 // cnt[s] = wedge centres of edge segment s if it holds the edge marker, else 0
 // (voff: variable-width values, the marker is empty; voff null: fixed 8-byte
-// values vals, the marker is -1)
-void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, const int64_t* vals, int64_t* cnt,
-                      hipStream_t s);
+// values vals, the marker is the key's first vertex)
+void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, const int64_t* vals, const int64_t* ekey,
+                      int64_t* cnt, hipStream_t s);
 // rows (centre, e0, e1) at pos[s].. (pos = exclusive scan of cnt)
 void trimr_emit_write(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vdata,
                       const int64_t* ekey, const int64_t* pos, int64_t* out, hipStream_t s);

@@ -81,13 +81,13 @@ __global__ __launch_bounds__(NT) void k_low_degree(const int64_t* __restrict__ e
 // 8-byte values, vals)
 __global__ __launch_bounds__(NT) void k_emit_count(const int64_t* __restrict__ seg, int64_t nkey,
                                                   const int64_t* __restrict__ voff, const int64_t* __restrict__ vals,
-                                                  int64_t* __restrict__ cnt) {
+                                                  const int64_t* __restrict__ ekey, int64_t* __restrict__ cnt) {
   for (int64_t s = (int64_t)blockIdx.x * NT + threadIdx.x; s < nkey; s += (int64_t)gridDim.x * NT) {
     int64_t c = 0;
     bool marker = false;
     for (int64_t j = seg[s]; j < seg[s + 1]; ++j) {
-      if (!voff) {  // fixed 8-byte values: the edge marker is the value -1
-        const bool m = vals[j] == -1;
+      if (!voff) {  // fixed 8-byte values: an edge carries its first vertex
+        const bool m = vals[j] == ekey[2 * s];
         marker |= m;
         c += !m;
         continue;
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(NT) void k_emit_write(const int64_t* __restrict__ s
       int64_t c;
       if (!voff) {
         c = reinterpret_cast<const int64_t*>(vdata)[j];
-        if (c == -1) continue;
+        if (c == e0) continue;
       } else {
         const int64_t b = voff[j];
         if (voff[j + 1] - b != 8) continue;
@@ -185,9 +185,10 @@ __global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ s
     }
     const int64_t k = k0 + lo;
     const int64_t c = vals[j];
+    const bool mark = c == ekey[2 * k];  // an edge carries its first vertex
     if (PHASE == 0) {
-      if (c == -1) marked[k] = 1;  // every writer stores the same byte
-    } else if (c != -1 && marked[k]) {
+      if (mark) marked[k] = 1;  // every writer stores the same byte
+    } else if (!mark && marked[k]) {
       c_[it] = c;
       key_[it] = k;
       ++mine;
@@ -252,10 +253,10 @@ void trimr_low_degree(const int64_t* e, const int32_t* dg, int64_t n, int64_t* k
   MRH_CHECK_LAUNCH();
 }
 
-void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, const int64_t* vals, int64_t* cnt,
-                      hipStream_t s) {
+void trimr_emit_count(const int64_t* seg, int64_t nkey, const int64_t* voff, const int64_t* vals, const int64_t* ekey,
+                      int64_t* cnt, hipStream_t s) {
   if (nkey <= 0) return;
-  hipLaunchKernelGGL(k_emit_count, dim3(blocks(nkey)), dim3(NT), 0, s, seg, nkey, voff, vals, cnt);
+  hipLaunchKernelGGL(k_emit_count, dim3(blocks(nkey)), dim3(NT), 0, s, seg, nkey, voff, vals, ekey, cnt);
   MRH_CHECK_LAUNCH();
 }
 

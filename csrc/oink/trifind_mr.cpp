@@ -75,10 +75,13 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
     });
   });
   stage("add edges", mrt, [&] {
-    // the edges carry the marker kTriEdgeMark (not an empty value), so the
-    // pairs of collate 4 all have one 8-byte value (fixed-width gathers)
+    // an edge (vi, vj) carries the value vi as its marker (not an empty
+    // value): every pair of collate 4 has one narrow 8-byte value, so the
+    // collate groups them as packed (edge, vertex) words
     mre.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {
-      if (src.n) add_tensors(kv, edges_of(src), at::full({src.n}, kTriEdgeMark, src.kdata.options().dtype(at::kLong)));
+      if (!src.n) return;
+      at::Tensor e = edges_of(src);
+      add_tensors(kv, e, e.select(1, 0).contiguous());
     });
     mrt.add(mre);
   });
