@@ -6,7 +6,9 @@ are grouped exactly by the ordinary convert, so there only the key order
 differs), including the exact fallback on forced hash
 collisions and the fall back to plain chunks on a layout change.
 The CPU engine runs the same algorithm as the HIP kernels (group.hip)."""
+import collections
 import os
+import struct
 import random
 import subprocess
 import sys
@@ -180,3 +182,35 @@ def test_grouped_convert_gpu_fixed_wide():
     assert a[1] == b[1]
     # packed-word order (ordinary convert) vs hash order (incremental index)
     assert sorted(a[2]) == sorted(b[2])
+
+
+def _pairs_part(keys, vals, dev, words=1):
+    kd = torch.tensor(keys, dtype=torch.int64).reshape(-1, words).contiguous().view(torch.uint8).reshape(-1)
+    vd = torch.tensor(vals, dtype=torch.int64).view(torch.uint8)
+    return C.make_kv(kd, None, vd, None, len(vals), dev)
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("words", [1, 2])
+def test_convert_packed_pairs_vs_dict(dev, words):
+    """narrow fixed keys (1 or 2 words) with narrow 8-byte values group as one
+    packed u64 per pair: every key's values in input order, against a Python
+    dict; with a value too wide to pack the ordinary path gives the same groups"""
+    rng = random.Random(11 + words)
+    n = 50_000
+    keys = [rng.randrange(0, 3000) for _ in range(n * words)]
+    vals = [rng.randrange(0, 1 << 20) for _ in range(n)]
+    want = collections.defaultdict(list)
+    for i in range(n):
+        want[tuple(keys[i * words:(i + 1) * words])].append(vals[i])
+    for wide in (False, True):
+        vv = [v | (1 << 62) for v in vals] if wide else vals  # 63 value bits: not packable
+        mr = MapReduce(g.Comm(device=dev))
+        mr.map(1, lambda itask, kv: kv.add_kv(_pairs_part(keys, vv, dev, words)))
+        assert mr.convert() == len(want)
+        got = {}
+        for k, mv in mr.kmv_pairs():
+            kk = tuple(struct.unpack(f"<{words}q", k))
+            got[kk] = [struct.unpack("<q", v)[0] & ((1 << 62) - 1) for v in mv]
+        assert got == dict(want)
+        assert mr.last_convert.exact
