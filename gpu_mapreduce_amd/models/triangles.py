@@ -179,7 +179,9 @@ def bench_trifind_mr(comm, args):
             host = int(getattr(args, "mr_ooc_host", 2 << 30))
             sync()
             t0 = time.perf_counter()
-            r2 = tri_find_mr(comm, e2, hbm_budget=budget, host_budget=host, fpath=root, memsize=-(16 << 20))
+            # pages of the reference's default memsize (64 MB): spool pieces of
+            # min(page, budget / 4) = 64 MiB
+            r2 = tri_find_mr(comm, e2, hbm_budget=budget, host_budget=host, fpath=root, memsize=64)
             sync()
             dt2 = comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
             out["ooc"] = {"scale": oscale, "ms": dt2 * 1e3, "triangles": int(r2["triangles"]),
