@@ -698,6 +698,12 @@ def main():
                               steps=args.extra_steps, warmup=6))  # steady state after ~6 jobs:
             # warmup 1 / 2 / 6 -> 27.1 / 24.7 / 22.8 ms (profiles/r3_wordfreq_input.txt)
             mark("wordfreq")
+            if comm.is_cuda and args.wordfreq_bytes > (1 << 30):
+                # the round-3 shape too (1 GiB per GPU), for comparison with earlier records
+                r1 = _extra(comm, "wordfreq_1gib", bench_wordfreq, args, bytes_per_gpu=float(1 << 30),
+                            file_bytes=args.file_bytes, steps=args.extra_steps, warmup=6)
+                res.update({k: v for k, v in r1.items() if k in ("wordfreq_1gib_ms", "wordfreq_1gib_kvps",
+                                                                   "wordfreq_1gib_error", "wordfreq_1gib_input_GBps")})
         if args.wordfreq_bytes > 0 and args.file_io_steps > 0:
             try:
                 res["wordfreq_with_file_io"] = bench_wordfreq_files(comm, args)
