@@ -396,7 +396,7 @@ def _extra(comm, prefix, fn, args, **over):
            f"{prefix}_config": dict(r["config"], steps=a.steps, warmup=a.warmup, scaling=r.get("scaling", "weak"),
                                     metric=r["metric"])}
     for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices", "build",
-              "triangles_check", "stages", "wedge_pairs", "ooc"):
+              "triangles_check", "stages", "wedge_pairs", "ooc", "ms_per_step_prefetch"):
         if k in r:
             out[f"{prefix}_{k}"] = r[k]
     return out
@@ -703,7 +703,8 @@ def main():
                 r1 = _extra(comm, "wordfreq_1gib", bench_wordfreq, args, bytes_per_gpu=float(1 << 30),
                             file_bytes=args.file_bytes, steps=args.extra_steps, warmup=6)
                 res.update({k: v for k, v in r1.items() if k in ("wordfreq_1gib_ms", "wordfreq_1gib_kvps",
-                                                                   "wordfreq_1gib_error", "wordfreq_1gib_input_GBps")})
+                                                                   "wordfreq_1gib_error", "wordfreq_1gib_input_GBps",
+                                                                   "wordfreq_1gib_ms_per_step_prefetch")})
         if args.wordfreq_bytes > 0 and args.file_io_steps > 0:
             try:
                 res["wordfreq_with_file_io"] = bench_wordfreq_files(comm, args)
