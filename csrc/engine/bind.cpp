@@ -165,6 +165,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("passes", &ConvertStats::passes)
       .def_readonly("collisions", &ConvertStats::collisions)
       .def_readonly("grouped", &ConvertStats::grouped)
+      .def_readonly("dict", &ConvertStats::dict)
+      .def_readonly("dict_cap", &ConvertStats::dict_cap)
       .def_readonly("exact", &ConvertStats::exact);
   py::class_<ShuffleStats>(m, "ShuffleStats")
       .def(py::init<>())
@@ -201,7 +203,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            })
       .def("add_kv", &KeyValue::add_kv, py::call_guard<py::gil_scoped_release>())
       .def("enable_grouping", &KeyValue::enable_grouping)
-      .def("reserve_grouping", &KeyValue::reserve_grouping)
+      .def("reserve_grouping", &KeyValue::reserve_grouping, py::arg("rows"), py::arg("key_bytes"),
+           py::arg("value_bytes"), py::arg("groups") = -1)
       .def_property_readonly("grouping", &KeyValue::grouping)
       .def("size", &KeyValue::size)
       .def("finish", &KeyValue::finish)

@@ -4,6 +4,7 @@
 //   cpu: straightforward host loops with identical semantics and identical
 //        output order (they are the oracle the GPU tests compare against).
 #include "kv.h"
+#include "grouper.h"
 
 #include <ATen/hip/HIPContext.h>
 #include <algorithm>
@@ -728,6 +729,9 @@ KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tenso
   } else if (force_hash_bits >= 64 && !prehash.defined() && (end_bit = narrow_keys(kv, &sk_in, &idx)) > 0) {
     st->exact = true;  // wide fixed keys whose words carry <= 64 significant bits together (edges, tuples)
   } else {
+    // keys that repeat (words, hot keys): one pass over a hash dictionary of
+    // the distinct keys instead of a 64-bit sort of every pair (grouper.h)
+    if (force_hash_bits >= 64 && convert_dict(kv, &out, st, prehash)) return out;
     // the 64-bit grouping hash of every key, unless the producer already
     // computed it (the pipelined InvertedIndex map hashes each file's URLs
     // while the next file is still on the PCIe link)

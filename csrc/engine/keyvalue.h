@@ -78,8 +78,8 @@ class KeyValue {
   int64_t piece_bytes() const { return spool_ ? piece_bytes_ : 0; }
   bool grouping() const { return grp_ != nullptr; }
   // capacity hint for the grouped arenas (GroupIndex::reserve); no-op without grouping
-  void reserve_grouping(int64_t rows, int64_t key_bytes, int64_t value_bytes) {
-    if (grp_) grp_->reserve(rows, key_bytes, value_bytes);
+  void reserve_grouping(int64_t rows, int64_t key_bytes, int64_t value_bytes, int64_t groups = -1) {
+    if (grp_) grp_->reserve(rows, key_bytes, value_bytes, groups);
   }
   // the index of the KV the last finish() returned (null if not grouped)
   std::shared_ptr<GroupIndex> take_group() { return std::move(done_); }

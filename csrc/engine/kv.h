@@ -90,6 +90,11 @@ struct ConvertStats {
   // incremental group-by (grouper.h): 0 not used, 1 used, 2 a hash collision
   // sent it to the ordinary convert
   int grouped = 0;
+  // hash-dictionary group-by of a whole KV (grouper.h convert_dict): 0 not
+  // tried, 1 used, 2 tried and handed to the sort path (collision / too many
+  // distinct keys)
+  int dict = 0;
+  int64_t dict_cap = 0;  // its final table capacity
 };
 // group-by (MR-MPI convert): KV -> KMV. Order of unique keys: sorted by key
 // (fixed <= 8B keys) or by 64-bit hash (others).

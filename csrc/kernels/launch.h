@@ -410,18 +410,39 @@ void ii_write(const uint8_t* kd, const int64_t* koff, const int32_t* vals, int64
 }  // namespace mrh
 
 // ---------------------------------------------------------------- group.hip
-// incremental exact group-by (GroupIndex, csrc/engine/grouper.h). Table of
-// `cap` (power of two) u64 hash slots + i32 group ids; ctr = [ngroups, collisions].
+// exact hash-dictionary group-by (HashDict / GroupIndex, csrc/engine/grouper.h)
 namespace mrh {
 namespace k {
-// code[i] = CLAIM|g (pair i created group g: rep[g] = row0+i, ghash[g] = hash) or its slot
-void grp_insert(const uint64_t* h, int64_t n, int64_t row0, uint64_t* slots, int32_t* sgid, int64_t cap,
-                uint64_t* ctr, int64_t* rep, uint64_t* ghash, uint32_t* code, hipStream_t s);
-// gid[row0+i] from code; key bytes of every non-claiming row checked against rep (ctr[1] += mismatches)
-void grp_resolve(const uint32_t* code, int64_t n, int64_t row0, const int32_t* sgid, const int64_t* rep,
-                 const uint8_t* kd, const int64_t* koff, int kw, int32_t* gid, uint64_t* ctr, hipStream_t s);
-void grp_rehash(const uint64_t* old_slots, const int32_t* old_gid, int64_t old_cap, uint64_t* new_slots,
-                int32_t* new_gid, int64_t new_cap, hipStream_t s);
+// one slot of the table (32 bytes; all zero = empty)
+struct alignas(32) DictSlot {
+  unsigned long long hash;  // key hash (a zero hash is stored as 1), 0 = empty
+  int32_t gid1;             // group id + 1, 0 until published
+  int32_t len;              // key bytes
+  uint32_t key[4];          // the key's first 16 bytes, zero padded
+};
+struct DictTable {
+  DictSlot* slots;            // [cap]
+  uint64_t mask;              // cap - 1 (cap a power of two)
+  int64_t* rep;               // [cap] first row of a group, -1 until published
+  uint64_t* ghash;            // [cap] hash of a group
+  unsigned long long* ctr;    // [groups, collisions, rows left unassigned, full flag]
+  int64_t limit;              // no new group past this many
+};
+// group every row row0+i (i < n) of the key column (kd, koff | kw): gid[row]
+// = its group or -1 when the table was full; h: optional
+// precomputed hashes (else lookup3 hashlittle2 of the bytes); retry: only
+// rows whose gid is -1.
+void dict_insert(const uint8_t* kd, const int64_t* koff, int kw, const uint64_t* h, int64_t n, int64_t row0,
+                 const DictTable& t, int32_t* gid, bool retry, hipStream_t s);
+void dict_rehash(const DictSlot* old_slots, int64_t old_cap, DictSlot* new_slots, int64_t new_cap, hipStream_t s);
+// out[j] = hash of row j*n/m, j < m
+void dict_sample(const uint8_t* kd, const int64_t* koff, int kw, int64_t n, int64_t m, uint64_t* out, hipStream_t s);
+// cnt[g] = rows with gid == g, g < m (LDS histograms, no per-row global atomic)
+// ws: dict_counts_ws_elems() u32 of scratch
+void dict_counts(const int32_t* gid, int64_t n, int64_t m, uint64_t* cnt, uint32_t* ws, hipStream_t s);
+int64_t dict_counts_ws_elems();
+// cnt[j] = gcount[order[j]]
+void dict_ranked_counts(const uint32_t* order, int64_t m, const uint64_t* gcount, int64_t* cnt, hipStream_t s);
 // aoff[i] = poff[i] + base for i in [0, n]
 void grp_append_off(const int64_t* poff, int64_t n, int64_t base, int64_t* aoff, hipStream_t s);
 // rank[order[j]] = j, heads[j] = rep[order[j]]

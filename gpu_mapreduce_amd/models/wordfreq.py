@@ -76,12 +76,29 @@ class WordFreq:
         if not self.chunks:
             return
         wc = C.WordCounter(self.mr.device) if self.combiner else None
+        # one rank, no combiner: the pairs are grouped chunk by chunk as the
+        # map emits them (the KeyValue's hash dictionary, csrc/engine/
+        # grouper.h) in the shadow of the next chunk's H2D copy, so the
+        # collate's convert only ranks the groups; with several ranks the
+        # pairs are shuffled first and grouped as the exchange rounds land
+        group = wc is None and self.mr.nprocs == 1 and self.is_cuda
+        if group:
+            kv.enable_grouping()
+        total = sum(t.numel() for t in self.chunks)
+        reserved = [False]
 
         def consume(buf, n):
             if wc is not None:
                 wc.add(buf, n)
-            else:
-                kv.add_kv(C.map_words(buf, n))
+                return
+            part = C.map_words(buf, n)
+            if group and not reserved[0] and part.n > 0:
+                # arenas for the whole map from the first chunk's density
+                # (+15 %); the table is sized from a sample of its words
+                reserved[0] = True
+                f = 1.15 * total / max(1, n)
+                kv.reserve_grouping(int(part.n * f) + 1024, int(part.kdata.numel() * f) + 4096, 0, groups=0)
+            kv.add_kv(part)
         if not self.is_cuda:
             for i, t in enumerate(self.chunks):
                 if self.ready[i] is not None:
@@ -140,8 +157,12 @@ class WordFreq:
             elif nb == 1 and i > 0:
                 issue(i)
             if i == n - 1 and nb > 1 and self.prefetch_next:
-                nxt = self.prefetch_next[0]
+                first = self.prefetch_next[0]
+                # entries as in `chunks`: a tensor or (tensor, ready)
+                nxt = first[0] if isinstance(first, (tuple, list)) else first
                 if nxt.numel() + PAD <= self.bufs[0].numel():
+                    if isinstance(first, (tuple, list)) and len(first) > 1 and first[1] is not None:
+                        first[1].result()  # its bytes are read into the host buffer
                     slot = (base + n) % nb
                     ev = torch.cuda.Event()
                     copy_into(slot, nxt, ev)
@@ -152,18 +173,29 @@ class WordFreq:
             pools.mark_use(dev, 8 + b, main)
         pools.ring_cursor(dev, "wf", advance=n, n=nb)
 
-    def run(self):
+    def run(self, phases=None):
+        """phases: optional dict; if given, per-stage seconds (device-synced,
+        barrier between stages) are added under map / collate / reduce / top_n"""
+        from .inverted_index import _Ticker
         mr = self.mr
+        tick = _Ticker(phases, mr.comm)
         nkv = mr.map(mr.nprocs, self._map)
+        tick("map")
         if self.combiner:
             # pairs are (word, local count): total words = sum of the counts
             self.nwords = int(mr.comm.allreduce(self.local_words, "sum"))
+            self.npairs = nkv  # map returns the global pair count
             self.nunique = mr.collate()
+            tick("collate")
             mr.reduce("sum:int32")
         else:
-            self.nwords = nkv
+            # one (word, NULL) pair per occurrence through the shuffle
+            # (reference examples/wordfreq.cpp:64-67, 104-130)
+            self.nwords = self.npairs = nkv
             self.nunique = mr.collate()
+            tick("collate")
             mr.reduce("count")
+        tick("reduce")
         mr.sort_values(-1)
         ntop = self.ntop
 
@@ -178,6 +210,7 @@ class WordFreq:
         mr.sort_values(-1)
         self.top = [(k.rstrip(b"\0").decode("utf-8", "replace"), struct.unpack("<i", v)[0])
                     for k, v in mr.kv_pairs()][:ntop]
+        tick("top_n")
         return self.nwords
 
 

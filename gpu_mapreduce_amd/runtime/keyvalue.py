@@ -98,10 +98,13 @@ class KeyValue:
         the device would otherwise idle between batches."""
         self._h.enable_grouping()
 
-    def reserve_grouping(self, rows: int, key_bytes: int, value_bytes: int):
+    def reserve_grouping(self, rows: int, key_bytes: int, value_bytes: int, groups: int | None = None):
         """Capacity hint for the grouped arenas: sized once for the whole map
-        (no regrow copies or hash-table rehash while the input streams)."""
-        self._h.reserve_grouping(int(rows), int(key_bytes), int(value_bytes))
+        (no regrow copies or hash-table rehash while the input streams).
+        groups: distinct keys to size the hash table for (None: as many as
+        rows — mostly distinct keys; 0: sized from a sample of the first
+        part — keys that repeat, such as words)."""
+        self._h.reserve_grouping(int(rows), int(key_bytes), int(value_bytes), -1 if groups is None else int(groups))
 
     @property
     def grouping(self) -> bool:
