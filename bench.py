@@ -396,7 +396,8 @@ def _extra(comm, prefix, fn, args, **over):
            f"{prefix}_config": dict(r["config"], steps=a.steps, warmup=a.warmup, scaling=r.get("scaling", "weak"),
                                     metric=r["metric"])}
     for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices", "build",
-              "triangles_check", "stages", "wedge_pairs", "ooc", "ms_per_step_prefetch"):
+              "triangles_check", "stages", "wedge_pairs", "ooc", "ms_per_step_prefetch", "pairs",
+              "pairs_per_s_by_stage", "top10", "top10_equals_combiner"):
         if k in r:
             out[f"{prefix}_{k}"] = r[k]
     return out
@@ -698,6 +699,13 @@ def main():
                               steps=args.extra_steps, warmup=6))  # steady state after ~6 jobs:
             # warmup 1 / 2 / 6 -> 27.1 / 24.7 / 22.8 ms (profiles/r3_wordfreq_input.txt)
             mark("wordfreq")
+            # BASELINE config 3 as the reference runs it: one (word, NULL) pair
+            # per occurrence through the shuffle (no in-mapper combiner;
+            # examples/wordfreq.cpp:64-67, 104-130; oink/wordfreq.cpp:40-90)
+            res.update(_extra(comm, "wordfreq_shuffle", bench_wordfreq, args, bytes_per_gpu=args.wordfreq_bytes,
+                              file_bytes=min(args.file_bytes, int(args.wordfreq_bytes)), steps=args.extra_steps,
+                              warmup=2, combiner=False))
+            mark("wordfreq_shuffle")
             if comm.is_cuda and args.wordfreq_bytes > (1 << 30):
                 # the round-3 shape too (1 GiB per GPU), for comparison with earlier records
                 r1 = _extra(comm, "wordfreq_1gib", bench_wordfreq, args, bytes_per_gpu=float(1 << 30),

@@ -226,6 +226,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("size", &Comm::size)
       .def_property_readonly("members", &Comm::members)
       .def_property_readonly("transport", &Comm::transport)
+      .def_property_readonly("max_msg", &Comm::max_msg)
       .def_property_readonly("distributed", &Comm::distributed)
       .def_property_readonly("failed", [](const Comm& c) { return c.monitor() && c.monitor()->failed(); })
       .def("rccl_info",

@@ -1,5 +1,7 @@
 // Native communicator (see comm.h).
 #include "comm.h"
+
+#include <numeric>
 #include "guardalloc.h"
 #include "hbmpool.h"
 
@@ -99,6 +101,7 @@ static void install_allocator() {
 Comm::Comm(at::Device dev) : dev_(dev) {
   if (dev_.is_cuda()) install_allocator();
   if (dev_.is_cuda() && force_rccl()) init_transport("", "self");
+  max_msg_ = rccl_ ? rccl_->max_msg() : max_msg_env();
 }
 
 Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const std::string& transport,
@@ -127,6 +130,13 @@ Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const s
     }
   }
   init_transport(transport, "world");
+  // rank 0's piece size on every rank (a collective: every member constructs)
+  if (rccl_) {
+    max_msg_ = rccl_->max_msg();
+  } else {
+    const int64_t mine = max_msg_env();
+    max_msg_ = size_ > 1 && pg_ ? allreduce(rank_ == 0 ? mine : 0, SUM) : mine;
+  }
 }
 
 void Comm::init_transport(const std::string& transport, const std::string& tag) {
@@ -343,19 +353,19 @@ void Comm::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& rec
     }
     return;
   }
-  // process group: pack per peer in order, one byte all-to-all, unpack
+  // process group: pack per peer in order, byte all-to-alls of at most
+  // max_msg_ bytes per peer each (the round count agreed: a pair's bytes are
+  // known to both ends, the longest pair sets it), unpack
   const int P = size_;
   std::vector<int64_t> sb(P, 0), rb(P, 0);
   for (const Xfer& x : sends) sb[x.peer] += x.bytes;
   for (const Xfer& x : recvs) rb[x.peer] += x.bytes;
-  int64_t st = 0, rt = 0;
   std::vector<int64_t> soff(P + 1, 0), roff(P + 1, 0);
   for (int p = 0; p < P; ++p) {
     soff[p + 1] = soff[p] + sb[p];
     roff[p + 1] = roff[p] + rb[p];
   }
-  st = soff[P];
-  rt = roff[P];
+  const int64_t st = soff[P], rt = roff[P];
   auto bo = at::TensorOptions().device(dev_).dtype(at::kByte);
   at::Tensor sbuf = at::empty({st}, bo), rbuf = at::empty({rt}, bo);
   std::vector<int64_t> fill = soff;
@@ -363,7 +373,33 @@ void Comm::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& rec
     copy_bytes((uint8_t*)sbuf.data_ptr() + fill[x.peer], x.ptr, x.bytes, dev_);
     fill[x.peer] += x.bytes;
   }
-  pg_->alltoall_base(rbuf, sbuf, rb, sb)->wait();
+  const int64_t m = std::max<int64_t>(max_msg_, 1);
+  int64_t rounds = 1;
+  for (int p = 0; p < P; ++p) rounds = std::max({rounds, (sb[p] + m - 1) / m, (rb[p] + m - 1) / m});
+  rounds = allreduce(rounds, MAX);
+  if (rounds == 1) {
+    pg_->alltoall_base(rbuf, sbuf, rb, sb)->wait();
+  } else {
+    for (int64_t r = 0; r < rounds; ++r) {
+      std::vector<int64_t> ps(P), pr(P);
+      std::vector<at::Tensor> sp, rp;
+      for (int p = 0; p < P; ++p) {
+        const int64_t a = std::min(sb[p], r * m), b = std::min(sb[p], (r + 1) * m);
+        const int64_t c = std::min(rb[p], r * m), d = std::min(rb[p], (r + 1) * m);
+        ps[p] = b - a;
+        pr[p] = d - c;
+        sp.push_back(sbuf.narrow(0, soff[p] + a, b - a));
+        rp.push_back(rbuf.narrow(0, roff[p] + c, d - c));
+      }
+      at::Tensor s1 = at::cat(sp), r1 = at::empty({std::accumulate(pr.begin(), pr.end(), int64_t(0))}, bo);
+      pg_->alltoall_base(r1, s1, pr, ps)->wait();
+      int64_t o = 0;
+      for (int p = 0; p < P; ++p) {
+        if (pr[p]) rp[p].copy_(r1.narrow(0, o, pr[p]));
+        o += pr[p];
+      }
+    }
+  }
   fill = roff;
   for (const Xfer& x : recvs) {
     copy_bytes(x.ptr, (uint8_t*)rbuf.data_ptr() + fill[x.peer], x.bytes, dev_);
@@ -514,6 +550,7 @@ std::shared_ptr<Comm> Comm::split(int color) const {
   c->pg_ = make_host_pg(pst, newrank, newsize, mon_);
   c->host_pg_ = true;
   if (rccl_) c->rccl_ = shared_rccl(newrank, newsize, rccl_device(), store_, "split", members, mon_.get());
+  c->max_msg_ = max_msg_;  // the parent's agreed value
   return c;
 }
 

@@ -120,6 +120,10 @@ class Comm {
   // against the current stream, or packed through the process group. Buffers
   // live on the engine device. Synchronous with respect to the current stream.
   void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) const;
+  // bytes per point-to-point piece (rank 0's MRH_RCCL_MAX_MSG, the same on
+  // every rank: the RCCL path and the process-group path both cut transfers
+  // into pieces of this size)
+  int64_t max_msg() const { return max_msg_; }
   // all ranks' `bytes`-byte blocks concatenated in rank order into recv
   // (device buffers of the engine device)
   void allgather_bytes(const void* send, void* recv, int64_t bytes) const;
@@ -149,6 +153,7 @@ class Comm {
   void fail_now(const std::string& why) const;
   bool host_scalars() const { return pg_ && host_pg_ && size_ > 1; }
   bool host_pg_ = false;  // pg_ has a CPU backend
+  int64_t max_msg_ = 0;   // point-to-point piece size, agreed at construction
   int rccl_device() const;  // the device index (the current one for "cuda")
 
   int rank_ = 0, size_ = 1;

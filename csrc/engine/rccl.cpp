@@ -31,6 +31,17 @@ void hip_ok(hipError_t e, const char* what) {
 constexpr int64_t kPoison = -(int64_t(1) << 40);
 }  // namespace
 
+// point-to-point piece size asked for by this process: MRH_RCCL_MAX_MSG bytes
+// (default 256 MiB; <= 0: whole messages). A communicator uses rank 0's value
+// (Rccl: sent with the unique id; Comm's process-group path: broadcast at
+// construction), so ranks with different environments still cut every
+// transfer into the same pieces.
+int64_t max_msg_env() {
+  const char* e = std::getenv("MRH_RCCL_MAX_MSG");
+  const long long v = e && *e ? std::atoll(e) : (1LL << 28);
+  return v > 0 ? (int64_t)v : std::numeric_limits<int64_t>::max();
+}
+
 // ====================================================================== Monitor
 
 Monitor::Monitor(c10::intrusive_ptr<c10d::Store> root, int rank, int size)
@@ -215,6 +226,7 @@ Rccl::Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>
   hip_ok(hipSetDevice(device), "hipSetDevice");
   ncclUniqueId id;
   IdRendezvous rv;
+  max_msg_ = max_msg_env();
   if (size == 1) {
     check(ncclGetUniqueId(&id), "ncclGetUniqueId");
   } else {
@@ -222,13 +234,18 @@ Rccl::Rccl(int rank, int size, int device, const c10::intrusive_ptr<c10d::Store>
     if (members.empty())
       for (int r = 0; r < size; ++r) members.push_back(r);
     if ((int)members.size() != size) throw std::runtime_error("mrhip rccl: member list does not match the size");
+    // the payload: the unique id, then rank 0's piece size
     rv = rendezvous_id(store, tag, members, rank, [&] {
       ncclUniqueId u;
       check(ncclGetUniqueId(&u), "ncclGetUniqueId");
-      return std::vector<uint8_t>((uint8_t*)&u, (uint8_t*)&u + sizeof(u));
+      std::vector<uint8_t> b((uint8_t*)&u, (uint8_t*)&u + sizeof(u));
+      b.resize(sizeof(u) + sizeof(int64_t));
+      std::memcpy(b.data() + sizeof(u), &max_msg_, sizeof(int64_t));
+      return b;
     }, mon);
-    if (rv.id.size() != sizeof(id)) throw std::runtime_error("mrhip rccl: bad unique id in store");
+    if (rv.id.size() != sizeof(id) + sizeof(int64_t)) throw std::runtime_error("mrhip rccl: bad unique id in store");
     std::memcpy(&id, rv.id.data(), sizeof(id));
+    std::memcpy(&max_msg_, rv.id.data() + sizeof(id), sizeof(int64_t));
     id_key_ = rv.key;
   }
   check(ncclCommInitRank(&comm_, size, id, rank), "ncclCommInitRank");
@@ -273,17 +290,13 @@ hipEvent_t Rccl::fence_out() {
 hipEvent_t Rccl::sendrecv_async(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
   if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
   fence_in(s);
-  // one transfer is posted as pieces of at most max_msg bytes (MRH_RCCL_MAX_MSG,
-  // default 256 MiB; both ends cut the same byte count the same way): on
-  // MI355X (RCCL 2.26.6) a single point-to-point message of 1 GiB + 40 bytes
-  // came back wrong from element 67141632 on (~512 MiB) while the same data in
-  // 1 GiB pieces arrived intact up to 4 GiB (tools/rccl_big.py,
-  // profiles/r4_rccl_big_messages.txt)
-  static const int64_t max_msg = [] {
-    const char* e = std::getenv("MRH_RCCL_MAX_MSG");
-    const long long v = e && *e ? std::atoll(e) : (1LL << 28);
-    return v > 0 ? (int64_t)v : std::numeric_limits<int64_t>::max();
-  }();
+  // one transfer is posted as pieces of at most max_msg_ bytes (agreed at
+  // init: both ends cut the same byte count the same way): on MI355X (RCCL
+  // 2.26.6) a single point-to-point message of 1 GiB + 40 bytes came back
+  // wrong from element 67141632 on (~512 MiB) while the same data in 1 GiB
+  // pieces arrived intact up to 4 GiB (profiles/r4_rccl_big_messages.txt;
+  // tests/test_rccl_gpu.py test_forced_rccl_large_transfers_bitwise)
+  const int64_t max_msg = max_msg_;
   check(ncclGroupStart(), "ncclGroupStart");
   for (const Xfer& x : recvs)
     for (int64_t o = 0; o < x.bytes; o += max_msg)

@@ -151,6 +151,8 @@ class Rccl {
   int user_rank();
   // the store key the id came through ("" for a local id)
   const std::string& id_key() const { return id_key_; }
+  // bytes per point-to-point piece: rank 0's MRH_RCCL_MAX_MSG, agreed at init
+  int64_t max_msg() const { return max_msg_; }
 
   // nccl async error (ncclSuccess / ncclInProgress when healthy)
   ncclResult_t async_error();
@@ -170,7 +172,11 @@ class Rccl {
   size_t ev_next_ = 0;
   bool aborted_ = false;
   std::string id_key_;
+  int64_t max_msg_ = 0;
 };
+
+// this process's MRH_RCCL_MAX_MSG (default 256 MiB; <= 0: no limit)
+int64_t max_msg_env();
 
 // The process's communicator over (store, tag, members, device): an existing
 // live one is shared, otherwise a new one is bootstrapped (collectively: every

@@ -12,8 +12,11 @@ MI355X pipeline (same op sequence on device-resident data):
             map emits KV(word+NUL, int32 count) once per distinct word — the
             pairs map + compress(count) would leave, without materialising a
             KV per occurrence; without it the tokenizer kernel emits
-            KV(word+NUL, NULL) per occurrence;
-  collate   hashlittle partition + RCCL all-to-all + group-by;
+            KV(word+NUL, NULL) per occurrence (the reference's pairs), and on
+            one rank the KeyValue groups them chunk by chunk on a device hash
+            dictionary while the next chunk is on the PCIe link;
+  collate   hashlittle partition + RCCL all-to-all + group-by (as the rounds
+            land: the same hash dictionary, csrc/engine/grouper.h);
   reduce    "sum:int32" (or "count" without the combiner) segmented reduce;
   top-N     sort_values(-1) (radix on negated counts) -> slice -> gather(1) ->
             sort_values(-1).
@@ -241,12 +244,15 @@ def bench_wordfreq(comm, args):
         i += 1
     setup = comm.allreduce(time.perf_counter() - ts, "max", dtype=torch.float64)
 
+    combiner = bool(getattr(args, "combiner", True))
+
     def steps(k, pipelined):
         """k back-to-back jobs; pipelined: job s copies job s+1's first chunk
         behind its own last one (never the last job of the window)"""
         app = None
         for s in range(k):
-            app = WordFreq(MapReduce(comm), chunks, prefetch_next=chunks if (pipelined and s < k - 1) else None)
+            app = WordFreq(MapReduce(comm), chunks, combiner=combiner,
+                           prefetch_next=chunks if (pipelined and s < k - 1) else None)
             app.run()
         return app
 
@@ -271,21 +277,41 @@ def bench_wordfreq(comm, args):
     app, dt = timed(args.steps, False)
     _, dt_pipe = timed(args.steps, True)
     total = comm.allreduce(per_gpu, "sum")
-    return {
+    out = {
         "metric": "KV-pairs/sec (whole node), wordfreq words counted end-to-end",
         "value": app.nwords / dt,
         "unit": "KV/s",
         "ms_per_step": dt * 1e3,
         "ms_per_step_prefetch": dt_pipe * 1e3,
-        "timed_step": "host(pinned)->HBM chunks, in-mapper count, collate, reduce, top-N; jobs strictly one after "
-                      "another (ms_per_step_prefetch: job s copies job s+1's first chunk behind its own last one)",
+        "timed_step": ("host(pinned)->HBM chunks, in-mapper count, collate, reduce, top-N" if combiner else
+                       "host(pinned)->HBM chunks, one (word, NULL) pair per occurrence, collate (hash partition + "
+                       "all-to-all when N>1, group-by), reduce(count), sort_values, top-N, gather") +
+                      "; jobs strictly one after another (ms_per_step_prefetch: job s copies job s+1's first chunk "
+                      "behind its own last one)",
         "vs_baseline": None,
         "baseline_note": "reference publishes no wordfreq number",
         "input_GBps": total / dt / 1e9,
         "words": app.nwords,
+        "pairs": app.npairs,
         "unique_words": app.nunique,
         "top3": app.top[:3],
         "setup_ms": setup * 1e3,
-        "config": {"model": "wordfreq", "global_batch": total, "seq_len": chunk,
-                   "parallelism": f"dp{comm.size}", "bytes_per_gpu": per_gpu},
+        "config": {"model": "wordfreq" if combiner else "wordfreq (no combiner: a pair per occurrence)",
+                   "global_batch": total, "seq_len": chunk, "parallelism": f"dp{comm.size}",
+                   "bytes_per_gpu": per_gpu, "combiner": combiner},
     }
+    if not combiner:
+        # one more job with device-synced stage boundaries (not the timed
+        # steps): per-stage times and pair rates, and the combiner's top-10
+        # as the check
+        ph = {}
+        a2 = WordFreq(MapReduce(comm), chunks, combiner=False)
+        a2.run(ph)
+        st = {k: comm.allreduce(v, "max", dtype=torch.float64) for k, v in ph.items()}
+        out["stages"] = {k: round(v * 1e3, 3) for k, v in st.items()}
+        out["pairs_per_s_by_stage"] = {k: (a2.npairs / v if v > 0 else None) for k, v in st.items()}
+        comb = WordFreq(MapReduce(comm), chunks, combiner=True)
+        comb.run()
+        out["top10"] = app.top
+        out["top10_equals_combiner"] = comb.top == app.top
+    return out

@@ -203,6 +203,79 @@ def case_inverted_index(comm):
     return got, {k.decode(): v for k, v in ref.items()}
 
 
+def case_wordfreq_shuffle(comm):
+    """wordfreq without the combiner (a (word, NULL) pair per occurrence
+    through the hash-partition exchange and the group-by of each round), and
+    the same pairs collated + counted with every count returned"""
+    import gpu_mapreduce_amd as g
+    from gpu_mapreduce_amd import C
+    from gpu_mapreduce_amd.models.wordfreq import WordFreq
+    from gpu_mapreduce_amd.utils import synth
+    dev = comm.device
+    chunks = [synth.zipf_text(700_000, seed=900 + 10 * comm.rank + i, device="cpu") for i in range(2)]
+    app = WordFreq(g.MapReduce(comm), chunks, ntop=10, combiner=False)
+    nwords = app.run()
+    mr = g.MapReduce(comm)
+
+    def fn(itask, kv):
+        for c in chunks:
+            buf = torch.zeros(c.numel() + 64, dtype=torch.uint8, device=dev)
+            buf[: c.numel()].copy_(c)
+            kv.add_kv(C.map_words(buf, c.numel()))
+    mr.map(comm.size, fn)
+    mr.collate()
+    mr.reduce("count")
+    local = {k.rstrip(b"\0"): struct.unpack("<i", v)[0] for k, v in mr.kv_pairs()}
+    text = [bytes(c.numpy()) for c in chunks]
+    return nwords, app.nunique, app.top, local, text
+
+
+def _check_wordfreq_shuffle(out):
+    cnt = collections.Counter()
+    for _, (_, _, _, _, text) in out.items():
+        for t in text:
+            cnt.update(t.split())
+    total = {}
+    for r, (nwords, nunique, top, local, _) in out.items():
+        assert nwords == sum(cnt.values()) and nunique == len(cnt)
+        assert not (set(total) & set(local)), "word owned by two ranks"
+        total.update(local)
+    assert total == dict(cnt)
+    top = out[0][2]
+    want = sorted(cnt.values(), reverse=True)[:10]
+    assert [c for _, c in top] == want
+    assert all(cnt[w.encode()] == c for w, c in top)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_wordfreq_shuffle_distributed(world):
+    _check_wordfreq_shuffle(run_world("case_wordfreq_shuffle", world))
+
+
+def case_max_msg_mismatch(comm):
+    """every rank asks for a different point-to-point piece size; the
+    communicator must agree on rank 0's, and a shuffle whose per-peer bytes
+    span many pieces must still deliver every pair exactly once"""
+    import gpu_mapreduce_amd as g
+    os.environ["MRH_RCCL_MAX_MSG"] = str(4096 if comm.rank == 0 else 1_000_000 + 7 * comm.rank)
+    nc = comm.native  # built now, from this environment
+    n = 40_000
+    keys = torch.arange(comm.rank * n, (comm.rank + 1) * n, dtype=torch.int64)
+    mr = g.MapReduce(comm)
+    mr.map(comm.size, lambda i, kv: kv.add_tensors(keys.to(comm.device), keys.to(comm.device) * 3))
+    mr.aggregate()
+    got = sorted((struct.unpack("<q", k)[0], struct.unpack("<q", v)[0]) for k, v in mr.kv_pairs())
+    return nc.max_msg, got
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_max_msg_agreed_across_ranks(world):
+    out = run_world("case_max_msg_mismatch", world)
+    assert {m for m, _ in out.values()} == {4096}
+    allp = sorted(p for _, got in out.values() for p in got)
+    assert allp == [(k, 3 * k) for k in range(world * 40_000)]
+
+
 def case_pagerank(comm):
     import numpy as np
     import gpu_mapreduce_amd as g

@@ -40,6 +40,13 @@ def test_mixed_layouts_gpu():
     assert merged[struct.pack("<q", 3)] == 10
 
 
+def test_wordfreq_shuffle_gpu_two_ranks():
+    """wordfreq with combiner=False on the device engine, 2 ranks: every
+    word's count equals collections.Counter, top-10 too"""
+    from test_distributed_cpu import _check_wordfreq_shuffle
+    _check_wordfreq_shuffle(run_world("case_wordfreq_shuffle", 2, DEV))
+
+
 def test_inverted_index_gpu_two_ranks():
     out = run_world("case_inverted_index", 2, DEV)
     got, ref = {}, collections.defaultdict(list)
