@@ -97,6 +97,7 @@ int main(int argc, char** argv) {
     // checksum: the counts add up to the number of ints
     if (do_reduce) {
       int64_t local = 0;
+      mr.flatten();
       if (mr.kv && mr.kv->n) local = mr.kv->vdata.view(at::kInt).sum().item<int64_t>();
       const int64_t tot = comm->allreduce(local, Comm::SUM);
       if (me == 0) std::printf("Counts sum: %lld\n", (long long)tot);

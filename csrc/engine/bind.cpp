@@ -302,12 +302,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property(
           "kv", [](MR& r) -> py::object {
             r.ensure_resident();
+            r.flatten();  // appended parts concatenated: the whole KV
             return r.kv ? py::cast(*r.kv) : py::none();
           },
           [](MR& r, py::object o) {
+            r.flatten();
             if (o.is_none()) r.kv.reset();
             else r.kv = o.cast<KV>();
           })
+      .def_property_readonly("kv_parts", [](MR& r) { return (int64_t)r.kv_tail().size() + (r.kv ? 1 : 0); })
       .def_property(
           "kmv", [](MR& r) -> py::object {
             r.ensure_resident();
@@ -645,7 +648,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       [](std::shared_ptr<Comm> c, at::Tensor edges, int64_t hbm_budget, int64_t host_budget, std::string fpath,
          int memsize, bool upper) {
         oink::TriMRRun r;
-        int64_t spool_files = 0, spool_host = 0, spool_disk = 0;
+        int64_t spool_files = 0, spool_host = 0, spool_disk = 0, in_vw = -2, in_n = -1;
         {
           py::gil_scoped_release nogil;
           r = poisoning(c, "tri_find_mr", [&] {
@@ -661,6 +664,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
               if (memsize != 0) m->set.memsize = memsize;
             }
             oink::TriMRRun out = oink::tri_find_mr(mre, mrt, upper);
+            mre.flatten();
+            in_vw = mre.kv ? mre.kv->vw : -1;  // the edge MR as the pipeline left it
+            in_n = mre.kv ? mre.kv->n : 0;
             spool_files = mrt.spool_stats.files + mre.spool_stats.files;
             spool_host = mrt.spool_stats.host_bytes + mre.spool_stats.host_bytes;
             spool_disk = mrt.spool_stats.disk_bytes + mre.spool_stats.disk_bytes;
@@ -682,6 +688,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["spool_files"] = spool_files;
         d["spool_host_bytes"] = spool_host;
         d["spool_disk_bytes"] = spool_disk;
+        d["input_value_width_after"] = in_vw;
+        d["input_pairs_after"] = in_n;
         return d;
       },
       py::arg("comm"), py::arg("edges"), py::arg("hbm_budget") = 0, py::arg("host_budget") = 0,

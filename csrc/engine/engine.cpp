@@ -624,49 +624,83 @@ bool packed_pairs_disabled() {
 // keys-only radix sort over the key bits (stable: every group keeps its
 // values in input order), no index column, no gather of keys or values
 // afterwards (the values are the low bits, the unique keys unpacked from
-// the heads). Returns false when the pairs are not that narrow.
-bool convert_packed_pairs(const KV& kv, KMV* out, ConvertStats* st) {
-  if (!kv.kfixed() || kv.kw < 8 || kv.kw % 8 || kv.kw > 64 || kv.vw != 8 || kv.n == 0) return false;
+// the heads). The pairs may come in parts (a KV with appended parts,
+// mapreduce.h): each part is packed in place into its rows of the sort
+// input, nothing is concatenated. Returns false when the pairs are not that
+// narrow.
+bool convert_packed_parts(const std::vector<KV>& parts_in, KMV* out, ConvertStats* st) {
+  if (packed_pairs_disabled()) return false;
+  std::vector<KV> parts;
+  for (const KV& p : parts_in)
+    if (p.n > 0) parts.push_back(p);
+  if (parts.empty()) return false;
+  const KV& k0 = parts[0];
+  if (!k0.kfixed() || k0.kw < 8 || k0.kw % 8 || k0.kw > 64 || k0.vw != 8) return false;
   auto aligned = [&](const at::Tensor& t, int64_t bytes) {
     return t.defined() && t.is_contiguous() && reinterpret_cast<uintptr_t>(t.data_ptr()) % 8 == 0 && t.numel() >= bytes;
   };
-  if (!aligned(kv.kdata, kv.n * kv.kw) || !aligned(kv.vdata, kv.n * 8)) return false;
-  const at::Device dev = kv.device();
-  const int nw = kv.kw / 8;
-  at::Tensor kw = kv.kdata.narrow(0, 0, kv.n * kv.kw).view(at::kLong).view({kv.n, nw});
-  at::Tensor vv = kv.vdata.narrow(0, 0, kv.n * 8).view(at::kLong);
-  auto [kmn, kmx] = at::aminmax(kw, 0);
-  auto [vmn, vmx] = at::aminmax(vv);
-  at::Tensor b = at::cat({kmn, kmx, vmn.view({1}), vmx.view({1})}).to(at::kCPU);
-  const int64_t* bp = P0<int64_t>(b);
+  const at::Device dev = k0.device();
+  const int nw = k0.kw / 8;
+  int64_t n = 0;
+  std::vector<at::Tensor> mm;  // per part: key word minima, maxima, value min, max
+  for (const KV& p : parts) {
+    if (p.kw != k0.kw || p.vw != 8 || p.device() != dev) return false;
+    if (!aligned(p.kdata, p.n * p.kw) || !aligned(p.vdata, p.n * 8)) return false;
+    at::Tensor kw = p.kdata.narrow(0, 0, p.n * p.kw).view(at::kLong).view({p.n, nw});
+    at::Tensor vv = p.vdata.narrow(0, 0, p.n * 8).view(at::kLong);
+    auto [kmn, kmx] = at::aminmax(kw, 0);
+    auto [vmn, vmx] = at::aminmax(vv);
+    mm.push_back(at::cat({kmn, kmx, vmn.view({1}), vmx.view({1})}).view({1, -1}));
+    n += p.n;
+  }
+  // one host sync for every part's ranges; the packing covers all of them
+  at::Tensor all = at::cat(mm).to(at::kCPU);
+  const int64_t* ap = P0<int64_t>(all);
+  const int64_t np = (int64_t)parts.size(), row = 2 * nw + 2;
+  std::vector<int64_t> b(row);
+  for (int j = 0; j < row; ++j) {
+    const bool is_min = j < nw || j == 2 * nw;
+    int64_t v = ap[j];
+    for (int64_t i = 1; i < np; ++i) {
+      const int64_t x = ap[i * row + j];
+      // signed compare is right for the bit-width test below (a negative
+      // word needs 64 bits either way)
+      v = is_min ? std::min(v, x) : std::max(v, x);
+    }
+    b[j] = v;
+  }
   auto bits_of = [](int64_t lo, int64_t hi) { return lo < 0 ? 64 : (hi == 0 ? 0 : 64 - __builtin_clzll((uint64_t)hi)); };
-  const int vbits = std::max(1, bits_of(bp[2 * nw], bp[2 * nw + 1]));
+  const int vbits = std::max(1, bits_of(b[2 * nw], b[2 * nw + 1]));
   if (vbits >= 64) return false;
   k::PackShifts sh{};
   sh.nw = nw;
   std::vector<int> kwbits(nw);
   int kbits = 0;
   for (int w = 0; w < nw; ++w) {
-    kwbits[w] = bits_of(bp[w], bp[nw + w]);
+    kwbits[w] = bits_of(b[w], b[nw + w]);
     sh.s[w] = kwbits[w] ? vbits + kbits : -1;
     kbits += kwbits[w];
   }
   if (kbits + vbits > 64) return false;
-  at::Tensor packed = at::empty({kv.n}, opt(dev, at::kLong));
-  if (dev.is_cuda()) {
-    k::pack_kv(reinterpret_cast<const uint64_t*>(kv.kdata.data_ptr()), reinterpret_cast<const uint64_t*>(vv.data_ptr()),
-               kv.n, sh, P0<uint64_t>(packed), cur_stream());
-  } else {
-    const uint64_t* kd = reinterpret_cast<const uint64_t*>(kv.kdata.data_ptr());
-    const uint64_t* vd = reinterpret_cast<const uint64_t*>(vv.data_ptr());
-    uint64_t* o = P0<uint64_t>(packed);
-    for (int64_t i = 0; i < kv.n; ++i) {
-      uint64_t k = vd[i];
-      for (int w = 0; w < nw; ++w)
-        if (sh.s[w] >= 0) k |= kd[i * nw + w] << sh.s[w];
-      o[i] = k;
+  at::Tensor packed = at::empty({n}, opt(dev, at::kLong));
+  int64_t row0 = 0;
+  for (const KV& p : parts) {  // every part packed in place into its rows
+    const uint64_t* kd = reinterpret_cast<const uint64_t*>(p.kdata.data_ptr());
+    const uint64_t* vd = reinterpret_cast<const uint64_t*>(p.vdata.data_ptr());
+    uint64_t* o = P0<uint64_t>(packed) + row0;
+    if (dev.is_cuda()) {
+      k::pack_kv(kd, vd, p.n, sh, o, cur_stream());
+    } else {
+      for (int64_t i = 0; i < p.n; ++i) {
+        uint64_t kk = vd[i];
+        for (int w = 0; w < nw; ++w)
+          if (sh.s[w] >= 0) kk |= kd[i * nw + w] << sh.s[w];
+        o[i] = kk;
+      }
     }
+    row0 += p.n;
   }
+  parts.clear();
   at::Tensor sk = kbits > 0 ? radix_sort_keys(packed, vbits, vbits + kbits, false) : packed;
   packed = at::Tensor();
   at::Tensor keyp = at::bitwise_right_shift(sk, vbits);
@@ -689,7 +723,7 @@ bool convert_packed_pairs(const KV& kv, KMV* out, ConvertStats* st) {
     off += kwbits[w];
   }
   out->keys.n = nseg;
-  out->keys.kw = kv.kw;
+  out->keys.kw = k0.kw;
   out->keys.vw = 0;
   out->keys.kdata = at::stack(cols, 1).contiguous().view(at::kByte).view({-1});
   out->keys.vdata = at::empty({0}, opt(dev, at::kByte));
@@ -697,11 +731,13 @@ bool convert_packed_pairs(const KV& kv, KMV* out, ConvertStats* st) {
   out->vdata = at::bitwise_and(sk, (int64_t)((1ull << vbits) - 1)).contiguous().view(at::kByte).view({-1});
   out->seg = seg;
   out->nkey = nseg;
-  out->nval = kv.n;
+  out->nval = n;
   st->exact = true;
   st->passes = (kbits + 7) / 8;
   return true;
 }
+
+bool convert_packed_pairs(const KV& kv, KMV* out, ConvertStats* st) { return convert_packed_parts({kv}, out, st); }
 
 KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tensor& prehash) {
   const at::Device dev = kv.device();

@@ -319,8 +319,9 @@ MapReduce::~MapReduce() {
 
 // every op's entry: fault injection point, and data spilled to host (spill()
 // or spill-on-OOM) comes back to HBM before the op touches it
-void MapReduce::enter(const char* op, bool ooc_ok) {
+void MapReduce::enter(const char* op, bool ooc_ok, bool parts_ok) {
   guard::fault_point(op, comm_->rank());
+  if (!parts_ok) flatten();
   if (guard::alloc_guard_active()) {  // an overrun found at the end of an earlier op fails the next one
     static size_t raised = 0;
     const auto reps = guard::guard_reports();
@@ -379,16 +380,15 @@ OocEnv MapReduce::ooc_env() const {
   return e;
 }
 
-// append b to a: on the device, or — for a bounded MR — through a Spool, so
-// an addflag map never concatenates past the budgets
+// concatenation of the KV's parts: on the device, or — for a bounded MR —
+// where the budgets allow (out-of-core data is written once, to pinned host
+// memory or one spool file)
 KV MapReduce::append_kv(const KV& a, const KV& b) {
   if (budget() <= 0 && set.host_budget <= 0) return concat({a, b}, device());
   if (!a.device().is_cuda() && device().is_cuda()) {
-    // a is already out of core (pinned host or a spool file): the result is
-    // written once where it fits — not spooled piece by piece and gathered
-    // into a second copy
     const int64_t total = a.nbytes() + b.nbytes();
     if (set.host_budget <= 0 || total <= set.host_budget) {
+      // one pinned output of the final size, each part copied in once
       KV o = concat({a, b}, at::Device(at::kCPU));
       auto pin = [](const at::Tensor& t) { return t.defined() && !t.is_pinned() ? t.pin_memory() : t; };
       o.kdata = pin(o.kdata);
@@ -411,6 +411,50 @@ KV MapReduce::append_kv(const KV& a, const KV& b) {
   return o;
 }
 
+std::vector<KV> MapReduce::kv_parts() const {
+  std::vector<KV> p;
+  if (kv) p.push_back(*kv);
+  for (const KV& t : kv_tail_) p.push_back(t);
+  return p;
+}
+
+int64_t MapReduce::kv_rows() const {
+  int64_t n = kv ? kv->n : 0;
+  for (const KV& t : kv_tail_) n += t.n;
+  return n;
+}
+
+void MapReduce::flatten() {
+  if (kv_tail_.empty()) return;
+  std::vector<KV> tail;
+  tail.swap(kv_tail_);
+  for (const KV& t : tail) kv = kv ? append_kv(*kv, t) : t;
+  grouped_.reset();
+}
+
+void MapReduce::append_part(const KV& b) {
+  grouped_.reset();
+  if (!kv) {
+    kv = b;
+    return;
+  }
+  if (b.n == 0) return;
+  KV p = b;
+  if (budget() > 0 && b.device().is_cuda()) {
+    int64_t on_dev = b.nbytes();
+    for (const KV& x : kv_parts())
+      if (x.device().is_cuda()) on_dev += x.nbytes();
+    if (on_dev > budget()) {  // the new part leaves HBM through a bounded builder (its pieces only)
+      KeyValue tmp(device());
+      bound(tmp);
+      tmp.add_kv(b);
+      p = tmp.finish();
+      note_spool(tmp);
+    }
+  }
+  kv_tail_.push_back(p);
+}
+
 void MapReduce::note_spool(const KeyValue& b) {
   const SpoolStats s = b.spool_stats();
   spool_stats.add(s);
@@ -419,6 +463,7 @@ void MapReduce::note_spool(const KeyValue& b) {
 int64_t MapReduce::data_bytes() const {
   int64_t b = 0;
   if (kv) b += kv->nbytes();
+  for (const KV& t : kv_tail_) b += t.nbytes();
   if (kmv) b += kmv->nbytes();
   return b;
 }
@@ -434,6 +479,7 @@ void MapReduce::note_ooc(const char* op, const OocStats& st) {
 
 std::unique_ptr<MapReduce> MapReduce::copy() const {
   const_cast<MapReduce*>(this)->ensure_resident();  // a disk-resident MR copies its data, not nothing
+  const_cast<MapReduce*>(this)->flatten();
   auto mr = std::make_unique<MapReduce>(comm_);
   mr->set = set;
   if (kv) mr->kv = clone_kv(*kv);
@@ -486,9 +532,7 @@ void MapReduce::stats(const char* heading, int which) {
     if (kv) guard::check_kv(*kv, heading);
     if (kmv) guard::check_kmv(*kmv, heading);
   }
-  int64_t b = 0;
-  if (kv) b += kv->nbytes();
-  if (kmv) b += kmv->nbytes();
+  const int64_t b = data_bytes();
   msize = b;
   if (b > msizemax) msizemax = b;
   if (set.timer) {
@@ -527,16 +571,18 @@ void MapReduce::note_shuffle(const ShuffleStats& st) {
 // ====================================================================== add / open / close
 
 uint64_t MapReduce::add(MapReduce& other) {  // :348-374
+  // O(appended): other's pairs become parts of this KV where they are (the
+  // reference reopens only the last page, src/keyvalue.cpp:185-209); nothing
+  // this object holds is copied
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__, true);  // out-of-core data is appended where it lives (a bounded MR appends through a Spool)
+  enter(__func__, true, true);
   need_kv("add");
   other.ensure_resident();
   if (!other.kv) fail("MapReduce passed to add() does not have KeyValue pairs");
-  kv = append_kv(*kv, *other.kv);
-  grouped_.reset();
+  for (const KV& p : other.kv_parts()) append_part(p);
   stats("Add", 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 void MapReduce::open(int addflag) {  // :1648-1664
@@ -559,14 +605,14 @@ uint64_t MapReduce::close() {  // :658-672
   if (open_add_) ensure_resident();  // appending to data that was spilled to disk
   else drop_disk();                  // replacing it: the spilled copy must never be read back over n
   if (open_add_ && kv) {
-    kv = append_kv(*kv, n);
-    grouped_.reset();
+    append_part(n);
   } else {
+    kv_tail_.clear();
     kv = n;
     grouped_ = g;
   }
   stats("Close", 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 // ====================================================================== map
@@ -596,15 +642,15 @@ uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) 
   note_spool(kvb);
   std::shared_ptr<GroupIndex> g = kvb.take_group();
   if (addflag && kv) {
-    kv = append_kv(*kv, n);
-    grouped_.reset();
+    append_part(n);
   } else {
+    kv_tail_.clear();
     kv = n;
     grouped_ = g;
   }
   kmv.reset();
   stats(heading, 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 uint64_t MapReduce::map(int nmap, const MapTaskFn& fn, int addflag) {  // :1044-1051
@@ -762,6 +808,7 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
   drop_for_map(addflag, &src);
   enter(__func__);
   src.ensure_resident();
+  src.flatten();
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   HostCol k = host_col(s.kdata, s.koff, s.kw), v = host_col(s.vdata, s.voff, s.vw);
@@ -773,10 +820,11 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
   if (&src == this && addflag) {
     KV n = kvb.finish();
     note_spool(kvb);
-    kv = concat({s, n}, device());
+    kv = s;
+    append_part(n);
     kmv.reset();
     stats("Map", 0);
-    return count(kv->n);
+    return count(kv_rows());
   }
   return finish_map(kvb, addflag);
 }
@@ -787,6 +835,7 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
   drop_for_map(addflag, &src);
   enter(__func__);
   src.ensure_resident();
+  src.flatten();
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   KeyValue kvb(device());
@@ -795,10 +844,11 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
   if (&src == this && addflag) {
     KV n = kvb.finish();
     note_spool(kvb);
-    kv = concat({s, n}, device());
+    kv = s;
+    append_part(n);
     kmv.reset();
     stats("Map", 0);
-    return count(kv->n);
+    return count(kv_rows());
   }
   return finish_map(kvb, addflag);
 }
@@ -808,7 +858,7 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
 uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__, true);
+  enter(__func__, true, !comm_->distributed());  // one rank: nothing moves, appended parts stay
   need_kv("aggregate");
   if (comm_->distributed() && ooc_shuffle()) {
     // larger than the budget: budget-sized chunks in lock-step, received into
@@ -830,7 +880,7 @@ uint64_t MapReduce::aggregate(const HashFn& hash) {  // :385-563
     note_shuffle(st);
   }
   stats("Aggregate", 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 // owner rank of every pair by a user hash (MR-MPI's hash callback, run on the
@@ -859,7 +909,7 @@ bool MapReduce::ooc_shuffle() const {
 uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__, true);
+  enter(__func__, true, !comm_->distributed());
   need_kv("aggregate");
   if (comm_->distributed()) {
     ShuffleStats st;
@@ -880,7 +930,7 @@ uint64_t MapReduce::aggregate_dest(const at::Tensor& dest) {
     note_shuffle(st);
   }
   stats("Aggregate", 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 uint64_t MapReduce::broadcast(int root) {  // :569-623
@@ -922,13 +972,28 @@ uint64_t MapReduce::convert() { return convert_prehashed(at::Tensor()); }
 uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
   start();
   OpTrace tr_("convert", this);
-  enter("convert", true);
+  enter("convert", true, !prehash.defined());
   need_kv("convert");
   last_convert = ConvertStats();
-  if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
+  if (needs_ooc(data_bytes(), budget(), 4.0)) {
     OocStats os;
-    kmv = ooc_convert(*kv, ooc_env(), device(), &os);  // hash-partitioned spools (src/keymultivalue.cpp:645-789)
+    // hash-partitioned spools (src/keymultivalue.cpp:645-789), fed from every
+    // part where it lies
+    kmv = ooc_convert(kv_parts(), ooc_env(), device(), &os);
     note_ooc("Convert", os);
+  } else if (!kv_tail_.empty()) {
+    // appended parts: grouped together (packed pairs read every part in
+    // place), or concatenated once for the other paths
+    std::vector<KV> parts = kv_parts();
+    bool all_dev = true;
+    for (const KV& p : parts) all_dev = all_dev && p.device() == device();
+    KMV m;
+    if (all_dev && convert_packed_parts(parts, &m, &last_convert)) {
+      kmv = std::move(m);
+    } else {
+      flatten();
+      kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert, 64); });
+    }
   } else if (grouped_ && grouped_->describes(*kv) && !prehash.defined()) {
     // grouped while the map produced it: only the two short sorts are left
     KMV m;
@@ -946,6 +1011,7 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
   }
   grouped_.reset();
   kv.reset();
+  kv_tail_.clear();
   stats("Convert", 1);
   return count(kmv->nkey);
 }
@@ -953,7 +1019,9 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
 uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__, true);  // with a budget: aggregate and convert stream out-of-core data themselves
+  // with a budget: aggregate and convert stream out-of-core data themselves;
+  // on one rank they also read appended parts in place
+  enter(__func__, true, !comm_->distributed());
   need_kv("collate");
   // pipelined collate: the hash-partition exchange hands every received round
   // to a GroupIndex, which groups it on the compute stream while the next
@@ -1008,7 +1076,7 @@ KMV MapReduce::local_groups(const char* heading) {
   last_convert = ConvertStats();
   if (needs_ooc(kv->nbytes(), budget(), 4.0)) {
     OocStats os;
-    KMV m = ooc_convert(*kv, ooc_env(), device(), &os);
+    KMV m = ooc_convert({*kv}, ooc_env(), device(), &os);
     note_ooc(heading, os);
     return m;
   }
@@ -1338,6 +1406,7 @@ void MapReduce::print(int proc, int nstride, int kflag, int vflag) { print(nullp
 
 void MapReduce::print(const char* file, int fflag, int proc, int nstride, int kflag, int vflag) {
   ensure_resident();
+  flatten();
   if (!kv && !kmv) fail("Cannot print without KeyValue or KeyMultiValue");
   if (kflag < 0 || kflag > 7 || vflag < 0 || vflag > 7 || nstride < 1) fail("Invalid print args");
   const int me = comm_->rank();
@@ -1403,6 +1472,7 @@ void MapReduce::print(const char* file, int fflag, int proc, int nstride, int kf
 
 uint64_t MapReduce::kv_stats(int level) {  // :2937-2966
   ensure_resident();
+  flatten();
   need_kv("print stats");
   std::vector<int64_t> t =
       comm_->allreduce({kv->n, kv->key_bytes(), kv->value_bytes(), kv->nbytes(), pages(kv->nbytes())}, Comm::SUM);
@@ -1468,6 +1538,7 @@ void MapReduce::cummulative_stats(int level, int reset) {  // :3007-3066
 // ====================================================================== spill tier
 
 void MapReduce::spill() {
+  flatten();
   const bool pin = device().is_cuda();
   if (kv) kv = kv_host(*kv, pin);
   if (kmv) kmv = kmv_to(*kmv, at::Device(at::kCPU), pin);
@@ -1551,6 +1622,7 @@ KV get_kv(std::FILE* f, at::Device dev) {
 void MapReduce::save(const std::string& path) const {
   if (disk_path_.empty() && !kv && !kmv) fail("Cannot save without KeyValue or KeyMultiValue");
   const_cast<MapReduce*>(this)->ensure_resident();
+  const_cast<MapReduce*>(this)->flatten();
   write_file(rank_path(path, *comm_));
 }
 
@@ -1609,6 +1681,7 @@ int64_t MapReduce::read_file(const std::string& p) {
     KV k = get_kv(f.get(), device());
     guard::check_kv(k, "load");  // offsets/arena sizes consistent before any kernel reads them
     kv = k;
+    kv_tail_.clear();
     kmv.reset();
     n = kv->n;
   } else if (kind == 1) {
@@ -1625,6 +1698,7 @@ int64_t MapReduce::read_file(const std::string& p) {
     guard::check_kmv(m, "load");
     kmv = m;
     kv.reset();
+    kv_tail_.clear();
     n = m.nkey;
   } else {
     fail("load: corrupt checkpoint kind in " + p);
@@ -1639,6 +1713,7 @@ int64_t MapReduce::read_file(const std::string& p) {
 // (fpath/mrmpi.<kv|kmv>.<instance>.<counter>.<rank>, src/mapreduce.cpp:3187-3205)
 // and comes back on the MR's next op (ensure_resident, called from enter()).
 void MapReduce::spill_disk() {
+  flatten();
   if (!kv && !kmv) return;
   char name[96];
   std::snprintf(name, sizeof(name), "mrmpi.%s.%d.%d.%d", kv ? "kv" : "kmv", instance_me_, ++disk_counter_,
@@ -1663,6 +1738,7 @@ void MapReduce::drop_for_map(int addflag, const MapReduce* src) {
   if (addflag || src == this) return;
   drop_disk();
   kv.reset();
+  kv_tail_.clear();
   kmv.reset();
   grouped_.reset();
 }

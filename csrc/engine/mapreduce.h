@@ -95,9 +95,19 @@ class MapReduce {
   int mapfilecount = 0;
 
   // ---------------------------------------------------------------- data
+  // The KV is `kv` followed by the parts appended to it and not yet
+  // concatenated (add, an addflag map / close): appending is O(appended) —
+  // the parts stay where they were made (HBM, pinned host, spool file). Ops
+  // that stream their input (convert, collate and aggregate on one rank)
+  // read the parts in place; every other op, and code reading `kv`
+  // directly, flattens first (flatten(): one concatenation).
   std::optional<KV> kv;
   std::optional<KMV> kmv;
   ConvertStats last_convert;
+  void flatten();
+  // pairs of the KV including the appended parts
+  int64_t kv_rows() const;
+  const std::vector<KV>& kv_tail() const { return kv_tail_; }
 
   // ---------------------------------------------------------------- object ops
   std::unique_ptr<MapReduce> copy() const;
@@ -196,7 +206,13 @@ class MapReduce {
 
  private:
   void start();
-  void enter(const char* op, bool ooc_ok = false);
+  // parts_ok: the op reads the appended parts itself (else they are flattened)
+  void enter(const char* op, bool ooc_ok = false, bool parts_ok = false);
+  // append `b` as a part: device parts past the HBM budget go through a
+  // bounded builder (pinned host / spool files), nothing already held moves
+  void append_part(const KV& b);
+  // the KV and its appended parts, in order
+  std::vector<KV> kv_parts() const;
   int64_t data_bytes() const;
   void bound(KeyValue& b);
   KV append_kv(const KV& a, const KV& b);
@@ -241,6 +257,7 @@ class MapReduce {
   void drop_for_map(int addflag, const MapReduce* src = nullptr);
 
   CommPtr comm_;
+  std::vector<KV> kv_tail_;
   std::string disk_path_;
   int disk_counter_ = 0;
   // group-by index of the KV built by the last map / close with grouping

@@ -177,21 +177,32 @@ SpoolConfig spool_cfg(const OocEnv& env, const std::shared_ptr<SpoolBudget>& b, 
   return c;
 }
 
-// spool the chunks of kv into M bucket spools by a per-pair bucket id
-// produced on the device by `dest_of(chunk)`; the spools share the host
-// budget and go to disk beyond it (HBM holds only the chunks in flight)
+// spool the chunks of the parts (in order) into M bucket spools by a per-pair
+// bucket id produced on the device by `dest_of(chunk)`; the spools share the
+// host budget and go to disk beyond it (HBM holds only the chunks in flight)
 template <typename F>
-std::vector<Spool> spool(const KV& kv, int64_t cap, at::Device dev, int M, F&& dest_of, const OocEnv& env,
-                         OocStats* st) {
+std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev, int M, F&& dest_of,
+                         const OocEnv& env, OocStats* st) {
   auto budget = std::make_shared<SpoolBudget>();
   budget->hbm = 0;
   budget->host = env.host;
   std::vector<Spool> parts;
   parts.reserve((size_t)M);
   for (int d = 0; d < M; ++d) parts.emplace_back(dev, spool_cfg(env, budget, "part"));
-  const HostOff h = host_off(kv);
-  const auto ch = chunks(kv, h, cap);
-  const bool cuda = dev.is_cuda() && kv.device().is_cpu() && env.streams != 1;
+  // every chunk of every part, in order: (part, first pair, end pair)
+  std::vector<HostOff> h;
+  struct Ch {
+    size_t part;
+    int64_t a, b;
+  };
+  std::vector<Ch> ch;
+  bool host_side = false;
+  for (size_t p = 0; p < kvs.size(); ++p) {
+    h.push_back(host_off(kvs[p]));
+    for (auto [a, b] : chunks(kvs[p], h.back(), cap)) ch.push_back({p, a, b});
+    host_side = host_side || kvs[p].device().is_cpu();
+  }
+  const bool cuda = dev.is_cuda() && host_side && env.streams != 1;
   c10::optional<c10::hip::HIPStream> side, drain, main;
   if (cuda) {
     main = c10::hip::getCurrentHIPStream(dev.index());
@@ -199,10 +210,10 @@ std::vector<Spool> spool(const KV& kv, int64_t cap, at::Device dev, int M, F&& d
     drain = c10::hip::getStreamFromPool(false, dev.index());
   }
   auto load = [&](size_t i) {
-    const KV slice = kv_slice(kv, ch[i].first, ch[i].second, h.kp(), h.vp());
-    if (!cuda) return kv_to(slice, dev);
-    KV c = kv_to_async(slice, dev, *side, *main);
-    return c;
+    const KV& kv = kvs[ch[i].part];
+    const KV slice = kv_slice(kv, ch[i].a, ch[i].b, h[ch[i].part].kp(), h[ch[i].part].vp());
+    if (!cuda || !kv.device().is_cpu()) return kv_to(slice, dev);
+    return kv_to_async(slice, dev, *side, *main);
   };
   std::vector<hipEvent_t> ready(2, nullptr);
   if (cuda)
@@ -240,7 +251,7 @@ std::vector<Spool> spool(const KV& kv, int64_t cap, at::Device dev, int M, F&& d
     }
     if (st) {
       st->chunks++;
-      st->bytes_staged += row_bytes(kv, h, ch[i].first, ch[i].second);
+      st->bytes_staged += row_bytes(kvs[ch[i].part], h[ch[i].part], ch[i].a, ch[i].b);
     }
   }
   for (auto& p : parts) p.sync();
@@ -326,11 +337,14 @@ KMV kmv_concat_host(const std::vector<KMV>& parts, const KV& like) {
 
 bool needs_ooc(int64_t bytes, int64_t budget, double factor) { return budget > 0 && bytes * factor > budget; }
 
-KMV ooc_convert(const KV& kv, const OocEnv& env, at::Device dev, OocStats* st) {
+KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, OocStats* st) {
   const int64_t budget = env.hbm;
-  const int M = parts_for(kv.nbytes(), budget, 4.0);
+  int64_t bytes = 0;
+  for (const KV& k : kvs) bytes += k.nbytes();
+  const KV& kv = kvs.at(0);
+  const int M = parts_for(bytes, budget, 4.0);
   if (st) st->parts = M;
-  auto parts = spool(kv, std::max<int64_t>(budget / 4, 1), dev, M, [&](const KV& c) {
+  auto parts = spool(kvs, std::max<int64_t>(budget / 4, 1), dev, M, [&](const KV& c) {
     // a hash independent of the shuffle's owner hash (every key on this rank
     // has the same owner hash mod P): bits 20.. of the 64-bit grouping hash
     at::Tensor h = hash64_keys(c);
@@ -396,7 +410,7 @@ KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device
   at::Tensor sp = at::from_blob(split.data(), {(int64_t)split.size()}, opt(at::kCPU, at::kLong)).clone().to(dev);
   // pass 2: range partition, bucket = number of splitters below the key
   // (a binary search over the splitters in LDS, k_bucket_by_splitters)
-  auto parts = spool(kv, cap, dev, MB, [&](const KV& c) {
+  auto parts = spool({kv}, cap, dev, MB, [&](const KV& c) {
     at::Tensor k = skeys(c).contiguous();
     at::Tensor out = at::empty({c.n}, opt(dev, at::kInt));
     if (c.n == 0) return out;

@@ -30,7 +30,9 @@ bool needs_ooc(int64_t bytes, int64_t budget, double factor);
 // results are host-resident: pinned while they fit env.host, else one
 // memory-mapped file under env.dir; inputs may be on the host (pinned,
 // pageable or memory-mapped) or the device
-KMV ooc_convert(const KV& kv, const OocEnv& env, at::Device dev, OocStats* st = nullptr);
+// kvs: the KV as parts in order (a KV with appended parts, mapreduce.h); each
+// is read where it lies
+KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, OocStats* st = nullptr);
 KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device dev, OocStats* st = nullptr);
 KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, const OocEnv& env,
                       at::Device dev, OocStats* st = nullptr);

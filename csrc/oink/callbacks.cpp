@@ -327,6 +327,7 @@ struct HostKV {
   int64_t vlen(int64_t i) const { return vw >= 0 ? vw : voff.data_ptr<int64_t>()[i + 1] - voff.data_ptr<int64_t>()[i]; }
 };
 HostKV host_kv(MapReduce& mr) {
+  mr.flatten();
   if (!mr.kv) throw Error("Command output requires KeyValue pairs");
   const KV& kv = *mr.kv;
   HostKV h;

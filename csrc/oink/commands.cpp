@@ -81,6 +81,7 @@ int64_t nvert_global(const Comm& comm, const at::Tensor& e) {
 
 // "  <b> ... <a> ..." lines of an (int key a, int value b) histogram on rank 0
 void print_histo(Oink& o, MapReduce& mr, const char* f) {
+  mr.flatten();
   if (o.me != 0 || !mr.kv || mr.kv->n == 0) return;
   at::Tensor k = mr.kv->kdata.to(at::kCPU).contiguous(), v = mr.kv->vdata.to(at::kCPU).contiguous();
   const int kw = mr.kv->kw > 0 ? mr.kv->kw : 4, vw = mr.kv->vw > 0 ? mr.kv->vw : 4;
@@ -346,6 +347,7 @@ class WordFreq : public Command {
       });
       mr->gather(1);
       mr->sort_values(-1);
+      mr->flatten();
       if (me == 0 && mr->kv) {
         const KV& kv = *mr->kv;
         at::Tensor kd = kv.kdata.to(at::kCPU).contiguous(), ko = kv.koff.to(at::kCPU).contiguous();
@@ -484,6 +486,7 @@ class TriFind : public Command {
   TriFind(Oink& o) : Command(o) { ninputs = noutputs = 1; }
   void run() override {
     MapReduce& mre = obj.input(1, rd(parse_edge), rc(parse_edge));
+    mre.flatten();
     at::Tensor e = mre.kv ? edges_of(*mre.kv) : at::empty({0, 2}, opt(comm->device(), at::kLong));
     TriangleGraph g(comm, e, -1);
     at::Tensor tri = g.triangles();
@@ -534,6 +537,7 @@ class CCFind : public Command {
   }
   void run() override {
     MapReduce& mre = obj.input(1, rd(parse_edge), rc(parse_edge));
+    mre.flatten();
     at::Tensor e = mre.kv ? edges_of(*mre.kv) : at::empty({0, 2}, opt(comm->device(), at::kLong));
     const int64_t N = nvert_global(*comm, e);
     EdgePlan plan(comm, e, N, std::nullopt, true);
@@ -683,6 +687,7 @@ class LubyFind : public Command {
   }
   void run() override {
     MapReduce& mre = obj.input(1, rd(parse_edge), rc(parse_edge));
+    mre.flatten();
     at::Tensor e = mre.kv ? edges_of(*mre.kv) : at::empty({0, 2}, opt(comm->device(), at::kLong));
     e = e.index({e.select(1, 0) != e.select(1, 1)});
     const int64_t N = nvert_global(*comm, e);
@@ -716,6 +721,7 @@ class SSSP : public Command {
   void run() override {
     MapReduce& mre = obj.input(1, rd(parse_edge_weight), rc(parse_edge_weight));
     const at::Device dev = comm->device();
+    mre.flatten();
     at::Tensor e = mre.kv ? edges_of(*mre.kv) : at::empty({0, 2}, opt(dev, at::kLong));
     at::Tensor w = (mre.kv && mre.kv->vw == 8) ? mre.kv->vdata.view(at::kDouble)
                                                : at::ones({e.size(0)}, opt(dev, at::kDouble));
@@ -766,6 +772,7 @@ class PageRankCmd : public Command {
   }
   void run() override {
     MapReduce& mre = obj.input(1, rd(parse_edge), rc(parse_edge));
+    mre.flatten();
     at::Tensor e = mre.kv ? edges_of(*mre.kv) : at::empty({0, 2}, opt(comm->device(), at::kLong));
     const int64_t N = nvert_global(*comm, e);
     PageRankPlan pr(comm, e, N, alpha);

@@ -12,7 +12,7 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
   TriMRRun run;
   const Comm& comm = *mrt.comm();
   auto npairs = [&](MapReduce& m) -> int64_t {
-    const int64_t n = m.kv ? m.kv->n : m.kmv ? m.kmv->nkey : 0;
+    const int64_t n = m.kv ? m.kv_rows() : m.kmv ? m.kmv->nkey : 0;
     return comm.allreduce(n, Comm::SUM);
   };
   // one stage: the op, then a device sync so its kernels count in its time
@@ -75,15 +75,37 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
     });
   });
   stage("add edges", mrt, [&] {
-    // an edge (vi, vj) carries the value vi as its marker (not an empty
-    // value): every pair of collate 4 has one narrow 8-byte value, so the
-    // collate groups them as packed (edge, vertex) words
-    mre.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {
+    // the reference adds the edge MR unchanged (oink/tri_find.cpp:71): the
+    // marked copies go through a temporary MR, the input is left as it was.
+    // An upper edge (vi < vj) carries vi as its marker, not an empty value:
+    // every pair of collate 4 then has one narrow 8-byte value and the
+    // collate groups them as packed (edge, vertex) words. A wedge centre is
+    // never vi then (the centre of wedge (vi, vj) is a third vertex), but it
+    // can be when some edge is not upper (self-loops, vi > vj): then, on
+    // every rank alike, edges carry the reference's empty value instead.
+    int64_t bad = 0;
+    if (mre.kv && mre.kv->n) {
+      mre.flatten();
+      at::Tensor e = edges_of(*mre.kv);
+      bad = (e.select(1, 0) >= e.select(1, 1)).any().item<bool>() ? 1 : 0;
+    }
+    const bool marked_by_vertex = comm.allreduce(bad, Comm::MAX) == 0;
+    MapReduce marked(mre.comm());
+    marked.set = mre.set;
+    marked.map_mr_batch(mre, [&](const KV& src, KeyValue& kv) {
       if (!src.n) return;
       at::Tensor e = edges_of(src);
-      add_tensors(kv, e, e.select(1, 0).contiguous());
+      if (marked_by_vertex) {
+        add_tensors(kv, e, e.select(1, 0).contiguous());
+      } else {
+        KV x = make_kv(e.contiguous().view(at::kByte).view({-1}), c10::nullopt,
+                       at::empty({0}, at::TensorOptions().device(e.device()).dtype(at::kByte)),
+                       at::zeros({src.n + 1}, at::TensorOptions().device(e.device()).dtype(at::kLong)), src.n,
+                       e.device());
+        kv.add_kv(x);
+      }
     });
-    mrt.add(mre);
+    mrt.add(marked);
   });
   stage("collate 4", mrt, [&] { mrt.collate(); });
   stage("reduce emit_triangles", mrt, [&] {

@@ -305,3 +305,26 @@ def test_tri_find_mr_out_of_core_three_ranks():
     for a, b, spooled, want in out.values():
         assert a == b == want
     assert sum(v[2] for v in out.values()) > 0
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_tri_find_mr_leaves_edge_mr_unchanged(dev):
+    """advisor r4: the edge MR tri_find_mr reads (a named OINK object) keeps
+    its pairs and its NULL values (reference oink/tri_find.cpp:71 adds it
+    unchanged); upper edges are marked by their first vertex in a temporary
+    MR, non-upper input falls back to empty-value markers with the same count"""
+    from gpu_mapreduce_amd.models.triangles import tri_find_mr
+    import gpu_mapreduce_amd as gm
+    e = _rmat(8, 8, 3)
+    want = brute_force_count(e.numpy())
+    comm = gm.Comm(device=dev)
+    u = torch.unique(torch.sort(e, dim=1).values[e[:, 0] != e[:, 1]], dim=0)  # upper, no self-loops, no dups
+    r = tri_find_mr(comm, u, upper=False)
+    assert r["triangles"] == want
+    assert r["input_value_width_after"] == 0 and r["input_pairs_after"] == u.shape[0]
+    # non-upper rows (each edge as (vj, vi), vj > vi): edges carry the empty
+    # value marker; wedge keys are (min, max) as in the reference
+    # (oink/tri_find.cpp:219-227), so no such edge closes a wedge — the
+    # reference counts 0 on this input too (its scripts run edge_upper first)
+    r2 = tri_find_mr(comm, torch.flip(u, dims=[1]).contiguous(), upper=False)
+    assert r2["input_value_width_after"] == 0 and r2["triangles"] == 0
