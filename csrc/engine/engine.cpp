@@ -126,12 +126,23 @@ KV to_var_values(const KV& kv) {
 
 namespace {
 // concat of one column (data + optional offsets)
+// cat into a pinned host tensor when `pin` (one copy: no pageable
+// intermediate that is pinned afterwards)
+at::Tensor cat_maybe_pinned(const std::vector<at::Tensor>& ts, at::Device dev, at::ScalarType ty, bool pin) {
+  if (!pin || !dev.is_cpu()) return at::cat(ts, 0);
+  int64_t n = 0;
+  for (auto& t : ts) n += t.numel();
+  at::Tensor out = at::empty({n}, at::TensorOptions().dtype(ty).pinned_memory(true));
+  at::cat_out(out, ts, 0);
+  return out;
+}
+
 void concat_col(const std::vector<const at::Tensor*>& datas, const std::vector<const at::Tensor*>& offs,
                 const std::vector<int64_t>& ns, bool fixed, at::Device dev, at::Tensor* data_out,
-                at::Tensor* off_out) {
+                at::Tensor* off_out, bool pin) {
   std::vector<at::Tensor> d;
   for (auto* t : datas) d.push_back(t->to(dev));
-  *data_out = d.empty() ? at::empty({0}, opt(dev, at::kByte)) : at::cat(d, 0);
+  *data_out = d.empty() ? at::empty({0}, opt(dev, at::kByte)) : cat_maybe_pinned(d, dev, at::kByte, pin);
   if (fixed) return;
   std::vector<at::Tensor> o;
   int64_t base = 0;
@@ -140,11 +151,11 @@ void concat_col(const std::vector<const at::Tensor*>& datas, const std::vector<c
     o.push_back((i + 1 < offs.size() ? oi.narrow(0, 0, ns[i]) : oi) + base);
     base += datas[i]->numel();
   }
-  *off_out = o.empty() ? at::zeros({1}, opt(dev, at::kLong)) : at::cat(o, 0);
+  *off_out = o.empty() ? at::zeros({1}, opt(dev, at::kLong)) : cat_maybe_pinned(o, dev, at::kLong, pin);
 }
 }  // namespace
 
-KV concat(const std::vector<KV>& parts_in, at::Device dev) {
+KV concat(const std::vector<KV>& parts_in, at::Device dev, bool pin) {
   std::vector<KV> parts;
   for (auto& p : parts_in)
     if (p.n > 0) parts.push_back(p);
@@ -178,8 +189,8 @@ KV concat(const std::vector<KV>& parts_in, at::Device dev) {
     ns.push_back(p.n);
     o.n += p.n;
   }
-  concat_col(kd, ko, ns, kf, dev, &o.kdata, &o.koff);
-  concat_col(vd, vo, ns, vf, dev, &o.vdata, &o.voff);
+  concat_col(kd, ko, ns, kf, dev, &o.kdata, &o.koff, pin);
+  concat_col(vd, vo, ns, vf, dev, &o.vdata, &o.voff, pin);
   return o;
 }
 

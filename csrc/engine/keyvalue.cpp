@@ -63,4 +63,25 @@ KV KeyValue::finish() {
   return out;
 }
 
+std::vector<KV> KeyValue::finish_parts() {
+  flush();
+  const KV none = empty_kv(dev_, kw_ >= 0 ? kw_ : 0, vw_ >= 0 ? vw_ : 0);
+  if (spool_) {
+    std::vector<KV> out = spool_->take();
+    last_spool_ = spool_->stats();
+    spool_.reset();
+    done_.reset();
+    if (out.empty()) out.push_back(none);
+    return out;
+  }
+  if (grp_) return {finish()};
+  done_.reset();
+  std::vector<KV> out;
+  for (const KV& c : chunks_)
+    if (c.n) out.push_back(c);
+  chunks_.clear();
+  if (out.empty()) out.push_back(none);
+  return out;
+}
+
 }  // namespace mrh

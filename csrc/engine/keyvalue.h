@@ -89,6 +89,10 @@ class KeyValue {
     return n;
   }
   KV finish();
+  // the same pairs as parts in order, nothing concatenated: the chunks as
+  // added, a spool's pieces where they lie (HBM / pinned host / files), the
+  // grouped arenas as one part. Never empty (one empty KV at least).
+  std::vector<KV> finish_parts();
   at::Device device() const { return dev_; }
 
  private:

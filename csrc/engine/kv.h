@@ -57,7 +57,8 @@ KV empty_kv(at::Device dev, int kw = 0, int vw = 0);
 KV make_kv(at::Tensor kdata, c10::optional<at::Tensor> koff, at::Tensor vdata,
            c10::optional<at::Tensor> voff, int64_t n, at::Device dev);
 KV kv_to(const KV& kv, at::Device dev);
-KV concat(const std::vector<KV>& parts, at::Device dev);
+// pin: a CPU result goes straight into pinned host memory
+KV concat(const std::vector<KV>& parts, at::Device dev, bool pin = false);
 KV to_var_keys(const KV& kv);
 KV to_var_values(const KV& kv);
 // offsets of a fixed-width column: [0, w, 2w, ...]

@@ -380,35 +380,27 @@ OocEnv MapReduce::ooc_env() const {
   return e;
 }
 
-// concatenation of the KV's parts: on the device, or — for a bounded MR —
-// where the budgets allow (out-of-core data is written once, to pinned host
-// memory or one spool file)
-KV MapReduce::append_kv(const KV& a, const KV& b) {
-  if (budget() <= 0 && set.host_budget <= 0) return concat({a, b}, device());
-  if (!a.device().is_cuda() && device().is_cuda()) {
-    const int64_t total = a.nbytes() + b.nbytes();
-    if (set.host_budget <= 0 || total <= set.host_budget) {
-      // one pinned output of the final size, each part copied in once
-      KV o = concat({a, b}, at::Device(at::kCPU));
-      auto pin = [](const at::Tensor& t) { return t.defined() && !t.is_pinned() ? t.pin_memory() : t; };
-      o.kdata = pin(o.kdata);
-      o.vdata = pin(o.vdata);
-      o.koff = pin(o.koff);
-      o.voff = pin(o.voff);
-      spool_stats.host_bytes += total;
-      return o;
-    }
-    spool_stats.files++;
-    spool_stats.disk_bytes += total;
-    return kv_to_file({a, b}, spool_path(set.fpath, "kv", instance_me_, comm_->rank()));
+// concatenation of the KV's parts (one pass over all of them): on the
+// device, or — for a bounded MR — where the budgets allow (data past the HBM
+// budget is written once, to pinned host memory or one spool file)
+KV MapReduce::concat_parts(const std::vector<KV>& parts) {
+  if (parts.size() == 1) return parts[0];
+  int64_t total = 0;
+  bool on_dev = true;
+  for (const KV& p : parts) {
+    total += p.nbytes();
+    on_dev = on_dev && p.device() == device();
   }
-  KeyValue tmp(device());
-  bound(tmp);
-  tmp.add_kv(a);
-  tmp.add_kv(b);
-  KV o = tmp.finish();
-  note_spool(tmp);
-  return o;
+  if ((budget() <= 0 && set.host_budget <= 0) || !device().is_cuda() || (on_dev && (budget() <= 0 || total <= budget())))
+    return concat(parts, device());
+  if (set.host_budget <= 0 || total <= set.host_budget) {
+    KV o = concat(parts, at::Device(at::kCPU), /*pin=*/true);  // written once, straight to pinned memory
+    spool_stats.host_bytes += total;
+    return o;
+  }
+  spool_stats.files++;
+  spool_stats.disk_bytes += total;
+  return kv_to_file(parts, spool_path(set.fpath, "kv", instance_me_, comm_->rank()));
 }
 
 std::vector<KV> MapReduce::kv_parts() const {
@@ -426,10 +418,20 @@ int64_t MapReduce::kv_rows() const {
 
 void MapReduce::flatten() {
   if (kv_tail_.empty()) return;
-  std::vector<KV> tail;
-  tail.swap(kv_tail_);
-  for (const KV& t : tail) kv = kv ? append_kv(*kv, t) : t;
+  std::vector<KV> parts = kv_parts();
+  kv_tail_.clear();
+  kv = concat_parts(parts);
   grouped_.reset();
+}
+
+void MapReduce::set_kv_parts(std::vector<KV> parts) {
+  kv_tail_.clear();
+  kv.reset();
+  grouped_.reset();
+  for (size_t i = 0; i < parts.size(); ++i) {
+    if (i == 0) kv = parts[0];
+    else if (parts[i].n) kv_tail_.push_back(parts[i]);
+  }
 }
 
 void MapReduce::append_part(const KV& b) {
@@ -638,14 +640,14 @@ std::vector<int> MapReduce::my_tasks(int nmap) {  // :1102-1225
 }
 
 uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) {
-  KV n = kvb.finish();
+  // the builder's chunks / spool pieces become the KV's parts (no concatenation)
+  std::vector<KV> n = kvb.finish_parts();
   note_spool(kvb);
   std::shared_ptr<GroupIndex> g = kvb.take_group();
   if (addflag && kv) {
-    append_part(n);
+    for (const KV& p : n) append_part(p);
   } else {
-    kv_tail_.clear();
-    kv = n;
+    set_kv_parts(std::move(n));
     grouped_ = g;
   }
   kmv.reset();
@@ -1202,11 +1204,11 @@ uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
   KeyValue kvb(device());
   bound(kvb);
   run_host_kmv(*kmv, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
-  kv = kvb.finish();
+  set_kv_parts(kvb.finish_parts());
   note_spool(kvb);
   kmv.reset();
   stats("Reduce", 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dtype) {
@@ -1243,11 +1245,11 @@ uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
   } else {
     fn(*kmv, kvb);
   }
-  kv = kvb.finish();
+  set_kv_parts(kvb.finish_parts());
   note_spool(kvb);
   kmv.reset();
   stats("Reduce", 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
@@ -1259,10 +1261,10 @@ uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
   KeyValue kvb(device());
   bound(kvb);
   run_host_kmv(m, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
-  kv = kvb.finish();
+  set_kv_parts(kvb.finish_parts());
   note_spool(kvb);
   stats("Compress", 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& dtype) {

@@ -213,9 +213,11 @@ class MapReduce {
   void append_part(const KV& b);
   // the KV and its appended parts, in order
   std::vector<KV> kv_parts() const;
+  // the KV becomes `parts` (a builder's parts: no concatenation)
+  void set_kv_parts(std::vector<KV> parts);
   int64_t data_bytes() const;
   void bound(KeyValue& b);
-  KV append_kv(const KV& a, const KV& b);
+  KV concat_parts(const std::vector<KV>& parts);
  public:
   // the tiers and names an out-of-core op of this MR may use
   OocEnv ooc_env() const;

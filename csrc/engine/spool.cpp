@@ -378,6 +378,13 @@ void Spool::clear() {
   n_ = bytes_ = 0;
 }
 
+std::vector<KV> Spool::take() {
+  sync();
+  std::vector<KV> parts = pieces_;
+  clear();
+  return parts;
+}
+
 KV Spool::gather_host() {
   sync();
   if (pieces_.empty()) {
@@ -389,17 +396,7 @@ KV Spool::gather_host() {
   clear();  // budget shares back before deciding where the whole goes
   SpoolBudget& B = *cfg_.budget;
   if (parts.size() == 1 && parts[0].device().is_cpu()) return parts[0];
-  if (B.host < 0 || B.host >= total) {
-    KV o = concat(parts, at::Device(at::kCPU));
-    if (dev_.is_cuda()) {
-      auto pin = [](const at::Tensor& t) { return t.defined() && !t.is_pinned() ? t.pin_memory() : t; };
-      o.kdata = pin(o.kdata);
-      o.vdata = pin(o.vdata);
-      o.koff = pin(o.koff);
-      o.voff = pin(o.voff);
-    }
-    return o;
-  }
+  if (B.host < 0 || B.host >= total) return concat(parts, at::Device(at::kCPU), /*pin=*/dev_.is_cuda());
   st_.files++;
   st_.disk_bytes += total;
   return kv_to_file(parts, next_path());

@@ -87,6 +87,9 @@ class Spool {
   KV gather();
   // every piece as one HOST KV (pinned if it fits the host tier, else a file)
   KV gather_host();
+  // every piece as it is (HBM / pinned host / file), in order, nothing
+  // concatenated; the spool is empty afterwards (budget shares returned)
+  std::vector<KV> take();
   void clear();
   const SpoolStats& stats() const { return st_; }
 
