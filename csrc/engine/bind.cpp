@@ -689,6 +689,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["spool_host_bytes"] = spool_host;
         d["spool_disk_bytes"] = spool_disk;
         d["input_value_width_after"] = in_vw;
+        d["compact_vb"] = r.compact_vb;
         d["input_pairs_after"] = in_n;
         return d;
       },

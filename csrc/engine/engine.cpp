@@ -637,31 +637,43 @@ bool packed_pairs_disabled() {
 // afterwards (the values are the low bits, the unique keys unpacked from
 // the heads). The pairs may come in parts (a KV with appended parts,
 // mapreduce.h): each part is packed in place into its rows of the sort
-// input, nothing is concatenated. Returns false when the pairs are not that
-// narrow.
-bool convert_packed_parts(const std::vector<KV>& parts_in, KMV* out, ConvertStats* st) {
+// input and released, nothing is concatenated. Values may be 4 or 8 bytes.
+// Key + value bits past 64 (R-MAT-22 wedges: 44 + 22), or more than 2^31
+// pairs, take B bucket bits: a stable partition by (low B key bits) ^
+// mix(other key bits) — balanced for skewed keys, and invertible — then one
+// sort per bucket; keys then come out bucket by bucket, in key order inside
+// a bucket. Returns false when the pairs are not that narrow.
+namespace {
+inline uint32_t split_mix_host(uint64_t rest, int B) {
+  return B ? (uint32_t)((rest * 0x9E3779B97F4A7C15ull) >> (64 - B)) : 0u;
+}
+}  // namespace
+
+bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st) {
   if (packed_pairs_disabled()) return false;
   std::vector<KV> parts;
-  for (const KV& p : parts_in)
+  for (const KV& p : parts_io)
     if (p.n > 0) parts.push_back(p);
   if (parts.empty()) return false;
-  const KV& k0 = parts[0];
-  if (!k0.kfixed() || k0.kw < 8 || k0.kw % 8 || k0.kw > 64 || k0.vw != 8) return false;
+  // widths and device by value: the parts are released while packing
+  const int vw = parts[0].vw, kwidth = parts[0].kw;
+  if (kwidth < 8 || kwidth % 8 || kwidth > 64 || (vw != 8 && vw != 4)) return false;
   auto aligned = [&](const at::Tensor& t, int64_t bytes) {
     return t.defined() && t.is_contiguous() && reinterpret_cast<uintptr_t>(t.data_ptr()) % 8 == 0 && t.numel() >= bytes;
   };
-  const at::Device dev = k0.device();
-  const int nw = k0.kw / 8;
+  const at::Device dev = parts[0].device();
+  const bool cuda = dev.is_cuda();
+  const int nw = kwidth / 8;
   int64_t n = 0;
   std::vector<at::Tensor> mm;  // per part: key word minima, maxima, value min, max
   for (const KV& p : parts) {
-    if (p.kw != k0.kw || p.vw != 8 || p.device() != dev) return false;
-    if (!aligned(p.kdata, p.n * p.kw) || !aligned(p.vdata, p.n * 8)) return false;
+    if (p.kw != kwidth || p.vw != vw || p.device() != dev) return false;
+    if (!aligned(p.kdata, p.n * p.kw) || !aligned(p.vdata, p.n * vw)) return false;
     at::Tensor kw = p.kdata.narrow(0, 0, p.n * p.kw).view(at::kLong).view({p.n, nw});
-    at::Tensor vv = p.vdata.narrow(0, 0, p.n * 8).view(at::kLong);
+    at::Tensor vv = p.vdata.narrow(0, 0, p.n * vw).view(vw == 8 ? at::kLong : at::kInt);
     auto [kmn, kmx] = at::aminmax(kw, 0);
     auto [vmn, vmx] = at::aminmax(vv);
-    mm.push_back(at::cat({kmn, kmx, vmn.view({1}), vmx.view({1})}).view({1, -1}));
+    mm.push_back(at::cat({kmn, kmx, vmn.to(at::kLong).view({1}), vmx.to(at::kLong).view({1})}).view({1, -1}));
     n += p.n;
   }
   // one host sync for every part's ranges; the packing covers all of them
@@ -675,80 +687,150 @@ bool convert_packed_parts(const std::vector<KV>& parts_in, KMV* out, ConvertStat
     for (int64_t i = 1; i < np; ++i) {
       const int64_t x = ap[i * row + j];
       // signed compare is right for the bit-width test below (a negative
-      // word needs 64 bits either way)
+      // word needs all its bits either way)
       v = is_min ? std::min(v, x) : std::max(v, x);
     }
     b[j] = v;
   }
-  auto bits_of = [](int64_t lo, int64_t hi) { return lo < 0 ? 64 : (hi == 0 ? 0 : 64 - __builtin_clzll((uint64_t)hi)); };
-  const int vbits = std::max(1, bits_of(b[2 * nw], b[2 * nw + 1]));
+  auto bits_of = [](int64_t lo, int64_t hi, int width) {
+    return lo < 0 ? width : (hi == 0 ? 0 : 64 - __builtin_clzll((uint64_t)hi));
+  };
+  const int vbits = std::max(1, bits_of(b[2 * nw], b[2 * nw + 1], 8 * vw));
   if (vbits >= 64) return false;
-  k::PackShifts sh{};
-  sh.nw = nw;
+  k::PackShifts sh{}, wb{};  // key word shifts inside K (from bit 0), and their widths
+  sh.nw = wb.nw = nw;
   std::vector<int> kwbits(nw);
   int kbits = 0;
   for (int w = 0; w < nw; ++w) {
-    kwbits[w] = bits_of(b[w], b[nw + w]);
-    sh.s[w] = kwbits[w] ? vbits + kbits : -1;
+    kwbits[w] = bits_of(b[w], b[nw + w], 64);
+    sh.s[w] = kwbits[w] ? kbits : -1;
+    wb.s[w] = kwbits[w];
     kbits += kwbits[w];
   }
-  if (kbits + vbits > 64) return false;
-  at::Tensor packed = at::empty({n}, opt(dev, at::kLong));
+  if (kbits > 64) return false;
+  // B bucket bits: what does not fit one sort word, and enough buckets that
+  // each stays below 2^30 pairs (sort buffers, 32-bit segment positions)
+  int B = std::max(0, kbits + vbits - 64);
+  if (n > (int64_t(1) << 31)) {
+    int need = 0;
+    while ((n >> need) > (int64_t(1) << 30)) ++need;
+    B = std::max(B, need);
+  }
+  if (B > 8 || B > kbits) return false;  // at most 256 buckets (the partition kernels' LDS histogram)
+  const int M = 1 << B;
+  parts_io.clear();  // from here on this function holds the only references
+  const int sbits = kbits - B;  // key bits inside a sort word, above the value
+  // every part packed in place into its rows, then released
+  at::Tensor words = at::empty({n}, opt(dev, at::kLong));
+  at::Tensor bkt = B ? at::empty({n}, opt(dev, at::kInt)) : at::Tensor();
   int64_t row0 = 0;
-  for (const KV& p : parts) {  // every part packed in place into its rows
+  for (KV& p : parts) {
     const uint64_t* kd = reinterpret_cast<const uint64_t*>(p.kdata.data_ptr());
-    const uint64_t* vd = reinterpret_cast<const uint64_t*>(p.vdata.data_ptr());
-    uint64_t* o = P0<uint64_t>(packed) + row0;
-    if (dev.is_cuda()) {
-      k::pack_kv(kd, vd, p.n, sh, o, cur_stream());
+    uint64_t* o = P0<uint64_t>(words) + row0;
+    int32_t* bo = B ? P0<int32_t>(bkt) + row0 : nullptr;
+    if (cuda) {
+      k::pack_kv_split(kd, p.vdata.data_ptr(), vw, p.n, sh, vbits, B, o, bo, cur_stream());
     } else {
       for (int64_t i = 0; i < p.n; ++i) {
-        uint64_t kk = vd[i];
+        uint64_t K = 0;
         for (int w = 0; w < nw; ++w)
-          if (sh.s[w] >= 0) kk |= kd[i * nw + w] << sh.s[w];
-        o[i] = kk;
+          if (sh.s[w] >= 0) K |= kd[i * nw + w] << sh.s[w];
+        const uint64_t v = vw == 4 ? (uint64_t)static_cast<const uint32_t*>(p.vdata.data_ptr())[i]
+                                   : static_cast<const uint64_t*>(p.vdata.data_ptr())[i];
+        const uint64_t rest = B ? K >> B : K;
+        o[i] = (rest << vbits) | v;
+        if (bo) bo[i] = (int32_t)((uint32_t)(K & ((1ull << B) - 1)) ^ split_mix_host(rest, B));
       }
     }
     row0 += p.n;
+    p = KV();  // the part's memory goes back while the others are packed
   }
   parts.clear();
-  at::Tensor sk = kbits > 0 ? radix_sort_keys(packed, vbits, vbits + kbits, false) : packed;
-  packed = at::Tensor();
-  at::Tensor keyp = at::bitwise_right_shift(sk, vbits);
-  at::Tensor flags, pos, seg;
-  int64_t nseg = 0;
-  segments_from_sorted(keyp, &flags, &pos, &seg, &nseg);
-  flags = pos = at::Tensor();
-  at::Tensor heads = keyp.index_select(0, seg.narrow(0, 0, nseg));
-  keyp = at::Tensor();
-  std::vector<at::Tensor> cols;
-  int off = 0;
-  for (int w = 0; w < nw; ++w) {
-    if (!kwbits[w]) {
-      cols.push_back(at::zeros({nseg}, opt(dev, at::kLong)));
-      continue;
-    }
-    at::Tensor c = at::bitwise_right_shift(heads, off);
-    if (off + kwbits[w] < 64) c = at::bitwise_and(c, (int64_t)((1ull << kwbits[w]) - 1));
-    cols.push_back(c);
-    off += kwbits[w];
+  // buckets (B > 0): a stable partition of the sort words, balanced by the mix
+  std::vector<int64_t> bcount{n};
+  if (B) {
+    KV w;
+    w.n = n;
+    w.kw = 8;
+    w.vw = 0;
+    w.kdata = words.view(at::kByte);
+    w.vdata = at::empty({0}, opt(dev, at::kByte));
+    Buckets bk = bucket_local(w, bkt, M);
+    bkt = at::Tensor();
+    words = bk.kv.kdata.view(at::kLong);
+    bcount = bk.count;
   }
+  at::Tensor vout = at::empty({n * vw}, opt(dev, at::kByte));
+  std::vector<at::Tensor> keys_b, seg_b;
+  int64_t v0 = 0, nseg = 0, passes = 0;
+  for (int bi = 0; bi < (int)bcount.size(); ++bi) {
+    const int64_t nb = bcount[bi];
+    if (nb == 0) continue;
+    at::Tensor wsl = words.narrow(0, v0, nb);
+    at::Tensor sk = sbits > 0 ? radix_sort_keys(wsl, vbits, vbits + sbits, false) : wsl;
+    passes += (sbits + 7) / 8;
+    // the key bits above the value (a logical shift: the word's top bit may be set)
+    at::Tensor keyp = sbits > 0 ? at::bitwise_right_shift(sk, vbits) : at::zeros({nb}, opt(dev, at::kLong));
+    if (sbits > 0 && sbits < 64) keyp = at::bitwise_and(keyp, (int64_t)((1ull << sbits) - 1));
+    at::Tensor flags, pos, seg;
+    int64_t ns = 0;
+    segments_from_sorted(keyp, &flags, &pos, &seg, &ns);
+    flags = pos = at::Tensor();
+    at::Tensor heads = keyp.index_select(0, seg.narrow(0, 0, ns));
+    keyp = at::Tensor();
+    at::Tensor kb = at::empty({ns, nw}, opt(dev, at::kLong));
+    if (cuda) {
+      k::unpack_split(P0<uint64_t>(heads), ns, bi, B, sh, wb, P0<uint64_t>(kb), cur_stream());
+      k::split_values(P0<uint64_t>(sk), nb, vbits, vw, P0<uint8_t>(vout) + v0 * vw, cur_stream());
+    } else {
+      const uint64_t* hp = P0<uint64_t>(heads);
+      uint64_t* kp = P0<uint64_t>(kb);
+      for (int64_t j = 0; j < ns; ++j) {
+        const uint64_t rest = hp[j];
+        const uint64_t K = B ? (rest << B) | (uint64_t)(((uint32_t)bi ^ split_mix_host(rest, B)) & ((1u << B) - 1)) : rest;
+        for (int w = 0; w < nw; ++w) {
+          uint64_t x = 0;
+          if (sh.s[w] >= 0) {
+            x = K >> sh.s[w];
+            if (wb.s[w] < 64) x &= (1ull << wb.s[w]) - 1;
+          }
+          kp[j * nw + w] = x;
+        }
+      }
+      const uint64_t* sp = P0<uint64_t>(sk);
+      uint8_t* vo = P0<uint8_t>(vout) + v0 * vw;
+      for (int64_t i = 0; i < nb; ++i) {
+        const uint64_t v = sp[i] & ((1ull << vbits) - 1);
+        if (vw == 4) reinterpret_cast<uint32_t*>(vo)[i] = (uint32_t)v;
+        else reinterpret_cast<uint64_t*>(vo)[i] = v;
+      }
+    }
+    keys_b.push_back(kb);
+    seg_b.push_back(seg.narrow(0, 0, ns) + v0);
+    v0 += nb;
+    nseg += ns;
+  }
+  words = at::Tensor();
+  seg_b.push_back(at::full({1}, n, opt(dev, at::kLong)));
   out->keys.n = nseg;
-  out->keys.kw = k0.kw;
+  out->keys.kw = kwidth;
   out->keys.vw = 0;
-  out->keys.kdata = at::stack(cols, 1).contiguous().view(at::kByte).view({-1});
+  out->keys.kdata = (keys_b.size() == 1 ? keys_b[0] : at::cat(keys_b, 0)).contiguous().view(at::kByte).view({-1});
   out->keys.vdata = at::empty({0}, opt(dev, at::kByte));
-  out->vw = 8;
-  out->vdata = at::bitwise_and(sk, (int64_t)((1ull << vbits) - 1)).contiguous().view(at::kByte).view({-1});
-  out->seg = seg;
+  out->vw = vw;
+  out->vdata = vout;
+  out->seg = at::cat(seg_b, 0);
   out->nkey = nseg;
   out->nval = n;
   st->exact = true;
-  st->passes = (kbits + 7) / 8;
+  st->passes = passes + (B ? 1 : 0);
   return true;
 }
 
-bool convert_packed_pairs(const KV& kv, KMV* out, ConvertStats* st) { return convert_packed_parts({kv}, out, st); }
+bool convert_packed_pairs(const KV& kv, KMV* out, ConvertStats* st) {
+  std::vector<KV> parts{kv};
+  return convert_packed_parts(parts, out, st);
+}
 
 KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tensor& prehash) {
   const at::Device dev = kv.device();
@@ -764,9 +846,9 @@ KMV convert(const KV& kv, ConvertStats* st, int force_hash_bits, const at::Tenso
     return out;
   }
   const int64_t n = kv.n;
-  if (n > 0xFFFFFFFFll) fail("convert: more than 2^32 pairs on one rank");
   if (force_hash_bits >= 64 && !prehash.defined() && !packed_pairs_disabled() && convert_packed_pairs(kv, &out, st))
     return out;
+  if (n > 0xFFFFFFFFll) fail("convert: more than 2^32 pairs on one rank (only narrow pairs group past that)");
   at::Tensor sk_in, idx;
   int end_bit;
   st->exact = kv.kfixed() && kv.kw <= 8 && force_hash_bits >= 64;

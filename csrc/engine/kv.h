@@ -102,8 +102,11 @@ struct ConvertStats {
 // prehash (optional): hash64_keys(kv) already computed by the producer
 KMV convert(const KV& kv, ConvertStats* st = nullptr, int force_hash_bits = 64, const at::Tensor& prehash = {});
 // convert of a KV given as parts (in order), for the packed-pairs case
-// (narrow fixed keys and 8-byte values); false = not applicable, nothing done
-bool convert_packed_parts(const std::vector<KV>& parts, KMV* out, ConvertStats* st);
+// (narrow fixed keys and 4- or 8-byte values); false = not applicable,
+// nothing done and `parts` untouched. Otherwise `parts` is emptied: each
+// part is released once packed, so a caller holding no other reference
+// peaks at ~ the parts + 8 bytes a pair
+bool convert_packed_parts(std::vector<KV>& parts, KMV* out, ConvertStats* st);
 // one value per key (MR-MPI clone)
 KMV clone(const KV& kv);
 // whole KV -> one KMV pair key -> [k0,v0,k1,v1,...] (MR-MPI collapse)

@@ -983,19 +983,6 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
     // part where it lies
     kmv = ooc_convert(kv_parts(), ooc_env(), device(), &os);
     note_ooc("Convert", os);
-  } else if (!kv_tail_.empty()) {
-    // appended parts: grouped together (packed pairs read every part in
-    // place), or concatenated once for the other paths
-    std::vector<KV> parts = kv_parts();
-    bool all_dev = true;
-    for (const KV& p : parts) all_dev = all_dev && p.device() == device();
-    KMV m;
-    if (all_dev && convert_packed_parts(parts, &m, &last_convert)) {
-      kmv = std::move(m);
-    } else {
-      flatten();
-      kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert, 64); });
-    }
   } else if (grouped_ && grouped_->describes(*kv) && !prehash.defined()) {
     // grouped while the map produced it: only the two short sorts are left
     KMV m;
@@ -1006,6 +993,29 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
       last_convert = ConvertStats();
       kmv = mrh::convert(*kv, &last_convert, 64);  // a 64-bit hash collision: exact regroup
       last_convert.grouped = 2;
+    }
+  } else if (!prehash.defined() && (!kv_tail_.empty() || kv->kfixed())) {
+    // narrow pairs, possibly in parts: grouped with every part read in place
+    // and released once packed (packed pairs), else concatenated once for
+    // the other paths
+    std::vector<KV> parts = kv_parts();
+    bool all_dev = true;
+    for (const KV& p : parts) all_dev = all_dev && p.device() == device();
+    KMV m;
+    bool done = false;
+    if (all_dev) {
+      // the converter holds the only references: every part is freed once packed
+      kv.reset();
+      kv_tail_.clear();
+      grouped_.reset();
+      done = convert_packed_parts(parts, &m, &last_convert);
+      if (!done) set_kv_parts(std::move(parts));
+    }
+    if (done) {
+      kmv = std::move(m);
+    } else {
+      flatten();
+      kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert, 64); });
     }
   } else {
     kmv = oom_retry(this, device(), my_proc(), "convert",

@@ -59,5 +59,8 @@ std::pair<at::Tensor, at::Tensor> trimr_low_degree(const KV& kv);
 // tri_find_mr's last collate, fixed 8-byte values: an edge (vi, vj) carries
 // the value vi (a wedge's centre is never one of its key's endpoints), so
 // the pairs stay narrow (vertex-sized values) and group as packed words
-at::Tensor trimr_emit(const KMV& m);
+// compact_vb > 0: the compact layout of large graphs — keys one packed word
+// vi << compact_vb | vj, values u32 (wedges 12 bytes instead of 24)
+at::Tensor trimr_emit(const KMV& m, int compact_vb = 0);
+at::Tensor trimr_emit_compact(const KMV& m, int vb);
 }  // namespace mrh

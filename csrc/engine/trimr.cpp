@@ -97,11 +97,51 @@ std::pair<at::Tensor, at::Tensor> trimr_low_degree(const KV& kv) {
   return {key, val};
 }
 
+// Compact layout (large graphs): keys are one packed word vi << vb | vj,
+// values u32 centres; an edge carries vi as its marker (tri.h)
+at::Tensor trimr_emit_compact(const KMV& m, int vb) {
+  const at::Device dev = m.seg.device();
+  if (!m.nkey || !m.nval) return at::empty({0, 3}, opt(dev, at::kLong));
+  need(m.keys.kw == 8 && m.vw == 4, "tri_find_mr emit (compact): packed 8-byte edge keys, 4-byte centres");
+  const int64_t* seg = P0<int64_t>(m.seg);
+  const int64_t* ek = P0<int64_t>(m.keys.kdata);
+  if (dev.is_cuda()) {
+    const int64_t nval = m.nval;
+    at::Tensor marked = at::zeros({m.nkey}, opt(dev, at::kByte));
+    const int64_t nt = k::trimr_emit_tiles(nval);
+    at::Tensor tcount = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kLong));
+    const void* vals = m.vdata.data_ptr();
+    k::trimr_emit_fixed(0, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, nullptr, ek, nullptr, vb, cur());
+    k::trimr_emit_fixed(1, seg, m.nkey, nval, vals, P0<uint8_t>(marked), P0<int64_t>(tcount), nullptr, ek, nullptr, vb,
+                        cur());
+    at::Tensor tbase = exclusive_scan(tcount.narrow(0, 0, nt).contiguous());
+    const int64_t T = nt > 0 ? tbase[nt].item<int64_t>() : 0;
+    at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
+    if (T)
+      k::trimr_emit_fixed(2, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, P0<int64_t>(tbase), ek,
+                          P0<int64_t>(out), vb, cur());
+    return out;
+  }
+  const uint32_t* v = P0<uint32_t>(m.vdata);
+  const uint64_t mask = (1ull << vb) - 1;
+  std::vector<int64_t> rows;
+  for (int64_t s = 0; s < m.nkey; ++s) {
+    const int64_t vi = (int64_t)((uint64_t)ek[s] >> vb), vj = (int64_t)((uint64_t)ek[s] & mask);
+    bool marker = false;
+    for (int64_t j = seg[s]; j < seg[s + 1]; ++j) marker |= (int64_t)v[j] == vi;
+    if (!marker) continue;
+    for (int64_t j = seg[s]; j < seg[s + 1]; ++j)
+      if ((int64_t)v[j] != vi) rows.insert(rows.end(), {(int64_t)v[j], vi, vj});
+  }
+  return at::tensor(rows, opt(at::kCPU, at::kLong)).view({-1, 3});
+}
+
 // Edge markers: an empty value (the reference's NULL) or, with fixed 8-byte
 // values, the key's first vertex (tri.h) — the pipeline marks its edges
 // that way so that the last collate moves one narrow fixed-width value column
-at::Tensor trimr_emit(const KMV& m) {
+at::Tensor trimr_emit(const KMV& m, int compact_vb) {
   const at::Device dev = m.seg.device();
+  if (compact_vb > 0) return trimr_emit_compact(m, compact_vb);
   // fixed widths other than 8: only markers (0) or no marker at all
   if (!m.nkey || (m.vw >= 0 && m.vw != 8)) return at::empty({0, 3}, opt(dev, at::kLong));
   need(m.keys.kw == 16, "tri_find_mr emit: EDGE keys");
@@ -115,15 +155,15 @@ at::Tensor trimr_emit(const KMV& m) {
     at::Tensor marked = at::zeros({m.nkey}, opt(dev, at::kByte));
     const int64_t nt = k::trimr_emit_tiles(nval);
     at::Tensor tcount = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kLong));
-    k::trimr_emit_fixed(0, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, nullptr, ek, nullptr, cur());
-    k::trimr_emit_fixed(1, seg, m.nkey, nval, vals, P0<uint8_t>(marked), P0<int64_t>(tcount), nullptr, ek, nullptr,
+    k::trimr_emit_fixed(0, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, nullptr, ek, nullptr, 0, cur());
+    k::trimr_emit_fixed(1, seg, m.nkey, nval, vals, P0<uint8_t>(marked), P0<int64_t>(tcount), nullptr, ek, nullptr, 0,
                         cur());
     at::Tensor tbase = exclusive_scan(tcount.narrow(0, 0, nt).contiguous());
     const int64_t T = nt > 0 ? tbase[nt].item<int64_t>() : 0;
     at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
     if (T)
       k::trimr_emit_fixed(2, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, P0<int64_t>(tbase), ek,
-                          P0<int64_t>(out), cur());
+                          P0<int64_t>(out), 0, cur());
     return out;
   }
   if (dev.is_cuda()) {

@@ -210,6 +210,58 @@ __global__ __launch_bounds__(NT) void k_pack_kv(const uint64_t* __restrict__ kd,
   out[i] = k;
 }
 
+// narrow pairs whose key and value bits together exceed one u64 by B <= 16
+// bits (or whose count asks for buckets): the key K (words at shifts s[w],
+// relative to bit 0) is cut into rest = K >> B and low = K & (2^B - 1); the
+// pair goes to bucket low ^ mix(rest) (balanced for skewed keys, and
+// invertible: low = bucket ^ mix(rest)) and its sort word is
+// rest << vbits | value. vw: value width 4 (u32) or 8 (u64).
+__device__ __forceinline__ uint32_t split_mix(uint64_t rest, int B) {
+  return B ? (uint32_t)((rest * 0x9E3779B97F4A7C15ull) >> (64 - B)) : 0u;
+}
+__global__ __launch_bounds__(NT) void k_pack_kv_split(const uint64_t* __restrict__ kd, const void* __restrict__ vd,
+                                                     int vw, int64_t n, PackShifts sh, int vbits, int B,
+                                                     uint64_t* __restrict__ out, int32_t* __restrict__ bkt) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  uint64_t K = 0;
+  for (int w = 0; w < sh.nw; ++w)
+    if (sh.s[w] >= 0) K |= kd[i * sh.nw + w] << sh.s[w];
+  const uint64_t v = vw == 4 ? (uint64_t)static_cast<const uint32_t*>(vd)[i] : static_cast<const uint64_t*>(vd)[i];
+  const uint64_t rest = B ? K >> B : K;
+  out[i] = (rest << vbits) | v;
+  if (bkt) bkt[i] = (int32_t)((uint32_t)(K & ((1ull << B) - 1)) ^ split_mix(rest, B));
+}
+
+// the unique keys of one bucket back to key words: heads hold rest (the
+// sorted words shifted down by vbits); K = rest << B | (bucket ^ mix(rest));
+// word w = (K >> s[w]) & mask[w]
+__global__ __launch_bounds__(NT) void k_unpack_split(const uint64_t* __restrict__ heads, int64_t m, int bucket, int B,
+                                                    PackShifts sh, PackShifts bits, uint64_t* __restrict__ keys) {
+  const int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (j >= m) return;
+  const uint64_t rest = heads[j];
+  const uint64_t K = B ? (rest << B) | (uint64_t)(((uint32_t)bucket ^ split_mix(rest, B)) & ((1u << B) - 1)) : rest;
+  for (int w = 0; w < sh.nw; ++w) {
+    uint64_t x = 0;
+    if (sh.s[w] >= 0) {
+      x = K >> sh.s[w];
+      if (bits.s[w] < 64) x &= (1ull << bits.s[w]) - 1;
+    }
+    keys[j * sh.nw + w] = x;
+  }
+}
+
+// values of sorted words: the low vbits, as u32 (vw 4) or u64 (vw 8)
+__global__ __launch_bounds__(NT) void k_split_values(const uint64_t* __restrict__ words, int64_t n, int vbits, int vw,
+                                                    void* __restrict__ vout) {
+  const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t v = vbits >= 64 ? words[i] : words[i] & ((1ull << vbits) - 1);
+  if (vw == 4) static_cast<uint32_t*>(vout)[i] = (uint32_t)v;
+  else static_cast<uint64_t*>(vout)[i] = v;
+}
+
 // head bitmap (bit i of 64-bit word i / 64 set where a segment starts) ->
 // per-word counts, then the positions of the set bits (one word per thread)
 __global__ __launch_bounds__(NT) void k_bits_count(const uint64_t* __restrict__ H, int64_t nw,
@@ -430,6 +482,25 @@ void pack_words(const uint64_t* kd, int64_t n, const PackShifts& sh, uint64_t* o
 void pack_kv(const uint64_t* kd, const uint64_t* vd, int64_t n, const PackShifts& sh, uint64_t* out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_pack_kv, dim3(nblk(n)), dim3(NT), 0, s, kd, vd, n, sh, out);
+  MRH_CHECK_LAUNCH();
+}
+void pack_kv_split(const uint64_t* kd, const void* vd, int vw, int64_t n, const PackShifts& sh, int vbits, int B,
+                   uint64_t* out, int32_t* bkt, hipStream_t s) {
+  if (n <= 0) return;
+  check_arg(vw == 4 || vw == 8, "pack_kv_split: 4- or 8-byte values");
+  check_arg(B >= 0 && B <= 16, "pack_kv_split: at most 16 bucket bits");
+  hipLaunchKernelGGL(k_pack_kv_split, dim3(nblk(n)), dim3(NT), 0, s, kd, vd, vw, n, sh, vbits, B, out, bkt);
+  MRH_CHECK_LAUNCH();
+}
+void unpack_split(const uint64_t* heads, int64_t m, int bucket, int B, const PackShifts& sh, const PackShifts& bits,
+                  uint64_t* keys, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_unpack_split, dim3(nblk(m)), dim3(NT), 0, s, heads, m, bucket, B, sh, bits, keys);
+  MRH_CHECK_LAUNCH();
+}
+void split_values(const uint64_t* words, int64_t n, int vbits, int vw, void* vout, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_split_values, dim3(nblk(n)), dim3(NT), 0, s, words, n, vbits, vw, vout);
   MRH_CHECK_LAUNCH();
 }
 void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s) {

@@ -135,6 +135,17 @@ struct PackShifts {
 void pack_words(const uint64_t* kd, int64_t n, const PackShifts& sh, uint64_t* out, uint32_t* idx, hipStream_t s);
 // out[i] = vd[i] | OR of key word w << s[w] (narrow keys and values on one u64)
 void pack_kv(const uint64_t* kd, const uint64_t* vd, int64_t n, const PackShifts& sh, uint64_t* out, hipStream_t s);
+// narrow pairs past one u64 (kvops.hip k_pack_kv_split): out[i] =
+// (K >> B) << vbits | value, bkt[i] = low B bits of K ^ mix(K >> B) (bkt may
+// be null when B == 0); vw 4 or 8; shifts s[w] place key word w in K
+void pack_kv_split(const uint64_t* kd, const void* vd, int vw, int64_t n, const PackShifts& sh, int vbits, int B,
+                   uint64_t* out, int32_t* bkt, hipStream_t s);
+// keys[j * nw + w] from the sorted heads (rest) of bucket `bucket`; bits.s[w]:
+// significant bits of word w
+void unpack_split(const uint64_t* heads, int64_t m, int bucket, int B, const PackShifts& sh, const PackShifts& bits,
+                  uint64_t* keys, hipStream_t s);
+// vout[i] = words[i] & (2^vbits - 1) as u32 (vw 4) or u64 (vw 8)
+void split_values(const uint64_t* words, int64_t n, int vbits, int vw, void* vout, hipStream_t s);
 // head bitmap H (nw 64-bit words): cnt[w] = popcount; then seg[pos[w] + k] =
 // position of the k-th set bit of word w, seg[pos[nw]] = n
 void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s);
@@ -377,10 +388,12 @@ void trimr_low_degree(const int64_t* e, const int32_t* dg, int64_t n, int64_t* k
 // fixed 8-byte values (marker: the key's first vertex), value-parallel in tiles: phase 0 sets
 // marked[key] (zeroed by the caller) for the keys holding a marker, phase 1
 // writes each tile's count of centres of marked keys to tcount[tile], phase 2
-// writes rows (centre, edge key) from tbase[tile] on
+// writes rows (centre, edge key) from tbase[tile] on. compact_vb > 0: keys are
+// one packed word vi << vb | vj and values u32 (else EDGE keys, int64 values)
 int64_t trimr_emit_tiles(int64_t nval);
-void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval, const int64_t* vals, uint8_t* marked,
-                      int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, hipStream_t s);
+void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval, const void* vals, uint8_t* marked,
+                      int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, int compact_vb,
+                      hipStream_t s);
 // cnt[s] = wedge centres of edge segment s if it holds the edge marker, else 0
 // (voff: variable-width values, the marker is empty; voff null: fixed 8-byte
 // values vals, the marker is the key's first vertex)

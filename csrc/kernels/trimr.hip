@@ -146,11 +146,25 @@ __device__ __forceinline__ int64_t et_upper(const int64_t* __restrict__ a, int64
   return lo;
 }
 
-template <int PHASE>
+// an edge key's two vertices: EDGE {vi, vj} words, or (CMP) one packed word
+// vi << vb | vj (the compact wedges of large graphs: 8-byte keys, 4-byte values)
+template <int CMP>
+__device__ __forceinline__ void edge_of(const int64_t* ekey, int64_t k, int vb, int64_t* vi, int64_t* vj) {
+  if (CMP) {
+    const uint64_t K = (uint64_t)ekey[k];
+    *vi = (int64_t)(K >> vb);
+    *vj = (int64_t)(K & ((1ull << vb) - 1));
+  } else {
+    *vi = ekey[2 * k];
+    *vj = ekey[2 * k + 1];
+  }
+}
+
+template <int PHASE, int CMP>
 __global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ seg, int64_t nkey, int64_t nval,
-                                                   const int64_t* __restrict__ vals, uint8_t* __restrict__ marked,
+                                                   const void* __restrict__ vals_, uint8_t* __restrict__ marked,
                                                    int64_t* __restrict__ tcount, const int64_t* __restrict__ tbase,
-                                                   const int64_t* __restrict__ ekey, int64_t* __restrict__ out) {
+                                                   const int64_t* __restrict__ ekey, int64_t* __restrict__ out, int vb) {
   __shared__ int64_t s_seg[ET_TILE + 1];
   __shared__ int64_t s_k0;
   __shared__ int s_n;
@@ -184,8 +198,10 @@ __global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ s
       else hi = mid;
     }
     const int64_t k = k0 + lo;
-    const int64_t c = vals[j];
-    const bool mark = c == ekey[2 * k];  // an edge carries its first vertex
+    const int64_t c = CMP ? (int64_t)static_cast<const uint32_t*>(vals_)[j] : static_cast<const int64_t*>(vals_)[j];
+    int64_t vi, vj;
+    edge_of<CMP>(ekey, k, vb, &vi, &vj);
+    const bool mark = c == vi;  // an edge carries its first vertex
     if (PHASE == 0) {
       if (mark) marked[k] = 1;  // every writer stores the same byte
     } else if (!mark && marked[k]) {
@@ -205,9 +221,11 @@ __global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ s
 #pragma unroll
   for (int it = 0; it < ET_IT; ++it) {
     if (key_[it] < 0) continue;
+    int64_t vi, vj;
+    edge_of<CMP>(ekey, key_[it], vb, &vi, &vj);
     out[3 * o] = c_[it];
-    out[3 * o + 1] = ekey[2 * key_[it]];
-    out[3 * o + 2] = ekey[2 * key_[it] + 1];
+    out[3 * o + 1] = vi;
+    out[3 * o + 2] = vj;
     ++o;
   }
 }
@@ -216,19 +234,25 @@ __global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ s
 
 int64_t trimr_emit_tiles(int64_t nval) { return (nval + ET_TILE - 1) / ET_TILE; }
 
-void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval, const int64_t* vals, uint8_t* marked,
-                      int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, hipStream_t s) {
+void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval, const void* vals, uint8_t* marked,
+                      int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, int compact_vb,
+                      hipStream_t s) {
   if (nval <= 0 || nkey <= 0) return;
   const unsigned g = (unsigned)trimr_emit_tiles(nval);
-  if (phase == 0)
-    hipLaunchKernelGGL(k_emit_tiles<0>, dim3(g), dim3(NT), 0, s, seg, nkey, nval, vals, marked, tcount, tbase, ekey,
-                       out);
-  else if (phase == 1)
-    hipLaunchKernelGGL(k_emit_tiles<1>, dim3(g), dim3(NT), 0, s, seg, nkey, nval, vals, marked, tcount, tbase, ekey,
-                       out);
-  else
-    hipLaunchKernelGGL(k_emit_tiles<2>, dim3(g), dim3(NT), 0, s, seg, nkey, nval, vals, marked, tcount, tbase, ekey,
-                       out);
+  const int vb = compact_vb;
+#define MRH_EMIT(P, C)                                                                                             \
+  hipLaunchKernelGGL((k_emit_tiles<P, C>), dim3(g), dim3(NT), 0, s, seg, nkey, nval, vals, marked, tcount, tbase, \
+                     ekey, out, vb)
+  if (vb > 0) {
+    if (phase == 0) MRH_EMIT(0, 1);
+    else if (phase == 1) MRH_EMIT(1, 1);
+    else MRH_EMIT(2, 1);
+  } else {
+    if (phase == 0) MRH_EMIT(0, 0);
+    else if (phase == 1) MRH_EMIT(1, 0);
+    else MRH_EMIT(2, 0);
+  }
+#undef MRH_EMIT
   MRH_CHECK_LAUNCH();
 }
 

@@ -1,6 +1,8 @@
 // MapReduce triangle finder (see trifind_mr.h).
 #include "trifind_mr.h"
 
+#include <cstdlib>
+
 #include "callbacks.h"
 #include "engine/comm.h"
 #include "engine/tri.h"
@@ -65,37 +67,63 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
     });
   });
   stage("collate 3", mrt, [&] { mrt.collate(); });
+  // Edge markers and the layout of the last collate, decided on every rank
+  // alike (allreduced). An upper edge (vi < vj) carries vi as its marker, not
+  // an empty value: every pair of collate 4 then has one narrow value and the
+  // collate groups them as packed (edge, vertex) words. A wedge centre is
+  // never vi then (the centre of wedge (vi, vj) is a third vertex), but it
+  // can be when some edge is not upper (self-loops, vi > vj): then edges
+  // carry the reference's empty value instead. Compact layout (upper edges,
+  // vertex ids below 2^32): an edge key is one word vi << vb | vj (vb = the
+  // bits of the largest id) and a centre 4 bytes — a wedge is 12 bytes, not
+  // 24 (R-MAT-22's ~6 G wedges fit in HBM); MRH_TRIMR_COMPACT=0 turns it off.
+  int64_t bad = 0, vmax = 0;
+  if (mre.kv_rows()) {
+    mre.flatten();
+    at::Tensor e = edges_of(*mre.kv);
+    bad = (e.select(1, 0) >= e.select(1, 1)).any().item<bool>() ? 1 : 0;
+    bad = std::max<int64_t>(bad, (e.min().item<int64_t>() < 0) ? 1 : 0);
+    vmax = e.max().item<int64_t>();
+  }
+  const bool marked_by_vertex = comm.allreduce(bad, Comm::MAX) == 0;
+  vmax = comm.allreduce(vmax, Comm::MAX);
+  int vb = 1;
+  while (vb < 63 && (vmax >> vb) != 0) ++vb;
+  static const bool compact_env = [] {
+    const char* e = std::getenv("MRH_TRIMR_COMPACT");
+    return !(e && *e == '0');
+  }();
+  const bool compact = compact_env && marked_by_vertex && vb <= 32;
+  run.compact_vb = compact ? vb : 0;
   stage("reduce nsq_angles", mrt, [&] {
-    mrt.reduce_batch([](const KMV& m, KeyValue& kv) {  // O(d^2) wedges, load-balanced kernel
+    mrt.reduce_batch([&](const KMV& m, KeyValue& kv) {  // O(d^2) wedges, load-balanced kernel
       if (!m.nkey) return;
-      // under a page budget the wedges go out in spool pieces (24 B a wedge)
-      const int64_t chunk = kv.piece_bytes() / 24;
+      // wedges are generated in bounded chunks (24 B a wedge while generated):
+      // spool pieces under a page budget, 2^28 wedges otherwise
+      const int64_t chunk = kv.piece_bytes() ? kv.piece_bytes() / 24 : (compact ? int64_t(1) << 28 : 0);
       for_each_wedge_chunk(m.seg, m.vdata.view(at::kLong), m.keys.kdata.view(at::kLong), chunk,
-                           [&](const at::Tensor& e, const at::Tensor& c) { add_tensors(kv, e, c); });
+                           [&](const at::Tensor& e, const at::Tensor& c) {
+                             if (!compact) {
+                               add_tensors(kv, e, c);
+                               return;
+                             }
+                             at::Tensor key = at::bitwise_or(at::bitwise_left_shift(e.select(1, 0), vb), e.select(1, 1));
+                             add_tensors(kv, key, c.to(at::kInt));
+                           });
     });
   });
   stage("add edges", mrt, [&] {
     // the reference adds the edge MR unchanged (oink/tri_find.cpp:71): the
-    // marked copies go through a temporary MR, the input is left as it was.
-    // An upper edge (vi < vj) carries vi as its marker, not an empty value:
-    // every pair of collate 4 then has one narrow 8-byte value and the
-    // collate groups them as packed (edge, vertex) words. A wedge centre is
-    // never vi then (the centre of wedge (vi, vj) is a third vertex), but it
-    // can be when some edge is not upper (self-loops, vi > vj): then, on
-    // every rank alike, edges carry the reference's empty value instead.
-    int64_t bad = 0;
-    if (mre.kv && mre.kv->n) {
-      mre.flatten();
-      at::Tensor e = edges_of(*mre.kv);
-      bad = (e.select(1, 0) >= e.select(1, 1)).any().item<bool>() ? 1 : 0;
-    }
-    const bool marked_by_vertex = comm.allreduce(bad, Comm::MAX) == 0;
+    // marked copies go through a temporary MR, the input is left as it was
     MapReduce marked(mre.comm());
     marked.set = mre.set;
     marked.map_mr_batch(mre, [&](const KV& src, KeyValue& kv) {
       if (!src.n) return;
       at::Tensor e = edges_of(src);
-      if (marked_by_vertex) {
+      if (compact) {
+        at::Tensor key = at::bitwise_or(at::bitwise_left_shift(e.select(1, 0), vb), e.select(1, 1));
+        add_tensors(kv, key, e.select(1, 0).to(at::kInt));
+      } else if (marked_by_vertex) {
         add_tensors(kv, e, e.select(1, 0).contiguous());
       } else {
         KV x = make_kv(e.contiguous().view(at::kByte).view({-1}), c10::nullopt,
@@ -109,8 +137,8 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
   });
   stage("collate 4", mrt, [&] { mrt.collate(); });
   stage("reduce emit_triangles", mrt, [&] {
-    run.triangles = mrt.reduce_batch([](const KMV& m, KeyValue& kv) {
-      at::Tensor tri = trimr_emit(m);
+    run.triangles = mrt.reduce_batch([&](const KMV& m, KeyValue& kv) {
+      at::Tensor tri = trimr_emit(m, compact ? vb : 0);
       if (tri.size(0)) add_tensors(kv, tri);
     });
   });

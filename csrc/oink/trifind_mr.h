@@ -18,6 +18,7 @@ struct TriMRStage {
 };
 struct TriMRRun {
   uint64_t triangles = 0;
+  int compact_vb = 0;  // > 0: the last collate ran on the compact layout (12-byte wedges)
   std::vector<TriMRStage> stages;
 };
 

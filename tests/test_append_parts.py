@@ -86,3 +86,37 @@ def test_add_out_of_core_writes_only_the_new_part(dev, tmp_path):
     assert mr.kv_parts >= 2
     mr.collate()
     assert _groups(mr) == _want(a, b)
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("vbit", [54, 58])
+def test_packed_pairs_past_64_bits_bucketed(dev, vbit):
+    """narrow pairs whose key + value bits exceed 64 (R-MAT-22 wedges: 44 +
+    22) group in 2^B buckets (B = the excess bits; the bucket of a key is its
+    low B bits ^ a mix of the others: balanced and invertible) — exact, every
+    key's values in input order, 4- and 8-byte values, given as parts"""
+    gen = torch.Generator().manual_seed(vbit)
+    n = 60_000
+    k = torch.randint(0, 3000, (n,), generator=gen, dtype=torch.int64)
+    k[: n // 3] = 7  # a hot key
+    v8 = torch.randint(0, 1 << 20, (n,), generator=gen, dtype=torch.int64) | (1 << (vbit - 1))
+    v4 = torch.randint(0, 1 << 31, (n,), generator=gen, dtype=torch.int64).to(torch.int32)
+    comm = g.Comm(device=dev)
+    for vals, wide in ((v8, 8), (v4, 4)):
+        if wide == 4:  # 12 key bits + 31 value bits fit: force a wide key instead
+            kk = k | (1 << 40)
+        else:
+            kk = k
+        want = collections.defaultdict(list)
+        for a, b in zip(kk.tolist(), vals.tolist()):
+            want[a].append(b)
+        mr, other = g.MapReduce(comm), g.MapReduce(comm)
+        h = n // 2
+        mr.map(1, lambda i, kv: kv.add_tensors(kk[:h].to(dev), vals[:h].to(dev)))
+        other.map(1, lambda i, kv: kv.add_tensors(kk[h:].to(dev), vals[h:].to(dev)))
+        mr.add(other)
+        assert mr.convert() == len(want)
+        assert mr.last_convert.exact
+        fmt = "<q" if wide == 8 else "<i"
+        got = {struct.unpack("<q", key)[0]: [struct.unpack(fmt, x)[0] for x in vs] for key, vs in mr.kmv_pairs()}
+        assert got == dict(want)
