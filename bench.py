@@ -397,7 +397,7 @@ def _extra(comm, prefix, fn, args, **over):
                                     metric=r["metric"])}
     for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices", "build",
               "triangles_check", "stages", "wedge_pairs", "ooc", "ms_per_step_prefetch", "pairs",
-              "pairs_per_s_by_stage", "top10", "top10_equals_combiner"):
+              "pairs_per_s_by_stage", "top10", "top10_equals_combiner", "big", "compact_vb"):
         if k in r:
             out[f"{prefix}_{k}"] = r[k]
     return out
@@ -599,6 +599,9 @@ def main():
     ap.add_argument("--trifind-mr-scale", type=int, default=None,
                     help="RMAT scale of the tri_find_mr extra (the 4-collate MapReduce pipeline: 20 on GPU, 10 on "
                          "CPU; 0 = skip)")
+    ap.add_argument("--trifind-mr-big-scale", type=int, default=None,
+                    help="RMAT scale of a second, larger tri_find_mr run in HBM (22 on GPU: ~7 G wedge pairs as "
+                         "12-byte compact pairs; 0 = skip)")
     ap.add_argument("--trifind-mr-ooc-scale", type=int, default=None,
                     help="RMAT scale of its out-of-core run under a 256 MiB HBM budget (18 on GPU, 0 on CPU)")
     ap.add_argument("--wordfreq-bytes", type=float, default=None,
@@ -633,6 +636,8 @@ def main():
         args.trifind_mr_scale = 20 if comm.is_cuda else 10
     if args.trifind_mr_ooc_scale is None:
         args.trifind_mr_ooc_scale = 18 if comm.is_cuda else 0
+    if args.trifind_mr_big_scale is None:
+        args.trifind_mr_big_scale = 22 if comm.is_cuda else 0
     if args.wordfreq_bytes is None:
         args.wordfreq_bytes = float(8 << 30) if comm.is_cuda else 4e6
     if args.workload == "invertedindex":
@@ -728,7 +733,7 @@ def main():
         if args.trifind_mr_scale > 0:
             from gpu_mapreduce_amd.models.triangles import bench_trifind_mr
             r = _extra(comm, "trifind_mr", bench_trifind_mr, args, scale=args.trifind_mr_scale, steps=1, warmup=1,
-                       mr_ooc_scale=args.trifind_mr_ooc_scale)
+                       mr_ooc_scale=args.trifind_mr_ooc_scale, mr_big_scale=args.trifind_mr_big_scale)
             res.update(r)
             mark("trifind_mr")
 

@@ -326,6 +326,27 @@ std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor
   return wedge_range(seg, ws, nb, centre, 0, ws.nw);
 }
 
+void for_each_wedge_chunk_compact(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre,
+                                  int64_t max_w, int vb,
+                                  const std::function<void(const at::Tensor&, const at::Tensor&)>& fn) {
+  need(vb > 0 && vb <= 32, "wedges (compact): vertex bits in (0, 32]");
+  const WedgeScan ws = wedge_scan(seg, nb, centre);
+  const int64_t step = max_w > 0 ? max_w : std::max<int64_t>(ws.nw, 1);
+  for (int64_t w0 = 0; w0 < ws.nw; w0 += step) {
+    const int64_t n = std::min(ws.nw, w0 + step) - w0;
+    if (seg.is_cuda()) {
+      at::Tensor key = at::empty({n}, nb.options());
+      at::Tensor c = at::empty({n}, nb.options().dtype(at::kInt));
+      k::wedges_compact(P0<int64_t>(seg), P0<int64_t>(ws.gidx), P0<int64_t>(ws.wscan), ws.ngw, P0<int64_t>(nb),
+                        P0<int64_t>(centre), w0, n, vb, P0<int64_t>(key), P0<uint32_t>(c), cur());
+      fn(key, c);
+    } else {
+      auto r = wedge_range(seg, ws, nb, centre, w0, w0 + n);
+      fn(at::bitwise_or(at::bitwise_left_shift(r.first.select(1, 0), vb), r.first.select(1, 1)), r.second.to(at::kInt));
+    }
+  }
+}
+
 void for_each_wedge_chunk(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre, int64_t max_w,
                           const std::function<void(const at::Tensor&, const at::Tensor&)>& fn) {
   const WedgeScan ws = wedge_scan(seg, nb, centre);

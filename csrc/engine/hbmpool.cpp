@@ -12,6 +12,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -42,6 +44,35 @@ struct Block {
   int dev = 0;
   hipStream_t stream = nullptr;
   std::vector<hipStream_t> used_on;  // other streams that touched the block (record_stream)
+  struct Seg* seg = nullptr;         // big blocks: the arena segment and offset they were cut from
+  int64_t off = 0;
+};
+
+// an event recorded when a big block was freed, shared by the free ranges cut
+// from or merged with it; a later user on any stream waits for it
+struct Ev {
+  hipEvent_t e = nullptr;
+  ~Ev() {
+    if (e) (void)hipEventDestroy(e);
+  }
+};
+using EvP = std::shared_ptr<Ev>;
+
+// Big blocks (>= kBigBlock) are cut best-fit from hipMalloc'd segments and
+// coalesce with their free neighbours when freed, so the memory a job held
+// at its peak serves any later mix of sizes (R-MAT-22's collate: 56, 28, 7 GB
+// pieces) instead of growing the device allocation for every new size; fully
+// free segments go back to the driver only when the pool holds much more
+// than it uses (reserved > 1.5x in use).
+struct FreeRange {
+  int64_t size = 0;
+  std::vector<EvP> evs;  // the frees this range's memory waits for
+};
+struct Seg {
+  char* base = nullptr;
+  int64_t size = 0;
+  int64_t free_bytes = 0;
+  std::map<int64_t, FreeRange> free;  // offset -> free range (coalesced)
 };
 
 // a freed block that other streams used: reusable once their events complete
@@ -56,14 +87,16 @@ struct Dev {
   int64_t in_use = 0, peak = 0, cap = 0, cached = 0, allocs = 0, frees = 0, failures = 0, cross = 0;
   int64_t grows = 0, releases = 0, oom_retries = 0;
   double grow_ms = 0;
-  // blocks of >= kBigBlock come from hipMalloc, not the HIP pool: re-growing
-  // the stream-ordered pool by tens of GB after its free memory came back in
-  // other sizes took seconds (a 30 GB concat of tri_find_mr: 4.5 s), a fresh
-  // hipMalloc of the same size ~0.1 s. They are cached like every block and
-  // hipFree'd (after a checked device sync) when the caches are released.
-  std::unordered_set<void*> big;
-  int64_t big_bytes = 0;     // held by big blocks (live + cached): part of reserved
+  // blocks of >= kBigBlock come from hipMalloc'd segments, not the HIP pool:
+  // re-growing the stream-ordered pool by tens of GB after its free memory
+  // came back in other sizes took seconds (a 30 GB concat of tri_find_mr:
+  // 4.5 s). They are cut best-fit from the segments and coalesce when freed.
+  int64_t big_bytes = 0;     // held by the big-block segments (live + free): part of reserved
   int64_t big_peak = 0;
+  std::vector<std::unique_ptr<Seg>> segs;
+  std::set<std::tuple<int64_t, Seg*, int64_t>> by_size;  // (size, segment, offset) of every free range
+  int64_t big_free = 0;                                   // free bytes inside the segments
+  int64_t reserved_peak_true = 0;                         // hi-water of (HIP pool reserved + segments)
   int64_t total_mem = 0;     // device memory (hipMemGetInfo at the first growth)
   int64_t base_cap = 0;                   // set_cap's cap; cap = min(base_cap, active OpCaps)
   std::multiset<int64_t> op_caps;         // caps of the ops running now (any thread)
@@ -165,7 +198,6 @@ constexpr int64_t kBigBlock = int64_t(256) << 20;
 
 void release_cached(Dev& d) {  // g_mu held
   ++d.releases;
-  bool synced = false;
   for (Pending& q : d.pending) {
     bool ok = true;
     for (hipEvent_t e : q.evs) {
@@ -184,23 +216,6 @@ void release_cached(Dev& d) {  // g_mu held
   d.pending.clear();
   for (auto& [k, v] : d.free)
     for (void* p : v) {
-      if (d.big.count(p)) {
-        // hipMalloc'd: free once the device has drained (its last users were
-        // stream-ordered before the free that cached it)
-        if (!synced) {
-          const hipError_t r = hipDeviceSynchronize();
-          if (r != hipSuccess) {
-            (void)hipGetLastError();
-            set_fault(d, std::string("device fault while releasing cached blocks: ") + hipGetErrorString(r));
-            return;
-          }
-          synced = true;
-        }
-        if (hipFree(p) != hipSuccess) (void)hipGetLastError();
-        d.big.erase(p);
-        d.big_bytes -= k.second;
-        continue;
-      }
       if (hipFreeAsync(p, k.first) != hipSuccess) {
         (void)hipGetLastError();
         const hipError_t r = hipDeviceSynchronize();
@@ -243,6 +258,99 @@ void* take_other_stream(Dev& d, hipStream_t stream, int64_t bytes) {  // g_mu he
   return nullptr;
 }
 
+constexpr int64_t kSegAlign = int64_t(2) << 20;   // big blocks: 2 MiB granules
+constexpr int64_t kSegMin = int64_t(2) << 30;     // a new segment holds at least 2 GiB
+
+int64_t pool_reserved(Dev& d) {  // g_mu held
+  uint64_t r = 0;
+  if (d.pool && hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemCurrent, &r) != hipSuccess) {
+    (void)hipGetLastError();
+    r = 0;
+  }
+  return (int64_t)r + d.big_bytes;
+}
+
+void note_reserved(Dev& d) {  // g_mu held
+  d.reserved_peak_true = std::max(d.reserved_peak_true, pool_reserved(d));
+}
+
+void range_add(Dev& d, Seg* sg, int64_t off, int64_t size, std::vector<EvP> evs) {  // g_mu held
+  // coalesce with the free neighbours (their events join: a user waits for all)
+  auto nx = sg->free.lower_bound(off);
+  if (nx != sg->free.end() && nx->first == off + size) {
+    d.by_size.erase({nx->second.size, sg, nx->first});
+    size += nx->second.size;
+    for (auto& e : nx->second.evs) evs.push_back(e);
+    nx = sg->free.erase(nx);
+  }
+  if (nx != sg->free.begin()) {
+    auto pv = std::prev(nx);
+    if (pv->first + pv->second.size == off) {
+      d.by_size.erase({pv->second.size, sg, pv->first});
+      off = pv->first;
+      size += pv->second.size;
+      for (auto& e : pv->second.evs) evs.push_back(e);
+      sg->free.erase(pv);
+    }
+  }
+  // completed events need no wait; drop them (and duplicates) to keep lists short
+  std::vector<EvP> live;
+  for (auto& e : evs) {
+    if (!e || std::find(live.begin(), live.end(), e) != live.end()) continue;
+    const hipError_t r = hipEventQuery(e->e);
+    if (r == hipSuccess) continue;
+    if (r != hipErrorNotReady) (void)hipGetLastError();
+    live.push_back(e);
+  }
+  sg->free[off] = FreeRange{size, std::move(live)};
+  d.by_size.insert({size, sg, off});
+}
+
+// best fit among the free ranges; the rest of the range stays free
+void* arena_take(Dev& d, int64_t bytes, hipStream_t stream, Seg** seg, int64_t* off) {  // g_mu held
+  auto it = d.by_size.lower_bound({bytes, nullptr, 0});
+  if (it == d.by_size.end()) return nullptr;
+  auto [size, sg, o] = *it;
+  d.by_size.erase(it);
+  auto fr = sg->free.find(o);
+  std::vector<EvP> evs = std::move(fr->second.evs);
+  sg->free.erase(fr);
+  for (auto& e : evs) {  // the block's earlier users (any stream) finish first
+    if (hipStreamWaitEvent(stream, e->e, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      set_fault(d, "stream wait on a freed big block");
+      return nullptr;
+    }
+  }
+  if (size > bytes) range_add(d, sg, o + bytes, size - bytes, evs);
+  sg->free_bytes -= bytes;
+  d.big_free -= bytes;
+  *seg = sg;
+  *off = o;
+  return sg->base + o;
+}
+
+// segments with nothing in use go back to the driver (after their last users)
+void release_free_segments(Dev& d) {  // g_mu held
+  for (size_t i = 0; i < d.segs.size();) {
+    Seg* sg = d.segs[i].get();
+    if (sg->free_bytes != sg->size) {
+      ++i;
+      continue;
+    }
+    for (auto& [o, fr] : sg->free) {
+      for (auto& e : fr.evs)
+        if (hipEventSynchronize(e->e) != hipSuccess) (void)hipGetLastError();
+      d.by_size.erase({fr.size, sg, o});
+    }
+    if (hipFree(sg->base) != hipSuccess) (void)hipGetLastError();
+    d.big_bytes -= sg->size;
+    d.big_free -= sg->size;
+    d.segs.erase(d.segs.begin() + (std::ptrdiff_t)i);
+    ++d.releases;
+  }
+}
+
 void* pool_alloc(size_t size, int dev, hipStream_t stream) {
   if (size == 0) return nullptr;
   TORCH_CHECK(dev >= 0 && dev < kMaxDev, "mrhip page pool: device index out of range");
@@ -272,6 +380,71 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
                        " (maxpage x memsize / hbm_budget) on device ", dev, " in ", guard::current_op());
     }
     if (!d.pending.empty()) reap(d);
+    if (bytes >= kBigBlock) {
+      const int64_t bb = (bytes + kSegAlign - 1) / kSegAlign * kSegAlign;
+      Seg* sg = nullptr;
+      int64_t off = 0;
+      void* p = arena_take(d, bb, stream, &sg, &off);
+      if (!p && !d.fault.empty()) TORCH_CHECK(false, "mrhip page pool: device ", dev, " faulted: ", d.fault);
+      if (!p) {
+        // a new segment: first hand back what the pool holds beyond 1.5x its use
+        if (pool_reserved(d) + std::max(bb, kSegMin) > (d.in_use + bb) * 3 / 2) {
+          release_free_segments(d);
+          if (d.cached > (int64_t(1) << 30)) release_cached(d);
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        int64_t segsz = std::max(bb, kSegMin);
+        char* base = nullptr;
+        hipError_t e = hipMalloc((void**)&base, (size_t)segsz);
+        if (e != hipSuccess && segsz > bb) {  // no room for the margin: exactly the block
+          (void)hipGetLastError();
+          segsz = bb;
+          e = hipMalloc((void**)&base, (size_t)segsz);
+        }
+        if (e != hipSuccess) {  // everything idle back to the driver, then once more
+          (void)hipGetLastError();
+          ++d.oom_retries;
+          release_free_segments(d);
+          release_cached(d);
+          const hipError_t se = hipDeviceSynchronize();
+          if (se != hipSuccess) {
+            (void)hipGetLastError();
+            set_fault(d, std::string("device fault seen by an allocation retry: ") + hipGetErrorString(se));
+            TORCH_CHECK(false, "mrhip page pool: device error on device ", dev, ": ", hipGetErrorString(se));
+          }
+          if (d.pool) (void)hipMemPoolTrimTo(d.pool, 0);
+          e = hipMalloc((void**)&base, (size_t)segsz);
+        }
+        ++d.grows;
+        d.grow_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (e != hipSuccess || !base) {
+          (void)hipGetLastError();
+          ++d.failures;
+          TORCH_CHECK_WITH(OutOfMemoryError, false, "mrhip page pool: HIP out of memory allocating ", mib(bb),
+                           " on device ", dev, " (", mib(d.in_use), " in use): ", hipGetErrorString(e));
+        }
+        auto seg = std::make_unique<Seg>();
+        seg->base = base;
+        seg->size = segsz;
+        seg->free_bytes = segsz;
+        d.big_bytes += segsz;
+        d.big_free += segsz;
+        d.big_peak = std::max(d.big_peak, d.big_bytes);
+        range_add(d, seg.get(), 0, segsz, {});
+        d.segs.push_back(std::move(seg));
+        note_reserved(d);
+        p = arena_take(d, bb, stream, &sg, &off);
+        TORCH_CHECK(p, "mrhip page pool: a fresh segment could not serve its block");
+      }
+      d.in_use += bb;
+      d.peak = std::max(d.peak, d.in_use);
+      ++d.allocs;
+      Block b{bb, dev, stream, {}};
+      b.seg = sg;
+      b.off = off;
+      g_blocks[p] = std::move(b);
+      return p;
+    }
     auto it = d.free.find({stream, bytes});
     void* p = nullptr;
     if (it != d.free.end() && !it->second.empty()) {  // stream-ordered reuse: no HIP call
@@ -310,10 +483,7 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
   }
   void* p = nullptr;
   const auto t0 = std::chrono::steady_clock::now();
-  const bool is_big = bytes >= kBigBlock;
-  auto grow = [&] {
-    return is_big ? hipMalloc(&p, (size_t)bytes) : hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream);
-  };
+  auto grow = [&] { return hipMallocFromPoolAsync(&p, (size_t)bytes, pool, stream); };
   hipError_t e = grow();
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -349,11 +519,7 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
     TORCH_CHECK_WITH(OutOfMemoryError, false, "mrhip page pool: HIP out of memory allocating ", mib(bytes),
                      " on device ", dev, " (", mib(g_dev[dev].in_use), " in use): ", hipGetErrorString(e));
   }
-  if (is_big) {
-    g_dev[dev].big.insert(p);
-    g_dev[dev].big_bytes += bytes;
-    g_dev[dev].big_peak = std::max(g_dev[dev].big_peak, g_dev[dev].big_bytes);
-  }
+  note_reserved(g_dev[dev]);
   g_blocks[p] = Block{bytes, dev, stream, {}};
   return p;
 }
@@ -367,8 +533,32 @@ void pool_free(void* ptr, size_t /*size*/, int /*dev*/, hipStream_t /*stream*/) 
   g_blocks.erase(it);
   Dev& d = g_dev[b.dev];
   d.in_use -= b.bytes;
-  d.cached += b.bytes;
   ++d.frees;
+  if (b.seg) {
+    // an event on every stream that used it: the next user, on any stream, waits
+    std::vector<EvP> evs;
+    std::vector<hipStream_t> ss = b.used_on;
+    ss.push_back(b.stream);
+    for (hipStream_t st : ss) {
+      auto e = std::make_shared<Ev>();
+      if (hipEventCreateWithFlags(&e->e, hipEventDisableTiming) != hipSuccess || hipEventRecord(e->e, st) != hipSuccess) {
+        (void)hipGetLastError();
+        const hipError_t r = hipStreamSynchronize(st);  // cannot order by event: drain instead
+        if (r != hipSuccess) {
+          (void)hipGetLastError();
+          set_fault(d, std::string("freeing a big block: ") + hipGetErrorString(r));
+          return;  // never reused
+        }
+        continue;
+      }
+      evs.push_back(std::move(e));
+    }
+    b.seg->free_bytes += b.bytes;
+    d.big_free += b.bytes;
+    range_add(d, b.seg, b.off, b.bytes, std::move(evs));
+    return;
+  }
+  d.cached += b.bytes;
   if (b.used_on.empty()) {
     // later work on the allocating stream runs after every earlier use
     cache_put(d, b.stream, b.bytes, ptr);
@@ -451,13 +641,11 @@ PoolStats stats(int device) {
   s.grow_ms = d.grow_ms;
   s.releases = d.releases;
   s.oom_retries = d.oom_retries;
-  if (d.pool) {
-    uint64_t r = 0;
-    if (hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemCurrent, &r) == hipSuccess) s.reserved = (int64_t)r;
-    if (hipMemPoolGetAttribute(d.pool, hipMemPoolAttrReservedMemHigh, &r) == hipSuccess) s.reserved_peak = (int64_t)r;
-  }
-  s.reserved += d.big_bytes;
-  s.reserved_peak += d.big_peak;  // an upper bound: the two hi-water marks need not coincide
+  Dev& dm = const_cast<Dev&>(d);
+  s.reserved = pool_reserved(dm);
+  note_reserved(dm);
+  s.reserved_peak = d.reserved_peak_true;  // hi-water of (HIP pool reserved + big-block segments)
+  s.cached += d.big_free;
   return s;
 }
 
@@ -465,6 +653,12 @@ void reset_peak(int device) {
   if (device < 0 || device >= kMaxDev) return;
   std::lock_guard<std::mutex> l(g_mu);
   g_dev[device].peak = g_dev[device].in_use;
+}
+
+void reset_reserved_peak(int device) {
+  if (device < 0 || device >= kMaxDev) return;
+  std::lock_guard<std::mutex> l(g_mu);
+  g_dev[device].reserved_peak_true = pool_reserved(g_dev[device]);
 }
 
 int64_t set_cap(int device, int64_t cap) {
@@ -484,6 +678,7 @@ void trim(int device, int64_t keep_bytes) {
     std::lock_guard<std::mutex> l(g_mu);
     p = g_dev[device].pool;
     if (p) release_cached(g_dev[device]);
+    release_free_segments(g_dev[device]);
   }
   if (!p) return;
   // freed blocks are returned to the pool in stream order: let the device

@@ -27,6 +27,12 @@
 //    later allocation throws (MRH_FAULT=hip:pool:<rank> injects it), so the
 //    op fails and poisons its communicator instead of handing out memory a
 //    faulted stream may still write;
+//  * big blocks (>= 256 MiB): cut best-fit (2 MiB granules) from hipMalloc'd
+//    segments of >= 2 GiB and coalesced with their free neighbours when
+//    freed, so the memory held at a job's peak serves any later mix of
+//    sizes; every free records an event on each stream that used the block
+//    and the next user waits for them. A new segment first hands back the
+//    fully free ones when the pool holds over 1.5x the bytes in use;
 //  * freepage: trim() returns the pool's cached free memory to the driver;
 //  * stats: bytes in use, hi-water mark, reserved bytes, counts.
 #pragma once
@@ -39,11 +45,11 @@ namespace mrh::hbm {
 struct PoolStats {
   int64_t in_use = 0;    // bytes of live allocations (512-byte granules)
   int64_t peak = 0;      // hi-water mark of in_use since the last reset_peak
-  int64_t reserved = 0;  // bytes the HIP pool holds from the driver
-  int64_t reserved_peak = 0;  // hi-water mark of reserved
+  int64_t reserved = 0;  // bytes held from the driver (HIP pool + big-block segments)
+  int64_t reserved_peak = 0;  // hi-water mark of reserved (sampled at every growth)
   int64_t cap = 0;       // hard cap on in_use (0: none)
   int64_t allocs = 0, frees = 0, failures = 0;
-  int64_t cached = 0;              // bytes of freed blocks held in the per-(stream, class) caches
+  int64_t cached = 0;              // bytes of freed blocks held in the caches and the segments' free ranges
   int64_t cross_stream_reuse = 0;  // allocations served from another stream's cache behind an event
   bool faulted = false;            // an event / stream wait of the pool failed: no allocation is served
   int64_t grows = 0;               // allocations the caches could not serve (hipMallocFromPoolAsync)
@@ -61,6 +67,8 @@ bool install_default();
 bool installed();
 PoolStats stats(int device);
 void reset_peak(int device);
+// restart the reserved hi-water mark from what is reserved now
+void reset_reserved_peak(int device);
 // set the hard cap on bytes in use (0 = none); returns the previous cap
 int64_t set_cap(int device, int64_t cap);
 // release cached free memory of the pool down to keep_bytes

@@ -218,6 +218,11 @@ std::pair<at::Tensor, at::Tensor> wedges(const at::Tensor& seg, const at::Tensor
 // O(d^2) set (a hub of degree 20k alone makes 2e8 wedges, 4.8 GB)
 void for_each_wedge_chunk(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre, int64_t max_w,
                           const std::function<void(const at::Tensor& edges, const at::Tensor& centre)>& fn);
+// the same in the compact layout of large graphs: keys (min << vb | max)
+// int64, centres int32 (12 bytes a wedge)
+void for_each_wedge_chunk_compact(const at::Tensor& seg, const at::Tensor& nb, const at::Tensor& centre,
+                                  int64_t max_w, int vb,
+                                  const std::function<void(const at::Tensor& keys, const at::Tensor& centre)>& fn);
 // segment id of every value of a CSR segment array (seg[nseg+1], nval values)
 at::Tensor segment_ids(const at::Tensor& seg, int64_t nseg, int64_t nval);
 // counts of each bin in [0, K) of an integer index column (device histogram)

@@ -620,11 +620,14 @@ __device__ __forceinline__ int64_t wg_upper(const int64_t* __restrict__ a, int64
   return lo;
 }
 
+// CMP: the compact layout of large graphs — one word (min << vb | max) per
+// wedge and a 4-byte centre (12 bytes a wedge instead of 24)
+template <int CMP>
 __global__ __launch_bounds__(NT) void k_wedges(const int64_t* __restrict__ seg, const int64_t* __restrict__ gidx,
                                               const int64_t* __restrict__ wscan, int64_t ngw,
                                               const int64_t* __restrict__ nb, const int64_t* __restrict__ centre,
                                               int64_t w0, int64_t nwedge, int64_t* __restrict__ out_edge,
-                                              int64_t* __restrict__ out_centre) {
+                                              void* __restrict__ out_centre, int vb) {
   __shared__ int64_t s_scan[WG_TILE + 1];
   __shared__ int64_t s_gi[WG_TILE];
   __shared__ int64_t s_g0;
@@ -668,9 +671,14 @@ __global__ __launch_bounds__(NT) void k_wedges(const int64_t* __restrict__ seg, 
     const int64_t k = j + 1 + (t - j * (2 * d - j - 1) / 2);
     const int64_t a = nb[base + j], b = nb[base + k];
     const bool lt = (uint64_t)a < (uint64_t)b;
-    out_edge[2 * (t0 + o)] = lt ? a : b;
-    out_edge[2 * (t0 + o) + 1] = lt ? b : a;
-    out_centre[t0 + o] = centre[g];
+    if (CMP) {
+      out_edge[t0 + o] = (int64_t)(((uint64_t)(lt ? a : b) << vb) | (uint64_t)(lt ? b : a));
+      static_cast<uint32_t*>(out_centre)[t0 + o] = (uint32_t)centre[g];
+    } else {
+      out_edge[2 * (t0 + o)] = lt ? a : b;
+      out_edge[2 * (t0 + o) + 1] = lt ? b : a;
+      static_cast<int64_t*>(out_centre)[t0 + o] = centre[g];
+    }
   }
 }
 
@@ -774,8 +782,18 @@ void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_
 void wedges(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
             const int64_t* centre, int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s) {
   if (nwedge <= 0 || ngw <= 0) return;
-  hipLaunchKernelGGL(k_wedges, dim3((unsigned)((nwedge + WG_TILE - 1) / WG_TILE)), dim3(NT), 0, s, seg, gidx, wscan,
-                     ngw, nb, centre, w0, nwedge, out_edge, out_centre);
+  hipLaunchKernelGGL(k_wedges<0>, dim3((unsigned)((nwedge + WG_TILE - 1) / WG_TILE)), dim3(NT), 0, s, seg, gidx,
+                     wscan, ngw, nb, centre, w0, nwedge, out_edge, (void*)out_centre, 0);
+  MRH_CHECK_LAUNCH();
+}
+
+void wedges_compact(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
+                    const int64_t* centre, int64_t w0, int64_t nwedge, int vb, int64_t* out_key, uint32_t* out_centre,
+                    hipStream_t s) {
+  if (nwedge <= 0 || ngw <= 0) return;
+  check_arg(vb > 0 && vb <= 32, "wedges_compact: vertex bits in (0, 32]");
+  hipLaunchKernelGGL(k_wedges<1>, dim3((unsigned)((nwedge + WG_TILE - 1) / WG_TILE)), dim3(NT), 0, s, seg, gidx,
+                     wscan, ngw, nb, centre, w0, nwedge, out_key, (void*)out_centre, vb);
   MRH_CHECK_LAUNCH();
 }
 

@@ -292,6 +292,10 @@ void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_
 // group set is generated in bounded chunks
 void wedges(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
             const int64_t* centre, int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);
+// the same wedges in the compact layout: out_key = min << vb | max, out_centre u32
+void wedges_compact(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
+                    const int64_t* centre, int64_t w0, int64_t nwedge, int vb, int64_t* out_key, uint32_t* out_centre,
+                    hipStream_t s);
 
 // ---------------------------------------------------------------- pbpr.hip
 // propagation-blocked PageRank (graphplan.cpp PageRankPlan, one GPU)

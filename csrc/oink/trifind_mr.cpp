@@ -100,16 +100,15 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
       if (!m.nkey) return;
       // wedges are generated in bounded chunks (24 B a wedge while generated):
       // spool pieces under a page budget, 2^28 wedges otherwise
-      const int64_t chunk = kv.piece_bytes() ? kv.piece_bytes() / 24 : (compact ? int64_t(1) << 28 : 0);
+      if (compact) {  // 12 bytes a wedge, written so by the wedge kernel
+        const int64_t chunk = kv.piece_bytes() ? kv.piece_bytes() / 12 : int64_t(1) << 29;
+        for_each_wedge_chunk_compact(m.seg, m.vdata.view(at::kLong), m.keys.kdata.view(at::kLong), chunk, vb,
+                                     [&](const at::Tensor& key, const at::Tensor& c) { add_tensors(kv, key, c); });
+        return;
+      }
+      const int64_t chunk = kv.piece_bytes() / 24;
       for_each_wedge_chunk(m.seg, m.vdata.view(at::kLong), m.keys.kdata.view(at::kLong), chunk,
-                           [&](const at::Tensor& e, const at::Tensor& c) {
-                             if (!compact) {
-                               add_tensors(kv, e, c);
-                               return;
-                             }
-                             at::Tensor key = at::bitwise_or(at::bitwise_left_shift(e.select(1, 0), vb), e.select(1, 1));
-                             add_tensors(kv, key, c.to(at::kInt));
-                           });
+                           [&](const at::Tensor& e, const at::Tensor& c) { add_tensors(kv, e, c); });
     });
   });
   stage("add edges", mrt, [&] {

@@ -168,7 +168,28 @@ def bench_trifind_mr(comm, args):
         "triangles": int(r["triangles"]), "triangles_check": int(want),
         "stages": stages, "scaling": "strong",
         "wedge_pairs": max((s["pairs_out"] for s in r["stages"] if s["op"] == "reduce nsq_angles"), default=0),
+        "compact_vb": int(r.get("compact_vb", 0)),
     }
+    bscale = getattr(args, "mr_big_scale", 0) or 0
+    if bscale > 0:
+        # a larger graph in HBM: R-MAT-22's ~7 G wedge pairs go through collate
+        # 4 as 12-byte compact pairs, grouped in hash-balanced buckets
+        eb = edges_of(bscale)
+        wantb = TriangleGraph(comm, eb, 1 << bscale).count()
+        tri_find_mr(comm, eb)  # warm: the pool holds the peak afterwards
+        sync()
+        t0 = time.perf_counter()
+        rb = tri_find_mr(comm, eb)
+        sync()
+        dtb = comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
+        out["big"] = {"scale": bscale, "ms": dtb * 1e3, "triangles": int(rb["triangles"]),
+                      "triangles_check": int(wantb), "compact_vb": int(rb.get("compact_vb", 0)),
+                      "edges": (1 << bscale) * ef,
+                      "wedge_pairs": max((s["pairs_out"] for s in rb["stages"] if s["op"] == "reduce nsq_angles"),
+                                         default=0),
+                      "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"],
+                                  "pairs_out": s["pairs_out"]} for s in rb["stages"]]}
+        del eb
     oscale = getattr(args, "mr_ooc_scale", 0) or 0
     if oscale > 0:
         root = tempfile.mkdtemp(prefix=f"mrh_trimr_{me}_")

@@ -163,3 +163,53 @@ print("ok", hbm_pool.stats(0))
 @pytest.mark.gpu
 def test_pool_cross_stream_reuse_and_concurrent_caps_gpu():
     assert _child(CROSS).startswith("ok")
+
+
+ARENA = r'''
+import torch
+import gpu_mapreduce_amd as g
+from gpu_mapreduce_amd.runtime import hbm_pool
+comm = g.Comm(device="cuda:0")
+GiB = 1 << 30
+st0 = hbm_pool.stats(0)
+# a job's mix of big sizes: once a segment holds the peak, later sizes are cut
+# from it (best fit) and coalesce again when freed: no new device allocation
+big = torch.empty(6 * GiB, dtype=torch.uint8, device="cuda")
+del big
+grows = hbm_pool.stats(0)["grows"]
+a = torch.empty(3 * GiB, dtype=torch.uint8, device="cuda")
+b = torch.empty(2 * GiB, dtype=torch.uint8, device="cuda")
+a.fill_(1); b.fill_(2)
+assert hbm_pool.stats(0)["grows"] == grows
+del a, b
+c = torch.empty(6 * GiB - (64 << 20), dtype=torch.uint8, device="cuda")  # the freed pieces coalesced
+c.fill_(3)
+assert hbm_pool.stats(0)["grows"] == grows, hbm_pool.stats(0)
+del c
+# data written on another stream before a free is not overwritten by the next user early
+s = torch.cuda.Stream()
+x = torch.empty(GiB, dtype=torch.uint8, device="cuda")
+with torch.cuda.stream(s):
+    x.fill_(7)
+    x.record_stream(s)
+del x
+y = torch.zeros(GiB, dtype=torch.uint8, device="cuda")  # waits for the fill on s
+torch.cuda.synchronize()
+assert int(y.max().item()) == 0
+del y
+st3 = hbm_pool.stats(0)
+assert st3["reserved_peak"] <= int(1.5 * max(st3["peak"], 6 * GiB)) + 2 * GiB, st3
+hbm_pool.trim(0)
+st4 = hbm_pool.stats(0)
+assert st4["reserved"] < st3["reserved"], (st3, st4)
+print("ok", st4)
+'''
+
+
+@pytest.mark.gpu
+def test_pool_big_block_arena_gpu():
+    """big blocks (>= 256 MiB) are cut best-fit from segments and coalesce, so
+    a new mix of sizes reuses the memory held (no growth); a block freed
+    after use on another stream is handed out behind that stream's work;
+    reserved stays within 1.5x of the bytes in use; trim returns segments"""
+    assert _child(ARENA).startswith("ok")
