@@ -639,15 +639,69 @@ bool packed_pairs_disabled() {
 // mapreduce.h): each part is packed in place into its rows of the sort
 // input and released, nothing is concatenated. Values may be 4 or 8 bytes.
 // Key + value bits past 64 (R-MAT-22 wedges: 44 + 22), or more than 2^31
-// pairs, take B bucket bits: a stable partition by (low B key bits) ^
-// mix(other key bits) — balanced for skewed keys, and invertible — then one
-// sort per bucket; keys then come out bucket by bucket, in key order inside
-// a bucket. Returns false when the pairs are not that narrow.
+// pairs, take B bucket bits, a stable partition, then one sort per bucket.
+// Up to 2^31 pairs the buckets are the top B key bits (keys come out in key
+// order, however skewed the buckets); past that they are (low B key bits) ^
+// mix(other key bits) — balanced for skewed keys, and invertible — and keys
+// come out bucket by bucket, in key order inside a bucket. Returns false when
+// the pairs are not that narrow.
 namespace {
 inline uint32_t split_mix_host(uint64_t rest, int B) {
   return B ? (uint32_t)((rest * 0x9E3779B97F4A7C15ull) >> (64 - B)) : 0u;
 }
+// host twins of kvops.hip split_cut / split_join
+inline uint32_t split_cut_host(uint64_t K, int B, int hi, uint64_t* rest) {
+  if (hi >= 0) {
+    *rest = hi >= 64 ? K : (K & ((1ull << hi) - 1));
+    return hi >= 64 ? 0u : (uint32_t)(K >> hi);
+  }
+  *rest = B ? K >> B : K;
+  return B ? (uint32_t)(K & ((1ull << B) - 1)) ^ split_mix_host(*rest, B) : 0u;
+}
+inline uint64_t split_join_host(uint64_t rest, uint32_t bucket, int B, int hi) {
+  if (hi >= 0) return hi >= 64 ? rest : (((uint64_t)bucket << hi) | rest);
+  return B ? (rest << B) | (uint64_t)((bucket ^ split_mix_host(rest, B)) & ((1u << B) - 1)) : rest;
+}
 }  // namespace
+
+// sorted packed words -> segment starts (seg[ns] = n), the head words' key
+// bits ((w >> vb) & (2^sbits - 1)) and every word's value (the low vb bits,
+// vw bytes each, into vout): two reads of the words on the GPU
+void segments_packed(const at::Tensor& sk, int vb, int sbits, int vw, uint8_t* vout, at::Tensor* seg,
+                     at::Tensor* heads, int64_t* nseg) {
+  const int64_t n = sk.numel();
+  const at::Device dev = sk.device();
+  const uint64_t km = sbits >= 64 ? ~0ull : ((1ull << sbits) - 1);
+  const uint64_t* w = P0<uint64_t>(sk);
+  if (dev.is_cuda()) {
+    const int64_t nt = k::seg_packed_tiles(n);
+    at::Tensor tb = at::zeros({nt + 1}, opt(dev, at::kLong));
+    k::seg_packed_count(w, n, vb, km, P0<int64_t>(tb) + 1, cur_stream());
+    at::cumsum_out(tb, tb, 0);  // tb[t] = heads before tile t
+    *nseg = tb[nt].item<int64_t>();
+    *seg = at::empty({*nseg + 1}, opt(dev, at::kLong));
+    *heads = at::empty({*nseg}, opt(dev, at::kLong));
+    seg->narrow(0, *nseg, 1).fill_(n);
+    k::seg_packed_write(w, n, vb, km, P0<int64_t>(tb), P0<int64_t>(*seg), P0<uint64_t>(*heads), vout, vw,
+                        cur_stream());
+    return;
+  }
+  std::vector<int64_t> sv;
+  std::vector<uint64_t> hv;
+  const uint64_t vmask = (1ull << vb) - 1;
+  for (int64_t i = 0; i < n; ++i) {
+    if (i == 0 || (((w[i] ^ w[i - 1]) >> vb) & km) != 0) {
+      sv.push_back(i);
+      hv.push_back((w[i] >> vb) & km);
+    }
+    if (vw == 4) reinterpret_cast<uint32_t*>(vout)[i] = (uint32_t)(w[i] & vmask);
+    else reinterpret_cast<uint64_t*>(vout)[i] = w[i] & vmask;
+  }
+  *nseg = (int64_t)sv.size();
+  sv.push_back(n);
+  *seg = at::from_blob(sv.data(), {(int64_t)sv.size()}, opt(at::kCPU, at::kLong)).clone();
+  *heads = at::from_blob(hv.data(), {(int64_t)hv.size()}, opt(at::kCPU, at::kLong)).clone();
+}
 
 bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st) {
   if (packed_pairs_disabled()) return false;
@@ -711,13 +765,18 @@ bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st)
   // B bucket bits: what does not fit one sort word, and enough buckets that
   // each stays below 2^30 pairs (sort buffers, 32-bit segment positions)
   int B = std::max(0, kbits + vbits - 64);
-  if (n > (int64_t(1) << 31)) {
+  // MRH_PACKED_MIXED=1 takes the mixed cut at any size (tests)
+  const char* fm = std::getenv("MRH_PACKED_MIXED");
+  const bool force_mixed = fm && *fm == '1';
+  const bool mixed = n > (int64_t(1) << 31) || force_mixed;
+  if (mixed && n > (int64_t(1) << 31)) {
     int need = 0;
     while ((n >> need) > (int64_t(1) << 30)) ++need;
     B = std::max(B, need);
   }
   if (B > 8 || B > kbits) return false;  // at most 256 buckets (the partition kernels' LDS histogram)
   const int M = 1 << B;
+  const int hi = mixed ? -1 : kbits - B;  // ordered cut: bucket = K >> hi
   parts_io.clear();  // from here on this function holds the only references
   const int sbits = kbits - B;  // key bits inside a sort word, above the value
   // every part packed in place into its rows, then released
@@ -729,7 +788,7 @@ bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st)
     uint64_t* o = P0<uint64_t>(words) + row0;
     int32_t* bo = B ? P0<int32_t>(bkt) + row0 : nullptr;
     if (cuda) {
-      k::pack_kv_split(kd, p.vdata.data_ptr(), vw, p.n, sh, vbits, B, o, bo, cur_stream());
+      k::pack_kv_split(kd, p.vdata.data_ptr(), vw, p.n, sh, vbits, B, hi, o, bo, cur_stream());
     } else {
       for (int64_t i = 0; i < p.n; ++i) {
         uint64_t K = 0;
@@ -737,16 +796,17 @@ bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st)
           if (sh.s[w] >= 0) K |= kd[i * nw + w] << sh.s[w];
         const uint64_t v = vw == 4 ? (uint64_t)static_cast<const uint32_t*>(p.vdata.data_ptr())[i]
                                    : static_cast<const uint64_t*>(p.vdata.data_ptr())[i];
-        const uint64_t rest = B ? K >> B : K;
+        uint64_t rest;
+        const uint32_t bk = split_cut_host(K, B, hi, &rest);
         o[i] = (rest << vbits) | v;
-        if (bo) bo[i] = (int32_t)((uint32_t)(K & ((1ull << B) - 1)) ^ split_mix_host(rest, B));
+        if (bo) bo[i] = (int32_t)bk;
       }
     }
     row0 += p.n;
     p = KV();  // the part's memory goes back while the others are packed
   }
   parts.clear();
-  // buckets (B > 0): a stable partition of the sort words, balanced by the mix
+  // buckets (B > 0): a stable partition of the sort words
   std::vector<int64_t> bcount{n};
   if (B) {
     KV w;
@@ -769,25 +829,19 @@ bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st)
     at::Tensor wsl = words.narrow(0, v0, nb);
     at::Tensor sk = sbits > 0 ? radix_sort_keys(wsl, vbits, vbits + sbits, false) : wsl;
     passes += (sbits + 7) / 8;
-    // the key bits above the value (a logical shift: the word's top bit may be set)
-    at::Tensor keyp = sbits > 0 ? at::bitwise_right_shift(sk, vbits) : at::zeros({nb}, opt(dev, at::kLong));
-    if (sbits > 0 && sbits < 64) keyp = at::bitwise_and(keyp, (int64_t)((1ull << sbits) - 1));
-    at::Tensor flags, pos, seg;
+    // segments, head key bits (a logical shift: the word's top bit may be
+    // set) and values straight from the sorted words
+    at::Tensor seg, heads;
     int64_t ns = 0;
-    segments_from_sorted(keyp, &flags, &pos, &seg, &ns);
-    flags = pos = at::Tensor();
-    at::Tensor heads = keyp.index_select(0, seg.narrow(0, 0, ns));
-    keyp = at::Tensor();
+    segments_packed(sk, vbits, sbits, vw, P0<uint8_t>(vout) + v0 * vw, &seg, &heads, &ns);
     at::Tensor kb = at::empty({ns, nw}, opt(dev, at::kLong));
     if (cuda) {
-      k::unpack_split(P0<uint64_t>(heads), ns, bi, B, sh, wb, P0<uint64_t>(kb), cur_stream());
-      k::split_values(P0<uint64_t>(sk), nb, vbits, vw, P0<uint8_t>(vout) + v0 * vw, cur_stream());
+      k::unpack_split(P0<uint64_t>(heads), ns, bi, B, hi, sh, wb, P0<uint64_t>(kb), cur_stream());
     } else {
       const uint64_t* hp = P0<uint64_t>(heads);
       uint64_t* kp = P0<uint64_t>(kb);
       for (int64_t j = 0; j < ns; ++j) {
-        const uint64_t rest = hp[j];
-        const uint64_t K = B ? (rest << B) | (uint64_t)(((uint32_t)bi ^ split_mix_host(rest, B)) & ((1u << B) - 1)) : rest;
+        const uint64_t K = split_join_host(hp[j], (uint32_t)bi, B, hi);
         for (int w = 0; w < nw; ++w) {
           uint64_t x = 0;
           if (sh.s[w] >= 0) {
@@ -797,21 +851,15 @@ bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st)
           kp[j * nw + w] = x;
         }
       }
-      const uint64_t* sp = P0<uint64_t>(sk);
-      uint8_t* vo = P0<uint8_t>(vout) + v0 * vw;
-      for (int64_t i = 0; i < nb; ++i) {
-        const uint64_t v = sp[i] & ((1ull << vbits) - 1);
-        if (vw == 4) reinterpret_cast<uint32_t*>(vo)[i] = (uint32_t)v;
-        else reinterpret_cast<uint64_t*>(vo)[i] = v;
-      }
     }
     keys_b.push_back(kb);
-    seg_b.push_back(seg.narrow(0, 0, ns) + v0);
+    // one bucket: seg (its last entry is n) is the KMV's as it is
+    seg_b.push_back(B == 0 ? seg : (v0 ? seg.narrow(0, 0, ns) + v0 : seg.narrow(0, 0, ns)));
     v0 += nb;
     nseg += ns;
   }
   words = at::Tensor();
-  seg_b.push_back(at::full({1}, n, opt(dev, at::kLong)));
+  if (B || seg_b.empty()) seg_b.push_back(at::full({1}, n, opt(dev, at::kLong)));
   out->keys.n = nseg;
   out->keys.kw = kwidth;
   out->keys.vw = 0;
@@ -819,7 +867,7 @@ bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st)
   out->keys.vdata = at::empty({0}, opt(dev, at::kByte));
   out->vw = vw;
   out->vdata = vout;
-  out->seg = at::cat(seg_b, 0);
+  out->seg = seg_b.size() == 1 ? seg_b[0] : at::cat(seg_b, 0);
   out->nkey = nseg;
   out->nval = n;
   st->exact = true;

@@ -251,7 +251,7 @@ void seg_gather_reduce(const SegIndex& ix, const at::Tensor& src, const at::Tens
   need(out.scalar_type() == x.scalar_type() && x.is_contiguous() && out.is_contiguous(), "seg_gather_reduce: out");
   k::ws_gather_reduce(dcode(x), P0<uint32_t>(ix.H), P0<int64_t>(ix.wbase), ix.nval, P0<int32_t>(src), x.data_ptr(),
                       hw ? w.data_ptr() : nullptr, (int)op, out.data_ptr(), P0<void>(ix.scratch), cur(),
-                      ix.sched.defined() ? P0<int32_t>(ix.sched) : nullptr, ix.slen);
+                      ix.sched.defined() ? P0<int32_t>(ix.sched) : nullptr, ix.slen, x.numel());
 }
 
 // all neighbour pairs per group: returns (edges [W,2] int64 (min,max), centre [W])

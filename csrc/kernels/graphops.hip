@@ -755,7 +755,7 @@ void ws_index(const int64_t* seg, int64_t nseg, int64_t nval, uint32_t* H, int64
 
 template <typename T>
 static void ws_gr_t(const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src, const T* x, const T* w,
-                    int op, T* out, void* scratch, hipStream_t s, const int32_t* sched, int64_t slen) {
+                    int op, T* out, void* scratch, hipStream_t s, const int32_t* sched, int64_t slen, int64_t nx) {
   // scratch: carry (2 nw) ids + values, then the level-2 carry (2 ceil(2 nw / 64)) ids + values
   const int64_t nc = dev::ws_nwave(nval) * 2, nc2 = 2 * ((nc + 63) / 64);
   char* p = reinterpret_cast<char*>(scratch);
@@ -763,19 +763,19 @@ static void ws_gr_t(const uint32_t* H, const int64_t* wbase, int64_t nval, const
   T* cv = reinterpret_cast<T*>(p + (size_t)nc * sizeof(int64_t));
   int64_t* cs2 = reinterpret_cast<int64_t*>(p + (size_t)nc * 16);
   T* cv2 = reinterpret_cast<T*>(p + (size_t)nc * 16 + (size_t)nc2 * sizeof(int64_t));
-  if (op == 0) dev::ws_gather_reduce<T, 0>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen);
-  else if (op == 1) dev::ws_gather_reduce<T, 1>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen);
-  else dev::ws_gather_reduce<T, 2>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen);
+  if (op == 0) dev::ws_gather_reduce<T, 0>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen, nx);
+  else if (op == 1) dev::ws_gather_reduce<T, 1>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen, nx);
+  else dev::ws_gather_reduce<T, 2>(H, wbase, nval, src, x, w, out, cs, cv, s, cs2, cv2, sched, slen, nx);
 }
 
 void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src,
                       const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s,
-                      const int32_t* sched, int64_t slen) {
+                      const int32_t* sched, int64_t slen, int64_t nx) {
   if (nval <= 0) return;
   switch (dtype) {
-    case 1: ws_gr_t<int64_t>(H, wbase, nval, src, (const int64_t*)x, (const int64_t*)w, op, (int64_t*)out, scratch, s, sched, slen); break;
-    case 2: ws_gr_t<float>(H, wbase, nval, src, (const float*)x, (const float*)w, op, (float*)out, scratch, s, sched, slen); break;
-    default: ws_gr_t<double>(H, wbase, nval, src, (const double*)x, (const double*)w, op, (double*)out, scratch, s, sched, slen); break;
+    case 1: ws_gr_t<int64_t>(H, wbase, nval, src, (const int64_t*)x, (const int64_t*)w, op, (int64_t*)out, scratch, s, sched, slen, nx); break;
+    case 2: ws_gr_t<float>(H, wbase, nval, src, (const float*)x, (const float*)w, op, (float*)out, scratch, s, sched, slen, nx); break;
+    default: ws_gr_t<double>(H, wbase, nval, src, (const double*)x, (const double*)w, op, (double*)out, scratch, s, sched, slen, nx); break;
   }
 }
 

@@ -212,15 +212,31 @@ __global__ __launch_bounds__(NT) void k_pack_kv(const uint64_t* __restrict__ kd,
 
 // narrow pairs whose key and value bits together exceed one u64 by B <= 16
 // bits (or whose count asks for buckets): the key K (words at shifts s[w],
-// relative to bit 0) is cut into rest = K >> B and low = K & (2^B - 1); the
-// pair goes to bucket low ^ mix(rest) (balanced for skewed keys, and
-// invertible: low = bucket ^ mix(rest)) and its sort word is
-// rest << vbits | value. vw: value width 4 (u32) or 8 (u64).
+// relative to bit 0) is cut into a bucket and a rest, and the sort word is
+// rest << vbits | value. Two cuts:
+//  * hi >= 0 (ordered): bucket = K >> hi, rest = the low hi bits — buckets in
+//    key order, so the KMV's keys stay sorted (used while every bucket fits
+//    a sort, however skewed);
+//  * hi < 0 (mixed): rest = K >> B, bucket = (K & (2^B - 1)) ^ mix(rest) —
+//    balanced for skewed keys (more than 2^31 pairs), and invertible.
+// vw: value width 4 (u32) or 8 (u64).
 __device__ __forceinline__ uint32_t split_mix(uint64_t rest, int B) {
   return B ? (uint32_t)((rest * 0x9E3779B97F4A7C15ull) >> (64 - B)) : 0u;
 }
+__device__ __forceinline__ uint32_t split_cut(uint64_t K, int B, int hi, uint64_t* rest) {
+  if (hi >= 0) {
+    *rest = hi >= 64 ? K : (K & ((1ull << hi) - 1));
+    return hi >= 64 ? 0u : (uint32_t)(K >> hi);
+  }
+  *rest = B ? K >> B : K;
+  return B ? (uint32_t)(K & ((1ull << B) - 1)) ^ split_mix(*rest, B) : 0u;
+}
+__device__ __forceinline__ uint64_t split_join(uint64_t rest, uint32_t bucket, int B, int hi) {
+  if (hi >= 0) return hi >= 64 ? rest : (((uint64_t)bucket << hi) | rest);
+  return B ? (rest << B) | (uint64_t)((bucket ^ split_mix(rest, B)) & ((1u << B) - 1)) : rest;
+}
 __global__ __launch_bounds__(NT) void k_pack_kv_split(const uint64_t* __restrict__ kd, const void* __restrict__ vd,
-                                                     int vw, int64_t n, PackShifts sh, int vbits, int B,
+                                                     int vw, int64_t n, PackShifts sh, int vbits, int B, int hi,
                                                      uint64_t* __restrict__ out, int32_t* __restrict__ bkt) {
   const int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
@@ -228,20 +244,21 @@ __global__ __launch_bounds__(NT) void k_pack_kv_split(const uint64_t* __restrict
   for (int w = 0; w < sh.nw; ++w)
     if (sh.s[w] >= 0) K |= kd[i * sh.nw + w] << sh.s[w];
   const uint64_t v = vw == 4 ? (uint64_t)static_cast<const uint32_t*>(vd)[i] : static_cast<const uint64_t*>(vd)[i];
-  const uint64_t rest = B ? K >> B : K;
+  uint64_t rest;
+  const uint32_t b = split_cut(K, B, hi, &rest);
   out[i] = (rest << vbits) | v;
-  if (bkt) bkt[i] = (int32_t)((uint32_t)(K & ((1ull << B) - 1)) ^ split_mix(rest, B));
+  if (bkt) bkt[i] = (int32_t)b;
 }
 
 // the unique keys of one bucket back to key words: heads hold rest (the
-// sorted words shifted down by vbits); K = rest << B | (bucket ^ mix(rest));
+// sorted words shifted down by vbits); K = split_join(rest, bucket);
 // word w = (K >> s[w]) & mask[w]
 __global__ __launch_bounds__(NT) void k_unpack_split(const uint64_t* __restrict__ heads, int64_t m, int bucket, int B,
-                                                    PackShifts sh, PackShifts bits, uint64_t* __restrict__ keys) {
+                                                    int hi, PackShifts sh, PackShifts bits,
+                                                    uint64_t* __restrict__ keys) {
   const int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x;
   if (j >= m) return;
-  const uint64_t rest = heads[j];
-  const uint64_t K = B ? (rest << B) | (uint64_t)(((uint32_t)bucket ^ split_mix(rest, B)) & ((1u << B) - 1)) : rest;
+  const uint64_t K = split_join(heads[j], (uint32_t)bucket, B, hi);
   for (int w = 0; w < sh.nw; ++w) {
     uint64_t x = 0;
     if (sh.s[w] >= 0) {
@@ -261,6 +278,80 @@ __global__ __launch_bounds__(NT) void k_split_values(const uint64_t* __restrict_
   if (vw == 4) static_cast<uint32_t*>(vout)[i] = (uint32_t)v;
   else static_cast<uint64_t*>(vout)[i] = v;
 }
+
+// Segments of sorted packed words (key bits [vb, vb + sbits), value bits
+// below vb) without materialising the keys: a tile of SG_TILE words counts
+// its heads (word i starts a segment when its key bits differ from word
+// i - 1's); after the scan of the tile counts the second kernel writes every
+// head's position and key bits and every word's value (coalesced, word i of
+// step j is base + j * SG_NT + thread). Two reads of the words replace the
+// shift, mask, flag, scan, compact, head-gather and value-split passes.
+constexpr int SG_NT = 256, SG_IT = 16, SG_TILE = SG_NT * SG_IT;
+__device__ __forceinline__ bool sg_head(const uint64_t* __restrict__ w, int64_t i, uint64_t cur, int vb,
+                                        uint64_t km) {
+  return i == 0 || (((cur ^ w[i - 1]) >> vb) & km) != 0;
+}
+__global__ __launch_bounds__(SG_NT) void k_seg_packed_count(const uint64_t* __restrict__ w, int64_t n, int vb,
+                                                           uint64_t km, int64_t* __restrict__ tcnt) {
+  __shared__ int64_t red[SG_NT / MRH_WAVE];
+  const int64_t base = (int64_t)blockIdx.x * SG_TILE;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < SG_IT; ++j) {
+    const int64_t i = base + (int64_t)j * SG_NT + threadIdx.x;
+    if (i < n) c += sg_head(w, i, w[i], vb, km) ? 1 : 0;
+  }
+  c = dev::wave_sum(c);
+  if (dev::lane_id() == 0) red[dev::wave_id()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int q = 0; q < SG_NT / MRH_WAVE; ++q) t += red[q];
+    tcnt[blockIdx.x] = t;
+  }
+}
+__global__ __launch_bounds__(SG_NT) void k_seg_packed_write(const uint64_t* __restrict__ w, int64_t n, int vb,
+                                                           uint64_t km, const int64_t* __restrict__ tbase,
+                                                           int64_t* __restrict__ seg, uint64_t* __restrict__ heads,
+                                                           void* __restrict__ vout, int vw) {
+  constexpr int NW = SG_NT / MRH_WAVE;
+  __shared__ uint32_t wc[SG_IT * NW];
+  const int lane = dev::lane_id(), wid = dev::wave_id();
+  const int64_t base = (int64_t)blockIdx.x * SG_TILE;
+  const uint64_t vmask = vb >= 64 ? ~0ull : ((1ull << vb) - 1);
+  uint64_t kk[SG_IT], hm[SG_IT];
+#pragma unroll
+  for (int j = 0; j < SG_IT; ++j) {
+    const int64_t i = base + (int64_t)j * SG_NT + threadIdx.x;
+    const bool valid = i < n;
+    kk[j] = valid ? w[i] : 0ull;
+    const bool h = valid && sg_head(w, i, kk[j], vb, km);
+    hm[j] = __ballot(h);
+    if (lane == 0) wc[j * NW + wid] = (uint32_t)__popcll(hm[j]);
+    if (valid) {
+      if (vw == 4) static_cast<uint32_t*>(vout)[i] = (uint32_t)(kk[j] & vmask);
+      else static_cast<uint64_t*>(vout)[i] = kk[j] & vmask;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < MRH_WAVE) {  // SG_IT * NW = 64 counts, index order (step, wave)
+    const uint32_t x = wc[threadIdx.x];
+    const uint32_t inc = dev::wave_incl_scan(x);
+    wc[threadIdx.x] = inc - x;
+  }
+  __syncthreads();
+  const int64_t tb = tbase[blockIdx.x];
+  const uint64_t lt = dev::lanemask_lt();
+#pragma unroll
+  for (int j = 0; j < SG_IT; ++j) {
+    if ((hm[j] >> lane) & 1ull) {
+      const int64_t pos = tb + wc[j * NW + wid] + __popcll(hm[j] & lt);
+      seg[pos] = base + (int64_t)j * SG_NT + threadIdx.x;
+      heads[pos] = (kk[j] >> vb) & km;
+    }
+  }
+}
+static_assert(SG_IT * (SG_NT / MRH_WAVE) == MRH_WAVE, "k_seg_packed_write scans its step counts in one wave");
 
 // head bitmap (bit i of 64-bit word i / 64 set where a segment starts) ->
 // per-word counts, then the positions of the set bits (one word per thread)
@@ -484,18 +575,31 @@ void pack_kv(const uint64_t* kd, const uint64_t* vd, int64_t n, const PackShifts
   hipLaunchKernelGGL(k_pack_kv, dim3(nblk(n)), dim3(NT), 0, s, kd, vd, n, sh, out);
   MRH_CHECK_LAUNCH();
 }
-void pack_kv_split(const uint64_t* kd, const void* vd, int vw, int64_t n, const PackShifts& sh, int vbits, int B,
+void pack_kv_split(const uint64_t* kd, const void* vd, int vw, int64_t n, const PackShifts& sh, int vbits, int B, int hi,
                    uint64_t* out, int32_t* bkt, hipStream_t s) {
   if (n <= 0) return;
   check_arg(vw == 4 || vw == 8, "pack_kv_split: 4- or 8-byte values");
   check_arg(B >= 0 && B <= 16, "pack_kv_split: at most 16 bucket bits");
-  hipLaunchKernelGGL(k_pack_kv_split, dim3(nblk(n)), dim3(NT), 0, s, kd, vd, vw, n, sh, vbits, B, out, bkt);
+  hipLaunchKernelGGL(k_pack_kv_split, dim3(nblk(n)), dim3(NT), 0, s, kd, vd, vw, n, sh, vbits, B, hi, out, bkt);
   MRH_CHECK_LAUNCH();
 }
-void unpack_split(const uint64_t* heads, int64_t m, int bucket, int B, const PackShifts& sh, const PackShifts& bits,
+void unpack_split(const uint64_t* heads, int64_t m, int bucket, int B, int hi, const PackShifts& sh, const PackShifts& bits,
                   uint64_t* keys, hipStream_t s) {
   if (m <= 0) return;
-  hipLaunchKernelGGL(k_unpack_split, dim3(nblk(m)), dim3(NT), 0, s, heads, m, bucket, B, sh, bits, keys);
+  hipLaunchKernelGGL(k_unpack_split, dim3(nblk(m)), dim3(NT), 0, s, heads, m, bucket, B, hi, sh, bits, keys);
+  MRH_CHECK_LAUNCH();
+}
+int64_t seg_packed_tiles(int64_t n) { return (n + SG_TILE - 1) / SG_TILE; }
+void seg_packed_count(const uint64_t* w, int64_t n, int vb, uint64_t km, int64_t* tcnt, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_seg_packed_count, dim3((unsigned)seg_packed_tiles(n)), dim3(SG_NT), 0, s, w, n, vb, km, tcnt);
+  MRH_CHECK_LAUNCH();
+}
+void seg_packed_write(const uint64_t* w, int64_t n, int vb, uint64_t km, const int64_t* tbase, int64_t* seg,
+                      uint64_t* heads, void* vout, int vw, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_seg_packed_write, dim3((unsigned)seg_packed_tiles(n)), dim3(SG_NT), 0, s, w, n, vb, km, tbase,
+                     seg, heads, vout, vw);
   MRH_CHECK_LAUNCH();
 }
 void split_values(const uint64_t* words, int64_t n, int vbits, int vw, void* vout, hipStream_t s) {

@@ -136,16 +136,25 @@ void pack_words(const uint64_t* kd, int64_t n, const PackShifts& sh, uint64_t* o
 // out[i] = vd[i] | OR of key word w << s[w] (narrow keys and values on one u64)
 void pack_kv(const uint64_t* kd, const uint64_t* vd, int64_t n, const PackShifts& sh, uint64_t* out, hipStream_t s);
 // narrow pairs past one u64 (kvops.hip k_pack_kv_split): out[i] =
-// (K >> B) << vbits | value, bkt[i] = low B bits of K ^ mix(K >> B) (bkt may
-// be null when B == 0); vw 4 or 8; shifts s[w] place key word w in K
-void pack_kv_split(const uint64_t* kd, const void* vd, int vw, int64_t n, const PackShifts& sh, int vbits, int B,
+// rest << vbits | value, bkt[i] = the bucket (bkt may be null when B == 0);
+// hi >= 0: ordered cut (bucket K >> hi, rest the low hi bits), hi < 0: mixed
+// cut (rest K >> B, bucket low B bits ^ mix(rest)); vw 4 or 8; shifts s[w]
+// place key word w in K
+void pack_kv_split(const uint64_t* kd, const void* vd, int vw, int64_t n, const PackShifts& sh, int vbits, int B, int hi,
                    uint64_t* out, int32_t* bkt, hipStream_t s);
-// keys[j * nw + w] from the sorted heads (rest) of bucket `bucket`; bits.s[w]:
-// significant bits of word w
-void unpack_split(const uint64_t* heads, int64_t m, int bucket, int B, const PackShifts& sh, const PackShifts& bits,
-                  uint64_t* keys, hipStream_t s);
+// keys[j * nw + w] from the sorted heads (rest) of bucket `bucket` (the same
+// B, hi as the packing); bits.s[w]: significant bits of word w
+void unpack_split(const uint64_t* heads, int64_t m, int bucket, int B, int hi, const PackShifts& sh,
+                  const PackShifts& bits, uint64_t* keys, hipStream_t s);
 // vout[i] = words[i] & (2^vbits - 1) as u32 (vw 4) or u64 (vw 8)
 void split_values(const uint64_t* words, int64_t n, int vbits, int vw, void* vout, hipStream_t s);
+// segments of sorted packed words (kvops.hip k_seg_packed_*): per-tile head
+// counts, then (tbase = their exclusive scan) segment starts, head key bits
+// ((w >> vb) & km) and values (w & (2^vb - 1), vw 4 or 8)
+int64_t seg_packed_tiles(int64_t n);
+void seg_packed_count(const uint64_t* w, int64_t n, int vb, uint64_t km, int64_t* tcnt, hipStream_t s);
+void seg_packed_write(const uint64_t* w, int64_t n, int vb, uint64_t km, const int64_t* tbase, int64_t* seg,
+                      uint64_t* heads, void* vout, int vw, hipStream_t s);
 // head bitmap H (nw 64-bit words): cnt[w] = popcount; then seg[pos[w] + k] =
 // position of the k-th set bit of word w, seg[pos[nw]] = n
 void bits_count(const uint64_t* H, int64_t nw, uint32_t* cnt, hipStream_t s);
@@ -283,9 +292,11 @@ void ws_bases(const int64_t* seg, int64_t nseg, int64_t nval, int64_t* wbase, hi
 size_t ws_scratch_bytes(int64_t nval);
 // sched (nullable): 8 x slen wave ids (-1 = none); blocks b and b + 8 share an
 // XCD, so slot b % 8 runs the waves of row b % 8 (an XCD-pinned schedule)
+// nx: entries of x (> 0 enables the hot-prefix kernel: x[0, 32k) in LDS,
+// wavesegred.h k_ws_gather_reduce_hot; MRH_PR_HOT=<ids> / 0)
 void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_t nval, const int32_t* src,
                       const void* x, const void* w, int op, void* out, void* scratch, hipStream_t s,
-                      const int32_t* sched = nullptr, int64_t slen = 0);
+                      const int32_t* sched = nullptr, int64_t slen = 0, int64_t nx = 0);
 // tri_find wedges: all pairs of each neighbour group with d >= 2 (gidx:
 // those groups, wscan: the exclusive scan of their C(d,2), ngw + 1 entries);
 // wedge ids [w0, w0 + nwedge), output slot i holds wedge w0 + i, so a huge

@@ -7,8 +7,9 @@
 // and the hash-table group-by of KeyMultiValue::convert (src/keymultivalue.cpp:645-789).
 //
 //   k_global_hist : one read of the keys -> the digit histograms of all eight
-//                   8-bit digit positions (LDS atomics, one per wave for a
-//                   digit uniform over the wave; one global atomic per bin)
+//                   8-bit digit positions (wave match by ballots, one LDS
+//                   atomic per distinct digit of a wave; one global atomic
+//                   per bin)
 //   k_digit_base  : per digit position, the exclusive scan of its 256 counts =
 //                   the global start of every digit (no host round trip)
 //   k_onesweep    : one kernel per pass. A workgroup takes the next 4096-pair
@@ -57,24 +58,24 @@ __global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restric
   __shared__ uint32_t h[8][RX_BINS];
   for (int i = threadIdx.x; i < 8 * RX_BINS; i += RX_NT) (&h[0][0])[i] = 0;
   __syncthreads();
-  const int lane = dev::lane_id();
+  const uint64_t lt = dev::lanemask_lt();
   for (int64_t i = (int64_t)blockIdx.x * RX_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * RX_NT) {
-    uint64_t k = keys[i];
+    const uint64_t k = keys[i];
     const uint64_t active = __ballot(1);
-    const int first = __ffsll((long long)active) - 1;
 #pragma unroll
     for (int p = 0; p < 8; ++p)
       if (p < npos) {
-        // a digit that is the same on every active lane (the constant high
-        // bytes of small ids, or runs of sorted keys) is one add of the lane
-        // count: same-address LDS atomics from 64 lanes serialise
-        const uint32_t d = (uint32_t)(k >> (sh0 + 8 * p)) & (p == npos - 1 ? (1u << lastbits) - 1u : 255u);
-        const uint32_t d0 = (uint32_t)__shfl((int)d, first, MRH_WAVE);
-        if (__ballot(d == d0) == active) {
-          if (lane == first) atomicAdd(&h[p][d0], (uint32_t)__popcll(active));
-        } else {
-          atomicAdd(&h[p][d], 1u);
+        // lanes of equal digit found by one ballot per digit bit; the lowest
+        // of them adds their count: skewed digits (the zero high bytes of
+        // small ids, hub ids) would serialise same-address LDS atomics
+        const int nb = p == npos - 1 ? lastbits : 8;
+        const uint32_t d = (uint32_t)(k >> (sh0 + 8 * p)) & ((1u << nb) - 1u);
+        uint64_t peers = active;
+        for (int b = 0; b < nb; ++b) {
+          const uint64_t bb = __ballot((d >> b) & 1u);
+          peers &= ((d >> b) & 1u) ? bb : ~bb;
         }
+        if ((peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
       }
   }
   __syncthreads();

@@ -90,11 +90,18 @@ def test_add_out_of_core_writes_only_the_new_part(dev, tmp_path):
 
 @pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
 @pytest.mark.parametrize("vbit", [54, 58])
-def test_packed_pairs_past_64_bits_bucketed(dev, vbit):
+@pytest.mark.parametrize("mixed", [False, True])
+def test_packed_pairs_past_64_bits_bucketed(dev, vbit, mixed, monkeypatch):
     """narrow pairs whose key + value bits exceed 64 (R-MAT-22 wedges: 44 +
-    22) group in 2^B buckets (B = the excess bits; the bucket of a key is its
-    low B bits ^ a mix of the others: balanced and invertible) — exact, every
-    key's values in input order, 4- and 8-byte values, given as parts"""
+    22) group in 2^B buckets (B = the excess bits) — exact, every key's values
+    in input order, 4- and 8-byte values, given as parts. Up to 2^31 pairs the
+    bucket is the top B key bits (keys come out sorted); past that (forced
+    here by MRH_PACKED_MIXED=1) the low B bits ^ a mix of the others
+    (balanced and invertible)"""
+    if mixed:
+        monkeypatch.setenv("MRH_PACKED_MIXED", "1")
+    else:
+        monkeypatch.delenv("MRH_PACKED_MIXED", raising=False)
     gen = torch.Generator().manual_seed(vbit)
     n = 60_000
     k = torch.randint(0, 3000, (n,), generator=gen, dtype=torch.int64)
@@ -120,3 +127,5 @@ def test_packed_pairs_past_64_bits_bucketed(dev, vbit):
         fmt = "<q" if wide == 8 else "<i"
         got = {struct.unpack("<q", key)[0]: [struct.unpack(fmt, x)[0] for x in vs] for key, vs in mr.kmv_pairs()}
         assert got == dict(want)
+        if not mixed:
+            assert list(got) == sorted(got)
