@@ -297,6 +297,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                d["host_bytes"] = r.spool_stats.host_bytes;
                                d["disk_bytes"] = r.spool_stats.disk_bytes;
                                d["files"] = r.spool_stats.files;
+                               d["ooc_hot_keys"] = r.ooc_hot_keys;
+                               d["ooc_split_keys"] = r.ooc_split_keys;
                                return d;
                              })
       .def_property(

@@ -474,6 +474,8 @@ void MapReduce::note_ooc(const char* op, const OocStats& st) {
   pages_ = std::max<int64_t>(pages_, st.parts);
   spool_stats.files += st.files;
   spool_stats.disk_bytes += st.disk_bytes;
+  ooc_hot_keys += st.hot_keys;
+  ooc_split_keys += st.split_keys;
   if (set.verbosity > 0 && comm_->rank() == 0)
     out(fmt("%s out of core: %" PRId64 " partitions, %" PRId64 " budget-sized chunks through HBM, %" PRId64
             " spool files\n", op, st.parts, st.chunks, st.files));

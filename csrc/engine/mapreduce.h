@@ -172,6 +172,8 @@ class MapReduce {
 
   // tiers the bounded builders of this MR's ops spooled to (spool.h), summed
   SpoolStats spool_stats;
+  // out-of-core hot keys: grouped on the host (convert) / cut into value blocks (reduce)
+  int64_t ooc_hot_keys = 0, ooc_split_keys = 0;
 
   // host spill tier: move the data to pinned host DRAM and back
   void spill();

@@ -40,6 +40,8 @@
 #include <cstring>
 #include <limits>
 #include <stdexcept>
+#include <tuple>
+#include <unordered_map>
 
 #include "../kernels/launch.h"
 #include "kv.h"
@@ -337,6 +339,170 @@ KMV kmv_concat_host(const std::vector<KMV>& parts, const KV& like) {
 
 bool needs_ooc(int64_t bytes, int64_t budget, double factor) { return budget > 0 && bytes * factor > budget; }
 
+namespace {
+
+// one KMV whose single key holds every value of `pieces` (host / file KVs of
+// one key, in order): the key once, the values concatenated where the host
+// budget allows, else in one file. Every key is checked equal to the first on
+// the device (the pieces were routed by a 64-bit hash).
+KMV one_key_kmv(std::vector<KV>& pieces, const OocEnv& env, at::Device dev, OocStats* st, bool* in_file) {
+  const int64_t cap = std::max<int64_t>(env.hbm / 4, 1);
+  KV first;
+  std::vector<KV> vals;
+  int64_t n = 0, vbytes = 0;
+  for (KV& p : pieces) {
+    if (p.n == 0) continue;
+    const HostOff h = host_off(p);
+    if (!first.kdata.defined()) first = kv_host(kv_slice(p, 0, 1, h.kp(), h.vp()));
+    at::Tensor k0 = first.kdata.to(dev);
+    for (auto [a, b] : chunks(p, h, cap)) {
+      const KV c = kv_slice(p, a, b, h.kp(), h.vp());
+      at::Tensor kd = c.kdata.to(dev);
+      bool same;
+      if (c.kfixed()) {
+        same = c.kw == 0 || kd.view({c.n, c.kw}).eq(k0.view({1, c.kw})).all().item<bool>();
+      } else {
+        at::Tensor ko = c.koff.to(dev);
+        at::Tensor len = ko.narrow(0, 1, c.n) - ko.narrow(0, 0, c.n);
+        const int64_t L = k0.numel();
+        same = len.eq(L).all().item<bool>() && (L == 0 || kd.view({c.n, L}).eq(k0.view({1, L})).all().item<bool>());
+      }
+      if (!same) throw std::runtime_error("out-of-core convert: 64-bit key hash collision between hot keys");
+    }
+    KV v;
+    v.n = p.n;
+    v.kw = 0;
+    v.vw = p.vw;
+    v.kdata = at::empty({0}, opt(at::kCPU, at::kByte));
+    v.vdata = p.vdata;
+    v.voff = p.voff;
+    vals.push_back(v);
+    n += p.n;
+    vbytes += p.nbytes();
+  }
+  pieces.clear();
+  KMV m;
+  m.keys = first;
+  m.keys.vw = 0;
+  m.keys.vdata = at::empty({0}, opt(at::kCPU, at::kByte));
+  m.keys.voff = at::Tensor();
+  m.nkey = 1;
+  m.nval = n;
+  m.seg = at::tensor({int64_t(0), n}, opt(at::kCPU, at::kLong));
+  KV vcat;
+  *in_file = false;
+  if (env.host < 0 || vbytes <= env.host) {
+    vcat = concat(vals, at::Device(at::kCPU), /*pin=*/dev.is_cuda());
+  } else {
+    vcat = kv_to_file(vals, spool_path(env.dir, "kmv", env.instance, env.rank));
+    *in_file = true;
+    if (st) {
+      st->files++;
+      st->disk_bytes += vbytes;
+    }
+  }
+  m.vw = vcat.vw;
+  m.vdata = vcat.vdata;
+  m.voff = vcat.voff;
+  return m;
+}
+
+// sub-partition hash of level L (independent of the first pass's bits)
+at::Tensor level_hash(const at::Tensor& h, int level) {
+  static const int64_t mult[4] = {(int64_t)0x9E3779B97F4A7C15ull, (int64_t)0xC2B2AE3D27D4EB4Full,
+                                  (int64_t)0x165667B19E3779F9ull, (int64_t)0xD6E8FEB86659FD93ull};
+  at::Tensor x = at::bitwise_xor(h, at::bitwise_right_shift(h, 29)).mul_(mult[level & 3]);
+  return at::bitwise_right_shift(x, 33).bitwise_and_((int64_t(1) << 31) - 1);
+}
+
+// A partition more than a quarter of the budget (one key, or a few, hold most
+// of it: the extended-KMV case of the reference, src/keymultivalue.cpp:845-846,
+// 974-999): count pass — every chunk's keys counted on the device, candidates
+// (over 1/nchunks of the hot threshold in some chunk) summed on the host;
+// split pass — hot keys' pairs to a spool each, the rest re-partitioned by a
+// new hash; then each hot key becomes one KMV pair of values on the host (no
+// HBM copy of it ever), each sub-partition is converted in HBM or split again.
+void ooc_convert_big(std::vector<KV> pieces, const OocEnv& env, at::Device dev, OocStats* st, int level,
+                     const std::function<void(KMV&&, bool)>& keep) {
+  const int64_t budget = env.hbm, cap = std::max<int64_t>(budget / 4, 1);
+  int64_t n = 0, bytes = 0;
+  for (const KV& p : pieces) {
+    n += p.n;
+    bytes += p.nbytes();
+  }
+  if (n == 0) return;
+  // hot threshold: a quarter of a chunk's pairs
+  const int64_t chunk_pairs = std::max<int64_t>(1, (int64_t)((double)n * (double)cap / (double)std::max<int64_t>(bytes, 1)));
+  const int64_t T = std::max<int64_t>(2, chunk_pairs / 4);
+  std::vector<std::tuple<size_t, int64_t, int64_t>> ch;  // piece, a, b
+  std::vector<HostOff> hs;
+  hs.reserve(pieces.size());
+  for (size_t q = 0; q < pieces.size(); ++q) {
+    hs.push_back(host_off(pieces[q]));
+    for (auto [a, b] : chunks(pieces[q], hs.back(), cap)) ch.emplace_back(q, a, b);
+  }
+  const int64_t per_chunk = std::max<int64_t>(1, T / (int64_t)std::max<size_t>(ch.size(), 1));
+  std::unordered_map<uint64_t, int64_t> cand;
+  {
+    for (size_t i = 0; i < ch.size(); ++i) {
+      const size_t pi = std::get<0>(ch[i]);
+      KV c = kv_to(kv_slice(pieces[pi], std::get<1>(ch[i]), std::get<2>(ch[i]), hs[pi].kp(), hs[pi].vp()), dev);
+      at::Tensor h = std::get<0>(at::sort(hash64_keys(c)));
+      auto [u, inv, cnt] = at::unique_consecutive(h, false, true);
+      at::Tensor sel = cnt.gt(per_chunk);
+      at::Tensor hu = u.masked_select(sel).to(at::kCPU), hc = cnt.masked_select(sel).to(at::kCPU);
+      const int64_t* up = hu.data_ptr<int64_t>();
+      const int64_t* cp = hc.data_ptr<int64_t>();
+      for (int64_t j = 0; j < hu.numel(); ++j) cand[(uint64_t)up[j]] += cp[j];
+    }
+  }
+  std::vector<std::pair<int64_t, uint64_t>> hot;
+  for (auto& [k, c] : cand)
+    if (c >= T / 2) hot.emplace_back(c, k);
+  std::sort(hot.begin(), hot.end(), std::greater<>());
+  if (hot.size() > 64) hot.resize(64);
+  const int H = (int)hot.size();
+  const int M2 = std::min(parts_for(bytes, budget, 4.0), 256 - H);
+  if (level >= 6 || (H == 0 && M2 < 2)) {  // nothing left to cut: convert as it is
+    KV p = kv_to(concat(pieces, at::Device(at::kCPU)), dev);
+    keep(convert(p), false);
+    return;
+  }
+  std::vector<uint64_t> hk;
+  for (auto& x : hot) hk.push_back(x.second);
+  std::sort(hk.begin(), hk.end(), [](uint64_t a, uint64_t b) { return (int64_t)a < (int64_t)b; });
+  at::Tensor hot_dev = at::from_blob(hk.data(), {(int64_t)hk.size()}, opt(at::kCPU, at::kLong)).clone().to(dev);
+  auto parts = spool(pieces, cap, dev, M2 + H, [&](const KV& c) {
+    at::Tensor h = hash64_keys(c);
+    at::Tensor sub = at::remainder(level_hash(h, level), M2);
+    if (H == 0) return sub.to(at::kInt);
+    at::Tensor idx = at::searchsorted(hot_dev, h).clamp_max_(H - 1);
+    at::Tensor is_hot = hot_dev.index_select(0, idx).eq(h);
+    return at::where(is_hot, idx + M2, sub).to(at::kInt);
+  }, env, st);
+  pieces.clear();
+  for (int d = 0; d < M2; ++d) {
+    if (parts[d].empty()) continue;
+    if (parts[d].bytes() * 4 <= budget) {
+      KV p = kv_to(parts[d].gather_host(), dev);
+      parts[d].clear();
+      keep(convert(p), false);
+    } else {
+      ooc_convert_big(parts[d].take(), env, dev, st, level + 1, keep);
+    }
+  }
+  for (int j = 0; j < H; ++j) {
+    if (parts[M2 + j].empty()) continue;
+    std::vector<KV> pc = parts[M2 + j].take();
+    bool in_file = false;
+    KMV m = one_key_kmv(pc, env, dev, st, &in_file);
+    keep(std::move(m), in_file);
+    if (st) st->hot_keys++;
+  }
+}
+
+}  // namespace
+
 KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, OocStats* st) {
   const int64_t budget = env.hbm;
   int64_t bytes = 0;
@@ -352,16 +518,15 @@ KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, O
   }, env, st);
   std::vector<KMV> out;
   int64_t used = 0;
-  for (int d = 0; d < M; ++d) {
-    if (parts[d].empty()) continue;
-    KV p = kv_to(parts[d].gather_host(), dev);
-    parts[d].clear();
-    KMV m = convert(p);
-    p = KV();
+  // in_file: a hot key whose values one_key_kmv already put in a file
+  auto keep = [&](KMV&& m, bool in_file) {
     const int64_t b = m.nbytes();
-    if (env.host < 0 || used + b <= env.host) {
-      out.push_back(kmv_host(m));
-      used += b;
+    const bool on_host = m.seg.is_cpu();
+    if (env.host < 0 || used + b <= env.host || in_file) {
+      // pinned results while the host budget lasts (a file-backed hot key
+      // stays where it is)
+      out.push_back(on_host ? m : kmv_host(m));
+      if (!in_file) used += b;
     } else {  // the disk tier: one file per partition result
       out.push_back(kmv_to_file({kmv_host(m)}, spool_path(env.dir, "kmv", env.instance, env.rank)));
       if (st) {
@@ -369,6 +534,18 @@ KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, O
         st->disk_bytes += b;
       }
     }
+  };
+  for (int d = 0; d < M; ++d) {
+    if (parts[d].empty()) continue;
+    if (parts[d].bytes() * 4 > budget) {  // over budget: a hot key (or a few)
+      ooc_convert_big(parts[d].take(), env, dev, st, 1, keep);
+      continue;
+    }
+    KV p = kv_to(parts[d].gather_host(), dev);
+    parts[d].clear();
+    KMV m = convert(p);
+    p = KV();
+    keep(std::move(m), false);
   }
   int64_t total = 0;
   for (auto& m : out) total += m.nbytes();
@@ -478,8 +655,8 @@ KV ooc_exchange(const KV& kv, const at::Tensor& dest_host, const Comm& comm, con
   return sink.finish(kv);
 }
 
-void ooc_for_each_kmv_piece(const KMV& kmv, const OocEnv& env, at::Device dev, const std::function<void(const KMV&)>& fn,
-                            OocStats* st) {
+void ooc_for_each_kmv_block(const KMV& kmv, const OocEnv& env, at::Device dev,
+                            const std::function<void(const KMV&, int)>& fn, bool split, OocStats* st) {
   const int64_t budget = env.hbm;
   at::Tensor seg = kmv.seg.to(at::kCPU).contiguous();
   const int64_t* s = seg.data_ptr<int64_t>();
@@ -487,40 +664,121 @@ void ooc_for_each_kmv_piece(const KMV& kmv, const OocEnv& env, at::Device dev, c
   at::Tensor ko = kmv.keys.kw < 0 ? kmv.keys.koff.to(at::kCPU).contiguous() : at::Tensor();
   const int64_t* vop = vo.defined() ? vo.data_ptr<int64_t>() : nullptr;
   const int64_t* kop = ko.defined() ? ko.data_ptr<int64_t>() : nullptr;
-  auto vbytes = [&](int64_t a, int64_t b) {  // values of keys [a, b)
-    return kmv.vw >= 0 ? (s[b] - s[a]) * kmv.vw : vop[s[b]] - vop[s[a]] + 8 * (s[b] - s[a]);
+  auto vbytes_rows = [&](int64_t j0, int64_t j1) {  // values [j0, j1)
+    return kmv.vw >= 0 ? (j1 - j0) * kmv.vw : vop[j1] - vop[j0] + 8 * (j1 - j0);
   };
-  const int64_t cap = std::max<int64_t>(budget / 4, 1);
-  int64_t a = 0;
-  while (a < kmv.nkey) {
-    const int64_t b = grow(a, kmv.nkey, [&](int64_t e) { return vbytes(a, e) <= cap; });
+  auto vbytes = [&](int64_t a, int64_t b) { return vbytes_rows(s[a], s[b]); };  // values of keys [a, b)
+  // keys [a, b), values [j0, j1) (a block of key a when b == a + 1 and the
+  // range is part of its values) as a device KMV
+  auto piece = [&](int64_t a, int64_t b, int64_t j0, int64_t j1) {
     KMV m;
     m.nkey = b - a;
-    m.nval = s[b] - s[a];
+    m.nval = j1 - j0;
     m.keys = kv_slice(kmv.keys, a, b, kop, nullptr);
     m.vw = kmv.vw;
     if (kmv.vw >= 0) {
-      m.vdata = kmv.vdata.narrow(0, s[a] * kmv.vw, m.nval * kmv.vw);
+      m.vdata = kmv.vdata.narrow(0, j0 * kmv.vw, m.nval * kmv.vw);
     } else {
-      m.vdata = kmv.vdata.narrow(0, vop[s[a]], vop[s[b]] - vop[s[a]]);
-      m.voff = kmv.voff.narrow(0, s[a], m.nval + 1) - vop[s[a]];
+      m.vdata = kmv.vdata.narrow(0, vop[j0], vop[j1] - vop[j0]);
+      m.voff = kmv.voff.narrow(0, j0, m.nval + 1) - vop[j0];
     }
-    m.seg = kmv.seg.narrow(0, a, m.nkey + 1) - s[a];
+    if (j0 == s[a] && j1 == s[b]) m.seg = kmv.seg.narrow(0, a, m.nkey + 1) - s[a];
+    else m.seg = at::tensor({int64_t(0), m.nval}, opt(at::kCPU, at::kLong));
     KMV md = m;
     md.keys = kv_to(m.keys, dev);
     md.vdata = m.vdata.to(dev);
     if (m.voff.defined()) md.voff = m.voff.to(dev);
     md.seg = m.seg.to(dev);
-    fn(md);
+    return md;
+  };
+  const int64_t cap = std::max<int64_t>(budget / 4, 1);
+  int64_t a = 0;
+  while (a < kmv.nkey) {
+    if (split && vbytes(a, a + 1) > cap && s[a + 1] - s[a] > 1) {
+      // one key past the piece size (an extended KMV pair): its values in
+      // blocks of at most cap bytes, first / last flagged
+      int64_t j0 = s[a];
+      const int64_t je = s[a + 1];
+      while (j0 < je) {
+        int64_t j1;
+        if (kmv.vw > 0) {
+          j1 = std::min(je, j0 + std::max<int64_t>(1, cap / kmv.vw));
+        } else if (kmv.vw == 0) {
+          j1 = je;
+        } else {
+          j1 = grow(j0, je, [&](int64_t e) { return vbytes_rows(j0, e) <= cap; });
+        }
+        int flags = kBlock;
+        if (j0 == s[a]) flags |= kFirst;
+        if (j1 == je) flags |= kLast;
+        fn(piece(a, a + 1, j0, j1), flags);
+        if (st) st->chunks++;
+        j0 = j1;
+      }
+      if (st) st->split_keys++;
+      ++a;
+      continue;
+    }
+    const int64_t b = grow(a, kmv.nkey, [&](int64_t e) { return vbytes(a, e) <= cap; });
+    fn(piece(a, b, s[a], s[b]), 0);
     if (st) st->chunks++;
     a = b;
   }
 }
 
+void ooc_for_each_kmv_piece(const KMV& kmv, const OocEnv& env, at::Device dev, const std::function<void(const KMV&)>& fn,
+                            OocStats* st) {
+  ooc_for_each_kmv_block(kmv, env, dev, [&](const KMV& m, int) { fn(m); }, false, st);
+}
+
+namespace {
+// fold a block's partial result (one pair, host) into the key's running one
+void fold_partial(KV& acc, const KV& part, const std::string& op, const std::string& dtype) {
+  if (op == "first") return;
+  if (op == "last") {
+    acc = part;
+    return;
+  }
+  if (op == "count") {
+    int32_t* a = reinterpret_cast<int32_t*>(acc.vdata.data_ptr());
+    *a += *reinterpret_cast<const int32_t*>(part.vdata.data_ptr());
+    return;
+  }
+  const int opc = op == "sum" ? 0 : op == "min" ? 1 : 2;
+  auto f = [&](auto* a, const auto* b) {
+    using T = std::remove_pointer_t<decltype(a)>;
+    const T x = *b;
+    *a = opc == 0 ? T(*a + x) : opc == 1 ? (x < *a ? x : *a) : (x > *a ? x : *a);
+  };
+  void* ap = acc.vdata.data_ptr();
+  const void* bp = part.vdata.data_ptr();
+  if (dtype == "int32" || dtype == "int" || dtype == "uint32") f((int32_t*)ap, (const int32_t*)bp);
+  else if (dtype == "int64" || dtype == "uint64") f((int64_t*)ap, (const int64_t*)bp);
+  else if (dtype == "float32" || dtype == "float") f((float*)ap, (const float*)bp);
+  else f((double*)ap, (const double*)bp);
+}
+}  // namespace
+
 KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, const OocEnv& env,
                       at::Device dev, OocStats* st) {
   KVSink sink{env, st};
-  ooc_for_each_kmv_piece(kmv, env, dev, [&](const KMV& md) { sink.add(reduce_builtin(md, op, dtype)); }, st);
+  KV acc;  // the split key's running result (host, one pair)
+  ooc_for_each_kmv_block(kmv, env, dev, [&](const KMV& md, int flags) {
+    KV r = reduce_builtin(md, op, dtype);
+    if (!(flags & kBlock)) {
+      sink.add(r);
+      return;
+    }
+    // a key cut across pieces: partials carried to its last block
+    KV rh = kv_host(r);
+    rh.vdata = rh.vdata.clone();
+    if (flags & kFirst) acc = rh;
+    else fold_partial(acc, rh, op, dtype);
+    if (flags & kLast) {
+      sink.add(acc);
+      acc = KV();
+    }
+  }, true, st);
   if (sink.parts.empty()) return kv_host(reduce_builtin(kmv, op, dtype));
   return sink.finish(sink.parts[0]);
 }

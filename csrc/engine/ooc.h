@@ -14,6 +14,8 @@ struct OocStats {
   int64_t bytes_staged = 0;  // bytes moved host -> HBM in the partition pass
   int64_t files = 0;         // spool / result files written under fpath (disk tier)
   int64_t disk_bytes = 0;    // bytes those files held
+  int64_t hot_keys = 0;      // convert: keys over a quarter budget grouped on the host, never in HBM whole
+  int64_t split_keys = 0;    // reduce: keys whose values were cut into blocks across pieces
 };
 
 // where an out-of-core op may put its data (MapReduce settings)
@@ -40,6 +42,13 @@ KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& 
 // budget, as a device KMV, to fn in key order (the reduce-family ops)
 void ooc_for_each_kmv_piece(const KMV& kmv, const OocEnv& env, at::Device dev, const std::function<void(const KMV&)>& fn,
                             OocStats* st = nullptr);
+// the same, and with `split` a key whose values exceed the piece size comes as
+// several one-key pieces of consecutive value blocks (the reference's
+// extended KMV pair, src/keymultivalue.cpp:1219-1350): fn's flags are 0 for
+// whole keys, else kBlock | kFirst on its first block | kLast on its last
+constexpr int kBlock = 1, kFirst = 2, kLast = 4;
+void ooc_for_each_kmv_block(const KMV& kmv, const OocEnv& env, at::Device dev,
+                            const std::function<void(const KMV&, int)>& fn, bool split, OocStats* st = nullptr);
 // the shuffle of a KV larger than the budget (MR-MPI's paged aggregate,
 // src/mapreduce.cpp:385-563: pages in lock-step up to the global page count,
 // a two-page receive window): budget/4-byte chunks go to HBM one at a time,
