@@ -111,15 +111,18 @@ at::Tensor trimr_emit_compact(const KMV& m, int vb) {
     const int64_t nt = k::trimr_emit_tiles(nval);
     at::Tensor tcount = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kLong));
     const void* vals = m.vdata.data_ptr();
-    k::trimr_emit_fixed(0, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, nullptr, ek, nullptr, vb, cur());
+    at::Tensor tk = at::empty({nt + 1}, opt(dev, at::kLong));
+    const int64_t* tkp = P0<int64_t>(tk);
+    k::trimr_emit_tile_keys(seg, m.nkey, nval, P0<int64_t>(tk), cur());
+    k::trimr_emit_fixed(0, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, nullptr, ek, nullptr, vb, tkp, cur());
     k::trimr_emit_fixed(1, seg, m.nkey, nval, vals, P0<uint8_t>(marked), P0<int64_t>(tcount), nullptr, ek, nullptr, vb,
-                        cur());
+                        tkp, cur());
     at::Tensor tbase = exclusive_scan(tcount.narrow(0, 0, nt).contiguous());
     const int64_t T = nt > 0 ? tbase[nt].item<int64_t>() : 0;
     at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
     if (T)
       k::trimr_emit_fixed(2, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, P0<int64_t>(tbase), ek,
-                          P0<int64_t>(out), vb, cur());
+                          P0<int64_t>(out), vb, tkp, cur());
     return out;
   }
   const uint32_t* v = P0<uint32_t>(m.vdata);
@@ -155,15 +158,18 @@ at::Tensor trimr_emit(const KMV& m, int compact_vb) {
     at::Tensor marked = at::zeros({m.nkey}, opt(dev, at::kByte));
     const int64_t nt = k::trimr_emit_tiles(nval);
     at::Tensor tcount = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kLong));
-    k::trimr_emit_fixed(0, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, nullptr, ek, nullptr, 0, cur());
+    at::Tensor tk = at::empty({nt + 1}, opt(dev, at::kLong));
+    const int64_t* tkp = P0<int64_t>(tk);
+    k::trimr_emit_tile_keys(seg, m.nkey, nval, P0<int64_t>(tk), cur());
+    k::trimr_emit_fixed(0, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, nullptr, ek, nullptr, 0, tkp, cur());
     k::trimr_emit_fixed(1, seg, m.nkey, nval, vals, P0<uint8_t>(marked), P0<int64_t>(tcount), nullptr, ek, nullptr, 0,
-                        cur());
+                        tkp, cur());
     at::Tensor tbase = exclusive_scan(tcount.narrow(0, 0, nt).contiguous());
     const int64_t T = nt > 0 ? tbase[nt].item<int64_t>() : 0;
     at::Tensor out = at::empty({T, 3}, opt(dev, at::kLong));
     if (T)
       k::trimr_emit_fixed(2, seg, m.nkey, nval, vals, P0<uint8_t>(marked), nullptr, P0<int64_t>(tbase), ek,
-                          P0<int64_t>(out), 0, cur());
+                          P0<int64_t>(out), 0, tkp, cur());
     return out;
   }
   if (dev.is_cuda()) {

@@ -405,10 +405,13 @@ void trimr_low_degree(const int64_t* e, const int32_t* dg, int64_t n, int64_t* k
 // writes each tile's count of centres of marked keys to tcount[tile], phase 2
 // writes rows (centre, edge key) from tbase[tile] on. compact_vb > 0: keys are
 // one packed word vi << vb | vj and values u32 (else EDGE keys, int64 values)
+// tk (trimr_emit_tiles(nval) + 1 entries, from trimr_emit_tile_keys): the key
+// of every tile's first value, found once for the three phases
 int64_t trimr_emit_tiles(int64_t nval);
+void trimr_emit_tile_keys(const int64_t* seg, int64_t nkey, int64_t nval, int64_t* tk, hipStream_t s);
 void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval, const void* vals, uint8_t* marked,
                       int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, int compact_vb,
-                      hipStream_t s);
+                      const int64_t* tk, hipStream_t s);
 // cnt[s] = wedge centres of edge segment s if it holds the edge marker, else 0
 // (voff: variable-width values, the marker is empty; voff null: fixed 8-byte
 // values vals, the marker is the key's first vertex)

@@ -7,9 +7,9 @@
 // and the hash-table group-by of KeyMultiValue::convert (src/keymultivalue.cpp:645-789).
 //
 //   k_global_hist : one read of the keys -> the digit histograms of all eight
-//                   8-bit digit positions (wave match by ballots, one LDS
-//                   atomic per distinct digit of a wave; one global atomic
-//                   per bin)
+//                   8-bit digit positions (LDS atomics into lane-striped
+//                   copies, one per wave for a digit uniform over the wave;
+//                   one global atomic per bin)
 //   k_digit_base  : per digit position, the exclusive scan of its 256 counts =
 //                   the global start of every digit (no host round trip)
 //   k_onesweep    : one kernel per pass. A workgroup takes the next 4096-pair
@@ -52,35 +52,50 @@ constexpr uint64_t LB_AGG = 1ull << 56, LB_PRE = 2ull << 56;
 
 // the npos digits of the sorted bit range only (digit q at bit sh0 + 8q, the
 // last one lastbits wide): bits outside it are constant-heavy (zero high
-// bytes) and would serialise on one LDS bin
+// bytes) and would serialise on one LDS bin. Skewed digits (the zero high
+// bytes of small ids, hub ids) still put many lanes of a wave on one bin:
+// RX_HREP copies of the histograms, lane l adding to copy l % RX_HREP, cut
+// those same-address LDS atomics RX_HREP-fold; a digit uniform over the wave
+// is one add of the lane count.
+constexpr int RX_HREP = 4;
 __global__ __launch_bounds__(RX_NT) void k_global_hist(const uint64_t* __restrict__ keys, int64_t n, int sh0, int npos,
                                                       int lastbits, uint32_t* __restrict__ counts /*[8][256]*/) {
-  __shared__ uint32_t h[8][RX_BINS];
-  for (int i = threadIdx.x; i < 8 * RX_BINS; i += RX_NT) (&h[0][0])[i] = 0;
+  __shared__ uint32_t h[8][RX_BINS][RX_HREP];  // copies of a bin side by side: different banks
+  for (int i = threadIdx.x; i < RX_HREP * 8 * RX_BINS; i += RX_NT) (&h[0][0][0])[i] = 0;
   __syncthreads();
-  const uint64_t lt = dev::lanemask_lt();
-  for (int64_t i = (int64_t)blockIdx.x * RX_NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * RX_NT) {
-    const uint64_t k = keys[i];
+  const int lane = dev::lane_id();
+  const int rep = lane % RX_HREP;
+  auto add = [&](uint64_t k) {
     const uint64_t active = __ballot(1);
+    const int first = __ffsll((long long)active) - 1;
 #pragma unroll
     for (int p = 0; p < 8; ++p)
       if (p < npos) {
-        // lanes of equal digit found by one ballot per digit bit; the lowest
-        // of them adds their count: skewed digits (the zero high bytes of
-        // small ids, hub ids) would serialise same-address LDS atomics
-        const int nb = p == npos - 1 ? lastbits : 8;
-        const uint32_t d = (uint32_t)(k >> (sh0 + 8 * p)) & ((1u << nb) - 1u);
-        uint64_t peers = active;
-        for (int b = 0; b < nb; ++b) {
-          const uint64_t bb = __ballot((d >> b) & 1u);
-          peers &= ((d >> b) & 1u) ? bb : ~bb;
+        const uint32_t d = (uint32_t)(k >> (sh0 + 8 * p)) & (p == npos - 1 ? (1u << lastbits) - 1u : 255u);
+        const uint32_t d0 = (uint32_t)__shfl((int)d, first, MRH_WAVE);
+        if (__ballot(d == d0) == active) {
+          if (lane == first) atomicAdd(&h[p][d0][0], (uint32_t)__popcll(active));
+        } else {
+          atomicAdd(&h[p][d][rep], 1u);
         }
-        if ((peers & lt) == 0) atomicAdd(&h[p][d], (uint32_t)__popcll(peers));
       }
+  };
+  // four loads in flight per thread, then their digits
+  const int64_t stride = (int64_t)gridDim.x * RX_NT;
+  int64_t i = (int64_t)blockIdx.x * RX_NT + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const uint64_t k0 = keys[i], k1 = keys[i + stride], k2 = keys[i + 2 * stride], k3 = keys[i + 3 * stride];
+    add(k0);
+    add(k1);
+    add(k2);
+    add(k3);
   }
+  for (; i < n; i += stride) add(keys[i]);
   __syncthreads();
   for (int i = threadIdx.x; i < 8 * RX_BINS; i += RX_NT) {
-    uint32_t v = (&h[0][0])[i];
+    uint32_t v = 0;
+#pragma unroll
+    for (int r = 0; r < RX_HREP; ++r) v += (&h[0][0][0])[i * RX_HREP + r];
     if (v) atomicAdd(&counts[i], v);
   }
 }

@@ -129,22 +129,15 @@ __global__ __launch_bounds__(NT) void k_emit_write(const int64_t* __restrict__ s
 // Fixed 8-byte values (marker -1): value-parallel instead of a thread per key
 // (RMAT-20's last reduce: 1.24 G values over 190 M keys, hub pairs with 10^5
 // centres, and uncoalesced per-thread walks). One block per tile of ET_TILE
-// values stages the tile's segment starts in LDS (at most ET_TILE + 1:
-// every segment has a value) and finds each value's key by an LDS binary
-// search. PHASE 0 marks the keys holding a marker, PHASE 1 counts the
-// centres of marked keys per tile, PHASE 2 writes them at the tile's offset.
+// values: its first key comes from tk (k_emit_tile_keys, once for the three
+// phases), the key of every value from an LDS map (each key's index written
+// at its first value, then a max-scan), the marks of its keys are staged in
+// LDS, and only values of marked keys (an existing edge: ~8 % of RMAT-20's
+// wedge keys) touch the edge key. PHASE 0 marks the keys holding a marker,
+// PHASE 1 counts the centres of marked keys per tile, PHASE 2 writes them at
+// the tile's offset.
 constexpr int ET_IT = 16;
 constexpr int ET_TILE = NT * ET_IT;
-
-__device__ __forceinline__ int64_t et_upper(const int64_t* __restrict__ a, int64_t n, int64_t x) {
-  int64_t lo = 0, hi = n;  // first index with a[idx] > x
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (a[mid] <= x) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
 
 // an edge key's two vertices: EDGE {vi, vj} words, or (CMP) one packed word
 // vi << vb | vj (the compact wedges of large graphs: 8-byte keys, 4-byte values)
@@ -160,27 +153,66 @@ __device__ __forceinline__ void edge_of(const int64_t* ekey, int64_t k, int vb, 
   }
 }
 
+// the key of every tile's first value (tk[t]), one thread per key: a key
+// whose values start tiles writes their entries (every value belongs to one
+// key, so each tile is written once); tk[nt] = nkey - 1
+__global__ __launch_bounds__(NT) void k_emit_tile_keys(const int64_t* __restrict__ seg, int64_t nkey, int64_t nt,
+                                                       int64_t* __restrict__ tk) {
+  for (int64_t k = (int64_t)blockIdx.x * NT + threadIdx.x; k < nkey; k += (int64_t)gridDim.x * NT) {
+    const int64_t a = seg[k], b = seg[k + 1];
+    for (int64_t t = (a + ET_TILE - 1) / ET_TILE; t * ET_TILE < b; ++t) tk[t] = k;
+    if (k == nkey - 1) tk[nt] = k;
+  }
+}
+
 template <int PHASE, int CMP>
 __global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ seg, int64_t nkey, int64_t nval,
                                                    const void* __restrict__ vals_, uint8_t* __restrict__ marked,
                                                    int64_t* __restrict__ tcount, const int64_t* __restrict__ tbase,
-                                                   const int64_t* __restrict__ ekey, int64_t* __restrict__ out, int vb) {
-  __shared__ int64_t s_seg[ET_TILE + 1];
-  __shared__ int64_t s_k0;
-  __shared__ int s_n;
+                                                   const int64_t* __restrict__ ekey, int64_t* __restrict__ out, int vb,
+                                                   const int64_t* __restrict__ tk) {
+  // the key of every value of the tile, as an index from k0: each key
+  // starting inside the tile writes its index at its first value, a max-scan
+  // fills the rest (no per-value search)
+  __shared__ uint16_t s_kidx[ET_TILE];
+  __shared__ uint8_t s_mark[ET_TILE + 2];
+  __shared__ int32_t s_run[NT];
   __shared__ int64_t sh[NT / MRH_WAVE + 1];
   const int64_t t0 = (int64_t)blockIdx.x * ET_TILE;
   const int tn = (int)(nval - t0 < ET_TILE ? nval - t0 : ET_TILE);
-  if (threadIdx.x == 0) {
-    const int64_t k0 = et_upper(seg, nkey, t0) - 1;            // key of the tile's first value
-    const int64_t k1 = et_upper(seg, nkey, t0 + tn - 1) - 1;   // and of its last
-    s_k0 = k0;
-    s_n = (int)(k1 - k0 + 1);
+  // keys k0 .. k0 + nk - 1: the tile's first value's key to the next tile's
+  // (one more than the tile's last key when a key starts the next tile)
+  const int64_t k0 = tk[blockIdx.x];
+  const int nk = (int)(tk[blockIdx.x + 1] - k0 + 1);
+  for (int i = threadIdx.x; i < ET_TILE; i += NT) s_kidx[i] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nk; i += NT) {
+    const int64_t pos = seg[k0 + i] - t0;
+    if (pos > 0 && pos < tn) s_kidx[pos] = (uint16_t)i;
+    if (PHASE > 0) s_mark[i] = marked[k0 + i];
   }
   __syncthreads();
-  const int64_t k0 = s_k0;
-  const int nk = s_n;
-  for (int i = threadIdx.x; i <= nk; i += NT) s_seg[i] = seg[k0 + i];
+  {  // inclusive max-scan: thread t owns entries [ET_IT t, ET_IT t + ET_IT)
+    const int b = threadIdx.x * ET_IT;
+    int m = 0;
+#pragma unroll
+    for (int q = 0; q < ET_IT; ++q) m = max(m, (int)s_kidx[b + q]);
+    s_run[threadIdx.x] = m;
+    __syncthreads();
+    // exclusive max over the threads before (a log-step scan in LDS)
+    for (int o = 1; o < NT; o <<= 1) {
+      const int v = threadIdx.x >= o ? s_run[threadIdx.x - o] : 0;
+      __syncthreads();
+      s_run[threadIdx.x] = max(s_run[threadIdx.x], v);
+      __syncthreads();
+    }
+    int run = threadIdx.x ? s_run[threadIdx.x - 1] : 0;
+#pragma unroll
+    for (int q = 0; q < ET_IT; ++q) {
+      run = max(run, (int)s_kidx[b + q]);
+      s_kidx[b + q] = (uint16_t)run;
+    }
+  }
   __syncthreads();
   int64_t mine = 0;
   int64_t c_[ET_IT];
@@ -190,21 +222,17 @@ __global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ s
     const int o = it * NT + threadIdx.x;
     key_[it] = -1;
     if (o >= tn) continue;
+    const int lk = s_kidx[o];
+    if (PHASE > 0 && !s_mark[lk]) continue;  // a key without its edge: no triangle (most keys)
     const int64_t j = t0 + o;
-    int lo = 0, hi = nk;  // last key with s_seg <= j
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (s_seg[mid] <= j) lo = mid;
-      else hi = mid;
-    }
-    const int64_t k = k0 + lo;
+    const int64_t k = k0 + lk;
     const int64_t c = CMP ? (int64_t)static_cast<const uint32_t*>(vals_)[j] : static_cast<const int64_t*>(vals_)[j];
     int64_t vi, vj;
     edge_of<CMP>(ekey, k, vb, &vi, &vj);
     const bool mark = c == vi;  // an edge carries its first vertex
     if (PHASE == 0) {
       if (mark) marked[k] = 1;  // every writer stores the same byte
-    } else if (!mark && marked[k]) {
+    } else if (!mark) {
       c_[it] = c;
       key_[it] = k;
       ++mine;
@@ -234,15 +262,21 @@ __global__ __launch_bounds__(NT) void k_emit_tiles(const int64_t* __restrict__ s
 
 int64_t trimr_emit_tiles(int64_t nval) { return (nval + ET_TILE - 1) / ET_TILE; }
 
+void trimr_emit_tile_keys(const int64_t* seg, int64_t nkey, int64_t nval, int64_t* tk, hipStream_t s) {
+  if (nval <= 0 || nkey <= 0) return;
+  hipLaunchKernelGGL(k_emit_tile_keys, dim3(blocks(nkey)), dim3(NT), 0, s, seg, nkey, trimr_emit_tiles(nval), tk);
+  MRH_CHECK_LAUNCH();
+}
+
 void trimr_emit_fixed(int phase, const int64_t* seg, int64_t nkey, int64_t nval, const void* vals, uint8_t* marked,
                       int64_t* tcount, const int64_t* tbase, const int64_t* ekey, int64_t* out, int compact_vb,
-                      hipStream_t s) {
+                      const int64_t* tk, hipStream_t s) {
   if (nval <= 0 || nkey <= 0) return;
   const unsigned g = (unsigned)trimr_emit_tiles(nval);
   const int vb = compact_vb;
 #define MRH_EMIT(P, C)                                                                                             \
   hipLaunchKernelGGL((k_emit_tiles<P, C>), dim3(g), dim3(NT), 0, s, seg, nkey, nval, vals, marked, tcount, tbase, \
-                     ekey, out, vb)
+                     ekey, out, vb, tk)
   if (vb > 0) {
     if (phase == 0) MRH_EMIT(0, 1);
     else if (phase == 1) MRH_EMIT(1, 1);
