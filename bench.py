@@ -325,6 +325,10 @@ def spawn_ranks(n, argv):
     return rc
 
 
+def _round16(x):
+    return (x + 15) // 16 * 16
+
+
 def bench_pagerank_extra(comm, args):
     """PageRank RMAT-2^scale x iters inside the headline run (extra keys)."""
     from gpu_mapreduce_amd import MapReduce
@@ -368,6 +372,11 @@ def bench_pagerank_extra(comm, args):
         "pagerank_kvps_incl_setup": nedge * iters / (dt + setup),
         "pagerank_hip_graph_iterations": pr.graph_iterations,
         "pagerank_layout": pr.layout,
+        "pagerank_comm_bytes_per_iter": comm.allreduce(pr.comm_bytes_per_iter, "max"),
+        "pagerank_comm_overlapped": bool(pr.overlapped),
+        # what the replicated plan moves per rank and iteration at P = 8: the
+        # other 7 ranks' c slices (active sources / 8, 64-byte aligned), fp32
+        "pagerank_comm_bytes_per_iter_p8_predicted": 7 * 4 * _round16(-(-((1 << scale) - pr.ndangling) // 8)) + 16,
         "pagerank_config": {"graph": f"RMAT-2^{scale}", "edgefactor": ef, "edges": nedge, "iters": iters,
                             "runs_timed": args.pagerank_steps, "alpha": 0.85, "scaling": "strong",
                             "rank_dtype": "fp32 ranks, fp64 L1/dangling reductions"},
@@ -505,7 +514,8 @@ def bench_dist_plans(comm, args):
         try:
             r = bench_pagerank_extra(fc, args)
             out.update({"pagerank_dist_ms": r["pagerank_ms"], "pagerank_dist_setup_ms": r["pagerank_setup_ms"],
-                        "pagerank_dist_layout": r.get("pagerank_layout")})
+                        "pagerank_dist_layout": r.get("pagerank_layout"),
+                        "pagerank_dist_comm_bytes_per_iter": r.get("pagerank_comm_bytes_per_iter")})
         except Exception as e:  # noqa: BLE001
             out["pagerank_dist_error"] = f"{type(e).__name__}: {e}"[:500]
         if args.trifind_scale > 0:

@@ -682,6 +682,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           d["ms"] = s.seconds * 1e3;
           d["pairs_in"] = s.pairs_in;
           d["pairs_out"] = s.pairs_out;
+          d["h2d_bytes"] = s.h2d_bytes;
+          d["d2h_bytes"] = s.d2h_bytes;
           st.append(d);
         }
         py::dict d;
@@ -776,6 +778,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("xcd_ranges", &PageRankPlan::xcd_ranges_count)
       .def_property_readonly("layout", &PageRankPlan::layout)
       .def_property_readonly("c_slice", &PageRankPlan::c_slice)
+      .def_property_readonly("comm_bytes_per_iter", &PageRankPlan::comm_bytes_per_iter)
+      .def_property_readonly("overlapped", &PageRankPlan::overlapped)
       .def_readwrite("use_graph", &PageRankPlan::use_graph)
       .def_property_readonly("graph_iterations", &PageRankPlan::graph_iterations)
       .def_readonly("nedge", &PageRankPlan::nedge)

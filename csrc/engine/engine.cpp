@@ -4,6 +4,7 @@
 //   cpu: straightforward host loops with identical semantics and identical
 //        output order (they are the oracle the GPU tests compare against).
 #include "kv.h"
+#include "xfer.h"
 #include "grouper.h"
 
 #include <ATen/hip/HIPContext.h>
@@ -101,6 +102,7 @@ KV make_kv(at::Tensor kdata, c10::optional<at::Tensor> koff, at::Tensor vdata, c
 }
 
 KV kv_to(const KV& kv, at::Device dev) {
+  for (const at::Tensor* t : {&kv.kdata, &kv.vdata, &kv.koff, &kv.voff}) note_xfer(*t, dev);
   KV o = kv;
   o.kdata = kv.kdata.to(dev);
   o.vdata = kv.vdata.to(dev);

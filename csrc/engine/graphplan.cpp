@@ -594,21 +594,63 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   nedge = pk.numel();
   if (nedge >= (int64_t(1) << 32)) throw std::runtime_error("PageRankPlan: >= 2^32 in-edges on one rank");
   clk("exchange to dest owner");
-  // 3. XCD source ranges over the interleaved global order; the degree of
-  // every gid is the all-gathered degree array read column-major
+  // 3. XCD source ranges over the interleaved global order gid = new id * P +
+  // rank (the degree of every gid: the all-gathered degree array read
+  // column-major). Several ranks (MRH_PR_OVERLAP != 0): first cut into K
+  // source chunks of equal edge count (MRH_PR_PIECES, default 4) — chunk j =
+  // new ids [b_j, b_j+1) of every rank, a contiguous run of gids — each with
+  // its own ranges, so that chunk j's edges are one contiguous run the gather
+  // can take on as soon as round j of the c exchange has landed.
   const int dbits = pr_bits_for(std::max<int64_t>(nlocal - 1, 0));
+  const char* oenv = std::getenv("MRH_PR_OVERLAP");
+  const bool by_piece = P > 1 && !(oenv && *oenv == '0');
   std::vector<int64_t> rb, redge;
-  if (degn.defined()) {
+  std::vector<int> piece_nr;  // ranges of every chunk (by_piece)
+  at::Tensor dg;
+  {
     at::Tensor dl = at::zeros({S}, opt(dev, at::kInt));
-    const int64_t k0 = std::min(S, nlocal);
+    const int64_t k0 = degn.defined() ? std::min(S, nlocal) : 0;
     if (k0 > 0) dl.narrow(0, 0, k0).copy_(degn.narrow(0, 0, k0));
-    at::Tensor dall = at::empty({P * S}, opt(dev, at::kInt));
-    comm->allgather_bytes(dl.data_ptr(), dall.data_ptr(), S * 4);
-    at::Tensor dg = dall.view({P, S}).t().contiguous().view({-1});
-    dl = dall = at::Tensor();
+    if (degn.defined() || by_piece) {
+      at::Tensor dall = at::empty({P * S}, opt(dev, at::kInt));
+      comm->allgather_bytes(dl.data_ptr(), dall.data_ptr(), S * 4);
+      dg = dall.view({P, S}).t().contiguous().view({-1});
+    }
+  }
+  const bool want_ranges = degn.defined();
+  degn = at::Tensor();
+  if (by_piece) {
+    int K = 4;
+    if (const char* e = std::getenv("MRH_PR_PIECES")) K = std::max(1, std::min(64, std::atoi(e)));
+    // chunk boundaries b_j (new ids, multiples of 16: 64-byte aligned
+    // transfers) at the edge-count quantiles of the degree-sorted ids
+    at::Tensor cum = at::cumsum(dg.to(at::kLong), 0);
+    const int64_t total = S > 0 ? cum[P * S - 1].item<int64_t>() : 0;
+    std::vector<int64_t> b{0};
+    for (int j = 1; j < K && total > 0; ++j) {
+      at::Tensor t = at::tensor({total * j / K}, opt(at::kCPU, at::kLong)).to(dev);
+      const int64_t g = at::searchsorted(cum, t).item<int64_t>();  // first gid reaching the quantile
+      const int64_t id = std::min(S, (g / P + 16) / 16 * 16);
+      if (id > b.back() && id < S) b.push_back(id);
+    }
+    b.push_back(S);
+    chunk_b_ = b;
+    // at most 2^(32 - dbits) ranges in all, shared by the chunks
+    const int nch = (int)b.size() - 1;
+    const int cap_each = std::max(1, (1 << std::max(0, std::min(9, 32 - dbits))) / nch);
+    for (int j = 0; j < nch; ++j) {
+      const int64_t g0 = P * b[j], len = P * (b[j + 1] - b[j]);
+      std::vector<int64_t> rbq, rdq;
+      if (want_ranges && cap_each >= 9) xcd_ranges(dg.narrow(0, g0, len), len, dbits, rbq, rdq, cap_each);
+      rb.push_back(g0);
+      for (size_t q = 1; q < rbq.size(); ++q) rb.push_back(g0 + rbq[q]);
+      piece_nr.push_back(std::max<int>(1, (int)rbq.size()));
+    }
+  } else if (want_ranges) {
     xcd_ranges(dg, P * S, dbits, rb, redge);
   }
-  degn = at::Tensor();
+  dg = at::Tensor();
+  // nhot: range boundaries past the first (ranges = nhot + 1)
   const int nhot = rb.empty() ? 0 : (int)rb.size() - 1;
   at::Tensor rbd;
   if (nhot > 0) {
@@ -618,6 +660,7 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   int rbits = 0;
   while ((1 << rbits) < nhot + 1) ++rbits;
   if (nhot == 0) rbits = 0;
+  if (dbits + rbits > 32) throw std::runtime_error("PageRankPlan: range and destination bits exceed 32");
   // 4. sort by (range, destination), unpack
   at::Tensor sorted;
   {
@@ -645,7 +688,9 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   k::pr_group_vid(hi.data_ptr<int64_t>(), ngrp, nullptr, (int64_t(1) << dbits) - 1, ghi_.data_ptr<int32_t>(), s);
   xoff_ = at::empty({xr_ * (xtile_ + 1)}, opt(dev, at::kLong));
   k::pr_range_offsets(hi.data_ptr<int64_t>(), ngrp, dbits, xr_, xtile_, xoff_.data_ptr<int64_t>(), s);
-  if (nhot > 0 && ngrp > 0) {
+  if (by_piece) {
+    build_pieces(piece_nr);
+  } else if (nhot > 0 && ngrp > 0) {
     // exact first edge of every range on this rank (the gather's wave
     // schedule); the ranges themselves came from the global degrees
     at::Tensor first = xoff_.view({xr_, xtile_ + 1}).select(1, 0).clamp_max(ngrp).contiguous();
@@ -662,20 +707,116 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   clk("unpack + groups");
 }
 
+// the source pieces of the overlapped iteration (see graphplan.h): the first
+// group / edge of every range from the plan, each piece's run of source ids
+// copied to a 16-byte aligned slot of srcp_, its segment index and schedule
+void PageRankPlan::build_pieces(const std::vector<int>& piece_nr) {
+  pieces_.clear();
+  const int K = (int)piece_nr.size();
+  const int64_t ngrp = seg_.numel() - 1;
+  std::vector<int64_t> fg = to_vec(xoff_.view({xr_, xtile_ + 1}).select(1, 0).clamp_max(ngrp).contiguous());
+  fg.push_back(ngrp);
+  at::Tensor fgd = at::from_blob(fg.data(), {(int64_t)fg.size()}, opt(at::kCPU, at::kLong)).to(dev);
+  std::vector<int64_t> fe = to_vec(seg_.index_select(0, fgd));  // first edge of every range, then nedge
+  std::vector<int64_t> R0(K + 1, 0);                           // first range of every piece
+  for (int q = 0; q < K; ++q) R0[q + 1] = R0[q] + piece_nr[q];
+  if (R0[K] != xr_) throw std::runtime_error("PageRankPlan: piece ranges do not add up");
+  std::vector<int64_t> off(K + 1, 0);
+  for (int q = 0; q < K; ++q) off[q + 1] = off[q] + (fe[R0[q + 1]] - fe[R0[q]] + 3) / 4 * 4;
+  srcp_ = at::empty({std::max<int64_t>(off[K], 4)}, opt(dev, at::kInt));
+  for (int q = 0; q < K; ++q) {
+    Piece pc;
+    const int64_t e0 = fe[R0[q]];
+    pc.g0 = fg[R0[q]];
+    pc.ng = fg[R0[q + 1]] - pc.g0;
+    pc.n = fe[R0[q + 1]] - e0;
+    if (pc.n > 0 && pc.ng > 0) {
+      pc.src = srcp_.narrow(0, off[q], pc.n);
+      pc.src.copy_(src_.narrow(0, e0, pc.n));
+      pc.six = seg_index(seg_.narrow(0, pc.g0, pc.ng + 1) - e0, pc.n);
+      if (piece_nr[q] > 1) {
+        std::vector<int64_t> re;
+        for (int64_t r = R0[q]; r < R0[q + 1]; ++r) re.push_back(fe[r] - e0);
+        re.push_back(pc.n);
+        auto [sc, sl] = wave_schedule(re, pc.n);
+        pc.six.sched = sc;
+        pc.six.slen = sl;
+      }
+    }
+    pieces_.push_back(std::move(pc));
+  }
+  pr_chk(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate");
+  ring_ev_.assign(K + 1, nullptr);
+  for (auto& e : ring_ev_) pr_chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+}
+
+void PageRankPlan::ring_free() {
+  for (auto& e : ring_ev_)
+    if (e) (void)hipEventDestroy(e);
+  ring_ev_.clear();
+  if (side_) (void)hipStreamDestroy(side_);
+  side_ = nullptr;
+}
+
+// the c exchange on side_, behind the work queued so far on the current
+// stream (the last tile step): round j sends chunk j of this rank's slice to
+// every peer and receives theirs — one grouped round over all xGMI links at
+// once, not a ring over one — and records ring_ev_[j + 1]
+void PageRankPlan::ring_start() {
+  const hipStream_t cs = at::hip::getCurrentHIPStream();
+  pr_chk(hipEventRecord(ring_ev_[0], cs), "hipEventRecord");
+  pr_chk(hipStreamWaitEvent(side_, ring_ev_[0], 0), "hipStreamWaitEvent");
+  const c10::DeviceIndex di = dev.has_index() ? dev.index() : c10::hip::current_device();
+  c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(side_, di));
+  uint8_t* base = reinterpret_cast<uint8_t*>(cfull_.data_ptr());
+  for (size_t j = 0; j + 1 < chunk_b_.size(); ++j) {
+    const int64_t a = chunk_b_[j] * 4, len = (chunk_b_[j + 1] - chunk_b_[j]) * 4;
+    std::vector<Xfer> xs, xr;
+    for (int p = 0; p < P; ++p) {
+      if (p == me) continue;
+      xs.push_back(Xfer{p, base + (int64_t)me * S_ * 4 + a, len});
+      xr.push_back(Xfer{p, base + (int64_t)p * S_ * 4 + a, len});
+    }
+    comm->sendrecv(xs, xr);
+    pr_chk(hipEventRecord(ring_ev_[j + 1], side_), "hipEventRecord");
+  }
+}
+
 // one multi-GPU iteration from r into rn: gather from the replicated c,
 // fused tile step (writes this rank's c slice in place), (L1, dangling)
-// partials -> allreduce, in-place all-gather of the c slices
+// partials -> allreduce; then the c slices go to every rank. With source
+// pieces the exchange of the previous tile step's slices runs on side_ in
+// chunk rounds, and piece j is gathered right after round j landed (while
+// round j + 1 is in flight); the tile step waits for every piece. Else one
+// all-gather after the tile step.
 void PageRankPlan::launch_iter_dist(const at::Tensor& r, at::Tensor& rn) {
-  if (six_.defined()) seg_gather_reduce(six_, src_, cfull_, at::Tensor(), 0, send_);
-  const double base = (1.0 - alpha) / (double)N;
   const hipStream_t s = at::hip::getCurrentHIPStream();
+  const bool pieces = !pieces_.empty();
+  if (pieces) {
+    const bool ring = !c_fresh_;
+    if (ring) ring_start();
+    for (size_t q = 0; q < pieces_.size(); ++q) {
+      // every round is waited for, even by an empty piece: the tile step
+      // below writes past this rank's slice into the next rank's chunk 0
+      if (ring) pr_chk(hipStreamWaitEvent(s, ring_ev_[q + 1], 0), "hipStreamWaitEvent");
+      Piece& pc = pieces_[q];
+      if (pc.n > 0 && pc.ng > 0) {
+        at::Tensor o = send_.narrow(0, pc.g0, pc.ng);
+        seg_gather_reduce(pc.six, pc.src, cfull_, at::Tensor(), 0, o);
+      }
+    }
+  } else if (six_.defined()) {
+    seg_gather_reduce(six_, src_, cfull_, at::Tensor(), 0, send_);
+  }
+  const double base = (1.0 - alpha) / (double)N;
   k::pr_tile_step(send_.data_ptr<float>(), ghi_.data_ptr<int32_t>(), xoff_.data_ptr<int64_t>(), (int)xr_, xtile_,
                   nlocal, r.data_ptr<float>(), rn.data_ptr<float>(), dangling_.data_ptr<uint8_t>(), (float)base,
                   (float)alpha, stats_.data_ptr<double>() + 1, 1.0 / (double)N, invdeg_.data_ptr<float>(),
                   c_.data_ptr<float>(), part_.data_ptr<double>(), s);
   k::pr_partials_sum(part_.data_ptr<double>(), xtile_, stats_.data_ptr<double>(), s);
   comm->allreduce_tensor(stats_, Comm::SUM);
-  comm->allgather_bytes(c_.data_ptr(), cfull_.data_ptr(), S_ * 4);
+  if (pieces) c_fresh_ = false;  // the next iteration starts the ring
+  else comm->allgather_bytes(c_.data_ptr(), cfull_.data_ptr(), S_ * 4);
 }
 
 // XCD source ranges. Each XCD has its own 4 MiB L2; the pull gather reads
@@ -689,7 +830,7 @@ void PageRankPlan::launch_iter_dist(const at::Tensor& r, at::Tensor& rn) {
 // rb: the hot range boundaries (nhot + 1 new ids), redge: the first edge of
 // every range, hot and cold (nhot + 2 entries, redge.back() = nedge).
 void PageRankPlan::xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits, std::vector<int64_t>& rb,
-                              std::vector<int64_t>& redge) {
+                              std::vector<int64_t>& redge, int maxr_cap) {
   // the widest range's slice of x is 85 % of l2: 3 MiB of each XCD's 4 MiB L2
   // measured best with the fused tile step — RMAT-26 x20 at 2 / 3 / 4 / 5 /
   // 6 MiB: 124.4 / 122.8 / 125.1 / 138.6 / 143.6 ms (profiles/r3_pagerank_sweep.txt)
@@ -697,7 +838,7 @@ void PageRankPlan::xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits
   if (const char* e = std::getenv("MRH_PR_L2_BYTES")) l2 = std::max<int64_t>(4096, std::atoll(e));
   const int64_t cap = l2 / 4 * 85 / 100;
   if (nactive <= cap) return;  // the whole active rank vector fits one L2
-  const int maxr = std::min(64, 1 << std::max(0, std::min(6, 32 - dbits)));
+  const int maxr = std::min(std::min(64, maxr_cap), 1 << std::max(0, std::min(6, 32 - dbits)));
   int maxl = (maxr - 1) / 8;
   if (const char* e = std::getenv("MRH_PR_XCD_LAYERS")) maxl = std::max(0, std::min(maxl, std::atoi(e)));
   if (maxl <= 0) return;
@@ -751,22 +892,27 @@ void PageRankPlan::xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits
 // the 8 x slen wave schedule of the gather: wave w (edges [1024 w, 1024 w +
 // 1024)) belongs to the range holding its first edge; hot range r runs on
 // slot r % 8 in layer order, the cold waves are dealt round-robin after them
-void PageRankPlan::xcd_schedule(const std::vector<int64_t>& redge) {
+std::pair<at::Tensor, int64_t> PageRankPlan::wave_schedule(const std::vector<int64_t>& redge, int64_t n) const {
   const int64_t T = 1024;  // wavesegred.h WS_TILE
-  const int64_t nw = (nedge + T - 1) / T;
+  const int64_t nw = (n + T - 1) / T;
   const int nhot = (int)redge.size() - 2;
   std::vector<std::vector<int32_t>> rows(8);
   auto wave_of = [&](int64_t e) { return std::min(nw, (e + T - 1) / T); };
   for (int r = 0; r < nhot; ++r)
     for (int64_t w = wave_of(redge[r]); w < wave_of(redge[r + 1]); ++w) rows[r % 8].push_back((int32_t)w);
   int64_t c = 0;
-  for (int64_t w = wave_of(redge[nhot]); w < nw; ++w, ++c) rows[c % 8].push_back((int32_t)w);
+  for (int64_t w = wave_of(redge[std::max(nhot, 0)]); w < nw; ++w, ++c) rows[c % 8].push_back((int32_t)w);
   size_t slen = 0;
   for (auto& r : rows) slen = std::max(slen, r.size());
   std::vector<int32_t> flat(8 * slen, -1);
   for (int x = 0; x < 8; ++x) std::copy(rows[x].begin(), rows[x].end(), flat.begin() + x * slen);
-  xsched_ = at::from_blob(flat.data(), {8, (int64_t)slen}, opt(at::kCPU, at::kInt)).to(dev);
-  xslen_ = (int64_t)slen;
+  return {at::from_blob(flat.data(), {8, (int64_t)slen}, opt(at::kCPU, at::kInt)).to(dev), (int64_t)slen};
+}
+
+void PageRankPlan::xcd_schedule(const std::vector<int64_t>& redge) {
+  auto [sc, slen] = wave_schedule(redge, nedge);
+  xsched_ = sc;
+  xslen_ = slen;
 }
 
 void PageRankPlan::build_exchange(const at::Tensor& ujv, const at::Tensor& new_of_old) {
@@ -904,6 +1050,7 @@ void PageRankPlan::reset() {
   dmass_ = stats_.narrow(0, 1, 1);  // the dangling mass of the previous iteration
   acc_.zero_();
   if (dist_dev_) comm->allgather_bytes(c_.data_ptr(), cfull_.data_ptr(), S_ * 4);
+  c_fresh_ = true;
 }
 
 // one XCD-path iteration: gather + segmented reduce of c into send_, then
@@ -920,7 +1067,10 @@ void PageRankPlan::launch_iter(const at::Tensor& r, at::Tensor& rn) {
   k::pr_partials_sum(part_.data_ptr<double>(), xtile_, stats_.data_ptr<double>(), s);
 }
 
-PageRankPlan::~PageRankPlan() { graph_free(); }
+PageRankPlan::~PageRankPlan() {
+  graph_free();
+  ring_free();
+}
 
 void PageRankPlan::graph_free() {
   if (gexec_) (void)hipGraphExecDestroy(gexec_);

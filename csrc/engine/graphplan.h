@@ -113,9 +113,13 @@ class PageRankPlan {
   hipEvent_t gev_[2] = {nullptr, nullptr};
   std::vector<const void*> gkey_;
   int64_t graph_iters_ = 0;
+  // maxr_cap: at most this many ranges (hot + cold)
   void xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits, std::vector<int64_t>& rb,
-                  std::vector<int64_t>& redge);
+                  std::vector<int64_t>& redge, int maxr_cap = 64);
   void xcd_schedule(const std::vector<int64_t>& redge);
+  // the 8 x slen wave schedule of n edges whose ranges start at redge (hot
+  // ranges, then the cold one; redge.back() = n)
+  std::pair<at::Tensor, int64_t> wave_schedule(const std::vector<int64_t>& redge, int64_t n) const;
   // the plan from this rank's edges (source-owned): device kernels, or the
   // tensor-op twin on the CPU engine
   void build_device(const at::Tensor& e);
@@ -134,6 +138,27 @@ class PageRankPlan {
   bool dist_dev_ = false, mix_ = false;
   int64_t S_ = 0;      // c slice length per rank
   at::Tensor cfull_;   // the replicated c vector, P slices of S_ (+ slack)
+  // several GPUs: the edges cut into K pieces by source chunk (chunk j = new
+  // ids [chunk_b_[j], chunk_b_[j + 1]) of every rank, equal edge counts),
+  // each with its own XCD ranges, segment index and 16-byte aligned source
+  // stream; the c exchange runs on side_ in K rounds (round j: chunk j of
+  // every slice, to and from every peer at once) and piece j is gathered as
+  // soon as round j has landed (MRH_PR_OVERLAP=0: one all-gather after the
+  // tile step, then one gather)
+  struct Piece {
+    SegIndex six;
+    at::Tensor src;
+    int64_t g0 = 0, ng = 0, n = 0;  // first group, groups, edges
+  };
+  std::vector<Piece> pieces_;
+  std::vector<int64_t> chunk_b_;
+  at::Tensor srcp_;
+  bool c_fresh_ = true;  // cfull_ holds every rank's slice of the last tile step
+  hipStream_t side_ = nullptr;
+  std::vector<hipEvent_t> ring_ev_;
+  void build_pieces(const std::vector<int>& piece_nr);
+  void ring_start();
+  void ring_free();
   // several ranks: the destination-owner side of the exchange from the
   // group destinations ujv (global ids) and the new id of every old local id
   void build_exchange(const at::Tensor& ujv, const at::Tensor& new_of_old);
@@ -150,6 +175,10 @@ class PageRankPlan {
   // "partials" (source-owned + all-to-all of partial sums), "local"
   std::string layout() const { return dist_dev_ ? "replicated" : comm->distributed() ? "partials" : "local"; }
   int64_t c_slice() const { return S_; }
+  // bytes this rank receives per iteration (the c slices of the other ranks
+  // and the 16-byte stats allreduce; 0 on one rank)
+  int64_t comm_bytes_per_iter() const { return dist_dev_ && P > 1 ? (int64_t)(P - 1) * S_ * 4 + 16 : 0; }
+  bool overlapped() const { return !pieces_.empty(); }
   int64_t xcd_ranges_count() const { return xr_; }
   // fixed-count run() replays a captured HIP graph (MRH_PR_GRAPH=0: off)
   bool use_graph = true;

@@ -1,5 +1,6 @@
 // Native MapReduce object (see mapreduce.h). Reference behaviour cited per
 // method as src/mapreduce.cpp:<lines>.
+#include "xfer.h"
 #include "mapreduce.h"
 #include "guard.h"
 #include "hbmpool.h"
@@ -212,6 +213,7 @@ KMV clone_kmv(const KMV& m) {
 }
 at::Tensor to_host(const at::Tensor& t, bool pin) {
   if (!t.defined()) return t;
+  note_xfer(t, at::Device(at::kCPU));
   at::Tensor h = t.to(at::kCPU);
   if (pin && t.is_cuda()) h = h.pin_memory();
   return h;
@@ -233,6 +235,7 @@ KMV kmv_to(const KMV& m, at::Device d, bool pin) {
     o.seg = to_host(m.seg, pin);
   } else {
     o.keys = kv_to(m.keys, d);
+    for (const at::Tensor* t : {&m.vdata, &m.voff, &m.seg}) note_xfer(*t, d);
     o.vdata = m.vdata.to(d);
     if (m.voff.defined()) o.voff = m.voff.to(d);
     o.seg = m.seg.to(d);

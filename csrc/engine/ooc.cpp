@@ -48,6 +48,7 @@
 #include "comm.h"
 #include "ooc.h"
 #include "spool.h"
+#include "xfer.h"
 
 namespace mrh {
 
@@ -58,6 +59,7 @@ at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions
 at::Tensor host(const at::Tensor& t) {
   if (!t.defined()) return t;
   if (t.is_cpu()) return t.contiguous();
+  note_xfer(t, at::Device(at::kCPU));
   return t.to(at::TensorOptions().device(at::kCPU).pinned_memory(true), /*non_blocking=*/false, /*copy=*/true);
 }
 KV kv_host(const KV& kv) {
@@ -157,6 +159,7 @@ KV kv_to_async(const KV& kv, at::Device dev, const c10::hip::HIPStream& side, co
   c10::hip::HIPStreamGuard g(side);
   auto one = [&](const at::Tensor& t) {
     if (!t.defined()) return t;
+    note_xfer(t, dev);
     at::Tensor d = t.to(dev, /*non_blocking=*/true);
     if (d.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(d.storage().data_ptr(), use);
     return d;
@@ -686,6 +689,9 @@ void ooc_for_each_kmv_block(const KMV& kmv, const OocEnv& env, at::Device dev,
     else m.seg = at::tensor({int64_t(0), m.nval}, opt(at::kCPU, at::kLong));
     KMV md = m;
     md.keys = kv_to(m.keys, dev);
+    note_xfer(m.vdata, dev);
+    note_xfer(m.voff, dev);
+    note_xfer(m.seg, dev);
     md.vdata = m.vdata.to(dev);
     if (m.voff.defined()) md.voff = m.voff.to(dev);
     md.seg = m.seg.to(dev);

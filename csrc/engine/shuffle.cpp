@@ -41,6 +41,7 @@
 #include <exception>
 #include <stdexcept>
 
+#include "xfer.h"
 #include "../kernels/hashfn.h"
 #include "../kernels/launch.h"
 #include "comm.h"
@@ -542,11 +543,13 @@ KV exchange(KV kv, const at::Tensor& dest_given, const Comm& comm, const Exchang
     }
     const hipStream_t cp = copy_stream->stream();
     guard::hip_check(hipStreamWaitEvent(cp, landed, 0), "drain_wait", me);
-    for (const Drain& d : drains)
+    for (const Drain& d : drains) {
+      note_xfer_bytes(false, d.bytes);
       if (d.bytes)
         guard::hip_check(hipMemcpyAsync(d.dst, P0<uint8_t>(stage[k % 2]) + d.stage_off, (size_t)d.bytes,
                                         hipMemcpyDeviceToHost, cp),
                          "drain_copy", me);
+    }
     guard::hip_check(hipEventRecord(drained[k % 2], cp), "drain_event", me);
     if (!comm.uses_rccl()) guard::hip_check(hipEventDestroy(landed), "landed_event", me);
   }

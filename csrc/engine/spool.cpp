@@ -1,4 +1,5 @@
 // Spool (spool.h): HBM -> pinned host -> memory-mapped disk file.
+#include "xfer.h"
 #include "spool.h"
 
 #include <ATen/hip/HIPContext.h>
@@ -329,6 +330,7 @@ void Spool::add(const KV& piece, hipStream_t copy) {
       if (!t.defined()) return t;
       if (t.is_cpu() && (!cuda || t.is_pinned())) return t;
       at::Tensor o = at::empty(t.sizes(), t.options().device(at::kCPU).pinned_memory(cuda));
+      note_xfer(t, at::Device(at::kCPU));
       if (async) {
         at::Tensor src = t.contiguous();
         const size_t nb = (size_t)src.numel() * src.element_size();

@@ -6,6 +6,7 @@
 #include "callbacks.h"
 #include "engine/comm.h"
 #include "engine/tri.h"
+#include "engine/xfer.h"
 
 namespace mrh {
 namespace oink {
@@ -24,11 +25,15 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
     s.pairs_in = npairs(m);
     comm.host_wait();
     comm.barrier();
+    const XferCount x0 = xfer_count();
     const double t0 = Comm::wtime();
     op();
     comm.host_wait();
     comm.barrier();
     s.seconds = Comm::wtime() - t0;
+    const XferCount x1 = xfer_count();
+    s.h2d_bytes = x1.h2d - x0.h2d;
+    s.d2h_bytes = x1.d2h - x0.d2h;
     s.pairs_out = npairs(m);
     run.stages.push_back(s);
   };

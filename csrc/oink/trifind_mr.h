@@ -15,6 +15,7 @@ struct TriMRStage {
   std::string op;       // "map_edge_vert", "collate 1", ...
   double seconds = 0;   // device-synchronised wall time of the op
   int64_t pairs_in = 0, pairs_out = 0;  // global pair counts before / after
+  int64_t h2d_bytes = 0, d2h_bytes = 0;  // this rank's host <-> device copies during the op (xfer.h)
 };
 struct TriMRRun {
   uint64_t triangles = 0;

@@ -75,6 +75,11 @@ class PageRank:
         # all-to-all of partial sums: CPU engine / MRH_PR_DIST=partials)
         self.layout = self._p.layout
         self.c_slice = self._p.c_slice
+        # bytes this rank receives per iteration (other ranks' c slices + the
+        # 16-byte stats allreduce); overlapped: the ring all-gather of c runs
+        # under the gather of the slices already in (several GPUs)
+        self.comm_bytes_per_iter = self._p.comm_bytes_per_iter
+        self.overlapped = self._p.overlapped
         return self
 
     def reset(self):

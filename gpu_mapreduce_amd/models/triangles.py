@@ -209,7 +209,12 @@ def bench_trifind_mr(comm, args):
                           "triangles_check": int(want2), "hbm_budget": budget, "host_budget": host,
                           "spool_files": r2["spool_files"], "spool_host_bytes": r2["spool_host_bytes"],
                           "spool_disk_bytes": r2["spool_disk_bytes"],
-                          "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"]}
+                          # per stage: host <-> device bytes of this rank, and
+                          # the time at the PCIe floor (50 GB/s) they imply
+                          "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"],
+                                      "pcie_bytes": s["h2d_bytes"] + s["d2h_bytes"],
+                                      "pcie_floor_ms": round((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 3),
+                                      "x_floor": round(s["ms"] / max((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 1e-3), 2)}
                                      for s in r2["stages"]]}
         finally:
             shutil.rmtree(root, ignore_errors=True)

@@ -303,7 +303,8 @@ def case_pagerank_ranges(comm):
     pr = PageRank(mr, 1 << 14).build()
     pr.run(15)
     ids, r = pr.ranks()
-    return edges, ids.cpu().numpy(), r.cpu().numpy().copy(), pr.layout, pr.xcd_ranges, pr.nedge
+    return (edges, ids.cpu().numpy(), r.cpu().numpy().copy(), pr.layout, pr.xcd_ranges, pr.nedge, pr.overlapped,
+            pr.comm_bytes_per_iter, pr.c_slice)
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -76,20 +76,27 @@ def test_shuffle_is_deterministic_gpu():
     assert sum(u for _, _, u in out.values()) == 211
 
 
+@pytest.mark.parametrize("overlap", ["1", "0"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_pagerank_replicated_plan_gpu(world):
+def test_pagerank_replicated_plan_gpu(world, overlap, monkeypatch):
     """the multi-GPU PageRank plan (destination-owned edges, all-gathered c,
-    sigma-mixed vertex owners, XCD source ranges on the interleaved order)
-    against the float64 oracle; R-MAT in-edges spread evenly over the ranks"""
+    sigma-mixed vertex owners) against the float64 oracle; R-MAT in-edges
+    spread evenly over the ranks. overlap 1 (the default): edges cut by source
+    rank into pieces with their own XCD ranges, the c slices go round a ring
+    on a side stream while the pieces already in are gathered; 0: XCD ranges
+    on the interleaved order, one all-gather after the tile step"""
     from gpu_mapreduce_amd.models.pagerank import reference_pagerank
+    monkeypatch.setenv("MRH_PR_OVERLAP", overlap)
     out = run_world("case_pagerank_ranges", world, DEV)
     edges = np.concatenate([out[r][0] for r in range(world)])
     ref = reference_pagerank(edges, 1 << 14, iters=15)
     got = np.full(1 << 14, np.nan)
     for r in range(world):
-        _, ids, rk, layout, nranges, _ = out[r]
+        _, ids, rk, layout, nranges, _, overlapped, cbytes, S = out[r]
         assert layout == "replicated"
         assert nranges > 9  # several layers of 8 ranges + the cold range
+        assert overlapped == (overlap == "1")
+        assert cbytes == (world - 1) * S * 4 + 16
         got[ids] = rk
     assert not np.isnan(got).any()  # every vertex owned exactly once
     np.testing.assert_allclose(got, ref, rtol=2e-4, atol=1e-9)

@@ -1,7 +1,15 @@
 """tri_find_mr (the 4-collate MapReduce pipeline) on one R-MAT graph, twice
-(the second run is warm); prints the per-stage times of each run."""
+(the second run is warm); prints the per-stage times of each run.
+
+    python tools/trimr_time.py SCALE [ooc [HBM_MIB [HOST_MIB]]]
+
+ooc: under an HBM budget (default 256 MiB) and a host budget (default 2 GiB),
+spool files in a temporary directory; each stage also shows this rank's
+host <-> device bytes and its time against the 50 GB/s PCIe floor."""
 import os
+import shutil
 import sys
+import tempfile
 
 import torch
 
@@ -12,17 +20,34 @@ from gpu_mapreduce_amd.models.pagerank import GRAPH500  # noqa: E402
 from gpu_mapreduce_amd.models.triangles import tri_find_mr  # noqa: E402
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+ooc = len(sys.argv) > 2 and sys.argv[2] == "ooc"
+hbm = (int(sys.argv[3]) if len(sys.argv) > 3 else 256) << 20
+host = (int(sys.argv[4]) if len(sys.argv) > 4 else 2048) << 20
 comm = g.Comm(device=os.environ.get("DEV", "cuda:0"))
 kv = C.map_rmat((1 << scale) * 16, scale, *GRAPH500, 0.0, 1, 0, comm.device)
 e = kv.kdata.view(torch.int64).view(-1, 2)
 for rep in range(2):
-    r = tri_find_mr(comm, e)
+    root = tempfile.mkdtemp(prefix="mrh_trimr_") if ooc else ""
+    try:
+        r = (tri_find_mr(comm, e, hbm_budget=hbm, host_budget=host, fpath=root, memsize=64) if ooc
+             else tri_find_mr(comm, e))
+    finally:
+        if root:
+            shutil.rmtree(root, ignore_errors=True)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     tot = sum(s["ms"] for s in r["stages"])
     print(f"rep {rep}: {tot:.1f} ms, {r['triangles']} triangles", flush=True)
+    if ooc:
+        print(f"   spool files {r['spool_files']}, host {r['spool_host_bytes'] / 1e9:.2f} GB, "
+              f"disk {r['spool_disk_bytes'] / 1e9:.2f} GB", flush=True)
     if torch.cuda.is_available():
         from gpu_mapreduce_amd.runtime import hbm_pool
         print("   pool:", hbm_pool.stats(0), flush=True)
     for s in r["stages"]:
-        print(f"   {s['op']:<24} {s['ms']:9.2f} ms  in {s['pairs_in']:>12}  out {s['pairs_out']:>12}", flush=True)
+        line = f"   {s['op']:<24} {s['ms']:9.2f} ms  in {s['pairs_in']:>12}  out {s['pairs_out']:>12}"
+        b = s.get("h2d_bytes", 0) + s.get("d2h_bytes", 0)
+        if ooc:
+            floor = b / 50e6
+            line += f"  pcie {b / 1e6:9.1f} MB  floor {floor:7.2f} ms  x{s['ms'] / max(floor, 1e-3):6.1f}"
+        print(line, flush=True)
