@@ -290,8 +290,9 @@ std::pair<at::Tensor, at::Tensor> wedge_range(const at::Tensor& seg, const Wedge
   at::Tensor oc = at::empty({n}, nb.options());
   if (n == 0) return {oe, oc};
   if (seg.is_cuda()) {
+    at::Tensor tg = at::empty({k::wedge_tiles(n) + 1}, nb.options());
     k::wedges(P0<int64_t>(seg), P0<int64_t>(ws.gidx), P0<int64_t>(ws.wscan), ws.ngw, P0<int64_t>(nb),
-              P0<int64_t>(centre), w0, n, P0<int64_t>(oe), P0<int64_t>(oc), cur());
+              P0<int64_t>(centre), w0, n, P0<int64_t>(oe), P0<int64_t>(oc), P0<int64_t>(tg), cur());
     return {oe, oc};
   }
   const int64_t* sg = P0<int64_t>(seg);
@@ -337,8 +338,9 @@ void for_each_wedge_chunk_compact(const at::Tensor& seg, const at::Tensor& nb, c
     if (seg.is_cuda()) {
       at::Tensor key = at::empty({n}, nb.options());
       at::Tensor c = at::empty({n}, nb.options().dtype(at::kInt));
+      at::Tensor tg = at::empty({k::wedge_tiles(n) + 1}, nb.options());
       k::wedges_compact(P0<int64_t>(seg), P0<int64_t>(ws.gidx), P0<int64_t>(ws.wscan), ws.ngw, P0<int64_t>(nb),
-                        P0<int64_t>(centre), w0, n, vb, P0<int64_t>(key), P0<uint32_t>(c), cur());
+                        P0<int64_t>(centre), w0, n, vb, P0<int64_t>(key), P0<uint32_t>(c), P0<int64_t>(tg), cur());
       fn(key, c);
     } else {
       auto r = wedge_range(seg, ws, nb, centre, w0, w0 + n);

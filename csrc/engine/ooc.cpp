@@ -37,6 +37,9 @@
 #include <c10/hip/HIPGuard.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <string>
+#include <utility>
 #include <cstring>
 #include <limits>
 #include <stdexcept>
@@ -55,6 +58,40 @@ namespace mrh {
 namespace {
 
 at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
+
+// MRH_OOC_TRACE=1: host time per phase of an out-of-core op (device
+// synchronised at each mark), summed by name and printed at the end
+struct PhaseClock {
+  bool on = false;
+  double t = 0;
+  std::vector<std::pair<std::string, double>> acc;
+  const char* op;
+  explicit PhaseClock(const char* o) : op(o) {
+    const char* e = std::getenv("MRH_OOC_TRACE");
+    on = e && *e == '1';
+    if (on) {
+      (void)hipDeviceSynchronize();
+      t = Comm::wtime();
+    }
+  }
+  void operator()(const char* what) {
+    if (!on) return;
+    (void)hipDeviceSynchronize();
+    const double now = Comm::wtime();
+    for (auto& [k, v] : acc)
+      if (k == what) {
+        v += now - t;
+        t = now;
+        return;
+      }
+    acc.emplace_back(what, now - t);
+    t = now;
+  }
+  ~PhaseClock() {
+    if (!on) return;
+    for (auto& [k, v] : acc) std::fprintf(stderr, "mrhip ooc %s %-18s %9.2f ms\n", op, k.c_str(), 1e3 * v);
+  }
+};
 
 at::Tensor host(const at::Tensor& t) {
   if (!t.defined()) return t;
@@ -231,6 +268,7 @@ std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev
         if (e) (void)hipEventDestroy(e);
     }
   } ev_guard{&ready};
+  PhaseClock clk("spool");
   KV next;
   if (!ch.empty()) {
     next = load(0);
@@ -245,21 +283,25 @@ std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev
       if (cuda && hipEventRecord(ready[(i + 1) % 2], side->stream()) != hipSuccess)
         throw std::runtime_error("ooc: event");
     }
+    clk("load");
     at::Tensor dest = dest_of(c);
     Buckets B = bucket_local(c, dest, M);
     const HostOff bh = host_off(B.kv);
+    clk("partition");
     int64_t s = 0;
     for (int d = 0; d < M; ++d) {
       const int64_t e = s + B.count[d];
       if (e > s) parts[d].add(kv_slice(B.kv, s, e, bh.kp(), bh.vp()), cuda ? drain->stream() : nullptr);
       s = e;
     }
+    clk("spool add");
     if (st) {
       st->chunks++;
       st->bytes_staged += row_bytes(kvs[ch[i].part], h[ch[i].part], ch[i].a, ch[i].b);
     }
   }
   for (auto& p : parts) p.sync();
+  clk("drain sync");
   if (st)
     for (auto& p : parts) {
       st->files += p.stats().files;
@@ -513,12 +555,14 @@ KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, O
   const KV& kv = kvs.at(0);
   const int M = parts_for(bytes, budget, 4.0);
   if (st) st->parts = M;
+  PhaseClock clk("convert");
   auto parts = spool(kvs, std::max<int64_t>(budget / 4, 1), dev, M, [&](const KV& c) {
     // a hash independent of the shuffle's owner hash (every key on this rank
     // has the same owner hash mod P): bits 20.. of the 64-bit grouping hash
     at::Tensor h = hash64_keys(c);
     return at::remainder(at::bitwise_right_shift(h, 20).bitwise_and_((int64_t(1) << 40) - 1), M).to(at::kInt);
   }, env, st);
+  clk("partition pass");
   std::vector<KMV> out;
   int64_t used = 0;
   // in_file: a hot key whose values one_key_kmv already put in a file
@@ -544,17 +588,29 @@ KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, O
       ooc_convert_big(parts[d].take(), env, dev, st, 1, keep);
       continue;
     }
-    KV p = kv_to(parts[d].gather_host(), dev);
+    KV ph = parts[d].gather_host();
+    clk("gather_host");
+    KV p = kv_to(ph, dev);
+    ph = KV();
     parts[d].clear();
+    clk("to device");
     KMV m = convert(p);
     p = KV();
+    clk("convert");
     keep(std::move(m), false);
+    clk("result to host");
   }
   int64_t total = 0;
   for (auto& m : out) total += m.nbytes();
-  if (env.host < 0 || total <= env.host || out.empty()) return kmv_concat_host(out, kv);
+  if (env.host < 0 || total <= env.host || out.empty()) {
+    KMV r = kmv_concat_host(out, kv);
+    clk("concat results");
+    return r;
+  }
   if (st) st->files++;
-  return kmv_to_file(out, spool_path(env.dir, "kmv", env.instance, env.rank));
+  KMV r = kmv_to_file(out, spool_path(env.dir, "kmv", env.instance, env.rank));
+  clk("results to file");
+  return r;
 }
 
 KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device dev, OocStats* st) {
@@ -698,6 +754,8 @@ void ooc_for_each_kmv_block(const KMV& kmv, const OocEnv& env, at::Device dev,
     return md;
   };
   const int64_t cap = std::max<int64_t>(budget / 4, 1);
+  PhaseClock clk("kmv pieces");
+  clk("host offsets");
   int64_t a = 0;
   while (a < kmv.nkey) {
     if (split && vbytes(a, a + 1) > cap && s[a + 1] - s[a] > 1) {
@@ -726,7 +784,10 @@ void ooc_for_each_kmv_block(const KMV& kmv, const OocEnv& env, at::Device dev,
       continue;
     }
     const int64_t b = grow(a, kmv.nkey, [&](int64_t e) { return vbytes(a, e) <= cap; });
-    fn(piece(a, b, s[a], s[b]), 0);
+    KMV pc = piece(a, b, s[a], s[b]);
+    clk("piece to device");
+    fn(pc, 0);
+    clk("callback");
     if (st) st->chunks++;
     a = b;
   }

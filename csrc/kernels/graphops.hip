@@ -600,64 +600,87 @@ __global__ __launch_bounds__(NT) void k_scatter_t(const T* __restrict__ v, const
 // for group g with neighbour list nb[seg[g]..seg[g+1]) emit every pair
 // (min, max) with value = centre key[g]. Only groups with a wedge (d >= 2)
 // take part: gidx lists them and wscan is the exclusive scan of their C(d,2).
-// One block per tile of WG_TILE consecutive wedge ids: lane 0 finds the
-// tile's first and last group by binary search in global memory, the block
-// stages their scan entries and ids in LDS (at most WG_TILE groups: each has
-// a wedge), and every wedge finds its group by a binary search in LDS — a
-// per-wedge search through global memory was latency-bound (1.2 G wedges of
-// RMAT-20: 4.2 s). The pair (j, k) comes from the triangular index;
-// thread t writes wedges t, t + NT, ... of the tile (coalesced stores).
+// One block per tile of WG_TILE consecutive wedge ids: the tile's first group
+// comes from tg (k_wedge_tile_groups, one pass over the groups per call —
+// a per-block global binary search cost ~40 us of latency per tile), the
+// block stages the scan entries and ids of its groups in LDS (at most
+// WG_TILE + 1: each has a wedge), and every wedge finds its group in an LDS
+// map (each group's index written at its first wedge, then a max-scan). The
+// pair (j, k) comes from the triangular index; thread t writes wedges t,
+// t + NT, ... of the tile (coalesced stores).
 constexpr int WG_IT = 16;
 constexpr int WG_TILE = NT * WG_IT;
 
-__device__ __forceinline__ int64_t wg_upper(const int64_t* __restrict__ a, int64_t n, int64_t x) {
-  int64_t lo = 0, hi = n;  // first index with a[idx] > x
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (a[mid] <= x) lo = mid + 1;
-    else hi = mid;
+// tg[t] = the group of wedge w0 + t * WG_TILE; tg[ntile] = the group of the
+// call's last wedge (grid-stride over the groups)
+__global__ __launch_bounds__(NT) void k_wedge_tile_groups(const int64_t* __restrict__ wscan, int64_t ngw, int64_t w0,
+                                                          int64_t nwedge, int64_t ntile, int64_t* __restrict__ tg) {
+  const int64_t w1 = w0 + nwedge;
+  for (int64_t g = (int64_t)blockIdx.x * NT + threadIdx.x; g < ngw; g += (int64_t)gridDim.x * NT) {
+    const int64_t a = wscan[g] > w0 ? wscan[g] : w0, b = wscan[g + 1] < w1 ? wscan[g + 1] : w1;
+    if (a >= b) continue;
+    for (int64_t t = (a - w0 + WG_TILE - 1) / WG_TILE; w0 + t * WG_TILE < b; ++t) tg[t] = g;
+    if (b == w1) tg[ntile] = g;
   }
-  return lo;
 }
 
 // CMP: the compact layout of large graphs — one word (min << vb | max) per
 // wedge and a 4-byte centre (12 bytes a wedge instead of 24)
 template <int CMP>
 __global__ __launch_bounds__(NT) void k_wedges(const int64_t* __restrict__ seg, const int64_t* __restrict__ gidx,
-                                              const int64_t* __restrict__ wscan, int64_t ngw,
+                                              const int64_t* __restrict__ wscan, const int64_t* __restrict__ tg,
                                               const int64_t* __restrict__ nb, const int64_t* __restrict__ centre,
                                               int64_t w0, int64_t nwedge, int64_t* __restrict__ out_edge,
                                               void* __restrict__ out_centre, int vb) {
-  __shared__ int64_t s_scan[WG_TILE + 1];
-  __shared__ int64_t s_gi[WG_TILE];
-  __shared__ int64_t s_g0;
-  __shared__ int s_n;
+  __shared__ int64_t s_scan[WG_TILE + 2];
+  __shared__ int64_t s_gi[WG_TILE + 2];
+  __shared__ uint16_t s_map[WG_TILE];
+  __shared__ int32_t s_run[NT];
   const int64_t t0 = (int64_t)blockIdx.x * WG_TILE;  // tile offset in this call's output
-  const int64_t tn = nwedge - t0 < WG_TILE ? nwedge - t0 : WG_TILE;
-  if (threadIdx.x == 0) {
-    const int64_t g0 = wg_upper(wscan, ngw, w0 + t0) - 1;
-    const int64_t g1 = wg_upper(wscan, ngw, w0 + t0 + tn - 1) - 1;
-    s_g0 = g0;
-    s_n = (int)(g1 - g0 + 1);
-  }
+  const int tn = (int)(nwedge - t0 < WG_TILE ? nwedge - t0 : WG_TILE);
+  // groups g0 .. g0 + ng - 1: the tile's first wedge's group to the next
+  // tile's (one more than the tile's last group when a group starts it)
+  const int64_t g0 = tg[blockIdx.x];
+  const int ng = (int)(tg[blockIdx.x + 1] - g0 + 1);
+  for (int i = threadIdx.x; i < WG_TILE; i += NT) s_map[i] = 0;
   __syncthreads();
-  const int64_t g0 = s_g0;
-  const int ng = s_n;
   for (int i = threadIdx.x; i <= ng; i += NT) {
-    s_scan[i] = wscan[g0 + i];
-    if (i < ng) s_gi[i] = gidx[g0 + i];
+    const int64_t sc = wscan[g0 + i];
+    s_scan[i] = sc;
+    if (i < ng) {
+      s_gi[i] = gidx[g0 + i];
+      const int64_t pos = sc - (w0 + t0);
+      if (pos > 0 && pos < tn) s_map[pos] = (uint16_t)i;
+    }
   }
   __syncthreads();
+  {  // inclusive max-scan of the map: thread t owns entries [WG_IT t, WG_IT t + WG_IT)
+    const int b0 = threadIdx.x * WG_IT;
+    int m = 0;
+#pragma unroll
+    for (int q = 0; q < WG_IT; ++q) m = max(m, (int)s_map[b0 + q]);
+    s_run[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 1; o < NT; o <<= 1) {
+      const int v = threadIdx.x >= o ? s_run[threadIdx.x - o] : 0;
+      __syncthreads();
+      s_run[threadIdx.x] = max(s_run[threadIdx.x], v);
+      __syncthreads();
+    }
+    int run = threadIdx.x ? s_run[threadIdx.x - 1] : 0;
+#pragma unroll
+    for (int q = 0; q < WG_IT; ++q) {
+      run = max(run, (int)s_map[b0 + q]);
+      s_map[b0 + q] = (uint16_t)run;
+    }
+  }
+  __syncthreads();
+#pragma unroll 4
   for (int it = 0; it < WG_IT; ++it) {
-    const int64_t o = (int64_t)it * NT + threadIdx.x;
+    const int o = it * NT + threadIdx.x;
     if (o >= tn) break;
     const int64_t w = w0 + t0 + o;
-    int lo = 0, hi = ng;  // last group with s_scan <= w
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (s_scan[mid] <= w) lo = mid;
-      else hi = mid;
-    }
+    const int lo = s_map[o];
     const int64_t g = s_gi[lo];
     const int64_t t = w - s_scan[lo];
     const int64_t base = seg[g];
@@ -779,21 +802,33 @@ void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_
   }
 }
 
+int64_t wedge_tiles(int64_t nwedge) { return (nwedge + WG_TILE - 1) / WG_TILE; }
+
+static void wedge_tile_groups(const int64_t* wscan, int64_t ngw, int64_t w0, int64_t nwedge, int64_t* tg,
+                              hipStream_t s) {
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ngw + NT - 1) / NT, 1 << 16));
+  hipLaunchKernelGGL(k_wedge_tile_groups, dim3(g), dim3(NT), 0, s, wscan, ngw, w0, nwedge, wedge_tiles(nwedge), tg);
+  MRH_CHECK_LAUNCH();
+}
+
 void wedges(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
-            const int64_t* centre, int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s) {
+            const int64_t* centre, int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, int64_t* tg,
+            hipStream_t s) {
   if (nwedge <= 0 || ngw <= 0) return;
-  hipLaunchKernelGGL(k_wedges<0>, dim3((unsigned)((nwedge + WG_TILE - 1) / WG_TILE)), dim3(NT), 0, s, seg, gidx,
-                     wscan, ngw, nb, centre, w0, nwedge, out_edge, (void*)out_centre, 0);
+  wedge_tile_groups(wscan, ngw, w0, nwedge, tg, s);
+  hipLaunchKernelGGL(k_wedges<0>, dim3((unsigned)wedge_tiles(nwedge)), dim3(NT), 0, s, seg, gidx, wscan, tg, nb,
+                     centre, w0, nwedge, out_edge, (void*)out_centre, 0);
   MRH_CHECK_LAUNCH();
 }
 
 void wedges_compact(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
                     const int64_t* centre, int64_t w0, int64_t nwedge, int vb, int64_t* out_key, uint32_t* out_centre,
-                    hipStream_t s) {
+                    int64_t* tg, hipStream_t s) {
   if (nwedge <= 0 || ngw <= 0) return;
   check_arg(vb > 0 && vb <= 32, "wedges_compact: vertex bits in (0, 32]");
-  hipLaunchKernelGGL(k_wedges<1>, dim3((unsigned)((nwedge + WG_TILE - 1) / WG_TILE)), dim3(NT), 0, s, seg, gidx,
-                     wscan, ngw, nb, centre, w0, nwedge, out_key, (void*)out_centre, vb);
+  wedge_tile_groups(wscan, ngw, w0, nwedge, tg, s);
+  hipLaunchKernelGGL(k_wedges<1>, dim3((unsigned)wedge_tiles(nwedge)), dim3(NT), 0, s, seg, gidx, wscan, tg, nb,
+                     centre, w0, nwedge, out_key, (void*)out_centre, vb);
   MRH_CHECK_LAUNCH();
 }
 

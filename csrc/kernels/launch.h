@@ -300,13 +300,16 @@ void ws_gather_reduce(int dtype, const uint32_t* H, const int64_t* wbase, int64_
 // tri_find wedges: all pairs of each neighbour group with d >= 2 (gidx:
 // those groups, wscan: the exclusive scan of their C(d,2), ngw + 1 entries);
 // wedge ids [w0, w0 + nwedge), output slot i holds wedge w0 + i, so a huge
-// group set is generated in bounded chunks
+// group set is generated in bounded chunks; tg: scratch of
+// wedge_tiles(nwedge) + 1 entries (each tile's first group)
+int64_t wedge_tiles(int64_t nwedge);
 void wedges(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
-            const int64_t* centre, int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, hipStream_t s);
+            const int64_t* centre, int64_t w0, int64_t nwedge, int64_t* out_edge, int64_t* out_centre, int64_t* tg,
+            hipStream_t s);
 // the same wedges in the compact layout: out_key = min << vb | max, out_centre u32
 void wedges_compact(const int64_t* seg, const int64_t* gidx, const int64_t* wscan, int64_t ngw, const int64_t* nb,
                     const int64_t* centre, int64_t w0, int64_t nwedge, int vb, int64_t* out_key, uint32_t* out_centre,
-                    hipStream_t s);
+                    int64_t* tg, hipStream_t s);
 
 // ---------------------------------------------------------------- pbpr.hip
 // propagation-blocked PageRank (graphplan.cpp PageRankPlan, one GPU)

@@ -162,6 +162,9 @@ def bench_pagerank(comm, args):
         "setup_s": setup,
         "l1_delta_last": pr.delta(),
         "hip_graph_iterations": pr.graph_iterations,
+        "layout": pr.layout,
+        "comm_bytes_per_iter": comm.allreduce(pr.comm_bytes_per_iter, "max"),
+        "comm_overlapped": bool(pr.overlapped),
         "config": {"model": "PageRank", "global_batch": nedge, "seq_len": iters,
                    "parallelism": f"dp{comm.size}", "scale": scale, "edgefactor": ef, "alpha": 0.85},
         "scaling": "strong",
