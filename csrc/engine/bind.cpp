@@ -313,12 +313,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
             else r.kv = o.cast<KV>();
           })
       .def_property_readonly("kv_parts", [](MR& r) { return (int64_t)r.kv_tail().size() + (r.kv ? 1 : 0); })
+      .def_property_readonly("kmv_parts", [](MR& r) { return (int64_t)r.kmv_part_count(); })
       .def_property(
           "kmv", [](MR& r) -> py::object {
             r.ensure_resident();
+            r.flatten_kmv();
             return r.kmv ? py::cast(*r.kmv) : py::none();
           },
           [](MR& r, py::object o) {
+            r.flatten_kmv();
             if (o.is_none()) r.kmv.reset();
             else r.kmv = o.cast<KMV>();
           })

@@ -196,6 +196,111 @@ KV concat(const std::vector<KV>& parts_in, at::Device dev, bool pin) {
   return o;
 }
 
+KMV kmv_concat(const std::vector<KMV>& parts, at::Device dev, bool pin) {
+  std::vector<const KMV*> ps;
+  for (const KMV& m : parts)
+    if (m.nkey > 0) ps.push_back(&m);
+  if (ps.size() == 1) {
+    KMV o = *ps[0];
+    if (o.seg.device() != dev || (pin && dev.is_cpu() && o.seg.is_cpu() && !o.vdata.is_pinned())) {
+      auto mv = [&](const at::Tensor& t) {
+        if (!t.defined()) return t;
+        note_xfer(t, dev);
+        if (pin && dev.is_cpu()) return t.to(at::TensorOptions().device(at::kCPU).pinned_memory(true), false, true);
+        return t.to(dev);
+      };
+      o.keys = concat({o.keys}, dev, pin);
+      o.vdata = mv(o.vdata);
+      o.voff = mv(o.voff);
+      o.seg = mv(o.seg);
+    }
+    return o;
+  }
+  KMV out;
+  std::vector<KV> keys, vals;
+  std::vector<at::Tensor> segs;
+  int64_t base = 0;
+  for (const KMV* m : ps) {
+    keys.push_back(m->keys);
+    KV v;
+    v.n = m->nval;
+    v.kw = 0;
+    v.vw = m->vw;
+    v.kdata = at::empty({0}, opt(m->vdata.device(), at::kByte));
+    v.vdata = m->vdata;
+    v.voff = m->voff;
+    vals.push_back(v);
+    at::Tensor sg = m->seg.narrow(0, 0, m->nkey);
+    note_xfer(sg, dev);
+    segs.push_back(base ? sg.to(dev) + base : sg.to(dev));
+    base += m->nval;
+    out.nkey += m->nkey;
+  }
+  segs.push_back(at::full({1}, base, opt(dev, at::kLong)));
+  const KV& like = parts.empty() ? KV() : parts[0].keys;
+  out.keys = ps.empty() ? empty_kv(dev, like.kw, 0) : concat(keys, dev, pin);
+  out.keys.vw = 0;
+  KV vcat = ps.empty() ? empty_kv(dev, 0, parts.empty() ? 0 : parts[0].vw) : concat(vals, dev, pin);
+  out.vdata = vcat.vdata;
+  out.voff = vcat.voff;
+  out.vw = vcat.vw;
+  out.nval = base;
+  at::Tensor sg = at::cat(segs);
+  out.seg = pin && dev.is_cpu() ? sg.pin_memory() : sg;
+  return out;
+}
+
+KV concat_upload(const std::vector<KV>& parts_in, at::Device dev) {
+  std::vector<KV> parts;
+  for (const KV& p : parts_in)
+    if (p.n > 0) parts.push_back(p);
+  if (parts.empty() || !dev.is_cuda()) return concat(parts_in, dev);
+  bool kf = true, vf = true;
+  for (const KV& p : parts) {
+    kf = kf && p.kfixed() && p.kw == parts[0].kw;
+    vf = vf && p.vfixed() && p.vw == parts[0].vw;
+  }
+  // one column: data bytes back to back, offsets rebased on the device
+  auto column = [&](bool fixed, auto data_of, auto off_of, at::Tensor* data_out, at::Tensor* off_out) {
+    int64_t bytes = 0, rows = 0;
+    for (const KV& p : parts) {
+      bytes += data_of(p).numel();
+      rows += p.n;
+    }
+    *data_out = at::empty({bytes}, opt(dev, at::kByte));
+    if (!fixed) *off_out = at::empty({rows + 1}, opt(dev, at::kLong));
+    int64_t b = 0, r = 0;
+    for (const KV& p : parts) {
+      const at::Tensor& d = data_of(p);
+      note_xfer(d, dev);
+      if (d.numel()) data_out->narrow(0, b, d.numel()).copy_(d, /*non_blocking=*/true);
+      if (!fixed) {
+        at::Tensor o = off_of(p).narrow(0, 0, p.n);
+        note_xfer(o, dev);
+        at::Tensor dst = off_out->narrow(0, r, p.n);
+        dst.copy_(o, /*non_blocking=*/true);
+        if (b) dst.add_(b);
+      }
+      b += d.numel();
+      r += p.n;
+    }
+    if (!fixed) off_out->narrow(0, rows, 1).fill_(b);
+  };
+  KV o;
+  o.n = 0;
+  for (const KV& p : parts) o.n += p.n;
+  o.kw = kf ? parts[0].kw : -1;
+  o.vw = vf ? parts[0].vw : -1;
+  std::vector<KV> ps;
+  for (const KV& p : parts) ps.push_back(kf ? (vf ? p : to_var_values(p)) : (vf ? to_var_keys(p) : to_var_values(to_var_keys(p))));
+  parts.swap(ps);
+  column(kf, [](const KV& p) -> const at::Tensor& { return p.kdata; }, [](const KV& p) -> const at::Tensor& { return p.koff; },
+         &o.kdata, &o.koff);
+  column(vf, [](const KV& p) -> const at::Tensor& { return p.vdata; }, [](const KV& p) -> const at::Tensor& { return p.voff; },
+         &o.vdata, &o.voff);
+  return o;
+}
+
 // ====================================================================== primitives
 
 // int32 lengths or int64 values -> int64 exclusive offsets (n+1)

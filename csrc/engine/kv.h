@@ -59,6 +59,11 @@ KV make_kv(at::Tensor kdata, c10::optional<at::Tensor> koff, at::Tensor vdata,
 KV kv_to(const KV& kv, at::Device dev);
 // pin: a CPU result goes straight into pinned host memory
 KV concat(const std::vector<KV>& parts, at::Device dev, bool pin = false);
+// KMVs one after the other (keys, values, rebased segments) on dev
+KMV kmv_concat(const std::vector<KMV>& parts, at::Device dev, bool pin = false);
+// the parts copied host -> device straight into one device KV (no host
+// concatenation; fixed widths and offsets alike)
+KV concat_upload(const std::vector<KV>& parts, at::Device dev);
 KV to_var_keys(const KV& kv);
 KV to_var_values(const KV& kv);
 // offsets of a fixed-width column: [0, w, 2w, ...]

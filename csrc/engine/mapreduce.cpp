@@ -89,9 +89,9 @@ struct OpTrace {
       const double t1 = Comm::wtime();
       int64_t b = 0;
       if (mr_->kv) b += mr_->kv->nbytes();
-      if (mr_->kmv) b += mr_->kmv->nbytes();
+      for (const KMV& m : mr_->kmv_parts()) b += m.nbytes();
       guard::trace_op(mr_->my_proc(), name_, mr_->instance(), g_op_depth, t0_, (t1 - t0_) * 1e3,
-                      mr_->kv ? mr_->kv->n : 0, mr_->kmv ? mr_->kmv->nkey : 0, b, MapReduce::cssize.load() - s0_,
+                      mr_->kv ? mr_->kv->n : 0, mr_->kmv_keys(), b, MapReduce::cssize.load() - s0_,
                       MapReduce::crsize.load() - r0_);
     }
     // freepage (reference: pages freed after every op, src/mapreduce.cpp:
@@ -322,9 +322,10 @@ MapReduce::~MapReduce() {
 
 // every op's entry: fault injection point, and data spilled to host (spill()
 // or spill-on-OOM) comes back to HBM before the op touches it
-void MapReduce::enter(const char* op, bool ooc_ok, bool parts_ok) {
+void MapReduce::enter(const char* op, bool ooc_ok, bool parts_ok, bool kmv_parts_ok) {
   guard::fault_point(op, comm_->rank());
   if (!parts_ok) flatten();
+  if (!kmv_parts_ok) flatten_kmv();
   if (guard::alloc_guard_active()) {  // an overrun found at the end of an earlier op fails the next one
     static size_t raised = 0;
     const auto reps = guard::guard_reports();
@@ -406,6 +407,41 @@ KV MapReduce::concat_parts(const std::vector<KV>& parts) {
   return kv_to_file(parts, spool_path(set.fpath, "kv", instance_me_, comm_->rank()));
 }
 
+std::vector<KMV> MapReduce::kmv_parts() const {
+  std::vector<KMV> p;
+  if (kmv) p.push_back(*kmv);
+  for (const KMV& t : kmv_tail_) p.push_back(t);
+  return p;
+}
+
+int64_t MapReduce::kmv_keys() const {
+  int64_t n = kmv ? kmv->nkey : 0;
+  for (const KMV& t : kmv_tail_) n += t.nkey;
+  return n;
+}
+
+void MapReduce::flatten_kmv() {
+  if (kmv_tail_.empty()) return;
+  std::vector<KMV> parts = kmv_parts();
+  kmv_tail_.clear();
+  const at::Device d = parts[0].seg.device();
+  kmv = kmv_concat(parts, d, d.is_cpu() && device().is_cuda());
+}
+
+void MapReduce::set_kmv_parts(std::vector<KMV> parts) {
+  kmv_tail_.clear();
+  kmv.reset();
+  for (size_t i = 0; i < parts.size(); ++i) {
+    if (i == 0) kmv = parts[0];
+    else if (parts[i].nkey) kmv_tail_.push_back(parts[i]);
+  }
+}
+
+void MapReduce::drop_kmv() {
+  kmv.reset();
+  kmv_tail_.clear();
+}
+
 std::vector<KV> MapReduce::kv_parts() const {
   std::vector<KV> p;
   if (kv) p.push_back(*kv);
@@ -470,6 +506,7 @@ int64_t MapReduce::data_bytes() const {
   if (kv) b += kv->nbytes();
   for (const KV& t : kv_tail_) b += t.nbytes();
   if (kmv) b += kmv->nbytes();
+  for (const KMV& t : kmv_tail_) b += t.nbytes();
   return b;
 }
 
@@ -487,6 +524,7 @@ void MapReduce::note_ooc(const char* op, const OocStats& st) {
 std::unique_ptr<MapReduce> MapReduce::copy() const {
   const_cast<MapReduce*>(this)->ensure_resident();  // a disk-resident MR copies its data, not nothing
   const_cast<MapReduce*>(this)->flatten();
+  const_cast<MapReduce*>(this)->flatten_kmv();
   auto mr = std::make_unique<MapReduce>(comm_);
   mr->set = set;
   if (kv) mr->kv = clone_kv(*kv);
@@ -537,7 +575,7 @@ void MapReduce::histo(double v, const char* heading) const {
 void MapReduce::stats(const char* heading, int which) {
   if (guard::check_enabled()) {
     if (kv) guard::check_kv(*kv, heading);
-    if (kmv) guard::check_kmv(*kmv, heading);
+    for (const KMV& m : kmv_parts()) guard::check_kmv(m, heading);
   }
   const int64_t b = data_bytes();
   msize = b;
@@ -596,7 +634,7 @@ void MapReduce::open(int addflag) {  // :1648-1664
   open_ = std::make_unique<KeyValue>(device());
   bound(*open_);
   open_add_ = addflag;
-  kmv.reset();
+  drop_kmv();
 }
 
 KeyValue& MapReduce::kv_open() {
@@ -655,7 +693,7 @@ uint64_t MapReduce::finish_map(KeyValue& kvb, int addflag, const char* heading) 
     set_kv_parts(std::move(n));
     grouped_ = g;
   }
-  kmv.reset();
+  drop_kmv();
   stats(heading, 0);
   return count(kv_rows());
 }
@@ -816,6 +854,7 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
   enter(__func__);
   src.ensure_resident();
   src.flatten();
+  src.flatten_kmv();
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   HostCol k = host_col(s.kdata, s.koff, s.kw), v = host_col(s.vdata, s.voff, s.vw);
@@ -829,7 +868,7 @@ uint64_t MapReduce::map_mr(MapReduce& src, const MapKVFn& fn, int addflag) {  //
     note_spool(kvb);
     kv = s;
     append_part(n);
-    kmv.reset();
+    drop_kmv();
     stats("Map", 0);
     return count(kv_rows());
   }
@@ -843,6 +882,7 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
   enter(__func__);
   src.ensure_resident();
   src.flatten();
+  src.flatten_kmv();
   if (!src.kv) fail("MapReduce passed to map() does not have KeyValue pairs");
   KV s = *src.kv;
   KeyValue kvb(device());
@@ -853,7 +893,7 @@ uint64_t MapReduce::map_mr_batch(MapReduce& src, const MapBatchFn& fn, int addfl
     note_spool(kvb);
     kv = s;
     append_part(n);
-    kmv.reset();
+    drop_kmv();
     stats("Map", 0);
     return count(kv_rows());
   }
@@ -986,7 +1026,7 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
     OocStats os;
     // hash-partitioned spools (src/keymultivalue.cpp:645-789), fed from every
     // part where it lies
-    kmv = ooc_convert(kv_parts(), ooc_env(), device(), &os);
+    set_kmv_parts(ooc_convert_parts(kv_parts(), ooc_env(), device(), &os));
     note_ooc("Convert", os);
   } else if (grouped_ && grouped_->describes(*kv) && !prehash.defined()) {
     // grouped while the map produced it: only the two short sorts are left
@@ -1020,6 +1060,7 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
       kmv = std::move(m);
     } else {
       flatten();
+      flatten_kmv();
       kmv = oom_retry(this, device(), my_proc(), "convert", [&] { return mrh::convert(*kv, &last_convert, 64); });
     }
   } else {
@@ -1030,7 +1071,7 @@ uint64_t MapReduce::convert_prehashed(const at::Tensor& prehash) {  // :861-886
   kv.reset();
   kv_tail_.clear();
   stats("Convert", 1);
-  return count(kmv->nkey);
+  return count(kmv_keys());
 }
 
 uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
@@ -1076,7 +1117,7 @@ uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
     kv.reset();
     grouped_.reset();
     stats("Collate", 1);
-    return count(kmv->nkey);
+    return count(kmv_keys());
   }
   const int v = set.verbosity, t = set.timer;
   set.verbosity = set.timer = 0;
@@ -1085,7 +1126,7 @@ uint64_t MapReduce::collate(const HashFn& hash) {  // :710-738
   set.verbosity = v;
   set.timer = t;
   stats("Collate", 1);
-  return count(kmv->nkey);
+  return count(kmv_keys());
 }
 
 // compress's local group-by: out of core (hash-partitioned spools) past the budget
@@ -1108,7 +1149,7 @@ uint64_t MapReduce::clone() {  // :631-652
   kmv = oom_retry(this, device(), my_proc(), "clone", [&] { return mrh::clone(*kv); });
   kv.reset();
   stats("Clone", 1);
-  return count(kmv->nkey);
+  return count(kmv_keys());
 }
 
 uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
@@ -1119,7 +1160,7 @@ uint64_t MapReduce::collapse(const char* key, int kb) {  // :681-702
   kmv = mrh::collapse(*kv, std::string(key, (size_t)kb));
   kv.reset();
   stats("Collapse", 1);
-  return count(kmv->nkey);
+  return count(kmv_keys());
 }
 
 uint64_t MapReduce::scrunch(int nprocs, const char* key, int kb) {  // :2075-2095
@@ -1133,7 +1174,7 @@ uint64_t MapReduce::scrunch(int nprocs, const char* key, int kb) {  // :2075-209
   set.verbosity = v;
   set.timer = t;
   stats("Scrunch", 1);
-  return count(kmv->nkey);
+  return count(kmv_keys());
 }
 
 // ====================================================================== reduce family
@@ -1214,14 +1255,15 @@ int MapReduce::multivalue_block(int iblock, char** mv, int** valuebytes) {
 uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__, true);  // host callbacks read host-resident data in place
+  enter(__func__, true, false, true);  // host callbacks read host-resident data (every KMV part) in place
   need_kmv("reduce");
   KeyValue kvb(device());
   bound(kvb);
-  run_host_kmv(*kmv, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
+  for (const KMV& m : kmv_parts())
+    run_host_kmv(m, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
   set_kv_parts(kvb.finish_parts());
   note_spool(kvb);
-  kmv.reset();
+  drop_kmv();
   stats("Reduce", 0);
   return count(kv_rows());
 }
@@ -1229,40 +1271,44 @@ uint64_t MapReduce::reduce(const ReduceFn& fn) {  // :1769-1867
 uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dtype) {
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__, true);
+  enter(__func__, true, false, kmv_part_count() > 1);
   need_kmv("reduce");
-  if (needs_ooc(kmv->nbytes(), budget(), 2.0)) {  // values stream through HBM in budget-sized key ranges
+  if (kmv_part_count() > 1 || needs_ooc(kmv->nbytes(), budget(), 2.0)) {
+    // values stream through HBM in budget-sized key ranges, part by part
     OocStats os;
-    kv = ooc_reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype, ooc_env(), device(), &os);
+    std::vector<KV> outs;
+    for (const KMV& m : kmv_parts()) outs.push_back(ooc_reduce_builtin(m, op, dtype.empty() ? "int32" : dtype, ooc_env(), device(), &os));
+    set_kv_parts(std::move(outs));
     note_ooc("Reduce", os);
   } else {
     kv = oom_retry(this, device(), my_proc(), "reduce_builtin",
                    [&] { return mrh::reduce_builtin(*kmv, op, dtype.empty() ? "int32" : dtype); });
   }
-  kmv.reset();
+  drop_kmv();
   stats("Reduce", 0);
-  return count(kv->n);
+  return count(kv_rows());
 }
 
 uint64_t MapReduce::reduce_batch(const ReduceBatchFn& fn) {
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__, true);
+  enter(__func__, true, false, kmv_part_count() > 1);
   need_kmv("reduce");
   KeyValue kvb(device());
   bound(kvb);
-  if (needs_ooc(kmv->nbytes(), budget(), 2.0)) {
-    // key ranges whose values fit the budget go to HBM one at a time; the
-    // batch callback sees each as a KMV of its own (in key order)
+  if (kmv_part_count() > 1 || needs_ooc(kmv->nbytes(), budget(), 2.0)) {
+    // key ranges whose values fit the budget go to HBM one at a time, part
+    // by part; the batch callback sees each as a KMV of its own (in key order)
     OocStats os;
-    ooc_for_each_kmv_piece(*kmv, ooc_env(), device(), [&](const KMV& piece) { fn(piece, kvb); }, &os);
+    for (const KMV& m : kmv_parts())
+      ooc_for_each_kmv_piece(m, ooc_env(), device(), [&](const KMV& piece) { fn(piece, kvb); }, &os);
     note_ooc("Reduce", os);
   } else {
     fn(*kmv, kvb);
   }
   set_kv_parts(kvb.finish_parts());
   note_spool(kvb);
-  kmv.reset();
+  drop_kmv();
   stats("Reduce", 0);
   return count(kv_rows());
 }
@@ -1315,11 +1361,11 @@ uint64_t MapReduce::scan_kv(const ScanKVFn& fn) {  // :1933-1976
 uint64_t MapReduce::scan_kmv(const ScanKMVFn& fn) {  // :1984-2065
   start();
   OpTrace tr_(__func__, this);
-  enter(__func__, true);  // host callbacks read host-resident data in place
+  enter(__func__, true, false, true);  // host callbacks read host-resident data (every KMV part) in place
   need_kmv("scan");
-  run_host_kmv(*kmv, fn);
+  for (const KMV& m : kmv_parts()) run_host_kmv(m, fn);
   stats("Scan", 1);
-  return count(kmv->nkey);
+  return count(kmv_keys());
 }
 
 // ====================================================================== sorting
@@ -1392,7 +1438,7 @@ uint64_t MapReduce::sort_multivalues(int flag) {  // :2210-2352
   need_kmv("sort_multivalues");
   kmv = mrh::sort_multivalues(*kmv, flag);
   stats("Sort_multivalues", 1);
-  return count(kmv->nkey);
+  return count(kmv_keys());
 }
 uint64_t MapReduce::sort_multivalues(const CompareFn& fn) {
   start();
@@ -1424,6 +1470,7 @@ void MapReduce::print(int proc, int nstride, int kflag, int vflag) { print(nullp
 void MapReduce::print(const char* file, int fflag, int proc, int nstride, int kflag, int vflag) {
   ensure_resident();
   flatten();
+  flatten_kmv();
   if (!kv && !kmv) fail("Cannot print without KeyValue or KeyMultiValue");
   if (kflag < 0 || kflag > 7 || vflag < 0 || vflag > 7 || nstride < 1) fail("Invalid print args");
   const int me = comm_->rank();
@@ -1490,6 +1537,7 @@ void MapReduce::print(const char* file, int fflag, int proc, int nstride, int kf
 uint64_t MapReduce::kv_stats(int level) {  // :2937-2966
   ensure_resident();
   flatten();
+  flatten_kmv();
   need_kv("print stats");
   std::vector<int64_t> t =
       comm_->allreduce({kv->n, kv->key_bytes(), kv->value_bytes(), kv->nbytes(), pages(kv->nbytes())}, Comm::SUM);
@@ -1556,12 +1604,14 @@ void MapReduce::cummulative_stats(int level, int reset) {  // :3007-3066
 
 void MapReduce::spill() {
   flatten();
+  flatten_kmv();
   const bool pin = device().is_cuda();
   if (kv) kv = kv_host(*kv, pin);
   if (kmv) kmv = kmv_to(*kmv, at::Device(at::kCPU), pin);
 }
 
 void MapReduce::unspill() {
+  flatten_kmv();
   if (kv) kv = kv_to(*kv, device());
   if (kmv) kmv = kmv_to(*kmv, device(), false);
 }
@@ -1640,6 +1690,7 @@ void MapReduce::save(const std::string& path) const {
   if (disk_path_.empty() && !kv && !kmv) fail("Cannot save without KeyValue or KeyMultiValue");
   const_cast<MapReduce*>(this)->ensure_resident();
   const_cast<MapReduce*>(this)->flatten();
+  const_cast<MapReduce*>(this)->flatten_kmv();
   write_file(rank_path(path, *comm_));
 }
 
@@ -1699,7 +1750,7 @@ int64_t MapReduce::read_file(const std::string& p) {
     guard::check_kv(k, "load");  // offsets/arena sizes consistent before any kernel reads them
     kv = k;
     kv_tail_.clear();
-    kmv.reset();
+    drop_kmv();
     n = kv->n;
   } else if (kind == 1) {
     KMV m;
@@ -1731,6 +1782,7 @@ int64_t MapReduce::read_file(const std::string& p) {
 // and comes back on the MR's next op (ensure_resident, called from enter()).
 void MapReduce::spill_disk() {
   flatten();
+  flatten_kmv();
   if (!kv && !kmv) return;
   char name[96];
   std::snprintf(name, sizeof(name), "mrmpi.%s.%d.%d.%d", kv ? "kv" : "kmv", instance_me_, ++disk_counter_,
@@ -1738,7 +1790,7 @@ void MapReduce::spill_disk() {
   const std::string p = (std::filesystem::path(set.fpath) / name).string();
   write_file(p);
   kv.reset();
-  kmv.reset();
+  drop_kmv();
   disk_path_ = p;
 }
 
@@ -1756,7 +1808,7 @@ void MapReduce::drop_for_map(int addflag, const MapReduce* src) {
   drop_disk();
   kv.reset();
   kv_tail_.clear();
-  kmv.reset();
+  drop_kmv();
   grouped_.reset();
 }
 

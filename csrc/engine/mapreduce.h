@@ -102,12 +102,21 @@ class MapReduce {
   // read the parts in place; every other op, and code reading `kv`
   // directly, flattens first (flatten(): one concatenation).
   std::optional<KV> kv;
+  // The KMV likewise is `kmv` followed by parts: an out-of-core convert
+  // leaves one host-resident KMV per partition (pinned, or a file) instead of
+  // concatenating them on the host; the reduce family and scan walk the
+  // parts, every other op (and code reading `kmv`) flattens first.
   std::optional<KMV> kmv;
   ConvertStats last_convert;
   void flatten();
+  void flatten_kmv();
   // pairs of the KV including the appended parts
   int64_t kv_rows() const;
   const std::vector<KV>& kv_tail() const { return kv_tail_; }
+  // keys of the KMV including its parts; its parts in order
+  int64_t kmv_keys() const;
+  std::vector<KMV> kmv_parts() const;
+  size_t kmv_part_count() const { return kmv ? 1 + kmv_tail_.size() : 0; }
 
   // ---------------------------------------------------------------- object ops
   std::unique_ptr<MapReduce> copy() const;
@@ -208,8 +217,11 @@ class MapReduce {
 
  private:
   void start();
-  // parts_ok: the op reads the appended parts itself (else they are flattened)
-  void enter(const char* op, bool ooc_ok = false, bool parts_ok = false);
+  // parts_ok: the op reads the appended KV parts itself (else they are
+  // flattened); kmv_parts_ok: the same for the KMV's parts
+  void enter(const char* op, bool ooc_ok = false, bool parts_ok = false, bool kmv_parts_ok = false);
+  void set_kmv_parts(std::vector<KMV> parts);
+  void drop_kmv();
   // append `b` as a part: device parts past the HBM budget go through a
   // bounded builder (pinned host / spool files), nothing already held moves
   void append_part(const KV& b);
@@ -262,6 +274,7 @@ class MapReduce {
 
   CommPtr comm_;
   std::vector<KV> kv_tail_;
+  std::vector<KMV> kmv_tail_;
   std::string disk_path_;
   int disk_counter_ = 0;
   // group-by index of the KV built by the last map / close with grouping

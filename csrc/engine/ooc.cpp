@@ -529,8 +529,7 @@ void ooc_convert_big(std::vector<KV> pieces, const OocEnv& env, at::Device dev, 
   for (int d = 0; d < M2; ++d) {
     if (parts[d].empty()) continue;
     if (parts[d].bytes() * 4 <= budget) {
-      KV p = kv_to(parts[d].gather_host(), dev);
-      parts[d].clear();
+      KV p = concat_upload(parts[d].take(), dev);
       keep(convert(p), false);
     } else {
       ooc_convert_big(parts[d].take(), env, dev, st, level + 1, keep);
@@ -548,7 +547,7 @@ void ooc_convert_big(std::vector<KV> pieces, const OocEnv& env, at::Device dev, 
 
 }  // namespace
 
-KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, OocStats* st) {
+std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, OocStats* st) {
   const int64_t budget = env.hbm;
   int64_t bytes = 0;
   for (const KV& k : kvs) bytes += k.nbytes();
@@ -588,11 +587,8 @@ KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, O
       ooc_convert_big(parts[d].take(), env, dev, st, 1, keep);
       continue;
     }
-    KV ph = parts[d].gather_host();
-    clk("gather_host");
-    KV p = kv_to(ph, dev);
-    ph = KV();
-    parts[d].clear();
+    // the partition's pieces straight into one device KV (no host concat)
+    KV p = concat_upload(parts[d].take(), dev);
     clk("to device");
     KMV m = convert(p);
     p = KV();
@@ -600,17 +596,18 @@ KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, O
     keep(std::move(m), false);
     clk("result to host");
   }
+  if (out.empty()) out.push_back(kmv_concat_host(out, kv));  // an empty KMV of the KV's widths
+  return out;
+}
+
+KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, OocStats* st) {
+  std::vector<KMV> out = ooc_convert_parts(kvs, env, dev, st);
+  if (out.size() == 1) return out[0];
   int64_t total = 0;
   for (auto& m : out) total += m.nbytes();
-  if (env.host < 0 || total <= env.host || out.empty()) {
-    KMV r = kmv_concat_host(out, kv);
-    clk("concat results");
-    return r;
-  }
+  if (env.host < 0 || total <= env.host) return kmv_concat_host(out, kvs.at(0));
   if (st) st->files++;
-  KMV r = kmv_to_file(out, spool_path(env.dir, "kmv", env.instance, env.rank));
-  clk("results to file");
-  return r;
+  return kmv_to_file(out, spool_path(env.dir, "kmv", env.instance, env.rank));
 }
 
 KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device dev, OocStats* st) {

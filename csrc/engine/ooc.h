@@ -35,6 +35,11 @@ bool needs_ooc(int64_t bytes, int64_t budget, double factor);
 // kvs: the KV as parts in order (a KV with appended parts, mapreduce.h); each
 // is read where it lies
 KMV ooc_convert(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev, OocStats* st = nullptr);
+// the same result as one host-resident KMV per partition (pinned while the
+// host budget lasts, else a file each), not concatenated: the MapReduce
+// object keeps them as its KMV's parts
+std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env, at::Device dev,
+                                   OocStats* st = nullptr);
 KV ooc_sort(const KV& kv, int flag, bool by_value, const OocEnv& env, at::Device dev, OocStats* st = nullptr);
 KV ooc_reduce_builtin(const KMV& kmv, const std::string& op, const std::string& dtype, const OocEnv& env,
                       at::Device dev, OocStats* st = nullptr);

@@ -95,7 +95,7 @@ class MapReduce(metaclass=_Counters):
 
     # ------------------------------------------------------------------ settings / data
     def __getattr__(self, name):
-        if name in _SETTINGS or name in ("mapfilecount", "kv", "kmv", "last_convert", "spool_stats", "kv_parts"):
+        if name in _SETTINGS or name in ("mapfilecount", "kv", "kmv", "last_convert", "spool_stats", "kv_parts", "kmv_parts"):
             return getattr(self.__dict__["_m"], name)
         raise AttributeError(name)
 

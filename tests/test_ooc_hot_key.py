@@ -85,6 +85,7 @@ def _run(dev, tmp_path):
     assert mr.kv.nbytes() > 8 * BUDGET
     assert mr.collate() == len(want)
     assert mr.spool_stats["ooc_hot_keys"] >= 1      # grouped on the host, never in HBM whole
+    assert mr.kmv_parts > 1                          # one host-resident KMV per partition, not concatenated
     blocks = {}
 
     def red(k, mv, kv):
