@@ -574,7 +574,7 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
       out.push_back(on_host ? m : kmv_host(m));
       if (!in_file) used += b;
     } else {  // the disk tier: one file per partition result
-      out.push_back(kmv_to_file({kmv_host(m)}, spool_path(env.dir, "kmv", env.instance, env.rank)));
+      out.push_back(kmv_to_file({m}, spool_path(env.dir, "kmv", env.instance, env.rank)));
       if (st) {
         st->files++;
         st->disk_bytes += b;

@@ -34,7 +34,13 @@ struct Mapping {
   void* p = nullptr;
   size_t len = 0;
   std::string path;
+  int fd = -1;  // open while the file is being written (pwrite, not through the mapping)
+  void done_writing() {
+    if (fd >= 0) ::close(fd);
+    fd = -1;
+  }
   ~Mapping() {
+    done_writing();
     if (p && len) munmap(p, len);
     if (!path.empty()) {
       ::unlink(path.c_str());
@@ -78,11 +84,51 @@ std::shared_ptr<Mapping> create_mapping(const std::string& path, size_t len) {
     fail("cannot size " + path + " to " + std::to_string(len) + " bytes: " + e);
   }
   void* p = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  ::close(fd);
-  if (p == MAP_FAILED) fail("cannot map " + path + ": " + std::strerror(errno));
+  if (p == MAP_FAILED) {
+    ::close(fd);
+    fail("cannot map " + path + ": " + std::strerror(errno));
+  }
   m->p = p;
   m->len = len;
+  m->fd = fd;
   return m;
+}
+
+// The data goes in by pwrite, not through the fresh shared mapping: writing
+// the mapping takes a page fault per 4 KiB page (a spooled GB is 250 k
+// faults); pwrite fills the page cache the mapping then reads. Device data
+// passes through a pinned staging buffer.
+void pwrite_all(const std::shared_ptr<Mapping>& m, const void* src, size_t bytes, size_t off) {
+  const char* p = static_cast<const char*>(src);
+  while (bytes > 0) {
+    const ssize_t w = ::pwrite(m->fd, p, bytes, (off_t)off);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      fail("cannot write " + m->path + ": " + std::strerror(errno));
+    }
+    p += w;
+    off += (size_t)w;
+    bytes -= (size_t)w;
+  }
+}
+void write_tensor(const std::shared_ptr<Mapping>& m, const at::Tensor& t_in, size_t off) {
+  const at::Tensor t = t_in.contiguous();
+  const size_t bytes = (size_t)t.numel() * t.element_size();
+  if (bytes == 0) return;
+  if (t.is_cpu()) {
+    pwrite_all(m, t.data_ptr(), bytes, off);
+    return;
+  }
+  note_xfer(t, at::Device(at::kCPU));
+  const size_t chunk = size_t(16) << 20;
+  at::Tensor stage = at::empty({(int64_t)std::min(chunk, bytes)}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  at::Tensor tb = t.view(at::kByte).view({-1});
+  for (size_t a = 0; a < bytes; a += chunk) {
+    const size_t c = std::min(chunk, bytes - a);
+    at::Tensor st = stage.narrow(0, 0, (int64_t)c);
+    st.copy_(tb.narrow(0, (int64_t)a, (int64_t)c));
+    pwrite_all(m, st.data_ptr(), c, off + a);
+  }
 }
 
 // a host tensor viewing [off, off + numel * elem) of the mapping
@@ -96,8 +142,7 @@ void put_bytes(const std::shared_ptr<Mapping>& m, size_t off, const std::vector<
   size_t at_ = off;
   for (size_t i = 0; i < data.size(); ++i) {
     if (bytes[i] <= 0) continue;
-    at::Tensor dst = view(m, at_, bytes[i], at::kByte);
-    dst.copy_(data[i].narrow(0, first[i], bytes[i]));
+    write_tensor(m, data[i].view(at::kByte).narrow(0, first[i], bytes[i]), at_);
     at_ += (size_t)bytes[i];
   }
 }
@@ -105,7 +150,9 @@ void put_bytes(const std::shared_ptr<Mapping>& m, size_t off, const std::vector<
 // concatenated offset column: part i's offsets rebased to the bytes before it
 void put_offsets(const std::shared_ptr<Mapping>& m, size_t off, const std::vector<at::Tensor>& hoff,
                  const std::vector<int64_t>& ns) {
-  int64_t* d = reinterpret_cast<int64_t*>(static_cast<char*>(m->p) + off);
+  int64_t total = 0;
+  for (int64_t x : ns) total += x;
+  std::vector<int64_t> d((size_t)total + 1);
   int64_t row = 0, base = 0;
   d[0] = 0;
   for (size_t i = 0; i < hoff.size(); ++i) {
@@ -114,6 +161,7 @@ void put_offsets(const std::shared_ptr<Mapping>& m, size_t off, const std::vecto
     row += ns[i];
     base = d[row];
   }
+  pwrite_all(m, d.data(), d.size() * 8, off);
 }
 
 struct Col {
@@ -214,6 +262,7 @@ KV kv_to_file(const std::vector<KV>& parts, const std::string& path) {
   auto m = create_mapping(path, L.total);
   size_t slot = 0;
   KV o = kv_of(m, L, slot, k, v);
+  m->done_writing();
   totals().files++;
   totals().disk_bytes += (int64_t)L.total;
   return o;
@@ -253,7 +302,7 @@ KMV kmv_to_file(const std::vector<KMV>& parts, const std::string& path) {
   o.vw = vals_kv.vw;
   o.nkey = nkey;
   o.nval = vals_kv.n;
-  int64_t* sg = reinterpret_cast<int64_t*>(static_cast<char*>(m->p) + L.off[slot]);
+  std::vector<int64_t> sg((size_t)nkey + 1);
   int64_t row = 0, base = 0;
   for (auto& p : parts) {
     at::Tensor s = host_i64(p.seg);
@@ -263,6 +312,8 @@ KMV kmv_to_file(const std::vector<KMV>& parts, const std::string& path) {
     base += p.nval;
   }
   sg[nkey] = base;
+  pwrite_all(m, sg.data(), sg.size() * 8, L.off[slot]);
+  m->done_writing();
   o.seg = view(m, L.off[slot], nkey + 1, at::kLong);
   totals().files++;
   totals().disk_bytes += (int64_t)L.total;
