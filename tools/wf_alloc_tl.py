@@ -1,5 +1,5 @@
 """Allocations against the H2D copy timeline of a wordfreq trace
-(tools/gpu/gpu_wf_alloc.sh): for the last 3 jobs, every 128 MiB copy (start,
+(tools/gpu/archive/gpu_wf_alloc.sh): for the last 3 jobs, every 128 MiB copy (start,
 duration) interleaved with every device allocation or free that started
 within 1 ms of a copy.
 
