@@ -687,6 +687,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           d["pairs_out"] = s.pairs_out;
           d["h2d_bytes"] = s.h2d_bytes;
           d["d2h_bytes"] = s.d2h_bytes;
+          d["disk_bytes"] = s.disk_bytes;
           st.append(d);
         }
         py::dict d;

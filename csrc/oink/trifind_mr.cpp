@@ -6,6 +6,7 @@
 #include "callbacks.h"
 #include "engine/comm.h"
 #include "engine/tri.h"
+#include "engine/spool.h"
 #include "engine/xfer.h"
 
 namespace mrh {
@@ -15,7 +16,7 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
   TriMRRun run;
   const Comm& comm = *mrt.comm();
   auto npairs = [&](MapReduce& m) -> int64_t {
-    const int64_t n = m.kv ? m.kv_rows() : m.kmv ? m.kmv->nkey : 0;
+    const int64_t n = m.kv ? m.kv_rows() : m.kmv ? m.kmv_keys() : 0;
     return comm.allreduce(n, Comm::SUM);
   };
   // one stage: the op, then a device sync so its kernels count in its time
@@ -26,6 +27,7 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
     comm.host_wait();
     comm.barrier();
     const XferCount x0 = xfer_count();
+    const int64_t d0 = spool_totals().disk_bytes;
     const double t0 = Comm::wtime();
     op();
     comm.host_wait();
@@ -34,6 +36,7 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
     const XferCount x1 = xfer_count();
     s.h2d_bytes = x1.h2d - x0.h2d;
     s.d2h_bytes = x1.d2h - x0.d2h;
+    s.disk_bytes = spool_totals().disk_bytes - d0;
     s.pairs_out = npairs(m);
     run.stages.push_back(s);
   };

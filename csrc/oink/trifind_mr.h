@@ -16,6 +16,7 @@ struct TriMRStage {
   double seconds = 0;   // device-synchronised wall time of the op
   int64_t pairs_in = 0, pairs_out = 0;  // global pair counts before / after
   int64_t h2d_bytes = 0, d2h_bytes = 0;  // this rank's host <-> device copies during the op (xfer.h)
+  int64_t disk_bytes = 0;                 // bytes this process wrote to spool / result files during the op
 };
 struct TriMRRun {
   uint64_t triangles = 0;

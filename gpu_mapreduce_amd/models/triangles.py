@@ -198,23 +198,30 @@ def bench_trifind_mr(comm, args):
             want2 = TriangleGraph(comm, e2, 1 << oscale).count()
             budget = int(getattr(args, "mr_ooc_hbm", 256 << 20))
             host = int(getattr(args, "mr_ooc_host", 2 << 30))
-            sync()
-            t0 = time.perf_counter()
             # pages of the reference's default memsize (64 MB): spool pieces of
-            # min(page, budget / 4) = 64 MiB
-            r2 = tri_find_mr(comm, e2, hbm_budget=budget, host_budget=host, fpath=root, memsize=64)
-            sync()
-            dt2 = comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
-            out["ooc"] = {"scale": oscale, "ms": dt2 * 1e3, "triangles": int(r2["triangles"]),
+            # min(page, budget / 4) = 64 MiB. Run twice: the first (cold) run
+            # also pays the pinned host allocations the caching host allocator
+            # keeps for later jobs; the record's numbers are the second run's
+            dts = []
+            for _ in range(2):
+                sync()
+                t0 = time.perf_counter()
+                r2 = tri_find_mr(comm, e2, hbm_budget=budget, host_budget=host, fpath=root, memsize=64)
+                sync()
+                dts.append(comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64))
+            dt2 = dts[-1]
+            out["ooc"] = {"scale": oscale, "ms": dt2 * 1e3, "ms_cold": dts[0] * 1e3, "triangles": int(r2["triangles"]),
                           "triangles_check": int(want2), "hbm_budget": budget, "host_budget": host,
                           "spool_files": r2["spool_files"], "spool_host_bytes": r2["spool_host_bytes"],
                           "spool_disk_bytes": r2["spool_disk_bytes"],
                           # per stage: host <-> device bytes of this rank, and
-                          # the time at the PCIe floor (50 GB/s) they imply
+                          # the time at the PCIe floor (50 GB/s) they imply;
+                          # disk_bytes: spool / result files written (the disk tier)
                           "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"],
                                       "pcie_bytes": s["h2d_bytes"] + s["d2h_bytes"],
                                       "pcie_floor_ms": round((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 3),
-                                      "x_floor": round(s["ms"] / max((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 1e-3), 2)}
+                                      "x_floor": round(s["ms"] / max((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 1e-3), 2),
+                                      "disk_bytes": s["disk_bytes"]}
                                      for s in r2["stages"]]}
         finally:
             shutil.rmtree(root, ignore_errors=True)

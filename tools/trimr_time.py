@@ -49,5 +49,6 @@ for rep in range(2):
         b = s.get("h2d_bytes", 0) + s.get("d2h_bytes", 0)
         if ooc:
             floor = b / 50e6
-            line += f"  pcie {b / 1e6:9.1f} MB  floor {floor:7.2f} ms  x{s['ms'] / max(floor, 1e-3):6.1f}"
+            line += (f"  pcie {b / 1e6:9.1f} MB  floor {floor:7.2f} ms  x{s['ms'] / max(floor, 1e-3):6.1f}"
+                     f"  disk {s.get('disk_bytes', 0) / 1e6:7.1f} MB")
         print(line, flush=True)
