@@ -602,8 +602,10 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   // its own ranges, so that chunk j's edges are one contiguous run the gather
   // can take on as soon as round j of the c exchange has landed.
   const int dbits = pr_bits_for(std::max<int64_t>(nlocal - 1, 0));
+  // MRH_PR_OVERLAP=0: off; =2: also on one rank (the forced-RCCL mode:
+  // chunked gathers, side-stream rounds and their events without peers)
   const char* oenv = std::getenv("MRH_PR_OVERLAP");
-  const bool by_piece = P > 1 && !(oenv && *oenv == '0');
+  const bool by_piece = (P > 1 && !(oenv && *oenv == '0')) || (oenv && *oenv == '2');
   std::vector<int64_t> rb, redge;
   std::vector<int> piece_nr;  // ranges of every chunk (by_piece)
   at::Tensor dg;
@@ -622,30 +624,37 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   if (by_piece) {
     int K = 4;
     if (const char* e = std::getenv("MRH_PR_PIECES")) K = std::max(1, std::min(64, std::atoi(e)));
-    // chunk boundaries b_j (new ids, multiples of 16: 64-byte aligned
-    // transfers) at the edge-count quantiles of the degree-sorted ids
-    at::Tensor cum = at::cumsum(dg.to(at::kLong), 0);
-    const int64_t total = S > 0 ? cum[P * S - 1].item<int64_t>() : 0;
+    // the one-GPU ranges over the interleaved order, then grouped into K
+    // chunks of about equal edge count: a chunk ends at a range boundary
+    // moved to a multiple of 16 P (so it is new id b_j of every rank, b_j a
+    // multiple of 16: 64-byte aligned transfers); no range is added
+    std::vector<int64_t> grb, gre;
+    if (want_ranges) xcd_ranges(dg, P * S, dbits, grb, gre);
+    if (grb.empty()) {
+      grb = {0};
+      gre = {0, dg.defined() && S > 0 ? dg.sum().item<int64_t>() : 0};
+    }
+    const int nr = (int)grb.size();  // ranges: nr - 1 hot, then the cold one
+    const int64_t total = gre.back();
+    std::vector<int> cut{0};  // first range of every chunk
     std::vector<int64_t> b{0};
     for (int j = 1; j < K && total > 0; ++j) {
-      at::Tensor t = at::tensor({total * j / K}, opt(at::kCPU, at::kLong)).to(dev);
-      const int64_t g = at::searchsorted(cum, t).item<int64_t>();  // first gid reaching the quantile
-      const int64_t id = std::min(S, (g / P + 16) / 16 * 16);
-      if (id > b.back() && id < S) b.push_back(id);
+      const int64_t target = total * j / K;
+      int r = (int)(std::lower_bound(gre.begin(), gre.begin() + nr, target) - gre.begin());
+      if (r <= cut.back() || r >= nr) continue;
+      const int64_t id = (grb[r] / P + 8) / 16 * 16;  // nearest multiple of 16 new ids
+      const int64_t g = id * P;
+      if (id <= b.back() || g <= grb[r - 1] || (r + 1 < nr && g >= grb[r + 1]) || id >= S) continue;
+      grb[r] = g;
+      cut.push_back(r);
+      b.push_back(id);
     }
     b.push_back(S);
     chunk_b_ = b;
-    // at most 2^(32 - dbits) ranges in all, shared by the chunks
-    const int nch = (int)b.size() - 1;
-    const int cap_each = std::max(1, (1 << std::max(0, std::min(9, 32 - dbits))) / nch);
-    for (int j = 0; j < nch; ++j) {
-      const int64_t g0 = P * b[j], len = P * (b[j + 1] - b[j]);
-      std::vector<int64_t> rbq, rdq;
-      if (want_ranges && cap_each >= 9) xcd_ranges(dg.narrow(0, g0, len), len, dbits, rbq, rdq, cap_each);
-      rb.push_back(g0);
-      for (size_t q = 1; q < rbq.size(); ++q) rb.push_back(g0 + rbq[q]);
-      piece_nr.push_back(std::max<int>(1, (int)rbq.size()));
-    }
+    for (size_t j = 0; j + 1 < cut.size(); ++j) piece_nr.push_back(cut[j + 1] - cut[j]);
+    piece_nr.push_back(nr - cut.back());
+    rb = grb;
+    if (rb.size() == 1) rb.clear();  // one cold range: no range ids at all
   } else if (want_ranges) {
     xcd_ranges(dg, P * S, dbits, rb, redge);
   }
@@ -734,11 +743,14 @@ void PageRankPlan::build_pieces(const std::vector<int>& piece_nr) {
       pc.src = srcp_.narrow(0, off[q], pc.n);
       pc.src.copy_(src_.narrow(0, e0, pc.n));
       pc.six = seg_index(seg_.narrow(0, pc.g0, pc.ng + 1) - e0, pc.n);
-      if (piece_nr[q] > 1) {
+      // hot range r on XCD slot r % 8 as in the one-GPU schedule; only the
+      // last chunk ends with the cold range (dealt round-robin)
+      const bool last = q + 1 == K;
+      if (piece_nr[q] > 1 || !last) {
         std::vector<int64_t> re;
         for (int64_t r = R0[q]; r < R0[q + 1]; ++r) re.push_back(fe[r] - e0);
         re.push_back(pc.n);
-        auto [sc, sl] = wave_schedule(re, pc.n);
+        auto [sc, sl] = wave_schedule(re, pc.n, (int)R0[q], last);
         pc.six.sched = sc;
         pc.six.slen = sl;
       }
@@ -777,7 +789,7 @@ void PageRankPlan::ring_start() {
       xs.push_back(Xfer{p, base + (int64_t)me * S_ * 4 + a, len});
       xr.push_back(Xfer{p, base + (int64_t)p * S_ * 4 + a, len});
     }
-    comm->sendrecv(xs, xr);
+    if (!xs.empty()) comm->sendrecv(xs, xr);
     pr_chk(hipEventRecord(ring_ev_[j + 1], side_), "hipEventRecord");
   }
 }
@@ -892,14 +904,15 @@ void PageRankPlan::xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits
 // the 8 x slen wave schedule of the gather: wave w (edges [1024 w, 1024 w +
 // 1024)) belongs to the range holding its first edge; hot range r runs on
 // slot r % 8 in layer order, the cold waves are dealt round-robin after them
-std::pair<at::Tensor, int64_t> PageRankPlan::wave_schedule(const std::vector<int64_t>& redge, int64_t n) const {
+std::pair<at::Tensor, int64_t> PageRankPlan::wave_schedule(const std::vector<int64_t>& redge, int64_t n, int r_base,
+                                                           bool last_cold) const {
   const int64_t T = 1024;  // wavesegred.h WS_TILE
   const int64_t nw = (n + T - 1) / T;
-  const int nhot = (int)redge.size() - 2;
+  const int nhot = (int)redge.size() - (last_cold ? 2 : 1);
   std::vector<std::vector<int32_t>> rows(8);
   auto wave_of = [&](int64_t e) { return std::min(nw, (e + T - 1) / T); };
   for (int r = 0; r < nhot; ++r)
-    for (int64_t w = wave_of(redge[r]); w < wave_of(redge[r + 1]); ++w) rows[r % 8].push_back((int32_t)w);
+    for (int64_t w = wave_of(redge[r]); w < wave_of(redge[r + 1]); ++w) rows[(r_base + r) % 8].push_back((int32_t)w);
   int64_t c = 0;
   for (int64_t w = wave_of(redge[std::max(nhot, 0)]); w < nw; ++w, ++c) rows[c % 8].push_back((int32_t)w);
   size_t slen = 0;

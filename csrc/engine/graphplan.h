@@ -117,9 +117,11 @@ class PageRankPlan {
   void xcd_ranges(const at::Tensor& degn, int64_t nactive, int dbits, std::vector<int64_t>& rb,
                   std::vector<int64_t>& redge, int maxr_cap = 64);
   void xcd_schedule(const std::vector<int64_t>& redge);
-  // the 8 x slen wave schedule of n edges whose ranges start at redge (hot
-  // ranges, then the cold one; redge.back() = n)
-  std::pair<at::Tensor, int64_t> wave_schedule(const std::vector<int64_t>& redge, int64_t n) const;
+  // the 8 x slen wave schedule of n edges whose ranges start at redge
+  // (redge.back() = n): hot range r on XCD slot (r_base + r) % 8, then (if
+  // last_cold) the cold range's waves round-robin
+  std::pair<at::Tensor, int64_t> wave_schedule(const std::vector<int64_t>& redge, int64_t n, int r_base = 0,
+                                               bool last_cold = true) const;
   // the plan from this rank's edges (source-owned): device kernels, or the
   // tensor-op twin on the CPU engine
   void build_device(const at::Tensor& e);
@@ -139,9 +141,9 @@ class PageRankPlan {
   int64_t S_ = 0;      // c slice length per rank
   at::Tensor cfull_;   // the replicated c vector, P slices of S_ (+ slack)
   // several GPUs: the edges cut into K pieces by source chunk (chunk j = new
-  // ids [chunk_b_[j], chunk_b_[j + 1]) of every rank, equal edge counts),
-  // each with its own XCD ranges, segment index and 16-byte aligned source
-  // stream; the c exchange runs on side_ in K rounds (round j: chunk j of
+  // ids [chunk_b_[j], chunk_b_[j + 1]) of every rank, about equal edge
+  // counts: consecutive XCD ranges of the one-GPU plan), each with its own
+  // segment index, schedule and 16-byte aligned source stream; the c exchange runs on side_ in K rounds (round j: chunk j of
   // every slice, to and from every peer at once) and piece j is gathered as
   // soon as round j has landed (MRH_PR_OVERLAP=0: one all-gather after the
   // tile step, then one gather)

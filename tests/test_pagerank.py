@@ -258,3 +258,31 @@ def test_pagerank_hot_prefix_gather_matches_global_gather(tmp_path):
         res[name] = np.load(path)
     assert np.abs(res["hot"] - res["off"]).sum() <= 1e-6
     assert np.abs(res["small"] - res["off"]).sum() <= 1e-6
+
+
+@pytest.mark.gpu
+def test_pagerank_forced_rccl_overlapped_pieces_match_local(tmp_path):
+    """MRH_PR_OVERLAP=2 on a forced one-rank RCCL communicator: the multi-GPU
+    plan's source chunks (their own XCD ranges, segment indexes and source
+    streams), the side-stream exchange rounds (no peers at one rank) and
+    their events — the ranks of 27 iterations (a 20-run after reset, then a
+    7-run) equal the local plan's to float32 accumulation differences"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res, info = {}, {}
+    for name, extra in (("local", {}), ("pieces", {"MRH_FORCE_RCCL": "1", "MRH_PR_OVERLAP": "2"})):
+        env = dict(os.environ, PYTHONPATH=root, **extra)
+        if name == "local":
+            env.pop("MRH_FORCE_RCCL", None)
+            env.pop("MRH_PR_OVERLAP", None)
+        path = str(tmp_path / f"{name}.npy")
+        p = subprocess.run([sys.executable, "-c", FORCED_CHILD, path], env=env, cwd=root, capture_output=True,
+                           text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-3000:]
+        info[name] = p.stdout.split()[-3:]
+        res[name] = np.load(path)
+    assert info["pieces"][0] == "replicated" and info["pieces"][2] == "rccl", info
+    assert int(info["pieces"][1]) > 9, info  # several chunks' ranges
+    np.testing.assert_allclose(res["pieces"], res["local"], rtol=1e-4, atol=1e-10)

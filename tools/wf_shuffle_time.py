@@ -34,10 +34,18 @@ for rep in range(jobs):
     t = (time.perf_counter() - t0) * 1e3
     print(f"job {rep}: {t:.1f} ms  " + "  ".join(f"{k} {v * 1e3:.1f}" for k, v in ph.items())
           + f"  pairs {app.npairs} unique {app.nunique} top {app.top[:3]}", flush=True)
+from gpu_mapreduce_amd.runtime import hbm_pool  # noqa: E402
 for rep in range(jobs):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    del app  # the previous job's MapReduce goes away here (inside the bench's timed loop too)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
     app = WordFreq(g.MapReduce(comm), chunks, combiner=comb)
     app.run()
     torch.cuda.synchronize()
-    print(f"plain job {rep}: {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+    t2 = time.perf_counter()
+    st = hbm_pool.stats(0) if hbm_pool.installed() else {}
+    print(f"plain job {rep}: {(t2 - t0) * 1e3:.1f} ms (teardown of the previous {(t1 - t0) * 1e3:.1f}, job "
+          f"{(t2 - t1) * 1e3:.1f}); pool grows {st.get('grows')} grow_ms {st.get('grow_ms')} releases "
+          f"{st.get('releases')} reserved {st.get('reserved', 0) / 1e9:.1f} GB", flush=True)
