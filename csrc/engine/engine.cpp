@@ -1526,19 +1526,27 @@ KV map_words(const at::Tensor& text, int64_t n) {
   kv.vw = 0;
   kv.vdata = at::empty({0}, opt(dev, at::kByte));
   if (dev.is_cuda()) {
+    // per-tile words and key bytes, their scans, one host read of both
+    // totals, then keys and offsets in one pass (text.hip k_tok_emit2)
     auto s = cur_stream();
-    int64_t nt = k::tok_num_tiles(n);
-    at::Tensor cnt = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kInt));
-    k::tok_count(P0<uint8_t>(text), n, P0<uint32_t>(cnt), s);
-    at::Tensor toff = scan_u32(cnt.narrow(0, 0, nt));
-    int64_t nw = (int64_t)(uint32_t)toff[nt].item<int32_t>();
-    at::Tensor starts = at::empty({std::max<int64_t>(nw, 1)}, opt(dev, at::kLong));
-    at::Tensor klen = at::empty({std::max<int64_t>(nw, 1)}, opt(dev, at::kInt));
-    k::tok_emit(P0<uint8_t>(text), n, P0<uint32_t>(toff), P0<int64_t>(starts), P0<int32_t>(klen), s);
-    kv.koff = exclusive_scan(klen.narrow(0, 0, nw));
-    int64_t kb = scalar_i64(kv.koff, nw);
+    const int64_t nt = k::tok_num_tiles(n);
+    if (nt <= 0) {
+      kv.n = 0;
+      kv.koff = at::zeros({1}, opt(dev, at::kLong));
+      kv.kdata = at::empty({0}, opt(dev, at::kByte));
+      return kv;
+    }
+    at::Tensor cw = at::empty({nt}, opt(dev, at::kInt)), cb = at::empty({nt}, opt(dev, at::kInt));
+    k::tok_count2(P0<uint8_t>(text), n, P0<uint32_t>(cw), P0<uint32_t>(cb), s);
+    at::Tensor tw = scan_u32(cw);        // u32 [nt + 1]
+    at::Tensor tb = exclusive_scan(cb);  // i64 [nt + 1]
+    at::Tensor tot = at::cat({tw.narrow(0, nt, 1).to(at::kLong), tb.narrow(0, nt, 1)}).to(at::kCPU);
+    const int64_t nw = (int64_t)(uint32_t)tot.data_ptr<int64_t>()[0], kb = tot.data_ptr<int64_t>()[1];
+    kv.koff = at::empty({nw + 1}, opt(dev, at::kLong));
     kv.kdata = at::empty({kb}, opt(dev, at::kByte));
-    k::copy_strings_nul(P0<uint8_t>(text), P0<int64_t>(starts), P0<int64_t>(kv.koff), nw, P0<uint8_t>(kv.kdata), s);
+    k::tok_emit2(P0<uint8_t>(text), n, P0<uint32_t>(tw), P0<int64_t>(tb), P0<int64_t>(kv.koff), P0<uint8_t>(kv.kdata),
+                 s);
+    kv.koff.narrow(0, nw, 1).fill_(kb);
     kv.n = nw;
     return kv;
   }

@@ -624,9 +624,9 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   if (by_piece) {
     int K = 4;
     if (const char* e = std::getenv("MRH_PR_PIECES")) K = std::max(1, std::min(64, std::atoi(e)));
-    // the one-GPU ranges over the interleaved order, then grouped into K
-    // chunks of about equal edge count: a chunk ends at a range boundary
-    // moved to a multiple of 16 P (so it is new id b_j of every rank, b_j a
+    // the one-GPU ranges over the interleaved order, then grouped into at
+    // most K chunks of whole layers (8 ranges) near the edge-count quantiles:
+    // a chunk ends at a range boundary moved to a multiple of 16 P (so it is new id b_j of every rank, b_j a
     // multiple of 16: 64-byte aligned transfers); no range is added
     std::vector<int64_t> grb, gre;
     if (want_ranges) xcd_ranges(dg, P * S, dbits, grb, gre);
@@ -641,6 +641,9 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
     for (int j = 1; j < K && total > 0; ++j) {
       const int64_t target = total * j / K;
       int r = (int)(std::lower_bound(gre.begin(), gre.begin() + nr, target) - gre.begin());
+      // whole layers only: a layer's 8 ranges run side by side on the 8
+      // XCDs, a chunk holding part of one would leave XCDs idle
+      r = (r + 4) / 8 * 8;
       if (r <= cut.back() || r >= nr) continue;
       const int64_t id = (grb[r] / P + 8) / 16 * 16;  // nearest multiple of 16 new ids
       const int64_t g = id * P;

@@ -195,6 +195,13 @@ void url_copy(const uint8_t* text, const int64_t* starts, const int64_t* koff, i
               uint8_t* kdata, hipStream_t s);
 // whitespace tokenizer (wordfreq): word starts/lengths; keys are word + NUL
 int64_t tok_num_tiles(int64_t n);
+// wordfreq pairs in one pass (text.hip k_tok_count2 / k_tok_emit2): per tile
+// the words and the key bytes (non-separators + one NUL per word), then the
+// key bytes and key offsets written from their exclusive scans (toff_w u32,
+// toff_b i64; koff[nw] is the caller's)
+void tok_count2(const uint8_t* text, int64_t n, uint32_t* tile_words, uint32_t* tile_bytes, hipStream_t s);
+void tok_emit2(const uint8_t* text, int64_t n, const uint32_t* toff_w, const int64_t* toff_b, int64_t* koff,
+               uint8_t* kd, hipStream_t s);
 void tok_count(const uint8_t* text, int64_t n, uint32_t* tile_counts, hipStream_t s);
 void tok_emit(const uint8_t* text, int64_t n, const uint32_t* tile_off, int64_t* starts,
               int32_t* keylen, hipStream_t s);

@@ -149,6 +149,87 @@ __global__ __launch_bounds__(NT) void k_tok_emit(const uint8_t* __restrict__ tex
   }
 }
 
+// wordfreq's pairs in one pass (map_words): a thread's 16 bytes give a start
+// mask S, an end mask E (last byte of a word) and a non-separator mask; the
+// keys are the words compacted with a NUL after each, so byte i of a word
+// lands at (non-separator bytes before i) + (words ended before i), and word
+// w's offset is where its first byte lands. k_tok_count2 counts per tile
+// (words; non-separator bytes + ends), k_tok_emit2 writes the key bytes and
+// offsets from the two scans — no start array, no per-word length walk, no
+// separate copy kernel.
+__device__ __forceinline__ void word_masks(const uint8_t* text, int64_t p, int64_t n, uint32_t* S, uint32_t* E,
+                                           uint32_t* B) {
+  const uint4 a = *reinterpret_cast<const uint4*>(text + p);
+  const uint32_t nxt = (uint32_t)text[p + 16];
+  const uint32_t prev = (p == 0) ? 0u : (uint32_t)text[p - 1];
+  const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+  bool ws[18];
+  ws[0] = is_ws(prev);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) ws[k + 1] = is_ws((w[k >> 2] >> (8 * (k & 3))) & 0xffu) | (p + k >= n);
+  ws[17] = is_ws(nxt) | (p + 16 >= n);
+  uint32_t s = 0, e = 0, b = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    s |= (uint32_t)(!ws[k + 1] && ws[k]) << k;
+    e |= (uint32_t)(!ws[k + 1] && ws[k + 2]) << k;
+    b |= (uint32_t)(!ws[k + 1]) << k;
+  }
+  *S = s;
+  *E = e;
+  *B = b;
+}
+
+__global__ __launch_bounds__(NT) void k_tok_count2(const uint8_t* __restrict__ text, int64_t n,
+                                                  uint32_t* __restrict__ tile_words,
+                                                  uint32_t* __restrict__ tile_bytes) {
+  __shared__ uint32_t sh[2][NT / MRH_WAVE];
+  const int64_t p = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * 16;
+  uint32_t cw = 0, cb = 0;
+  if (p < n) {
+    uint32_t S, E, B;
+    word_masks(text, p, n, &S, &E, &B);
+    cw = (uint32_t)__popc(S);
+    cb = (uint32_t)(__popc(B) + __popc(E));
+  }
+  cw = dev::wave_sum(cw);
+  cb = dev::wave_sum(cb);
+  if (dev::lane_id() == 0) {
+    sh[0][dev::wave_id()] = cw;
+    sh[1][dev::wave_id()] = cb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tile_words[blockIdx.x] = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+    tile_bytes[blockIdx.x] = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_tok_emit2(const uint8_t* __restrict__ text, int64_t n,
+                                                 const uint32_t* __restrict__ toff_w,
+                                                 const int64_t* __restrict__ toff_b,
+                                                 int64_t* __restrict__ koff, uint8_t* __restrict__ kd) {
+  __shared__ uint32_t shw[NT / MRH_WAVE + 1];
+  __shared__ uint32_t shb[NT / MRH_WAVE + 1];
+  const int64_t p = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * 16;
+  uint32_t S = 0, E = 0, B = 0;
+  if (p < n) word_masks(text, p, n, &S, &E, &B);
+  uint32_t tw, tb;
+  const uint32_t pw = dev::block_excl_scan<uint32_t, NT>((uint32_t)__popc(S), shw, &tw);
+  const uint32_t pb = dev::block_excl_scan<uint32_t, NT>((uint32_t)(__popc(B) + __popc(E)), shb, &tb);
+  if (!(S | B)) return;
+  int64_t w = (int64_t)toff_w[blockIdx.x] + pw;
+  int64_t o = toff_b[blockIdx.x] + pb;
+  const uint4 a = *reinterpret_cast<const uint4*>(text + p);
+  const uint32_t wd[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if ((S >> k) & 1u) koff[w++] = o;
+    if ((B >> k) & 1u) kd[o++] = (uint8_t)((wd[k >> 2] >> (8 * (k & 3))) & 0xffu);
+    if ((E >> k) & 1u) kd[o++] = 0;
+  }
+}
+
 // 16 lanes per string
 __global__ __launch_bounds__(NT) void k_copy_nul(const uint8_t* __restrict__ text,
                                                 const int64_t* __restrict__ starts,
@@ -205,6 +286,19 @@ void copy_strings_nul(const uint8_t* text, const int64_t* starts, const int64_t*
 void url_copy(const uint8_t* text, const int64_t* starts, const int64_t* koff, int64_t nurl,
               uint8_t* kdata, hipStream_t s) {
   copy_strings_nul(text, starts, koff, nurl, kdata, s);
+}
+void tok_count2(const uint8_t* text, int64_t n, uint32_t* tile_words, uint32_t* tile_bytes, hipStream_t s) {
+  const int64_t nt = tok_num_tiles(n);
+  if (nt <= 0) return;
+  hipLaunchKernelGGL(k_tok_count2, dim3((unsigned)nt), dim3(NT), 0, s, text, n, tile_words, tile_bytes);
+  MRH_CHECK_LAUNCH();
+}
+void tok_emit2(const uint8_t* text, int64_t n, const uint32_t* toff_w, const int64_t* toff_b, int64_t* koff,
+               uint8_t* kd, hipStream_t s) {
+  const int64_t nt = tok_num_tiles(n);
+  if (nt <= 0) return;
+  hipLaunchKernelGGL(k_tok_emit2, dim3((unsigned)nt), dim3(NT), 0, s, text, n, toff_w, toff_b, koff, kd);
+  MRH_CHECK_LAUNCH();
 }
 void tok_count(const uint8_t* text, int64_t n, uint32_t* tile_counts, hipStream_t s) {
   int64_t nt = tok_num_tiles(n);

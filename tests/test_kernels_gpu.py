@@ -203,6 +203,30 @@ def test_map_urls_and_words_match_cpu():
     assert len(a) > 1000 and a == b
 
 
+def test_map_words_separators_and_tile_edges():
+    """one-pass word keys (text.hip k_tok_emit2): runs of mixed separators,
+    leading / trailing separators, words across 16-byte thread and 4 KiB tile
+    boundaries, a 10 KB word, a word ending exactly at n (bytes past n are
+    separators even when the padding is not)"""
+    import random
+    from gpu_mapreduce_amd.utils import synth
+    rng = random.Random(7)
+    parts = [b"  \t"]
+    for i in range(40000):
+        parts.append(b"w%d" % rng.randrange(5000) + b"x" * rng.choice([0, 0, 1, 5, 13, 30]))
+        parts.append(rng.choice([b" ", b" ", b"\n", b"\t\r ", b"   \f  "]))
+    parts.append(b"L" * 10000)
+    parts.append(b" tail")
+    raw = b"".join(parts)
+    t = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+    for cut in (len(raw), len(raw) - 2, 4096 * 7 + 3):
+        w = synth.pad_text(t[:cut].clone())
+        w[cut:cut + 8] = ord("z")  # non-separators right past n must not extend the last word
+        a = _kv_rows(C.map_words(w, cut))
+        b = _kv_rows(C.map_words(w.to(DEV), cut))
+        assert len(a) > 100 and a == b, cut
+
+
 def test_rmat_bit_exact():
     a = C.map_rmat(100_000, 16, 0.57, 0.19, 0.19, 0.05, 0.0, 12345, 777, "cpu")
     b = C.map_rmat(100_000, 16, 0.57, 0.19, 0.19, 0.05, 0.0, 12345, 777, DEV)
