@@ -61,14 +61,18 @@ class WordFreq:
         self.combiner = combiner
         self.is_cuda = mr.device.startswith("cuda")
         maxlen = max((t.numel() for t in chunks), default=0)
-        # staging ring depth = the MR's `streams` setting (0 = auto: 3, or
+        # staging ring depth = the MR's `streams` setting (0 = auto, or
         # MRH_WF_BUFS) — with two buffers the copy of chunk i+2 waits for the
         # count kernel of chunk i; 1 GiB step 29.0 / 24.5 / 25.3 ms with 2 / 3 /
-        # 4 buffers on one MI355X (profiles/r2_wordfreq_ring.txt); streams = 1
-        # copies and counts one chunk at a time
+        # 4 buffers on one MI355X (profiles/r2_wordfreq_ring.txt). Without the
+        # combiner every chunk's pairs are grouped too, and a copy behind a
+        # buffer still read ran at half speed: 8 GiB 197 / 188 / 180 ms with
+        # 3 / 4 / 6 buffers (profiles/r5_wordfreq_ring.txt) — 6 there, 3 with
+        # the combiner. streams = 1 copies and counts one chunk at a time
         import os
         st = int(mr.streams)
-        self.nbuf = st if st > 0 else max(2, int(os.environ.get("MRH_WF_BUFS", "3")))
+        auto = 3 if combiner else 6
+        self.nbuf = st if st > 0 else max(2, int(os.environ.get("MRH_WF_BUFS", str(auto))))
         self.bufs = [pools.device_buffer(mr.device, maxlen + PAD, 8 + s) for s in range(self.nbuf if chunks else 0)]
         # the process's persistent H2D stream (a new stream per job would be
         # a new HIP queue each time)

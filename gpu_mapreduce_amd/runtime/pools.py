@@ -29,7 +29,11 @@ def device_buffer(device: str, nbytes: int, slot: int = 0) -> torch.Tensor:
             # prefetch into it is void (take_prefetch also checks the buffer)
             torch.cuda.synchronize(device)
             _prefetch.pop(key, None)
-        b = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        # MRH_STAGE_MIN_BYTES: allocate staging buffers at least this large
+        # (an experiment on H2D copy speed by allocation path)
+        import os
+        floor = int(os.environ.get("MRH_STAGE_MIN_BYTES", "0") or 0)
+        b = torch.empty(max(nbytes, floor, 1), dtype=torch.uint8, device=device)
         _dev[key] = b
     return b
 

@@ -17,6 +17,8 @@ from gpu_mapreduce_amd.utils import synth  # noqa: E402
 gib = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
 jobs = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 comb = bool(int(sys.argv[3])) if len(sys.argv) > 3 else False
+from gpu_mapreduce_amd.parallel.comm import bind_numa_local  # noqa: E402
+bind_numa_local(0)  # as bench.py: host buffers on the GPU's NUMA node
 nb = int(gib * (1 << 30))
 chunk = 128 << 20
 chunks = []
@@ -49,3 +51,19 @@ for rep in range(jobs):
     print(f"plain job {rep}: {(t2 - t0) * 1e3:.1f} ms (teardown of the previous {(t1 - t0) * 1e3:.1f}, job "
           f"{(t2 - t1) * 1e3:.1f}); pool grows {st.get('grows')} grow_ms {st.get('grow_ms')} releases "
           f"{st.get('releases')} reserved {st.get('reserved', 0) / 1e9:.1f} GB", flush=True)
+# H2D into each staging slot of the ring, from one pinned chunk (is one slot slow?)
+src = chunks[0]
+for b, buf in enumerate(app.bufs):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        buf[: src.numel()].copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 5
+    print(f"slot {b}: {src.numel() / dt / 1e9:.1f} GB/s  ptr {buf.data_ptr():#x}", flush=True)
+for i in range(min(6, len(chunks))):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    app.bufs[0][: chunks[i].numel()].copy_(chunks[i], non_blocking=True)
+    torch.cuda.synchronize()
+    print(f"chunk {i} -> slot 0: {chunks[i].numel() / (time.perf_counter() - t0) / 1e9:.1f} GB/s  host ptr {chunks[i].data_ptr():#x}", flush=True)
