@@ -12,6 +12,8 @@
 #include <cstdio>
 #include <cstring>
 #include <filesystem>
+#include <future>
+#include <mutex>
 #include <stdexcept>
 
 namespace mrh {
@@ -28,6 +30,8 @@ SpoolStats& totals() {
   static SpoolStats s;
   return s;
 }
+// totals are also updated by the background file writers
+std::mutex g_totals_mu;
 
 // one memory-mapped spool file; unmapped and deleted with the last view
 struct Mapping {
@@ -263,8 +267,11 @@ KV kv_to_file(const std::vector<KV>& parts, const std::string& path) {
   size_t slot = 0;
   KV o = kv_of(m, L, slot, k, v);
   m->done_writing();
-  totals().files++;
-  totals().disk_bytes += (int64_t)L.total;
+  {
+    std::lock_guard<std::mutex> g(g_totals_mu);
+    totals().files++;
+    totals().disk_bytes += (int64_t)L.total;
+  }
   return o;
 }
 
@@ -315,8 +322,11 @@ KMV kmv_to_file(const std::vector<KMV>& parts, const std::string& path) {
   pwrite_all(m, sg.data(), sg.size() * 8, L.off[slot]);
   m->done_writing();
   o.seg = view(m, L.off[slot], nkey + 1, at::kLong);
-  totals().files++;
-  totals().disk_bytes += (int64_t)L.total;
+  {
+    std::lock_guard<std::mutex> g(g_totals_mu);
+    totals().files++;
+    totals().disk_bytes += (int64_t)L.total;
+  }
   return o;
 }
 
@@ -332,6 +342,17 @@ Spool::~Spool() {
 }
 
 void Spool::sync() {
+  // background file writes first (their drains are in pending_ too)
+  std::exception_ptr err;
+  for (auto& [i, f] : writing_) {
+    try {
+      pieces_[i] = f.get();
+    } catch (...) {
+      if (!err) err = std::current_exception();
+    }
+  }
+  writing_.clear();
+  if (err) std::rethrow_exception(err);
   for (hipEvent_t e : pending_) {
     const hipError_t r = hipEventSynchronize(e);
     (void)hipEventDestroy(e);
@@ -409,6 +430,45 @@ void Spool::add(const KV& piece, hipStream_t copy) {
         fail("drain event failed");
       pending_.push_back(done);
     }
+  } else if (copy && cuda && piece.device().is_cuda()) {
+    // the disk tier off the caller's path: drain into pinned memory on the
+    // copy stream, then a background thread writes and maps the file
+    hipStream_t cs = at::hip::getCurrentHIPStream().stream();
+    hipEvent_t fence, done;
+    if (hipEventCreateWithFlags(&fence, hipEventDisableTiming) != hipSuccess || hipEventRecord(fence, cs) != hipSuccess ||
+        hipStreamWaitEvent(copy, fence, 0) != hipSuccess)
+      fail("drain fence failed");
+    (void)hipEventDestroy(fence);
+    auto h = [&](const at::Tensor& t) {
+      if (!t.defined()) return t;
+      at::Tensor src = t.contiguous();
+      at::Tensor o = at::empty(src.sizes(), src.options().device(at::kCPU).pinned_memory(true));
+      note_xfer(src, at::Device(at::kCPU));
+      const size_t nb = (size_t)src.numel() * src.element_size();
+      if (nb && hipMemcpyAsync(o.data_ptr(), src.data_ptr(), nb, hipMemcpyDeviceToHost, copy) != hipSuccess)
+        fail("asynchronous drain copy failed");
+      c10::hip::HIPCachingAllocator::recordStream(src.storage().data_ptr(),
+                                                 c10::hip::getStreamFromExternal(copy, dev_.index()));
+      return o;
+    };
+    KV hp = piece;
+    hp.kdata = h(piece.kdata);
+    hp.vdata = h(piece.vdata);
+    hp.koff = h(piece.koff);
+    hp.voff = h(piece.voff);
+    if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess || hipEventRecord(done, copy) != hipSuccess)
+      fail("drain event failed");
+    const std::string path = next_path();
+    writing_.emplace_back(pieces_.size(), std::async(std::launch::async, [hp, done, path]() {
+                            const hipError_t r = hipEventSynchronize(done);
+                            (void)hipEventDestroy(done);
+                            if (r != hipSuccess) fail(std::string("asynchronous drain failed: ") + hipGetErrorString(r));
+                            return kv_to_file({hp}, path);
+                          }));
+    p = KV();  // filled in by sync()
+    tier = 2;
+    st_.disk_bytes += b;
+    st_.files++;
   } else {
     p = kv_to_file({piece}, next_path());
     tier = 2;

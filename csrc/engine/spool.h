@@ -20,7 +20,9 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <future>
 #include <memory>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -70,7 +72,9 @@ class Spool {
   // append one piece (device or host tensors) to the first tier with room.
   // With `copy` set, a device piece bound for the host tier drains on that
   // stream (ordered after the work queued so far on the current stream) while
-  // the caller goes on; every read of the spool waits for the drains first.
+  // the caller goes on, and one bound for disk drains the same way into
+  // pinned memory that a background thread writes to its file; every read of
+  // the spool waits for the drains and writes first.
   void add(const KV& piece, hipStream_t copy = nullptr);
   // wait for the asynchronous drains
   void sync();
@@ -102,6 +106,10 @@ class Spool {
   std::vector<KV> pieces_;
   std::vector<int> tier_;  // 0 HBM, 1 pinned host, 2 disk
   std::vector<hipEvent_t> pending_;
+  // disk-tier pieces being written by a background thread (index into
+  // pieces_, the file-backed KV): the device piece drained into pinned
+  // memory on the copy stream, then written and mapped off the caller's path
+  std::vector<std::pair<size_t, std::future<KV>>> writing_;
   int64_t n_ = 0, bytes_ = 0;
   SpoolStats st_;
 };
