@@ -1100,15 +1100,23 @@ void PageRankPlan::graph_free() {
   gkey_.clear();
 }
 
-// graph replay: one GPU, the XCD tile-step path, a fixed iteration count, no
-// serialising diagnostic mode
+// graph replay: the XCD tile-step path, a fixed iteration count, no
+// serialising diagnostic mode. One GPU; or the replicated multi-GPU plan over
+// the native RCCL communicator, whose exchange rounds (side_), allreduce and
+// the RCCL stream join the capture through their events
+// (MRH_PR_DIST_GRAPH=0 keeps the multi-GPU iteration eager)
 bool PageRankPlan::graph_ok() const {
   static const bool sync = [] {
     const char* v = std::getenv("MRH_SYNC");
     return v && *v && *v != '0';
   }();
-  return use_graph && !sync && dev.is_cuda() && !comm->distributed() && !pb_ && xr_ > 0 && six_.defined() &&
-         send_.numel() > 0;
+  static const bool dist_graph = [] {
+    const char* v = std::getenv("MRH_PR_DIST_GRAPH");
+    return !(v && *v == '0');
+  }();
+  if (!use_graph || sync || !dev.is_cuda() || pb_ || xr_ <= 0 || send_.numel() == 0) return false;
+  if (dist_dev_) return dist_graph && !dist_graph_failed_ && comm->uses_rccl() && !pieces_.empty();
+  return !comm->distributed() && six_.defined();
 }
 
 // capture two iterations (r_ -> rn_, rn_ -> r_) on a private stream: every
@@ -1133,8 +1141,13 @@ void PageRankPlan::graph_build() {
       throw std::runtime_error("PageRank graph: the capture stream is not current");
     chk(hipStreamBeginCapture(gstream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
     try {
-      launch_iter(r_, rn_);
-      launch_iter(rn_, r_);
+      if (dist_dev_) {  // ring on in both (run() made c_fresh_ false first)
+        launch_iter_dist(r_, rn_);
+        launch_iter_dist(rn_, r_);
+      } else {
+        launch_iter(r_, rn_);
+        launch_iter(rn_, r_);
+      }
     } catch (...) {
       hipGraph_t bad = nullptr;
       (void)hipStreamEndCapture(gstream_, &bad);
@@ -1146,7 +1159,12 @@ void PageRankPlan::graph_build() {
   const hipError_t e = hipGraphInstantiate(&gexec_, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   chk(e, "hipGraphInstantiate");
-  gkey_ = {r_.data_ptr(), rn_.data_ptr(), c_.data_ptr(), stats_.data_ptr(), send_.data_ptr(), part_.data_ptr()};
+  gkey_ = graph_key();
+}
+
+std::vector<const void*> PageRankPlan::graph_key() const {
+  return {r_.data_ptr(), rn_.data_ptr(), c_.data_ptr(), stats_.data_ptr(), send_.data_ptr(), part_.data_ptr(),
+          cfull_.defined() ? cfull_.data_ptr() : nullptr};
 }
 
 void PageRankPlan::step() {
@@ -1200,21 +1218,58 @@ void PageRankPlan::step() {
 
 int PageRankPlan::run(int maxiter, double tol) {
   if (tol <= 0 && maxiter >= 2 && graph_ok()) {
-    const std::vector<const void*> key = {r_.data_ptr(), rn_.data_ptr(), c_.data_ptr(), stats_.data_ptr(),
-                                          send_.data_ptr(), part_.data_ptr()};
-    if (!gexec_ || key != gkey_) graph_build();
+    int eager = 0;
+    if (dist_dev_) {
+      // the captured pair has the exchange ring on: the first iteration after
+      // reset() runs eagerly (c is fresh), and eager iterations come first
+      // until RCCL's peer connections exist (they are made on first use,
+      // which capture does not allow)
+      const int need = dist_warm_ ? 0 : 2;
+      while (eager < maxiter && (c_fresh_ || eager < need)) {
+        step();
+        ++eager;
+      }
+      dist_warm_ = true;
+      if (maxiter - eager < 2) {
+        for (; eager < maxiter; ++eager) step();
+        return maxiter;
+      }
+    }
+    const int todo = maxiter - eager;
+    if (!gexec_ || graph_key() != gkey_) {
+      bool built = true;
+      try {
+        graph_build();
+      } catch (const std::exception&) {
+        if (!dist_dev_) throw;
+        graph_free();
+        built = false;
+      }
+      if (dist_dev_) {
+        // every rank replays or none does: a rank whose capture failed would
+        // leave its peers' captured rounds without a partner
+        at::Tensor f = at::full({1}, built ? 1 : 0, opt(dev, at::kInt));
+        comm->allreduce_tensor(f, Comm::MIN);
+        if (f.item<int>() == 0) {
+          graph_free();
+          dist_graph_failed_ = true;
+          for (; eager < maxiter; ++eager) step();
+          return maxiter;
+        }
+      }
+    }
     const hipStream_t cs = at::hip::getCurrentHIPStream();
     auto chk = [](hipError_t e, const char* what) {
       if (e != hipSuccess) throw std::runtime_error(std::string("PageRank graph: ") + what + ": " + hipGetErrorString(e));
     };
     chk(hipEventRecord(gev_[0], cs), "hipEventRecord");
     chk(hipStreamWaitEvent(gstream_, gev_[0], 0), "hipStreamWaitEvent");
-    for (int p = 0; p < maxiter / 2; ++p) chk(hipGraphLaunch(gexec_, gstream_), "hipGraphLaunch");
+    for (int p = 0; p < todo / 2; ++p) chk(hipGraphLaunch(gexec_, gstream_), "hipGraphLaunch");
     chk(hipEventRecord(gev_[1], gstream_), "hipEventRecord");
     chk(hipStreamWaitEvent(cs, gev_[1], 0), "hipStreamWaitEvent");
-    graph_iters_ += 2 * (maxiter / 2);
+    graph_iters_ += 2 * (todo / 2);
     dmass_ = stats_.narrow(0, 1, 1);  // r_ holds the latest ranks after every pair
-    if (maxiter % 2) step();
+    if (todo % 2) step();
     return maxiter;
   }
   int it = 0;

@@ -156,6 +156,8 @@ class PageRankPlan {
   std::vector<int64_t> chunk_b_;
   at::Tensor srcp_;
   bool c_fresh_ = true;  // cfull_ holds every rank's slice of the last tile step
+  bool dist_warm_ = false, dist_graph_failed_ = false;  // eager exchange rounds ran (RCCL connections exist)
+  std::vector<const void*> graph_key() const;
   hipStream_t side_ = nullptr;
   std::vector<hipEvent_t> ring_ev_;
   void build_pieces(const std::vector<int>& piece_nr);

@@ -289,10 +289,25 @@ std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev
     const HostOff bh = host_off(B.kv);
     clk("partition");
     int64_t s = 0;
-    for (int d = 0; d < M; ++d) {
-      const int64_t e = s + B.count[d];
-      if (e > s) parts[d].add(kv_slice(B.kv, s, e, bh.kp(), bh.vp()), cuda ? drain->stream() : nullptr);
-      s = e;
+    if (cuda && B.kv.kfixed() && B.kv.vfixed() && B.kv.device().is_cuda() &&
+        (parts[0].host_room() < 0 || parts[0].host_room() >= B.kv.nbytes())) {
+      // the whole partitioned chunk drains in one copy per column; each
+      // partition's piece is a view of the pinned buffer (fixed widths: no
+      // offsets to rebase before the copy lands); the buffer is freed with
+      // the last partition viewing it
+      KV hk;
+      const std::shared_ptr<DrainEvent> ev = drain_to_pinned(B.kv, drain->stream(), &hk);
+      for (int d = 0; d < M; ++d) {
+        const int64_t e = s + B.count[d];
+        if (e > s) parts[d].add_drained(kv_slice(hk, s, e, nullptr, nullptr), ev);
+        s = e;
+      }
+    } else {
+      for (int d = 0; d < M; ++d) {
+        const int64_t e = s + B.count[d];
+        if (e > s) parts[d].add(kv_slice(B.kv, s, e, bh.kp(), bh.vp()), cuda ? drain->stream() : nullptr);
+        s = e;
+      }
     }
     clk("spool add");
     if (st) {
@@ -564,6 +579,15 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
   clk("partition pass");
   std::vector<KMV> out;
   int64_t used = 0;
+  // on a GPU the pass is a pipeline: partition d+1 uploads on one side stream
+  // while d converts, and d's result drains to pinned memory on another
+  const bool pipe = dev.is_cuda();
+  c10::optional<c10::hip::HIPStream> ups, dns;
+  if (pipe) {
+    ups = c10::hip::getStreamFromPool(false, dev.index());
+    dns = c10::hip::getStreamFromPool(false, dev.index());
+  }
+  std::vector<std::shared_ptr<DrainEvent>> drains;
   // in_file: a hot key whose values one_key_kmv already put in a file
   auto keep = [&](KMV&& m, bool in_file) {
     const int64_t b = m.nbytes();
@@ -571,7 +595,24 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
     if (env.host < 0 || used + b <= env.host || in_file) {
       // pinned results while the host budget lasts (a file-backed hot key
       // stays where it is)
-      out.push_back(on_host ? m : kmv_host(m));
+      if (on_host) {
+        out.push_back(m);
+      } else if (pipe) {
+        const hipStream_t c = dns->stream();
+        fence_after_current(c);
+        KMV h = m;
+        h.keys.kdata = drain_tensor(m.keys.kdata, c);
+        h.keys.vdata = drain_tensor(m.keys.vdata, c);
+        h.keys.koff = drain_tensor(m.keys.koff, c);
+        h.keys.voff = drain_tensor(m.keys.voff, c);
+        h.vdata = drain_tensor(m.vdata, c);
+        h.voff = drain_tensor(m.voff, c);
+        h.seg = drain_tensor(m.seg, c);
+        drains.push_back(record_event(c));
+        out.push_back(h);
+      } else {
+        out.push_back(kmv_host(m));
+      }
       if (!in_file) used += b;
     } else {  // the disk tier: one file per partition result
       out.push_back(kmv_to_file({m}, spool_path(env.dir, "kmv", env.instance, env.rank)));
@@ -581,21 +622,62 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
       }
     }
   };
+  auto fits = [&](int d) { return !parts[d].empty() && parts[d].bytes() * 4 <= budget; };
+  // partition d's pieces straight into one device KV (no host concat); on
+  // the upload stream when pipelined (the pool orders the new blocks there)
+  auto upload = [&](int d, std::shared_ptr<DrainEvent>* ev) {
+    if (!pipe) return concat_upload(parts[d].take(), dev);
+    KV p;
+    {
+      c10::hip::HIPStreamGuard g(*ups);
+      p = concat_upload(parts[d].take(), dev);
+    }
+    *ev = record_event(ups->stream());
+    return p;
+  };
+  int pre_d = -1;
+  KV pre;
+  std::shared_ptr<DrainEvent> pre_ev;
   for (int d = 0; d < M; ++d) {
     if (parts[d].empty()) continue;
-    if (parts[d].bytes() * 4 > budget) {  // over budget: a hot key (or a few)
+    if (!fits(d)) {  // over budget: a hot key (or a few)
       ooc_convert_big(parts[d].take(), env, dev, st, 1, keep);
       continue;
     }
-    // the partition's pieces straight into one device KV (no host concat)
-    KV p = concat_upload(parts[d].take(), dev);
+    KV p;
+    std::shared_ptr<DrainEvent> ev;
+    if (pre_d == d) {
+      p = std::move(pre);
+      ev = std::move(pre_ev);
+      pre = KV();
+      pre_d = -1;
+    } else {
+      p = upload(d, &ev);
+    }
+    if (ev) {  // the current stream reads what the upload stream wrote
+      const hipStream_t cs = at::hip::getCurrentHIPStream().stream();
+      if (hipStreamWaitEvent(cs, ev->e, 0) != hipSuccess) throw std::runtime_error("ooc: upload wait");
+      for (const at::Tensor* t : {&p.kdata, &p.vdata, &p.koff, &p.voff})
+        if (t->defined() && t->is_cuda())
+          c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), at::hip::getCurrentHIPStream());
+    }
     clk("to device");
+    int n = d + 1;
+    while (n < M && parts[n].empty()) ++n;
+    if (pipe && n < M && fits(n)) {
+      pre = upload(n, &pre_ev);
+      pre_d = n;
+    }
+    clk("prefetch");
     KMV m = convert(p);
     p = KV();
     clk("convert");
     keep(std::move(m), false);
     clk("result to host");
   }
+  for (const auto& e : drains)
+    if (hipEventSynchronize(e->e) != hipSuccess) throw std::runtime_error("ooc: result drain failed");
+  clk("drain sync");
   if (out.empty()) out.push_back(kmv_concat_host(out, kv));  // an empty KMV of the KV's widths
   return out;
 }

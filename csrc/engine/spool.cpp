@@ -39,12 +39,22 @@ struct Mapping {
   size_t len = 0;
   std::string path;
   int fd = -1;  // open while the file is being written (pwrite, not through the mapping)
+  // the data is in the page cache now: map it again in place (same address,
+  // so every view stays valid) with MAP_POPULATE — the page tables are
+  // filled in one pass here (a background writer's thread, for async
+  // pieces) instead of by a fault per 4 KiB page when the piece is read
   void done_writing() {
-    if (fd >= 0) ::close(fd);
+    if (fd >= 0) {
+      void* q = p && len ? ::mmap(p, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED | MAP_POPULATE, fd, 0) : p;
+      const int e = errno;
+      ::close(fd);
+      fd = -1;
+      if (q == MAP_FAILED) fail("cannot map " + path + " again: " + std::strerror(e));
+    }
     fd = -1;
   }
   ~Mapping() {
-    done_writing();
+    if (fd >= 0) ::close(fd);
     if (p && len) munmap(p, len);
     if (!path.empty()) {
       ::unlink(path.c_str());
@@ -353,16 +363,69 @@ void Spool::sync() {
   }
   writing_.clear();
   if (err) std::rethrow_exception(err);
-  for (hipEvent_t e : pending_) {
-    const hipError_t r = hipEventSynchronize(e);
-    (void)hipEventDestroy(e);
+  for (const auto& ev : pending_) {
+    const hipError_t r = hipEventSynchronize(ev->e);
     if (r != hipSuccess) {
-      for (hipEvent_t x : pending_) (void)hipEventQuery(x);
       pending_.clear();
       fail(std::string("asynchronous drain failed: ") + hipGetErrorString(r));
     }
   }
   pending_.clear();
+}
+
+void fence_after_current(hipStream_t copy) {
+  hipStream_t cs = at::hip::getCurrentHIPStream().stream();
+  hipEvent_t fence;
+  if (hipEventCreateWithFlags(&fence, hipEventDisableTiming) != hipSuccess || hipEventRecord(fence, cs) != hipSuccess ||
+      hipStreamWaitEvent(copy, fence, 0) != hipSuccess)
+    fail("drain fence failed");
+  (void)hipEventDestroy(fence);
+}
+
+at::Tensor drain_tensor(const at::Tensor& t, hipStream_t copy) {
+  if (!t.defined() || t.is_cpu()) return t;
+  at::Tensor src = t.contiguous();
+  at::Tensor o = at::empty(src.sizes(), src.options().device(at::kCPU).pinned_memory(true));
+  note_xfer(src, at::Device(at::kCPU));
+  const size_t nb = (size_t)src.numel() * src.element_size();
+  if (nb && hipMemcpyAsync(o.data_ptr(), src.data_ptr(), nb, hipMemcpyDeviceToHost, copy) != hipSuccess)
+    fail("asynchronous drain copy failed");
+  c10::hip::HIPCachingAllocator::recordStream(src.storage().data_ptr(),
+                                             c10::hip::getStreamFromExternal(copy, src.device().index()));
+  return o;
+}
+
+std::shared_ptr<DrainEvent> record_event(hipStream_t s) {
+  auto ev = std::make_shared<DrainEvent>();
+  if (hipEventCreateWithFlags(&ev->e, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev->e, s) != hipSuccess)
+    fail("drain event failed");
+  return ev;
+}
+
+std::shared_ptr<DrainEvent> drain_to_pinned(const KV& dev_kv, hipStream_t copy, KV* host_out) {
+  fence_after_current(copy);
+  KV o = dev_kv;
+  o.kdata = drain_tensor(dev_kv.kdata, copy);
+  o.vdata = drain_tensor(dev_kv.vdata, copy);
+  o.koff = drain_tensor(dev_kv.koff, copy);
+  o.voff = drain_tensor(dev_kv.voff, copy);
+  *host_out = o;
+  return record_event(copy);
+}
+
+void Spool::add_drained(const KV& piece, const std::shared_ptr<DrainEvent>& ev) {
+  if (piece.n == 0) return;
+  const int64_t b = piece.nbytes();
+  SpoolBudget& B = *cfg_.budget;
+  if (B.host >= 0) B.host -= b;
+  st_.host_bytes += b;
+  pieces_.push_back(piece);
+  tier_.push_back(1);
+  pending_.push_back(ev);
+  n_ += piece.n;
+  bytes_ += b;
+  st_.pieces++;
+  totals().pieces++;
 }
 
 std::string Spool::next_path() const { return spool_path(cfg_.dir, cfg_.kind, cfg_.instance, cfg_.rank); }
@@ -389,79 +452,34 @@ void Spool::add(const KV& piece, hipStream_t copy) {
   } else if (B.host < 0 || B.host >= b) {
     // the host tier (pinned when a GPU will read it back); a device piece
     // with a copy stream drains asynchronously behind the current stream
-    const bool async = copy && cuda && piece.device().is_cuda();
-    hipStream_t cs = async ? at::hip::getCurrentHIPStream().stream() : nullptr;
-    if (async) {
-      hipEvent_t e;
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess || hipEventRecord(e, cs) != hipSuccess ||
-          hipStreamWaitEvent(copy, e, 0) != hipSuccess)
-        fail("drain fence failed");
-      (void)hipEventDestroy(e);
-    }
-    auto h = [&](const at::Tensor& t) {
-      if (!t.defined()) return t;
-      if (t.is_cpu() && (!cuda || t.is_pinned())) return t;
-      at::Tensor o = at::empty(t.sizes(), t.options().device(at::kCPU).pinned_memory(cuda));
-      note_xfer(t, at::Device(at::kCPU));
-      if (async) {
-        at::Tensor src = t.contiguous();
-        const size_t nb = (size_t)src.numel() * src.element_size();
-        if (nb && hipMemcpyAsync(o.data_ptr(), src.data_ptr(), nb, hipMemcpyDeviceToHost, copy) != hipSuccess)
-          fail("asynchronous drain copy failed");
-        // the device source must outlive the copy on `copy`
-        c10::hip::HIPCachingAllocator::recordStream(src.storage().data_ptr(),
-                                                   c10::hip::getStreamFromExternal(copy, dev_.index()));
-      } else {
+    if (copy && cuda && piece.device().is_cuda()) {
+      pending_.push_back(drain_to_pinned(piece, copy, &p));
+    } else {
+      auto h = [&](const at::Tensor& t) {
+        if (!t.defined()) return t;
+        if (t.is_cpu() && (!cuda || t.is_pinned())) return t;
+        at::Tensor o = at::empty(t.sizes(), t.options().device(at::kCPU).pinned_memory(cuda));
+        note_xfer(t, at::Device(at::kCPU));
         o.copy_(t);
-      }
-      return o;
-    };
-    p = piece;
-    p.kdata = h(piece.kdata);
-    p.vdata = h(piece.vdata);
-    p.koff = h(piece.koff);
-    p.voff = h(piece.voff);
+        return o;
+      };
+      p = piece;
+      p.kdata = h(piece.kdata);
+      p.vdata = h(piece.vdata);
+      p.koff = h(piece.koff);
+      p.voff = h(piece.voff);
+    }
     if (B.host >= 0) B.host -= b;
     tier = 1;
     st_.host_bytes += b;
-    if (async) {
-      hipEvent_t done;
-      if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess || hipEventRecord(done, copy) != hipSuccess)
-        fail("drain event failed");
-      pending_.push_back(done);
-    }
   } else if (copy && cuda && piece.device().is_cuda()) {
     // the disk tier off the caller's path: drain into pinned memory on the
     // copy stream, then a background thread writes and maps the file
-    hipStream_t cs = at::hip::getCurrentHIPStream().stream();
-    hipEvent_t fence, done;
-    if (hipEventCreateWithFlags(&fence, hipEventDisableTiming) != hipSuccess || hipEventRecord(fence, cs) != hipSuccess ||
-        hipStreamWaitEvent(copy, fence, 0) != hipSuccess)
-      fail("drain fence failed");
-    (void)hipEventDestroy(fence);
-    auto h = [&](const at::Tensor& t) {
-      if (!t.defined()) return t;
-      at::Tensor src = t.contiguous();
-      at::Tensor o = at::empty(src.sizes(), src.options().device(at::kCPU).pinned_memory(true));
-      note_xfer(src, at::Device(at::kCPU));
-      const size_t nb = (size_t)src.numel() * src.element_size();
-      if (nb && hipMemcpyAsync(o.data_ptr(), src.data_ptr(), nb, hipMemcpyDeviceToHost, copy) != hipSuccess)
-        fail("asynchronous drain copy failed");
-      c10::hip::HIPCachingAllocator::recordStream(src.storage().data_ptr(),
-                                                 c10::hip::getStreamFromExternal(copy, dev_.index()));
-      return o;
-    };
-    KV hp = piece;
-    hp.kdata = h(piece.kdata);
-    hp.vdata = h(piece.vdata);
-    hp.koff = h(piece.koff);
-    hp.voff = h(piece.voff);
-    if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess || hipEventRecord(done, copy) != hipSuccess)
-      fail("drain event failed");
+    KV hp;
+    std::shared_ptr<DrainEvent> done = drain_to_pinned(piece, copy, &hp);
     const std::string path = next_path();
     writing_.emplace_back(pieces_.size(), std::async(std::launch::async, [hp, done, path]() {
-                            const hipError_t r = hipEventSynchronize(done);
-                            (void)hipEventDestroy(done);
+                            const hipError_t r = hipEventSynchronize(done->e);
                             if (r != hipSuccess) fail(std::string("asynchronous drain failed: ") + hipGetErrorString(r));
                             return kv_to_file({hp}, path);
                           }));

@@ -61,6 +61,25 @@ struct SpoolStats {
 SpoolStats& spool_totals();
 int64_t spool_files_live();
 
+// a device->host drain's completion event, shared by every spool holding a
+// piece of the drained buffer (destroyed with the last holder)
+struct DrainEvent {
+  hipEvent_t e = nullptr;
+  ~DrainEvent() {
+    if (e) (void)hipEventDestroy(e);
+  }
+};
+// the device KV `dev_kv` copied into one pinned host KV on stream `copy`,
+// ordered after the work queued so far on the current stream; the returned
+// event completes with the copy
+std::shared_ptr<DrainEvent> drain_to_pinned(const KV& dev_kv, hipStream_t copy, KV* host_out);
+// building blocks of asynchronous drains: `copy` waits for the work queued so
+// far on the current stream; `t` (device) copied into new pinned memory on
+// `copy` (the source kept alive until the copy ran); an event recorded on `s`
+void fence_after_current(hipStream_t copy);
+at::Tensor drain_tensor(const at::Tensor& t, hipStream_t copy);
+std::shared_ptr<DrainEvent> record_event(hipStream_t s);
+
 class Spool {
  public:
   Spool(at::Device dev, SpoolConfig cfg);
@@ -76,6 +95,11 @@ class Spool {
   // pinned memory that a background thread writes to its file; every read of
   // the spool waits for the drains and writes first.
   void add(const KV& piece, hipStream_t copy = nullptr);
+  // a piece of a host buffer still being drained (drain_to_pinned): host
+  // tier, counted against the host budget, readable once `ev` completes
+  void add_drained(const KV& host_piece, const std::shared_ptr<DrainEvent>& ev);
+  // host budget bytes left to the spools sharing this one's budget (< 0: unlimited)
+  int64_t host_room() const { return cfg_.budget->host; }
   // wait for the asynchronous drains
   void sync();
   int64_t n() const { return n_; }
@@ -105,7 +129,7 @@ class Spool {
   SpoolConfig cfg_;
   std::vector<KV> pieces_;
   std::vector<int> tier_;  // 0 HBM, 1 pinned host, 2 disk
-  std::vector<hipEvent_t> pending_;
+  std::vector<std::shared_ptr<DrainEvent>> pending_;
   // disk-tier pieces being written by a background thread (index into
   // pieces_, the file-backed KV): the device piece drained into pinned
   // memory on the copy stream, then written and mapped off the caller's path

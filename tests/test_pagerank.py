@@ -187,6 +187,7 @@ ids, r = pr.ranks()
 out = np.zeros(1 << 18, dtype=np.float32)
 out[ids.cpu().numpy()] = r.cpu().numpy()
 np.save(sys.argv[1], out)
+print(pr.graph_iterations)
 print(pr.layout, pr.xcd_ranges, comm.native.transport)
 """
 
@@ -266,13 +267,16 @@ def test_pagerank_forced_rccl_overlapped_pieces_match_local(tmp_path):
     plan's source chunks (their own XCD ranges, segment indexes and source
     streams), the side-stream exchange rounds (no peers at one rank) and
     their events — the ranks of 27 iterations (a 20-run after reset, then a
-    7-run) equal the local plan's to float32 accumulation differences"""
+    7-run) equal the local plan's to float32 accumulation differences. The
+    distributed iteration replays as a HIP graph (side stream, RCCL stream and
+    events captured) bit for bit like its eager run (MRH_PR_DIST_GRAPH=0)"""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res, info = {}, {}
-    for name, extra in (("local", {}), ("pieces", {"MRH_FORCE_RCCL": "1", "MRH_PR_OVERLAP": "2"})):
+    forced = {"MRH_FORCE_RCCL": "1", "MRH_PR_OVERLAP": "2"}
+    for name, extra in (("local", {}), ("pieces", forced), ("eager", dict(forced, MRH_PR_DIST_GRAPH="0"))):
         env = dict(os.environ, PYTHONPATH=root, **extra)
         if name == "local":
             env.pop("MRH_FORCE_RCCL", None)
@@ -281,8 +285,11 @@ def test_pagerank_forced_rccl_overlapped_pieces_match_local(tmp_path):
         p = subprocess.run([sys.executable, "-c", FORCED_CHILD, path], env=env, cwd=root, capture_output=True,
                            text=True, timeout=240)
         assert p.returncode == 0, p.stderr[-3000:]
-        info[name] = p.stdout.split()[-3:]
+        info[name] = p.stdout.split()[-4:]
         res[name] = np.load(path)
-    assert info["pieces"][0] == "replicated" and info["pieces"][2] == "rccl", info
-    assert int(info["pieces"][1]) > 9, info  # several chunks' ranges
+    assert info["pieces"][1] == "replicated" and info["pieces"][3] == "rccl", info
+    assert int(info["pieces"][2]) > 9, info  # several chunks' ranges
+    # 20-run: 2 eager (fresh c, RCCL connections), 18 replayed; 7-run: 1 + 6
+    assert int(info["pieces"][0]) == 24 and int(info["eager"][0]) == 0, info
     np.testing.assert_allclose(res["pieces"], res["local"], rtol=1e-4, atol=1e-10)
+    assert np.array_equal(res["pieces"], res["eager"])
