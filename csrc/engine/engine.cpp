@@ -250,7 +250,7 @@ KMV kmv_concat(const std::vector<KMV>& parts, at::Device dev, bool pin) {
   return out;
 }
 
-KV concat_upload(const std::vector<KV>& parts_in, at::Device dev) {
+KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at::Tensor>* hold) {
   std::vector<KV> parts;
   for (const KV& p : parts_in)
     if (p.n > 0) parts.push_back(p);
@@ -270,15 +270,30 @@ KV concat_upload(const std::vector<KV>& parts_in, at::Device dev) {
     *data_out = at::empty({bytes}, opt(dev, at::kByte));
     if (!fixed) *off_out = at::empty({rows + 1}, opt(dev, at::kLong));
     int64_t b = 0, r = 0;
+    const hipStream_t cs = at::hip::getCurrentHIPStream().stream();
+    // a pinned source goes by one hipMemcpyAsync with the caller holding it
+    // until the stream passed the copy (`hold`): ATen's copy_ costs ~50 us of
+    // host time per call (checks, a host-allocator event), which at a few
+    // dozen pieces per partition was the out-of-core pass's critical path
+    auto put = [&](const at::Tensor& dst, const at::Tensor& src) {
+      if (hold && src.is_cpu() && src.is_contiguous() && src.is_pinned()) {
+        const size_t nb = (size_t)src.numel() * src.element_size();
+        if (hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nb, hipMemcpyHostToDevice, cs) != hipSuccess)
+          throw std::runtime_error("mrhip: host to device copy failed");
+        hold->push_back(src);
+      } else {
+        dst.copy_(src, /*non_blocking=*/true);
+      }
+    };
     for (const KV& p : parts) {
       const at::Tensor& d = data_of(p);
       note_xfer(d, dev);
-      if (d.numel()) data_out->narrow(0, b, d.numel()).copy_(d, /*non_blocking=*/true);
+      if (d.numel()) put(data_out->narrow(0, b, d.numel()), d);
       if (!fixed) {
         at::Tensor o = off_of(p).narrow(0, 0, p.n);
         note_xfer(o, dev);
         at::Tensor dst = off_out->narrow(0, r, p.n);
-        dst.copy_(o, /*non_blocking=*/true);
+        put(dst, o);
         if (b) dst.add_(b);
       }
       b += d.numel();

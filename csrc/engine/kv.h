@@ -63,7 +63,10 @@ KV concat(const std::vector<KV>& parts, at::Device dev, bool pin = false);
 KMV kmv_concat(const std::vector<KMV>& parts, at::Device dev, bool pin = false);
 // the parts copied host -> device straight into one device KV (no host
 // concatenation; fixed widths and offsets alike)
-KV concat_upload(const std::vector<KV>& parts, at::Device dev);
+// (hold set: pinned sources are copied by hipMemcpyAsync on the current
+// stream and appended to *hold, which the caller keeps until the stream passed
+// the copies)
+KV concat_upload(const std::vector<KV>& parts, at::Device dev, std::vector<at::Tensor>* hold = nullptr);
 KV to_var_keys(const KV& kv);
 KV to_var_values(const KV& kv);
 // offsets of a fixed-width column: [0, w, 2w, ...]

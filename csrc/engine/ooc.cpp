@@ -315,8 +315,9 @@ std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev
       st->bytes_staged += row_bytes(kvs[ch[i].part], h[ch[i].part], ch[i].a, ch[i].b);
     }
   }
-  for (auto& p : parts) p.sync();
-  clk("drain sync");
+  // no sync here: each spool waits for its own drains and background file
+  // writes when it is read (take / gather), so the last chunks' disk writes
+  // overlap the first partitions' work
   if (st)
     for (auto& p : parts) {
       st->files += p.stats().files;
@@ -625,22 +626,30 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
   auto fits = [&](int d) { return !parts[d].empty() && parts[d].bytes() * 4 <= budget; };
   // partition d's pieces straight into one device KV (no host concat); on
   // the upload stream when pipelined (the pool orders the new blocks there)
+  // pinned pieces of an upload, held until its event passed
+  std::vector<std::pair<std::shared_ptr<DrainEvent>, std::vector<at::Tensor>>> held;
   auto upload = [&](int d, std::shared_ptr<DrainEvent>* ev) {
     if (!pipe) return concat_upload(parts[d].take(), dev);
+    for (size_t i = 0; i < held.size();)  // release the sources of finished uploads
+      if (hipEventQuery(held[i].first->e) == hipSuccess) held.erase(held.begin() + (long)i);
+      else ++i;
     KV p;
+    std::vector<at::Tensor> hold;
     {
       c10::hip::HIPStreamGuard g(*ups);
-      p = concat_upload(parts[d].take(), dev);
+      p = concat_upload(parts[d].take(), dev, &hold);
     }
     *ev = record_event(ups->stream());
+    held.emplace_back(*ev, std::move(hold));
     return p;
   };
   int pre_d = -1;
   KV pre;
   std::shared_ptr<DrainEvent> pre_ev;
   for (int d = 0; d < M; ++d) {
-    if (parts[d].empty()) continue;
-    if (!fits(d)) {  // over budget: a hot key (or a few)
+    // (a prefetched partition's spool is already empty: its pieces are in pre)
+    if (pre_d != d && parts[d].empty()) continue;
+    if (pre_d != d && !fits(d)) {  // over budget: a hot key (or a few)
       ooc_convert_big(parts[d].take(), env, dev, st, 1, keep);
       continue;
     }
@@ -664,7 +673,7 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
     clk("to device");
     int n = d + 1;
     while (n < M && parts[n].empty()) ++n;
-    if (pipe && n < M && fits(n)) {
+    if (n < M && fits(n)) {  // (on the CPU too: the same bookkeeping, no streams)
       pre = upload(n, &pre_ev);
       pre_d = n;
     }
@@ -677,6 +686,8 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
   }
   for (const auto& e : drains)
     if (hipEventSynchronize(e->e) != hipSuccess) throw std::runtime_error("ooc: result drain failed");
+  for (const auto& h : held)
+    if (hipEventSynchronize(h.first->e) != hipSuccess) throw std::runtime_error("ooc: upload failed");
   clk("drain sync");
   if (out.empty()) out.push_back(kmv_concat_host(out, kv));  // an empty KMV of the KV's widths
   return out;
