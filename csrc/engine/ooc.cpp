@@ -289,17 +289,22 @@ std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev
     const HostOff bh = host_off(B.kv);
     clk("partition");
     int64_t s = 0;
-    if (cuda && B.kv.kfixed() && B.kv.vfixed() && B.kv.device().is_cuda() &&
-        (parts[0].host_room() < 0 || parts[0].host_room() >= B.kv.nbytes())) {
+    if (cuda && B.kv.kfixed() && B.kv.vfixed() && B.kv.device().is_cuda()) {
       // the whole partitioned chunk drains in one copy per column; each
       // partition's piece is a view of the pinned buffer (fixed widths: no
-      // offsets to rebase before the copy lands); the buffer is freed with
-      // the last partition viewing it
+      // offsets to rebase before the copy lands), kept as the host tier or
+      // written to its file by a background thread; the buffer is freed with
+      // the last piece viewing it
       KV hk;
       const std::shared_ptr<DrainEvent> ev = drain_to_pinned(B.kv, drain->stream(), &hk);
       for (int d = 0; d < M; ++d) {
         const int64_t e = s + B.count[d];
-        if (e > s) parts[d].add_drained(kv_slice(hk, s, e, nullptr, nullptr), ev);
+        if (e > s) {
+          const KV piece = kv_slice(hk, s, e, nullptr, nullptr);
+          const int64_t room = parts[d].host_room();
+          if (room < 0 || room >= piece.nbytes()) parts[d].add_drained(piece, ev);
+          else parts[d].add_drained_to_disk(piece, ev);
+        }
         s = e;
       }
     } else {

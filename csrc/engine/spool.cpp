@@ -428,6 +428,25 @@ void Spool::add_drained(const KV& piece, const std::shared_ptr<DrainEvent>& ev) 
   totals().pieces++;
 }
 
+void Spool::add_drained_to_disk(const KV& piece, const std::shared_ptr<DrainEvent>& ev) {
+  if (piece.n == 0) return;
+  const int64_t b = piece.nbytes();
+  const std::string path = next_path();
+  writing_.emplace_back(pieces_.size(), std::async(std::launch::async, [piece, ev, path]() {
+                          const hipError_t r = hipEventSynchronize(ev->e);
+                          if (r != hipSuccess) fail(std::string("asynchronous drain failed: ") + hipGetErrorString(r));
+                          return kv_to_file({piece}, path);
+                        }));
+  pieces_.push_back(KV());  // filled in by sync()
+  tier_.push_back(2);
+  st_.disk_bytes += b;
+  st_.files++;
+  n_ += piece.n;
+  bytes_ += b;
+  st_.pieces++;
+  totals().pieces++;
+}
+
 std::string Spool::next_path() const { return spool_path(cfg_.dir, cfg_.kind, cfg_.instance, cfg_.rank); }
 
 void Spool::release(const KV& piece, int tier) {

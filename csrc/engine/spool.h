@@ -98,6 +98,9 @@ class Spool {
   // a piece of a host buffer still being drained (drain_to_pinned): host
   // tier, counted against the host budget, readable once `ev` completes
   void add_drained(const KV& host_piece, const std::shared_ptr<DrainEvent>& ev);
+  // the same piece for the disk tier: a background thread waits for `ev`,
+  // then writes and maps the file (no host budget taken)
+  void add_drained_to_disk(const KV& host_piece, const std::shared_ptr<DrainEvent>& ev);
   // host budget bytes left to the spools sharing this one's budget (< 0: unlimited)
   int64_t host_room() const { return cfg_.budget->host; }
   // wait for the asynchronous drains
