@@ -8,10 +8,14 @@
 // libmrhip.so, shared with the C API (csrc/capi).
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 
+#include <csignal>
 #include <cstring>
+#include <execinfo.h>
 #include <random>
+#include <unistd.h>
 #include <string>
 
 #include "kv.h"
@@ -132,7 +136,25 @@ CompareFn py_cmp(py::object c) {
 
 }  // namespace
 
+namespace {
+// MRH_SEGV_TRACE=1: a host segfault prints the native call stack to stderr
+// before the default action (Python's faulthandler shows only Python frames)
+void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "mrhip: native stack at the fault:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  std::signal(sig, SIG_DFL);
+  std::raise(sig);
+}
+}  // namespace
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  if (const char* v = std::getenv("MRH_SEGV_TRACE"); v && *v == '1') {
+    std::signal(SIGSEGV, segv_trace);
+    std::signal(SIGBUS, segv_trace);
+  }
   m.doc() = "gpu_mapreduce_amd native engine (HIP/CDNA4 kernels + ATen + c10d)";
 
   py::class_<KV>(m, "KV")
@@ -506,6 +528,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // HBM page pool (hbmpool.h): the engine's device allocator with a hard cap
   m.def("hbm_pool_install", &hbm::install);
   m.def("hbm_pool_installed", &hbm::installed);
+  // a block cached on a stream that is then destroyed (after forget_stream)
+  // must not be reached through that stream again: allocate and free blocks of
+  // one class on a private stream, retire the stream, then allocate the class
+  // from the current stream (the cross-stream reuse path) and free it
+  m.def("hbm_pool_stream_retire_check", [](int dev, int64_t bytes) {
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) throw std::runtime_error("hipStreamCreate");
+    {
+      c10::hip::HIPStreamGuard g(c10::hip::getStreamFromExternal(s, (c10::DeviceIndex)dev));
+      at::Tensor a = at::empty({bytes}, at::TensorOptions().device(at::kCUDA, dev).dtype(at::kByte));
+      a.fill_(1);
+    }
+    hbm::forget_stream(s);
+    (void)hipStreamDestroy(s);
+    at::Tensor b = at::empty({bytes}, at::TensorOptions().device(at::kCUDA, dev).dtype(at::kByte));
+    b.fill_(2);
+    return b.sum().item<int64_t>();
+  });
   m.def("hbm_pool_stats", [](int dev) {
     const hbm::PoolStats s = hbm::stats(dev);
     py::dict d;

@@ -1,5 +1,6 @@
 // Native graph engines (see graphplan.h).
 #include "graphplan.h"
+#include "hbmpool.h"
 
 #include <algorithm>
 #include <cmath>
@@ -769,7 +770,10 @@ void PageRankPlan::ring_free() {
   for (auto& e : ring_ev_)
     if (e) (void)hipEventDestroy(e);
   ring_ev_.clear();
-  if (side_) (void)hipStreamDestroy(side_);
+  if (side_) {
+    hbm::forget_stream(side_);  // the pg transport allocates on it
+    (void)hipStreamDestroy(side_);
+  }
   side_ = nullptr;
 }
 
@@ -1095,7 +1099,10 @@ void PageRankPlan::graph_free() {
     if (e) (void)hipEventDestroy(e);
     e = nullptr;
   }
-  if (gstream_) (void)hipStreamDestroy(gstream_);
+  if (gstream_) {
+    hbm::forget_stream(gstream_);
+    (void)hipStreamDestroy(gstream_);
+  }
   gstream_ = nullptr;
   gkey_.clear();
 }

@@ -586,6 +586,32 @@ void pool_free(void* ptr, size_t /*size*/, int /*dev*/, hipStream_t /*stream*/) 
   d.pending.push_back(std::move(q));
 }
 
+void forget_stream_locked(hipStream_t s) {  // g_mu held
+  if (!s) return;
+  for (Dev& d : g_dev) {
+    for (auto it = d.free.begin(); it != d.free.end();) {
+      if (it->first.first != s) {
+        ++it;
+        continue;
+      }
+      for (void* p : it->second) {
+        if (hipFreeAsync(p, s) != hipSuccess) (void)hipGetLastError();
+        d.cached -= it->first.second;
+      }
+      it = d.free.erase(it);
+    }
+    d.streams.erase(std::remove(d.streams.begin(), d.streams.end(), s), d.streams.end());
+    for (Pending& q : d.pending) {
+      if (q.b.stream == s) q.b.stream = nullptr;
+      q.b.used_on.erase(std::remove(q.b.used_on.begin(), q.b.used_on.end(), s), q.b.used_on.end());
+    }
+  }
+  for (auto& [p, b] : g_blocks) {
+    if (b.stream == s) b.stream = nullptr;
+    b.used_on.erase(std::remove(b.used_on.begin(), b.used_on.end(), s), b.used_on.end());
+  }
+}
+
 void pool_record_stream(void* ptr, hipStream_t s) {
   std::lock_guard<std::mutex> l(g_mu);
   auto it = g_blocks.find(ptr);
@@ -714,6 +740,13 @@ OpCap::~OpCap() {
   auto it = d.op_caps.find(prev_);
   if (it != d.op_caps.end()) d.op_caps.erase(it);
   recompute_cap(d);
+}
+
+void forget_stream(hipStream_t s) {
+  if (!s) return;
+  (void)hipStreamSynchronize(s);
+  std::lock_guard<std::mutex> l(g_mu);
+  forget_stream_locked(s);
 }
 
 }  // namespace mrh::hbm

@@ -73,6 +73,12 @@ void reset_reserved_peak(int device);
 int64_t set_cap(int device, int64_t cap);
 // release cached free memory of the pool down to keep_bytes
 void trim(int device, int64_t keep_bytes);
+// a stream is about to be destroyed: its cached blocks go back to the HIP
+// pool, and live or pending blocks that name it (allocated or used on it) are
+// re-homed to the null stream, so no later allocation or free records an
+// event on, or waits with, a dead stream (the caller has synchronised it).
+// Every engine-owned stream calls this before hipStreamDestroy
+void forget_stream(hipStream_t s);
 
 // RAII: a MapReduce op's cap (in use at entry + extra bytes) while it runs;
 // concurrent ops' caps combine (the tightest is in force)

@@ -1,5 +1,6 @@
 // Native RCCL transport + peer monitor (see rccl.h).
 #include "rccl.h"
+#include "hbmpool.h"
 
 #include <chrono>
 #include <cstdio>
@@ -272,7 +273,10 @@ Rccl::~Rccl() {
     }
   }
   for (auto& e : ev_) (void)hipEventDestroy(e);
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (stream_) {
+    if (!aborted_) hbm::forget_stream(stream_);
+    (void)hipStreamDestroy(stream_);
+  }
 }
 
 void Rccl::fence_in(hipStream_t s) {

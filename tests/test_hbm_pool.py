@@ -213,3 +213,25 @@ def test_pool_big_block_arena_gpu():
     after use on another stream is handed out behind that stream's work;
     reserved stays within 1.5x of the bytes in use; trim returns segments"""
     assert _child(ARENA).startswith("ok")
+
+
+@pytest.mark.gpu
+def test_pool_retired_stream_is_forgotten():
+    """Blocks cached on an engine stream that is destroyed (a PageRank plan's
+    exchange stream, an RCCL communicator's stream) are released by
+    forget_stream first: a later allocation of the same class from another
+    stream must not record an event on the dead stream (that was a segfault
+    inside the HIP runtime at 2 ranks, bench.py --gpus 2 on one GPU)"""
+    assert _child(RETIRE).startswith("ok")
+
+
+RETIRE = r"""
+import torch
+import gpu_mapreduce_amd as g
+from gpu_mapreduce_amd.runtime import hbm_pool
+assert hbm_pool.installed()
+n = 3 << 20
+for _ in range(3):
+    assert g._ext.C.hbm_pool_stream_retire_check(0, n) == 2 * n
+print("ok")
+"""
