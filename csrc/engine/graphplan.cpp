@@ -1110,19 +1110,24 @@ void PageRankPlan::graph_free() {
 // graph replay: the XCD tile-step path, a fixed iteration count, no
 // serialising diagnostic mode. One GPU; or the replicated multi-GPU plan over
 // the native RCCL communicator, whose exchange rounds (side_), allreduce and
-// the RCCL stream join the capture through their events
-// (MRH_PR_DIST_GRAPH=0 keeps the multi-GPU iteration eager)
+// the RCCL stream join the capture through their events. MRH_PR_DIST_GRAPH:
+// 0 = the multi-GPU iteration stays eager, 1 = replay at any P; unset =
+// replay on a one-rank communicator only (validated on the 1-GPU box; a
+// multi-rank capture of RCCL peers has not run on an 8-GPU node yet)
 bool PageRankPlan::graph_ok() const {
   static const bool sync = [] {
     const char* v = std::getenv("MRH_SYNC");
     return v && *v && *v != '0';
   }();
-  static const bool dist_graph = [] {
+  static const int dist_graph = [] {
     const char* v = std::getenv("MRH_PR_DIST_GRAPH");
-    return !(v && *v == '0');
+    return v && *v ? std::atoi(v) : -1;
   }();
   if (!use_graph || sync || !dev.is_cuda() || pb_ || xr_ <= 0 || send_.numel() == 0) return false;
-  if (dist_dev_) return dist_graph && !dist_graph_failed_ && comm->uses_rccl() && !pieces_.empty();
+  if (dist_dev_) {
+    const bool on = dist_graph > 0 || (dist_graph < 0 && P == 1);
+    return on && !dist_graph_failed_ && comm->uses_rccl() && !pieces_.empty();
+  }
   return !comm->distributed() && six_.defined();
 }
 
