@@ -23,6 +23,9 @@ scale = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 ooc = len(sys.argv) > 2 and sys.argv[2] == "ooc"
 hbm = (int(sys.argv[3]) if len(sys.argv) > 3 else 256) << 20
 host = (int(sys.argv[4]) if len(sys.argv) > 4 else 2048) << 20
+if os.environ.get("NUMA") == "1":  # bind like bench.py's ranks (parallel/comm.py bind_numa_local)
+    from gpu_mapreduce_amd.parallel.comm import bind_numa_local
+    print("numa cpus", bind_numa_local(0), "of", len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else "?")
 comm = g.Comm(device=os.environ.get("DEV", "cuda:0"))
 kv = C.map_rmat((1 << scale) * 16, scale, *GRAPH500, 0.0, 1, 0, comm.device)
 e = kv.kdata.view(torch.int64).view(-1, 2)
