@@ -170,26 +170,6 @@ def bench_trifind_mr(comm, args):
         "wedge_pairs": max((s["pairs_out"] for s in r["stages"] if s["op"] == "reduce nsq_angles"), default=0),
         "compact_vb": int(r.get("compact_vb", 0)),
     }
-    bscale = getattr(args, "mr_big_scale", 0) or 0
-    if bscale > 0:
-        # a larger graph in HBM: R-MAT-22's ~7 G wedge pairs go through collate
-        # 4 as 12-byte compact pairs, grouped in hash-balanced buckets
-        eb = edges_of(bscale)
-        wantb = TriangleGraph(comm, eb, 1 << bscale).count()
-        tri_find_mr(comm, eb)  # warm: the pool holds the peak afterwards
-        sync()
-        t0 = time.perf_counter()
-        rb = tri_find_mr(comm, eb)
-        sync()
-        dtb = comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
-        out["big"] = {"scale": bscale, "ms": dtb * 1e3, "triangles": int(rb["triangles"]),
-                      "triangles_check": int(wantb), "compact_vb": int(rb.get("compact_vb", 0)),
-                      "edges": (1 << bscale) * ef,
-                      "wedge_pairs": max((s["pairs_out"] for s in rb["stages"] if s["op"] == "reduce nsq_angles"),
-                                         default=0),
-                      "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"],
-                                  "pairs_out": s["pairs_out"]} for s in rb["stages"]]}
-        del eb
     oscale = getattr(args, "mr_ooc_scale", 0) or 0
     if oscale > 0:
         root = tempfile.mkdtemp(prefix=f"mrh_trimr_{me}_")
@@ -210,7 +190,10 @@ def bench_trifind_mr(comm, args):
                 sync()
                 dts.append(comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64))
             dt2 = dts[-1]
-            out["ooc"] = {"scale": oscale, "ms": dt2 * 1e3, "ms_cold": dts[0] * 1e3, "triangles": int(r2["triangles"]),
+            out["ooc"] = {"note": "run before the in-HBM big graph: after that job (a ~180 GB peak) the same "
+                                  "out-of-core run measured 850-913 ms instead of ~587 ms on this box, with or "
+                                  "without a pool trim and an emptied pinned host cache (tools/trimr_time.py BIG=22)",
+                          "scale": oscale, "ms": dt2 * 1e3, "ms_cold": dts[0] * 1e3, "triangles": int(r2["triangles"]),
                           "triangles_check": int(want2), "hbm_budget": budget, "host_budget": host,
                           "spool_files": r2["spool_files"], "spool_host_bytes": r2["spool_host_bytes"],
                           "spool_disk_bytes": r2["spool_disk_bytes"],
@@ -225,4 +208,24 @@ def bench_trifind_mr(comm, args):
                                      for s in r2["stages"]]}
         finally:
             shutil.rmtree(root, ignore_errors=True)
+    bscale = getattr(args, "mr_big_scale", 0) or 0
+    if bscale > 0:
+        # a larger graph in HBM: R-MAT-22's ~7 G wedge pairs go through collate
+        # 4 as 12-byte compact pairs, grouped in hash-balanced buckets
+        eb = edges_of(bscale)
+        wantb = TriangleGraph(comm, eb, 1 << bscale).count()
+        tri_find_mr(comm, eb)  # warm: the pool holds the peak afterwards
+        sync()
+        t0 = time.perf_counter()
+        rb = tri_find_mr(comm, eb)
+        sync()
+        dtb = comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64)
+        out["big"] = {"scale": bscale, "ms": dtb * 1e3, "triangles": int(rb["triangles"]),
+                      "triangles_check": int(wantb), "compact_vb": int(rb.get("compact_vb", 0)),
+                      "edges": (1 << bscale) * ef,
+                      "wedge_pairs": max((s["pairs_out"] for s in rb["stages"] if s["op"] == "reduce nsq_angles"),
+                                         default=0),
+                      "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"],
+                                  "pairs_out": s["pairs_out"]} for s in rb["stages"]]}
+        del eb
     return out

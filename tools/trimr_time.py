@@ -27,7 +27,26 @@ if os.environ.get("NUMA") == "1":  # bind like bench.py's ranks (parallel/comm.p
     from gpu_mapreduce_amd.parallel.comm import bind_numa_local
     print("numa cpus", bind_numa_local(0), "of", len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else "?")
 comm = g.Comm(device=os.environ.get("DEV", "cuda:0"))
+if os.environ.get("BIG"):  # first the bench's in-HBM run at scale BIG (the pool holds its peak after it)
+    big = int(os.environ["BIG"])
+    kb = C.map_rmat((1 << big) * 16, big, *GRAPH500, 0.0, 1, 0, comm.device)
+    eb = kb.kdata.view(torch.int64).view(-1, 2)
+    for _ in range(2):
+        tri_find_mr(comm, eb)
+    del kb, eb
+    torch.cuda.synchronize()
+    from gpu_mapreduce_amd.runtime import hbm_pool
+    print("after BIG pool:", hbm_pool.stats(0), flush=True)
+    if os.environ.get("TRIM") in ("1", "2"):
+        hbm_pool.trim(0)
+        print("trimmed pool:", hbm_pool.stats(0), flush=True)
+    if os.environ.get("TRIM") == "2":  # the pinned host blocks cached by the caching host allocator too
+        torch._C._host_emptyCache()
+        print("host cache emptied", flush=True)
 kv = C.map_rmat((1 << scale) * 16, scale, *GRAPH500, 0.0, 1, 0, comm.device)
+if os.environ.get("BIG"):
+    import resource
+    print("host maxrss GB", resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, flush=True)
 e = kv.kdata.view(torch.int64).view(-1, 2)
 for rep in range(2):
     root = tempfile.mkdtemp(prefix="mrh_trimr_") if ooc else ""
