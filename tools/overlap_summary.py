@@ -85,6 +85,8 @@ def main():
     print(f"copies under kernels  {ms(length(intersect(copies, kern))):9.2f} ms  "
           f"({100 * length(intersect(copies, kern)) / max(length(copies), 1):.0f} % of the copy time)")
     print(f"H2D under D2H         {ms(length(intersect(h2d, d2h))):9.2f} ms")
+    print(f"H2D under blit copies {ms(length(intersect(h2d, blit))):9.2f} ms")
+    print(f"GPU busy (any)        {ms(length(busy)):9.2f} ms")
     print(f"idle (no kernel, no copy) {ms((w1 - w0) - length(busy)):9.2f} ms")
 
 
