@@ -214,9 +214,12 @@ KMV clone_kmv(const KMV& m) {
 at::Tensor to_host(const at::Tensor& t, bool pin) {
   if (!t.defined()) return t;
   note_xfer(t, at::Device(at::kCPU));
-  at::Tensor h = t.to(at::kCPU);
-  if (pin && t.is_cuda()) h = h.pin_memory();
-  return h;
+  if (pin && t.is_cuda()) {  // one copy, straight into pinned memory (not pageable, then pinned)
+    at::Tensor h = at::empty(t.sizes(), t.options().device(at::kCPU).pinned_memory(true));
+    h.copy_(t);
+    return h;
+  }
+  return t.to(at::kCPU);
 }
 KV kv_host(const KV& kv, bool pin) {
   KV o = kv;
