@@ -406,7 +406,7 @@ def _extra(comm, prefix, fn, args, **over):
                                     metric=r["metric"])}
     for k in ("triangles", "unique_edges", "words", "unique_words", "input_GBps", "hub_vertices", "build",
               "triangles_check", "stages", "wedge_pairs", "ooc", "ms_per_step_prefetch", "pairs",
-              "pairs_per_s_by_stage", "top10", "top10_equals_combiner", "big", "compact_vb"):
+              "pairs_per_s_by_stage", "top10", "top10_equals_combiner", "big", "compact_vb", "route", "cfg5"):
         if k in r:
             out[f"{prefix}_{k}"] = r[k]
     return out
@@ -483,14 +483,16 @@ def bench_wordfreq_files(comm, args):
         shutil.rmtree(root, ignore_errors=True)
 
 
-def _forced_rccl_comm(comm):
+def _forced_rccl_comm(comm, level="2"):
     """A one-rank communicator on this rank's GPU that runs the native RCCL
-    transport (MRH_FORCE_RCCL=1, csrc/engine/comm.h): every multi-GPU code
-    path — the exchanges, the all-gathers and allreduces of the PageRank and
-    tri_find plans — runs through a real RCCL communicator on one GPU."""
+    transport (csrc/engine/comm.h): every multi-GPU code path — the
+    exchanges, the all-gathers and allreduces of the PageRank and tri_find
+    plans — runs through a real RCCL communicator on one GPU. Level 2
+    (MRH_FORCE_RCCL=2): the collectives call ncclAllReduce / ncclAllGather /
+    ncclBroadcast too (level 1: they are the one-rank identity)."""
     from gpu_mapreduce_amd.parallel.comm import Comm
     prev = os.environ.get("MRH_FORCE_RCCL")
-    os.environ["MRH_FORCE_RCCL"] = "1"
+    os.environ["MRH_FORCE_RCCL"] = level
     try:
         c = Comm(group=None, device=comm.device)
         c.__dict__["_force"] = True
@@ -508,8 +510,10 @@ def bench_dist_plans(comm, args):
     """One GPU (N=1): PageRank RMAT-26 x20 and tri_find RMAT-24 again through
     the multi-GPU plans on a forced one-rank RCCL communicator (the paths the
     8-GPU BASELINE configs run), reported next to the local-path numbers"""
+    from gpu_mapreduce_amd._ext import C
     out = {}
     fc = _forced_rccl_comm(comm)
+    c0 = dict(C.rccl_counters())
     try:
         try:
             r = bench_pagerank_extra(fc, args)
@@ -524,12 +528,28 @@ def bench_dist_plans(comm, args):
                        warmup=1)
             out.update({k: v for k, v in r.items() if k in ("trifind_dist_ms", "trifind_dist_triangles",
                                                              "trifind_dist_error", "trifind_dist_build")})
-        out["dist_plans_note"] = ("MRH_FORCE_RCCL=1 one-rank RCCL communicator: the PageRank plan of several GPUs "
-                                  "(destination-owned edges, all-gathered c, per-iteration allreduce + all-gather) "
-                                  "and the tri_find split build (key-range exchange, allreduced degrees, row-range "
-                                  "exchange, column all-gather); at one rank the all-gathers, allreduces and broadcasts "
-                                  "of device tensors are the identity (no collective kernel), the exchanges go through "
-                                  "RCCL send/recv")
+        if args.wordfreq_bytes > 0 and getattr(args, "wordfreq_dist", 1):
+            # BASELINE config 3's P > 1 route at full size on one GPU: the
+            # (word, NULL) pairs are materialised, hash-partitioned, sent
+            # through RCCL (to this rank) and grouped as the rounds land
+            from gpu_mapreduce_amd.models.wordfreq import bench_wordfreq
+            from gpu_mapreduce_amd.runtime import hbm_pool
+            dev = torch.device(comm.device).index or 0
+            hbm_pool.reset_peak(dev)
+            r = _extra(fc, "wordfreq_shuffle_dist", bench_wordfreq, args, bytes_per_gpu=args.wordfreq_bytes,
+                       file_bytes=min(args.file_bytes, int(args.wordfreq_bytes)), steps=args.extra_steps,
+                       warmup=1, combiner=False)
+            out.update(r)
+            out["wordfreq_shuffle_dist_hbm_peak"] = hbm_pool.stats(dev)["peak"]
+        c1 = dict(C.rccl_counters())
+        out["dist_rccl_calls"] = {k: c1[k] - c0.get(k, 0) for k in c1}
+        out["dist_plans_note"] = ("MRH_FORCE_RCCL=2 one-rank RCCL communicator: the PageRank plan of several GPUs "
+                                  "(destination-owned edges, source pieces exchanged in side-stream rounds sent to "
+                                  "this rank itself, per-iteration stats ncclAllReduce; the iteration replays as a "
+                                  "HIP graph that holds those RCCL operations), the tri_find split build (key-range "
+                                  "exchange, allreduced degrees, row-range exchange, column all-gather) and "
+                                  "wordfreq without the combiner on its P > 1 route; every collective calls its "
+                                  "nccl* function (dist_rccl_calls counts them)")
     finally:
         del fc
     return out
@@ -581,6 +601,63 @@ def rccl_record(comm):
     return rec
 
 
+def _r(x, nd=2):
+    return None if x is None else round(float(x), nd)
+
+
+def compact_record(res):
+    """The driver-visible subset of the record: one number per BASELINE
+    config and extra workload, with its correctness check; no stage arrays.
+    (The full record, stage by stage, is written to --detail-out.)"""
+    out = {}
+
+    def put(key, src=None, nd=2):
+        v = res.get(src or key)
+        if v is not None and not isinstance(v, (dict, list)):
+            out[key] = _r(v, nd) if isinstance(v, float) else v
+    for k in ("ms_per_step_no_prefetch", "input_GBps", "kv_pairs_per_step", "unique_urls",
+              "pagerank_ms", "pagerank_setup_ms", "pagerank_setup_cold_ms", "pagerank_hip_graph_iterations",
+              "pagerank_dist_ms", "pagerank_dist_setup_ms",
+              "trifind_ms", "trifind_triangles", "trifind_build", "trifind_dist_ms", "trifind_dist_triangles",
+              "wordfreq_ms", "wordfreq_input_GBps", "wordfreq_words", "wordfreq_1gib_ms",
+              "wordfreq_shuffle_ms", "wordfreq_shuffle_top10_equals_combiner",
+              "wordfreq_shuffle_dist_ms", "wordfreq_shuffle_dist_hbm_peak", "wordfreq_shuffle_dist_top10_equals_combiner",
+              "wordfreq_shuffle_dist_route",
+              "trifind_mr_ms", "trifind_mr_triangles", "trifind_mr_triangles_check"):
+        put(k)
+    if "pagerank_kvps" in res:
+        out["pagerank_Gedges_per_s"] = _r(res["pagerank_kvps"] / 1e9)
+    if "stage_ms" in res and isinstance(res["stage_ms"], dict):
+        out["ii_stage_ms"] = {k: _r(v) for k, v in res["stage_ms"].items()}
+    for src, dst in (("with_file_io", "with_file_io_ms"), ("wordfreq_with_file_io", "wordfreq_with_file_io_ms")):
+        v = res.get(src)
+        if isinstance(v, dict):
+            out[dst] = _r(v["ms_per_step"]) if "ms_per_step" in v else str(v.get("error") or v.get("skipped"))[:120]
+    for tag, key in (("big", "trifind_mr_big"), ("ooc", "trifind_mr_ooc"), ("cfg5", "trifind_mr_cfg5")):
+        v = res.get(f"trifind_mr_{tag}")
+        if isinstance(v, dict):
+            out[f"{key}_scale"] = v.get("scale")
+            out[f"{key}_ms"] = _r(v.get("ms"))
+            if "ms_cold" in v:
+                out[f"{key}_ms_cold"] = _r(v["ms_cold"])
+            out[f"{key}_triangles_ok"] = v.get("triangles") == v.get("triangles_check")
+            for st in v.get("stages", []):
+                if st.get("op") == "collate 4" and "x_floor" in st:
+                    out[f"{key}_collate4_ms"] = st["ms"]
+                    out[f"{key}_collate4_x_floor"] = st["x_floor"]
+            if "spool_disk_bytes" in v:
+                out[f"{key}_disk_bytes"] = v["spool_disk_bytes"]
+    for k in ("pagerank_error", "pagerank_dist_error", "trifind_error", "trifind_dist_error", "wordfreq_error",
+              "wordfreq_shuffle_error", "wordfreq_shuffle_dist_error", "trifind_mr_error"):
+        if k in res:
+            out[k] = str(res[k])[:200]
+    for k in ("engine_transport", "rccl_comm_count", "rccl_check", "rccl_calls", "hbm_pool_peak_bytes",
+              "hbm_pool_reserved_peak_bytes", "ranks_joined"):
+        if k in res:
+            out[k] = res[k]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -623,6 +700,8 @@ def main():
                          "communicator (pagerank_dist_* / trifind_dist_* keys)")
     ap.add_argument("--file-io-steps", type=int, default=8,
                     help="timed steps of the headline job with part-file reads and output write (0 = skip)")
+    ap.add_argument("--detail-out", default="gpurun_out/bench_detail.json",
+                    help="rank 0 writes the full record (stage arrays, notes) here; '' = don't")
     args = ap.parse_args()
     if args.scale is None:
         args.scale = 24 if args.workload == "trifind" else 26
@@ -759,6 +838,9 @@ def main():
         res["hbm_pool_peak_bytes_by_part"] = peaks  # the hi-water of each workload of the record
     res["backend"] = {"torch.distributed": (comm.backend or "none (world size 1)") + " (host objects/scalars only)",
                       "engine_transport": rrec["engine_transport"]}
+    from gpu_mapreduce_amd._ext import C
+    if comm.is_cuda:
+        res["rccl_calls"] = dict(C.rccl_counters())
     out = {
         "metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": comm.size,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
@@ -766,11 +848,26 @@ def main():
         "dtype": res.get("dtype", "bytes+int32 (no float compute in MapReduce)"), "data": "synthetic",
         "config": res["config"],
     }
+    full = dict(out)
     for k, v in res.items():
-        if k not in out:
-            out[k] = v
+        if k not in full:
+            full[k] = v
     if comm.rank == 0:
-        print(json.dumps(out), flush=True)
+        # the whole record (per-stage arrays, notes, configs) goes to a side
+        # file; the printed line carries every BASELINE-config number in a few
+        # kB so that all of it is inside the driver's stdout tail
+        detail = args.detail_out
+        if detail:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(detail)), exist_ok=True)
+                with open(detail, "w") as f:
+                    json.dump(full, f, indent=1)
+            except OSError as e:
+                print(f"bench.py: could not write {detail}: {e}", file=sys.stderr, flush=True)
+        out.update(compact_record(res))
+        if detail:
+            out["detail_file"] = detail
+        print(json.dumps(out, separators=(",", ":")), flush=True)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

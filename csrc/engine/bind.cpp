@@ -250,6 +250,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("transport", &Comm::transport)
       .def_property_readonly("max_msg", &Comm::max_msg)
       .def_property_readonly("distributed", &Comm::distributed)
+      .def_property_readonly("loopback_collectives", &Comm::loopback_collectives)
       .def_property_readonly("failed", [](const Comm& c) { return c.monitor() && c.monitor()->failed(); })
       .def("rccl_info",
            [](const Comm& c) {
@@ -931,8 +932,35 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       },
       py::arg("store"), py::arg("tag"), py::arg("members"), py::arg("rank"));
   m.def("live_rccl_comms", &mrh::live_rccl_comms);
+  // host-side calls per nccl* entry point so far in this process (rccl.h)
+  m.def("rccl_counters", []() {
+    const mrh::RcclCounters& c = mrh::rccl_counters();
+    py::dict d;
+    d["all_reduce"] = c.all_reduce.load();
+    d["all_gather"] = c.all_gather.load();
+    d["broadcast"] = c.broadcast.load();
+    d["send"] = c.send.load();
+    d["recv"] = c.recv.load();
+    d["group"] = c.group.load();
+    return d;
+  });
+  m.def("rccl_counters_reset", &mrh::rccl_counters_reset);
+  m.def("rccl_graph_probe", &mrh::rccl_graph_probe, py::arg("device"), py::arg("what"), py::arg("capture"),
+        py::arg("mode") = 1, py::call_guard<py::gil_scoped_release>());
   // spool files currently on disk in this process (disk tier, spool.h)
   m.def("spool_files_live", &mrh::spool_files_live);
+  // the disk tier's background writer pool (spool.h WriterStats)
+  m.def("spool_writer_stats", []() {
+    const mrh::WriterStats w = mrh::spool_writer_stats();
+    py::dict d;
+    d["inflight_bytes"] = w.inflight_bytes;
+    d["peak_inflight_bytes"] = w.peak_inflight_bytes;
+    d["cap_bytes"] = w.cap_bytes;
+    d["threads"] = w.threads;
+    d["jobs"] = w.jobs;
+    return d;
+  });
+  m.def("spool_writer_reset_peak", &mrh::spool_writer_reset_peak);
   // world size 1 runs the local transport (no communicator); this builds a
   // one-rank RCCL communicator on `device` and returns what RCCL reports
   m.def("rccl_self_probe", [](int device) {

@@ -31,7 +31,14 @@ int env_int(const char* k, int d) {
   const char* v = std::getenv(k);
   return v && *v ? std::atoi(v) : d;
 }
-bool force_rccl() { return env_int("MRH_FORCE_RCCL", 0) != 0; }
+// MRH_FORCE_RCCL: 0 = a one-rank job has no communicator; 1 = it gets a
+// one-rank RCCL communicator whose data plane (send/recv rounds) runs through
+// RCCL while the collectives stay the identity; 2 = every collective also
+// calls its nccl* function (allreduce, all-gather, broadcast, the scalar
+// allreduce / bcast), so each RCCL call site of the multi-GPU paths executes
+// on one GPU (RCCL accepts nranks = 1)
+int force_rccl_level() { return env_int("MRH_FORCE_RCCL", 0); }
+bool force_rccl() { return force_rccl_level() != 0; }
 
 c10d::ReduceOp::RedOpType red(Comm::Op op) {
   return op == Comm::SUM ? c10d::ReduceOp::SUM : op == Comm::MAX ? c10d::ReduceOp::MAX : c10d::ReduceOp::MIN;
@@ -101,6 +108,7 @@ static void install_allocator() {
 Comm::Comm(at::Device dev) : dev_(dev) {
   if (dev_.is_cuda()) install_allocator();
   if (dev_.is_cuda() && force_rccl()) init_transport("", "self");
+  loop_coll_ = rccl_ && force_rccl_level() >= 2;
   max_msg_ = rccl_ ? rccl_->max_msg() : max_msg_env();
 }
 
@@ -130,6 +138,7 @@ Comm::Comm(PG pg, at::Device dev, c10::intrusive_ptr<c10d::Store> store, const s
     }
   }
   init_transport(transport, "world");
+  loop_coll_ = rccl_ && size_ == 1 && force_rccl_level() >= 2;
   // rank 0's piece size on every rank (a collective: every member constructs)
   if (rccl_) {
     max_msg_ = rccl_->max_msg();
@@ -252,8 +261,8 @@ void Comm::host_wait() const {
 // ---------------------------------------------------------------- scalars
 
 std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
-  // one rank (the forced-RCCL mode included): identity, no device round trip
-  if (v.empty() || !distributed() || size_ == 1) return v;
+  // one rank (MRH_FORCE_RCCL=1 included): identity, no device round trip
+  if (v.empty() || identity_coll()) return v;
   trace_coll(rank_, "allreduce_i64", (int64_t)v.size(), op);
   at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kLong));
   if (host_scalars()) {
@@ -273,7 +282,7 @@ std::vector<int64_t> Comm::allreduce(std::vector<int64_t> v, Op op) const {
 }
 
 std::vector<double> Comm::allreduce_f64(std::vector<double> v, Op op) const {
-  if (v.empty() || !distributed() || size_ == 1) return v;
+  if (v.empty() || identity_coll()) return v;
   trace_coll(rank_, "allreduce_f64", (int64_t)v.size(), op);
   at::Tensor t = at::tensor(v, at::TensorOptions().dtype(at::kDouble));
   if (host_scalars()) {
@@ -299,7 +308,7 @@ std::vector<double> Comm::allgather_f64(double x) const {
 }
 
 std::string Comm::bcast(const std::string& s, int root) const {
-  if (!distributed() || size_ == 1) return s;
+  if (identity_coll()) return s;
   int64_t n = rank_ == root ? (int64_t)s.size() : 0;
   n = allreduce(n, SUM);
   at::Tensor t = at::zeros({std::max<int64_t>(n, 1)}, at::TensorOptions().dtype(at::kByte));
@@ -374,8 +383,10 @@ void Comm::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& rec
     fill[x.peer] += x.bytes;
   }
   const int64_t m = std::max<int64_t>(max_msg_, 1);
+  // pieces of m bytes (no (b + m - 1) / m: m may be INT64_MAX, "no limit")
+  auto npieces = [m](int64_t b) { return b <= 0 ? int64_t(0) : 1 + (b - 1) / m; };
   int64_t rounds = 1;
-  for (int p = 0; p < P; ++p) rounds = std::max({rounds, (sb[p] + m - 1) / m, (rb[p] + m - 1) / m});
+  for (int p = 0; p < P; ++p) rounds = std::max({rounds, npieces(sb[p]), npieces(rb[p])});
   rounds = allreduce(rounds, MAX);
   if (rounds == 1) {
     pg_->alltoall_base(rbuf, sbuf, rb, sb)->wait();
@@ -410,7 +421,7 @@ void Comm::sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& rec
 
 void Comm::allgather_bytes(const void* send, void* recv, int64_t bytes) const {
   trace_coll(rank_, "allgather", bytes, 0);
-  if (size_ == 1) {  // one rank (the forced-RCCL mode): the identity, no collective kernel
+  if (size_ == 1 && !loop_coll_) {  // one rank (MRH_FORCE_RCCL=1): the identity, no collective kernel
     if (send != recv) copy_bytes(recv, send, bytes, dev_);
     return;
   }
@@ -490,7 +501,7 @@ at::Tensor Comm::allgather_var(const at::Tensor& in) const {
 }
 
 void Comm::allreduce_tensor(at::Tensor& t, Op op) const {
-  if (!distributed() || size_ == 1) return;
+  if (identity_coll()) return;
   trace_coll(rank_, "allreduce_tensor", t.numel(), op);
   if (rccl_) {
     if (!t.is_contiguous()) t = t.contiguous();
@@ -501,7 +512,7 @@ void Comm::allreduce_tensor(at::Tensor& t, Op op) const {
 }
 
 void Comm::broadcast_tensor(at::Tensor& t, int root) const {
-  if (!distributed() || size_ == 1) return;
+  if (identity_coll()) return;
   trace_coll(rank_, "broadcast", t.numel(), root);
   if (rccl_) {
     if (!t.is_contiguous()) t = t.contiguous();

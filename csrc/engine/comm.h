@@ -10,9 +10,10 @@
 //  * RCCL (device engine): the native RCCL communicator of rccl.h over xGMI,
 //    bootstrapped through the job's rendezvous store. Used whenever the
 //    engine device is a GPU and the job has more than one rank — and at world
-//    size 1 too when MRH_FORCE_RCCL=1, so the complete RCCL data path (header
-//    allgather, grouped send/recv rounds, allreduce, broadcast) runs and is
-//    tested on a single GPU;
+//    size 1 too when MRH_FORCE_RCCL=1 (the send/recv data path runs through
+//    RCCL, collectives are the identity) or MRH_FORCE_RCCL=2 (every
+//    collective also calls its nccl* function on the one-rank communicator),
+//    so the RCCL call sites run and are tested on a single GPU;
 //  * PG (host engine / rehearsal): a c10d ProcessGroup — gloo from
 //    torch.distributed, or the store transport of storepg.h for the native
 //    programs on CPU — moving packed host (or staged device) buffers.
@@ -76,6 +77,8 @@ class Comm {
   // single-rank RCCL mode)
   bool distributed() const { return size_ > 1 || rccl_ != nullptr; }
   bool uses_rccl() const { return rccl_ != nullptr; }
+  // MRH_FORCE_RCCL=2 on one rank: collectives call RCCL instead of the identity
+  bool loopback_collectives() const { return loop_coll_; }
   std::string transport() const;
   const PG& pg() const { return pg_; }
   const std::shared_ptr<Rccl>& rccl() const { return rccl_; }
@@ -152,6 +155,10 @@ class Comm {
   void init_transport(const std::string& transport, const std::string& tag);
   void fail_now(const std::string& why) const;
   bool host_scalars() const { return pg_ && host_pg_ && size_ > 1; }
+  // a collective is the identity: not distributed, or one rank whose
+  // communicator does not loop collectives through RCCL
+  bool identity_coll() const { return !distributed() || (size_ == 1 && !loop_coll_); }
+  bool loop_coll_ = false;  // MRH_FORCE_RCCL=2 (one rank)
   bool host_pg_ = false;  // pg_ has a CPU backend
   int64_t max_msg_ = 0;   // point-to-point piece size, agreed at construction
   int rccl_device() const;  // the device index (the current one for "cuda")

@@ -606,7 +606,9 @@ void PageRankPlan::build_device_dist(const at::Tensor& e) {
   // MRH_PR_OVERLAP=0: off; =2: also on one rank (the forced-RCCL mode:
   // chunked gathers, side-stream rounds and their events without peers)
   const char* oenv = std::getenv("MRH_PR_OVERLAP");
-  const bool by_piece = (P > 1 && !(oenv && *oenv == '0')) || (oenv && *oenv == '2');
+  // (MRH_FORCE_RCCL=2 on one rank takes the multi-rank default: pieces on)
+  const bool multi = P > 1 || comm->loopback_collectives();
+  const bool by_piece = (multi && !(oenv && *oenv == '0')) || (oenv && *oenv == '2');
   std::vector<int64_t> rb, redge;
   std::vector<int> piece_nr;  // ranges of every chunk (by_piece)
   at::Tensor dg;
@@ -788,11 +790,21 @@ void PageRankPlan::ring_start() {
   const c10::DeviceIndex di = dev.has_index() ? dev.index() : c10::hip::current_device();
   c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(side_, di));
   uint8_t* base = reinterpret_cast<uint8_t*>(cfull_.data_ptr());
+  // MRH_FORCE_RCCL=2 on one rank: the slice goes to this rank itself (in
+  // place, the identity), so the eager rounds hold real RCCL send/recv
+  // operations. Not under HIP-graph capture: RCCL 2.26.6 segfaults in
+  // hipStreamEndCapture on a captured self send/recv, while a captured
+  // ncclAllReduce replays correctly (tools/rccl_graph_probe.py,
+  // profiles/r6_rccl_graph_probe.txt) — the captured iteration keeps its
+  // stats allreduce as the RCCL operation inside the graph
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  pr_chk(hipStreamIsCapturing(cs, &cap), "hipStreamIsCapturing");
+  const bool self = P == 1 && comm->loopback_collectives() && cap == hipStreamCaptureStatusNone;
   for (size_t j = 0; j + 1 < chunk_b_.size(); ++j) {
     const int64_t a = chunk_b_[j] * 4, len = (chunk_b_[j + 1] - chunk_b_[j]) * 4;
     std::vector<Xfer> xs, xr;
     for (int p = 0; p < P; ++p) {
-      if (p == me) continue;
+      if (p == me && !self) continue;
       xs.push_back(Xfer{p, base + (int64_t)me * S_ * 4 + a, len});
       xr.push_back(Xfer{p, base + (int64_t)p * S_ * 4 + a, len});
     }

@@ -586,7 +586,10 @@ void pool_free(void* ptr, size_t /*size*/, int /*dev*/, hipStream_t /*stream*/) 
   d.pending.push_back(std::move(q));
 }
 
-void forget_stream_locked(hipStream_t s) {  // g_mu held
+// free_blocks = false (a stream that may never drain, e.g. an aborted RCCL
+// stream): its cached blocks are dropped from the cache and leaked rather
+// than freed behind work that may never finish
+void forget_stream_locked(hipStream_t s, bool free_blocks = true) {  // g_mu held
   if (!s) return;
   for (Dev& d : g_dev) {
     for (auto it = d.free.begin(); it != d.free.end();) {
@@ -595,7 +598,7 @@ void forget_stream_locked(hipStream_t s) {  // g_mu held
         continue;
       }
       for (void* p : it->second) {
-        if (hipFreeAsync(p, s) != hipSuccess) (void)hipGetLastError();
+        if (free_blocks && hipFreeAsync(p, s) != hipSuccess) (void)hipGetLastError();
         d.cached -= it->first.second;
       }
       it = d.free.erase(it);
@@ -747,6 +750,12 @@ void forget_stream(hipStream_t s) {
   (void)hipStreamSynchronize(s);
   std::lock_guard<std::mutex> l(g_mu);
   forget_stream_locked(s);
+}
+
+void forget_stream_nosync(hipStream_t s) {
+  if (!s) return;
+  std::lock_guard<std::mutex> l(g_mu);
+  forget_stream_locked(s, false);
 }
 
 }  // namespace mrh::hbm

@@ -79,6 +79,9 @@ void trim(int device, int64_t keep_bytes);
 // event on, or waits with, a dead stream (the caller has synchronised it).
 // Every engine-owned stream calls this before hipStreamDestroy
 void forget_stream(hipStream_t s);
+// the same without waiting for the stream (an aborted communicator's stream):
+// its cached blocks are leaked, not freed
+void forget_stream_nosync(hipStream_t s);
 
 // RAII: a MapReduce op's cap (in use at entry + extra bytes) while it runs;
 // concurrent ops' caps combine (the tightest is in force)

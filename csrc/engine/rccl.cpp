@@ -43,6 +43,20 @@ int64_t max_msg_env() {
   return v > 0 ? (int64_t)v : std::numeric_limits<int64_t>::max();
 }
 
+RcclCounters& rccl_counters() {
+  static RcclCounters c;
+  return c;
+}
+void rccl_counters_reset() {
+  RcclCounters& c = rccl_counters();
+  c.all_reduce = 0;
+  c.all_gather = 0;
+  c.broadcast = 0;
+  c.send = 0;
+  c.recv = 0;
+  c.group = 0;
+}
+
 // ====================================================================== Monitor
 
 Monitor::Monitor(c10::intrusive_ptr<c10d::Store> root, int rank, int size)
@@ -274,7 +288,11 @@ Rccl::~Rccl() {
   }
   for (auto& e : ev_) (void)hipEventDestroy(e);
   if (stream_) {
-    if (!aborted_) hbm::forget_stream(stream_);
+    // an aborted communicator's stream may never drain: drop the pool's
+    // references to it without waiting (a later event record on a destroyed
+    // stream is the segfault class of hbm::forget_stream)
+    if (aborted_) hbm::forget_stream_nosync(stream_);
+    else hbm::forget_stream(stream_);
     (void)hipStreamDestroy(stream_);
   }
 }
@@ -301,16 +319,22 @@ hipEvent_t Rccl::sendrecv_async(const std::vector<Xfer>& sends, const std::vecto
   // pieces arrived intact up to 4 GiB (profiles/r4_rccl_big_messages.txt;
   // tests/test_rccl_gpu.py test_forced_rccl_large_transfers_bitwise)
   const int64_t max_msg = max_msg_;
+  RcclCounters& cnt = rccl_counters();
   check(ncclGroupStart(), "ncclGroupStart");
   for (const Xfer& x : recvs)
-    for (int64_t o = 0; o < x.bytes; o += max_msg)
+    for (int64_t o = 0; o < x.bytes; o += max_msg) {
       check(ncclRecv((uint8_t*)x.ptr + o, (size_t)std::min(max_msg, x.bytes - o), ncclUint8, x.peer, comm_, stream_),
             "ncclRecv");
+      ++cnt.recv;
+    }
   for (const Xfer& x : sends)
-    for (int64_t o = 0; o < x.bytes; o += max_msg)
+    for (int64_t o = 0; o < x.bytes; o += max_msg) {
       check(ncclSend((uint8_t*)x.ptr + o, (size_t)std::min(max_msg, x.bytes - o), ncclUint8, x.peer, comm_, stream_),
             "ncclSend");
+      ++cnt.send;
+    }
   check(ncclGroupEnd(), "ncclGroupEnd");
+  ++cnt.group;
   return fence_out();
 }
 
@@ -323,6 +347,7 @@ void Rccl::allreduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op,
   if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
   fence_in(s);
   check(ncclAllReduce(buf, buf, count, dt, op, comm_, stream_), "ncclAllReduce");
+  ++rccl_counters().all_reduce;
   hip_ok(hipStreamWaitEvent(s, fence_out(), 0), "hipStreamWaitEvent");
 }
 
@@ -330,6 +355,7 @@ void Rccl::allgather(const void* send, void* recv, size_t bytes, hipStream_t s) 
   if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
   fence_in(s);
   check(ncclAllGather(send, recv, bytes, ncclUint8, comm_, stream_), "ncclAllGather");
+  ++rccl_counters().all_gather;
   hip_ok(hipStreamWaitEvent(s, fence_out(), 0), "hipStreamWaitEvent");
 }
 
@@ -337,6 +363,7 @@ void Rccl::broadcast(void* buf, size_t bytes, int root, hipStream_t s) {
   if (aborted_) throw PeerFailure("mrhip rccl: communicator aborted");
   fence_in(s);
   check(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, stream_), "ncclBroadcast");
+  ++rccl_counters().broadcast;
   hip_ok(hipStreamWaitEvent(s, fence_out(), 0), "hipStreamWaitEvent");
 }
 
@@ -379,6 +406,84 @@ int live_rccl_comms() {
   int n = 0;
   for (auto& kv : g_rccl) n += kv.second.expired() ? 0 : 1;
   return n;
+}
+
+// Diagnostic: one RCCL operation on a one-rank communicator, eagerly and then
+// captured into a HIP graph (ThreadLocal capture on a non-blocking stream, as
+// the PageRank plan does) and replayed; each step is logged to stderr first
+// so a crash names it. what: allreduce | allgather | broadcast | self (send to
+// a second buffer) | self_inplace. Returns "ok" or the failed check.
+std::string rccl_graph_probe(int device, const std::string& what, bool capture, int mode) {
+  auto step = [](const char* m) {
+    std::fprintf(stderr, "[rccl_graph_probe] %s\n", m);
+    std::fflush(stderr);
+  };
+  hip_ok(hipSetDevice(device), "hipSetDevice");
+  Rccl r(0, 1, device, c10::intrusive_ptr<c10d::Store>(), "gprobe");
+  hipStream_t s = nullptr;
+  hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  const size_t n = 1 << 16;
+  std::vector<float> h(2 * n);
+  for (size_t i = 0; i < 2 * n; ++i) h[i] = (float)(i % 977) + 0.5f;
+  float* a = nullptr;
+  hip_ok(hipMalloc((void**)&a, 2 * n * sizeof(float)), "hipMalloc");
+  hip_ok(hipMemcpy(a, h.data(), 2 * n * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
+  const int64_t bytes = (int64_t)(n * sizeof(float));
+  // "k_<op>": the op between two device copies of the second half onto
+  // itself, so the captured graph is not empty (the PageRank iteration's
+  // kernels around its RCCL rounds)
+  const bool bracket = what.rfind("k_", 0) == 0;
+  const std::string op = bracket ? what.substr(2) : what;
+  auto touch = [&] {
+    if (bracket) hip_ok(hipMemcpyAsync(a + n, a + n, (size_t)bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+  };
+  auto enqueue = [&] {
+    touch();
+    if (op == "allreduce") r.allreduce(a, n, ncclFloat32, ncclSum, s);
+    else if (op == "allgather") r.allgather(a, a, (size_t)bytes, s);
+    else if (op == "broadcast") r.broadcast(a, (size_t)bytes, 0, s);
+    else if (op == "self") r.sendrecv({Xfer{0, a, bytes}}, {Xfer{0, a + n, bytes}}, s);
+    else if (op == "self_inplace") r.sendrecv({Xfer{0, a, bytes}}, {Xfer{0, a, bytes}}, s);
+    else throw std::runtime_error("rccl_graph_probe: unknown op " + what);
+    touch();
+  };
+  step("eager");
+  enqueue();
+  hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize (eager)");
+  if (capture) {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    step("begin capture");
+    const hipStreamCaptureMode cm = mode == 0 ? hipStreamCaptureModeGlobal
+                                    : mode == 2 ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal;
+    hip_ok(hipStreamBeginCapture(s, cm), "hipStreamBeginCapture");
+    step("enqueue under capture");
+    enqueue();
+    step("end capture");
+    hip_ok(hipStreamEndCapture(s, &g), "hipStreamEndCapture");
+    size_t nn = 0;
+    hip_ok(hipGraphGetNodes(g, nullptr, &nn), "hipGraphGetNodes");
+    std::fprintf(stderr, "[rccl_graph_probe] graph nodes: %zu\n", nn);
+    step("instantiate");
+    hip_ok(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+    for (int i = 0; i < 3; ++i) {
+      step("launch");
+      hip_ok(hipGraphLaunch(ge, s), "hipGraphLaunch");
+    }
+    hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize (replay)");
+    step("replayed");
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+  }
+  std::vector<float> o(2 * n);
+  hip_ok(hipMemcpy(o.data(), a, 2 * n * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy back");
+  (void)hipFree(a);
+  (void)hipStreamDestroy(s);
+  for (size_t i = 0; i < n; ++i) {
+    const float want_hi = op == "self" ? h[i] : h[n + i];
+    if (o[i] != h[i] || o[n + i] != want_hi) return "mismatch at " + std::to_string(i);
+  }
+  return "ok";
 }
 
 ncclResult_t Rccl::async_error() {

@@ -178,6 +178,20 @@ class Rccl {
 // this process's MRH_RCCL_MAX_MSG (default 256 MiB; <= 0: no limit)
 int64_t max_msg_env();
 
+// Host-side calls per nccl* entry point made by this process's Rccl objects
+// (enqueue count: a call captured into a HIP graph counts once, at capture).
+// The forced one-rank modes and the tests read them to prove that a code path
+// really went through RCCL rather than the one-rank identity.
+struct RcclCounters {
+  std::atomic<int64_t> all_reduce{0}, all_gather{0}, broadcast{0}, send{0}, recv{0}, group{0};
+};
+RcclCounters& rccl_counters();
+// diagnostic (rccl.cpp): one RCCL op on a one-rank communicator, eager then
+// captured into a HIP graph and replayed; "ok" or what failed
+// (capture mode: 0 global, 1 thread-local, 2 relaxed)
+std::string rccl_graph_probe(int device, const std::string& what, bool capture, int mode = 1);
+void rccl_counters_reset();
+
 // The process's communicator over (store, tag, members, device): an existing
 // live one is shared, otherwise a new one is bootstrapped (collectively: every
 // member must ask in the same order).

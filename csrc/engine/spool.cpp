@@ -9,12 +9,16 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <filesystem>
 #include <future>
 #include <mutex>
 #include <stdexcept>
+#include <thread>
 
 namespace mrh {
 
@@ -30,8 +34,13 @@ SpoolStats& totals() {
   static SpoolStats s;
   return s;
 }
-// totals are also updated by the background file writers
+// totals are also updated by the background file writers: every access
+// (reads included) under this lock
 std::mutex g_totals_mu;
+void totals_piece() {
+  std::lock_guard<std::mutex> g(g_totals_mu);
+  totals().pieces++;
+}
 
 // one memory-mapped spool file; unmapped and deleted with the last view
 struct Mapping {
@@ -258,7 +267,10 @@ KV kv_of(const std::shared_ptr<Mapping>& m, const Layout& L, size_t& slot, const
 
 }  // namespace
 
-SpoolStats& spool_totals() { return totals(); }
+SpoolStats spool_totals() {
+  std::lock_guard<std::mutex> g(g_totals_mu);
+  return totals();
+}
 int64_t spool_files_live() { return g_files_live.load(); }
 
 std::string spool_path(const std::string& dir, const std::string& kind, int instance, int rank) {
@@ -339,6 +351,114 @@ KMV kmv_to_file(const std::vector<KMV>& parts, const std::string& path) {
   }
   return o;
 }
+
+// ---------------------------------------------------------------- disk writer
+// The disk tier's background writes go through ONE bounded pool per process:
+// MRH_SPOOL_WRITERS threads (default 4) and at most MRH_SPOOL_WRITE_INFLIGHT
+// bytes (default 1 GiB) of drained-but-unwritten pinned pieces. submit()
+// blocks while the bytes in flight would pass the cap (the caller waits for
+// the oldest writes), and a job drops its reference to the pinned piece as
+// soon as the file is written, so the pinned chunk it views can go back to the
+// host allocator before the spool is read. (Before: one std::async thread per
+// piece, each holding its pinned piece until the spool was read — every
+// spilled byte pinned at once and chunks x partitions threads.)
+class DiskWriter {
+ public:
+  static DiskWriter& get() {
+    static DiskWriter* w = new DiskWriter();  // never destroyed: no join at exit
+    return *w;
+  }
+  std::future<KV> submit(KV piece, std::shared_ptr<DrainEvent> ev, std::string path) {
+    const int64_t b = std::max<int64_t>(1, piece.nbytes());
+    auto job = std::make_unique<Job>();
+    job->piece = std::move(piece);
+    job->ev = std::move(ev);
+    job->path = std::move(path);
+    job->bytes = b;
+    std::future<KV> f = job->done.get_future();
+    std::unique_lock<std::mutex> l(mu_);
+    // one piece bigger than the cap still goes, alone
+    room_.wait(l, [&] { return inflight_ == 0 || inflight_ + b <= cap_; });
+    inflight_ += b;
+    peak_ = std::max(peak_, inflight_);
+    q_.push_back(std::move(job));
+    if ((int)threads_.size() < nthreads_ && (int)q_.size() > idle_) {
+      threads_.emplace_back([this] { loop(); });
+      threads_.back().detach();
+    }
+    work_.notify_one();
+    return f;
+  }
+  WriterStats stats() {
+    std::lock_guard<std::mutex> l(mu_);
+    WriterStats s;
+    s.inflight_bytes = inflight_;
+    s.peak_inflight_bytes = peak_;
+    s.threads = (int)threads_.size();
+    s.cap_bytes = cap_;
+    s.jobs = jobs_;
+    return s;
+  }
+  void reset_peak() {
+    std::lock_guard<std::mutex> l(mu_);
+    peak_ = inflight_;
+  }
+
+ private:
+  struct Job {
+    KV piece;
+    std::shared_ptr<DrainEvent> ev;
+    std::string path;
+    int64_t bytes = 0;
+    std::promise<KV> done;
+  };
+  DiskWriter() {
+    const char* t = std::getenv("MRH_SPOOL_WRITERS");
+    nthreads_ = std::max(1, t && *t ? std::atoi(t) : 4);
+    const char* c = std::getenv("MRH_SPOOL_WRITE_INFLIGHT");
+    cap_ = c && *c ? std::max<int64_t>(1, std::atoll(c)) : (int64_t(1) << 30);
+  }
+  void loop() {
+    for (;;) {
+      std::unique_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        ++idle_;
+        work_.wait(l, [&] { return !q_.empty(); });
+        --idle_;
+        j = std::move(q_.front());
+        q_.pop_front();
+      }
+      try {
+        const hipError_t r = hipEventSynchronize(j->ev->e);
+        if (r != hipSuccess) fail(std::string("asynchronous drain failed: ") + hipGetErrorString(r));
+        KV out = kv_to_file({j->piece}, j->path);
+        j->piece = KV();  // the pinned source goes back now, not when the spool is read
+        j->ev.reset();
+        j->done.set_value(std::move(out));
+      } catch (...) {
+        j->piece = KV();
+        j->ev.reset();
+        j->done.set_exception(std::current_exception());
+      }
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        inflight_ -= j->bytes;
+        ++jobs_;
+      }
+      room_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable work_, room_;
+  std::deque<std::unique_ptr<Job>> q_;
+  std::vector<std::thread> threads_;
+  int nthreads_ = 4, idle_ = 0;
+  int64_t cap_ = 0, inflight_ = 0, peak_ = 0, jobs_ = 0;
+};
+
+WriterStats spool_writer_stats() { return DiskWriter::get().stats(); }
+void spool_writer_reset_peak() { DiskWriter::get().reset_peak(); }
 
 Spool::Spool(at::Device dev, SpoolConfig cfg) : dev_(dev), cfg_(std::move(cfg)) {
   if (!cfg_.budget) cfg_.budget = std::make_shared<SpoolBudget>();
@@ -425,18 +545,13 @@ void Spool::add_drained(const KV& piece, const std::shared_ptr<DrainEvent>& ev) 
   n_ += piece.n;
   bytes_ += b;
   st_.pieces++;
-  totals().pieces++;
+  totals_piece();
 }
 
 void Spool::add_drained_to_disk(const KV& piece, const std::shared_ptr<DrainEvent>& ev) {
   if (piece.n == 0) return;
   const int64_t b = piece.nbytes();
-  const std::string path = next_path();
-  writing_.emplace_back(pieces_.size(), std::async(std::launch::async, [piece, ev, path]() {
-                          const hipError_t r = hipEventSynchronize(ev->e);
-                          if (r != hipSuccess) fail(std::string("asynchronous drain failed: ") + hipGetErrorString(r));
-                          return kv_to_file({piece}, path);
-                        }));
+  writing_.emplace_back(pieces_.size(), DiskWriter::get().submit(piece, ev, next_path()));
   pieces_.push_back(KV());  // filled in by sync()
   tier_.push_back(2);
   st_.disk_bytes += b;
@@ -444,7 +559,7 @@ void Spool::add_drained_to_disk(const KV& piece, const std::shared_ptr<DrainEven
   n_ += piece.n;
   bytes_ += b;
   st_.pieces++;
-  totals().pieces++;
+  totals_piece();
 }
 
 std::string Spool::next_path() const { return spool_path(cfg_.dir, cfg_.kind, cfg_.instance, cfg_.rank); }
@@ -496,12 +611,7 @@ void Spool::add(const KV& piece, hipStream_t copy) {
     // copy stream, then a background thread writes and maps the file
     KV hp;
     std::shared_ptr<DrainEvent> done = drain_to_pinned(piece, copy, &hp);
-    const std::string path = next_path();
-    writing_.emplace_back(pieces_.size(), std::async(std::launch::async, [hp, done, path]() {
-                            const hipError_t r = hipEventSynchronize(done->e);
-                            if (r != hipSuccess) fail(std::string("asynchronous drain failed: ") + hipGetErrorString(r));
-                            return kv_to_file({hp}, path);
-                          }));
+    writing_.emplace_back(pieces_.size(), DiskWriter::get().submit(std::move(hp), std::move(done), next_path()));
     p = KV();  // filled in by sync()
     tier = 2;
     st_.disk_bytes += b;
@@ -517,7 +627,7 @@ void Spool::add(const KV& piece, hipStream_t copy) {
   n_ += piece.n;
   bytes_ += b;
   st_.pieces++;
-  totals().pieces++;
+  totals_piece();
 }
 
 void Spool::clear() {

@@ -58,8 +58,19 @@ struct SpoolStats {
 };
 
 // process-wide totals (tests, cummulative_stats): files created / live on disk
-SpoolStats& spool_totals();
+// (a snapshot: background writers update them under a lock)
+SpoolStats spool_totals();
 int64_t spool_files_live();
+
+// the process's disk-tier writer pool (spool.cpp DiskWriter): drained pinned
+// bytes waiting for their file write (bounded by MRH_SPOOL_WRITE_INFLIGHT),
+// the hi-water of that, threads started (at most MRH_SPOOL_WRITERS), jobs done
+struct WriterStats {
+  int64_t inflight_bytes = 0, peak_inflight_bytes = 0, cap_bytes = 0, jobs = 0;
+  int threads = 0;
+};
+WriterStats spool_writer_stats();
+void spool_writer_reset_peak();
 
 // a device->host drain's completion event, shared by every spool holding a
 // piece of the drained buffer (destroyed with the last holder)

@@ -87,8 +87,12 @@ class WordFreq:
         # map emits them (the KeyValue's hash dictionary, csrc/engine/
         # grouper.h) in the shadow of the next chunk's H2D copy, so the
         # collate's convert only ranks the groups; with several ranks the
-        # pairs are shuffled first and grouped as the exchange rounds land
-        group = wc is None and self.mr.nprocs == 1 and self.is_cuda
+        # pairs are shuffled first and grouped as the exchange rounds land.
+        # A forced one-rank RCCL communicator (MRH_FORCE_RCCL=1/2) is
+        # "distributed" and takes that P > 1 route: the pairs are materialised,
+        # partitioned and sent through RCCL to this rank itself
+        group = wc is None and self.is_cuda and not self.mr.comm.native.distributed
+        self.route = "combiner" if wc is not None else ("grouped in the map" if group else "shuffle")
         if group:
             kv.enable_grouping()
         total = sum(t.numel() for t in self.chunks)
@@ -299,6 +303,7 @@ def bench_wordfreq(comm, args):
         "pairs": app.npairs,
         "unique_words": app.nunique,
         "top3": app.top[:3],
+        "route": getattr(app, "route", None),
         "setup_ms": setup * 1e3,
         "config": {"model": "wordfreq" if combiner else "wordfreq (no combiner: a pair per occurrence)",
                    "global_batch": total, "seq_len": chunk, "parallelism": f"dp{comm.size}",
