@@ -601,6 +601,22 @@ def rccl_record(comm):
     return rec
 
 
+def trifind_mr_big_scale_for(n_gpus, hbm_bytes=288e9):
+    """R-MAT scale of the big in-HBM tri_find_mr run at N GPUs (strong
+    scaling): the largest scale <= 24 (BASELINE config 5: tri_find on RMAT-24
+    over 8 GPUs) whose estimated per-GPU peak fits 65 % of one GPU's HBM.
+    Wedge pairs grow ~5.9x per two scales (RMAT-20: 1.23 G, RMAT-22: 7.27 G,
+    measured); the pipeline peaks at ~25 bytes per pair on one GPU (RMAT-22:
+    ~180 GB). N = 1, 2 -> 22; N = 4 -> 23; N = 8 -> 24 (the config-5 graph,
+    ~5.4 G pairs per GPU)."""
+    best = 20
+    for sc in range(20, 25):
+        pairs = 1.23e9 * (7.27 / 1.23) ** ((sc - 20) / 2)
+        if 25.0 * pairs / max(1, n_gpus) <= 0.65 * hbm_bytes:
+            best = sc
+    return best
+
+
 def _r(x, nd=2):
     return None if x is None else round(float(x), nd)
 
@@ -726,7 +742,7 @@ def main():
     if args.trifind_mr_ooc_scale is None:
         args.trifind_mr_ooc_scale = 18 if comm.is_cuda else 0
     if args.trifind_mr_big_scale is None:
-        args.trifind_mr_big_scale = 22 if comm.is_cuda else 0
+        args.trifind_mr_big_scale = trifind_mr_big_scale_for(comm.size) if comm.is_cuda else 0
     if args.wordfreq_bytes is None:
         args.wordfreq_bytes = float(8 << 30) if comm.is_cuda else 4e6
     if args.workload == "invertedindex":

@@ -95,18 +95,58 @@ void kmv_iter(const KMV& kmv, py::function fn) {
 
 py::object kvref(KeyValue& kv) { return py::cast(&kv, py::return_value_policy::reference); }
 
-// the values of one key as a list of bytes; in multi-block mode (mv == nullptr)
-// walk the blocks through the MR
+void append_block(py::list& out, char* p, int n, const int* sz) {
+  for (int j = 0; j < n; ++j) {
+    out.append(py::bytes(p, (size_t)sz[j]));
+    p += sz[j];
+  }
+}
+
+// A key whose values span several pages (the multi-block protocol, reference
+// src/mapreduce.cpp:1828-1848, 1874-1925): handed to a Python callback
+// instead of a list; block(i) materialises ONE page of values through the
+// MR's multivalue_block, so a hot key is never one Python list. Valid only
+// during the callback it was passed to.
+struct ValueBlocks {
+  MapReduce* mr = nullptr;
+  int nb = 0;
+  int64_t total = 0;
+  bool valid = true;
+  void check() const {
+    if (!valid) throw std::runtime_error("multivalue blocks used after their reduce callback returned");
+  }
+  py::list block(int i) {
+    check();
+    if (i < 0 || i >= nb) throw py::index_error("multivalue block index out of range");
+    char* p;
+    int* sz;
+    const int n = mr->multivalue_block(i, &p, &sz);
+    py::list out;
+    append_block(out, p, n, sz);
+    return out;
+  }
+};
+
+// the values of one key: a list of bytes, or (multi-block mode, mv ==
+// nullptr) a ValueBlocks cursor; `live` gets the cursor to invalidate after
+py::object value_arg(MapReduce& mr, char* mv, int nv, int* vb, std::shared_ptr<ValueBlocks>* live) {
+  if (mv) {
+    py::list out;
+    append_block(out, mv, nv, vb);
+    return out;
+  }
+  auto c = std::make_shared<ValueBlocks>();
+  c->mr = &mr;
+  c->total = (int64_t)mr.multivalue_blocks(c->nb);
+  *live = c;
+  return py::cast(c);
+}
+
+// every value of one key as one list (scan_kmv's read-only view)
 py::list value_list(MapReduce& mr, char* mv, int nv, int* vb) {
   py::list out;
-  auto one_block = [&](char* p, int n, int* sz) {
-    for (int j = 0; j < n; ++j) {
-      out.append(py::bytes(p, (size_t)sz[j]));
-      p += sz[j];
-    }
-  };
   if (mv) {
-    one_block(mv, nv, vb);
+    append_block(out, mv, nv, vb);
   } else {
     int nb = 0;
     mr.multivalue_blocks(nb);
@@ -114,7 +154,7 @@ py::list value_list(MapReduce& mr, char* mv, int nv, int* vb) {
       char* p;
       int* sz;
       int n = mr.multivalue_block(b, &p, &sz);
-      one_block(p, n, sz);
+      append_block(out, p, n, sz);
     }
   }
   return out;
@@ -232,6 +272,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("finish", &KeyValue::finish)
       .def_property_readonly("device", [](const KeyValue& kv) { return kv.device().str(); });
 
+  py::class_<ValueBlocks, std::shared_ptr<ValueBlocks>>(m, "ValueBlocks")
+      .def_readonly("nblocks", &ValueBlocks::nb)
+      .def_readonly("nvalues", &ValueBlocks::total)
+      .def("block", &ValueBlocks::block)
+      .def("__len__", [](const ValueBlocks& b) { return b.total; });
   py::class_<Comm, std::shared_ptr<Comm>>(m, "NativeComm")
       .def(py::init([](py::object pg, const std::string& dev, py::object store, const std::string& transport,
                        std::vector<int> members, int world_rank, int world_size) {
@@ -416,7 +461,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              py::gil_scoped_release nogil;
              return r.reduce([&](char* k, int kb, char* mv, int nv, int* vb, KeyValue& kv) {
                py::gil_scoped_acquire g;
-               fn(py::bytes(k, (size_t)kb), value_list(r, mv, nv, vb), kvref(kv));
+               std::shared_ptr<ValueBlocks> live;
+               struct Done {
+                 std::shared_ptr<ValueBlocks>& c;
+                 ~Done() {
+                   if (c) c->valid = false;
+                 }
+               } done{live};
+               fn(py::bytes(k, (size_t)kb), value_arg(r, mv, nv, vb, &live), kvref(kv));
              });
            })
       .def("compress",
@@ -424,7 +476,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              py::gil_scoped_release nogil;
              return r.compress([&](char* k, int kb, char* mv, int nv, int* vb, KeyValue& kv) {
                py::gil_scoped_acquire g;
-               fn(py::bytes(k, (size_t)kb), value_list(r, mv, nv, vb), kvref(kv));
+               std::shared_ptr<ValueBlocks> live;
+               struct Done {
+                 std::shared_ptr<ValueBlocks>& c;
+                 ~Done() {
+                   if (c) c->valid = false;
+                 }
+               } done{live};
+               fn(py::bytes(k, (size_t)kb), value_arg(r, mv, nv, vb, &live), kvref(kv));
              });
            })
       .def("reduce_builtin", &MR::reduce_builtin, py::call_guard<py::gil_scoped_release>())

@@ -568,8 +568,7 @@ at::Tensor raw_keys_u64(const KV& kv, int mode, bool desc, const at::Tensor& dat
   for (int64_t i = 0; i < n; ++i) {
     uint64_t raw = 0;
     for (int b = 0; b < w; ++b) raw |= (uint64_t)d[i * w + b] << (8 * b);
-    uint64_t kk = dev::sortkey_transform(raw, mode);
-    kp[i] = desc ? ~kk : kk;
+    kp[i] = dev::sortkey(raw, mode, desc);
     ip[i] = (uint32_t)i;
   }
   return keys;

@@ -330,25 +330,37 @@ void* arena_take(Dev& d, int64_t bytes, hipStream_t stream, Seg** seg, int64_t* 
   return sg->base + o;
 }
 
-// segments with nothing in use go back to the driver (after their last users)
-void release_free_segments(Dev& d) {  // g_mu held
+// segments with nothing in use leave the pool's books (g_mu held); the caller
+// hands them back to the driver with free_segments() AFTER dropping g_mu: the
+// waits for their last users and the synchronous hipFree would otherwise stall
+// every allocation and free of every thread and stream behind them
+std::vector<std::unique_ptr<Seg>> detach_free_segments(Dev& d) {  // g_mu held
+  std::vector<std::unique_ptr<Seg>> out;
   for (size_t i = 0; i < d.segs.size();) {
     Seg* sg = d.segs[i].get();
     if (sg->free_bytes != sg->size) {
       ++i;
       continue;
     }
-    for (auto& [o, fr] : sg->free) {
-      for (auto& e : fr.evs)
-        if (hipEventSynchronize(e->e) != hipSuccess) (void)hipGetLastError();
-      d.by_size.erase({fr.size, sg, o});
-    }
-    if (hipFree(sg->base) != hipSuccess) (void)hipGetLastError();
+    for (auto& [o, fr] : sg->free) d.by_size.erase({fr.size, sg, o});
     d.big_bytes -= sg->size;
     d.big_free -= sg->size;
+    out.push_back(std::move(d.segs[i]));
     d.segs.erase(d.segs.begin() + (std::ptrdiff_t)i);
     ++d.releases;
   }
+  return out;
+}
+
+// g_mu NOT held: wait for each detached segment's last users, then free it
+void free_segments(std::vector<std::unique_ptr<Seg>>& segs) {
+  for (auto& sg : segs) {
+    for (auto& [o, fr] : sg->free)
+      for (auto& e : fr.evs)
+        if (hipEventSynchronize(e->e) != hipSuccess) (void)hipGetLastError();
+    if (hipFree(sg->base) != hipSuccess) (void)hipGetLastError();
+  }
+  segs.clear();
 }
 
 void* pool_alloc(size_t size, int dev, hipStream_t stream) {
@@ -361,7 +373,7 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
   }();
   hipMemPool_t pool;
   {
-    std::lock_guard<std::mutex> l(g_mu);
+    std::unique_lock<std::mutex> l(g_mu);
     Dev& d = g_dev[dev];
     if (fault_armed) {  // MRH_FAULT=hip:pool:<rank>[:nth]: the nth allocation finds the pool faulted
       try {
@@ -387,14 +399,21 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
       void* p = arena_take(d, bb, stream, &sg, &off);
       if (!p && !d.fault.empty()) TORCH_CHECK(false, "mrhip page pool: device ", dev, " faulted: ", d.fault);
       if (!p) {
-        // a new segment: first hand back what the pool holds beyond 1.5x its use
+        // a new segment: first hand back what the pool holds beyond 1.5x its
+        // use. The driver calls (waits for the freed segments' users,
+        // hipFree, hipMalloc) run with g_mu dropped; the block's bytes are
+        // counted in use meanwhile so concurrent allocations see them
+        std::vector<std::unique_ptr<Seg>> drop;
         if (pool_reserved(d) + std::max(bb, kSegMin) > (d.in_use + bb) * 3 / 2) {
-          release_free_segments(d);
+          drop = detach_free_segments(d);
           if (d.cached > (int64_t(1) << 30)) release_cached(d);
         }
+        d.in_use += bb;
         const auto t0 = std::chrono::steady_clock::now();
         int64_t segsz = std::max(bb, kSegMin);
         char* base = nullptr;
+        l.unlock();
+        free_segments(drop);
         hipError_t e = hipMalloc((void**)&base, (size_t)segsz);
         if (e != hipSuccess && segsz > bb) {  // no room for the margin: exactly the block
           (void)hipGetLastError();
@@ -403,18 +422,30 @@ void* pool_alloc(size_t size, int dev, hipStream_t stream) {
         }
         if (e != hipSuccess) {  // everything idle back to the driver, then once more
           (void)hipGetLastError();
+          l.lock();
           ++d.oom_retries;
-          release_free_segments(d);
+          drop = detach_free_segments(d);
           release_cached(d);
+          l.unlock();
+          free_segments(drop);
           const hipError_t se = hipDeviceSynchronize();
           if (se != hipSuccess) {
             (void)hipGetLastError();
+            l.lock();
+            d.in_use -= bb;
             set_fault(d, std::string("device fault seen by an allocation retry: ") + hipGetErrorString(se));
             TORCH_CHECK(false, "mrhip page pool: device error on device ", dev, ": ", hipGetErrorString(se));
           }
-          if (d.pool) (void)hipMemPoolTrimTo(d.pool, 0);
+          hipMemPool_t hp;
+          {
+            std::lock_guard<std::mutex> g(g_mu);
+            hp = d.pool;
+          }
+          if (hp) (void)hipMemPoolTrimTo(hp, 0);
           e = hipMalloc((void**)&base, (size_t)segsz);
         }
+        l.lock();
+        d.in_use -= bb;  // counted again below, with the block
         ++d.grows;
         d.grow_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (e != hipSuccess || !base) {
@@ -703,12 +734,14 @@ int64_t set_cap(int device, int64_t cap) {
 void trim(int device, int64_t keep_bytes) {
   if (device < 0 || device >= kMaxDev) return;
   hipMemPool_t p;
+  std::vector<std::unique_ptr<Seg>> drop;
   {
     std::lock_guard<std::mutex> l(g_mu);
     p = g_dev[device].pool;
     if (p) release_cached(g_dev[device]);
-    release_free_segments(g_dev[device]);
+    drop = detach_free_segments(g_dev[device]);
   }
+  free_segments(drop);
   if (!p) return;
   // freed blocks are returned to the pool in stream order: let the device
   // drain so the trim sees them; a device fault here is the pool's too

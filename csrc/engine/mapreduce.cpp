@@ -1276,7 +1276,18 @@ uint64_t MapReduce::reduce_builtin(const std::string& op, const std::string& dty
   OpTrace tr_(__func__, this);
   enter(__func__, true, false, kmv_part_count() > 1);
   need_kmv("reduce");
-  if (kmv_part_count() > 1 || needs_ooc(kmv->nbytes(), budget(), 2.0)) {
+  if (kmv_part_count() > 1 && budget() <= 0) {
+    // parts left by an out-of-core convert, but no budget now (it was lowered
+    // to 0 = unlimited): each part reduced whole on the engine device (the
+    // block path would cut pieces of env.hbm / 4 = 1 byte)
+    std::vector<KV> outs;
+    for (const KMV& m : kmv_parts()) {
+      const KMV dm = m.seg.device() == device() ? m : kmv_to(m, device(), false);
+      outs.push_back(oom_retry(this, device(), my_proc(), "reduce_builtin",
+                               [&] { return mrh::reduce_builtin(dm, op, dtype.empty() ? "int32" : dtype); }));
+    }
+    set_kv_parts(std::move(outs));
+  } else if (kmv_part_count() > 1 || needs_ooc(kmv->nbytes(), budget(), 2.0)) {
     // values stream through HBM in budget-sized key ranges, part by part
     OocStats os;
     std::vector<KV> outs;

@@ -95,11 +95,19 @@ MRH_HD inline uint64_t sortkey_transform(uint64_t raw, int mode) {
     case 1: return (uint64_t)((uint32_t)raw ^ 0x80000000u);           // int32
     case 3: {                                                         // float
       uint32_t u = (uint32_t)raw;
+      // the reference's comparator (src/mapreduce.cpp:2736-2752) has -0.0 ==
+      // +0.0: one key, so a stable sort keeps their input order; every NaN
+      // is one key above +inf (numpy's order: NaNs last)
+      if ((u & 0x7fffffffu) == 0) u = 0;
+      else if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) u = 0x7fc00000u;
       u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
       return u;
     }
     case 4: {                                                         // double
       uint64_t u = raw;
+      if ((u & 0x7fffffffffffffffull) == 0) u = 0;
+      else if ((u & 0x7ff0000000000000ull) == 0x7ff0000000000000ull && (u & 0x000fffffffffffffull))
+        u = 0x7ff8000000000000ull;
       u = (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
       return u;
     }
@@ -107,6 +115,22 @@ MRH_HD inline uint64_t sortkey_transform(uint64_t raw, int mode) {
     case 8: return (uint32_t)raw;                                     // uint32
     default: return raw;                                              // raw / uint64
   }
+}
+
+// the radix key of one fixed-width value for flag `mode`, descending when
+// `desc`: the complement of the ascending key, except that NaN (flags 3 and
+// 4) stays the largest key — NaNs sort last in both directions, like
+// numpy / pandas (the reference's comparators leave NaN order undefined)
+MRH_HD inline bool sortkey_is_nan_key(uint64_t k, int mode) {
+  return (mode == 3 && k == (uint64_t)(0x7fc00000u | 0x80000000u)) ||
+         (mode == 4 && k == (0x7ff8000000000000ull | 0x8000000000000000ull));
+}
+MRH_HD inline uint64_t sortkey(uint64_t raw, int mode, bool desc) {
+  const uint64_t k = sortkey_transform(raw, mode);
+  if (!desc) return k;
+  // all ones: above every complemented key in the low 32 bits (a 4-byte
+  // column's sort) and in all 64
+  return sortkey_is_nan_key(k, mode) ? ~uint64_t(0) : ~k;
 }
 
 }  // namespace dev

@@ -29,9 +29,7 @@ __global__ __launch_bounds__(NT) void k_sortkeys_fixed(const uint8_t* __restrict
   if (w == 8) raw = *reinterpret_cast<const uint64_t*>(d + i * 8);
   else if (w == 4) raw = *reinterpret_cast<const uint32_t*>(d + i * 4);
   else raw = load_le(d + i * w, w);
-  uint64_t k = dev::sortkey_transform(raw, mode);
-  if (desc) k = ~k;
-  keys[i] = k;
+  keys[i] = dev::sortkey(raw, mode, desc);
   idx[i] = (uint32_t)i;
 }
 

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import pickle
 
-from .runtime.mapreduce import MapReduce
+from .runtime.mapreduce import BlockMultiValue, MapReduce
 
 
 def _dumps(x) -> bytes:
@@ -38,6 +38,7 @@ class mrmpi:  # noqa: N801  (reference class name)
         self.mr = MapReduce(comm)
         self.name = name
         self._kv = None
+        self._blocks = None  # the multi-block key of the running reduce / compress
 
     # ---------------------------------------------------------------- lifecycle
     def destroy(self):
@@ -129,13 +130,27 @@ class mrmpi:  # noqa: N801  (reference class name)
         return self.mr.map_mr(mr.mr, lambda i, k, v, kv: self._with(kv, f, i, _loads(k), _loads(v), self),
                               addflag=addflag)
 
+    def _kmv_call(self, f):
+        """reduce / compress callback: a key whose values span several pages
+        arrives as the reference's multi-block protocol (mvalue == [], i.e.
+        nvalues == 0; reference src/mapreduce.cpp:1828-1848): the callback
+        walks it with multivalue_blocks() / multivalue_block(i), one page of
+        unpickled values at a time — never one list of every value"""
+        def call(k, vals, kv):
+            if isinstance(vals, BlockMultiValue):
+                self._blocks = vals
+                try:
+                    return self._with(kv, f, _loads(k), [], self)
+                finally:
+                    self._blocks = None
+            return self._with(kv, f, _loads(k), [_loads(v) for v in vals], self)
+        return call
+
     def reduce(self, reduce, ptr=None):
-        f = self._cb(reduce, ptr, 3)
-        return self.mr.reduce(lambda k, vals, kv: self._with(kv, f, _loads(k), [_loads(v) for v in vals], self))
+        return self.mr.reduce(self._kmv_call(self._cb(reduce, ptr, 3)))
 
     def compress(self, compress, ptr=None):
-        f = self._cb(compress, ptr, 3)
-        return self.mr.compress(lambda k, vals, kv: self._with(kv, f, _loads(k), [_loads(v) for v in vals], self))
+        return self.mr.compress(self._kmv_call(self._cb(compress, ptr, 3)))
 
     def scan_kv(self, scan, ptr=None):
         f = self._cb(scan, ptr, 2)
@@ -146,10 +161,21 @@ class mrmpi:  # noqa: N801  (reference class name)
         return self.mr.scan_kmv(lambda k, vals: f(_loads(k), [_loads(v) for v in vals]))
 
     def multivalue_blocks(self, mvalue=None):
-        return 1 if mvalue is None else self.mr.multivalue_blocks(mvalue)[1]
+        """blocks of the current key: its page count inside a reduce /
+        compress callback of a multi-block key (reference
+        python/mrmpi.py:335-337), else 1"""
+        b = getattr(self, "_blocks", None)
+        if b is not None:
+            return b.nblocks()
+        return 1
 
-    def multivalue_block(self, iblock, mvalue):
-        return mvalue if iblock == 0 else []
+    def multivalue_block(self, iblock, mvalue=None):
+        """the unpickled values of block `iblock` of the current multi-block
+        key (one engine page); for an ordinary key block 0 is `mvalue`"""
+        b = getattr(self, "_blocks", None)
+        if b is not None:
+            return [_loads(v) for v in b.block(iblock)]
+        return (mvalue or []) if iblock == 0 else []
 
     # ---------------------------------------------------------------- sorting
     def sort_keys(self, compare):

@@ -70,6 +70,37 @@ class MultiValue(list):
     def block(self, i):
         return self[i * self.block_size:(i + 1) * self.block_size]
 
+    @staticmethod
+    def of(vals):
+        """a callback's values: a list, or the engine's multi-block cursor"""
+        return BlockMultiValue(vals) if isinstance(vals, C.ValueBlocks) else MultiValue(vals)
+
+
+class BlockMultiValue:
+    """The values of a key that spans several pages (the engine's multi-block
+    KMV, reference src/mapreduce.cpp:1828-1848): never one list — block(i)
+    materialises one page of values (bytes objects) through the engine's
+    multivalue_block; iteration walks the blocks in order. Valid only inside
+    the reduce / compress callback it was passed to."""
+
+    block_size = None  # set by the engine (the page size), not by the caller
+
+    def __init__(self, blocks):
+        self._b = blocks
+
+    def __len__(self):
+        return int(self._b.nvalues)
+
+    def nblocks(self):
+        return int(self._b.nblocks)
+
+    def block(self, i):
+        return self._b.block(int(i))
+
+    def __iter__(self):
+        for i in range(self.nblocks()):
+            yield from self._b.block(i)
+
 
 class _Counters(type):
     """MapReduce.cssize etc. read the native static counters
@@ -239,7 +270,7 @@ class MapReduce(metaclass=_Counters):
             op, _, dtype = fn.partition(":")
             return self._m.reduce_builtin(op, dtype or "int32")
         f = _bind(fn, 3, ptr)
-        return self._m.reduce(lambda k, vals, h: f(k, MultiValue(vals), KeyValue.wrap(h)))
+        return self._m.reduce(lambda k, vals, h: f(k, MultiValue.of(vals), KeyValue.wrap(h)))
 
     def reduce_batch(self, fn, ptr=None):
         """Device-tier reduce: fn(kmv, kv[, ptr]) gets the whole native KMV
@@ -253,7 +284,7 @@ class MapReduce(metaclass=_Counters):
             op, _, dtype = fn.partition(":")
             return self._m.compress_builtin(op, dtype or "int32")
         f = _bind(fn, 3, ptr)
-        return self._m.compress(lambda k, vals, h: f(k, MultiValue(vals), KeyValue.wrap(h)))
+        return self._m.compress(lambda k, vals, h: f(k, MultiValue.of(vals), KeyValue.wrap(h)))
 
     def scan_kv(self, fn, ptr=None):
         """Read-only fn(key, value[, ptr]) over the KV (reference :1933-1976)."""
@@ -269,13 +300,13 @@ class MapReduce(metaclass=_Counters):
 
     # multi-block KMV iteration for Python callbacks: values arrive as a whole
     # list; these give the reference's block view of it
-    def multivalue_blocks(self, mv: MultiValue):
+    def multivalue_blocks(self, mv):
         return len(mv), mv.nblocks()
 
     def multivalue_block_select(self, which):
         pass
 
-    def multivalue_block(self, mv: MultiValue, iblock):
+    def multivalue_block(self, mv, iblock):
         return mv.block(iblock)
 
     # ------------------------------------------------------------------ sorting

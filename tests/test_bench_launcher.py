@@ -15,19 +15,30 @@ ARGS = ["--bytes-per-gpu", "4e6", "--file-bytes", "1000000", "--steps", "1", "--
         "--pagerank-scale", "10", "--pagerank-steps", "1"]
 
 
-def _bench(n):
+def _bench(n, tmp, extra=()):
+    """the printed line merged over the detail file (the full record)"""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env["HIP_VISIBLE_DEVICES"] = ""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), *ARGS], cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=300)
+    detail = os.path.join(str(tmp), f"detail_{n}.json")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), *ARGS, *extra,
+                        "--detail-out", detail], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 prints exactly one JSON line
-    return json.loads(lines[0])
+    line = json.loads(lines[0])
+    # the printed line stays small enough for a driver's stdout tail
+    assert len(lines[0]) < 4000, len(lines[0])
+    assert line["detail_file"] == detail
+    with open(detail) as f:
+        full = json.load(f)
+    return {**full, **line}
 
 
-def test_bench_spawns_n_ranks():
-    one, three = _bench(1), _bench(3)
+def test_bench_spawns_n_ranks(tmp_path):
+    # the big in-HBM tri_find_mr run (BASELINE config 5 through the MapReduce
+    # engine: RMAT-24 on 8 GPUs) rehearsed at a small scale on 1 and 3 ranks
+    big = ("--trifind-mr-big-scale", "11")
+    one, three = _bench(1, tmp_path, big), _bench(3, tmp_path, big)
     assert one["n_gpus"] == 1 and one["ranks_joined"] == 1
     assert three["n_gpus"] == 3 and three["ranks_joined"] == 3
     assert three["config"]["parallelism"] == "dp3"
@@ -48,12 +59,19 @@ def test_bench_spawns_n_ranks():
         assert not [k for k in rec if k.endswith("_error")], [k for k in rec if k.endswith("_error")]
         assert rec["trifind_mr_triangles"] == rec["trifind_mr_triangles_check"] > 0
         assert "ms_per_step" in rec["with_file_io"] and "ms_per_step" in rec["wordfreq_with_file_io"]
+        # driver-visible (printed) keys of every BASELINE config
+        for k in ("pagerank_ms", "pagerank_setup_ms", "trifind_ms", "trifind_triangles", "trifind_mr_ms",
+                  "trifind_mr_big_ms", "trifind_mr_big_triangles_ok", "wordfreq_ms", "wordfreq_shuffle_ms",
+                  "with_file_io_ms", "wordfreq_with_file_io_ms"):
+            assert k in rec, k
+        assert rec["trifind_mr_big_scale"] == 11 and rec["trifind_mr_big_triangles_ok"] is True
+        assert rec["trifind_mr_big"]["triangles"] == one["trifind_mr_big"]["triangles"] > 0  # same graph
 
 
-def test_bench_eight_ranks():
+def test_bench_eight_ranks(tmp_path):
     """the driver's largest scaling point, N = 8 (one node), rehearsed on the
     CPU engine: 8 ranks join, global counts are 8x, PageRank keeps its graph"""
-    one, eight = _bench(1), _bench(8)
+    one, eight = _bench(1, tmp_path), _bench(8, tmp_path)
     assert eight["n_gpus"] == eight["ranks_joined"] == 8 and eight["config"]["parallelism"] == "dp8"
     assert eight["kv_pairs_per_step"] == 8 * one["kv_pairs_per_step"]
     assert eight["pagerank_config"]["edges"] == one["pagerank_config"]["edges"]
@@ -85,7 +103,9 @@ def test_bench_two_ranks_on_one_gpu():
         assert r.returncode == 0, r.stderr[-3000:]
         lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
         assert len(lines) == 1, r.stdout
-        out[n] = json.loads(lines[0])
+        line = json.loads(lines[0])
+        with open(line["detail_file"]) as f:
+            out[n] = {**json.load(f), **line}
     one, two = out[1], out[2]
     assert two["n_gpus"] == two["ranks_joined"] == 2 and two["backend"]["torch.distributed"].startswith("gloo")
     # ranks share the GPU: the engine runs the pg transport; the RCCL facts come

@@ -17,6 +17,7 @@ import torch
 
 import gpu_mapreduce_amd as g
 from gpu_mapreduce_amd import MapReduce
+from gpu_mapreduce_amd.runtime.mapreduce import BlockMultiValue
 
 HOT = 7
 BUDGET = 4 << 20          # hot key: 4.5 M x 8 B = 36 MB = 8.6 x the budget, past the op cap of 24 MiB
@@ -90,17 +91,19 @@ def _run(dev, tmp_path):
 
     def red(k, mv, kv):
         key = struct.unpack("<q", k)[0]
-        mv.block_size = PAGE // 8
         n, s = 0, 0
         for b in range(mr.multivalue_blocks(mv)[1]):
             blk = mr.multivalue_block(mv, b)
+            assert len(blk) * 8 <= PAGE or not isinstance(mv, BlockMultiValue)  # one engine page at a time
             n += len(blk)
             s += int(np.frombuffer(b"".join(blk), dtype=np.int64).sum())
-        blocks[key] = mv.nblocks()
+        blocks[key] = (mv.nblocks(), isinstance(mv, BlockMultiValue))
         kv.add(k, struct.pack("<qq", n, s))
     mr.reduce(red)
     assert _pairs(mr, "<qq") == {k: (w[0], w[1]) for k, w in want.items()}
-    assert blocks[HOT] >= 8
+    # the hot key came as the engine's page cursor, never one list
+    assert blocks[HOT][0] >= 8 and blocks[HOT][1], blocks[HOT]
+    assert not any(isb for k, (nb, isb) in blocks.items() if k != HOT)
 
     # collate -> builtin reduces: a partial carried across the hot key's blocks
     for op, fmt, pick in (("count", "<i", lambda w: (w[0],)), ("sum:int64", "<q", lambda w: (w[1],)),
@@ -145,3 +148,49 @@ def test_ooc_hot_key_cpu(tmp_path):
 @pytest.mark.gpu
 def test_ooc_hot_key_gpu(tmp_path):
     _run("cuda:0", tmp_path)
+
+
+def test_mrmpi_hot_key_blocks(tmp_path):
+    """the mrmpi wrapper (pickled keys/values): a hot key out of core reaches
+    the reduce as the reference's multi-block protocol (mvalue == []), and
+    multivalue_block(i) hands out one engine page of unpickled values at a
+    time (reference python/mrmpi.py:335-344, src/mapreduce.cpp:1874-1925)"""
+    from gpu_mapreduce_amd.mrmpi import mrmpi
+    nhot, page = 60_000, 1 << 16
+    m = mrmpi(g.Comm(device="cpu"))
+    m.mr.fpath = str(tmp_path)
+    m.mr.hbm_budget = 1 << 18
+    m.mr.host_budget = 1 << 20
+    m.mr.memsize = -page
+
+    def emit(itask, mr):
+        for i in range(itask, nhot, 4):
+            mr.add("hot", i)
+        for i in range(itask, 400, 4):
+            mr.add("k%d" % (i % 37), i)
+    m.map(4, emit)
+    m.collate()
+    seen = {}
+
+    def red(key, mvalue, mr):
+        nb = mr.multivalue_blocks()
+        if mvalue == [] and nb > 1:
+            tot, cnt, biggest = 0, 0, 0
+            for b in range(nb):
+                vals = mr.multivalue_block(b)
+                biggest = max(biggest, len(vals))
+                cnt += len(vals)
+                tot += sum(vals)
+            seen[key] = (nb, biggest)
+            mr.add(key, (cnt, tot))
+        else:
+            mr.add(key, (len(mvalue), sum(mvalue)))
+    m.reduce(red)
+    got = dict(m.pairs())
+    assert got["hot"] == (nhot, nhot * (nhot - 1) // 2)
+    assert seen["hot"][0] > 4 and seen["hot"][1] < nhot // 4, seen  # pages, not one list
+    want = {}
+    for i in range(400):
+        c, t = want.get("k%d" % (i % 37), (0, 0))
+        want["k%d" % (i % 37)] = (c + 1, t + i)
+    assert {k: v for k, v in got.items() if k != "hot"} == want

@@ -241,3 +241,19 @@ def test_ooc_distributed_pipeline_gpu(tmp_path, monkeypatch):
     HBM budget of 1/20 of the data and its pool cap (a chunk too large for
     the cap fails with "Cannot allocate page")"""
     _ooc_world(2, "cuda:0", tmp_path, monkeypatch)
+
+
+def test_reduce_after_budget_lowered_to_zero(tmp_path):
+    """an out-of-core convert leaves several KMV parts; with the budget then
+    set to 0 (unlimited) the builtin reduce takes every part whole, not the
+    block path with a piece size of budget / 4 = 0"""
+    comm = g.Comm(device="cpu")
+    mr = _tiered(comm, tmp_path, 1 << 20)
+    mr.map(3, lambda i, kv: [kv.add(w, struct.pack("<i", j)) for j, w in enumerate(WORDS[i::3])])
+    mr.convert()
+    assert mr.kmv_parts > 1
+    mr.hbm_budget = 0
+    mr.host_budget = 0
+    mr.reduce("count")
+    got = {k: struct.unpack("<i", v)[0] for k, v in mr.kv_pairs()}
+    assert got == dict(collections.Counter(WORDS))
