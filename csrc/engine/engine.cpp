@@ -10,7 +10,9 @@
 #include <ATen/hip/HIPContext.h>
 #include <algorithm>
 #include <cstring>
+#include <cstdlib>
 #include <map>
+#include <mutex>
 #include <numeric>
 #include <stdexcept>
 
@@ -250,6 +252,70 @@ KMV kmv_concat(const std::vector<KMV>& parts, at::Device dev, bool pin) {
   return out;
 }
 
+namespace {
+// MRH_STAGE_PAGEABLE=0: pageable pieces go by ATen's copy_ (the runtime's own path)
+bool stage_pageable() {
+  static const bool on = [] {
+    const char* e = std::getenv("MRH_STAGE_PAGEABLE");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+// Pageable host data (a disk-tier piece: a memory-mapped spool file) goes to
+// the device through this ring of pinned staging buffers: memcpy into a free
+// buffer, hipMemcpyAsync from it, an event per buffer. A hipMemcpyAsync
+// straight from pageable memory has the runtime pin the pages (or stage) on
+// every call; after a job that held ~180 GB of HBM that path ran ~2x slower
+// and made the out-of-core collate's disk-tier partitions host-bound
+// (docs/round6.md).
+class StageRing {
+ public:
+  static StageRing& get() {
+    static StageRing* r = new StageRing();  // never destroyed (pinned memory, events)
+    return *r;
+  }
+  void copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    std::lock_guard<std::mutex> l(mu_);
+    init();
+    const char* p = static_cast<const char*>(src);
+    char* d = static_cast<char*>(dst);
+    while (bytes > 0) {
+      Buf& b = bufs_[next_++ % bufs_.size()];
+      if (b.used && hipEventSynchronize(b.ev) != hipSuccess) throw std::runtime_error("mrhip: staging wait failed");
+      const size_t n = std::min(bytes, kBuf);
+      std::memcpy(b.p, p, n);
+      if (hipMemcpyAsync(d, b.p, n, hipMemcpyHostToDevice, s) != hipSuccess ||
+          hipEventRecord(b.ev, s) != hipSuccess)
+        throw std::runtime_error("mrhip: staged host to device copy failed");
+      b.used = true;
+      p += n;
+      d += n;
+      bytes -= n;
+    }
+  }
+
+ private:
+  static constexpr size_t kBuf = size_t(8) << 20;
+  struct Buf {
+    void* p = nullptr;
+    hipEvent_t ev = nullptr;
+    bool used = false;
+  };
+  void init() {
+    if (!bufs_.empty()) return;
+    bufs_.resize(4);
+    for (Buf& b : bufs_) {
+      if (hipHostMalloc(&b.p, kBuf, hipHostMallocDefault) != hipSuccess ||
+          hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess)
+        throw std::runtime_error("mrhip: staging ring allocation failed");
+    }
+  }
+  std::mutex mu_;
+  std::vector<Buf> bufs_;
+  size_t next_ = 0;
+};
+}  // namespace
+
 KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at::Tensor>* hold) {
   std::vector<KV> parts;
   for (const KV& p : parts_in)
@@ -281,6 +347,8 @@ KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at
         if (hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nb, hipMemcpyHostToDevice, cs) != hipSuccess)
           throw std::runtime_error("mrhip: host to device copy failed");
         hold->push_back(src);
+      } else if (hold && src.is_cpu() && src.is_contiguous() && dst.is_contiguous() && stage_pageable()) {
+        StageRing::get().copy(dst.data_ptr(), src.data_ptr(), (size_t)src.numel() * src.element_size(), cs);
       } else {
         dst.copy_(src, /*non_blocking=*/true);
       }

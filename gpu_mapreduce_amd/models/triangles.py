@@ -170,44 +170,6 @@ def bench_trifind_mr(comm, args):
         "wedge_pairs": max((s["pairs_out"] for s in r["stages"] if s["op"] == "reduce nsq_angles"), default=0),
         "compact_vb": int(r.get("compact_vb", 0)),
     }
-    oscale = getattr(args, "mr_ooc_scale", 0) or 0
-    if oscale > 0:
-        root = tempfile.mkdtemp(prefix=f"mrh_trimr_{me}_")
-        try:
-            e2 = edges_of(oscale)
-            want2 = TriangleGraph(comm, e2, 1 << oscale).count()
-            budget = int(getattr(args, "mr_ooc_hbm", 256 << 20))
-            host = int(getattr(args, "mr_ooc_host", 2 << 30))
-            # pages of the reference's default memsize (64 MB): spool pieces of
-            # min(page, budget / 4) = 64 MiB. Run twice: the first (cold) run
-            # also pays the pinned host allocations the caching host allocator
-            # keeps for later jobs; the record's numbers are the second run's
-            dts = []
-            for _ in range(2):
-                sync()
-                t0 = time.perf_counter()
-                r2 = tri_find_mr(comm, e2, hbm_budget=budget, host_budget=host, fpath=root, memsize=64)
-                sync()
-                dts.append(comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64))
-            dt2 = dts[-1]
-            out["ooc"] = {"note": "run before the in-HBM big graph: after that job (a ~180 GB peak) the same "
-                                  "out-of-core run measured 850-913 ms instead of ~587 ms on this box, with or "
-                                  "without a pool trim and an emptied pinned host cache (tools/trimr_time.py BIG=22)",
-                          "scale": oscale, "ms": dt2 * 1e3, "ms_cold": dts[0] * 1e3, "triangles": int(r2["triangles"]),
-                          "triangles_check": int(want2), "hbm_budget": budget, "host_budget": host,
-                          "spool_files": r2["spool_files"], "spool_host_bytes": r2["spool_host_bytes"],
-                          "spool_disk_bytes": r2["spool_disk_bytes"],
-                          # per stage: host <-> device bytes of this rank, and
-                          # the time at the PCIe floor (50 GB/s) they imply;
-                          # disk_bytes: spool / result files written (the disk tier)
-                          "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"],
-                                      "pcie_bytes": s["h2d_bytes"] + s["d2h_bytes"],
-                                      "pcie_floor_ms": round((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 3),
-                                      "x_floor": round(s["ms"] / max((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 1e-3), 2),
-                                      "disk_bytes": s["disk_bytes"]}
-                                     for s in r2["stages"]]}
-        finally:
-            shutil.rmtree(root, ignore_errors=True)
     bscale = getattr(args, "mr_big_scale", 0) or 0
     if bscale > 0:
         # a larger graph in HBM: R-MAT-22's ~7 G wedge pairs go through collate
@@ -228,4 +190,40 @@ def bench_trifind_mr(comm, args):
                       "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"],
                                   "pairs_out": s["pairs_out"]} for s in rb["stages"]]}
         del eb
+    oscale = getattr(args, "mr_ooc_scale", 0) or 0
+    if oscale > 0:
+        root = tempfile.mkdtemp(prefix=f"mrh_trimr_{me}_")
+        try:
+            e2 = edges_of(oscale)
+            want2 = TriangleGraph(comm, e2, 1 << oscale).count()
+            budget = int(getattr(args, "mr_ooc_hbm", 256 << 20))
+            host = int(getattr(args, "mr_ooc_host", 2 << 30))
+            # pages of the reference's default memsize (64 MB): spool pieces of
+            # min(page, budget / 4) = 64 MiB. Run twice: the first (cold) run
+            # also pays the pinned host allocations the caching host allocator
+            # keeps for later jobs; the record's numbers are the second run's
+            dts = []
+            for _ in range(2):
+                sync()
+                t0 = time.perf_counter()
+                r2 = tri_find_mr(comm, e2, hbm_budget=budget, host_budget=host, fpath=root, memsize=64)
+                sync()
+                dts.append(comm.allreduce(time.perf_counter() - t0, "max", dtype=torch.float64))
+            dt2 = dts[-1]
+            out["ooc"] = {"note": "run after the in-HBM big graph (its ~180 GB pool peak)",
+                          "scale": oscale, "ms": dt2 * 1e3, "ms_cold": dts[0] * 1e3, "triangles": int(r2["triangles"]),
+                          "triangles_check": int(want2), "hbm_budget": budget, "host_budget": host,
+                          "spool_files": r2["spool_files"], "spool_host_bytes": r2["spool_host_bytes"],
+                          "spool_disk_bytes": r2["spool_disk_bytes"],
+                          # per stage: host <-> device bytes of this rank, and
+                          # the time at the PCIe floor (50 GB/s) they imply;
+                          # disk_bytes: spool / result files written (the disk tier)
+                          "stages": [{"op": s["op"], "ms": round(s["ms"], 3), "pairs_in": s["pairs_in"],
+                                      "pcie_bytes": s["h2d_bytes"] + s["d2h_bytes"],
+                                      "pcie_floor_ms": round((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 3),
+                                      "x_floor": round(s["ms"] / max((s["h2d_bytes"] + s["d2h_bytes"]) / 50e6, 1e-3), 2),
+                                      "disk_bytes": s["disk_bytes"]}
+                                     for s in r2["stages"]]}
+        finally:
+            shutil.rmtree(root, ignore_errors=True)
     return out

@@ -43,6 +43,24 @@ if os.environ.get("BIG"):  # first the bench's in-HBM run at scale BIG (the pool
     if os.environ.get("TRIM") == "2":  # the pinned host blocks cached by the caching host allocator too
         torch._C._host_emptyCache()
         print("host cache emptied", flush=True)
+if os.environ.get("COPYBW") == "1":  # pinned <-> HBM copy rates in this process state
+    import time
+    h = torch.empty(1 << 30, dtype=torch.uint8, pin_memory=True)
+    dv = torch.empty(1 << 30, dtype=torch.uint8, device=comm.device)
+    for name, f in (("H2D", lambda: dv.copy_(h, non_blocking=True)), ("D2H", lambda: h.copy_(dv, non_blocking=True))):
+        f()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        print(f"copy {name} 1 GiB pinned: {3 * (1 << 30) / (time.perf_counter() - t0) / 1e9:.1f} GB/s", flush=True)
+    t0 = time.perf_counter()
+    for _ in range(20):
+        x = torch.empty(64 << 20, dtype=torch.uint8, pin_memory=True)
+        del x
+    print(f"pinned 64 MiB alloc+free (caching host allocator): {(time.perf_counter() - t0) / 20 * 1e3:.2f} ms", flush=True)
+    del h, dv
 kv = C.map_rmat((1 << scale) * 16, scale, *GRAPH500, 0.0, 1, 0, comm.device)
 if os.environ.get("BIG"):
     import resource
