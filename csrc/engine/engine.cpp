@@ -26,6 +26,7 @@ namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream(); }
 
+
 at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions().device(d).dtype(t); }
 
 at::Tensor scratch(size_t bytes, at::Device d) {
@@ -46,6 +47,28 @@ T* P0(const at::Tensor& t) {  // pointer even for empty tensors with storage
 int64_t scalar_i64(const at::Tensor& t, int64_t i) { return t[i].item<int64_t>(); }
 
 }  // namespace
+
+// a few device scalars to the host with one stream synchronisation: each
+// copied into this thread's pinned staging words (no ATen cat / to / item)
+void read_small(hipStream_t s, std::initializer_list<SmallRead> items) {
+  static thread_local void* stage = nullptr;
+  constexpr size_t kStage = 512;
+  if (!stage && hipHostMalloc(&stage, kStage, hipHostMallocDefault) != hipSuccess)
+    throw std::runtime_error("mrhip: pinned staging for scalar reads failed");
+  size_t off = 0;
+  for (const SmallRead& r : items) {
+    if (off + r.bytes > kStage) throw std::runtime_error("mrhip: read_small: too many bytes");
+    if (hipMemcpyAsync(static_cast<char*>(stage) + off, r.src, r.bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
+      throw std::runtime_error("mrhip: read_small copy failed");
+    off += (r.bytes + 7) & ~size_t(7);
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) throw std::runtime_error("mrhip: read_small sync failed");
+  off = 0;
+  for (const SmallRead& r : items) {
+    std::memcpy(r.dst, static_cast<char*>(stage) + off, r.bytes);
+    off += (r.bytes + 7) & ~size_t(7);
+  }
+}
 
 int64_t KV::nbytes() const {
   int64_t b = key_bytes() + value_bytes();
@@ -144,6 +167,37 @@ at::Tensor cat_maybe_pinned(const std::vector<at::Tensor>& ts, at::Device dev, a
 void concat_col(const std::vector<const at::Tensor*>& datas, const std::vector<const at::Tensor*>& offs,
                 const std::vector<int64_t>& ns, bool fixed, at::Device dev, at::Tensor* data_out,
                 at::Tensor* off_out, bool pin) {
+  // every part already on the device: the data by one D2D copy per part
+  // straight into place, each part's offsets rebased into place by one
+  // add kernel (ATen's add + cat were two kernels and a temporary per part)
+  bool on_dev = dev.is_cuda() && !datas.empty();
+  for (size_t i = 0; i < datas.size() && on_dev; ++i)
+    on_dev = datas[i]->device() == dev && datas[i]->is_contiguous() &&
+             (fixed || (offs[i]->device() == dev && offs[i]->is_contiguous() && offs[i]->scalar_type() == at::kLong));
+  if (on_dev) {
+    const hipStream_t s = cur_stream();
+    int64_t bytes = 0, rows = 0;
+    for (size_t i = 0; i < datas.size(); ++i) {
+      bytes += datas[i]->numel() * datas[i]->element_size();
+      rows += ns[i];
+    }
+    *data_out = at::empty({bytes}, opt(dev, at::kByte));
+    int64_t b = 0, r = 0;
+    for (size_t i = 0; i < datas.size(); ++i) {
+      const int64_t nb = datas[i]->numel() * datas[i]->element_size();
+      if (nb && hipMemcpyAsync(P0<uint8_t>(*data_out) + b, datas[i]->data_ptr(), (size_t)nb, hipMemcpyDeviceToDevice,
+                               s) != hipSuccess)
+        fail("concat: device copy failed");
+      if (!fixed) {
+        if (i == 0) *off_out = at::empty({rows + 1}, opt(dev, at::kLong));
+        // the last part brings its end offset too
+        k::add_i64(P0<int64_t>(*offs[i]), P0<int64_t>(*off_out) + r, ns[i] + (i + 1 == datas.size() ? 1 : 0), b, s);
+      }
+      b += nb;
+      r += ns[i];
+    }
+    return;
+  }
   std::vector<at::Tensor> d;
   for (auto* t : datas) d.push_back(t->to(dev));
   *data_out = d.empty() ? at::empty({0}, opt(dev, at::kByte)) : cat_maybe_pinned(d, dev, at::kByte, pin);
@@ -362,12 +416,12 @@ KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at
         note_xfer(o, dev);
         at::Tensor dst = off_out->narrow(0, r, p.n);
         put(dst, o);
-        if (b) dst.add_(b);
+        if (b) k::add_i64(P0<int64_t>(dst), P0<int64_t>(dst), p.n, b, cs);
       }
       b += d.numel();
       r += p.n;
     }
-    if (!fixed) off_out->narrow(0, rows, 1).fill_(b);
+    if (!fixed) k::fill_i64(P0<int64_t>(*off_out) + rows, 1, b, cs);
   };
   KV o;
   o.n = 0;
@@ -420,7 +474,7 @@ at::Tensor exclusive_scan(const at::Tensor& x_in) {
 }
 
 // uint32 (stored in kInt) exclusive scan -> n+1 uint32 (kInt)
-static at::Tensor scan_u32(const at::Tensor& x) {
+at::Tensor scan_u32(const at::Tensor& x) {
   const int64_t n = x.numel();
   const at::Device dev = x.device();
   at::Tensor out = at::empty({n + 1}, opt(dev, at::kInt));
@@ -767,6 +821,33 @@ at::Tensor segments_sorted(const at::Tensor& sorted_keys) {
 // (an R-MAT-20 edge: 20 + 20) are grouped exactly on one packed u64: no
 // 64-bit hash, no verification gather of every key, and the radix sort runs
 // only over the packed bits. Returns the packed bit count (0: not narrow).
+// per-column minima then maxima of a row-major [rows, cols] int64 matrix
+// into out[2 cols] (device: the engine's kernels and one small read; empty:
+// LLONG_MAX / LLONG_MIN)
+void col_minmax(const at::Tensor& m, int cols, int64_t* out) {
+  const int64_t rows = cols ? m.numel() / cols : 0;
+  if (m.is_cuda()) {
+    const hipStream_t s = cur_stream();
+    at::Tensor tmp = at::empty({k::minmax_scratch_words(rows, cols) + 2 * cols}, opt(m.device(), at::kLong));
+    int64_t* res = P0<int64_t>(tmp) + k::minmax_scratch_words(rows, cols);
+    k::col_minmax_i64(P0<int64_t>(m), rows, cols, P0<int64_t>(tmp), res, s);
+    if (hipMemcpyAsync(out, res, (size_t)(2 * cols) * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      fail("column range read failed");
+    return;
+  }
+  const int64_t* p = P0<int64_t>(m);
+  for (int c = 0; c < cols; ++c) {
+    out[c] = INT64_MAX;
+    out[cols + c] = INT64_MIN;
+  }
+  for (int64_t r = 0; r < rows; ++r)
+    for (int c = 0; c < cols; ++c) {
+      out[c] = std::min(out[c], p[r * cols + c]);
+      out[cols + c] = std::max(out[cols + c], p[r * cols + c]);
+    }
+}
+
 int narrow_keys(const KV& kv, at::Tensor* keys, at::Tensor* idx) {
   if (!kv.kfixed() || kv.kw <= 8 || kv.kw % 8 || kv.kw > 64 || kv.n == 0) return 0;
   if (!kv.kdata.is_contiguous() || reinterpret_cast<uintptr_t>(kv.kdata.data_ptr()) % 8 ||
@@ -775,9 +856,9 @@ int narrow_keys(const KV& kv, at::Tensor* keys, at::Tensor* idx) {
   const int nw = kv.kw / 8;
   at::Tensor words = kv.kdata.narrow(0, 0, kv.n * kv.kw).view(at::kLong).view({kv.n, nw});
   // unsigned significance: a negative word (top bit set) needs all 64 bits
-  auto [mn, mx] = at::aminmax(words, 0);
-  at::Tensor both = at::stack({mn, mx}).to(at::kCPU);
-  const int64_t* b = P0<int64_t>(both);
+  std::vector<int64_t> both(2 * nw);
+  col_minmax(words, nw, both.data());
+  const int64_t* b = both.data();
   k::PackShifts sh{};
   sh.nw = nw;
   int total = 0;
@@ -863,16 +944,16 @@ void segments_packed(const at::Tensor& sk, int vb, int sbits, int vw, uint8_t* v
   const uint64_t km = sbits >= 64 ? ~0ull : ((1ull << sbits) - 1);
   const uint64_t* w = P0<uint64_t>(sk);
   if (dev.is_cuda()) {
+    const hipStream_t s = cur_stream();
     const int64_t nt = k::seg_packed_tiles(n);
-    at::Tensor tb = at::zeros({nt + 1}, opt(dev, at::kLong));
-    k::seg_packed_count(w, n, vb, km, P0<int64_t>(tb) + 1, cur_stream());
-    at::cumsum_out(tb, tb, 0);  // tb[t] = heads before tile t
-    *nseg = tb[nt].item<int64_t>();
+    at::Tensor cnt = at::empty({nt}, opt(dev, at::kLong));
+    k::seg_packed_count(w, n, vb, km, P0<int64_t>(cnt), s);  // every tile's head count
+    at::Tensor tb = exclusive_scan(cnt);                     // tb[t] = heads before tile t, tb[nt] = all
+    read_small(s, {{P0<int64_t>(tb) + nt, nseg, 8}});
     *seg = at::empty({*nseg + 1}, opt(dev, at::kLong));
     *heads = at::empty({*nseg}, opt(dev, at::kLong));
-    seg->narrow(0, *nseg, 1).fill_(n);
-    k::seg_packed_write(w, n, vb, km, P0<int64_t>(tb), P0<int64_t>(*seg), P0<uint64_t>(*heads), vout, vw,
-                        cur_stream());
+    k::fill_i64(P0<int64_t>(*seg) + *nseg, 1, n, s);
+    k::seg_packed_write(w, n, vb, km, P0<int64_t>(tb), P0<int64_t>(*seg), P0<uint64_t>(*heads), vout, vw, s);
     return;
   }
   std::vector<int64_t> sv;
@@ -908,21 +989,44 @@ bool convert_packed_parts(std::vector<KV>& parts_io, KMV* out, ConvertStats* st)
   const bool cuda = dev.is_cuda();
   const int nw = kwidth / 8;
   int64_t n = 0;
-  std::vector<at::Tensor> mm;  // per part: key word minima, maxima, value min, max
   for (const KV& p : parts) {
     if (p.kw != kwidth || p.vw != vw || p.device() != dev) return false;
     if (!aligned(p.kdata, p.n * p.kw) || !aligned(p.vdata, p.n * vw)) return false;
-    at::Tensor kw = p.kdata.narrow(0, 0, p.n * p.kw).view(at::kLong).view({p.n, nw});
-    at::Tensor vv = p.vdata.narrow(0, 0, p.n * vw).view(vw == 8 ? at::kLong : at::kInt);
-    auto [kmn, kmx] = at::aminmax(kw, 0);
-    auto [vmn, vmx] = at::aminmax(vv);
-    mm.push_back(at::cat({kmn, kmx, vmn.to(at::kLong).view({1}), vmx.to(at::kLong).view({1})}).view({1, -1}));
     n += p.n;
   }
-  // one host sync for every part's ranges; the packing covers all of them
-  at::Tensor all = at::cat(mm).to(at::kCPU);
-  const int64_t* ap = P0<int64_t>(all);
+  // every part's key-word and value ranges into one device table, then one
+  // host sync for all of them (the engine's min/max kernels, util.hip)
   const int64_t np = (int64_t)parts.size(), row = 2 * nw + 2;
+  std::vector<int64_t> allv((size_t)(np * row));
+  {
+    int64_t scr = 0;
+    for (const KV& p : parts) scr = std::max(scr, std::max(k::minmax_scratch_words(p.n, nw), k::minmax_scratch_words(p.n, 1)));
+    if (cuda) {
+      at::Tensor table = at::empty({np * row}, opt(dev, at::kLong)), tmp = at::empty({scr}, opt(dev, at::kLong));
+      const hipStream_t s = cur_stream();
+      for (int64_t i = 0; i < np; ++i) {
+        const KV& p = parts[(size_t)i];
+        int64_t* t = P0<int64_t>(table) + i * row;
+        k::col_minmax_i64(reinterpret_cast<const int64_t*>(p.kdata.data_ptr()), p.n, nw, P0<int64_t>(tmp), t, s);
+        if (vw == 8) k::col_minmax_i64(reinterpret_cast<const int64_t*>(p.vdata.data_ptr()), p.n, 1, P0<int64_t>(tmp), t + 2 * nw, s);
+        else k::minmax_i32(reinterpret_cast<const int32_t*>(p.vdata.data_ptr()), p.n, P0<int64_t>(tmp), t + 2 * nw, s);
+      }
+      if (hipMemcpyAsync(allv.data(), table.data_ptr(), allv.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        fail("packed convert: range read failed");
+    } else {
+      for (int64_t i = 0; i < np; ++i) {
+        const KV& p = parts[(size_t)i];
+        at::Tensor kw = p.kdata.narrow(0, 0, p.n * p.kw).view(at::kLong).view({p.n, nw});
+        at::Tensor vv = p.vdata.narrow(0, 0, p.n * vw).view(vw == 8 ? at::kLong : at::kInt);
+        col_minmax(kw, nw, &allv[(size_t)(i * row)]);
+        auto [vmn, vmx] = at::aminmax(vv.to(at::kLong));
+        allv[(size_t)(i * row + 2 * nw)] = vmn.item<int64_t>();
+        allv[(size_t)(i * row + 2 * nw + 1)] = vmx.item<int64_t>();
+      }
+    }
+  }
+  const int64_t* ap = allv.data();
   std::vector<int64_t> b(row);
   for (int j = 0; j < row; ++j) {
     const bool is_min = j < nw || j == 2 * nw;
@@ -1622,13 +1726,15 @@ KV map_words(const at::Tensor& text, int64_t n) {
     k::tok_count2(P0<uint8_t>(text), n, P0<uint32_t>(cw), P0<uint32_t>(cb), s);
     at::Tensor tw = scan_u32(cw);        // u32 [nt + 1]
     at::Tensor tb = exclusive_scan(cb);  // i64 [nt + 1]
-    at::Tensor tot = at::cat({tw.narrow(0, nt, 1).to(at::kLong), tb.narrow(0, nt, 1)}).to(at::kCPU);
-    const int64_t nw = (int64_t)(uint32_t)tot.data_ptr<int64_t>()[0], kb = tot.data_ptr<int64_t>()[1];
+    uint32_t nw32 = 0;
+    int64_t kb = 0;
+    read_small(s, {{P0<uint32_t>(tw) + nt, &nw32, 4}, {P0<int64_t>(tb) + nt, &kb, 8}});
+    const int64_t nw = (int64_t)nw32;
     kv.koff = at::empty({nw + 1}, opt(dev, at::kLong));
     kv.kdata = at::empty({kb}, opt(dev, at::kByte));
     k::tok_emit2(P0<uint8_t>(text), n, P0<uint32_t>(tw), P0<int64_t>(tb), P0<int64_t>(kv.koff), P0<uint8_t>(kv.kdata),
                  s);
-    kv.koff.narrow(0, nw, 1).fill_(kb);
+    k::fill_i64(P0<int64_t>(kv.koff) + nw, 1, kb, s);
     kv.n = nw;
     return kv;
   }

@@ -19,8 +19,10 @@
 // tensor device; the CUDA branch always runs the hand-written HIP kernels.
 #pragma once
 #include <ATen/ATen.h>
+#include <hip/hip_runtime.h>
 #include <cstdint>
 #include <functional>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -66,6 +68,14 @@ KMV kmv_concat(const std::vector<KMV>& parts, at::Device dev, bool pin = false);
 // (hold set: pinned sources are copied by hipMemcpyAsync on the current
 // stream and appended to *hold, which the caller keeps until the stream passed
 // the copies)
+// device scalars read on the host with one synchronisation of stream s
+// (pinned staging; no ATen kernels): {device src, host dst, bytes}
+struct SmallRead {
+  const void* src;
+  void* dst;
+  size_t bytes;
+};
+void read_small(hipStream_t s, std::initializer_list<SmallRead> items);
 KV concat_upload(const std::vector<KV>& parts, at::Device dev, std::vector<at::Tensor>* hold = nullptr);
 KV to_var_keys(const KV& kv);
 KV to_var_values(const KV& kv);
@@ -75,6 +85,8 @@ at::Tensor fixed_offsets(int64_t n, int w, at::Device dev);
 // ------------------------------------------------------------------ primitives
 // exclusive scan returning n+1 entries (int64 result for int32/int64 input, uint32 for uint32)
 at::Tensor exclusive_scan(const at::Tensor& x);
+// uint32 flags / counts (stored as kInt) -> exclusive scan, n + 1 uint32 (kInt)
+at::Tensor scan_u32(const at::Tensor& x);
 // stable sort of (u64 key, u32 val); returns (keys_sorted, vals_sorted, passes).
 // skip_trivial: skip digit passes that are constant over all keys (costs one
 // host sync); pass false when every digit in [begin_bit, end_bit) varies

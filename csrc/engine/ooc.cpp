@@ -580,6 +580,12 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
     // a hash independent of the shuffle's owner hash (every key on this rank
     // has the same owner hash mod P): bits 20.. of the 64-bit grouping hash
     at::Tensor h = hash64_keys(c);
+    if (h.is_cuda()) {  // one kernel (util.hip) instead of shift, and, remainder and a cast
+      at::Tensor d = at::empty({h.numel()}, opt(h.device(), at::kInt));
+      k::part_of_hash(reinterpret_cast<const uint64_t*>(h.data_ptr<int64_t>()), h.numel(), 20,
+                      (uint64_t(1) << 40) - 1, M, d.data_ptr<int32_t>(), at::hip::getCurrentHIPStream());
+      return d;
+    }
     return at::remainder(at::bitwise_right_shift(h, 20).bitwise_and_((int64_t(1) << 40) - 1), M).to(at::kInt);
   }, env, st);
   clk("partition pass");

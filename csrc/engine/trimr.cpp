@@ -23,6 +23,17 @@ hipStream_t cur() { return at::hip::getCurrentHIPStream(); }
 void need(bool c, const char* m) {
   if (!c) throw std::runtime_error(std::string("mrhip: ") + m);
 }
+// zero-filled byte array: a runtime memset on the device (no ATen fill kernel)
+at::Tensor zeroed_bytes(int64_t n, at::Device dev) {
+  at::Tensor t = at::empty({n}, opt(dev, at::kByte));
+  if (dev.is_cuda()) {
+    if (n && hipMemsetAsync(t.data_ptr(), 0, (size_t)n, at::hip::getCurrentHIPStream()) != hipSuccess)
+      throw std::runtime_error("trimr: memset failed");
+  } else {
+    t.zero_();
+  }
+  return t;
+}
 }  // namespace
 
 std::pair<at::Tensor, at::Tensor> trimr_first_degree(const KMV& m) {
@@ -107,7 +118,7 @@ at::Tensor trimr_emit_compact(const KMV& m, int vb) {
   const int64_t* ek = P0<int64_t>(m.keys.kdata);
   if (dev.is_cuda()) {
     const int64_t nval = m.nval;
-    at::Tensor marked = at::zeros({m.nkey}, opt(dev, at::kByte));
+    at::Tensor marked = zeroed_bytes(m.nkey, dev);
     const int64_t nt = k::trimr_emit_tiles(nval);
     at::Tensor tcount = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kLong));
     const void* vals = m.vdata.data_ptr();
@@ -155,7 +166,7 @@ at::Tensor trimr_emit(const KMV& m, int compact_vb) {
   if (dev.is_cuda() && fixed) {
     const int64_t nval = m.nval;
     const int64_t* vals = P0<int64_t>(m.vdata);
-    at::Tensor marked = at::zeros({m.nkey}, opt(dev, at::kByte));
+    at::Tensor marked = zeroed_bytes(m.nkey, dev);
     const int64_t nt = k::trimr_emit_tiles(nval);
     at::Tensor tcount = at::empty({std::max<int64_t>(nt, 1)}, opt(dev, at::kLong));
     at::Tensor tk = at::empty({nt + 1}, opt(dev, at::kLong));

@@ -523,3 +523,35 @@ void kmeans_assign_accumulate(const float* pts, int64_t n, int D, const float* c
 void kmeans_accumulate(const float* pts, int64_t n, int D, const int64_t* idx, int K, double* acc, hipStream_t s);
 }  // namespace k
 }  // namespace mrh
+
+// ---------------------------------------------------------------- util.hip
+// Engine primitives in place of ATen expressions on hot paths (one launch or
+// two each, on the caller's stream, no host sync). The reductions need
+// minmax_scratch_words(rows, cols) int64 words of device scratch.
+namespace mrh {
+namespace k {
+int64_t minmax_scratch_words(int64_t rows, int cols);
+// per column of a row-major [rows, cols] int64 matrix (cols <= 8): out[c] =
+// min, out[cols + c] = max (rows == 0: LLONG_MAX / LLONG_MIN)
+void col_minmax_i64(const int64_t* p, int64_t rows, int cols, int64_t* scratch, int64_t* out, hipStream_t s);
+// out[0] = min, out[1] = max of int32 values (widened)
+void minmax_i32(const int32_t* p, int64_t n, int64_t* scratch, int64_t* out, hipStream_t s);
+void fill_i64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
+// dst[i] = src[i] + v (dst may be src)
+void add_i64(const int64_t* src, int64_t* dst, int64_t n, int64_t v, hipStream_t s);
+// out[i] = ((h[i] >> shift) & mask) % M
+void part_of_hash(const uint64_t* h, int64_t n, int shift, uint64_t mask, int M, int32_t* out, hipStream_t s);
+// edges [n, 2]: out[0] = min over both ends, out[1] = 1 if some a >= b, out[2] = max
+void edge_probe(const int64_t* e, int64_t n, int64_t* scratch, int64_t* out, hipStream_t s);
+// keys = [a; b], values = [b; a] (2n each)
+void edge_both_ways(const int64_t* e, int64_t n, int64_t* key, int64_t* val, hipStream_t s);
+// key = a << vb | b, value = (int32) a
+void edge_pack(const int64_t* e, int64_t n, int vb, uint64_t* key, int32_t* val, hipStream_t s);
+// value = a
+void edge_first(const int64_t* e, int64_t n, int64_t* val, hipStream_t s);
+// edge_upper (reference oink map_edge_upper): flag[i] = a != b; then the
+// flagged rows as (min, max) at pos[i] (the exclusive scan of the flags)
+void edge_ne_flags(const int64_t* e, int64_t n, uint32_t* flag, hipStream_t s);
+void edge_upper_write(const int64_t* e, int64_t n, const uint32_t* pos, int64_t* out, hipStream_t s);
+}  // namespace k
+}  // namespace mrh

@@ -165,17 +165,44 @@ __global__ __launch_bounds__(NT) void k_part_scatter(const int32_t* __restrict__
   }
 }
 
-// variable rows gathered by an int64 permutation: 16 lanes per row
+// variable rows gathered by an int64 permutation. One wave per tile of 64
+// rows copies the tile's destination bytes [doff[r0], doff[r0 + 64)) with all
+// 64 lanes busy: lane l owns byte base + l of each 64-byte step and finds its
+// row by a binary search over the tile's destination offsets (held one per
+// lane, read with shuffles). The stores of a step are one contiguous 64-byte
+// run (the 16-lanes-per-row version left 9 of 16 lanes idle on ~7-byte words
+// and scattered its stores: 61 ms for wordfreq's 1.15 G keys).
 __global__ __launch_bounds__(NT) void k_copy_var_i64(const uint8_t* __restrict__ src, const int64_t* __restrict__ soff,
                                                     const int64_t* __restrict__ perm, int64_t n,
                                                     uint8_t* __restrict__ dst, const int64_t* __restrict__ doff) {
-  const int g = threadIdx.x & 15;
-  int64_t row = ((int64_t)blockIdx.x * NT + threadIdx.x) >> 4;
-  const int64_t stride = ((int64_t)gridDim.x * NT) >> 4;
-  for (; row < n; row += stride) {
-    const int64_t r = perm[row];
-    const int64_t a = soff[r], len = soff[r + 1] - a, o = doff[row];
-    for (int64_t j = g; j < len; j += 16) dst[o + j] = src[a + j];
+  const int lane = threadIdx.x & 63;
+  const int64_t ntile = (n + 63) >> 6;
+  const int64_t nwave = ((int64_t)gridDim.x * NT) >> 6;
+  for (int64_t t = ((int64_t)blockIdx.x * NT + threadIdx.x) >> 6; t < ntile; t += nwave) {
+    const int64_t r0 = t << 6;
+    const int rows = (int)min<int64_t>(64, n - r0);
+    // this lane's row: its destination start and source start
+    int64_t dv = 0, sv = 0;
+    if (lane < rows) {
+      dv = doff[r0 + lane];
+      sv = soff[perm[r0 + lane]];
+    }
+    const int64_t d_lo = __shfl(dv, 0, 64);
+    const int64_t d_hi = doff[r0 + rows];  // same address on every lane: one broadcast load
+    for (int64_t base = d_lo; base < d_hi; base += 64) {  // uniform over the wave
+      const int64_t b = base + lane;
+      // largest row i < rows with doff[r0 + i] <= b (rows are non-empty or
+      // empty; an empty row shares its start with the next and loses the tie)
+      int lo = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const int cand = lo + step;
+        const int64_t dc = __shfl(dv, cand & 63, 64);
+        if (cand < rows && dc <= b) lo = cand;
+      }
+      const int64_t drow = __shfl(dv, lo, 64), srow = __shfl(sv, lo, 64);
+      if (b < d_hi) dst[b] = src[srow + (b - drow)];
+    }
   }
 }
 
@@ -267,7 +294,7 @@ void part_scatter(const int32_t* dest, int64_t n, int P, int nb, const int64_t* 
 void copy_var_i64(const uint8_t* src, const int64_t* soff, const int64_t* perm, int64_t n, uint8_t* dst,
                   const int64_t* doff, hipStream_t s) {
   if (n <= 0) return;
-  int64_t g = (n * 16 + NT - 1) / NT;
+  int64_t g = ((n + 63) / 64 * 64 + NT - 1) / NT;  // a wave per 64-row tile
   if (g > 65536) g = 65536;
   hipLaunchKernelGGL(k_copy_var_i64, dim3((unsigned)g), dim3(NT), 0, s, src, soff, perm, n, dst, doff);
   MRH_CHECK_LAUNCH();

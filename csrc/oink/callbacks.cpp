@@ -13,6 +13,9 @@
 #include <vector>
 
 #include "oink.h"
+#include "kernels/launch.h"
+
+#include <ATen/hip/HIPContext.h>
 
 namespace mrh {
 namespace oink {
@@ -217,6 +220,19 @@ void edge_to_vertex_pair(const KV& src, KeyValue& kv) {
 void edge_upper(const KV& src, KeyValue& kv) {
   if (!src.n) return;
   at::Tensor e = edges_of(src);
+  if (e.is_cuda() && e.is_contiguous()) {  // flags, the engine's scan, one write kernel (util.hip)
+    const hipStream_t s = at::hip::getCurrentHIPStream();
+    at::Tensor flag = at::empty({src.n}, opt(e.device(), at::kInt));
+    k::edge_ne_flags(e.data_ptr<int64_t>(), src.n, reinterpret_cast<uint32_t*>(flag.data_ptr<int32_t>()), s);
+    at::Tensor pos = scan_u32(flag);  // u32 [n + 1]
+    uint32_t m = 0;
+    read_small(s, {{reinterpret_cast<const uint32_t*>(pos.data_ptr()) + src.n, &m, 4}});
+    at::Tensor out = at::empty({(int64_t)m, 2}, opt(e.device(), at::kLong));
+    k::edge_upper_write(e.data_ptr<int64_t>(), src.n, reinterpret_cast<const uint32_t*>(pos.data_ptr()),
+                        out.data_ptr<int64_t>(), s);
+    add_tensors(kv, out);
+    return;
+  }
   at::Tensor a = e.select(1, 0), b = e.select(1, 1);
   at::Tensor keep = a != b;
   at::Tensor lo = at::minimum(a, b).index({keep}), hi = at::maximum(a, b).index({keep});

@@ -8,9 +8,17 @@
 #include "engine/tri.h"
 #include "engine/spool.h"
 #include "engine/xfer.h"
+#include "kernels/launch.h"
+
+#include <ATen/hip/HIPContext.h>
 
 namespace mrh {
 namespace oink {
+
+namespace {
+hipStream_t stream() { return at::hip::getCurrentHIPStream(); }
+at::TensorOptions like(const at::Tensor& t, at::ScalarType ty) { return at::TensorOptions().device(t.device()).dtype(ty); }
+}  // namespace
 
 TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
   TriMRRun run;
@@ -49,6 +57,12 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
     mrt.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {  // (vi, vj) and (vj, vi)
       if (!src.n) return;
       at::Tensor e = edges_of(src);
+      if (e.is_cuda() && e.is_contiguous()) {  // one kernel (util.hip), not two ATen cats of strided columns
+        at::Tensor key = at::empty({2 * src.n}, like(e, at::kLong)), val = at::empty({2 * src.n}, like(e, at::kLong));
+        k::edge_both_ways(e.data_ptr<int64_t>(), src.n, key.data_ptr<int64_t>(), val.data_ptr<int64_t>(), stream());
+        add_tensors(kv, key, val);
+        return;
+      }
       add_tensors(kv, at::cat({e.select(1, 0), e.select(1, 1)}), at::cat({e.select(1, 1), e.select(1, 0)}));
     });
   });
@@ -89,9 +103,20 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
   if (mre.kv_rows()) {
     mre.flatten();
     at::Tensor e = edges_of(*mre.kv);
-    bad = (e.select(1, 0) >= e.select(1, 1)).any().item<bool>() ? 1 : 0;
-    bad = std::max<int64_t>(bad, (e.min().item<int64_t>() < 0) ? 1 : 0);
-    vmax = e.max().item<int64_t>();
+    if (e.is_cuda() && e.is_contiguous()) {  // one pass, one small read (util.hip edge_probe)
+      const int64_t n = std::min<int64_t>(e.size(0), mre.kv->n);
+      at::Tensor tmp = at::empty({k::minmax_scratch_words(n, 3) + 3}, like(e, at::kLong));
+      int64_t* res = tmp.data_ptr<int64_t>() + k::minmax_scratch_words(n, 3);
+      k::edge_probe(e.data_ptr<int64_t>(), n, tmp.data_ptr<int64_t>(), res, stream());
+      int64_t r[3];
+      read_small(stream(), {{res, r, 24}});
+      bad = (r[1] != 0 || r[0] < 0) ? 1 : 0;
+      vmax = r[2];
+    } else {
+      bad = (e.select(1, 0) >= e.select(1, 1)).any().item<bool>() ? 1 : 0;
+      bad = std::max<int64_t>(bad, (e.min().item<int64_t>() < 0) ? 1 : 0);
+      vmax = e.max().item<int64_t>();
+    }
   }
   const bool marked_by_vertex = comm.allreduce(bad, Comm::MAX) == 0;
   vmax = comm.allreduce(vmax, Comm::MAX);
@@ -127,9 +152,19 @@ TriMRRun tri_find_mr(MapReduce& mre, MapReduce& mrt, bool upper) {
     marked.map_mr_batch(mre, [&](const KV& src, KeyValue& kv) {
       if (!src.n) return;
       at::Tensor e = edges_of(src);
-      if (compact) {
+      const bool dev = e.is_cuda() && e.is_contiguous();
+      if (compact && dev) {  // key vi << vb | vj and the vi marker in one kernel
+        at::Tensor key = at::empty({src.n}, like(e, at::kLong)), val = at::empty({src.n}, like(e, at::kInt));
+        k::edge_pack(e.data_ptr<int64_t>(), src.n, vb, reinterpret_cast<uint64_t*>(key.data_ptr<int64_t>()),
+                     val.data_ptr<int32_t>(), stream());
+        add_tensors(kv, key, val);
+      } else if (compact) {
         at::Tensor key = at::bitwise_or(at::bitwise_left_shift(e.select(1, 0), vb), e.select(1, 1));
         add_tensors(kv, key, e.select(1, 0).to(at::kInt));
+      } else if (marked_by_vertex && dev) {
+        at::Tensor val = at::empty({src.n}, like(e, at::kLong));
+        k::edge_first(e.data_ptr<int64_t>(), src.n, val.data_ptr<int64_t>(), stream());
+        add_tensors(kv, e, val);
       } else if (marked_by_vertex) {
         add_tensors(kv, e, e.select(1, 0).contiguous());
       } else {

@@ -83,26 +83,34 @@ class WordFreq:
         if not self.chunks:
             return
         wc = C.WordCounter(self.mr.device) if self.combiner else None
-        # one rank, no combiner: the pairs are grouped chunk by chunk as the
+        # no combiner, on a GPU: the pairs are grouped chunk by chunk as the
         # map emits them (the KeyValue's hash dictionary, csrc/engine/
         # grouper.h) in the shadow of the next chunk's H2D copy, so the
-        # collate's convert only ranks the groups; with several ranks the
-        # pairs are shuffled first and grouped as the exchange rounds land.
-        # A forced one-rank RCCL communicator (MRH_FORCE_RCCL=1/2) is
-        # "distributed" and takes that P > 1 route: the pairs are materialised,
-        # partitioned and sent through RCCL to this rank itself
-        group = wc is None and self.is_cuda and not self.mr.comm.native.distributed
-        self.route = "combiner" if wc is not None else ("grouped in the map" if group else "shuffle")
+        # collate's convert only ranks the groups. With several ranks each
+        # chunk's pairs are first hash-partitioned and exchanged (the chunked
+        # RCCL aggregate, as InvertedIndex does per part file) and grouped as
+        # they land, all under the next chunk's copy; the collate is then a
+        # local convert. A forced one-rank RCCL communicator (MRH_FORCE_RCCL=1/2)
+        # is "distributed" and takes that route (pairs sent to itself).
+        dist = self.mr.comm.native.distributed
+        group = wc is None and self.is_cuda
+        exchange = group and dist
+        self.route = ("combiner" if wc is not None else "exchanged per chunk" if exchange else
+                      "grouped in the map" if group else "shuffle")
+        self.exchanged = exchange
         if group:
             kv.enable_grouping()
         total = sum(t.numel() for t in self.chunks)
         reserved = [False]
+        native = self.mr.comm.native
 
         def consume(buf, n):
             if wc is not None:
                 wc.add(buf, n)
                 return
             part = C.map_words(buf, n)
+            if exchange:
+                part, _ = C.aggregate(part, native, chunk_bytes=self.mr.chunk_bytes)
             if group and not reserved[0] and part.n > 0:
                 # arenas for the whole map from the first chunk's density
                 # (+15 %); the table is sized from a sample of its words
@@ -122,6 +130,11 @@ class WordFreq:
                 consume(b, t.numel())
         else:
             self._stream_chunks(consume)
+        if exchange:
+            # lock-step exchanges: a rank with fewer chunks joins with empty parts
+            more = int(self.mr.comm.allreduce(len(self.chunks), "max")) - len(self.chunks)
+            for _ in range(more):
+                consume(torch.zeros(PAD, dtype=torch.uint8, device=self.mr.device), 0)
         if wc is not None:
             self.local_words = wc.words
             kv.add_kv(wc.finish())
@@ -201,9 +214,11 @@ class WordFreq:
             mr.reduce("sum:int32")
         else:
             # one (word, NULL) pair per occurrence through the shuffle
-            # (reference examples/wordfreq.cpp:64-67, 104-130)
+            # (reference examples/wordfreq.cpp:64-67, 104-130); exchanged
+            # chunk by chunk during the map already: the collate's aggregate
+            # is done, its convert remains
             self.nwords = self.npairs = nkv
-            self.nunique = mr.collate()
+            self.nunique = mr.convert() if getattr(self, "exchanged", False) else mr.collate()
             tick("collate")
             mr.reduce("count")
         tick("reduce")

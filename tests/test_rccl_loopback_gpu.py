@@ -72,7 +72,7 @@ def test_rccl_loopback_collectives_match_local(tmp_path):
         assert int(m["trifind_mr"][0]) == int(lo["trifind_mr"][0])
     # wordfreq without the combiner: the P > 1 route (no grouping in the map
     # shadow) with the same counts and top-10 as the local one-rank route
-    assert lr["wf_route"] == "grouped in the map" and r2["wf_route"] == r1["wf_route"] == "shuffle", (lr, r2)
+    assert lr["wf_route"] == "grouped in the map" and r2["wf_route"] == r1["wf_route"] == "exchanged per chunk", (lr, r2)
     for m, r in ((o1, r1), (o2, r2)):
         assert int(m["wf_nwords"][0]) == int(lo["wf_nwords"][0])
         assert int(m["wf_nunique"][0]) == int(lo["wf_nunique"][0])

@@ -1,0 +1,19 @@
+# GPU tests of the engine paths touched by the ATen replacement, then the ATen-window profiles again
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+o=gpurun_out/r6i; mkdir -p $o
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_kernels_gpu.py tests/test_triangles.py tests/test_wordfreq.py tests/test_outofcore.py tests/test_append_parts.py tests/test_dict_group.py tests/test_shuffle.py tests/test_sort_oracle.py > $o/tests.log 2>&1
+rc=$?; echo "tests rc=$rc" >> $o/tests.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+[ $rc -eq 0 ] || exit 1
+prof() {  # name marker-kernel command...
+  local name=$1 mark=$2; shift 2
+  timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/prof_$name -o t -- "$@" > $o/$name.log 2>&1 || return $?
+  python3 tools/aten_window.py $(find /tmp/prof_$name -name "*.db" | head -1) --after-kernel "$mark" > $o/${name}_kernels.txt 2>&1
+  rm -rf /tmp/prof_$name
+}
+prof trimr20 k_rmat python3 tools/trimr_time.py 20 || exit $?
+prof ooc18 k_rmat python3 tools/trimr_time.py 18 ooc || exit $?
+prof wf k_tok python3 tools/wf_shuffle_time.py 8 2 0 || exit $?
+export MRH_FORCE_RCCL=2
+prof wfd k_tok python3 tools/wf_shuffle_time.py 8 2 0
