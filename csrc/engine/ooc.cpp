@@ -61,22 +61,26 @@ at::TensorOptions opt(at::Device d, at::ScalarType t) { return at::TensorOptions
 
 // MRH_OOC_TRACE=1: host time per phase of an out-of-core op (device
 // synchronised at each mark), summed by name and printed at the end
+// MRH_OOC_TRACE=1: device-synchronised phase times (each phase's GPU work
+// included); =2: host wall time per phase without synchronising (where the
+// host thread spends its time, blocking waits included, GPU left alone)
 struct PhaseClock {
-  bool on = false;
+  bool on = false, sync = false;
   double t = 0;
   std::vector<std::pair<std::string, double>> acc;
   const char* op;
   explicit PhaseClock(const char* o) : op(o) {
     const char* e = std::getenv("MRH_OOC_TRACE");
-    on = e && *e == '1';
+    on = e && (*e == '1' || *e == '2');
+    sync = on && *e == '1';
     if (on) {
-      (void)hipDeviceSynchronize();
+      if (sync) (void)hipDeviceSynchronize();
       t = Comm::wtime();
     }
   }
   void operator()(const char* what) {
     if (!on) return;
-    (void)hipDeviceSynchronize();
+    if (sync) (void)hipDeviceSynchronize();
     const double now = Comm::wtime();
     for (auto& [k, v] : acc)
       if (k == what) {
@@ -285,7 +289,9 @@ std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev
     }
     clk("load");
     at::Tensor dest = dest_of(c);
+    clk("dest");
     Buckets B = bucket_local(c, dest, M);
+    clk("bucket");
     const HostOff bh = host_off(B.kv);
     clk("partition");
     int64_t s = 0;
@@ -297,6 +303,7 @@ std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev
       // the last piece viewing it
       KV hk;
       const std::shared_ptr<DrainEvent> ev = drain_to_pinned(B.kv, drain->stream(), &hk);
+      clk("drain issue");
       for (int d = 0; d < M; ++d) {
         const int64_t e = s + B.count[d];
         if (e > s) {
@@ -648,7 +655,10 @@ std::vector<KMV> ooc_convert_parts(const std::vector<KV>& kvs, const OocEnv& env
     std::vector<at::Tensor> hold;
     {
       c10::hip::HIPStreamGuard g(*ups);
-      p = concat_upload(parts[d].take(), dev, &hold);
+      std::vector<KV> pieces = parts[d].take();
+      clk("take (drains, file writes)");
+      p = concat_upload(pieces, dev, &hold);
+      clk("upload issue");
     }
     *ev = record_event(ups->stream());
     held.emplace_back(*ev, std::move(hold));
