@@ -9,6 +9,7 @@
 
 #include <ATen/hip/HIPContext.h>
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <cstdlib>
 #include <map>
@@ -306,6 +307,19 @@ KMV kmv_concat(const std::vector<KMV>& parts, at::Device dev, bool pin) {
   return out;
 }
 
+double wall_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+UploadTimes& upload_times() {
+  static UploadTimes t = [] {
+    UploadTimes u;
+    const char* e = std::getenv("MRH_OOC_TRACE");
+    u.on = e && *e == '2';
+    return u;
+  }();
+  return t;
+}
+
 namespace {
 // MRH_STAGE_PAGEABLE=0: pageable pieces go by ATen's copy_ (the runtime's own path)
 bool stage_pageable() {
@@ -387,8 +401,11 @@ KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at
       bytes += data_of(p).numel();
       rows += p.n;
     }
+    UploadTimes& ut = upload_times();
+    const double t0 = ut.on ? wall_s() : 0;
     *data_out = at::empty({bytes}, opt(dev, at::kByte));
     if (!fixed) *off_out = at::empty({rows + 1}, opt(dev, at::kLong));
+    if (ut.on) ut.alloc += wall_s() - t0;
     int64_t b = 0, r = 0;
     const hipStream_t cs = at::hip::getCurrentHIPStream().stream();
     // a pinned source goes by one hipMemcpyAsync with the caller holding it
@@ -396,13 +413,22 @@ KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at
     // host time per call (checks, a host-allocator event), which at a few
     // dozen pieces per partition was the out-of-core pass's critical path
     auto put = [&](const at::Tensor& dst, const at::Tensor& src) {
+      const double t1 = ut.on ? wall_s() : 0;
       if (hold && src.is_cpu() && src.is_contiguous() && src.is_pinned()) {
         const size_t nb = (size_t)src.numel() * src.element_size();
         if (hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nb, hipMemcpyHostToDevice, cs) != hipSuccess)
           throw std::runtime_error("mrhip: host to device copy failed");
         hold->push_back(src);
+        if (ut.on) {
+          ut.pinned += wall_s() - t1;
+          ++ut.pinned_calls;
+        }
       } else if (hold && src.is_cpu() && src.is_contiguous() && dst.is_contiguous() && stage_pageable()) {
         StageRing::get().copy(dst.data_ptr(), src.data_ptr(), (size_t)src.numel() * src.element_size(), cs);
+        if (ut.on) {
+          ut.staged += wall_s() - t1;
+          ++ut.staged_calls;
+        }
       } else {
         dst.copy_(src, /*non_blocking=*/true);
       }

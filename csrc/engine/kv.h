@@ -76,6 +76,14 @@ struct SmallRead {
   size_t bytes;
 };
 void read_small(hipStream_t s, std::initializer_list<SmallRead> items);
+// MRH_OOC_TRACE=2: host seconds concat_upload spent allocating, issuing
+// pinned copies and staging pageable ones (process totals)
+struct UploadTimes {
+  bool on = false;
+  double alloc = 0, pinned = 0, staged = 0;
+  int64_t pinned_calls = 0, staged_calls = 0;
+};
+UploadTimes& upload_times();
 KV concat_upload(const std::vector<KV>& parts, at::Device dev, std::vector<at::Tensor>* hold = nullptr);
 KV to_var_keys(const KV& kv);
 KV to_var_values(const KV& kv);

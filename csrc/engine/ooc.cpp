@@ -94,6 +94,13 @@ struct PhaseClock {
   ~PhaseClock() {
     if (!on) return;
     for (auto& [k, v] : acc) std::fprintf(stderr, "mrhip ooc %s %-18s %9.2f ms\n", op, k.c_str(), 1e3 * v);
+    UploadTimes& u = upload_times();
+    if (u.on) {
+      std::fprintf(stderr, "mrhip ooc %s upload totals: alloc %.2f ms, pinned copies %.2f ms (%lld), staged %.2f ms (%lld)\n",
+                   op, 1e3 * u.alloc, 1e3 * u.pinned, (long long)u.pinned_calls, 1e3 * u.staged,
+                   (long long)u.staged_calls);
+      u = UploadTimes{true};
+    }
   }
 };
 

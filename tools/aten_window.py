@@ -37,6 +37,14 @@ def main():
           f"{ft / 1e6:.3f} ms ({100 * ft / tot:.1f}% of kernel time)")
     for name, n, d, _, _ in foreign:
         print(f"{d / 1e6:10.3f} ms {n:7d}  {name[:150]}")
+    # where they come from: the engine kernels dispatched just before the
+    # first dispatch of each foreign kernel
+    if foreign:
+        print("\ncontext (the 3 kernels dispatched before the first dispatch of each):")
+        for name, _, _, first, _ in foreign[:20]:
+            prev = c.execute("select name from kernels where start < ? and start >= ? order by start desc limit 3",
+                             (first, t0)).fetchall()
+            print(f"  {name[:70]}  <-  " + "  <-  ".join(p[0][:50] for p in prev))
 
 
 if __name__ == "__main__":

@@ -2,6 +2,8 @@
 (the second run is warm); prints the per-stage times of each run.
 
     python tools/trimr_time.py SCALE [ooc [HBM_MIB [HOST_MIB]]]
+    env: REPS (runs, default 2), CHECK=1 (TriangleGraph count as the check),
+         FPATH (spool directory), BIG (an in-HBM run at that scale first), COPYBW=1
 
 ooc: under an HBM budget (default 256 MiB) and a host budget (default 2 GiB),
 spool files in a temporary directory; each stage also shows this rank's
@@ -66,8 +68,17 @@ if os.environ.get("BIG"):
     import resource
     print("host maxrss GB", resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, flush=True)
 e = kv.kdata.view(torch.int64).view(-1, 2)
-for rep in range(2):
-    root = tempfile.mkdtemp(prefix="mrh_trimr_") if ooc else ""
+if os.environ.get("CHECK") == "1":  # the specialised TriangleGraph count as the check
+    from gpu_mapreduce_amd.models.triangles import TriangleGraph
+    want = TriangleGraph(comm, e, 1 << scale).count()
+    print(f"check: TriangleGraph count {want}", flush=True)
+    torch.cuda.empty_cache() if torch.cuda.is_available() else None
+fdir = os.environ.get("FPATH") or None  # spool directory (default: a temporary one)
+if fdir:
+    import subprocess
+    print(subprocess.run(["df", "-h", fdir], capture_output=True, text=True).stdout, flush=True)
+for rep in range(int(os.environ.get("REPS", "2"))):
+    root = tempfile.mkdtemp(prefix="mrh_trimr_", dir=fdir) if ooc else ""
     try:
         r = (tri_find_mr(comm, e, hbm_budget=hbm, host_budget=host, fpath=root, memsize=64) if ooc
              else tri_find_mr(comm, e))
@@ -77,7 +88,9 @@ for rep in range(2):
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     tot = sum(s["ms"] for s in r["stages"])
-    print(f"rep {rep}: {tot:.1f} ms, {r['triangles']} triangles", flush=True)
+    print(f"rep {rep}: {tot:.1f} ms, {r['triangles']} triangles"
+          + (f" (check {want}: {'equal' if int(r['triangles']) == int(want) else 'DIFFERENT'})"
+             if os.environ.get("CHECK") == "1" else ""), flush=True)
     if ooc:
         print(f"   spool files {r['spool_files']}, host {r['spool_host_bytes'] / 1e9:.2f} GB, "
               f"disk {r['spool_disk_bytes'] / 1e9:.2f} GB", flush=True)
