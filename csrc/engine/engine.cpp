@@ -11,9 +11,11 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <condition_variable>
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <numeric>
 #include <stdexcept>
 
@@ -130,10 +132,10 @@ KV make_kv(at::Tensor kdata, c10::optional<at::Tensor> koff, at::Tensor vdata, c
 KV kv_to(const KV& kv, at::Device dev) {
   for (const at::Tensor* t : {&kv.kdata, &kv.vdata, &kv.koff, &kv.voff}) note_xfer(*t, dev);
   KV o = kv;
-  o.kdata = kv.kdata.to(dev);
-  o.vdata = kv.vdata.to(dev);
-  if (kv.koff.defined()) o.koff = kv.koff.to(dev);
-  if (kv.voff.defined()) o.voff = kv.voff.to(dev);
+  o.kdata = to_device(kv.kdata, dev);
+  o.vdata = to_device(kv.vdata, dev);
+  if (kv.koff.defined()) o.koff = to_device(kv.koff, dev);
+  if (kv.voff.defined()) o.voff = to_device(kv.voff, dev);
   return o;
 }
 
@@ -336,6 +338,72 @@ bool stage_pageable() {
 // every call; after a job that held ~180 GB of HBM that path ran ~2x slower
 // and made the out-of-core collate's disk-tier partitions host-bound
 // (docs/round6.md).
+// memcpy of large host ranges split over a few persistent threads (page-cache
+// data behind a spool file is copied at ~8 GB/s by one thread; the PCIe link
+// takes ~55 GB/s)
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool();  // never destroyed: detached workers
+    return *p;
+  }
+  void copy(void* dst, const void* src, size_t n) {
+    const int T = (int)workers_;
+    if (n < (size_t(1) << 20) || T <= 1) {
+      std::memcpy(dst, src, n);
+      return;
+    }
+    const size_t part = (n / (size_t)(T + 1) + 4095) & ~size_t(4095);
+    std::unique_lock<std::mutex> l(mu_);
+    jobs_.clear();
+    size_t o = 0;
+    for (int i = 0; i < T && o < n; ++i) {
+      const size_t len = std::min(part, n - o);
+      jobs_.push_back({static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, len});
+      o += len;
+    }
+    pending_ = (int)jobs_.size();
+    next_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    l.unlock();
+    if (o < n) std::memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, n - o);  // the caller's share
+    l.lock();
+    done_.wait(l, [&] { return pending_ == 0; });
+  }
+
+ private:
+  struct Job {
+    char* d;
+    const char* s;
+    size_t n;
+  };
+  CopyPool() {
+    const char* e = std::getenv("MRH_COPY_THREADS");
+    workers_ = (size_t)std::max(0, e && *e ? std::atoi(e) : 7);
+    for (size_t i = 0; i < workers_; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> l(mu_);
+    for (;;) {
+      cv_.wait(l, [&] { return gen_ != seen && next_ < jobs_.size(); });
+      const Job j = jobs_[next_++];
+      if (next_ >= jobs_.size()) seen = gen_;
+      l.unlock();
+      std::memcpy(j.d, j.s, j.n);
+      l.lock();
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::vector<Job> jobs_;
+  size_t next_ = 0, workers_ = 0;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
 class StageRing {
  public:
   static StageRing& get() {
@@ -349,9 +417,16 @@ class StageRing {
     char* d = static_cast<char*>(dst);
     while (bytes > 0) {
       Buf& b = bufs_[next_++ % bufs_.size()];
+      UploadTimes& ut = upload_times();
+      const double t0 = ut.on ? wall_s() : 0;
       if (b.used && hipEventSynchronize(b.ev) != hipSuccess) throw std::runtime_error("mrhip: staging wait failed");
+      const double t1 = ut.on ? wall_s() : 0;
       const size_t n = std::min(bytes, kBuf);
-      std::memcpy(b.p, p, n);
+      CopyPool::get().copy(b.p, p, n);
+      if (ut.on) {
+        ut.stage_wait += t1 - t0;
+        ut.stage_memcpy += wall_s() - t1;
+      }
       if (hipMemcpyAsync(d, b.p, n, hipMemcpyHostToDevice, s) != hipSuccess ||
           hipEventRecord(b.ev, s) != hipSuccess)
         throw std::runtime_error("mrhip: staged host to device copy failed");
@@ -363,7 +438,7 @@ class StageRing {
   }
 
  private:
-  static constexpr size_t kBuf = size_t(8) << 20;
+  static constexpr size_t kBuf = size_t(16) << 20;
   struct Buf {
     void* p = nullptr;
     hipEvent_t ev = nullptr;
@@ -371,7 +446,7 @@ class StageRing {
   };
   void init() {
     if (!bufs_.empty()) return;
-    bufs_.resize(4);
+    bufs_.resize(6);
     for (Buf& b : bufs_) {
       if (hipHostMalloc(&b.p, kBuf, hipHostMallocDefault) != hipSuccess ||
           hipEventCreateWithFlags(&b.ev, hipEventDisableTiming) != hipSuccess)
@@ -383,6 +458,15 @@ class StageRing {
   size_t next_ = 0;
 };
 }  // namespace
+
+at::Tensor to_device(const at::Tensor& t, at::Device dev, bool non_blocking) {
+  if (!t.defined() || !dev.is_cuda() || !t.is_cpu()) return t.defined() ? t.to(dev) : t;
+  if (t.is_pinned() || !t.is_contiguous() || !stage_pageable()) return t.to(dev, non_blocking);
+  at::Tensor d = at::empty(t.sizes(), t.options().device(dev));
+  const size_t nb = (size_t)t.numel() * t.element_size();
+  if (nb) StageRing::get().copy(d.data_ptr(), t.data_ptr(), nb, at::hip::getCurrentHIPStream().stream());
+  return d;
+}
 
 KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at::Tensor>* hold) {
   std::vector<KV> parts;

@@ -1537,6 +1537,20 @@ std::vector<int64_t> TriangleGraph::work_split(const at::Tensor& d_in, int64_t P
 // Per rank that is O(E/P) sorting, two all-to-alls of E/P keys and one
 // all-gather of the 4-byte columns, instead of the whole raw edge list
 // all-gathered and sorted on every rank.
+// owner of every key: the number of sorted splitters <= key (searchsorted
+// side right) — the engine's LDS binary-search kernel on the device (keys
+// and splitters non-negative int64: unsigned order = signed order)
+static at::Tensor owners_right(const at::Tensor& split, const at::Tensor& keys) {
+  if (!keys.is_cuda() || split.numel() > 4096) return at::searchsorted(split, keys, /*out_int32=*/true, /*right=*/true);
+  at::Tensor sp = split.contiguous(), k = keys.contiguous();
+  at::Tensor out = at::empty({k.numel()}, k.options().dtype(at::kInt));
+  if (k.numel())
+    k::bucket_by_splitters(reinterpret_cast<const uint64_t*>(k.data_ptr<int64_t>()), k.numel(),
+                           reinterpret_cast<const uint64_t*>(sp.data_ptr<int64_t>()), (int)sp.numel(),
+                           out.data_ptr<int32_t>(), at::hip::getCurrentHIPStream(), /*right=*/true);
+  return out;
+}
+
 void TriangleGraph::build_split(const at::Tensor& p_in) {
   const Comm& cm = *comm;
   const int P = cm.size(), me = cm.rank();
@@ -1560,8 +1574,7 @@ void TriangleGraph::build_split(const at::Tensor& p_in) {
     cm.allgather_bytes(smp.data_ptr(), all.data_ptr(), NS * 8);
     at::Tensor srt = std::get<0>(at::sort(all));
     at::Tensor spl = srt.index_select(0, at::arange(1, P, L) * NS).contiguous();  // P - 1 splitters
-    at::Tensor dest = P > 1 ? at::searchsorted(spl, p, /*out_int32=*/true, /*right=*/true)
-                            : at::zeros({n}, L.dtype(at::kInt));
+    at::Tensor dest = P > 1 ? owners_right(spl, p) : at::zeros({n}, L.dtype(at::kInt));
     p = route_u64(cm, p, dest);
   }
   at::Tensor uniq = unique_sorted(p);
@@ -1596,7 +1609,7 @@ void TriangleGraph::build_split(const at::Tensor& p_in) {
     std::vector<int64_t> bk;
     for (int r = 1; r < P; ++r) bk.push_back(rb[r] << 32);
     at::Tensor b = at::from_blob(bk.data(), {P - 1}, at::TensorOptions().dtype(at::kLong)).to(dev);
-    at::Tensor dest = at::searchsorted(b, os, /*out_int32=*/true, /*right=*/true);
+    at::Tensor dest = owners_right(b, os);
     os = route_u64(cm, os, dest);
     if (os.numel()) os = radix_sort_keys(os, 0, 64);
   }

@@ -80,10 +80,15 @@ void read_small(hipStream_t s, std::initializer_list<SmallRead> items);
 // pinned copies and staging pageable ones (process totals)
 struct UploadTimes {
   bool on = false;
-  double alloc = 0, pinned = 0, staged = 0;
+  double alloc = 0, pinned = 0, staged = 0, stage_wait = 0, stage_memcpy = 0;
   int64_t pinned_calls = 0, staged_calls = 0;
 };
 UploadTimes& upload_times();
+// a host tensor on the device, on the current stream: pinned by one async
+// copy, pageable (a memory-mapped spool file) through the pinned staging ring
+// with a multi-threaded memcpy (never HIP's on-the-fly pinning of pageable memory)
+// (non_blocking: a pinned source may still be read by the copy when this returns)
+at::Tensor to_device(const at::Tensor& t, at::Device dev, bool non_blocking = false);
 KV concat_upload(const std::vector<KV>& parts, at::Device dev, std::vector<at::Tensor>* hold = nullptr);
 KV to_var_keys(const KV& kv);
 KV to_var_values(const KV& kv);

@@ -96,9 +96,10 @@ struct PhaseClock {
     for (auto& [k, v] : acc) std::fprintf(stderr, "mrhip ooc %s %-18s %9.2f ms\n", op, k.c_str(), 1e3 * v);
     UploadTimes& u = upload_times();
     if (u.on) {
-      std::fprintf(stderr, "mrhip ooc %s upload totals: alloc %.2f ms, pinned copies %.2f ms (%lld), staged %.2f ms (%lld)\n",
+      std::fprintf(stderr, "mrhip ooc %s upload totals: alloc %.2f ms, pinned copies %.2f ms (%lld), staged %.2f ms (%lld: "
+                   "buffer waits %.2f ms, memcpy %.2f ms)\n",
                    op, 1e3 * u.alloc, 1e3 * u.pinned, (long long)u.pinned_calls, 1e3 * u.staged,
-                   (long long)u.staged_calls);
+                   (long long)u.staged_calls, 1e3 * u.stage_wait, 1e3 * u.stage_memcpy);
       u = UploadTimes{true};
     }
   }
@@ -208,7 +209,7 @@ KV kv_to_async(const KV& kv, at::Device dev, const c10::hip::HIPStream& side, co
   auto one = [&](const at::Tensor& t) {
     if (!t.defined()) return t;
     note_xfer(t, dev);
-    at::Tensor d = t.to(dev, /*non_blocking=*/true);
+    at::Tensor d = to_device(t, dev, /*non_blocking=*/true);  // pageable (spool file) pieces: staging ring
     if (d.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(d.storage().data_ptr(), use);
     return d;
   };
@@ -866,9 +867,9 @@ void ooc_for_each_kmv_block(const KMV& kmv, const OocEnv& env, at::Device dev,
     note_xfer(m.vdata, dev);
     note_xfer(m.voff, dev);
     note_xfer(m.seg, dev);
-    md.vdata = m.vdata.to(dev);
-    if (m.voff.defined()) md.voff = m.voff.to(dev);
-    md.seg = m.seg.to(dev);
+    md.vdata = to_device(m.vdata, dev);
+    if (m.voff.defined()) md.voff = to_device(m.voff, dev);
+    md.seg = to_device(m.seg, dev);
     return md;
   };
   const int64_t cap = std::max<int64_t>(budget / 4, 1);

@@ -467,6 +467,7 @@ void gather_fixed_t(const uint8_t* src, int w, const I* idx, int64_t n, uint8_t*
 // (lower_bound over the sorted unsigned splitters, staged in LDS; up to
 // 4096 splitters = 32 KiB) — the out-of-core sample sort's partition pass
 constexpr int SPLIT_MAX = 4096;
+template <bool RIGHT>
 __global__ __launch_bounds__(256) void k_bucket_by_splitters(const uint64_t* __restrict__ keys, int64_t n,
                                                             const uint64_t* __restrict__ split, int ns,
                                                             int32_t* __restrict__ out) {
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(256) void k_bucket_by_splitters(const uint64_t* __r
     int lo = 0, hi = ns;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (sp[mid] < k) lo = mid + 1;
+      if (RIGHT ? sp[mid] <= k : sp[mid] < k) lo = mid + 1;
       else hi = mid;
     }
     out[i] = lo;
@@ -641,12 +642,13 @@ void dest_byte_counts(const int32_t* dest, const int64_t* off, int64_t n, int P,
   MRH_CHECK_LAUNCH();
 }
 void bucket_by_splitters(const uint64_t* keys, int64_t n, const uint64_t* split, int nsplit, int32_t* out,
-                         hipStream_t s) {
+                         hipStream_t s, bool right) {
   check_arg(nsplit >= 0 && nsplit <= SPLIT_MAX, "bucket_by_splitters: at most 4096 splitters");
   if (n <= 0) return;
   int64_t g = (n + 255) / 256;
   if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(k_bucket_by_splitters, dim3((unsigned)g), dim3(256), 0, s, keys, n, split, nsplit, out);
+  if (right) hipLaunchKernelGGL(k_bucket_by_splitters<true>, dim3((unsigned)g), dim3(256), 0, s, keys, n, split, nsplit, out);
+  else hipLaunchKernelGGL(k_bucket_by_splitters<false>, dim3((unsigned)g), dim3(256), 0, s, keys, n, split, nsplit, out);
   MRH_CHECK_LAUNCH();
 }
 

@@ -209,9 +209,10 @@ void tok_emit(const uint8_t* text, int64_t n, const uint32_t* tile_off, int64_t*
 void copy_strings_nul(const uint8_t* text, const int64_t* starts, const int64_t* koff, int64_t n,
                       uint8_t* kdata, hipStream_t s);
 void fill_i32(int32_t* p, int64_t n, int32_t v, hipStream_t s);
-// out[i] = number of sorted (unsigned) splitters < keys[i]; nsplit <= 4096
+// out[i] = number of sorted (unsigned) splitters < keys[i] (right: <= keys[i],
+// numpy searchsorted side='right'); nsplit <= 4096
 void bucket_by_splitters(const uint64_t* keys, int64_t n, const uint64_t* split, int nsplit, int32_t* out,
-                         hipStream_t s);
+                         hipStream_t s, bool right = false);
 
 // ---------------------------------------------------------------- graph.hip
 // R-MAT edges: counter-based Philox RNG; edge e of stream `seed` is a pure

@@ -29,6 +29,15 @@ if os.environ.get("NUMA") == "1":  # bind like bench.py's ranks (parallel/comm.p
     from gpu_mapreduce_amd.parallel.comm import bind_numa_local
     print("numa cpus", bind_numa_local(0), "of", len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else "?")
 comm = g.Comm(device=os.environ.get("DEV", "cuda:0"))
+if os.environ.get("HEARTBEAT"):  # a line every N s: long out-of-core runs are not taken for hung
+    import threading
+    import time as _t
+
+    def _beat(every=float(os.environ["HEARTBEAT"]), t0=_t.perf_counter()):
+        while True:
+            _t.sleep(every)
+            print(f"alive {(_t.perf_counter() - t0):.0f} s", flush=True)
+    threading.Thread(target=_beat, daemon=True).start()
 if os.environ.get("BIG"):  # first the bench's in-HBM run at scale BIG (the pool holds its peak after it)
     big = int(os.environ["BIG"])
     kb = C.map_rmat((1 << big) * 16, big, *GRAPH500, 0.0, 1, 0, comm.device)
