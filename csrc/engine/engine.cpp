@@ -323,6 +323,25 @@ UploadTimes& upload_times() {
 }
 
 namespace {
+// MRH_GATHER_KERNEL=0: pinned pieces go by one hipMemcpyAsync each instead of
+// the zero-copy gather kernel (util.hip gather_pieces)
+bool gather_kernel() {
+  static const bool on = [] {
+    const char* e = std::getenv("MRH_GATHER_KERNEL");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+// the device reads this host pointer as is (pinned, mapped at the same
+// address): only then does a piece go through the gather kernel
+bool device_reads_host(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost && a.devicePointer == p;
+}
 // MRH_STAGE_PAGEABLE=0: pageable pieces go by ATen's copy_ (the runtime's own path)
 bool stage_pageable() {
   static const bool on = [] {
@@ -496,9 +515,29 @@ KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at
     // until the stream passed the copy (`hold`): ATen's copy_ costs ~50 us of
     // host time per call (checks, a host-allocator event), which at a few
     // dozen pieces per partition was the out-of-core pass's critical path
+    // pinned data pieces are gathered by kernels in batches (flushed at the end)
+    k::PieceTable tab;
+    uint8_t* tab_dst = nullptr;
+    auto flush = [&] {
+      if (tab.n) k::gather_pieces(tab, tab_dst, cs);
+      tab.n = 0;
+    };
     auto put = [&](const at::Tensor& dst, const at::Tensor& src) {
       const double t1 = ut.on ? wall_s() : 0;
-      if (hold && src.is_cpu() && src.is_contiguous() && src.is_pinned()) {
+      if (hold && gather_kernel() && src.is_cpu() && src.is_contiguous() && src.is_pinned() && dst.is_contiguous() &&
+          dst.scalar_type() == at::kByte && device_reads_host(src.data_ptr())) {
+        if (tab.n == k::PieceTable::kMax) flush();
+        tab_dst = P0<uint8_t>(*data_out);
+        tab.src[tab.n] = static_cast<const uint8_t*>(src.data_ptr());
+        tab.dst_off[tab.n] = P0<uint8_t>(dst) - tab_dst;
+        tab.bytes[tab.n] = (int64_t)src.numel() * src.element_size();
+        ++tab.n;
+        hold->push_back(src);
+        if (ut.on) {
+          ut.pinned += wall_s() - t1;
+          ++ut.pinned_calls;
+        }
+      } else if (hold && src.is_cpu() && src.is_contiguous() && src.is_pinned()) {
         const size_t nb = (size_t)src.numel() * src.element_size();
         if (hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), nb, hipMemcpyHostToDevice, cs) != hipSuccess)
           throw std::runtime_error("mrhip: host to device copy failed");
@@ -531,6 +570,7 @@ KV concat_upload(const std::vector<KV>& parts_in, at::Device dev, std::vector<at
       b += d.numel();
       r += p.n;
     }
+    flush();
     if (!fixed) k::fill_i64(P0<int64_t>(*off_out) + rows, 1, b, cs);
   };
   KV o;

@@ -238,7 +238,10 @@ template <typename F>
 std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev, int M, F&& dest_of,
                          const OocEnv& env, OocStats* st) {
   auto budget = std::make_shared<SpoolBudget>();
-  budget->hbm = 0;
+  // an HBM tier of a quarter of the budget (the chunk in flight and the
+  // per-partition converts use the rest): the first pieces stay on the
+  // device, then pinned host memory, then disk
+  budget->hbm = dev.is_cuda() && env.hbm > 0 ? env.hbm / 4 : 0;
   budget->host = env.host;
   std::vector<Spool> parts;
   parts.reserve((size_t)M);
@@ -309,18 +312,33 @@ std::vector<Spool> spool(const std::vector<KV>& kvs, int64_t cap, at::Device dev
       // offsets to rebase before the copy lands), kept as the host tier or
       // written to its file by a background thread; the buffer is freed with
       // the last piece viewing it
-      KV hk;
-      const std::shared_ptr<DrainEvent> ev = drain_to_pinned(B.kv, drain->stream(), &hk);
-      clk("drain issue");
-      for (int d = 0; d < M; ++d) {
+      // the HBM tier first: partitions [0, dk) of this chunk while it has
+      // room (each piece its own device copy), then the rest drains
+      const int64_t row = (int64_t)B.kv.kw + B.kv.vw;
+      int dk = 0;
+      for (int64_t left = budget->hbm; dk < M && B.count[dk] * row <= left; ++dk) left -= B.count[dk] * row;
+      for (int d = 0; d < dk; ++d) {
         const int64_t e = s + B.count[d];
-        if (e > s) {
-          const KV piece = kv_slice(hk, s, e, nullptr, nullptr);
-          const int64_t room = parts[d].host_room();
-          if (room < 0 || room >= piece.nbytes()) parts[d].add_drained(piece, ev);
-          else parts[d].add_drained_to_disk(piece, ev);
-        }
+        if (e > s) parts[d].add(kv_slice(B.kv, s, e, nullptr, nullptr));
         s = e;
+      }
+      clk("hbm tier");
+      const int64_t s0 = s;
+      if (s0 < B.kv.n) {
+        KV hk;
+        const std::shared_ptr<DrainEvent> ev =
+            drain_to_pinned(s0 ? kv_slice(B.kv, s0, B.kv.n, nullptr, nullptr) : B.kv, drain->stream(), &hk);
+        clk("drain issue");
+        for (int d = dk; d < M; ++d) {
+          const int64_t e = s + B.count[d];
+          if (e > s) {
+            const KV piece = kv_slice(hk, s - s0, e - s0, nullptr, nullptr);
+            const int64_t room = parts[d].host_room();
+            if (room < 0 || room >= piece.nbytes()) parts[d].add_drained(piece, ev);
+            else parts[d].add_drained_to_disk(piece, ev);
+          }
+          s = e;
+        }
       }
     } else {
       for (int d = 0; d < M; ++d) {

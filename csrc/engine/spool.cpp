@@ -579,7 +579,23 @@ void Spool::add(const KV& piece, hipStream_t copy) {
   int tier;
   const bool cuda = dev_.is_cuda();
   if (cuda && (B.hbm < 0 || B.hbm >= b)) {
-    p = piece.device() == dev_ ? piece : kv_to(piece, dev_);
+    // a device piece is kept as is, unless it is a view into a larger buffer
+    // (a slice of a partitioned chunk): then its own copy, so the tier holds
+    // the bytes it counts and the chunk buffer can go
+    auto own = [](const at::Tensor& t) {
+      if (!t.defined() || !t.is_cuda()) return t;
+      const int64_t used = t.numel() * t.element_size();
+      return (int64_t)t.storage().nbytes() > used + 4096 ? t.clone() : t;
+    };
+    if (piece.device() == dev_) {
+      p = piece;
+      p.kdata = own(piece.kdata);
+      p.vdata = own(piece.vdata);
+      p.koff = own(piece.koff);
+      p.voff = own(piece.voff);
+    } else {
+      p = kv_to(piece, dev_);
+    }
     if (B.hbm >= 0) B.hbm -= b;
     tier = 0;
     st_.hbm_bytes += b;

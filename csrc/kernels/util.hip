@@ -219,7 +219,49 @@ __global__ __launch_bounds__(NT) void k_edge_upper_write(const int64_t* __restri
   }
 }
 
+// zero-copy gather: block (x, p) copies its stride of piece p from pinned
+// host memory (device-accessible) into dst; dword granularity when the piece
+// allows, bytes otherwise
+__global__ __launch_bounds__(NT) void k_gather_pieces(PieceTable t, uint8_t* __restrict__ dst) {
+  const int p = blockIdx.y;
+  if (p >= t.n) return;
+  const uint8_t* __restrict__ s = t.src[p];
+  uint8_t* __restrict__ d = dst + t.dst_off[p];
+  const int64_t n = t.bytes[p];
+  const int64_t tid = (int64_t)blockIdx.x * NT + threadIdx.x, nth = (int64_t)gridDim.x * NT;
+  if ((((uintptr_t)s | (uintptr_t)d | (uintptr_t)n) & 3) == 0) {
+    const uint32_t* __restrict__ s4 = reinterpret_cast<const uint32_t*>(s);
+    uint32_t* __restrict__ d4 = reinterpret_cast<uint32_t*>(d);
+    const int64_t w = n >> 2;
+    for (int64_t i = tid * 4; i < w; i += nth * 4) {  // four dwords in flight per thread
+      if (i + 3 < w) {
+        const uint32_t a = __builtin_nontemporal_load(s4 + i), b = __builtin_nontemporal_load(s4 + i + 1);
+        const uint32_t c = __builtin_nontemporal_load(s4 + i + 2), e = __builtin_nontemporal_load(s4 + i + 3);
+        d4[i] = a;
+        d4[i + 1] = b;
+        d4[i + 2] = c;
+        d4[i + 3] = e;
+      } else {
+        for (int64_t j = i; j < w; ++j) d4[j] = s4[j];
+      }
+    }
+  } else {
+    for (int64_t i = tid; i < n; i += nth) d[i] = s[i];
+  }
+}
+
 }  // namespace
+
+void gather_pieces(const PieceTable& t, uint8_t* dst, hipStream_t s) {
+  if (t.n <= 0) return;
+  check_arg(t.n <= PieceTable::kMax, "gather_pieces: too many pieces");
+  int64_t mx = 0;
+  for (int i = 0; i < t.n; ++i) mx = std::max<int64_t>(mx, t.bytes[i]);
+  // ~64 KiB of a piece per block, at most 64 blocks on one piece
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (mx + 65535) / 65536));
+  hipLaunchKernelGGL(k_gather_pieces, dim3(gx, (unsigned)t.n), dim3(NT), 0, s, t, dst);
+  MRH_CHECK_LAUNCH();
+}
 
 void edge_ne_flags(const int64_t* e, int64_t n, uint32_t* flag, hipStream_t s) {
   if (n <= 0) return;
