@@ -8,4 +8,4 @@ rc=$?; echo "tests rc=$rc" >> $o/tests.log; [ $rc -eq 0 ] || exit 1
 MRH_OOC_TRACE=2 timeout -k 10 200 python -u tools/trimr_time.py 18 ooc > $o/alone.log 2>&1 || exit $?
 MRH_GATHER_KERNEL=0 MRH_OOC_TRACE=2 timeout -k 10 200 python -u tools/trimr_time.py 18 ooc > $o/alone_nokernel.log 2>&1 || exit $?
 BIG=22 MRH_OOC_TRACE=2 timeout -k 10 200 python -u tools/trimr_time.py 18 ooc > $o/big.log 2>&1 || exit $?
-HEARTBEAT=20 MRH_OOC_TRACE=2 REPS=1 CHECK=1 FPATH=/tmp timeout -k 10 700 python -u tools/trimr_time.py 23 ooc 204800 131072 > $o/ooc23.log 2>&1
+HEARTBEAT=20 MRH_OOC_TRACE=2 REPS=1 CHECK=1 FPATH=/tmp timeout -k 10 700 python -u tools/trimr_time.py 23 ooc 131072 131072 > $o/ooc23.log 2>&1
