@@ -384,3 +384,44 @@ def test_oink_graph_commands_distributed(tmp_path, monkeypatch):
     assert p1.keys() == p2.keys()
     for k in p1:
         assert abs(float(p1[k]) - float(p2[k])) <= 1e-5 * abs(float(p1[k])) + 1e-9
+
+
+# the reference's MapReduce formulations of sssp and luby_find
+# (oink/sssp.cpp:88-152, oink/luby_find.cpp:53-97): aggregate, cross-MR
+# appends (open(1)/kv_open/close), compress as the combiner and the
+# all-rank termination counts, at 2 ranks against 1
+OINK_MR_SCRIPT = """rmat 8 4 0.25 0.25 0.25 0.25 0.0 4242 -o NULL mre
+edge_upper -i mre -o NULL mre
+luby_find_mr 99 -i mre -o tmp.mis NULL
+mre map/mr mre add_weight
+sssp_mr 2 31 -i mre -o tmp.sssp NULL
+"""
+
+
+def oink_graph_mr(comm):
+    import io
+    from gpu_mapreduce_amd.oink.interp import OINK
+    os.chdir(os.environ["OINK_TEST_DIR"])
+    out = io.StringIO()
+    OINK(comm, screen=out, logfile="none").file(text=OINK_MR_SCRIPT)
+    return out.getvalue()
+
+
+def test_oink_graph_mr_commands_distributed(tmp_path, monkeypatch):
+    import io
+    import re
+    from gpu_mapreduce_amd.oink.interp import OINK
+    d1, d2 = tmp_path / "p1", tmp_path / "p2"
+    d1.mkdir()
+    d2.mkdir()
+    monkeypatch.chdir(d1)
+    out1 = io.StringIO()
+    OINK(screen=out1, logfile="none").file(text=OINK_MR_SCRIPT)
+    monkeypatch.setenv("OINK_TEST_DIR", str(d2))
+    text1, text2 = out1.getvalue(), run_world("oink_graph_mr", 2)[0]
+    pat = r"(Luby_find: \d+ MIS vertices in \d+ iterations|Source = \d+; Iterations = \d+; Num Vtx Labeled = \d+)"
+    assert re.findall(pat, text1) == re.findall(pat, text2) and len(re.findall(pat, text1)) == 3
+    assert _oink_files(d1, "tmp.mis") == _oink_files(d2, "tmp.mis")
+    s1 = sorted(tuple(ln.split()[:2]) for ln in _oink_files(d1, "tmp.sssp"))
+    s2 = sorted(tuple(ln.split()[:2]) for ln in _oink_files(d2, "tmp.sssp"))
+    assert s1 == s2 and len(s1) > 100
