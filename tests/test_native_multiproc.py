@@ -101,6 +101,8 @@ SCRIPTS_CASES = [
     ("in.pagerank", [], ("PageRank: 2",)),
     ("in.rmat", [], ("RMAT: 256", "DegreeStats", "  ")),
     ("in.sssp", [], ("SSSP:",)),
+    ("in.luby_mr", [], ("EdgeUpper", "Luby_find")),
+    ("in.sssp_mr", [], ("SSSP_MR:",)),
 ]
 
 
@@ -112,7 +114,7 @@ def _oink(script, n, cwd, extra, gpu=False):
 def test_oink_scripts_native_ranks(tmp_path, script, extra, keys):
     one = _oink(script, 1, tmp_path, extra)
     two = _oink(script, 2, tmp_path, extra)
-    if script == "in.sssp":
+    if script in ("in.sssp", "in.sssp_mr"):
         # sources are drawn per run; the per-source label counts must agree
         pick = lambda o: sorted(ln.split(";")[0] + ";" + ln.split(";")[2] for ln in o.splitlines()
                                 if "Source =" in ln)
