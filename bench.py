@@ -43,10 +43,15 @@ import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+# the out-of-core host tier's pinned reserve, pinned once at start-up
+# (gpu_mapreduce_amd/hostpin.py); torch reads PYTORCH_HIP_ALLOC_CONF once, so
+# the package (which configures it) is imported before torch
+os.environ.setdefault("MRH_PIN_RESERVE_MB", "8192")
+from gpu_mapreduce_amd import hostpin  # noqa: E402
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 REF_GBPS = 50.0 * 1e9 / 59.0 / 1e9  # reference end-to-end InvertedIndex, 50 GB in 59.0 s (decimal GB)
 
@@ -663,6 +668,9 @@ def compact_record(res):
                     out[f"{key}_collate4_x_floor"] = st["x_floor"]
             if "spool_disk_bytes" in v:
                 out[f"{key}_disk_bytes"] = v["spool_disk_bytes"]
+    hp = res.get("host_pin_reserve")
+    if isinstance(hp, dict) and hp.get("mib"):
+        out["host_pin_reserve_ms"] = hp["ms"]  # the start-up pinning of the out-of-core host tier's reserve
     for k in ("pagerank_error", "pagerank_dist_error", "trifind_error", "trifind_dist_error", "wordfreq_error",
               "wordfreq_shuffle_error", "wordfreq_shuffle_dist_error", "trifind_mr_error"):
         if k in res:
@@ -733,6 +741,7 @@ def main():
     comm = pcomm.init()
     if comm.size != args.gpus:
         raise SystemExit(f"bench.py: {comm.size} ranks joined, expected {args.gpus}")
+    pin_ms = hostpin.prepin() if comm.is_cuda else 0.0  # start-up, like the HBM pool: outside every timed region
     if args.pagerank_scale is None:
         args.pagerank_scale = 26 if comm.is_cuda else 14
     if args.trifind_scale is None:
@@ -845,6 +854,7 @@ def main():
     res.update(rrec)
     res["ranks_joined"] = comm.size
     from gpu_mapreduce_amd.runtime import hbm_pool
+    res["host_pin_reserve"] = {"mib": hostpin.configure(), "ms": round(pin_ms, 1)}
     res["device_allocator"] = "mrhip HBM page pool (csrc/engine/hbmpool.cpp)" if hbm_pool.installed() else "ATen caching allocator"
     if hbm_pool.installed() and comm.is_cuda:
         st = hbm_pool.stats(torch.device(comm.device).index or 0)

@@ -200,8 +200,9 @@ def bench_trifind_mr(comm, args):
             host = int(getattr(args, "mr_ooc_host", 2 << 30))
             # pages of the reference's default memsize (64 MB): spool pieces of
             # min(page, budget / 4) = 64 MiB. Run twice: the first (cold) run
-            # also pays the pinned host allocations the caching host allocator
-            # keeps for later jobs; the record's numbers are the second run's
+            # also pays what the process had not set up yet (pinned host
+            # allocations beyond the start-up reserve, gpu_mapreduce_amd/hostpin.py;
+            # pool growth); the record's numbers are the second run's
             dts = []
             for _ in range(2):
                 sync()
