@@ -43,15 +43,10 @@ import subprocess
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-# the out-of-core host tier's pinned reserve, pinned once at start-up
-# (gpu_mapreduce_amd/hostpin.py); torch reads PYTORCH_HIP_ALLOC_CONF once, so
-# the package (which configures it) is imported before torch
-os.environ.setdefault("MRH_PIN_RESERVE_MB", "8192")
-from gpu_mapreduce_amd import hostpin  # noqa: E402
+import torch
+import torch.distributed as dist
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 REF_GBPS = 50.0 * 1e9 / 59.0 / 1e9  # reference end-to-end InvertedIndex, 50 GB in 59.0 s (decimal GB)
 
@@ -741,7 +736,11 @@ def main():
     comm = pcomm.init()
     if comm.size != args.gpus:
         raise SystemExit(f"bench.py: {comm.size} ranks joined, expected {args.gpus}")
-    pin_ms = hostpin.prepin() if comm.is_cuda else 0.0  # start-up, like the HBM pool: outside every timed region
+    # the out-of-core host tier's pinned arena (gpu_mapreduce_amd/hostpin.py),
+    # pinned at start-up like the HBM pool: outside every timed region
+    from gpu_mapreduce_amd import hostpin
+    pin_mb = int(os.environ.get("MRH_PIN_RESERVE_MB", "8192"))
+    pin_ms = hostpin.prepin(pin_mb) if comm.is_cuda else 0.0
     if args.pagerank_scale is None:
         args.pagerank_scale = 26 if comm.is_cuda else 14
     if args.trifind_scale is None:
@@ -854,7 +853,8 @@ def main():
     res.update(rrec)
     res["ranks_joined"] = comm.size
     from gpu_mapreduce_amd.runtime import hbm_pool
-    res["host_pin_reserve"] = {"mib": hostpin.configure(), "ms": round(pin_ms, 1)}
+    res["host_pin_reserve"] = {"mib": pin_mb if comm.is_cuda else 0, "ms": round(pin_ms, 1),
+                               **(hostpin.stats() if comm.is_cuda else {})}
     res["device_allocator"] = "mrhip HBM page pool (csrc/engine/hbmpool.cpp)" if hbm_pool.installed() else "ATen caching allocator"
     if hbm_pool.installed() and comm.is_cuda:
         st = hbm_pool.stats(torch.device(comm.device).index or 0)

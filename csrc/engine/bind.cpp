@@ -18,6 +18,8 @@
 #include <unistd.h>
 #include <string>
 
+#include "graphmr.h"
+#include "hostarena.h"
 #include "kv.h"
 #include "graphplan.h"
 #include "guardalloc.h"
@@ -493,6 +495,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              py::gil_scoped_release nogil;
              return r.reduce_batch([&](const KMV& s, KeyValue& kv) { py::gil_scoped_acquire g; fn(s, kvref(kv)); });
            })
+      .def("compress_batch",
+           [](MR& r, py::function fn) {
+             py::gil_scoped_release nogil;
+             return r.compress_batch([&](const KMV& s, KeyValue& kv) { py::gil_scoped_acquire g; fn(s, kvref(kv)); });
+           })
       .def("scan_kv",
            [](MR& r, py::function fn) {
              py::gil_scoped_release nogil;
@@ -919,6 +926,36 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tri_hub_size", &mrh::tri_hub_size);
   m.def("tri_last_hub_size", &mrh::tri_last_hub_size);
   m.def("tri_list", &mrh::tri_list);
+  // sssp_mr / luby_find_mr callbacks (graphmr.h) for Python batch callbacks
+  m.def("ssspmr_pick", [](const KMV& m) {
+    SsspPick p = ssspmr_pick(m);
+    return py::make_tuple(p.dist, p.ckeys, p.cdist);
+  });
+  m.def("ssspmr_relax", [](const KMV& m) {
+    SsspRelax r = ssspmr_relax(m);
+    return py::make_tuple(r.ekeys, r.edges, r.pkeys, r.paths);
+  });
+  m.def("lubymr_random", &lubymr_random);
+  m.def("lubymr_edge_winner", &lubymr_edge_winner);
+  m.def("lubymr_vert", [](const KMV& m, bool loser) {
+    LubyVert r = lubymr_vert(m, loser);
+    return py::make_tuple(r.k24, r.v24, r.k16, r.v16);
+  });
+  m.def("lubymr_emit", [](const KMV& m) {
+    LubyEmit r = lubymr_emit(m);
+    return py::make_tuple(r.mis, r.kflag, r.fval, r.knull);
+  });
+  m.def("host_arena_reserve", &hostarena::reserve, py::call_guard<py::gil_scoped_release>());
+  m.def("host_arena_stats", [] {
+    hostarena::Stats s = hostarena::stats();
+    py::dict d;
+    d["reserved"] = s.reserved;
+    d["in_use"] = s.in_use;
+    d["peak"] = s.peak;
+    d["hits"] = s.hits;
+    d["misses"] = s.misses;
+    return d;
+  });
   m.def("kv_iter", &kv_iter);
   m.def("kmv_iter", &kmv_iter);
   // native OINK interpreter (csrc/oink)

@@ -3,6 +3,7 @@
 //        torch stream;
 //   cpu: straightforward host loops with identical semantics and identical
 //        output order (they are the oracle the GPU tests compare against).
+#include "hostarena.h"
 #include "kv.h"
 #include "xfer.h"
 #include "grouper.h"
@@ -162,7 +163,7 @@ at::Tensor cat_maybe_pinned(const std::vector<at::Tensor>& ts, at::Device dev, a
   if (!pin || !dev.is_cpu()) return at::cat(ts, 0);
   int64_t n = 0;
   for (auto& t : ts) n += t.numel();
-  at::Tensor out = at::empty({n}, at::TensorOptions().dtype(ty).pinned_memory(true));
+  at::Tensor out = hostarena::pinned_empty({n}, ty);
   at::cat_out(out, ts, 0);
   return out;
 }

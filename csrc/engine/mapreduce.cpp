@@ -1,5 +1,6 @@
 // Native MapReduce object (see mapreduce.h). Reference behaviour cited per
 // method as src/mapreduce.cpp:<lines>.
+#include "hostarena.h"
 #include "xfer.h"
 #include "mapreduce.h"
 #include "guard.h"
@@ -215,7 +216,7 @@ at::Tensor to_host(const at::Tensor& t, bool pin) {
   if (!t.defined()) return t;
   note_xfer(t, at::Device(at::kCPU));
   if (pin && t.is_cuda()) {  // one copy, straight into pinned memory (not pageable, then pinned)
-    at::Tensor h = at::empty(t.sizes(), t.options().device(at::kCPU).pinned_memory(true));
+    at::Tensor h = hostarena::pinned_empty(t.sizes(), t.scalar_type());
     h.copy_(t);
     return h;
   }
@@ -1336,6 +1337,30 @@ uint64_t MapReduce::compress(const ReduceFn& fn) {  // :749-851
   KeyValue kvb(device());
   bound(kvb);
   run_host_kmv(m, [&](char* k, int kb, char* mv, int nv, int* vb) { fn(k, kb, mv, nv, vb, kvb); });
+  set_kv_parts(kvb.finish_parts());
+  note_spool(kvb);
+  stats("Compress", 0);
+  return count(kv_rows());
+}
+
+// compress with a batch callback: the local groups of this rank's pairs as one
+// KMV (pieces of it when they exceed the budget), fn emits tensors — the
+// combiner form of reduce_batch (reference compress, src/mapreduce.cpp:749-851)
+uint64_t MapReduce::compress_batch(const ReduceBatchFn& fn) {
+  start();
+  OpTrace tr_(__func__, this);
+  enter(__func__, true);
+  need_kv("compress");
+  KMV m = local_groups("Compress");
+  KeyValue kvb(device());
+  bound(kvb);
+  if (needs_ooc(m.nbytes(), budget(), 2.0) || (device().is_cuda() && !m.seg.is_cuda())) {
+    OocStats os;
+    ooc_for_each_kmv_piece(m, ooc_env(), device(), [&](const KMV& piece) { fn(piece, kvb); }, &os);
+    note_ooc("Compress", os);
+  } else {
+    fn(m, kvb);
+  }
   set_kv_parts(kvb.finish_parts());
   note_spool(kvb);
   stats("Compress", 0);

@@ -130,6 +130,7 @@ class MapReduce {
   uint64_t collate(const HashFn& hash = nullptr);
   uint64_t compress(const ReduceFn& fn);
   uint64_t compress_builtin(const std::string& op, const std::string& dtype);
+  uint64_t compress_batch(const ReduceBatchFn& fn);
   uint64_t convert();
   // convert with the keys' hash64_keys() already computed by the producer
   uint64_t convert_prehashed(const at::Tensor& prehash);

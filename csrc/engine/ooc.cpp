@@ -46,6 +46,7 @@
 #include <tuple>
 #include <unordered_map>
 
+#include "hostarena.h"
 #include "../kernels/launch.h"
 #include "kv.h"
 #include "comm.h"
@@ -109,7 +110,9 @@ at::Tensor host(const at::Tensor& t) {
   if (!t.defined()) return t;
   if (t.is_cpu()) return t.contiguous();
   note_xfer(t, at::Device(at::kCPU));
-  return t.to(at::TensorOptions().device(at::kCPU).pinned_memory(true), /*non_blocking=*/false, /*copy=*/true);
+  at::Tensor h = hostarena::pinned_empty(t.sizes(), t.scalar_type());
+  h.copy_(t);
+  return h;
 }
 KV kv_host(const KV& kv) {
   KV o = kv;

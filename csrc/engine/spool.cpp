@@ -1,4 +1,5 @@
 // Spool (spool.h): HBM -> pinned host -> memory-mapped disk file.
+#include "hostarena.h"
 #include "xfer.h"
 #include "spool.h"
 
@@ -505,7 +506,7 @@ void fence_after_current(hipStream_t copy) {
 at::Tensor drain_tensor(const at::Tensor& t, hipStream_t copy) {
   if (!t.defined() || t.is_cpu()) return t;
   at::Tensor src = t.contiguous();
-  at::Tensor o = at::empty(src.sizes(), src.options().device(at::kCPU).pinned_memory(true));
+  at::Tensor o = hostarena::pinned_empty(src.sizes(), src.scalar_type());
   note_xfer(src, at::Device(at::kCPU));
   const size_t nb = (size_t)src.numel() * src.element_size();
   if (nb && hipMemcpyAsync(o.data_ptr(), src.data_ptr(), nb, hipMemcpyDeviceToHost, copy) != hipSuccess)
@@ -608,7 +609,8 @@ void Spool::add(const KV& piece, hipStream_t copy) {
       auto h = [&](const at::Tensor& t) {
         if (!t.defined()) return t;
         if (t.is_cpu() && (!cuda || t.is_pinned())) return t;
-        at::Tensor o = at::empty(t.sizes(), t.options().device(at::kCPU).pinned_memory(cuda));
+        at::Tensor o = cuda ? hostarena::pinned_empty(t.sizes(), t.scalar_type())
+                            : at::empty(t.sizes(), t.options().device(at::kCPU));
         note_xfer(t, at::Device(at::kCPU));
         o.copy_(t);
         return o;

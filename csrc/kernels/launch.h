@@ -403,6 +403,40 @@ void ccmr_reassign_seg(const int64_t* seg, int64_t nkey, const int64_t* keys, co
 void ccmr_reassign_emit(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vd, int64_t nval,
                         const int64_t* zone_seg, const int64_t* pos, int64_t* v, int64_t* zone, hipStream_t s);
 
+// ---------------------------------------------------------------- graphmr.hip
+// sssp_mr (oink/sssp.cpp:244-360) and luby_find_mr (oink/luby_find.cpp:120-344)
+// callbacks; voff may be null for fixed-width values of vw bytes where noted
+void sssp_pick(const int64_t* seg, int64_t nkey, const int64_t* voff, int64_t vw, const uint8_t* vd, int64_t* out,
+               int64_t* changed, hipStream_t s);
+void sssp_pick_emit(const int64_t* keys, int64_t nkey, const int64_t* dist, const int64_t* pos, int64_t* okey,
+                    int64_t* odist, hipStream_t s);
+// best = ~0 and idx = ~0 and found = 0 on entry
+void sssp_best(const int64_t* seg, int64_t nkey, const int64_t* voff, const uint8_t* vd, int64_t nval,
+               unsigned long long* best, unsigned long long* idx, int64_t* found, hipStream_t s);
+void sssp_relax_flags(const int64_t* seg, int64_t nkey, const int64_t* keys, const int64_t* voff, const uint8_t* vd,
+                      int64_t nval, const unsigned long long* idx, const int64_t* found, int64_t* fe, int64_t* fp,
+                      hipStream_t s);
+void sssp_relax_emit(const int64_t* seg, int64_t nkey, const int64_t* keys, const int64_t* voff, const uint8_t* vd,
+                     int64_t nval, const unsigned long long* idx, const int64_t* found, const int64_t* pe,
+                     const int64_t* pp, int64_t* ekey, int64_t* eval, int64_t* pkey, int64_t* pval, hipStream_t s);
+void luby_nonloop(const int64_t* e, int64_t n, int64_t* f, hipStream_t s);
+void luby_random(const int64_t* e, int64_t n, int64_t seed, const int64_t* pos, int64_t* out, hipStream_t s);
+// mark = 0 on entry; mode 0 flag-0 VFLAG, 1 value > 16 B, 2 value == 16 B, 3 value > 0 B
+void luby_mark(const int64_t* seg, int64_t nkey, const int64_t* voff, int64_t vw, const uint8_t* vd, int64_t nval,
+               int mode, int64_t* mark, hipStream_t s);
+void luby_key_flags(const int64_t* mark, int64_t nkey, int64_t want, int64_t* f, hipStream_t s);
+void luby_edge_emit(const int64_t* keys, int64_t nkey, const int64_t* pos, int64_t* okey, int64_t* oval,
+                    hipStream_t s);
+// mark null: f = value length != 16
+void luby_value_flags(const int64_t* seg, int64_t nkey, const int64_t* voff, int64_t vw, const int64_t* mark,
+                      int64_t nval, int64_t want, int64_t* f, hipStream_t s);
+void luby_vert_emit(const int64_t* seg, int64_t nkey, const int64_t* keys, const int64_t* voff, int64_t vw,
+                    const uint8_t* vd, int64_t nval, const int64_t* p24, int64_t* k24, int64_t* v24, int64_t* k16,
+                    int64_t* v16, hipStream_t s);
+void luby_edges_emit(const int64_t* seg, int64_t nkey, const int64_t* keys, const int64_t* voff, int64_t vw,
+                     const uint8_t* vd, int64_t nval, const int64_t* pf, int64_t* kf, int64_t* kn, hipStream_t s);
+void luby_mis_emit(const int64_t* keys, int64_t nkey, const int64_t* pos, int64_t* out, hipStream_t s);
+
 // ---------------------------------------------------------------- trimr.hip
 // tri_find_mr callbacks (oink/tri_find.cpp:104-325); edge rows are int64
 // pairs, degree rows int32 pairs

@@ -6,10 +6,12 @@
 // sssp, pagerank) and tri_find run on the native plans of
 // csrc/engine/graphplan.h instead of re-shuffling every edge each iteration.
 #include <algorithm>
+#include <chrono>
 #include <cinttypes>
 #include <cmath>
 #include <cstdarg>
 #include <cstdlib>
+#include <cstring>
 #include <filesystem>
 #include <limits>
 #include <random>
@@ -18,6 +20,7 @@
 
 #include "callbacks.h"
 #include "engine/ccmr.h"
+#include "engine/graphmr.h"
 #include "engine/graphplan.h"
 #include "engine/tri.h"
 #include "oink.h"
@@ -757,6 +760,228 @@ class SSSP : public Command {
   }
 };
 
+// sssp_mr ncnt seed -i weighted-edges -o file mr: the reference's MapReduce
+// formulation of SSSP (oink/sssp.cpp:49-184), the one pipeline that puts in
+// one loop an aggregate, cross-MR appends (kv->append/complete: open(1) /
+// kv_open / close here), compress as the combiner and an Allreduce
+// termination. Per iteration: aggregate the candidate distances (mrpath) to
+// their vertices' ranks; move them into mrvert; compress mrvert with
+// pick_shortest_distances, which emits every vertex's winner back and the
+// changed ones into mrpath; stop when no rank changed any (close() counts
+// over all ranks); else move mrpath into mredge (aggregated by source vertex)
+// and compress it with update_adjacent_distances, which re-emits the edges
+// and emits relaxed distances of the changed vertices' neighbours into mrpath.
+// Both compress callbacks are batch callbacks on device tensors
+// (graphmr.hip). Sources are picked as by `sssp` (vertices with out-edges,
+// shuffled by seed), so the two commands' outputs line up; the output is the
+// labelled vertices' "v distance predecessor" lines (the reference prints its
+// last mrpath, which is empty when the loop ends, oink/sssp.cpp:170-173).
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+class SSSPMR : public Command {
+ public:
+  SSSPMR(Oink& o) : Command(o) { ninputs = noutputs = 1; }
+  int64_t ncnt = 0, seed = 0;
+  void params(const Args& a) override {
+    if (a.size() != 2) throw Error("Illegal sssp_mr command");
+    ncnt = lval(a[0], "sssp_mr");
+    seed = lval(a[1], "sssp_mr");
+  }
+  void run() override {
+    constexpr double FLTMAX = 3.4028234663852886e+38;  // DISTANCE()'s weight (oink/sssp.h:50-54)
+    const at::Device dev = comm->device();
+    MapReduce& mre = obj.input(1, rd(parse_edge_weight), rc(parse_edge_weight));
+    // vertices from the edges (edge_to_vertices + collate + cull, :63-66)
+    MapReduce& mrvert = obj.create_mr();
+    mrvert.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {
+      if (!src.n) return;
+      at::Tensor e = edges_of(src);
+      add_tensors(kv, at::cat({e.select(1, 0), e.select(1, 1)}));
+    });
+    mrvert.collate();
+    mrvert.reduce_batch([](const KMV& m, KeyValue& kv) {
+      if (m.nkey) add_tensors(kv, m.keys.kdata.view(at::kLong));
+    });
+    // edges by source vertex: Vi -> EDGEVALUE {Vj, wt} (reorganize_edges + aggregate, :75-76)
+    MapReduce& mredge = obj.create_mr();
+    mredge.map_mr_batch(mre, [](const KV& src, KeyValue& kv) {
+      if (!src.n) return;
+      at::Tensor e = edges_of(src);
+      at::Tensor w = src.vw == 8 ? src.vdata.view(at::kLong)
+                                 : at::full({src.n}, (double)1.0, src.kdata.options().dtype(at::kDouble)).view(at::kLong);
+      add_tensors(kv, e.select(1, 0), at::stack({e.select(1, 1), w}, 1));
+    });
+    mredge.aggregate();
+    // sources: the distinct source vertices of the edges, every rank's, shuffled by seed
+    std::vector<int64_t> c;
+    {
+      MapReduce& mrs = obj.create_mr();
+      mrs.map_mr_batch(mredge, [](const KV& src, KeyValue& kv) {
+        if (src.n) add_tensors(kv, src.kdata.view(at::kLong));
+      });
+      at::Tensor mine = at::empty({0}, opt(dev, at::kLong));
+      mrs.compress_batch([&](const KMV& m, KeyValue&) {
+        if (m.nkey) mine = at::cat({mine, m.keys.kdata.view(at::kLong).to(dev)});
+      });
+      at::Tensor all = comm->allgather_var(mine.contiguous()).to(at::kCPU);
+      c.assign(all.data_ptr<int64_t>(), all.data_ptr<int64_t>() + all.numel());
+      std::sort(c.begin(), c.end());
+      std::mt19937_64 rng((uint64_t)seed);
+      std::shuffle(c.begin(), c.end(), rng);
+      if ((int64_t)c.size() > ncnt) c.resize((size_t)ncnt);
+    }
+    MapReduce& mrpath = obj.create_mr();
+    MapReduce& mrout = obj.create_mr();
+    const int64_t inf_bits = [&] {
+      int64_t b;
+      std::memcpy(&b, &FLTMAX, 8);
+      return b;
+    }();
+    double tcompute = 0;
+    for (size_t i = 0; i < c.size(); ++i) {
+      const int64_t source = c[i];
+      const double t0 = now_s();
+      // every vertex unreached, current (initialize_vertex_distances, :94)
+      mrvert.map_mr_batch(mrvert, [&](const KV& src, KeyValue& kv) {
+        if (!src.n) return;
+        at::Tensor d = at::empty({src.n, 3}, src.kdata.options().dtype(at::kLong));
+        d.select(1, 0).fill_(0);
+        d.select(1, 1).fill_(inf_bits);
+        d.select(1, 2).fill_(1);
+        add_tensors(kv, src.kdata.view(at::kLong), d);
+      });
+      // the source at distance 0, not yet current (add_source, :100)
+      mrpath.map(1, [&](int, KeyValue& kv) {
+        double z = 0.0;
+        int64_t d[3] = {0, 0, 0};
+        std::memcpy(&d[1], &z, 8);
+        kv.add((const char*)&source, 8, (const char*)d, 24);
+      });
+      int iter = 0;
+      while (true) {
+        ++iter;
+        mrpath.aggregate();
+        mrvert.open(1);  // mrvert->kv->append(); mrpath->map(move_to_new_mr) (:112-114)
+        mrpath.map_mr_batch(mrpath, [&](const KV& src, KeyValue&) {
+          if (src.n) mrvert.kv_open().add_kv(src);
+        });
+        mrvert.close();
+        mrpath.open();
+        mrvert.compress_batch([&](const KMV& m, KeyValue& kv) {  // pick_shortest_distances (:120-122)
+          if (!m.nkey) return;
+          SsspPick p = ssspmr_pick(m);
+          add_tensors(kv, m.keys.kdata.view(at::kLong), p.dist);
+          if (p.ckeys.numel()) add_tensors(mrpath.kv_open(), p.ckeys, p.cdist);
+        });
+        const uint64_t nchanged = mrpath.close();  // summed over ranks (:124-126)
+        if (nchanged == 0) break;
+        mredge.open(1);  // mredge->kv->append(); mrpath->map(move_to_new_mr) (:131-133)
+        mrpath.map_mr_batch(mrpath, [&](const KV& src, KeyValue&) {
+          if (src.n) mredge.kv_open().add_kv(src);
+        });
+        mredge.close();
+        mrpath.open();
+        mredge.compress_batch([&](const KMV& m, KeyValue& kv) {  // update_adjacent_distances (:135-137)
+          if (!m.nkey) return;
+          SsspRelax r = ssspmr_relax(m);
+          if (r.ekeys.numel()) add_tensors(kv, r.ekeys, r.edges);
+          if (r.pkeys.numel()) add_tensors(mrpath.kv_open(), r.pkeys, r.paths);
+        });
+        mrpath.close();
+      }
+      tcompute += now_s() - t0;
+      // labelled vertices -> (v, {distance, predecessor}) (print, :405-411)
+      int64_t nlab = 0;
+      mrout.map_mr_batch(
+          mrvert,
+          [&](const KV& src, KeyValue& kv) {
+            if (!src.n) return;
+            at::Tensor d = src.vdata.view(at::kLong).view({-1, 3});
+            at::Tensor w = d.select(1, 1).contiguous().view(at::kDouble);
+            at::Tensor ok = w < FLTMAX;
+            at::Tensor ids = src.kdata.view(at::kLong).index({ok});
+            nlab += ids.numel();
+            if (ids.numel()) add_tensors(kv, ids, at::stack({d.select(1, 1).index({ok}), d.select(1, 0).index({ok})}, 1));
+          },
+          1);
+      nlab = comm->allreduce(nlab, Comm::SUM);
+      message(fmt("%zu:  Source = %" PRId64 "; Iterations = %d; Num Vtx Labeled = %" PRId64, i, source, iter, nlab));
+    }
+    message(fmt("Total time in SSSP: %g", tcompute));
+    obj.output(1, mrout, print_sssp);
+    obj.cleanup();
+  }
+};
+
+// luby_find_mr seed -i edges -o file mr: the reference's MapReduce formulation
+// of Luby's maximal independent set (oink/luby_find.cpp:53-97). Every vertex
+// gets the reference's random number (drand48() after srand48(v + seed)),
+// edges become ERAND keys; per iteration four reduce + collate rounds: edge
+// winners (the end with the smaller (r, v)), vertices that won all their
+// edges, their neighbours (losers), and the emit round that adds the winners
+// to mrv — a second MR kept open across the whole loop (mrv->open() ...
+// close(), :73/:88) — and sends the edges back, flagged when an end was
+// removed. The loop ends when no live edge is left (reduce's global count).
+// The result is the greedy MIS in (r, v) order, so it is the reference's set
+// for the same seed. Self loops are dropped (the reference can loop forever on
+// one); an edge is deleted when any of its values is a flag (the reference
+// checks the first two only).
+class LubyFindMR : public Command {
+ public:
+  LubyFindMR(Oink& o) : Command(o) { ninputs = noutputs = 1; }
+  int64_t seed = 0;
+  void params(const Args& a) override {
+    if (a.size() != 1) throw Error("Illegal luby_find_mr command");
+    seed = lval(a[0], "luby_find_mr");
+  }
+  void run() override {
+    MapReduce& mre = obj.input(1, rd(parse_edge), rc(parse_edge));
+    MapReduce& mrv = obj.create_mr();
+    MapReduce& mrw = obj.create_mr();
+    mrw.map_mr_batch(mre, [&](const KV& src, KeyValue& kv) {  // map_vert_random (:120-136)
+      if (!src.n) return;
+      at::Tensor er = lubymr_random(edges_of(src), seed);
+      if (er.size(0)) add_tensors(kv, er);
+    });
+    mrw.clone();
+    int niter = 0;
+    mrv.open();
+    while (true) {
+      const uint64_t n = mrw.reduce_batch([](const KMV& m, KeyValue& kv) {  // reduce_edge_winner
+        if (!m.nkey) return;
+        auto [k, v] = lubymr_edge_winner(m);
+        if (k.size(0)) add_tensors(kv, k, v);
+      });
+      if (n == 0) break;
+      for (bool loser : {false, true}) {  // reduce_vert_winner, reduce_vert_loser
+        mrw.collate();
+        mrw.reduce_batch([&](const KMV& m, KeyValue& kv) {
+          if (!m.nkey) return;
+          LubyVert r = lubymr_vert(m, loser);
+          if (r.k24.size(0)) add_tensors(kv, r.k24, r.v24);
+          if (r.k16.size(0)) add_tensors(kv, r.k16, r.v16);
+        });
+      }
+      mrw.collate();
+      mrw.reduce_batch([&](const KMV& m, KeyValue& kv) {  // reduce_vert_emit
+        if (!m.nkey) return;
+        LubyEmit r = lubymr_emit(m);
+        if (r.mis.numel()) add_tensors(mrv.kv_open(), r.mis);
+        if (r.kflag.size(0)) add_tensors(kv, r.kflag, r.fval);
+        if (r.knull.size(0)) add_tensors(kv, r.knull);
+      });
+      mrw.collate();
+      ++niter;
+    }
+    const uint64_t nset = mrv.close();
+    obj.output(1, mrv, print_vertex);
+    message(fmt("Luby_find: %" PRIu64 " MIS vertices in %d iterations", nset, niter));
+    obj.cleanup();
+  }
+};
+
 // pagerank tol maxiter alpha -i edges -o file mr (the reference command is a
 // stub, oink/pagerank.cpp:54-56; implemented per oinkdoc/pagerank.txt)
 class PageRankCmd : public Command {
@@ -814,6 +1039,8 @@ struct Registrar {
     r["cc_stats"] = factory<CCStats>();
     r["luby_find"] = factory<LubyFind>();
     r["sssp"] = factory<SSSP>();
+    r["sssp_mr"] = factory<SSSPMR>();
+    r["luby_find_mr"] = factory<LubyFindMR>();
     r["pagerank"] = factory<PageRankCmd>();
   }
 } registrar;

@@ -7,12 +7,9 @@ HIP/CDNA4 kernels for hashing, partitioning, radix sort, group-by, segmented
 reduce and text/graph maps, and an RCCL all-to-all shuffle over xGMI with one
 process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm).
 """
-from . import hostpin as _hostpin
-
-_hostpin.configure()  # MRH_PIN_RESERVE_MB: before torch reads its allocator configuration
-from ._ext import C, so_path  # noqa: F401,E402
-from .parallel.comm import Comm, init, world  # noqa: F401,E402
-from .runtime.keyvalue import KeyValue, to_bytes  # noqa: F401,E402
-from .runtime.mapreduce import MapReduce, MultiValue  # noqa: F401,E402
+from ._ext import C, so_path  # noqa: F401
+from .parallel.comm import Comm, init, world  # noqa: F401
+from .runtime.keyvalue import KeyValue, to_bytes  # noqa: F401
+from .runtime.mapreduce import MapReduce, MultiValue  # noqa: F401
 
 __version__ = "0.1.0"

@@ -286,6 +286,12 @@ class MapReduce(metaclass=_Counters):
         f = _bind(fn, 3, ptr)
         return self._m.compress(lambda k, vals, h: f(k, MultiValue.of(vals), KeyValue.wrap(h)))
 
+    def compress_batch(self, fn, ptr=None):
+        """Device-tier compress: fn(kmv, kv[, ptr]) gets this rank's local
+        groups as one native KMV (no shuffle) and emits tensors."""
+        f = _bind(fn, 2, ptr)
+        return self._m.compress_batch(lambda kmv, h: f(kmv, KeyValue.wrap(h)))
+
     def scan_kv(self, fn, ptr=None):
         """Read-only fn(key, value[, ptr]) over the KV (reference :1933-1976)."""
         return self._m.scan_kv(_bind(fn, 2, ptr))
