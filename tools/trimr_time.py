@@ -29,11 +29,9 @@ if os.environ.get("NUMA") == "1":  # bind like bench.py's ranks (parallel/comm.p
     from gpu_mapreduce_amd.parallel.comm import bind_numa_local
     print("numa cpus", bind_numa_local(0), "of", len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else "?")
 comm = g.Comm(device=os.environ.get("DEV", "cuda:0"))
-if os.environ.get("PREPIN") == "1":  # the first pinned allocation before the job (the reserve segment, if configured)
-    import time as _tp
-    _t0 = _tp.perf_counter()
-    torch.empty(1, pin_memory=True)
-    print(f"prepin {(_tp.perf_counter() - _t0) * 1e3:.1f} ms ({os.environ.get('PYTORCH_HIP_ALLOC_CONF', '')})", flush=True)
+if os.environ.get("PREPIN"):  # PREPIN=MiB: the pinned host arena before the job (gpu_mapreduce_amd/hostpin.py)
+    from gpu_mapreduce_amd import hostpin
+    print(f"prepin {os.environ['PREPIN']} MiB: {hostpin.prepin(int(os.environ['PREPIN'])):.1f} ms", flush=True)
 if os.environ.get("HEARTBEAT"):  # a line every N s: long out-of-core runs are not taken for hung
     import threading
     import time as _t
@@ -102,6 +100,8 @@ for rep in range(int(os.environ.get("REPS", "2"))):
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     tot = sum(s["ms"] for s in r["stages"])
+    if os.environ.get("PREPIN"):
+        print("   arena", hostpin.stats(), flush=True)
     print(f"rep {rep}: {tot:.1f} ms, {r['triangles']} triangles"
           + (f" (check {want}: {'equal' if int(r['triangles']) == int(want) else 'DIFFERENT'})"
              if os.environ.get("CHECK") == "1" else ""), flush=True)
