@@ -18,6 +18,7 @@
 #include <unistd.h>
 #include <string>
 
+#include "devfn.h"
 #include "graphmr.h"
 #include "hostarena.h"
 #include "kv.h"
@@ -495,6 +496,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              py::gil_scoped_release nogil;
              return r.reduce_batch([&](const KMV& s, KeyValue& kv) { py::gil_scoped_acquire g; fn(s, kvref(kv)); });
            })
+      .def("map_device", &MR::map_device, py::arg("src"), py::arg("code"), py::arg("addflag") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("map_device_tasks", &MR::map_device_tasks, py::arg("ntask"), py::arg("code"), py::arg("addflag") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("reduce_device", &MR::reduce_device, py::call_guard<py::gil_scoped_release>())
+      .def("compress_device", &MR::compress_device, py::call_guard<py::gil_scoped_release>())
       .def("compress_batch",
            [](MR& r, py::function fn) {
              py::gil_scoped_release nogil;
@@ -945,6 +952,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     LubyEmit r = lubymr_emit(m);
     return py::make_tuple(r.mis, r.kflag, r.fval, r.knull);
   });
+  m.def("device_functor_check", &devfn::compile_check, py::arg("code"), py::arg("reduce"),
+        py::call_guard<py::gil_scoped_release>());
+  m.def("device_functor_source", &devfn::full_source, py::arg("code"), py::arg("reduce"));
   m.def("host_arena_reserve", &hostarena::reserve, py::call_guard<py::gil_scoped_release>());
   m.def("host_arena_stats", [] {
     hostarena::Stats s = hostarena::stats();

@@ -1,5 +1,6 @@
 // Native MapReduce object (see mapreduce.h). Reference behaviour cited per
 // method as src/mapreduce.cpp:<lines>.
+#include "devfn.h"
 #include "hostarena.h"
 #include "xfer.h"
 #include "mapreduce.h"
@@ -1365,6 +1366,53 @@ uint64_t MapReduce::compress_batch(const ReduceBatchFn& fn) {
   note_spool(kvb);
   stats("Compress", 0);
   return count(kv_rows());
+}
+
+// ====================================================================== device functors
+
+uint64_t MapReduce::map_device(MapReduce& src, const std::string& code, int addflag) {
+  const at::Device dev = device();
+  return map_mr_batch(
+      src,
+      [&](const KV& kv, KeyValue& out) {
+        if (!kv.n) return;
+        KV o = devfn::map_pairs(kv, code, dev);
+        if (o.n) out.add_kv(o);
+      },
+      addflag);
+}
+
+uint64_t MapReduce::map_device_tasks(int64_t ntask, const std::string& code, int addflag) {
+  // one map task per rank-sized range of the ntask items: task t runs
+  // [t * ntask / P, (t + 1) * ntask / P) in one launch (any mapstyle)
+  const int64_t P = comm_->size();
+  const at::Device dev = device();
+  return map(
+      (int)P,
+      [&](int t, KeyValue& out) {
+        const int64_t a = (int64_t)t * ntask / P, b = (int64_t)(t + 1) * ntask / P;
+        KV o = devfn::map_tasks(a, b - a, code, dev);
+        if (o.n) out.add_kv(o);
+      },
+      addflag);
+}
+
+uint64_t MapReduce::reduce_device(const std::string& code) {
+  const at::Device dev = device();
+  return reduce_batch([&](const KMV& m, KeyValue& out) {
+    if (!m.nkey) return;
+    KV o = devfn::reduce_groups(m, code, dev);
+    if (o.n) out.add_kv(o);
+  });
+}
+
+uint64_t MapReduce::compress_device(const std::string& code) {
+  const at::Device dev = device();
+  return compress_batch([&](const KMV& m, KeyValue& out) {
+    if (!m.nkey) return;
+    KV o = devfn::reduce_groups(m, code, dev);
+    if (o.n) out.add_kv(o);
+  });
 }
 
 uint64_t MapReduce::compress_builtin(const std::string& op, const std::string& dtype) {

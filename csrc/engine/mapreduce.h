@@ -131,6 +131,11 @@ class MapReduce {
   uint64_t compress(const ReduceFn& fn);
   uint64_t compress_builtin(const std::string& op, const std::string& dtype);
   uint64_t compress_batch(const ReduceBatchFn& fn);
+  // device functors (devfn.h): user HIP device code compiled at run time
+  uint64_t map_device(MapReduce& src, const std::string& code, int addflag = 0);
+  uint64_t map_device_tasks(int64_t ntask, const std::string& code, int addflag = 0);
+  uint64_t reduce_device(const std::string& code);
+  uint64_t compress_device(const std::string& code);
   uint64_t convert();
   // convert with the keys' hash64_keys() already computed by the producer
   uint64_t convert_prehashed(const at::Tensor& prehash);

@@ -292,6 +292,25 @@ class MapReduce(metaclass=_Counters):
         f = _bind(fn, 2, ptr)
         return self._m.compress_batch(lambda kmv, h: f(kmv, KeyValue.wrap(h)))
 
+    # ---- device functors (csrc/engine/devfn.h): HIP device code compiled at run time
+    def map_device(self, src, code, addflag=0):
+        """map with a device functor: `src` a MapReduce (every pair through
+        `__device__ void mr_map(mrd::Bytes key, mrd::Bytes value, long long
+        index, mrd::Emit& out)`) or a task count (key / value empty, index =
+        the task). One GPU thread per pair / task; no host round trip."""
+        if isinstance(src, int):
+            return self._m.map_device_tasks(int(src), code, addflag)
+        return self._m.map_device(src._m, code, addflag)
+
+    def reduce_device(self, code):
+        """reduce with a device functor: every key through `__device__ void
+        mr_reduce(mrd::Bytes key, mrd::Values values, mrd::Emit& out)`."""
+        return self._m.reduce_device(code)
+
+    def compress_device(self, code):
+        """compress (local groups, no shuffle) with a device reduce functor."""
+        return self._m.compress_device(code)
+
     def scan_kv(self, fn, ptr=None):
         """Read-only fn(key, value[, ptr]) over the KV (reference :1933-1976)."""
         return self._m.scan_kv(_bind(fn, 2, ptr))

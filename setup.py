@@ -62,7 +62,7 @@ HOSTDEFS = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_A
 HOSTFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-result", "-Wno-sign-compare", *HOSTDEFS,
              "-I", os.path.join(here, "csrc"), "-I", os.path.join(ROCM, "include")] + \
             [f"-I{p}" for p in include_paths()]
-LINKLIBS = [f"-L{os.path.join(ROCM, 'lib')}", f"-L{_torch_lib()}", "-lamdhip64", "-lc10_hip", "-ltorch_hip",
+LINKLIBS = [f"-L{os.path.join(ROCM, 'lib')}", f"-L{_torch_lib()}", "-lamdhip64", "-lhiprtc", "-lc10_hip", "-ltorch_hip",
             "-lc10", "-ltorch", "-ltorch_cpu", "-lrocprofiler-sdk-roctx",
             # RCCL: no -lrccl on purpose. The nccl* symbols resolve at load
             # time from the librccl that libtorch_hip already depends on, so a
