@@ -214,6 +214,18 @@ uint64_t MR_reduce(void* p, CReduce f, void* app) {
 uint64_t MR_reduce_builtin(void* p, const char* op, const char* dtype) {
   return guard([&] { return M(p)->reduce_builtin(op, dtype ? dtype : "int32"); }, (uint64_t)0);
 }
+uint64_t MR_map_device(void* p, void* src, const char* code, int addflag) {
+  return guard([&] { return M(p)->map_device(*M(src), code, addflag); }, (uint64_t)0);
+}
+uint64_t MR_map_device_tasks(void* p, uint64_t ntask, const char* code, int addflag) {
+  return guard([&] { return M(p)->map_device_tasks((int64_t)ntask, code, addflag); }, (uint64_t)0);
+}
+uint64_t MR_reduce_device(void* p, const char* code) {
+  return guard([&] { return M(p)->reduce_device(code); }, (uint64_t)0);
+}
+uint64_t MR_compress_device(void* p, const char* code) {
+  return guard([&] { return M(p)->compress_device(code); }, (uint64_t)0);
+}
 uint64_t MR_multivalue_blocks(void* p, int* nblock) {
   int nb = 0;
   uint64_t n = M(p)->multivalue_blocks(nb);

@@ -79,6 +79,12 @@ uint64_t MR_reduce(void *MRptr, void (*myreduce)(char *, int, char *, int, int *
                    void *APPptr);
 /* built-in device reducers: op = count|sum|min|max|first|last, dtype = int32|int64|float32|float64 */
 uint64_t MR_reduce_builtin(void *MRptr, const char *op, const char *dtype);
+/* device functors: HIP device source defining mr_map / mr_reduce (csrc/engine/devfn.h),
+   compiled at run time for the GPU; a GPU MapReduce only */
+uint64_t MR_map_device(void *MRptr, void *MRptr2, const char *code, int addflag);
+uint64_t MR_map_device_tasks(void *MRptr, uint64_t ntask, const char *code, int addflag);
+uint64_t MR_reduce_device(void *MRptr, const char *code);
+uint64_t MR_compress_device(void *MRptr, const char *code);
 uint64_t MR_multivalue_blocks(void *MRptr, int *nblock);
 void MR_multivalue_block_select(void *MRptr, int which);
 int MR_multivalue_block(void *MRptr, int iblock, char **ptr_multivalue, int **ptr_valuesizes);

@@ -269,3 +269,12 @@ def test_native_apps_gpu(tmp_path):
                  gpu=True)
     histo = lambda o: [ln for ln in o.splitlines() if "rows with" in ln]
     assert histo(cpu) == histo(gpu) != []
+
+
+@pytest.mark.gpu
+def test_c_api_device_functors_gpu(tmp_path):
+    """MR_map_device_tasks + MR_collate + MR_reduce_device (examples/c/cdevice.c):
+    map and reduce are device source strings compiled at run time"""
+    exe = _cc(os.path.join(ROOT, "examples", "c", "cdevice.c"), tmp_path / "cdevice")
+    out = launch([exe, "1000003", "101"], 1, tmp_path, gpu=True)
+    assert "keys 101 sum 1000003 count0 9902" in out, out
