@@ -69,8 +69,8 @@ struct Emit {
   i64* ovoff;
   __device__ void emit(const void* k, i64 kn, const void* v, i64 vn) {
     if (write) {
-      okoff[nrec] = kb;
-      ovoff[nrec] = vb;
+      if (okoff) okoff[nrec] = kb;
+      if (ovoff) ovoff[nrec] = vb;
       const u8* ks = (const u8*)k;
       const u8* vs = (const u8*)v;
       for (i64 i = 0; i < kn; ++i) okd[kb + i] = ks[i];
@@ -136,20 +136,23 @@ mrd_count(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* v
     atomicMax(wid + 3, vmax);
   }
 }
+// okw / ovw >= 0: every record's key / value has that width (the count pass
+// said so): byte positions follow from the record position, no offsets
 extern "C" __global__ void __launch_bounds__(256)
 mrd_write(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* vd, const mrd::i64* voff,
-          mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, const mrd::i64* pos, mrd::u8* okd,
-          mrd::i64* okoff, mrd::u8* ovd, mrd::i64* ovoff) {
-  const mrd::i64 np = n + 1;  // pos holds three scans of n + 1
+          mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, const mrd::i64* pos, mrd::i64 okw,
+          mrd::i64 ovw, mrd::u8* okd, mrd::i64* okoff, mrd::u8* ovd, mrd::i64* ovoff) {
+  const mrd::i64 np = n + 1;  // pos: scans of n + 1 (records, then key bytes, value bytes when variable)
   for (mrd::i64 i = (mrd::i64)blockIdx.x * 256 + threadIdx.x; i < n; i += (mrd::i64)gridDim.x * 256) {
     const mrd::i64 r = pos[i];
     if (pos[i + 1] == r) continue;
-    const mrd::i64 k0 = pos[np + i], v0 = pos[2 * np + i];
-    mrd::Emit e{true, 0, 0, 0, 0, 0, 0, 0, okd + k0, okoff + r, ovd + v0, ovoff + r};
+    const mrd::i64 k0 = okw >= 0 ? r * okw : pos[np + i], v0 = ovw >= 0 ? r * ovw : pos[2 * np + i];
+    mrd::Emit e{true, 0, 0, 0, 0, 0, 0, 0, okd + k0, okw >= 0 ? nullptr : okoff + r, ovd + v0,
+                ovw >= 0 ? nullptr : ovoff + r};
     mrd::run_item(kd, koff, kw, vd, voff, vw, seg, first, i, e);
     for (mrd::i64 j = 0; j < e.nrec; ++j) {  // offsets relative to the item -> absolute
-      okoff[r + j] += k0;
-      ovoff[r + j] += v0;
+      if (okw < 0) okoff[r + j] += k0;
+      if (ovw < 0) ovoff[r + j] += v0;
     }
   }
 }
@@ -254,24 +257,39 @@ KV run(const Items& it, const std::string& code, bool reduce, at::Device dev) {
     void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &first, &n, &c, &w};
     launch(m.count, it.n, args, s);
   }
-  // three scans (records, key bytes, value bytes) of n + 1 each
-  at::Tensor pos = at::empty({3 * (it.n + 1)}, opt(dev, at::kLong));
-  for (int c = 0; c < 3; ++c) pos.narrow(0, c * (it.n + 1), it.n + 1).copy_(exclusive_scan(cnt.narrow(0, c * it.n, it.n)));
-  int64_t tot[3] = {0, 0, 0};
+  // the record widths first: uniform widths need only the record scan
   int64_t wh[4] = {0, 0, 0, 0};
+  read_small(s, {{P0<int64_t>(wid), wh, 32}});
+  const int64_t okw = (wh[0] == wh[1]) ? wh[0] : -1, ovw = (wh[2] == wh[3]) ? wh[2] : -1;
+  at::Tensor pos = at::empty({3 * (it.n + 1)}, opt(dev, at::kLong));
+  for (int c = 0; c < 3; ++c) {
+    if ((c == 1 && okw >= 0) || (c == 2 && ovw >= 0)) continue;
+    pos.narrow(0, c * (it.n + 1), it.n + 1).copy_(exclusive_scan(cnt.narrow(0, c * it.n, it.n)));
+  }
   const int64_t* pp = P0<int64_t>(pos);
-  read_small(s, {{pp + it.n, &tot[0], 8}, {pp + 2 * (it.n + 1) - 1, &tot[1], 8}, {pp + 3 * (it.n + 1) - 1, &tot[2], 8},
-                 {P0<int64_t>(wid), wh, 32}});
+  int64_t tot[3] = {0, 0, 0};
+  {
+    const SmallRead rec{pp + it.n, &tot[0], 8}, kb{pp + 2 * (it.n + 1) - 1, &tot[1], 8},
+        vb{pp + 3 * (it.n + 1) - 1, &tot[2], 8};
+    if (okw < 0 && ovw < 0) read_small(s, {rec, kb, vb});
+    else if (okw < 0) read_small(s, {rec, kb});
+    else if (ovw < 0) read_small(s, {rec, vb});
+    else read_small(s, {rec});
+  }
   const int64_t nout = tot[0];
+  if (okw >= 0) tot[1] = nout * okw;
+  if (ovw >= 0) tot[2] = nout * ovw;
   out.n = nout;
   out.kdata = at::empty({tot[1]}, opt(dev, at::kByte));
   out.vdata = at::empty({tot[2]}, opt(dev, at::kByte));
-  out.koff = at::empty({nout + 1}, opt(dev, at::kLong));
-  out.voff = at::empty({nout + 1}, opt(dev, at::kLong));
+  if (nout && okw >= 0) out.kw = (int)okw;
+  else out.koff = at::empty({nout + 1}, opt(dev, at::kLong));
+  if (nout && ovw >= 0) out.vw = (int)ovw;
+  else out.voff = at::empty({nout + 1}, opt(dev, at::kLong));
   if (nout) {
     const uint8_t* kd = it.kd;
     const int64_t* koff = it.koff;
-    int64_t kw = it.kw, vw = it.vw, first = it.first, n = it.n;
+    int64_t kw = it.kw, vw = it.vw, first = it.first, n = it.n, kwo = okw, vwo = ovw;
     const uint8_t* vd = it.vd;
     const int64_t* voff = it.voff;
     const int64_t* seg = it.seg;
@@ -279,19 +297,11 @@ KV run(const Items& it, const std::string& code, bool reduce, at::Device dev) {
     uint8_t* ovd = P0<uint8_t>(out.vdata);
     int64_t* okoff = P0<int64_t>(out.koff);
     int64_t* ovoff = P0<int64_t>(out.voff);
-    void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &first, &n, &pp, &okd, &okoff, &ovd, &ovoff};
+    void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &first, &n, &pp, &kwo, &vwo, &okd, &okoff, &ovd, &ovoff};
     launch(m.write, it.n, args, s);
   }
-  k::fill_i64(P0<int64_t>(out.koff) + nout, 1, tot[1], s);
-  k::fill_i64(P0<int64_t>(out.voff) + nout, 1, tot[2], s);
-  if (nout && wh[0] == wh[1]) {  // uniform widths: fixed-width columns
-    out.kw = (int)wh[0];
-    out.koff = at::Tensor();
-  }
-  if (nout && wh[2] == wh[3]) {
-    out.vw = (int)wh[2];
-    out.voff = at::Tensor();
-  }
+  if (out.koff.defined()) k::fill_i64(P0<int64_t>(out.koff) + nout, 1, tot[1], s);
+  if (out.voff.defined()) k::fill_i64(P0<int64_t>(out.voff) + nout, 1, tot[2], s);
   return out;
 }
 }  // namespace
