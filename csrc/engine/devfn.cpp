@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <cstdlib>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -102,9 +103,23 @@ __device__ inline Bytes field(const u8* d, const i64* off, i64 w, i64 i) {
   if (!d) return Bytes{nullptr, 0};
   return off ? Bytes{d + off[i], off[i + 1] - off[i]} : Bytes{d + i * w, w};
 }
+__device__ inline i64 seg_of(const i64* seg, i64 nseg, i64 j) {
+  i64 lo = 0, hi = nseg;
+  while (hi - lo > 1) {
+    const i64 mid = (lo + hi) >> 1;
+    if (seg[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
 __device__ inline void run_item(const u8* kd, const i64* koff, i64 kw, const u8* vd, const i64* voff, i64 vw,
                                 const i64* seg, i64 first, i64 i, Emit& e) {
-#if MRD_REDUCE
+#if MRD_REDUCE == 2
+  // fold: vd = the merged accumulators, voff = each key's first chunk, vw = sizeof(mr_acc)
+  mr_acc a;
+  __builtin_memcpy(&a, vd + voff[i] * vw, sizeof(mr_acc));
+  mr_finish(field(kd, koff, kw, i), a, e);
+#elif MRD_REDUCE
   Values vals{vd + 0, voff, vw, seg[i + 1] - seg[i]};
   if (voff) vals.off = voff + seg[i];
   else vals.d = vd + seg[i] * vw;
@@ -136,6 +151,47 @@ mrd_count(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* v
     atomicMax(wid + 3, vmax);
   }
 }
+#if MRD_REDUCE == 2
+// fold tier: a key's values in chunks of C, one thread per chunk (so a key
+// with millions of values spreads over the whole GPU), then one thread per
+// key merges its chunks' accumulators into the first
+extern "C" __global__ void mrd_acc_size(mrd::i64* out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = sizeof(mr_acc);
+}
+extern "C" __global__ void __launch_bounds__(256)
+mrd_fold_nchunks(const mrd::i64* seg, mrd::i64 nkey, mrd::i64 C, mrd::i64* cnt) {
+  for (mrd::i64 s = (mrd::i64)blockIdx.x * 256 + threadIdx.x; s < nkey; s += (mrd::i64)gridDim.x * 256)
+    cnt[s] = (seg[s + 1] - seg[s] + C - 1) / C;
+}
+extern "C" __global__ void __launch_bounds__(256)
+mrd_fold_chunks(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* vd, const mrd::i64* voff,
+                mrd::i64 vw, const mrd::i64* seg, mrd::i64 nkey, const mrd::i64* cstart, mrd::i64 nchunk,
+                mrd::i64 C, mrd::u8* accs) {
+  for (mrd::i64 c = (mrd::i64)blockIdx.x * 256 + threadIdx.x; c < nchunk; c += (mrd::i64)gridDim.x * 256) {
+    const mrd::i64 s = mrd::seg_of(cstart, nkey, c);
+    const mrd::i64 a0 = seg[s] + (c - cstart[s]) * C;
+    const mrd::i64 a1 = a0 + C < seg[s + 1] ? a0 + C : seg[s + 1];
+    mr_acc a;
+    mr_init(mrd::field(kd, koff, kw, s), a);
+    for (mrd::i64 v = a0; v < a1; ++v) mr_add(a, mrd::field(vd, voff, vw, v));
+    __builtin_memcpy(accs + c * sizeof(mr_acc), &a, sizeof(mr_acc));
+  }
+}
+extern "C" __global__ void __launch_bounds__(256)
+mrd_fold_merge(const mrd::i64* cstart, mrd::i64 nkey, mrd::u8* accs) {
+  for (mrd::i64 s = (mrd::i64)blockIdx.x * 256 + threadIdx.x; s < nkey; s += (mrd::i64)gridDim.x * 256) {
+    const mrd::i64 c0 = cstart[s], c1 = cstart[s + 1];
+    if (c1 - c0 < 2) continue;
+    mr_acc a, b;
+    __builtin_memcpy(&a, accs + c0 * sizeof(mr_acc), sizeof(mr_acc));
+    for (mrd::i64 c = c0 + 1; c < c1; ++c) {
+      __builtin_memcpy(&b, accs + c * sizeof(mr_acc), sizeof(mr_acc));
+      mr_merge(a, b);
+    }
+    __builtin_memcpy(accs + c0 * sizeof(mr_acc), &a, sizeof(mr_acc));
+  }
+}
+#endif
 // okw / ovw >= 0: every record's key / value has that width (the count pass
 // said so): byte positions follow from the record position, no offsets
 extern "C" __global__ void __launch_bounds__(256)
@@ -161,7 +217,9 @@ mrd_write(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* v
 struct Module {
   hipModule_t mod = nullptr;
   hipFunction_t count = nullptr, write = nullptr;
+  hipFunction_t acc_size = nullptr, nchunks = nullptr, chunks = nullptr, merge = nullptr;  // fold tier
 };
+const char* kind_name(int kind) { return kind == 0 ? "mrd_map.hip" : kind == 1 ? "mrd_reduce.hip" : "mrd_fold.hip"; }
 
 std::string compile(const std::string& src, const char* name) {
   hiprtcProgram p;
@@ -185,18 +243,24 @@ std::string compile(const std::string& src, const char* name) {
   return code;
 }
 
-const Module& module_for(const std::string& code, bool reduce, int device) {
+const Module& module_for(const std::string& code, int kind, int device) {
   static std::mutex mu;
   static std::unordered_map<std::string, std::unique_ptr<Module>> cache;
-  const std::string key = std::to_string(device) + (reduce ? "R" : "M") + code;
+  const std::string key = std::to_string(device) + ":" + std::to_string(kind) + ":" + code;
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return *it->second;
-  const std::string obj = compile(full_source(code, reduce), reduce ? "mrd_reduce.hip" : "mrd_map.hip");
+  const std::string obj =
+      compile("#define MRD_REDUCE " + std::to_string(kind) + "\n" + kDevicePrelude + code + "\n" + kKernels,
+              kind_name(kind));
   auto m = std::make_unique<Module>();
   if (hipModuleLoadData(&m->mod, obj.data()) != hipSuccess ||
       hipModuleGetFunction(&m->count, m->mod, "mrd_count") != hipSuccess ||
-      hipModuleGetFunction(&m->write, m->mod, "mrd_write") != hipSuccess) {
+      hipModuleGetFunction(&m->write, m->mod, "mrd_write") != hipSuccess ||
+      (kind == 2 && (hipModuleGetFunction(&m->acc_size, m->mod, "mrd_acc_size") != hipSuccess ||
+                     hipModuleGetFunction(&m->nchunks, m->mod, "mrd_fold_nchunks") != hipSuccess ||
+                     hipModuleGetFunction(&m->chunks, m->mod, "mrd_fold_chunks") != hipSuccess ||
+                     hipModuleGetFunction(&m->merge, m->mod, "mrd_fold_merge") != hipSuccess))) {
     (void)hipGetLastError();
     throw std::runtime_error("mrhip: loading the device functor's code object failed");
   }
@@ -228,7 +292,7 @@ struct Items {
   int64_t first = 0, n = 0;
 };
 
-KV run(const Items& it, const std::string& code, bool reduce, at::Device dev) {
+KV run(const Items& it, const std::string& code, int kind, at::Device dev) {
   if (!dev.is_cuda()) throw std::runtime_error("mrhip: device functors run on a GPU MapReduce (device cuda)");
   KV out;
   out.kw = out.vw = -1;
@@ -238,7 +302,7 @@ KV run(const Items& it, const std::string& code, bool reduce, at::Device dev) {
     out.vdata = at::empty({0}, opt(dev, at::kByte));
     return out;
   }
-  const Module& m = module_for(code, reduce, dev.index());
+  const Module& m = module_for(code, kind, dev.index());
   hipStream_t s = at::hip::getCurrentHIPStream();
   at::Tensor cnt = at::empty({3 * it.n}, opt(dev, at::kLong));
   at::Tensor wid = at::empty({4}, opt(dev, at::kLong));
@@ -306,12 +370,16 @@ KV run(const Items& it, const std::string& code, bool reduce, at::Device dev) {
 }
 }  // namespace
 
+int kind_of(const std::string& code, bool reduce) {
+  return !reduce ? 0 : code.find("mr_finish") != std::string::npos ? 2 : 1;
+}
+
 std::string full_source(const std::string& code, bool reduce) {
-  return std::string("#define MRD_REDUCE ") + (reduce ? "1" : "0") + "\n" + kDevicePrelude + code + "\n" + kKernels;
+  return "#define MRD_REDUCE " + std::to_string(kind_of(code, reduce)) + "\n" + kDevicePrelude + code + "\n" + kKernels;
 }
 
 int64_t compile_check(const std::string& code, bool reduce) {
-  return (int64_t)compile(full_source(code, reduce), reduce ? "mrd_reduce.hip" : "mrd_map.hip").size();
+  return (int64_t)compile(full_source(code, reduce), kind_name(kind_of(code, reduce))).size();
 }
 
 KV map_pairs(const KV& kv_in, const std::string& code, at::Device dev) {
@@ -324,14 +392,14 @@ KV map_pairs(const KV& kv_in, const std::string& code, at::Device dev) {
   it.voff = kv.vfixed() ? nullptr : P0<int64_t>(kv.voff);
   it.vw = kv.vfixed() ? kv.vw : 0;
   it.n = kv.n;
-  return run(it, code, false, dev);
+  return run(it, code, 0, dev);
 }
 
 KV map_tasks(int64_t first, int64_t n, const std::string& code, at::Device dev) {
   Items it;
   it.first = first;
   it.n = n;
-  return run(it, code, false, dev);
+  return run(it, code, 0, dev);
 }
 
 KV reduce_groups(const KMV& m, const std::string& code, at::Device dev) {
@@ -346,7 +414,53 @@ KV reduce_groups(const KMV& m, const std::string& code, at::Device dev) {
   it.vw = m.vw >= 0 ? m.vw : 0;
   it.seg = P0<int64_t>(m.seg);
   it.n = m.nkey;
-  return run(it, code, true, dev);
+  if (kind_of(code, true) == 1) return run(it, code, 1, dev);
+  // fold tier: accumulators per chunk of values, merged per key, then mr_finish per key
+  if (!it.n) return run(it, code, 2, dev);
+  const Module& mod = module_for(code, 2, dev.index());
+  hipStream_t s = at::hip::getCurrentHIPStream();
+  static const int64_t C = [] {
+    const char* e = std::getenv("MRH_FOLD_CHUNK");
+    return e && std::atoll(e) > 0 ? std::atoll(e) : int64_t(256);
+  }();
+  at::Tensor asz_t = at::empty({1}, opt(dev, at::kLong));
+  {
+    int64_t* o = P0<int64_t>(asz_t);
+    void* args[] = {&o};
+    launch(mod.acc_size, 1, args, s);
+  }
+  at::Tensor cnt = at::empty({it.n}, opt(dev, at::kLong));
+  {
+    const int64_t* seg = it.seg;
+    int64_t nkey = it.n, c = C;
+    int64_t* o = P0<int64_t>(cnt);
+    void* args[] = {&seg, &nkey, &c, &o};
+    launch(mod.nchunks, it.n, args, s);
+  }
+  at::Tensor cstart = exclusive_scan(cnt);
+  int64_t asz = 0, nchunk = 0;
+  read_small(s, {{P0<int64_t>(asz_t), &asz, 8}, {P0<int64_t>(cstart) + it.n, &nchunk, 8}});
+  at::Tensor accs = at::empty({std::max<int64_t>(1, nchunk * asz)}, opt(dev, at::kByte));
+  {
+    const uint8_t* kd = it.kd;
+    const int64_t* koff = it.koff;
+    int64_t kw = it.kw, vw = it.vw, nkey = it.n, nc = nchunk, c = C;
+    const uint8_t* vd = it.vd;
+    const int64_t* voff = it.voff;
+    const int64_t* seg = it.seg;
+    const int64_t* cs = P0<int64_t>(cstart);
+    uint8_t* a = P0<uint8_t>(accs);
+    void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &nkey, &cs, &nc, &c, &a};
+    launch(mod.chunks, nchunk, args, s);
+    void* margs[] = {&cs, &nkey, &a};
+    launch(mod.merge, it.n, margs, s);
+  }
+  Items f = it;
+  f.vd = P0<uint8_t>(accs);
+  f.voff = P0<int64_t>(cstart);
+  f.vw = asz;
+  f.seg = nullptr;
+  return run(f, code, 2, dev);
 }
 
 }  // namespace devfn

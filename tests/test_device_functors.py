@@ -113,3 +113,58 @@ __device__ void mr_reduce(mrd::Bytes key, mrd::Values vals, mrd::Emit& out) {
 """)
     got = {k.decode(): struct.unpack("<q", v)[0] for k, v in pairs(mr)}
     assert got == {w: c * len(w) for w, c in want.items()}
+
+
+# the fold tier: an accumulator per chunk of values (one thread per chunk),
+# merged per key, finished per key — hot keys spread over the whole GPU
+FOLD = r"""
+struct mr_acc { long long s; long long n; int mn; int mx; };
+__device__ void mr_init(mrd::Bytes key, mr_acc& a) { a.s = 0; a.n = 0; a.mn = 2147483647; a.mx = -2147483647 - 1; }
+__device__ void mr_add(mr_acc& a, mrd::Bytes v) {
+  const int x = v.as<int>();
+  a.s += x; a.n += 1; a.mn = x < a.mn ? x : a.mn; a.mx = x > a.mx ? x : a.mx;
+}
+__device__ void mr_merge(mr_acc& a, const mr_acc& b) {
+  a.s += b.s; a.n += b.n; a.mn = b.mn < a.mn ? b.mn : a.mn; a.mx = b.mx > a.mx ? b.mx : a.mx;
+}
+__device__ void mr_finish(mrd::Bytes key, const mr_acc& a, mrd::Emit& out) {
+  long long r[4] = {a.s, a.n, a.mn, a.mx};
+  out.emit(key.p, key.n, r, 32);
+}
+"""
+
+HOT = r"""
+// task t -> key (t % 3 == 0 ? 0 : t % 1000), value t % 1009 - 500: key 0 holds a third of all pairs
+__device__ void mr_map(mrd::Bytes key, mrd::Bytes value, long long t, mrd::Emit& out) {
+  out.emit((long long)(t % 3 == 0 ? 0 : t % 1000), (int)(t % 1009 - 500));
+}
+"""
+
+
+def test_fold_functor_compiles():
+    assert C.device_functor_check(FOLD, True) > 0
+    assert "#define MRD_REDUCE 2" in C.device_functor_source(FOLD, True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("compress", [False, True])
+def test_fold_functor_hot_keys(compress):
+    from gpu_mapreduce_amd.parallel.comm import Comm
+    from gpu_mapreduce_amd.runtime.mapreduce import MapReduce
+    n = 3_000_000
+    mr = MapReduce(Comm(device="cuda"))
+    mr.map_device(n, HOT)
+    if compress:
+        mr.compress_device(FOLD)
+    else:
+        mr.collate()
+        mr.reduce_device(FOLD)
+    got = {struct.unpack("<q", k)[0]: struct.unpack("<4q", v) for k, v in pairs(mr)}
+    t = np.arange(n)
+    key = np.where(t % 3 == 0, 0, t % 1000)
+    val = t % 1009 - 500
+    want = {}
+    for k in np.unique(key):
+        v = val[key == k]
+        want[int(k)] = (int(v.sum()), len(v), int(v.min()), int(v.max()))
+    assert got == want

@@ -31,6 +31,13 @@ __device__ void mr_reduce(mrd::Bytes key, mrd::Values vals, mrd::Emit& out) {
   out.emit(key.as<long long>(), s);
 }
 """
+FOLD = """
+struct mr_acc { int s; };
+__device__ void mr_init(mrd::Bytes key, mr_acc& a) { a.s = 0; }
+__device__ void mr_add(mr_acc& a, mrd::Bytes v) { a.s += v.as<int>(); }
+__device__ void mr_merge(mr_acc& a, const mr_acc& b) { a.s += b.s; }
+__device__ void mr_finish(mrd::Bytes key, const mr_acc& a, mrd::Emit& out) { out.emit(key.as<long long>(), a.s); }
+"""
 comm = Comm(device="cuda")
 
 
@@ -48,16 +55,20 @@ for rep in range(4):
     _, tm = timed(lambda: mr.map_device(n, MAP))
     _, tc = timed(lambda: mr.collate())
     mr2 = mr.copy()
+    mr3 = mr.copy()
+    _, tf = timed(lambda: mr3.reduce_device(FOLD))
     _, tr = timed(lambda: mr.reduce_device(RED))
     _, tb = timed(lambda: mr2.reduce_builtin("sum:int32") if False else mr2._m.reduce_builtin("sum", "int32"))
     if rep == 0:  # compile + first-touch warm-up; check the two reduces agree
         a, b = {}, {}
         mr.scan_kv(lambda k, v: a.__setitem__(k, struct.unpack("<i", v)[0]))
         mr2.scan_kv(lambda k, v: b.__setitem__(k, struct.unpack("<i", v)[0]))
-        assert a == b and sum(a.values()) == n, "device reduce != builtin reduce"
-        print(f"n = 2^{ln} pairs, {len(a)} keys; device reduce == reduce_builtin('sum')", flush=True)
+        c = {}
+        mr3.scan_kv(lambda k, v: c.__setitem__(k, struct.unpack("<i", v)[0]))
+        assert a == b == c and sum(a.values()) == n, "device reduce / fold != builtin reduce"
+        print(f"n = 2^{ln} pairs, {len(a)} keys; device reduce == device fold == reduce_builtin('sum')", flush=True)
         continue
-    for k, v in (("map_device", tm), ("collate", tc), ("reduce_device", tr), ("reduce_builtin", tb)):
+    for k, v in (("map_device", tm), ("collate", tc), ("reduce_device", tr), ("reduce_device_fold", tf), ("reduce_builtin", tb)):
         best[k] = min(best.get(k, 1e30), v)
 for k, v in best.items():
     print(f"{k:16s} {v:8.2f} ms  {n / (v * 1e-3) / 1e9:7.2f} G pairs/s", flush=True)
