@@ -159,9 +159,13 @@ extern "C" __global__ void mrd_acc_size(mrd::i64* out) {
   if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = sizeof(mr_acc);
 }
 extern "C" __global__ void __launch_bounds__(256)
-mrd_fold_nchunks(const mrd::i64* seg, mrd::i64 nkey, mrd::i64 C, mrd::i64* cnt) {
-  for (mrd::i64 s = (mrd::i64)blockIdx.x * 256 + threadIdx.x; s < nkey; s += (mrd::i64)gridDim.x * 256)
+mrd_fold_nchunks(const mrd::i64* seg, mrd::i64 nkey, mrd::i64 C, mrd::i64* cnt, mrd::u64* maxc) {
+  mrd::u64 m = 0;
+  for (mrd::i64 s = (mrd::i64)blockIdx.x * 256 + threadIdx.x; s < nkey; s += (mrd::i64)gridDim.x * 256) {
     cnt[s] = (seg[s + 1] - seg[s] + C - 1) / C;
+    m = (mrd::u64)cnt[s] > m ? (mrd::u64)cnt[s] : m;
+  }
+  if (m) atomicMax(maxc, m);
 }
 extern "C" __global__ void __launch_bounds__(256)
 mrd_fold_chunks(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* vd, const mrd::i64* voff,
@@ -177,18 +181,20 @@ mrd_fold_chunks(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd:
     __builtin_memcpy(accs + c * sizeof(mr_acc), &a, sizeof(mr_acc));
   }
 }
+// one level of a fixed pairwise tree: chunk j of a key (j % 2*stride == 0)
+// takes in chunk j + stride; log2(most chunks of a key) levels leave each
+// key's total in its first chunk, in the same order on every run
 extern "C" __global__ void __launch_bounds__(256)
-mrd_fold_merge(const mrd::i64* cstart, mrd::i64 nkey, mrd::u8* accs) {
-  for (mrd::i64 s = (mrd::i64)blockIdx.x * 256 + threadIdx.x; s < nkey; s += (mrd::i64)gridDim.x * 256) {
-    const mrd::i64 c0 = cstart[s], c1 = cstart[s + 1];
-    if (c1 - c0 < 2) continue;
+mrd_fold_merge(const mrd::i64* cstart, mrd::i64 nkey, mrd::i64 nchunk, mrd::i64 stride, mrd::u8* accs) {
+  for (mrd::i64 c = (mrd::i64)blockIdx.x * 256 + threadIdx.x; c < nchunk; c += (mrd::i64)gridDim.x * 256) {
+    const mrd::i64 s = mrd::seg_of(cstart, nkey, c);
+    const mrd::i64 j = c - cstart[s];
+    if (j % (2 * stride) != 0 || c + stride >= cstart[s + 1]) continue;
     mr_acc a, b;
-    __builtin_memcpy(&a, accs + c0 * sizeof(mr_acc), sizeof(mr_acc));
-    for (mrd::i64 c = c0 + 1; c < c1; ++c) {
-      __builtin_memcpy(&b, accs + c * sizeof(mr_acc), sizeof(mr_acc));
-      mr_merge(a, b);
-    }
-    __builtin_memcpy(accs + c0 * sizeof(mr_acc), &a, sizeof(mr_acc));
+    __builtin_memcpy(&a, accs + c * sizeof(mr_acc), sizeof(mr_acc));
+    __builtin_memcpy(&b, accs + (c + stride) * sizeof(mr_acc), sizeof(mr_acc));
+    mr_merge(a, b);
+    __builtin_memcpy(accs + c * sizeof(mr_acc), &a, sizeof(mr_acc));
   }
 }
 #endif
@@ -429,17 +435,21 @@ KV reduce_groups(const KMV& m, const std::string& code, at::Device dev) {
     void* args[] = {&o};
     launch(mod.acc_size, 1, args, s);
   }
-  at::Tensor cnt = at::empty({it.n}, opt(dev, at::kLong));
+  at::Tensor cnt = at::empty({it.n + 1}, opt(dev, at::kLong));  // + the most chunks of one key
+  if (hipMemsetAsync(P0<int64_t>(cnt) + it.n, 0, 8, s) != hipSuccess)
+    throw std::runtime_error("mrhip: hipMemsetAsync failed");
   {
     const int64_t* seg = it.seg;
     int64_t nkey = it.n, c = C;
     int64_t* o = P0<int64_t>(cnt);
-    void* args[] = {&seg, &nkey, &c, &o};
+    int64_t* mx = o + it.n;
+    void* args[] = {&seg, &nkey, &c, &o, &mx};
     launch(mod.nchunks, it.n, args, s);
   }
-  at::Tensor cstart = exclusive_scan(cnt);
-  int64_t asz = 0, nchunk = 0;
-  read_small(s, {{P0<int64_t>(asz_t), &asz, 8}, {P0<int64_t>(cstart) + it.n, &nchunk, 8}});
+  at::Tensor cstart = exclusive_scan(cnt.narrow(0, 0, it.n));
+  int64_t asz = 0, nchunk = 0, maxc = 0;
+  read_small(s, {{P0<int64_t>(asz_t), &asz, 8}, {P0<int64_t>(cstart) + it.n, &nchunk, 8},
+                 {P0<int64_t>(cnt) + it.n, &maxc, 8}});
   at::Tensor accs = at::empty({std::max<int64_t>(1, nchunk * asz)}, opt(dev, at::kByte));
   {
     const uint8_t* kd = it.kd;
@@ -452,8 +462,11 @@ KV reduce_groups(const KMV& m, const std::string& code, at::Device dev) {
     uint8_t* a = P0<uint8_t>(accs);
     void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &nkey, &cs, &nc, &c, &a};
     launch(mod.chunks, nchunk, args, s);
-    void* margs[] = {&cs, &nkey, &a};
-    launch(mod.merge, it.n, margs, s);
+    for (int64_t stride = 1; stride < maxc; stride *= 2) {
+      int64_t st = stride;
+      void* margs[] = {&cs, &nkey, &nc, &st, &a};
+      launch(mod.merge, nchunk, margs, s);
+    }
   }
   Items f = it;
   f.vd = P0<uint8_t>(accs);

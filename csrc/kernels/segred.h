@@ -96,6 +96,33 @@ __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __
   for (int j = 0; j < SR_IT; ++j) lval[j * SR_NT + t] = v[j];
   __syncthreads();
   const int64_t sb = sb_sh, ns = ns_sh;
+  if (ns == 1) {
+    // the whole tile lies in one segment (a hot key's values): a block
+    // reduction of the registers in a fixed order, no partial lists — the
+    // general path below folds 2 x 256 partials serially in one thread
+    __shared__ T wred[SR_NT / 64];
+    T acc = v[0];
+#pragma unroll
+    for (int j = 1; j < SR_IT; ++j) acc = R::f(acc, v[j]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) acc = R::f(acc, __shfl_xor(acc, d, 64));
+    if ((t & 63) == 0) wred[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) {
+      T a = wred[0];
+#pragma unroll
+      for (int w = 1; w < SR_NT / 64; ++w) a = R::f(a, wred[w]);
+      const int64_t s0 = seg[sb], s1 = seg[sb + 1];
+      if (s0 >= b0 && s1 <= b1) {
+        out[sb] = a;
+      } else {
+        const int slot = s0 < b0 ? 0 : 1;
+        carry_seg[2 * blockIdx.x + slot] = sb;
+        carry_val[2 * blockIdx.x + slot] = a;
+      }
+    }
+    return;
+  }
   for (int64_t j = t; j <= ns; j += SR_NT) lseg[j] = seg[sb + j];
   ls[2 * t] = -1;
   ls[2 * t + 1] = -1;
