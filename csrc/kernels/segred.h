@@ -286,30 +286,38 @@ inline void segred_launch(G get, const int64_t* seg, int64_t nseg, int64_t nval,
   hipLaunchKernelGGL((k_segred_tiles<T, OP, G>), dim3((unsigned)nb), dim3(SR_NT), 0, s, get, seg, nseg, nval, out,
                      carry_seg, carry_val);
   MRH_CHECK_LAUNCH();
+  // carries folded in levels of k_carry_fold (64 entries per wave) until at
+  // most 64 are left for k_segred_carry's serial fold: one hot segment over
+  // thousands of tiles is never folded entry by entry in one thread
   int64_t nc = 2 * nb;
-  if (nc > 4096) {  // two-level fold; the level-2 carry sits behind the first (segred_carry_entries)
+  int64_t* cs = carry_seg;
+  T* cv = carry_val;
+  while (nc > 64) {
     const int64_t nw1 = (nc + 63) / 64;
-    int64_t* cs2 = carry_seg + nc;
-    T* cv2 = carry_val + nc;
+    int64_t* cs2 = cs + nc;  // the next level sits behind this one (segred_carry_entries)
+    T* cv2 = cv + nc;
     MRH_HIP(hipMemsetAsync(cs2, 0xff, sizeof(int64_t) * 2 * nw1, s));
-    hipLaunchKernelGGL((k_carry_fold<T, OP>), dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, carry_seg,
-                       carry_val, nc, out, cs2, cv2);
+    hipLaunchKernelGGL((k_carry_fold<T, OP>), dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, cs, cv, nc, out,
+                       cs2, cv2);
     MRH_CHECK_LAUNCH();
-    hipLaunchKernelGGL((k_segred_carry<T, OP>), dim3((unsigned)((2 * nw1 + SR_NT - 1) / SR_NT)), dim3(SR_NT), 0, s,
-                       cs2, cv2, 2 * nw1, out);
-    MRH_CHECK_LAUNCH();
-    return;
+    cs = cs2;
+    cv = cv2;
+    nc = 2 * nw1;
   }
-  hipLaunchKernelGGL((k_segred_carry<T, OP>), dim3((unsigned)((nc + SR_NT - 1) / SR_NT)), dim3(SR_NT), 0, s,
-                     carry_seg, carry_val, nc, out);
+  hipLaunchKernelGGL((k_segred_carry<T, OP>), dim3((unsigned)((nc + SR_NT - 1) / SR_NT)), dim3(SR_NT), 0, s, cs, cv,
+                     nc, out);
   MRH_CHECK_LAUNCH();
 }
 
-// carry entries a segred_launch needs per array: 2 per tile, plus the
-// level-2 carry of the two-level fold (2 per 64 first-level entries)
+// carry entries a segred_launch needs per array: 2 per tile, plus every
+// further level of the carry fold (2 per 64 entries of the level before)
 inline size_t segred_carry_entries(int64_t nval) {
-  const size_t nc = 2 * (size_t)((nval + SR_TILE - 1) / SR_TILE);
-  return nc + 2 * ((nc + 63) / 64) + 2;
+  size_t nc = 2 * (size_t)((nval + SR_TILE - 1) / SR_TILE), total = nc;
+  while (nc > 64) {
+    nc = 2 * ((nc + 63) / 64);
+    total += nc;
+  }
+  return total + 2;
 }
 
 }  // namespace dev
