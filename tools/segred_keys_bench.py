@@ -11,6 +11,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpu_mapreduce_amd import C  # noqa: E402
 
+if os.environ.get("POOL") == "1":  # the engine's HBM pool as the allocator (a Comm installs it)
+    from gpu_mapreduce_amd.parallel.comm import Comm
+    Comm(device="cuda")
+    from gpu_mapreduce_amd.runtime import hbm_pool
+    print("hbm pool installed:", hbm_pool.installed(), flush=True)
 n = 1 << 27
 for lk in (0, 5, 10, 15, 20):
     nk = 1 << lk
