@@ -75,6 +75,8 @@ __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __
   __shared__ T lval[SR_TILE];
   __shared__ int64_t ls[2 * SR_NT];
   __shared__ T lv[2 * SR_NT];
+  __shared__ int64_t eseg[2 * (2 * SR_NT / 64)];  // the 8 chunks' first / last runs
+  __shared__ T eval[2 * (2 * SR_NT / 64)];
   __shared__ int64_t sb_sh, ns_sh;
   const int t = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * SR_TILE;
@@ -126,6 +128,7 @@ __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __
   for (int64_t j = t; j <= ns; j += SR_NT) lseg[j] = seg[sb + j];
   ls[2 * t] = -1;
   ls[2 * t + 1] = -1;
+  if (t < 2 * (2 * SR_NT / 64)) eseg[t] = -1;
   __syncthreads();
 
   const int64_t t0 = b0 + (int64_t)t * SR_IT;
@@ -167,28 +170,79 @@ __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __
     }
   }
   __syncthreads();
-  // fold incomplete partials per segment, in thread order
-  for (int j = t; j < 2 * SR_NT; j += SR_NT) {
-    int64_t s = ls[j];
-    if (s < 0) continue;
-    int jp = j - 1;
-    while (jp >= 0 && ls[jp] < 0) --jp;
-    if (jp >= 0 && ls[jp] == s) continue;  // not the first entry of this segment
-    T acc = lv[j];
-    for (int k = j + 1; k < 2 * SR_NT; ++k) {
-      if (ls[k] < 0) continue;
-      if (ls[k] != s) break;
-      acc = R::f(acc, lv[k]);
-    }
-    bool inside = seg[s] >= b0 && seg[s + 1] <= b1;
-    if (inside) {
+  // fold the incomplete partials per segment: the 2 x 256 entries (thread
+  // order, segment ids non-decreasing, -1 = none) in 8 chunks of 64, two per
+  // wave, by a segmented wave scan; a run inside a chunk is the segment's
+  // whole block total; each chunk's first and last runs (which may continue
+  // in the neighbouring chunk) go to 16 edge slots that thread 0 folds in
+  // order. (A serial fold of up to 512 entries in one thread made a tile
+  // holding a segment boundary cost ~10x an interior one.)
+  auto finish = [&](int64_t s, T acc) {
+    const int64_t s0 = seg[s], s1 = seg[s + 1];
+    if (s0 >= b0 && s1 <= b1) {
       out[s] = acc;
-    } else {
-      // the block's first partial (segment started before b0) -> slot 0, else slot 1
-      int slot = seg[s] < b0 ? 0 : 1;
+    } else {  // the block's first partial (segment started before b0) -> slot 0, else slot 1
+      const int slot = s0 < b0 ? 0 : 1;
       carry_seg[2 * blockIdx.x + slot] = s;
       carry_val[2 * blockIdx.x + slot] = acc;
     }
+  };
+  const int lane = t & 63;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int j = t + pass * SR_NT, c = j >> 6;
+    int64_t sj = ls[j];
+    T v = sj >= 0 ? lv[j] : R::ident();
+    const uint64_t valid = __ballot(sj >= 0);
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // invalid entries join the run before them
+      const int64_t y = __shfl_up(sj, d, 64);
+      if (lane >= d && y > sj) sj = y;
+    }
+    const int64_t sp = __shfl_up(sj, 1, 64), sn = __shfl_down(sj, 1, 64);
+    const bool head = lane == 0 || sj != sp;
+    const uint64_t heads = __ballot(head);
+    T S = v;
+    int F = head;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const T ys = __shfl_up(S, d, 64);
+      const int yf = __shfl_up(F, d, 64);
+      if (lane >= d) {
+        if (!F) S = R::f(ys, S);
+        F |= yf;
+      }
+    }
+    const bool tail = lane == 63 || sj != sn;
+    if (tail && sj >= 0) {
+      const int fv = __ffsll((long long)valid) - 1;
+      const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+      const uint64_t after_fv = ~((2ull << fv) - 1ull);
+      const bool first = (heads & upto & after_fv) == 0ull;
+      if (first || lane == 63) {
+        eseg[2 * c + (first ? 0 : 1)] = sj;
+        eval[2 * c + (first ? 0 : 1)] = S;
+      } else {
+        finish(sj, S);
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int64_t cur = -1;
+    T acc = R::ident();
+    for (int e = 0; e < 2 * (2 * SR_NT / 64); ++e) {
+      const int64_t se = eseg[e];
+      if (se < 0) continue;
+      if (se != cur) {
+        if (cur >= 0) finish(cur, acc);
+        cur = se;
+        acc = eval[e];
+      } else {
+        acc = R::f(acc, eval[e]);
+      }
+    }
+    if (cur >= 0) finish(cur, acc);
   }
 }
 

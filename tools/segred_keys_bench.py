@@ -17,9 +17,9 @@ if os.environ.get("POOL") == "1":  # the engine's HBM pool as the allocator (a C
     from gpu_mapreduce_amd.runtime import hbm_pool
     print("hbm pool installed:", hbm_pool.installed(), flush=True)
 n = 1 << 27
-for lk in (0, 5, 10, 15, 20):
-    nk = 1 << lk
-    keys = (torch.arange(n, device="cuda", dtype=torch.int64) // (n // nk))
+for lk, unaligned in ((0, 0), (5, 0), (10, 0), (15, 0), (20, 0), (5, 1), (10, 1), (15, 1)):
+    nk = (1 << lk) - unaligned  # unaligned: segment ends fall inside the 4096-value tiles
+    keys = (torch.arange(n, device="cuda", dtype=torch.int64) * nk) // n
     vals = torch.ones(n, device="cuda", dtype=torch.int32)
     kv = C.make_kv(keys, None, vals, None, n, "cuda")
     kg, _ = C.convert(kv)
@@ -33,4 +33,4 @@ for lk in (0, 5, 10, 15, 20):
         best = min(best, a.elapsed_time(b))
     tot = int(torch.frombuffer(bytearray(r.vdata.cpu().numpy().tobytes()), dtype=torch.int32).sum())
     assert tot == n and r.n == nk
-    print(f"2^{lk:2d} keys: {best:7.3f} ms  {n * 4 / (best * 1e-3) / 1e9:7.1f} GB/s", flush=True)
+    print(f"{nk:8d} keys{' (unaligned)' if unaligned else ''}: {best:7.3f} ms  {n * 4 / (best * 1e-3) / 1e9:7.1f} GB/s", flush=True)
