@@ -66,13 +66,19 @@ __device__ __forceinline__ int64_t seg_upper(const int64_t* __restrict__ seg, in
 // LDS, then reduced BLOCKED (IT consecutive values per thread). The segment
 // boundaries overlapping the block are staged in LDS once (two global binary
 // searches per block instead of one per thread).
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+
 template <typename T, int OP, typename G>
 __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __restrict__ seg, int64_t nseg,
                                                         int64_t nval, T* __restrict__ out,
                                                         int64_t* __restrict__ carry_seg, T* __restrict__ carry_val) {
   using R = RedOp<T, OP>;
-  __shared__ int64_t lseg[SR_TILE + 2];
-  __shared__ T lval[SR_TILE];
+  // segment bounds relative to b0, clamped to [-1, TILE + 1] (int32: half
+  // the LDS of absolute offsets, so more blocks fit a CU); values padded one
+  // slot per 16 so the blocked reads (16 consecutive per thread) spread over
+  // the banks
+  __shared__ int32_t lseg[SR_TILE + 2];
+  __shared__ T lval[SR_TILE + SR_TILE / 16];
   __shared__ int64_t ls[2 * SR_NT];
   __shared__ T lv[2 * SR_NT];
   __shared__ int64_t eseg[2 * (2 * SR_NT / 64)];  // the 8 chunks' first / last runs
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __
     v[j] = e < b1 ? get(e) : R::ident();
   }
 #pragma unroll
-  for (int j = 0; j < SR_IT; ++j) lval[j * SR_NT + t] = v[j];
+  for (int j = 0; j < SR_IT; ++j) lval[lpad(j * SR_NT + t)] = v[j];
   __syncthreads();
   const int64_t sb = sb_sh, ns = ns_sh;
   if (ns == 1) {
@@ -125,14 +131,18 @@ __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __
     }
     return;
   }
-  for (int64_t j = t; j <= ns; j += SR_NT) lseg[j] = seg[sb + j];
+  for (int64_t j = t; j <= ns; j += SR_NT) {
+    const int64_t r = seg[sb + j] - b0;
+    lseg[j] = (int32_t)(r < 0 ? -1 : r > SR_TILE ? SR_TILE + 1 : r);
+  }
   ls[2 * t] = -1;
   ls[2 * t + 1] = -1;
   if (t < 2 * (2 * SR_NT / 64)) eseg[t] = -1;
   __syncthreads();
 
-  const int64_t t0 = b0 + (int64_t)t * SR_IT;
-  const int64_t t1 = min(t0 + (int64_t)SR_IT, b1);
+  // thread range [t0, t1) relative to b0
+  const int32_t t0 = t * SR_IT;
+  const int32_t t1 = (int32_t)min((int64_t)t0 + SR_IT, b1 - b0);
   if (t0 < t1) {
     // local segment of t0: largest q in [0, ns) with lseg[q] <= t0
     int64_t lo = 0, hi = ns - 1;
@@ -142,10 +152,10 @@ __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __
       else hi = mid - 1;
     }
     int64_t q = lo;
-    int64_t s_end = lseg[q + 1];
+    int32_t s_end = lseg[q + 1];
     T acc = R::ident();
     bool first_run = true;
-    for (int64_t i = t0; i < t1; ++i) {
+    for (int32_t i = t0; i < t1; ++i) {
       while (i >= s_end) {  // close run of segment sb+q
         if (lseg[q] >= t0) out[sb + q] = acc;  // started inside the thread: complete
         else { ls[2 * t] = sb + q; lv[2 * t] = acc; }
@@ -154,7 +164,7 @@ __global__ __launch_bounds__(SR_NT) void k_segred_tiles(G get, const int64_t* __
         s_end = lseg[q + 1];
         acc = R::ident();
       }
-      acc = R::f(acc, lval[i - b0]);
+      acc = R::f(acc, lval[lpad(i)]);
     }
     // last run of the thread ends at t1
     const bool starts_inside = lseg[q] >= t0;
