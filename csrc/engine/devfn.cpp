@@ -59,6 +59,18 @@ struct Values {
   template <class T>
   __device__ T get(i64 i, i64 byte = 0) const { return (*this)[i].template as<T>(byte); }
 };
+// n bytes to dst: the common widths as single wide copies
+__device__ inline void put(u8* dst, const u8* src, i64 n) {
+  switch (n) {
+    case 0: return;
+    case 4: __builtin_memcpy(dst, src, 4); return;
+    case 8: __builtin_memcpy(dst, src, 8); return;
+    case 12: __builtin_memcpy(dst, src, 12); return;
+    case 16: __builtin_memcpy(dst, src, 16); return;
+    case 24: __builtin_memcpy(dst, src, 24); return;
+    default: for (i64 i = 0; i < n; ++i) dst[i] = src[i];
+  }
+}
 // the emitter: counts in the first pass, writes in the second
 struct Emit {
   bool write;
@@ -72,10 +84,8 @@ struct Emit {
     if (write) {
       if (okoff) okoff[nrec] = kb;
       if (ovoff) ovoff[nrec] = vb;
-      const u8* ks = (const u8*)k;
-      const u8* vs = (const u8*)v;
-      for (i64 i = 0; i < kn; ++i) okd[kb + i] = ks[i];
-      for (i64 i = 0; i < vn; ++i) ovd[vb + i] = vs[i];
+      put(okd + kb, (const u8*)k, kn);
+      put(ovd + vb, (const u8*)v, vn);
     } else {
       kmin = (u64)kn < kmin ? (u64)kn : kmin;
       kmax = (u64)kn > kmax ? (u64)kn : kmax;
@@ -129,7 +139,7 @@ __device__ inline void run_item(const u8* kd, const i64* koff, i64 kw, const u8*
 #endif
 }
 }  // namespace mrd
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ __launch_bounds__(256) void
 mrd_count(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* vd, const mrd::i64* voff,
           mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, mrd::i64* cnt, mrd::u64* wid) {
   mrd::u64 kmin = ~0ull, kmax = 0, vmin = ~0ull, vmax = 0;
@@ -158,7 +168,7 @@ mrd_count(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* v
 extern "C" __global__ void mrd_acc_size(mrd::i64* out) {
   if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = sizeof(mr_acc);
 }
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ __launch_bounds__(256) void
 mrd_fold_nchunks(const mrd::i64* seg, mrd::i64 nkey, mrd::i64 C, mrd::i64* cnt, mrd::u64* maxc) {
   mrd::u64 m = 0;
   for (mrd::i64 s = (mrd::i64)blockIdx.x * 256 + threadIdx.x; s < nkey; s += (mrd::i64)gridDim.x * 256) {
@@ -167,7 +177,7 @@ mrd_fold_nchunks(const mrd::i64* seg, mrd::i64 nkey, mrd::i64 C, mrd::i64* cnt, 
   }
   if (m) atomicMax(maxc, m);
 }
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ __launch_bounds__(256) void
 mrd_fold_chunks(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* vd, const mrd::i64* voff,
                 mrd::i64 vw, const mrd::i64* seg, mrd::i64 nkey, const mrd::i64* cstart, mrd::i64 nchunk,
                 mrd::i64 C, mrd::u8* accs) {
@@ -184,7 +194,7 @@ mrd_fold_chunks(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd:
 // one level of a fixed pairwise tree: chunk j of a key (j % 2*stride == 0)
 // takes in chunk j + stride; log2(most chunks of a key) levels leave each
 // key's total in its first chunk, in the same order on every run
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ __launch_bounds__(256) void
 mrd_fold_merge(const mrd::i64* cstart, mrd::i64 nkey, mrd::i64 nchunk, mrd::i64 stride, mrd::u8* accs) {
   for (mrd::i64 c = (mrd::i64)blockIdx.x * 256 + threadIdx.x; c < nchunk; c += (mrd::i64)gridDim.x * 256) {
     const mrd::i64 s = mrd::seg_of(cstart, nkey, c);
@@ -200,7 +210,7 @@ mrd_fold_merge(const mrd::i64* cstart, mrd::i64 nkey, mrd::i64 nchunk, mrd::i64 
 #endif
 // okw / ovw >= 0: every record's key / value has that width (the count pass
 // said so): byte positions follow from the record position, no offsets
-extern "C" __global__ void __launch_bounds__(256)
+extern "C" __global__ __launch_bounds__(256) void
 mrd_write(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* vd, const mrd::i64* voff,
           mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, const mrd::i64* pos, mrd::i64 okw,
           mrd::i64 ovw, mrd::u8* okd, mrd::i64* okoff, mrd::u8* ovd, mrd::i64* ovoff) {
