@@ -154,11 +154,38 @@ mrd_count(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* v
     vmin = e.vmin < vmin ? e.vmin : vmin;
     vmax = e.vmax > vmax ? e.vmax : vmax;
   }
-  if (kmax || kmin != ~0ull) {
-    atomicMin(wid + 0, kmin);
-    atomicMax(wid + 1, kmax);
-    atomicMin(wid + 2, vmin);
-    atomicMax(wid + 3, vmax);
+  // the record widths: wave, then block min / max, one set of atomics per block
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const mrd::u64 a = __shfl_xor(kmin, d, 64), b = __shfl_xor(kmax, d, 64);
+    const mrd::u64 c = __shfl_xor(vmin, d, 64), e = __shfl_xor(vmax, d, 64);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+    vmin = c < vmin ? c : vmin;
+    vmax = e > vmax ? e : vmax;
+  }
+  __shared__ mrd::u64 red[4][4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w][0] = kmin;
+    red[w][1] = kmax;
+    red[w][2] = vmin;
+    red[w][3] = vmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i) {
+      kmin = red[i][0] < kmin ? red[i][0] : kmin;
+      kmax = red[i][1] > kmax ? red[i][1] : kmax;
+      vmin = red[i][2] < vmin ? red[i][2] : vmin;
+      vmax = red[i][3] > vmax ? red[i][3] : vmax;
+    }
+    if (kmax || kmin != ~0ull) {
+      atomicMin(wid + 0, kmin);
+      atomicMax(wid + 1, kmax);
+      atomicMin(wid + 2, vmin);
+      atomicMax(wid + 3, vmax);
+    }
   }
 }
 #if MRD_REDUCE == 2

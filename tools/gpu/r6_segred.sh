@@ -2,7 +2,7 @@
 # its GPU tests, and the device-functor timings
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-o=gpurun_out/r6s7; mkdir -p $o
+o=gpurun_out/r6s8; mkdir -p $o
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_kernels_gpu.py tests/test_oracles.py tests/test_wavesegred_gpu.py tests/test_pagerank.py tests/test_device_functors.py > $o/tests.log 2>&1
 rc=$?; echo "tests rc=$rc" >> $o/tests.log
 [ $rc -eq 0 ] || exit 1
