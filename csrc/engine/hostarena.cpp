@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdio>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -77,8 +78,11 @@ double reserve(int64_t bytes) {
   const auto t0 = std::chrono::steady_clock::now();
   void* p = nullptr;
   if (hipHostMalloc(&p, (size_t)n, hipHostMallocDefault) != hipSuccess || !p) {
+    // no arena: every pinned allocation keeps using the caching host allocator
     (void)hipGetLastError();
-    throw std::runtime_error("mrhip: hipHostMalloc of the pinned host arena failed");
+    std::fprintf(stderr, "mrhip: pinned host arena of %lld bytes not available; continuing without it\n",
+                 (long long)n);
+    return -1.0;
   }
   a.base = static_cast<uint8_t*>(p);
   a.size = n;

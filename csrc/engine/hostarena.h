@@ -16,7 +16,8 @@
 namespace mrh {
 namespace hostarena {
 // pin `bytes` (rounded up to 2 MiB) now, if no arena exists yet; returns the
-// milliseconds it took (0 when one exists or bytes <= 0)
+// milliseconds it took (0 when one exists or bytes <= 0; -1 when the memory
+// could not be pinned: the process goes on without an arena)
 double reserve(int64_t bytes);
 struct Stats {
   int64_t reserved = 0, in_use = 0, peak = 0, hits = 0, misses = 0;

@@ -20,7 +20,9 @@ def reserve_mb():
 
 
 def prepin(mb=None):
-    """pin the arena now (once per process); returns the milliseconds it took"""
+    """pin the arena now (once per process); returns the milliseconds it took
+    (0: it exists already or none was asked for; -1: the host could not pin
+    that much, the job goes on with the caching host allocator)"""
     import torch
     from ._ext import C
     mb = reserve_mb() if mb is None else int(mb)
