@@ -168,3 +168,31 @@ def test_fold_functor_hot_keys(compress):
         v = val[key == k]
         want[int(k)] = (int(v.sum()), len(v), int(v.min()), int(v.max()))
     assert got == want
+
+
+def test_compress_batch_is_a_local_combiner():
+    """compress_batch: this rank's groups as one KMV, no shuffle (the engine op
+    under sssp_mr's combiners); on the CPU engine too"""
+    import torch
+    from gpu_mapreduce_amd.parallel.comm import Comm
+    from gpu_mapreduce_amd.runtime.mapreduce import MapReduce
+    mr = MapReduce(Comm(device="cpu"))
+
+    def m(itask, kv):
+        for i in range(1000):
+            kv.add(struct.pack("<q", i % 37), struct.pack("<i", i))
+    mr.map(1, m)
+    seen = {}
+
+    def f(kmv, kv):
+        keys = kmv.keys.kdata.view(torch.int64)
+        seg = kmv.seg
+        vals = kmv.vdata.view(torch.int32)
+        sums = torch.stack([vals[seg[i]:seg[i + 1]].sum() for i in range(kmv.nkey)]).to(torch.int64)
+        seen["nkey"] = kmv.nkey
+        kv.add_tensors(keys, sums)
+    assert mr.compress_batch(f) == 37
+    assert seen["nkey"] == 37
+    got = {}
+    mr.scan_kv(lambda k, v: got.__setitem__(struct.unpack("<q", k)[0], struct.unpack("<q", v)[0]))
+    assert got == {k: sum(i for i in range(1000) if i % 37 == k) for k in range(37)}
