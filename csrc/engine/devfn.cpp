@@ -80,7 +80,9 @@ struct Emit {
   i64* okoff;
   u8* ovd;
   i64* ovoff;
+  i64 rlim, klim, vlim;  // write pass: the room the count pass measured (an impure functor cannot overrun it)
   __device__ void emit(const void* k, i64 kn, const void* v, i64 vn) {
+    if (write && (nrec >= rlim || kb + kn > klim || vb + vn > vlim)) return;
     if (write) {
       if (okoff) okoff[nrec] = kb;
       if (ovoff) ovoff[nrec] = vb;
@@ -144,7 +146,7 @@ mrd_count(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* v
           mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, mrd::i64* cnt, mrd::u64* wid) {
   mrd::u64 kmin = ~0ull, kmax = 0, vmin = ~0ull, vmax = 0;
   for (mrd::i64 i = (mrd::i64)blockIdx.x * 256 + threadIdx.x; i < n; i += (mrd::i64)gridDim.x * 256) {
-    mrd::Emit e{false, 0, 0, 0, ~0ull, 0, ~0ull, 0, nullptr, nullptr, nullptr, nullptr};
+    mrd::Emit e{false, 0, 0, 0, ~0ull, 0, ~0ull, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
     mrd::run_item(kd, koff, kw, vd, voff, vw, seg, first, i, e);
     cnt[i] = e.nrec;
     cnt[n + i] = e.kb;
@@ -245,11 +247,14 @@ mrd_write(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* v
   for (mrd::i64 i = (mrd::i64)blockIdx.x * 256 + threadIdx.x; i < n; i += (mrd::i64)gridDim.x * 256) {
     const mrd::i64 r = pos[i];
     if (pos[i + 1] == r) continue;
+    const mrd::i64 r1 = pos[i + 1];
     const mrd::i64 k0 = okw >= 0 ? r * okw : pos[np + i], v0 = ovw >= 0 ? r * ovw : pos[2 * np + i];
+    const mrd::i64 k1 = okw >= 0 ? r1 * okw : pos[np + i + 1], v1 = ovw >= 0 ? r1 * ovw : pos[2 * np + i + 1];
     mrd::Emit e{true, 0, 0, 0, 0, 0, 0, 0, okd + k0, okw >= 0 ? nullptr : okoff + r, ovd + v0,
-                ovw >= 0 ? nullptr : ovoff + r};
+                ovw >= 0 ? nullptr : ovoff + r, r1 - r, k1 - k0, v1 - v0};
     mrd::run_item(kd, koff, kw, vd, voff, vw, seg, first, i, e);
-    for (mrd::i64 j = 0; j < e.nrec; ++j) {  // offsets relative to the item -> absolute
+    const mrd::i64 nw = e.nrec < r1 - r ? e.nrec : r1 - r;
+    for (mrd::i64 j = 0; j < nw; ++j) {  // offsets relative to the item -> absolute
       if (okw < 0) okoff[r + j] += k0;
       if (ovw < 0) ovoff[r + j] += v0;
     }
