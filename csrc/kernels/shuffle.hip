@@ -23,6 +23,8 @@
 //
 // Stable means the send buffer (and so the receiver's pairs from each sender)
 // keeps input order: the shuffle is deterministic.
+#include <string>
+
 #include "common.h"
 #include "launch.h"
 
@@ -206,6 +208,69 @@ __global__ __launch_bounds__(NT) void k_copy_var_i64(const uint8_t* __restrict__
   }
 }
 
+// The same gather by block tiles of 256 rows: the tile's destination
+// offsets and source starts are staged in LDS once; every lane owns 16
+// consecutive destination bytes per step (4 KiB per block step), finds the
+// row of its first byte by a binary search in LDS and walks on across row
+// boundaries (empty rows included), gathers its bytes and writes them with one
+// 16-byte store (byte stores only at a tile's ragged ends). No cross-lane
+// shuffles per byte: the wave version spends 8 per byte. dst 16-aligned.
+constexpr int CV_ROWS = NT;
+__global__ __launch_bounds__(NT) void k_copy_var_blk(const uint8_t* __restrict__ src, const int64_t* __restrict__ soff,
+                                                    const int64_t* __restrict__ perm, int64_t n,
+                                                    uint8_t* __restrict__ dst, const int64_t* __restrict__ doff) {
+  __shared__ int64_t ldo[CV_ROWS + 1];
+  __shared__ int64_t lso[CV_ROWS];
+  const int t = threadIdx.x;
+  const int64_t ntile = (n + CV_ROWS - 1) / CV_ROWS;
+  for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {  // uniform over the block
+    const int64_t r0 = tile * CV_ROWS;
+    const int rows = (int)min<int64_t>(CV_ROWS, n - r0);
+    if (t < rows) {
+      ldo[t] = doff[r0 + t];
+      lso[t] = soff[perm[r0 + t]];
+    }
+    if (t == 0) ldo[rows] = doff[r0 + rows];
+    __syncthreads();
+    const int64_t d_lo = ldo[0], d_hi = ldo[rows];
+    for (int64_t base = (d_lo & ~int64_t(15)) + 16 * (int64_t)t; base < d_hi; base += 16 * NT) {
+      const int64_t q = base < d_lo ? d_lo : base;
+      int lo = 0, hi = rows - 1;  // the last row starting at or before q (an empty row loses the tie)
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (ldo[mid] <= q) lo = mid;
+        else hi = mid - 1;
+      }
+      int r = lo;
+      int64_t rbeg = ldo[r], rend = ldo[r + 1], sbeg = lso[r];
+      uint32_t wv[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int64_t pos = base + k;
+        if (pos >= d_lo && pos < d_hi) {
+          while (pos >= rend) {
+            ++r;
+            rbeg = rend;
+            rend = ldo[r + 1];
+            sbeg = lso[r];
+          }
+          wv[k >> 2] |= (uint32_t)src[sbeg + (pos - rbeg)] << (8 * (k & 3));
+        }
+      }
+      if (base >= d_lo && base + 16 <= d_hi) {
+        *reinterpret_cast<uint4*>(dst + base) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int64_t pos = base + k;
+          if (pos >= d_lo && pos < d_hi) dst[pos] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+        }
+      }
+    }
+    __syncthreads();  // the next tile overwrites the staged offsets
+  }
+}
+
 // header row of this rank for the exchange: per owner d {pairs, key bytes,
 // value bytes} from the scanned per-(d, block) tables (fixed columns: count x
 // width), then the two width codes
@@ -294,6 +359,16 @@ void part_scatter(const int32_t* dest, int64_t n, int P, int nb, const int64_t* 
 void copy_var_i64(const uint8_t* src, const int64_t* soff, const int64_t* perm, int64_t n, uint8_t* dst,
                   const int64_t* doff, hipStream_t s) {
   if (n <= 0) return;
+  static const bool wave = [] {  // MRH_COPY_VAR=wave: the wave-per-64-rows version (A/B)
+    const char* e = std::getenv("MRH_COPY_VAR");
+    return e && std::string(e) == "wave";
+  }();
+  if (!wave && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int64_t g = std::min<int64_t>((n + CV_ROWS - 1) / CV_ROWS, 65536);
+    hipLaunchKernelGGL(k_copy_var_blk, dim3((unsigned)g), dim3(NT), 0, s, src, soff, perm, n, dst, doff);
+    MRH_CHECK_LAUNCH();
+    return;
+  }
   int64_t g = ((n + 63) / 64 * 64 + NT - 1) / NT;  // a wave per 64-row tile
   if (g > 65536) g = 65536;
   hipLaunchKernelGGL(k_copy_var_i64, dim3((unsigned)g), dim3(NT), 0, s, src, soff, perm, n, dst, doff);
