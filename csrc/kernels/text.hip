@@ -205,28 +205,56 @@ __global__ __launch_bounds__(NT) void k_tok_count2(const uint8_t* __restrict__ t
   }
 }
 
+// The block stages its output in LDS — key bytes at their offset from the
+// 16-byte-aligned base below the block's first byte, word offsets in word
+// order — then writes both with coalesced stores: 16-byte stores for the
+// aligned interior of the key bytes (byte stores only at the block's two
+// ragged ends, never past its own range), one int64 store per offset. (Each
+// thread writing its own bytes and offsets straight to memory left every
+// store instruction touching ~16 scattered cache lines.)
 __global__ __launch_bounds__(NT) void k_tok_emit2(const uint8_t* __restrict__ text, int64_t n,
                                                  const uint32_t* __restrict__ toff_w,
                                                  const int64_t* __restrict__ toff_b,
                                                  int64_t* __restrict__ koff, uint8_t* __restrict__ kd) {
   __shared__ uint32_t shw[NT / MRH_WAVE + 1];
   __shared__ uint32_t shb[NT / MRH_WAVE + 1];
+  __shared__ __attribute__((aligned(16))) uint8_t sbytes[2 * TILE + 16];  // <= 2 bytes per text byte (a NUL per word)
+  __shared__ int64_t soffs[TILE / 2 + 1];                                // <= 1 word per 2 text bytes
   const int64_t p = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * 16;
   uint32_t S = 0, E = 0, B = 0;
   if (p < n) word_masks(text, p, n, &S, &E, &B);
   uint32_t tw, tb;
   const uint32_t pw = dev::block_excl_scan<uint32_t, NT>((uint32_t)__popc(S), shw, &tw);
   const uint32_t pb = dev::block_excl_scan<uint32_t, NT>((uint32_t)(__popc(B) + __popc(E)), shb, &tb);
-  if (!(S | B)) return;
-  int64_t w = (int64_t)toff_w[blockIdx.x] + pw;
-  int64_t o = toff_b[blockIdx.x] + pb;
-  const uint4 a = *reinterpret_cast<const uint4*>(text + p);
-  const uint32_t wd[4] = {a.x, a.y, a.z, a.w};
+  const int64_t wb = (int64_t)toff_w[blockIdx.x];
+  const int64_t ob = toff_b[blockIdx.x];
+  const int lead = (int)((reinterpret_cast<uintptr_t>(kd) + (uintptr_t)ob) & 15);  // LDS index of byte ob: 16-aligned addresses stay 16-aligned
+  if (S | B) {
+    uint32_t w = pw, o = pb;
+    const uint4 a = *reinterpret_cast<const uint4*>(text + p);
+    const uint32_t wd[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    if ((S >> k) & 1u) koff[w++] = o;
-    if ((B >> k) & 1u) kd[o++] = (uint8_t)((wd[k >> 2] >> (8 * (k & 3))) & 0xffu);
-    if ((E >> k) & 1u) kd[o++] = 0;
+    for (int k = 0; k < 16; ++k) {
+      if ((S >> k) & 1u) soffs[w++] = ob + o;
+      if ((B >> k) & 1u) sbytes[lead + o++] = (uint8_t)((wd[k >> 2] >> (8 * (k & 3))) & 0xffu);
+      if ((E >> k) & 1u) sbytes[lead + o++] = 0;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < tw; i += NT) koff[wb + i] = soffs[i];
+  // key bytes [ob, ob + tb) in 16-byte chunks of the aligned base ob - lead
+  const int64_t base = ob - lead, end = ob + tb;
+  const int64_t nchunk = (end - base + 15) >> 4;
+  for (int64_t c = threadIdx.x; c < nchunk; c += NT) {
+    const int64_t g0 = base + 16 * c;
+    if (g0 >= ob && g0 + 16 <= end) {
+      *reinterpret_cast<uint4*>(kd + g0) = *reinterpret_cast<const uint4*>(sbytes + 16 * c);
+    } else {
+      for (int k = 0; k < 16; ++k) {
+        const int64_t g = g0 + k;
+        if (g >= ob && g < end) kd[g] = sbytes[16 * c + k];
+      }
+    }
   }
 }
 
