@@ -83,16 +83,31 @@ __global__ __launch_bounds__(NT) void k_part_count(const int32_t* __restrict__ d
     const int64_t i = base + r * NT + threadIdx.x;
     const bool valid = i < n;
     int d = -1;
+    unsigned long long kl = 0, vl = 0;
     if (valid) {
       d = owner<MODE>(i, dest_in, kd, kw, koff, P);
       if (MODE != 0) dest_out[i] = d;
+      if (kbytes) kl = (unsigned long long)(koff[i + 1] - koff[i]);
+      if (vbytes) vl = (unsigned long long)(voff[i + 1] - voff[i]);
     }
-    const uint64_t peers = match_owner(d);
-    if (!valid) continue;
-    const bool leader = (__ffsll((unsigned long long)peers) - 1) == lane;
-    if (leader) atomicAdd(&hc[d], (uint32_t)__popcll(peers));
-    if (kbytes) atomicAdd(&hk[d], (unsigned long long)(koff[i + 1] - koff[i]));
-    if (vbytes) atomicAdd(&hv[d], (unsigned long long)(voff[i + 1] - voff[i]));
+    // per distinct owner in the wave: its pair count and byte sums by wave
+    // reductions, one LDS atomic each by the group's leader (a per-lane
+    // atomic on the same owner serialised 64-fold at small P)
+    uint64_t active = __ballot(d >= 0);
+    while (active) {
+      const int leader = __ffsll((unsigned long long)active) - 1;
+      const int ld = __shfl(d, leader, MRH_WAVE);
+      const bool in = d == ld;
+      const uint64_t m = __ballot(in);
+      const unsigned long long ks = kbytes ? dev::wave_sum(in ? kl : 0ull) : 0ull;
+      const unsigned long long vs = vbytes ? dev::wave_sum(in ? vl : 0ull) : 0ull;
+      if (lane == leader) {
+        atomicAdd(&hc[ld], (uint32_t)__popcll(m));
+        if (kbytes) atomicAdd(&hk[ld], ks);
+        if (vbytes) atomicAdd(&hv[ld], vs);
+      }
+      active &= ~m;
+    }
   }
   __syncthreads();
   for (int d = threadIdx.x; d < P; d += NT) {
