@@ -1,7 +1,7 @@
 # kernel time of wordfreq's P > 1 route (one-rank RCCL communicator, 8 GiB, 2 jobs)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-o=gpurun_out/r6w; mkdir -p $o
+o=gpurun_out/r6w2; mkdir -p $o
 cd /tmp && MRH_FORCE_RCCL=2 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/pf -o t -- python3 $GRAFT_REPO_ROOT/tools/wf_shuffle_time.py 8 2 0 > $GRAFT_REPO_ROOT/$o/run.log 2>&1 || exit $?
 cp /tmp/pf/t_kernel_stats.csv $GRAFT_REPO_ROOT/$o/kernel_stats.csv
 python3 - <<'PY' > $GRAFT_REPO_ROOT/$o/last_job.txt
