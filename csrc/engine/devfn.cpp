@@ -137,7 +137,7 @@ __device__ inline void run_item(const u8* kd, const i64* koff, i64 kw, const u8*
   else vals.d = vd + seg[i] * vw;
   mr_reduce(field(kd, koff, kw, i), vals, e);
 #else
-  mr_map(field(kd, koff, kw, i), field(vd, voff, vw, i), first + i, e);
+  mr_map(field(kd, koff, kw, first + i), field(vd, voff, vw, first + i), first + i, e);
 #endif
 }
 }  // namespace mrd
@@ -430,16 +430,18 @@ int64_t compile_check(const std::string& code, bool reduce) {
   return (int64_t)compile(full_source(code, reduce), kind_name(kind_of(code, reduce))).size();
 }
 
-KV map_pairs(const KV& kv_in, const std::string& code, at::Device dev) {
+KV map_pairs(const KV& kv_in, const std::string& code, at::Device dev, int64_t a, int64_t b) {
   KV kv = kv_in.device() == dev ? kv_in : kv_to(kv_in, dev);
+  if (b < 0 || b > kv.n) b = kv.n;
   Items it;
+  it.first = a;
   it.kd = P0<uint8_t>(kv.kdata);
   it.koff = kv.kfixed() ? nullptr : P0<int64_t>(kv.koff);
   it.kw = kv.kfixed() ? kv.kw : 0;
   it.vd = P0<uint8_t>(kv.vdata);
   it.voff = kv.vfixed() ? nullptr : P0<int64_t>(kv.voff);
   it.vw = kv.vfixed() ? kv.vw : 0;
-  it.n = kv.n;
+  it.n = std::max<int64_t>(0, b - a);
   return run(it, code, 0, dev);
 }
 

@@ -20,8 +20,9 @@
 
 namespace mrh {
 namespace devfn {
-// map: every pair of kv (on the GPU) through mr_map; index = the pair's index
-KV map_pairs(const KV& kv, const std::string& code, at::Device dev);
+// map: pairs [a, b) of kv (b < 0: to the end; on the GPU) through mr_map;
+// index = the pair's index in kv
+KV map_pairs(const KV& kv, const std::string& code, at::Device dev, int64_t a = 0, int64_t b = -1);
 // map over n tasks (no input): mr_map(empty, empty, task, out)
 KV map_tasks(int64_t first, int64_t n, const std::string& code, at::Device dev);
 // reduce: every key of m through mr_reduce

@@ -1370,14 +1370,28 @@ uint64_t MapReduce::compress_batch(const ReduceBatchFn& fn) {
 
 // ====================================================================== device functors
 
+namespace {
+// items per functor launch: all of them, unless the builder is bounded (out
+// of core): then about a spool piece's worth (the count / scan scratch and the
+// output take ~128 bytes per item), so the launch fits the HBM budget
+int64_t functor_chunk(const KeyValue& out, int64_t n) {
+  const int64_t pb = out.piece_bytes();
+  return pb > 0 ? std::max<int64_t>(4096, pb / 128) : std::max<int64_t>(n, 1);
+}
+}  // namespace
+
 uint64_t MapReduce::map_device(MapReduce& src, const std::string& code, int addflag) {
   const at::Device dev = device();
   return map_mr_batch(
       src,
       [&](const KV& kv, KeyValue& out) {
         if (!kv.n) return;
-        KV o = devfn::map_pairs(kv, code, dev);
-        if (o.n) out.add_kv(o);
+        const KV d = kv.device() == dev ? kv : kv_to(kv, dev);
+        const int64_t step = functor_chunk(out, d.n);
+        for (int64_t a = 0; a < d.n; a += step) {
+          KV o = devfn::map_pairs(d, code, dev, a, std::min(d.n, a + step));
+          if (o.n) out.add_kv(o);
+        }
       },
       addflag);
 }
@@ -1391,8 +1405,11 @@ uint64_t MapReduce::map_device_tasks(int64_t ntask, const std::string& code, int
       (int)P,
       [&](int t, KeyValue& out) {
         const int64_t a = (int64_t)t * ntask / P, b = (int64_t)(t + 1) * ntask / P;
-        KV o = devfn::map_tasks(a, b - a, code, dev);
-        if (o.n) out.add_kv(o);
+        const int64_t step = functor_chunk(out, b - a);
+        for (int64_t x = a; x < b; x += step) {
+          KV o = devfn::map_tasks(x, std::min(b, x + step) - x, code, dev);
+          if (o.n) out.add_kv(o);
+        }
       },
       addflag);
 }

@@ -196,3 +196,34 @@ def test_compress_batch_is_a_local_combiner():
     got = {}
     mr.scan_kv(lambda k, v: got.__setitem__(struct.unpack("<q", k)[0], struct.unpack("<q", v)[0]))
     assert got == {k: sum(i for i in range(1000) if i % 37 == k) for k in range(37)}
+
+
+@pytest.mark.gpu
+def test_functors_out_of_core(tmp_path):
+    """under an HBM budget ~1/20 of the data the map's output spools and the
+    collate / compress groups reach the functors in budget-sized pieces; the
+    fold totals must still equal the oracle's"""
+    from gpu_mapreduce_amd.parallel.comm import Comm
+    from gpu_mapreduce_amd.runtime.mapreduce import MapReduce
+    n = 4_000_000
+    data = n * 12
+    for op in ("reduce", "compress"):
+        mr = MapReduce(Comm(device="cuda"))
+        mr.hbm_budget = data // 20
+        mr.host_budget = data // 4
+        mr.memsize = -65536
+        mr.fpath = str(tmp_path)
+        mr.map_device(n, HOT)
+        if op == "compress":
+            mr.compress_device(FOLD)
+        else:
+            mr.collate()
+            mr.reduce_device(FOLD)
+        got = {struct.unpack("<q", k)[0]: struct.unpack("<4q", v) for k, v in pairs(mr)}
+        t = np.arange(n)
+        key = np.where(t % 3 == 0, 0, t % 1000)
+        val = t % 1009 - 500
+        assert len(got) == 1000
+        for k in (0, 1, 500, 999):
+            v = val[key == k]
+            assert got[k] == (int(v.sum()), len(v), int(v.min()), int(v.max())), (op, k)
