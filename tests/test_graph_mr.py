@@ -155,3 +155,34 @@ def test_graph_mr_callbacks_host_twin_edge_cases():
     assert picked[6] == [4, int(np.float64(2.5).view(np.int64)), 1]
     assert picked[7] == [3, int(np.float64(2.0).view(np.int64)), 1]  # the own record wins a tie
     assert picked["changed"] == [5]
+
+
+@pytest.mark.gpu
+def test_graph_mr_commands_out_of_core(tmp_path, monkeypatch):
+    """sssp_mr and luby_find_mr under a 128 KiB HBM budget (8 pages of 16 KiB):
+    their aggregates, appends and compress / reduce groups go through the
+    out-of-core paths; the results must not change"""
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import dijkstra
+    n = 3000
+    e, w = weighted_graph(tmp_path, n, 4 * n, 5)
+    s = ("set memsize -16384 maxpage 8\n"
+         "sssp_mr 2 777 -i graph.w -o tmp.ssspmr NULL\n"
+         "rmat 12 4 0.25 0.25 0.25 0.25 0.0 12345 -o tmp.rmat mre\n"
+         "edge_upper -i mre -o NULL mre\n"
+         "luby_find_mr 4321 -i mre -o tmp.mis NULL\n")
+    text = run(s, tmp_path, monkeypatch, comm_for("cuda"))
+    src = parse_sources(text)
+    G = csr_matrix((w, (e[:, 0], e[:, 1])), shape=(n, n))
+    rows = np.loadtxt(tmp_path / "tmp.ssspmr.0", ndmin=2)
+    start = 0
+    for s0, _, cnt in src:
+        r = rows[start:start + cnt]
+        start += cnt
+        d = dijkstra(G, indices=s0)
+        got = {int(v): dv for v, dv, _ in r}
+        assert set(got) == {i for i in range(n) if np.isfinite(d[i])}
+        assert all(got[v] == pytest.approx(d[v], rel=1e-5) for v in got)
+    ed = np.loadtxt(tmp_path / "tmp.rmat.0", dtype=np.int64, ndmin=2)
+    want, _ = greedy_mis(ed, 4321)
+    assert set(np.loadtxt(tmp_path / "tmp.mis.0", dtype=np.int64, ndmin=1).tolist()) == want
