@@ -227,3 +227,16 @@ def test_functors_out_of_core(tmp_path):
         for k in (0, 1, 500, 999):
             v = val[key == k]
             assert got[k] == (int(v.sum()), len(v), int(v.min()), int(v.max())), (op, k)
+
+
+@pytest.mark.gpu
+def test_python_example_runs():
+    """examples/python/device_functors.py (map + fold functors) end to end"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "examples", "python", "device_functors.py"), "2000000", "64"],
+                       env=dict(os.environ, PYTHONPATH=root), capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "2000000 pairs, 64 buckets, total count 2000000" in p.stdout
