@@ -502,6 +502,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("reduce_device", &MR::reduce_device, py::call_guard<py::gil_scoped_release>())
       .def("compress_device", &MR::compress_device, py::call_guard<py::gil_scoped_release>())
+      .def("sort_keys_device", &MR::sort_keys_device, py::arg("code"), py::arg("bits") = 64,
+           py::call_guard<py::gil_scoped_release>())
+      .def("sort_values_device", &MR::sort_values_device, py::arg("code"), py::arg("bits") = 64,
+           py::call_guard<py::gil_scoped_release>())
       .def("compress_batch",
            [](MR& r, py::function fn) {
              py::gil_scoped_release nogil;
@@ -955,6 +959,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("device_functor_check", &devfn::compile_check, py::arg("code"), py::arg("reduce"),
         py::call_guard<py::gil_scoped_release>());
   m.def("device_functor_source", &devfn::full_source, py::arg("code"), py::arg("reduce"));
+  m.def("device_sortkey_check", &devfn::compile_check_sortkey, py::arg("code"),
+        py::call_guard<py::gil_scoped_release>());
   m.def("host_arena_reserve", &hostarena::reserve, py::call_guard<py::gil_scoped_release>());
   m.def("host_arena_stats", [] {
     hostarena::Stats s = hostarena::stats();

@@ -262,12 +262,31 @@ mrd_write(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* v
 }
 )MRD";
 
+// kind 3: a sort-key functor, __device__ unsigned long long mr_sortkey(mrd::Bytes)
+const char* kSortKernel = R"MRD(
+// ---- mrd sort-key kernel ----
+extern "C" __global__ __launch_bounds__(256) void
+mrd_sortkey(const mrd::u8* d, const mrd::i64* off, mrd::i64 w, mrd::i64 n, mrd::u64* key, unsigned int* idx) {
+  for (mrd::i64 i = (mrd::i64)blockIdx.x * 256 + threadIdx.x; i < n; i += (mrd::i64)gridDim.x * 256) {
+    const mrd::Bytes b = off ? mrd::Bytes{d + off[i], off[i + 1] - off[i]} : mrd::Bytes{d + i * w, w};
+    key[i] = mr_sortkey(b);
+    idx[i] = (unsigned int)i;
+  }
+}
+)MRD";
+
 struct Module {
   hipModule_t mod = nullptr;
   hipFunction_t count = nullptr, write = nullptr;
   hipFunction_t acc_size = nullptr, nchunks = nullptr, chunks = nullptr, merge = nullptr;  // fold tier
 };
-const char* kind_name(int kind) { return kind == 0 ? "mrd_map.hip" : kind == 1 ? "mrd_reduce.hip" : "mrd_fold.hip"; }
+const char* kind_name(int kind) {
+  return kind == 0 ? "mrd_map.hip" : kind == 1 ? "mrd_reduce.hip" : kind == 2 ? "mrd_fold.hip" : "mrd_sortkey.hip";
+}
+std::string source_of(const std::string& code, int kind) {
+  if (kind == 3) return std::string(kDevicePrelude) + code + "\n" + kSortKernel;
+  return "#define MRD_REDUCE " + std::to_string(kind) + "\n" + kDevicePrelude + code + "\n" + kKernels;
+}
 
 std::string compile(const std::string& src, const char* name) {
   hiprtcProgram p;
@@ -298,10 +317,16 @@ const Module& module_for(const std::string& code, int kind, int device) {
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return *it->second;
-  const std::string obj =
-      compile("#define MRD_REDUCE " + std::to_string(kind) + "\n" + kDevicePrelude + code + "\n" + kKernels,
-              kind_name(kind));
+  const std::string obj = compile(source_of(code, kind), kind_name(kind));
   auto m = std::make_unique<Module>();
+  if (kind == 3) {
+    if (hipModuleLoadData(&m->mod, obj.data()) != hipSuccess ||
+        hipModuleGetFunction(&m->count, m->mod, "mrd_sortkey") != hipSuccess) {
+      (void)hipGetLastError();
+      throw std::runtime_error("mrhip: loading the sort-key functor's code object failed");
+    }
+    return *cache.emplace(key, std::move(m)).first->second;
+  }
   if (hipModuleLoadData(&m->mod, obj.data()) != hipSuccess ||
       hipModuleGetFunction(&m->count, m->mod, "mrd_count") != hipSuccess ||
       hipModuleGetFunction(&m->write, m->mod, "mrd_write") != hipSuccess ||
@@ -422,8 +447,28 @@ int kind_of(const std::string& code, bool reduce) {
   return !reduce ? 0 : code.find("mr_finish") != std::string::npos ? 2 : 1;
 }
 
-std::string full_source(const std::string& code, bool reduce) {
-  return "#define MRD_REDUCE " + std::to_string(kind_of(code, reduce)) + "\n" + kDevicePrelude + code + "\n" + kKernels;
+std::string full_source(const std::string& code, bool reduce) { return source_of(code, kind_of(code, reduce)); }
+
+int64_t compile_check_sortkey(const std::string& code) {
+  return (int64_t)compile(source_of(code, 3), kind_name(3)).size();
+}
+
+std::pair<at::Tensor, at::Tensor> sort_keys_of(const at::Tensor& data, const at::Tensor& off, int w, int64_t n,
+                                               const std::string& code, at::Device dev) {
+  if (!dev.is_cuda()) throw std::runtime_error("mrhip: device functors run on a GPU MapReduce (device cuda)");
+  at::Tensor key = at::empty({std::max<int64_t>(n, 1)}, opt(dev, at::kLong));
+  at::Tensor idx = at::empty({std::max<int64_t>(n, 1)}, opt(dev, at::kInt));
+  if (n > 0) {
+    const Module& m = module_for(code, 3, dev.index());
+    const uint8_t* d = P0<uint8_t>(data);
+    const int64_t* o = w >= 0 ? nullptr : P0<int64_t>(off);
+    int64_t ww = w >= 0 ? w : 0, nn = n;
+    int64_t* k = P0<int64_t>(key);
+    int32_t* ix = P0<int32_t>(idx);
+    void* args[] = {&d, &o, &ww, &nn, &k, &ix};
+    launch(m.count, n, args, at::hip::getCurrentHIPStream());
+  }
+  return {key.narrow(0, 0, n), idx.narrow(0, 0, n)};
 }
 
 int64_t compile_check(const std::string& code, bool reduce) {

@@ -15,6 +15,7 @@
 // documents mrd::Bytes / mrd::Values / mrd::Emit.
 #pragma once
 #include <string>
+#include <utility>
 
 #include "kv.h"
 
@@ -30,6 +31,13 @@ KV reduce_groups(const KMV& m, const std::string& code, at::Device dev);
 // compile only (syntax / type errors come back with the compiler log);
 // returns the code object size in bytes. Works without a GPU.
 int64_t compile_check(const std::string& code, bool reduce);
+// sort-key functor: `__device__ unsigned long long mr_sortkey(mrd::Bytes b)`
+// maps each key (or value) to a 64-bit key whose unsigned order is the wanted
+// order (a comparator expressed as a key extraction); returns (keys [n],
+// row index [n] int32) for the engine's stable radix sort
+std::pair<at::Tensor, at::Tensor> sort_keys_of(const at::Tensor& data, const at::Tensor& off, int w, int64_t n,
+                                               const std::string& code, at::Device dev);
+int64_t compile_check_sortkey(const std::string& code);
 // the full source handed to the compiler (prelude + code + kernels)
 std::string full_source(const std::string& code, bool reduce);
 }  // namespace devfn

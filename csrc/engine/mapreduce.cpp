@@ -1423,6 +1423,40 @@ uint64_t MapReduce::reduce_device(const std::string& code) {
   });
 }
 
+namespace {
+// stable radix sort of the pairs by the functor's 64-bit keys of one column
+KV sort_by_functor(const KV& kv_in, const std::string& code, int bits, bool by_value, at::Device dev) {
+  if (kv_in.n <= 1) return kv_in;
+  const KV kv = kv_in.device() == dev ? kv_in : kv_to(kv_in, dev);
+  auto [key, idx] = by_value ? devfn::sort_keys_of(kv.vdata, kv.voff, kv.vw, kv.n, code, dev)
+                             : devfn::sort_keys_of(kv.kdata, kv.koff, kv.kw, kv.n, code, dev);
+  auto [ks, perm, passes] = radix_sort_pairs(key, idx, 0, std::max(1, std::min(bits, 64)));
+  (void)ks;
+  (void)passes;
+  return gather(kv, perm);
+}
+}  // namespace
+
+uint64_t MapReduce::sort_keys_device(const std::string& code, int bits) {
+  start();
+  OpTrace tr_(__func__, this);
+  enter(__func__);
+  need_kv("sort_keys");
+  kv = sort_by_functor(*kv, code, bits, false, device());
+  stats("Sort_keys", 0);
+  return count(kv->n);
+}
+
+uint64_t MapReduce::sort_values_device(const std::string& code, int bits) {
+  start();
+  OpTrace tr_(__func__, this);
+  enter(__func__);
+  need_kv("sort_values");
+  kv = sort_by_functor(*kv, code, bits, true, device());
+  stats("Sort_values", 0);
+  return count(kv->n);
+}
+
 uint64_t MapReduce::compress_device(const std::string& code) {
   const at::Device dev = device();
   return compress_batch([&](const KMV& m, KeyValue& out) {

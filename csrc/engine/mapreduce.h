@@ -136,6 +136,9 @@ class MapReduce {
   uint64_t map_device_tasks(int64_t ntask, const std::string& code, int addflag = 0);
   uint64_t reduce_device(const std::string& code);
   uint64_t compress_device(const std::string& code);
+  // sort by a device sort-key functor (mr_sortkey: key -> u64 in the wanted order), stable
+  uint64_t sort_keys_device(const std::string& code, int bits = 64);
+  uint64_t sort_values_device(const std::string& code, int bits = 64);
   uint64_t convert();
   // convert with the keys' hash64_keys() already computed by the producer
   uint64_t convert_prehashed(const at::Tensor& prehash);

@@ -307,6 +307,17 @@ class MapReduce(metaclass=_Counters):
         mr_reduce(mrd::Bytes key, mrd::Values values, mrd::Emit& out)`."""
         return self._m.reduce_device(code)
 
+    def sort_keys_device(self, code, bits=64):
+        """stable sort by a device sort-key functor: `__device__ unsigned long
+        long mr_sortkey(mrd::Bytes key)` maps each key to a 64-bit key whose
+        unsigned order is the wanted one (a comparator as a key extraction;
+        `bits` low bits are sorted on)."""
+        return self._m.sort_keys_device(code, bits)
+
+    def sort_values_device(self, code, bits=64):
+        """sort_keys_device over the values."""
+        return self._m.sort_values_device(code, bits)
+
     def compress_device(self, code):
         """compress (local groups, no shuffle) with a device reduce functor."""
         return self._m.compress_device(code)

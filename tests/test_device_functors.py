@@ -240,3 +240,44 @@ def test_python_example_runs():
                        env=dict(os.environ, PYTHONPATH=root), capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     assert "2000000 pairs, 64 buckets, total count 2000000" in p.stdout
+
+
+# sort-key functor: (b descending, then a ascending) of a pair of int32 keys
+SORTKEY = r"""
+__device__ unsigned long long mr_sortkey(mrd::Bytes k) {
+  const unsigned int a = (unsigned int)k.as<int>(0) ^ 0x80000000u;   // signed -> unsigned order
+  const unsigned int b = (unsigned int)k.as<int>(4) ^ 0x80000000u;
+  return ((unsigned long long)(~b) << 32) | a;
+}
+"""
+
+
+def test_sortkey_functor_compiles():
+    assert C.device_sortkey_check(SORTKEY) > 0
+    with pytest.raises(RuntimeError, match="does not compile"):
+        C.device_sortkey_check("__device__ int mr_sortkey(int) { return x; }")
+
+
+@pytest.mark.gpu
+def test_sort_keys_device_composite_and_stable():
+    from gpu_mapreduce_amd.parallel.comm import Comm
+    from gpu_mapreduce_amd.runtime.mapreduce import MapReduce
+    rng = np.random.default_rng(7)
+    n = 200_000
+    a = rng.integers(-50, 50, n).astype(np.int32)
+    b = rng.integers(-20, 20, n).astype(np.int32)
+    mr = MapReduce(Comm(device="cuda"))
+
+    def m(itask, kv):
+        kv.add_multi_static([struct.pack("<ii", int(x), int(y)) for x, y in zip(a, b)],
+                            [struct.pack("<q", i) for i in range(n)])
+    mr.map(1, m)
+    assert mr.sort_keys_device(SORTKEY) == n
+    got = [(struct.unpack("<ii", k), struct.unpack("<q", v)[0]) for k, v in pairs(mr)]
+    want = sorted(((int(x), int(y)), i) for i, (x, y) in enumerate(zip(a, b)))
+    want.sort(key=lambda r: (-r[0][1], r[0][0]))  # stable: equal keys keep input order (i ascending)
+    assert got == want
+    # by value: the int64 row index descending
+    mr.sort_values_device("__device__ unsigned long long mr_sortkey(mrd::Bytes v) { return ~(unsigned long long)v.as<long long>(); }")
+    got = [struct.unpack("<q", v)[0] for _, v in pairs(mr)]
+    assert got == list(range(n - 1, -1, -1))
