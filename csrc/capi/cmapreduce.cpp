@@ -226,6 +226,12 @@ uint64_t MR_reduce_device(void* p, const char* code) {
 uint64_t MR_compress_device(void* p, const char* code) {
   return guard([&] { return M(p)->compress_device(code); }, (uint64_t)0);
 }
+uint64_t MR_sort_keys_device(void* p, const char* code, int bits) {
+  return guard([&] { return M(p)->sort_keys_device(code, bits); }, (uint64_t)0);
+}
+uint64_t MR_sort_values_device(void* p, const char* code, int bits) {
+  return guard([&] { return M(p)->sort_values_device(code, bits); }, (uint64_t)0);
+}
 uint64_t MR_multivalue_blocks(void* p, int* nblock) {
   int nb = 0;
   uint64_t n = M(p)->multivalue_blocks(nb);

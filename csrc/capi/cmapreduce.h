@@ -85,6 +85,9 @@ uint64_t MR_map_device(void *MRptr, void *MRptr2, const char *code, int addflag)
 uint64_t MR_map_device_tasks(void *MRptr, uint64_t ntask, const char *code, int addflag);
 uint64_t MR_reduce_device(void *MRptr, const char *code);
 uint64_t MR_compress_device(void *MRptr, const char *code);
+/* stable sort by a device sort-key functor (mr_sortkey: key -> 64-bit key in the wanted order) */
+uint64_t MR_sort_keys_device(void *MRptr, const char *code, int bits);
+uint64_t MR_sort_values_device(void *MRptr, const char *code, int bits);
 uint64_t MR_multivalue_blocks(void *MRptr, int *nblock);
 void MR_multivalue_block_select(void *MRptr, int which);
 int MR_multivalue_block(void *MRptr, int iblock, char **ptr_multivalue, int **ptr_valuesizes);

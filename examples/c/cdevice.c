@@ -3,8 +3,9 @@
  * (csrc/engine/devfn.h) — no host callback touches a pair.
  *
  * ntask tasks each emit (t % nkey, 1); collate; a device reduce sums each
- * key's values into an int64. Prints the number of keys and the sum of the
- * sums (= ntask), then the count of key 0 (= ceil(ntask / nkey)).
+ * key's values into an int64; a device sort-key functor orders the keys by
+ * count. Prints the number of keys and the sum of the sums (= ntask), then the
+ * count of key 0 (= ceil(ntask / nkey)).
  *
  *   ./cdevice ntask nkey      (on a GPU MapReduce)
  */
@@ -28,7 +29,7 @@ static const char *REDUCE_SRC =
     "}\n";
 
 struct Totals {
-  int64_t nkey, sum, count0;
+  int64_t nkey, sum, count0, first;
 };
 
 static void tally(char *key, int kb, char *value, int vb, void *app) {
@@ -36,6 +37,7 @@ static void tally(char *key, int kb, char *value, int vb, void *app) {
   int64_t k, v;
   memcpy(&k, key, 8);
   memcpy(&v, value, 8);
+  if (t->nkey == 0) t->first = v;
   t->nkey++;
   t->sum += v;
   if (k == 0) t->count0 = v;
@@ -54,10 +56,14 @@ int main(int argc, char **argv) {
   MR_map_device_tasks(mr, ntask, map_src, 0);
   MR_collate(mr, NULL);
   MR_reduce_device(mr, REDUCE_SRC);
-  struct Totals t = {0, 0, 0};
+  /* order the keys by their count, largest first (a sort on the values) */
+  MR_sort_values_device(mr, "__device__ unsigned long long mr_sortkey(mrd::Bytes v) {\n"
+                            "  return ~(unsigned long long)v.as<long long>();\n}\n", 64);
+  struct Totals t = {0, 0, 0, 0};
   MR_scan_kv(mr, tally, &t);
-  if (MR_my_proc(mr) == 0) printf("keys %lld sum %lld count0 %lld\n", (long long)t.nkey, (long long)t.sum,
-                                  (long long)t.count0);
+  if (MR_my_proc(mr) == 0)
+    printf("keys %lld sum %lld count0 %lld first %lld\n", (long long)t.nkey, (long long)t.sum, (long long)t.count0,
+           (long long)t.first);
   MR_destroy(mr);
   return 0;
 }
