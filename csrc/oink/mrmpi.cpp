@@ -4,6 +4,8 @@
 // the whole device KV. Reference defect not reproduced: its `set` method
 // checks narg != 2 but reads arg[1], arg[2] (mrmpi.cpp:330-344); here it is
 // `<mr> set <key> <value>`.
+#include <fstream>
+#include <sstream>
 #include <cstdlib>
 #include <cstring>
 
@@ -141,6 +143,37 @@ void run_mr_method(Oink& o, int index, const Args& args) {
     if (it == mr_maps().end()) throw Error("Unknown map/mr function " + a[1]);
     std::shared_ptr<MapReduce> src = obj.mrs[j].mr;
     mr.map_mr_batch(*src, it->second, n == 3 ? ival(a[2]) : 0);
+  } else if (cmd == "map/device" || cmd == "map/mr/device" || cmd == "reduce/device" || cmd == "compress/device" ||
+             cmd == "sort_keys/device" || cmd == "sort_values/device") {
+    // device functors (csrc/engine/devfn.h), the HIP source read from a file:
+    //   map/device ntask file [addflag] | map/mr/device mr file [addflag] |
+    //   reduce/device file | compress/device file | sort_keys/device file [bits] | sort_values/device file [bits]
+    auto source = [&](const std::string& path) {
+      std::ifstream f(path);
+      if (!f) throw Error("Cannot open device functor file " + path);
+      std::stringstream ss;
+      ss << f.rdbuf();
+      return ss.str();
+    };
+    if (cmd == "map/device") {
+      need(2, 3);
+      mr.map_device_tasks((int64_t)std::stoll(a[0]), source(a[1]), n == 3 ? ival(a[2]) : 0);
+    } else if (cmd == "map/mr/device") {
+      need(2, 3);
+      const int j = obj.find_mr(a[0]);
+      if (j < 0) throw Error("MR object map/mr/device ID does not exist");
+      std::shared_ptr<MapReduce> src = obj.mrs[j].mr;
+      mr.map_device(*src, source(a[1]), n == 3 ? ival(a[2]) : 0);
+    } else if (cmd == "reduce/device" || cmd == "compress/device") {
+      need(1, 1);
+      if (cmd == "reduce/device") mr.reduce_device(source(a[0]));
+      else mr.compress_device(source(a[0]));
+    } else {
+      need(1, 2);
+      const int bits = n == 2 ? ival(a[1]) : 64;
+      if (cmd == "sort_keys/device") mr.sort_keys_device(source(a[0]), bits);
+      else mr.sort_values_device(source(a[0]), bits);
+    }
   } else if (cmd == "print") {
     if (n == 4) mr.print(ival(a[0]), ival(a[1]), ival(a[2]), ival(a[3]));
     else if (n == 6) mr.print(a[0].c_str(), ival(a[1]), ival(a[2]), ival(a[3]), ival(a[4]), ival(a[5]));

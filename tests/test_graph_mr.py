@@ -186,3 +186,37 @@ def test_graph_mr_commands_out_of_core(tmp_path, monkeypatch):
     ed = np.loadtxt(tmp_path / "tmp.rmat.0", dtype=np.int64, ndmin=2)
     want, _ = greedy_mis(ed, 4321)
     assert set(np.loadtxt(tmp_path / "tmp.mis.0", dtype=np.int64, ndmin=1).tolist()) == want
+
+
+@pytest.mark.gpu
+def test_oink_device_functor_methods(tmp_path, monkeypatch):
+    """the OINK MR methods for device functors (map/mr/device, reduce/device,
+    compress/device, sort_values/device): out-degrees of an R-MAT graph,
+    largest first, against numpy"""
+    (tmp_path / "src.hip").write_text(
+        "__device__ void mr_map(mrd::Bytes k, mrd::Bytes v, long long i, mrd::Emit& out) {\n"
+        "  out.emit(k.as<long long>(0), (int)1);\n}\n")
+    (tmp_path / "sum.hip").write_text(
+        "struct mr_acc { long long n; };\n"
+        "__device__ void mr_init(mrd::Bytes k, mr_acc& a) { a.n = 0; }\n"
+        "__device__ void mr_add(mr_acc& a, mrd::Bytes v) { a.n += v.as<int>(); }\n"
+        "__device__ void mr_merge(mr_acc& a, const mr_acc& b) { a.n += b.n; }\n"
+        "__device__ void mr_finish(mrd::Bytes k, const mr_acc& a, mrd::Emit& out) {"
+        " out.emit(k.as<long long>(), a.n); }\n")
+    (tmp_path / "desc.hip").write_text(
+        "__device__ unsigned long long mr_sortkey(mrd::Bytes v) { return ~(unsigned long long)v.as<long long>(); }\n")
+    s = ("rmat 10 8 0.25 0.25 0.25 0.25 0.0 12345 -o tmp.rmat mre\n"
+         "mre map/mr/device mre src.hip\n"
+         "mre compress/device sum.hip\n"
+         "mre collate NULL\n"
+         "mre reduce/device sum.hip\n"
+         "mre sort_values/device desc.hip\n"
+         "mre print tmp.deg 0 0 1 2 2\n")
+    run(s, tmp_path, monkeypatch, comm_for("cuda"))
+    e = np.loadtxt(tmp_path / "tmp.rmat.0", dtype=np.int64, ndmin=2)
+    deg = np.bincount(e[:, 0])
+    lines = [ln for ln in (tmp_path / "tmp.deg").read_text().splitlines() if ln.startswith("KV pair")]
+    got = [(int(ln.split("key ")[1].split(",")[0]), int(ln.split("value ")[1])) for ln in lines]
+    assert dict(got) == {v: int(d) for v, d in enumerate(deg) if d}
+    counts = [c for _, c in got]
+    assert counts == sorted(counts, reverse=True)

@@ -1,4 +1,4 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-o=gpurun_out/r6g3; mkdir -p $o
+o=gpurun_out/r6g4; mkdir -p $o
 timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_graph_mr.py > $o/tests.log 2>&1
