@@ -143,14 +143,16 @@ __device__ inline void run_item(const u8* kd, const i64* koff, i64 kw, const u8*
 }  // namespace mrd
 extern "C" __global__ __launch_bounds__(256) void
 mrd_count(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* vd, const mrd::i64* voff,
-          mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, mrd::i64* cnt, mrd::u64* wid) {
+          mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, mrd::i64* cnt, mrd::u64* wid, int bytes) {
   mrd::u64 kmin = ~0ull, kmax = 0, vmin = ~0ull, vmax = 0;
   for (mrd::i64 i = (mrd::i64)blockIdx.x * 256 + threadIdx.x; i < n; i += (mrd::i64)gridDim.x * 256) {
     mrd::Emit e{false, 0, 0, 0, ~0ull, 0, ~0ull, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
     mrd::run_item(kd, koff, kw, vd, voff, vw, seg, first, i, e);
     cnt[i] = e.nrec;
-    cnt[n + i] = e.kb;
-    cnt[2 * n + i] = e.vb;
+    if (bytes) {  // the byte columns only when the widths turned out not uniform (a second count pass)
+      cnt[n + i] = e.kb;
+      cnt[2 * n + i] = e.vb;
+    }
     kmin = e.kmin < kmin ? e.kmin : kmin;
     kmax = e.kmax > kmax ? e.kmax : kmax;
     vmin = e.vmin < vmin ? e.vmin : vmin;
@@ -241,15 +243,17 @@ mrd_fold_merge(const mrd::i64* cstart, mrd::i64 nkey, mrd::i64 nchunk, mrd::i64 
 // said so): byte positions follow from the record position, no offsets
 extern "C" __global__ __launch_bounds__(256) void
 mrd_write(const mrd::u8* kd, const mrd::i64* koff, mrd::i64 kw, const mrd::u8* vd, const mrd::i64* voff,
-          mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, const mrd::i64* pos, mrd::i64 okw,
-          mrd::i64 ovw, mrd::u8* okd, mrd::i64* okoff, mrd::u8* ovd, mrd::i64* ovoff) {
-  const mrd::i64 np = n + 1;  // pos: scans of n + 1 (records, then key bytes, value bytes when variable)
+          mrd::i64 vw, const mrd::i64* seg, mrd::i64 first, mrd::i64 n, const mrd::i64* pr, const mrd::i64* pk,
+          const mrd::i64* pv, mrd::i64 okw, mrd::i64 ovw, mrd::u8* okd, mrd::i64* okoff, mrd::u8* ovd,
+          mrd::i64* ovoff) {
+  // pr / pk / pv: exclusive scans (n + 1) of records, key bytes, value bytes
+  // (pk / pv unused when that width is uniform: okw / ovw >= 0)
   for (mrd::i64 i = (mrd::i64)blockIdx.x * 256 + threadIdx.x; i < n; i += (mrd::i64)gridDim.x * 256) {
-    const mrd::i64 r = pos[i];
-    if (pos[i + 1] == r) continue;
-    const mrd::i64 r1 = pos[i + 1];
-    const mrd::i64 k0 = okw >= 0 ? r * okw : pos[np + i], v0 = ovw >= 0 ? r * ovw : pos[2 * np + i];
-    const mrd::i64 k1 = okw >= 0 ? r1 * okw : pos[np + i + 1], v1 = ovw >= 0 ? r1 * ovw : pos[2 * np + i + 1];
+    const mrd::i64 r = pr[i];
+    if (pr[i + 1] == r) continue;
+    const mrd::i64 r1 = pr[i + 1];
+    const mrd::i64 k0 = okw >= 0 ? r * okw : pk[i], v0 = ovw >= 0 ? r * ovw : pv[i];
+    const mrd::i64 k1 = okw >= 0 ? r1 * okw : pk[i + 1], v1 = ovw >= 0 ? r1 * ovw : pv[i + 1];
     mrd::Emit e{true, 0, 0, 0, 0, 0, 0, 0, okd + k0, okw >= 0 ? nullptr : okoff + r, ovd + v0,
                 ovw >= 0 ? nullptr : ovoff + r, r1 - r, k1 - k0, v1 - v0};
     mrd::run_item(kd, koff, kw, vd, voff, vw, seg, first, i, e);
@@ -382,7 +386,7 @@ KV run(const Items& it, const std::string& code, int kind, at::Device dev) {
   const int64_t w0[4] = {-1, 0, -1, 0};  // ~0 = u64 max for the mins
   if (hipMemcpyAsync(wid.data_ptr(), w0, sizeof(w0), hipMemcpyHostToDevice, s) != hipSuccess)
     throw std::runtime_error("mrhip: hipMemcpyAsync failed");
-  {
+  auto count = [&](int bytes) {
     const uint8_t* kd = it.kd;
     const int64_t* koff = it.koff;
     int64_t kw = it.kw, vw = it.vw, first = it.first, n = it.n;
@@ -391,26 +395,27 @@ KV run(const Items& it, const std::string& code, int kind, at::Device dev) {
     const int64_t* seg = it.seg;
     int64_t* c = P0<int64_t>(cnt);
     int64_t* w = P0<int64_t>(wid);
-    void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &first, &n, &c, &w};
+    int b = bytes;
+    void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &first, &n, &c, &w, &b};
     launch(m.count, it.n, args, s);
-  }
-  // the record widths first: uniform widths need only the record scan
+  };
+  count(0);
+  // the record widths first: uniform widths need only the record scan (the
+  // common case); otherwise a second count pass fills the byte columns
   int64_t wh[4] = {0, 0, 0, 0};
   read_small(s, {{P0<int64_t>(wid), wh, 32}});
   const int64_t okw = (wh[0] == wh[1]) ? wh[0] : -1, ovw = (wh[2] == wh[3]) ? wh[2] : -1;
-  at::Tensor pos = at::empty({3 * (it.n + 1)}, opt(dev, at::kLong));
-  for (int c = 0; c < 3; ++c) {
-    if ((c == 1 && okw >= 0) || (c == 2 && ovw >= 0)) continue;
-    pos.narrow(0, c * (it.n + 1), it.n + 1).copy_(exclusive_scan(cnt.narrow(0, c * it.n, it.n)));
-  }
-  const int64_t* pp = P0<int64_t>(pos);
+  if (okw < 0 || ovw < 0) count(1);
+  at::Tensor pr = exclusive_scan(cnt.narrow(0, 0, it.n));
+  at::Tensor pk = okw < 0 ? exclusive_scan(cnt.narrow(0, it.n, it.n)) : at::Tensor();
+  at::Tensor pv = ovw < 0 ? exclusive_scan(cnt.narrow(0, 2 * it.n, it.n)) : at::Tensor();
   int64_t tot[3] = {0, 0, 0};
   {
-    const SmallRead rec{pp + it.n, &tot[0], 8}, kb{pp + 2 * (it.n + 1) - 1, &tot[1], 8},
-        vb{pp + 3 * (it.n + 1) - 1, &tot[2], 8};
-    if (okw < 0 && ovw < 0) read_small(s, {rec, kb, vb});
-    else if (okw < 0) read_small(s, {rec, kb});
-    else if (ovw < 0) read_small(s, {rec, vb});
+    const SmallRead rec{P0<int64_t>(pr) + it.n, &tot[0], 8};
+    if (okw < 0 && ovw < 0)
+      read_small(s, {rec, {P0<int64_t>(pk) + it.n, &tot[1], 8}, {P0<int64_t>(pv) + it.n, &tot[2], 8}});
+    else if (okw < 0) read_small(s, {rec, {P0<int64_t>(pk) + it.n, &tot[1], 8}});
+    else if (ovw < 0) read_small(s, {rec, {P0<int64_t>(pv) + it.n, &tot[2], 8}});
     else read_small(s, {rec});
   }
   const int64_t nout = tot[0];
@@ -430,11 +435,14 @@ KV run(const Items& it, const std::string& code, int kind, at::Device dev) {
     const uint8_t* vd = it.vd;
     const int64_t* voff = it.voff;
     const int64_t* seg = it.seg;
+    const int64_t* ppr = P0<int64_t>(pr);
+    const int64_t* ppk = P0<int64_t>(pk);
+    const int64_t* ppv = P0<int64_t>(pv);
     uint8_t* okd = P0<uint8_t>(out.kdata);
     uint8_t* ovd = P0<uint8_t>(out.vdata);
     int64_t* okoff = P0<int64_t>(out.koff);
     int64_t* ovoff = P0<int64_t>(out.voff);
-    void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &first, &n, &pp, &kwo, &vwo, &okd, &okoff, &ovd, &ovoff};
+    void* args[] = {&kd, &koff, &kw, &vd, &voff, &vw, &seg, &first, &n, &ppr, &ppk, &ppv, &kwo, &vwo, &okd, &okoff, &ovd, &ovoff};
     launch(m.write, it.n, args, s);
   }
   if (out.koff.defined()) k::fill_i64(P0<int64_t>(out.koff) + nout, 1, tot[1], s);
