@@ -40,16 +40,7 @@ __global__ __launch_bounds__(NT) void k_col_minmax_part(const int64_t* __restric
     mn[c] = LLONG_MAX;
     mx[c] = LLONG_MIN;
   }
-  const int64_t stride = (int64_t)gridDim.x * NT;
-  int64_t r0 = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (cols == 1) {  // one column (the common key probe): four independent loads in flight per thread
-    for (; r0 + 3 * stride < rows; r0 += 4 * stride) {
-      const int64_t v0 = p[r0], v1 = p[r0 + stride], v2 = p[r0 + 2 * stride], v3 = p[r0 + 3 * stride];
-      mn[0] = min(mn[0], min(min(v0, v1), min(v2, v3)));
-      mx[0] = max(mx[0], max(max(v0, v1), max(v2, v3)));
-    }
-  }
-  for (int64_t r = r0; r < rows; r += stride) {
+  for (int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x; r < rows; r += (int64_t)gridDim.x * NT) {
 #pragma unroll
     for (int c = 0; c < 8; ++c)
       if (c < cols) {
@@ -109,14 +100,7 @@ __global__ __launch_bounds__(NT) void k_minmax_i32_part(const int32_t* __restric
                                                         int64_t* __restrict__ part) {
   __shared__ int64_t smn[NT / 64], smx[NT / 64];
   int64_t mn = LLONG_MAX, mx = LLONG_MIN;
-  const int64_t stride = (int64_t)gridDim.x * NT;
-  int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {  // four independent loads in flight per thread
-    const int32_t v0 = p[i], v1 = p[i + stride], v2 = p[i + 2 * stride], v3 = p[i + 3 * stride];
-    mn = min(mn, (int64_t)min(min(v0, v1), min(v2, v3)));
-    mx = max(mx, (int64_t)max(max(v0, v1), max(v2, v3)));
-  }
-  for (; i < n; i += stride) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     const int64_t v = p[i];
     mn = min(mn, v);
     mx = max(mx, v);
