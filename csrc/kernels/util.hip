@@ -219,17 +219,6 @@ __global__ __launch_bounds__(NT) void k_edge_upper_write(const int64_t* __restri
   }
 }
 
-// a load of pinned host memory at system scope: it misses in the GPU caches.
-// A plain (or non-temporal) load can hit L2 lines of an earlier read of the
-// same host addresses: a pinned block freed and refilled by a later
-// device -> host drain (DMA, which does not invalidate the GPU's L2) then
-// read stale bytes — sssp_mr under a 128 KiB HBM budget lost vertices in
-// ~1 of 12 runs (tools/sssp_ooc_repeat.py), never with hipMemcpy uploads
-template <typename T>
-__device__ __forceinline__ T host_load(const T* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // zero-copy gather: block (x, p) copies its stride of piece p from pinned
 // host memory (device-accessible) into dst; dword granularity when the piece
 // allows, bytes otherwise
@@ -246,18 +235,18 @@ __global__ __launch_bounds__(NT) void k_gather_pieces(PieceTable t, uint8_t* __r
     const int64_t w = n >> 2;
     for (int64_t i = tid * 4; i < w; i += nth * 4) {  // four dwords in flight per thread
       if (i + 3 < w) {
-        const uint32_t a = host_load(s4 + i), b = host_load(s4 + i + 1);
-        const uint32_t c = host_load(s4 + i + 2), e = host_load(s4 + i + 3);
+        const uint32_t a = __builtin_nontemporal_load(s4 + i), b = __builtin_nontemporal_load(s4 + i + 1);
+        const uint32_t c = __builtin_nontemporal_load(s4 + i + 2), e = __builtin_nontemporal_load(s4 + i + 3);
         d4[i] = a;
         d4[i + 1] = b;
         d4[i + 2] = c;
         d4[i + 3] = e;
       } else {
-        for (int64_t j = i; j < w; ++j) d4[j] = host_load(s4 + j);
+        for (int64_t j = i; j < w; ++j) d4[j] = s4[j];
       }
     }
   } else {
-    for (int64_t i = tid; i < n; i += nth) d[i] = host_load(s + i);
+    for (int64_t i = tid; i < n; i += nth) d[i] = s[i];
   }
 }
 
