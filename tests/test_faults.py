@@ -226,7 +226,10 @@ def test_rank_failure_inside_shuffle_ends_job_fast(tmp_path, kind):
     for r in (0, 2):
         assert res[r][2] - t_fail < 10.0, f"rank {r} outlived the failure by {res[r][2] - t_fail:.1f} s"
         msg = res[r][1]
-        assert ("stopped responding" in msg) if kind == "abort" else ("rank 1 failed" in msg), msg[-2000:]
+        # a crash: the heartbeat sees it, or a survivor's exchange with the
+        # dead peer errors first and that rank poisons the job with its own error
+        ok = ("stopped responding" in msg or "failed:" in msg) if kind == "abort" else ("rank 1 failed" in msg)
+        assert ok, msg[-2000:]
     if kind == "abort":
         assert codes[1] == 3 and "rank 1 aborts at exchange_round" in res[1][1]
 
